@@ -1,0 +1,159 @@
+/*
+ * svo_gpu.h -- C ABI of the MI355X-native ikryukov/svo front end (libsvo_gpu.so).
+ *
+ * This is the drop-in boundary for the four OpenCV calls the reference's
+ * Tracking makes on its hot path:
+ *
+ *   reference call (R: = ikryukov/svo)                         replaced by
+ *   ---------------------------------------------------------  ------------------------------
+ *   buildOpticalFlowPyramid inside calcOpticalFlowPyrLK          svo_image_upload /
+ *     R:src/tracking.cpp:101, :160                               svo_image_build_pyramid
+ *   mDetector->detect(img, kps, mask)  (FastFeatureDetector)     svo_fast_detect
+ *     R:src/tracking.cpp:82 (created :54-57)
+ *   cv::rectangle(mask, p-(10,10), p+(10,10), 0, FILLED)         svo_mask_boxes
+ *     R:src/tracking.cpp:76-79
+ *   FeatureSet::bucketingFeatures  R:src/bucket.cpp:24-68        svo_bucket_features
+ *   cv::calcOpticalFlowPyrLK(...)  R:src/tracking.cpp:101-105,   svo_calc_optical_flow_pyr_lk
+ *     :160-165
+ *   PnPRansacCallback::computeError + findInliers (inside        svo_pnp_residuals
+ *     cv::solvePnPRansac, R:src/tracking.cpp:191-196)
+ *   cv::solvePnPRansac(..., SOLVEPNP_SQPNP)                      svo_solve_pnp_ransac
+ *     R:src/tracking.cpp:191-196
+ *
+ * Conventions (no exceptions cross this ABI; no torch types):
+ *   - Host memory is caller-owned. Device memory is owned by the context.
+ *   - Every int-returning entry point returns SVO_OK (0) or a negative error
+ *     class; svo_last_error(ctx) holds the message. Where OpenCV would throw a
+ *     cv::Exception from CV_Assert (bad window, maxLevel < 0, < 4 PnP points),
+ *     the call returns SVO_ERR_ARG and writes nothing.
+ *   - One svo_ctx per (device, HIP stream, camera sequence). A context is not
+ *     thread-safe; distinct contexts may be used concurrently from different
+ *     threads and devices.
+ *   - Points are float (x, y) pairs laid out exactly like std::vector<cv::Point2f>.
+ */
+#ifndef SVO_GPU_H
+#define SVO_GPU_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SVO_OK 0
+#define SVO_ERR_ARG (-1)      /* argument outside the OpenCV contract */
+#define SVO_ERR_HIP (-2)      /* HIP runtime error */
+#define SVO_ERR_CAPACITY (-3) /* a fixed capacity was exceeded */
+#define SVO_ERR_NODEVICE (-4) /* no HIP device / extension not usable */
+
+/* cv::TermCriteria type bits and cv::calcOpticalFlowPyrLK flags */
+#define SVO_TERM_COUNT 1
+#define SVO_TERM_EPS 2
+#define SVO_LK_USE_INITIAL_FLOW 4
+#define SVO_LK_GET_MIN_EIGENVALS 8
+
+typedef struct svo_ctx svo_ctx;
+typedef struct svo_image svo_image; /* a device-resident 8U image + its pyramid */
+
+typedef struct svo_keypoint {
+    float x, y;     /* cv::KeyPoint::pt */
+    float response; /* cv::KeyPoint::response (FAST score with NMS, else 0) */
+} svo_keypoint;
+
+/* ------------------------------------------------------------ context */
+int svo_ctx_create(int device, svo_ctx** out);
+void svo_ctx_destroy(svo_ctx* ctx);
+const char* svo_last_error(const svo_ctx* ctx);
+int svo_ctx_synchronize(svo_ctx* ctx);
+/* Build identification, e.g. "svo_gpu gfx950 hip 7.2". */
+const char* svo_version(void);
+
+/* ------------------------------------------------------------ images / pyramids
+ * An svo_image holds a W x H 8U image and up to `max_levels` pyrDown levels in
+ * one device allocation (level l is ((w_{l-1}+1)/2, (h_{l-1}+1)/2), OpenCV
+ * pyrDown, BORDER_REFLECT_101). The number of levels a given LK call uses is
+ * clamped exactly as buildOpticalFlowPyramid clamps it for that call's window. */
+int svo_image_create(svo_ctx* ctx, int w, int h, int max_levels, svo_image** out);
+void svo_image_destroy(svo_ctx* ctx, svo_image* img);
+/* H2D copy of level 0 (row stride in bytes) and pyramid build. */
+int svo_image_upload(svo_ctx* ctx, svo_image* img, const uint8_t* gray, int stride);
+/* Rebuild levels 1..max_levels from the device-resident level 0. */
+int svo_image_build_pyramid(svo_ctx* ctx, svo_image* img);
+int svo_image_level_size(const svo_image* img, int level, int* w, int* h);
+int svo_image_download_level(svo_ctx* ctx, const svo_image* img, int level, uint8_t* dst, int stride);
+
+/* ------------------------------------------------------------ FAST
+ * cv::FastFeatureDetector(threshold, nonmaxSuppression, TYPE_9_16)::detect(
+ * image, keypoints, mask): keypoints in OpenCV's raster emission order, NMS
+ * strict-greater over 8 neighbours, then runByPixelsMask. mask: host W*H u8
+ * (row stride w) or NULL. Writes min(n, cap) keypoints; *n_out = n. */
+int svo_fast_detect(svo_ctx* ctx, const svo_image* img, int threshold, int nonmax,
+                    const uint8_t* mask, svo_keypoint* out, int cap, int* n_out);
+/* Kernel-level view for parity tests: per-pixel FAST score (0 = no corner)
+ * and corner flag, both W*H u8. */
+int svo_fast_score_map(svo_ctx* ctx, const svo_image* img, int threshold,
+                       uint8_t* score, uint8_t* corner);
+/* R:src/tracking.cpp:76-79: W*H mask of 255 with a filled box of +-half around
+ * each point (cvRound corners, inclusive, clipped). Host output. */
+int svo_mask_boxes(svo_ctx* ctx, int w, int h, const float* pts_xy, int n, float half,
+                   uint8_t* mask);
+
+/* ------------------------------------------------------------ bucketing
+ * FeatureSet::bucketingFeatures(image(w,h), bucket_size, features_per_bucket)
+ * with the reference's exact output (R:src/bucket.cpp:24-106 quirks included).
+ * ages may be NULL (all 0, as appendNewFeatures sets them). */
+int svo_bucket_features(svo_ctx* ctx, const float* xy, const int* ages, int n, int img_w,
+                        int img_h, int bucket_size, int per_bucket, float* xy_out,
+                        int* ages_out, int cap, int* n_out);
+
+/* ------------------------------------------------------------ LK
+ * cv::calcOpticalFlowPyrLK(prev, next, prevPts, nextPts, status, err,
+ * Size(win_w, win_h), max_level, TermCriteria(crit_type, max_count, epsilon),
+ * flags, min_eig_threshold). next_xy is read as the initial guess when
+ * SVO_LK_USE_INITIAL_FLOW is set. err may be NULL. Pyramids must have been
+ * built with at least the levels this window allows. */
+int svo_calc_optical_flow_pyr_lk(svo_ctx* ctx, const svo_image* prev, const svo_image* next,
+                                 const float* prev_xy, int n, float* next_xy,
+                                 uint8_t* status, float* err, int win_w, int win_h,
+                                 int max_level, int crit_type, int max_count, double epsilon,
+                                 int flags, double min_eig_threshold);
+/* Gauss-Newton iterations executed by the last LK call, summed over points and
+ * levels (the "LK iters/s" metric numerator). */
+int64_t svo_lk_last_iterations(const svo_ctx* ctx);
+
+/* ------------------------------------------------------------ PnP
+ * Batched reprojection residual: M hypotheses (R row-major 3x3, t 3: 12
+ * doubles each) x N points. Equals PnPRansacCallback::computeError (projectPoints
+ * with K, zero distortion, CV_32F output; err = |ipt - ppt|^2 in float) and
+ * findInliers (err <= thresh2). err (M*N floats), mask (M*N bytes), counts (M)
+ * may each be NULL. obj_xyz are floats (OpenCV converts Point3d to CV_32F). */
+int svo_pnp_residuals(svo_ctx* ctx, const float* obj_xyz, const float* img_xy, int n,
+                      const double* hyp_Rt, int m, const double K[9], float thresh2,
+                      float* err, uint8_t* mask, int* counts);
+
+/* cv::solvePnPRansac(obj(Point3d), img(Point2f), K, zeros(1,4), rvec, tvec,
+ * useExtrinsicGuess=false, iterations, reproj_err, confidence, inliers,
+ * SOLVEPNP_SQPNP). Returns 1 (model found), 0 (no model) or < 0 (error).
+ * inliers: capacity n ints, written in ascending order. */
+int svo_solve_pnp_ransac(svo_ctx* ctx, const double* obj_xyz, const float* img_xy, int n,
+                         const double K[9], int iterations, float reproj_err,
+                         double confidence, double rvec[3], double tvec[3], int* inliers,
+                         int* n_inliers);
+
+/* ------------------------------------------------------------ synthetic input
+ * Deterministic synthetic KITTI-like frames: a textured canvas
+ * of random rectangles, box-blurred, seen through a rotating pinhole camera
+ * (pure rotation => the frame-to-frame motion is a homography, any depth is
+ * consistent). Host-side generator, used by tests and bench only. */
+int svo_synth_canvas(uint64_t seed, int cw, int ch, int n_rect, uint8_t* canvas);
+/* frame = canvas seen by camera rotation R (row-major 3x3, world->camera),
+ * intrinsics K; canvas pixel (0,0) sits at image offset (-margin_x, -margin_y)
+ * of the unrotated view; adds U[-noise, noise] integer noise (seeded). */
+int svo_synth_frame(const uint8_t* canvas, int cw, int ch, int margin_x, int margin_y,
+                    const double R[9], const double K[9], uint64_t noise_seed, int noise,
+                    uint8_t* frame, int w, int h);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SVO_GPU_H */

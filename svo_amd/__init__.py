@@ -1,0 +1,330 @@
+"""svo_amd -- MI355X-native front end of ikryukov/svo (Python host side).
+
+Thin ctypes layer over the C ABI of ``svo_amd/lib/libsvo_gpu.so``
+(``include/svo_gpu.h``). The names mirror the OpenCV calls the reference's
+``Tracking`` makes (R: = ikryukov/svo):
+
+=================================  ===========================================
+svo_amd                            reference call site
+=================================  ===========================================
+``Context.image`` (pyramid)         pyramid built inside calcOpticalFlowPyrLK,
+                                    R:src/tracking.cpp:101, :160
+``FastFeatureDetector.detect``      mDetector->detect(img, kps, mask),
+                                    R:src/tracking.cpp:82 (created :54-57)
+``Context.mask_boxes``              cv::rectangle(mask, ...), :76-79
+``Context.bucket_features``         FeatureSet::bucketingFeatures,
+                                    R:src/bucket.cpp:24-68
+``Context.calc_optical_flow_pyr_lk``  cv::calcOpticalFlowPyrLK, :101-105, :160-165
+``Context.pnp_residuals``           PnPRansacCallback::computeError+findInliers
+``Context.solve_pnp_ransac``        cv::solvePnPRansac(..., SQPNP), :191-196
+=================================  ===========================================
+
+There is no CPU fallback: every compute call goes through the HIP kernels and
+raises ``SvoError`` if the extension or a GPU is missing.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+__all__ = [
+    "SvoError", "lib", "Context", "Image", "FastFeatureDetector",
+    "TERM_COUNT", "TERM_EPS", "LK_USE_INITIAL_FLOW", "LK_GET_MIN_EIGENVALS",
+    "synth_canvas", "synth_frame", "lib_path",
+]
+
+TERM_COUNT = 1
+TERM_EPS = 2
+LK_USE_INITIAL_FLOW = 4
+LK_GET_MIN_EIGENVALS = 8
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def lib_path() -> str:
+    return os.path.join(_HERE, "lib", "libsvo_gpu.so")
+
+
+class SvoError(RuntimeError):
+    pass
+
+
+_LIB = None
+
+_u8p = C.POINTER(C.c_uint8)
+_f32p = C.POINTER(C.c_float)
+_f64p = C.POINTER(C.c_double)
+_i32p = C.POINTER(C.c_int)
+_vp = C.c_void_p
+
+# (name, restype, argtypes) for every symbol include/svo_gpu.h declares
+_SIGS = [
+    ("svo_ctx_create", C.c_int, [C.c_int, C.POINTER(_vp)]),
+    ("svo_ctx_destroy", None, [_vp]),
+    ("svo_last_error", C.c_char_p, [_vp]),
+    ("svo_ctx_synchronize", C.c_int, [_vp]),
+    ("svo_version", C.c_char_p, []),
+    ("svo_image_create", C.c_int, [_vp, C.c_int, C.c_int, C.c_int, C.POINTER(_vp)]),
+    ("svo_image_destroy", None, [_vp, _vp]),
+    ("svo_image_upload", C.c_int, [_vp, _vp, _u8p, C.c_int]),
+    ("svo_image_build_pyramid", C.c_int, [_vp, _vp]),
+    ("svo_image_level_size", C.c_int, [_vp, C.c_int, _i32p, _i32p]),
+    ("svo_image_download_level", C.c_int, [_vp, _vp, C.c_int, _u8p, C.c_int]),
+    ("svo_fast_detect", C.c_int, [_vp, _vp, C.c_int, C.c_int, _u8p, _f32p, C.c_int, _i32p]),
+    ("svo_fast_score_map", C.c_int, [_vp, _vp, C.c_int, _u8p, _u8p]),
+    ("svo_mask_boxes", C.c_int, [_vp, C.c_int, C.c_int, _f32p, C.c_int, C.c_float, _u8p]),
+    ("svo_bucket_features", C.c_int, [_vp, _f32p, _i32p, C.c_int, C.c_int, C.c_int, C.c_int,
+                                      C.c_int, _f32p, _i32p, C.c_int, _i32p]),
+    ("svo_calc_optical_flow_pyr_lk", C.c_int, [_vp, _vp, _vp, _f32p, C.c_int, _f32p, _u8p, _f32p,
+                                               C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
+                                               C.c_double, C.c_int, C.c_double]),
+    ("svo_lk_last_iterations", C.c_int64, [_vp]),
+    ("svo_pnp_residuals", C.c_int, [_vp, _f32p, _f32p, C.c_int, _f64p, C.c_int, _f64p, C.c_float,
+                                    _f32p, _u8p, _i32p]),
+    ("svo_solve_pnp_ransac", C.c_int, [_vp, _f64p, _f32p, C.c_int, _f64p, C.c_int, C.c_float,
+                                       C.c_double, _f64p, _f64p, _i32p, _i32p]),
+    ("svo_synth_canvas", C.c_int, [C.c_uint64, C.c_int, C.c_int, C.c_int, _u8p]),
+    ("svo_synth_frame", C.c_int, [_u8p, C.c_int, C.c_int, C.c_int, C.c_int, _f64p, _f64p,
+                                  C.c_uint64, C.c_int, _u8p, C.c_int, C.c_int]),
+]
+
+SYMBOLS = [s[0] for s in _SIGS]
+
+
+def lib():
+    """Load libsvo_gpu.so (built by __graft_entry__.build() / make)."""
+    global _LIB
+    if _LIB is None:
+        path = lib_path()
+        if not os.path.exists(path):
+            raise SvoError(f"HIP extension not built: {path} missing (run __graft_entry__.build())")
+        L = C.CDLL(path)
+        for name, res, args in _SIGS:
+            f = getattr(L, name)
+            f.restype = res
+            f.argtypes = args
+        _LIB = L
+    return _LIB
+
+
+def _p(a, t):
+    return a.ctypes.data_as(t)
+
+
+def _c(a, dtype):
+    return np.ascontiguousarray(a, dtype=dtype)
+
+
+class Image:
+    """A device-resident 8U image with its pyrDown pyramid (levels 0..max_levels)."""
+
+    def __init__(self, ctx: "Context", handle, w: int, h: int, max_levels: int):
+        self.ctx, self.handle, self.w, self.h, self.max_levels = ctx, handle, w, h, max_levels
+
+    def level(self, l: int) -> np.ndarray:
+        L = lib()
+        w, h = C.c_int(), C.c_int()
+        if L.svo_image_level_size(self.handle, l, C.byref(w), C.byref(h)) != 0:
+            raise SvoError(f"no level {l}")
+        out = np.empty((h.value, w.value), np.uint8)
+        self.ctx._check(L.svo_image_download_level(self.ctx.handle, self.handle, l, _p(out, _u8p), w.value))
+        return out
+
+    def upload(self, gray: np.ndarray):
+        gray = _c(gray, np.uint8)
+        assert gray.shape == (self.h, self.w)
+        self.ctx._check(lib().svo_image_upload(self.ctx.handle, self.handle, _p(gray, _u8p), self.w))
+
+    def close(self):
+        if self.handle:
+            lib().svo_image_destroy(self.ctx.handle, self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class Context:
+    """One HIP device + stream (svo_ctx)."""
+
+    def __init__(self, device: int = 0):
+        L = lib()
+        h = _vp()
+        rc = L.svo_ctx_create(device, C.byref(h))
+        if rc != 0:
+            raise SvoError(f"svo_ctx_create(device={device}) failed: {rc} (no usable HIP device?)")
+        self.handle = h
+
+    def _check(self, rc):
+        if rc < 0:
+            raise SvoError(lib().svo_last_error(self.handle).decode() or f"error {rc}")
+        return rc
+
+    def close(self):
+        if getattr(self, "handle", None):
+            lib().svo_ctx_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ---------------------------------------------------------------- images
+    def image(self, gray: np.ndarray, max_levels: int = 4) -> Image:
+        gray = _c(gray, np.uint8)
+        h, w = gray.shape
+        hd = _vp()
+        self._check(lib().svo_image_create(self.handle, w, h, max_levels, C.byref(hd)))
+        img = Image(self, hd, w, h, max_levels)
+        img.upload(gray)
+        return img
+
+    # ---------------------------------------------------------------- FAST
+    def fast_detect(self, img: Image, threshold: int = 20, nonmax: bool = True, mask=None,
+                    cap: int = 1 << 20) -> np.ndarray:
+        """cv::FastFeatureDetector::detect -> float32 array (n, 3): x, y, response."""
+        out = np.empty((cap, 3), np.float32)
+        n = C.c_int()
+        mp = None
+        if mask is not None:
+            mask = _c(mask, np.uint8)
+            assert mask.shape == (img.h, img.w)
+            mp = _p(mask, _u8p)
+        self._check(lib().svo_fast_detect(self.handle, img.handle, int(threshold), int(bool(nonmax)), mp,
+                                          _p(out, _f32p), cap, C.byref(n)))
+        return out[: min(n.value, cap)].copy()
+
+    def fast_score_map(self, img: Image, threshold: int = 20):
+        score = np.empty((img.h, img.w), np.uint8)
+        corner = np.empty((img.h, img.w), np.uint8)
+        self._check(lib().svo_fast_score_map(self.handle, img.handle, int(threshold), _p(score, _u8p),
+                                             _p(corner, _u8p)))
+        return score, corner
+
+    def mask_boxes(self, w: int, h: int, pts, half: float = 10.0) -> np.ndarray:
+        pts = _c(pts, np.float32).reshape(-1, 2)
+        mask = np.empty((h, w), np.uint8)
+        self._check(lib().svo_mask_boxes(self.handle, w, h, _p(pts, _f32p), len(pts), float(half),
+                                         _p(mask, _u8p)))
+        return mask
+
+    # ---------------------------------------------------------------- bucket
+    def bucket_features(self, pts, img_w: int, img_h: int, bucket_size: int, per_bucket: int,
+                        ages=None):
+        pts = _c(pts, np.float32).reshape(-1, 2)
+        n = len(pts)
+        cap = (img_h // bucket_size + 1) * (img_w // bucket_size + 1) * per_bucket + 1
+        xy_out = np.empty((cap, 2), np.float32)
+        ages_out = np.empty(cap, np.int32)
+        ap = None
+        if ages is not None:
+            ages = _c(ages, np.int32)
+            ap = _p(ages, _i32p)
+        nout = C.c_int()
+        self._check(lib().svo_bucket_features(self.handle, _p(pts, _f32p), ap, n, img_w, img_h, bucket_size,
+                                              per_bucket, _p(xy_out, _f32p), _p(ages_out, _i32p), cap,
+                                              C.byref(nout)))
+        k = min(nout.value, cap)
+        return xy_out[:k].copy(), ages_out[:k].copy()
+
+    # ---------------------------------------------------------------- LK
+    def calc_optical_flow_pyr_lk(self, prev: Image, nxt: Image, prev_pts, next_pts=None,
+                                 win_size=(21, 21), max_level: int = 3,
+                                 criteria=(TERM_COUNT | TERM_EPS, 30, 0.01), flags: int = 0,
+                                 min_eig_threshold: float = 1e-4, want_err: bool = True):
+        """cv::calcOpticalFlowPyrLK -> (next_pts (n,2) f32, status (n,) u8, err (n,) f32)."""
+        prev_pts = _c(prev_pts, np.float32).reshape(-1, 2)
+        n = len(prev_pts)
+        if next_pts is None:
+            nxt_pts = np.zeros((n, 2), np.float32)
+        else:
+            nxt_pts = _c(next_pts, np.float32).reshape(-1, 2).copy()
+        status = np.zeros(n, np.uint8)
+        err = np.zeros(n, np.float32) if want_err else None
+        ctype, count, eps = criteria
+        self._check(lib().svo_calc_optical_flow_pyr_lk(
+            self.handle, prev.handle, nxt.handle, _p(prev_pts, _f32p), n, _p(nxt_pts, _f32p),
+            _p(status, _u8p), _p(err, _f32p) if err is not None else None, int(win_size[0]),
+            int(win_size[1]), int(max_level), int(ctype), int(count), float(eps), int(flags),
+            float(min_eig_threshold)))
+        return nxt_pts, status, err
+
+    def lk_last_iterations(self) -> int:
+        return int(lib().svo_lk_last_iterations(self.handle))
+
+    # ---------------------------------------------------------------- PnP
+    def pnp_residuals(self, obj, img_pts, hyps, K, thresh2: float = 64.0, want_err: bool = True):
+        """hyps: (m, 12) = R row-major + t. -> (err (m,n) f32, mask (m,n) u8, counts (m,))."""
+        obj = _c(obj, np.float32).reshape(-1, 3)
+        img_pts = _c(img_pts, np.float32).reshape(-1, 2)
+        hyps = _c(hyps, np.float64).reshape(-1, 12)
+        K = _c(K, np.float64).reshape(9)
+        n, m = len(obj), len(hyps)
+        err = np.empty((m, n), np.float32) if want_err else None
+        mask = np.empty((m, n), np.uint8)
+        counts = np.empty(m, np.int32)
+        self._check(lib().svo_pnp_residuals(self.handle, _p(obj, _f32p), _p(img_pts, _f32p), n,
+                                            _p(hyps, _f64p), m, _p(K, _f64p), float(thresh2),
+                                            _p(err, _f32p) if err is not None else None,
+                                            _p(mask, _u8p), _p(counts, _i32p)))
+        return err, mask, counts
+
+    def solve_pnp_ransac(self, obj, img_pts, K, iterations: int = 100, reproj_err: float = 8.0,
+                         confidence: float = 0.999):
+        """cv::solvePnPRansac(..., SOLVEPNP_SQPNP) -> (ok, rvec, tvec, inliers)."""
+        obj = _c(obj, np.float64).reshape(-1, 3)
+        img_pts = _c(img_pts, np.float32).reshape(-1, 2)
+        K = _c(K, np.float64).reshape(9)
+        n = len(obj)
+        rvec = np.zeros(3, np.float64)
+        tvec = np.zeros(3, np.float64)
+        inl = np.zeros(max(n, 1), np.int32)
+        ninl = C.c_int()
+        rc = self._check(lib().svo_solve_pnp_ransac(self.handle, _p(obj, _f64p), _p(img_pts, _f32p), n,
+                                                    _p(K, _f64p), int(iterations), float(reproj_err),
+                                                    float(confidence), _p(rvec, _f64p), _p(tvec, _f64p),
+                                                    _p(inl, _i32p), C.byref(ninl)))
+        return rc == 1, rvec, tvec, inl[: ninl.value].copy()
+
+
+class FastFeatureDetector:
+    """cv::FastFeatureDetector::create(threshold, nonmaxSuppression) (TYPE_9_16),
+    as the reference creates it at R:src/tracking.cpp:54-57."""
+
+    def __init__(self, ctx: Context, threshold: int = 20, nonmax_suppression: bool = True):
+        self.ctx, self.threshold, self.nonmax = ctx, threshold, nonmax_suppression
+
+    @classmethod
+    def create(cls, ctx: Context, threshold: int = 20, nonmax_suppression: bool = True):
+        return cls(ctx, threshold, nonmax_suppression)
+
+    def detect(self, img: Image, mask=None) -> np.ndarray:
+        return self.ctx.fast_detect(img, self.threshold, self.nonmax, mask)
+
+
+# -------------------------------------------------------------------- synthetic input
+def synth_canvas(seed: int, cw: int, ch: int, n_rect: int) -> np.ndarray:
+    out = np.empty((ch, cw), np.uint8)
+    if lib().svo_synth_canvas(seed, cw, ch, n_rect, _p(out, _u8p)) != 0:
+        raise SvoError("svo_synth_canvas failed")
+    return out
+
+
+def synth_frame(canvas: np.ndarray, margin: tuple, R, K, noise_seed: int, noise: int, w: int,
+                h: int) -> np.ndarray:
+    canvas = _c(canvas, np.uint8)
+    R = _c(R, np.float64).reshape(9)
+    K = _c(K, np.float64).reshape(9)
+    out = np.empty((h, w), np.uint8)
+    ch, cw = canvas.shape
+    if lib().svo_synth_frame(_p(canvas, _u8p), cw, ch, int(margin[0]), int(margin[1]), _p(R, _f64p),
+                             _p(K, _f64p), noise_seed, noise, _p(out, _u8p), w, h) != 0:
+        raise SvoError("svo_synth_frame failed")
+    return out

@@ -1,0 +1,376 @@
+// C ABI of libsvo_gpu.so: context, device images, and the host-pointer entry
+// points that mirror the reference's OpenCV calls (see include/svo_gpu.h for
+// the reference file:line each one replaces).
+#include <cstdarg>
+#include <cstring>
+#include <vector>
+
+#include "common.hpp"
+
+namespace svo {
+
+int set_error(svo_ctx* ctx, int code, const char* fmt, ...) {
+    if (ctx) {
+        char buf[1024];
+        va_list ap;
+        va_start(ap, fmt);
+        vsnprintf(buf, sizeof(buf), fmt, ap);
+        va_end(ap);
+        ctx->err = buf;
+    }
+    return code;
+}
+
+void* scratch(svo_ctx* ctx, int slot, size_t bytes) {
+    svo_scratch& s = ctx->s[slot];
+    if (s.bytes >= bytes && s.p) return s.p;
+    if (s.p) {
+        (void)hipStreamSynchronize(ctx->stream);
+        (void)hipFree(s.p);
+        s.p = nullptr;
+        s.bytes = 0;
+    }
+    size_t want = bytes < 4096 ? 4096 : bytes + bytes / 4;
+    if (hipMalloc(&s.p, want) != hipSuccess) {
+        s.p = nullptr;
+        return nullptr;
+    }
+    s.bytes = want;
+    return s.p;
+}
+
+void* pinned(svo_ctx* ctx, size_t bytes) {
+    if (ctx->pinned_bytes >= bytes && ctx->pinned) return ctx->pinned;
+    if (ctx->pinned) {
+        (void)hipStreamSynchronize(ctx->stream);
+        (void)hipHostFree(ctx->pinned);
+        ctx->pinned = nullptr;
+        ctx->pinned_bytes = 0;
+    }
+    size_t want = bytes < 65536 ? 65536 : bytes + bytes / 4;
+    if (hipHostMalloc(&ctx->pinned, want, hipHostMallocDefault) != hipSuccess) {
+        ctx->pinned = nullptr;
+        return nullptr;
+    }
+    ctx->pinned_bytes = want;
+    return ctx->pinned;
+}
+
+}  // namespace svo
+
+using namespace svo;
+
+extern "C" {
+
+const char* svo_version(void) { return "svo_gpu gfx950 hip " SVO_HIP_VERSION_STR; }
+
+int svo_ctx_create(int device, svo_ctx** out) {
+    if (!out) return SVO_ERR_ARG;
+    *out = nullptr;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return SVO_ERR_NODEVICE;
+    if (device < 0 || device >= ndev) return SVO_ERR_ARG;
+    if (hipSetDevice(device) != hipSuccess) return SVO_ERR_HIP;
+    svo_ctx* c = new svo_ctx();
+    c->device = device;
+    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete c;
+        return SVO_ERR_HIP;
+    }
+    *out = c;
+    return SVO_OK;
+}
+
+void svo_ctx_destroy(svo_ctx* ctx) {
+    if (!ctx) return;
+    (void)hipSetDevice(ctx->device);
+    (void)hipStreamSynchronize(ctx->stream);
+    for (auto& s : ctx->s)
+        if (s.p) (void)hipFree(s.p);
+    if (ctx->pinned) (void)hipHostFree(ctx->pinned);
+    (void)hipStreamDestroy(ctx->stream);
+    delete ctx;
+}
+
+const char* svo_last_error(const svo_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+
+int svo_ctx_synchronize(svo_ctx* ctx) {
+    if (!ctx) return SVO_ERR_ARG;
+    SVO_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    return SVO_OK;
+}
+
+// ------------------------------------------------------------------ images
+int svo_image_create(svo_ctx* ctx, int w, int h, int max_levels, svo_image** out) {
+    if (!ctx || !out || w <= 0 || h <= 0 || max_levels < 0)
+        return set_error(ctx, SVO_ERR_ARG, "svo_image_create: bad arguments");
+    if (max_levels > kMaxLevels - 1) max_levels = kMaxLevels - 1;
+    (void)hipSetDevice(ctx->device);
+    svo_image* im = new svo_image();
+    im->w = w;
+    im->h = h;
+    im->nlevels = max_levels + 1;
+    size_t off[kMaxLevels];
+    size_t total = 0;
+    int lw = w, lh = h;
+    for (int l = 0; l < im->nlevels; l++) {
+        int pitch = (lw + 63) & ~63;
+        off[l] = total;
+        total += (size_t)pitch * lh;
+        total = (total + 255) & ~(size_t)255;
+        im->desc.lv[l].w = lw;
+        im->desc.lv[l].h = lh;
+        im->desc.lv[l].pitch = pitch;
+        lw = (lw + 1) / 2;
+        lh = (lh + 1) / 2;
+    }
+    if (hipMalloc(&im->base, total) != hipSuccess) {
+        delete im;
+        return set_error(ctx, SVO_ERR_HIP, "svo_image_create: hipMalloc(%zu) failed", total);
+    }
+    im->bytes = total;
+    for (int l = 0; l < im->nlevels; l++) im->desc.lv[l].data = im->base + off[l];
+    im->desc.nlevels = im->nlevels;
+    *out = im;
+    return SVO_OK;
+}
+
+void svo_image_destroy(svo_ctx* ctx, svo_image* img) {
+    if (!img) return;
+    if (ctx) (void)hipStreamSynchronize(ctx->stream);
+    if (img->base) (void)hipFree(img->base);
+    delete img;
+}
+
+int svo_image_build_pyramid(svo_ctx* ctx, svo_image* img) {
+    if (!ctx || !img) return SVO_ERR_ARG;
+    SVO_HIP(ctx, launch_pyramid(img, 1, ctx->stream));
+    return SVO_OK;
+}
+
+int svo_image_upload(svo_ctx* ctx, svo_image* img, const uint8_t* gray, int stride) {
+    if (!ctx || !img || !gray || stride < img->w)
+        return set_error(ctx, SVO_ERR_ARG, "svo_image_upload: bad arguments");
+    const ImgLevel& L = img->desc.lv[0];
+    SVO_HIP(ctx, hipMemcpy2DAsync(const_cast<uint8_t*>(L.data), L.pitch, gray, stride, L.w, L.h,
+                                  hipMemcpyHostToDevice, ctx->stream));
+    return svo_image_build_pyramid(ctx, img);
+}
+
+int svo_image_level_size(const svo_image* img, int level, int* w, int* h) {
+    if (!img || level < 0 || level >= img->nlevels) return SVO_ERR_ARG;
+    if (w) *w = img->desc.lv[level].w;
+    if (h) *h = img->desc.lv[level].h;
+    return SVO_OK;
+}
+
+int svo_image_download_level(svo_ctx* ctx, const svo_image* img, int level, uint8_t* dst, int stride) {
+    if (!ctx || !img || !dst || level < 0 || level >= img->nlevels)
+        return set_error(ctx, SVO_ERR_ARG, "svo_image_download_level: bad arguments");
+    const ImgLevel& L = img->desc.lv[level];
+    if (stride < L.w) return set_error(ctx, SVO_ERR_ARG, "svo_image_download_level: stride");
+    SVO_HIP(ctx, hipMemcpy2DAsync(dst, stride, L.data, L.pitch, L.w, L.h, hipMemcpyDeviceToHost,
+                                  ctx->stream));
+    SVO_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    return SVO_OK;
+}
+
+// ------------------------------------------------------------------ FAST
+int svo_fast_score_map(svo_ctx* ctx, const svo_image* img, int threshold, uint8_t* score,
+                       uint8_t* corner) {
+    if (!ctx || !img) return SVO_ERR_ARG;
+    threshold = threshold < 0 ? 0 : threshold > 255 ? 255 : threshold;
+    const ImgLevel& L = img->desc.lv[0];
+    size_t npx = (size_t)L.w * L.h;
+    uint16_t* cs = (uint16_t*)scratch(ctx, 0, npx * 2);
+    if (!cs) return set_error(ctx, SVO_ERR_HIP, "scratch alloc");
+    SVO_HIP(ctx, launch_fast_score(L, threshold, 1, cs, ctx->stream));
+    std::vector<uint16_t> h(npx);
+    SVO_HIP(ctx, hipMemcpyAsync(h.data(), cs, npx * 2, hipMemcpyDeviceToHost, ctx->stream));
+    SVO_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    for (size_t i = 0; i < npx; i++) {
+        if (score) score[i] = (uint8_t)(h[i] & 0xFF);
+        if (corner) corner[i] = (uint8_t)(h[i] >> 8);
+    }
+    return SVO_OK;
+}
+
+int svo_fast_detect(svo_ctx* ctx, const svo_image* img, int threshold, int nonmax,
+                    const uint8_t* mask, svo_keypoint* out, int cap, int* n_out) {
+    if (!ctx || !img || (!out && cap > 0) || cap < 0)
+        return set_error(ctx, SVO_ERR_ARG, "svo_fast_detect: bad arguments");
+    threshold = threshold < 0 ? 0 : threshold > 255 ? 255 : threshold;
+    const ImgLevel& L = img->desc.lv[0];
+    size_t npx = (size_t)L.w * L.h;
+    uint16_t* cs = (uint16_t*)scratch(ctx, 0, npx * 2);
+    int* rowcnt = (int*)scratch(ctx, 1, sizeof(int) * ((size_t)L.h + 16));
+    uint8_t* dmask = mask ? (uint8_t*)scratch(ctx, 2, npx) : nullptr;
+    int kcap = cap > 0 ? cap : 1;
+    svo_keypoint* dout = (svo_keypoint*)scratch(ctx, 3, sizeof(svo_keypoint) * (size_t)kcap + 64);
+    int* dn = (int*)((char*)dout + sizeof(svo_keypoint) * (size_t)kcap);
+    if (!cs || !rowcnt || (mask && !dmask) || !dout) return set_error(ctx, SVO_ERR_HIP, "scratch alloc");
+    if (mask) SVO_HIP(ctx, hipMemcpyAsync(dmask, mask, npx, hipMemcpyHostToDevice, ctx->stream));
+    SVO_HIP(ctx, launch_fast_score(L, threshold, nonmax ? 1 : 0, cs, ctx->stream));
+    SVO_HIP(ctx, launch_fast_collect(L, cs, nonmax ? 1 : 0, dmask, rowcnt, dout, cap, dn, ctx->stream));
+    int n = 0;
+    SVO_HIP(ctx, hipMemcpyAsync(&n, dn, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
+    SVO_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    int nc = n < cap ? n : cap;
+    if (nc > 0)
+        SVO_HIP(ctx, hipMemcpy(out, dout, sizeof(svo_keypoint) * (size_t)nc, hipMemcpyDeviceToHost));
+    if (n_out) *n_out = n;
+    return SVO_OK;
+}
+
+int svo_mask_boxes(svo_ctx* ctx, int w, int h, const float* pts_xy, int n, float half, uint8_t* mask) {
+    if (!ctx || w <= 0 || h <= 0 || !mask || n < 0 || (n > 0 && !pts_xy))
+        return set_error(ctx, SVO_ERR_ARG, "svo_mask_boxes: bad arguments");
+    size_t npx = (size_t)w * h;
+    uint8_t* dmask = (uint8_t*)scratch(ctx, 2, npx);
+    float* dpts = (float*)scratch(ctx, 4, sizeof(float) * 2 * (size_t)(n > 0 ? n : 1));
+    if (!dmask || !dpts) return set_error(ctx, SVO_ERR_HIP, "scratch alloc");
+    if (n > 0) SVO_HIP(ctx, hipMemcpyAsync(dpts, pts_xy, sizeof(float) * 2 * n, hipMemcpyHostToDevice, ctx->stream));
+    SVO_HIP(ctx, launch_mask_boxes(w, h, dpts, n, half, dmask, ctx->stream));
+    SVO_HIP(ctx, hipMemcpyAsync(mask, dmask, npx, hipMemcpyDeviceToHost, ctx->stream));
+    SVO_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    return SVO_OK;
+}
+
+// ------------------------------------------------------------------ bucket
+int svo_bucket_features(svo_ctx* ctx, const float* xy, const int* ages, int n, int img_w, int img_h,
+                        int bucket_size, int per_bucket, float* xy_out, int* ages_out, int cap,
+                        int* n_out) {
+    if (!ctx || n < 0 || (n > 0 && !xy) || img_w <= 0 || img_h <= 0 || bucket_size <= 0 ||
+        per_bucket <= 0 || cap < 0 || (cap > 0 && !xy_out))
+        return set_error(ctx, SVO_ERR_ARG, "svo_bucket_features: bad arguments");
+    const int nh = img_h / bucket_size, nw = img_w / bucket_size;
+    if (nw <= 0) return set_error(ctx, SVO_ERR_ARG, "svo_bucket_features: bucket wider than image");
+    const size_t nb = (size_t)(nh + 1) * (nw + 1);
+    size_t scr_ints = nb + nb * per_bucket + (size_t)n + nb + 1;
+    int* scr = (int*)scratch(ctx, 5, sizeof(int) * scr_ints);
+    int ncap = cap > 0 ? cap : 1;
+    char* io = (char*)scratch(ctx, 6, sizeof(float) * 2 * ((size_t)n + ncap) + sizeof(int) * ((size_t)n + ncap) + 256);
+    if (!scr || !io) return set_error(ctx, SVO_ERR_HIP, "scratch alloc");
+    float* dxy = (float*)io;
+    int* dages = (int*)(dxy + 2 * (size_t)n);
+    float* dxy_out = (float*)(dages + n);
+    int* dages_out = (int*)(dxy_out + 2 * (size_t)ncap);
+    int* dn = dages_out + ncap;
+    if (n > 0) {
+        SVO_HIP(ctx, hipMemcpyAsync(dxy, xy, sizeof(float) * 2 * n, hipMemcpyHostToDevice, ctx->stream));
+        if (ages) SVO_HIP(ctx, hipMemcpyAsync(dages, ages, sizeof(int) * n, hipMemcpyHostToDevice, ctx->stream));
+    }
+    SVO_HIP(ctx, launch_bucket(dxy, ages ? dages : nullptr, n, img_w, img_h, bucket_size, per_bucket,
+                               dxy_out, dages_out, cap, dn, scr, ctx->stream));
+    int tot = 0;
+    SVO_HIP(ctx, hipMemcpyAsync(&tot, dn, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
+    SVO_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    int nc = tot < cap ? tot : cap;
+    if (nc > 0) {
+        SVO_HIP(ctx, hipMemcpy(xy_out, dxy_out, sizeof(float) * 2 * nc, hipMemcpyDeviceToHost));
+        if (ages_out) SVO_HIP(ctx, hipMemcpy(ages_out, dages_out, sizeof(int) * nc, hipMemcpyDeviceToHost));
+    }
+    if (n_out) *n_out = tot;
+    return SVO_OK;
+}
+
+// ------------------------------------------------------------------ LK
+int svo_calc_optical_flow_pyr_lk(svo_ctx* ctx, const svo_image* prev, const svo_image* next,
+                                 const float* prev_xy, int n, float* next_xy, uint8_t* status,
+                                 float* err, int win_w, int win_h, int max_level, int crit_type,
+                                 int max_count, double epsilon, int flags,
+                                 double min_eig_threshold) {
+    if (!ctx || !prev || !next) return SVO_ERR_ARG;
+    ctx->lk_iters = 0;
+    if (n == 0) return SVO_OK;  // OpenCV releases the outputs and returns
+    if (n < 0 || !prev_xy || !next_xy || !status || max_level < 0 || win_w <= 2 || win_h <= 2)
+        return set_error(ctx, SVO_ERR_ARG, "calcOpticalFlowPyrLK: bad arguments (CV_Assert)");
+    if (prev->w != next->w || prev->h != next->h)
+        return set_error(ctx, SVO_ERR_ARG, "calcOpticalFlowPyrLK: image sizes differ");
+    if (!lk_supported(win_w, win_h))
+        return set_error(ctx, SVO_ERR_CAPACITY, "calcOpticalFlowPyrLK: window %dx%d unsupported", win_w, win_h);
+    // criteria clamping as SparsePyrLKOpticalFlowImpl::calc
+    if ((crit_type & SVO_TERM_COUNT) == 0) max_count = 30;
+    else max_count = max_count < 0 ? 0 : max_count > 100 ? 100 : max_count;
+    if ((crit_type & SVO_TERM_EPS) == 0) epsilon = 0.01;
+    else epsilon = epsilon < 0. ? 0. : epsilon > 10. ? 10. : epsilon;
+    int ml = lk_levels_for_window(prev->w, prev->h, win_w, win_h, max_level);
+    if (ml > prev->nlevels - 1 || ml > next->nlevels - 1)
+        return set_error(ctx, SVO_ERR_CAPACITY, "calcOpticalFlowPyrLK: pyramid has %d levels, %d needed",
+                         prev->nlevels < next->nlevels ? prev->nlevels : next->nlevels, ml + 1);
+    LKParams p;
+    p.win_w = win_w;
+    p.win_h = win_h;
+    p.max_level = ml;
+    p.max_count = max_count;
+    p.eps2 = epsilon * epsilon;
+    p.flags = flags;
+    p.min_eig = (float)min_eig_threshold;
+    p.want_err = err ? 1 : 0;
+    size_t bytes = (size_t)n * (8 + 8 + 1 + 4 + 4) + 256;
+    char* d = (char*)scratch(ctx, 7, bytes);
+    if (!d) return set_error(ctx, SVO_ERR_HIP, "scratch alloc");
+    float* dprev = (float*)d;
+    float* dnext = dprev + 2 * (size_t)n;
+    float* derr = dnext + 2 * (size_t)n;
+    int* diters = (int*)(derr + n);
+    uint8_t* dst = (uint8_t*)(diters + n);
+    SVO_HIP(ctx, hipMemcpyAsync(dprev, prev_xy, sizeof(float) * 2 * n, hipMemcpyHostToDevice, ctx->stream));
+    if (flags & SVO_LK_USE_INITIAL_FLOW)
+        SVO_HIP(ctx, hipMemcpyAsync(dnext, next_xy, sizeof(float) * 2 * n, hipMemcpyHostToDevice, ctx->stream));
+    SVO_HIP(ctx, launch_lk(prev->desc, next->desc, dprev, dnext, dst, err ? derr : nullptr, diters, n, p,
+                           ctx->stream));
+    std::vector<int> it(n);
+    SVO_HIP(ctx, hipMemcpyAsync(next_xy, dnext, sizeof(float) * 2 * n, hipMemcpyDeviceToHost, ctx->stream));
+    SVO_HIP(ctx, hipMemcpyAsync(status, dst, n, hipMemcpyDeviceToHost, ctx->stream));
+    if (err) SVO_HIP(ctx, hipMemcpyAsync(err, derr, sizeof(float) * n, hipMemcpyDeviceToHost, ctx->stream));
+    SVO_HIP(ctx, hipMemcpyAsync(it.data(), diters, sizeof(int) * n, hipMemcpyDeviceToHost, ctx->stream));
+    SVO_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    int64_t s = 0;
+    for (int v : it) s += v;
+    ctx->lk_iters = s;
+    return SVO_OK;
+}
+
+int64_t svo_lk_last_iterations(const svo_ctx* ctx) { return ctx ? ctx->lk_iters : 0; }
+
+// ------------------------------------------------------------------ PnP residuals
+int svo_pnp_residuals(svo_ctx* ctx, const float* obj_xyz, const float* img_xy, int n,
+                      const double* hyp_Rt, int m, const double K[9], float thresh2, float* err,
+                      uint8_t* mask, int* counts) {
+    if (!ctx || n < 0 || m < 0 || (n > 0 && (!obj_xyz || !img_xy)) || (m > 0 && !hyp_Rt) || !K)
+        return set_error(ctx, SVO_ERR_ARG, "svo_pnp_residuals: bad arguments");
+    if (n == 0 || m == 0) {
+        if (counts)
+            for (int i = 0; i < m; i++) counts[i] = 0;
+        return SVO_OK;
+    }
+    const int words = (n + 31) / 32;
+    size_t bytes = sizeof(float) * 5 * (size_t)n + sizeof(double) * 12 * (size_t)m +
+                   (err ? sizeof(float) * (size_t)n * m : 0) + sizeof(uint32_t) * (size_t)words * m +
+                   sizeof(int) * (size_t)m + 1024;
+    char* d = (char*)scratch(ctx, 7, bytes);
+    if (!d) return set_error(ctx, SVO_ERR_HIP, "scratch alloc");
+    double* dh = (double*)d;
+    float* dobj = (float*)(dh + 12 * (size_t)m);
+    float* dimg = dobj + 3 * (size_t)n;
+    int* dcnt = (int*)(dimg + 2 * (size_t)n);
+    uint32_t* dbits = (uint32_t*)(dcnt + m);
+    float* derr = err ? (float*)(dbits + (size_t)words * m) : nullptr;
+    SVO_HIP(ctx, hipMemcpyAsync(dh, hyp_Rt, sizeof(double) * 12 * m, hipMemcpyHostToDevice, ctx->stream));
+    SVO_HIP(ctx, hipMemcpyAsync(dobj, obj_xyz, sizeof(float) * 3 * n, hipMemcpyHostToDevice, ctx->stream));
+    SVO_HIP(ctx, hipMemcpyAsync(dimg, img_xy, sizeof(float) * 2 * n, hipMemcpyHostToDevice, ctx->stream));
+    SVO_HIP(ctx, launch_pnp_residuals(dobj, dimg, n, dh, m, K[0], K[4], K[2], K[5], thresh2, derr, dbits,
+                                      dcnt, ctx->stream));
+    std::vector<uint32_t> bits((size_t)words * m);
+    SVO_HIP(ctx, hipMemcpyAsync(bits.data(), dbits, sizeof(uint32_t) * bits.size(), hipMemcpyDeviceToHost, ctx->stream));
+    if (counts) SVO_HIP(ctx, hipMemcpyAsync(counts, dcnt, sizeof(int) * m, hipMemcpyDeviceToHost, ctx->stream));
+    if (err) SVO_HIP(ctx, hipMemcpyAsync(err, derr, sizeof(float) * (size_t)n * m, hipMemcpyDeviceToHost, ctx->stream));
+    SVO_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    if (mask)
+        for (int h = 0; h < m; h++)
+            for (int i = 0; i < n; i++) mask[(size_t)h * n + i] = (bits[(size_t)h * words + (i >> 5)] >> (i & 31)) & 1;
+    return SVO_OK;
+}
+
+}  // extern "C"

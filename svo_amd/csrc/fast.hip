@@ -1,0 +1,243 @@
+// FAST-9/16 corner detection + score + non-max suppression + mask + stable
+// raster-order compaction for gfx950.
+//
+// Replaces mDetector->detect(leftImg, keypoints, mask) at R:src/tracking.cpp:82
+// (cv::FastFeatureDetector::create(threshold, nonmaxSuppression) at :54-57) and
+// the mask rectangles drawn at :76-79. Semantics follow OpenCV 4.x
+// features2d/src/fast.cpp FAST_t<16> / fast_score.cpp cornerScore<16> /
+// keypoint.cpp runByPixelsMask:
+//   * detection area rows/cols 3 .. dim-4; darker: x < v - t, brighter: x > v + t;
+//     corner = a circular run of >= 9 (the 25-entry walk of FAST_t is exactly a
+//     circular run test on the 16-bit ring mask);
+//   * score = cornerScore<16> (max threshold keeping the corner);
+//   * NMS: strict '>' against all 8 neighbours, non-corners score 0;
+//   * keypoints in raster order (y, then x) -- OpenCV's emission order;
+//   * the mask drops keypoints AFTER NMS (masked corners still suppress).
+//
+// Kernels: (1) tile score kernel -> u16 map {corner bit 8 | score}; (2) per-row
+// keep count; (3) per-row stable write at the row's exclusive offset.
+#include "common.hpp"
+
+namespace svo {
+
+namespace {
+
+constexpr int FT_TX = 64, FT_TY = 16;           // output tile
+constexpr int FT_IW = FT_TX + 6, FT_IH = FT_TY + 6;
+
+// ring offsets (dx, dy) of makeOffsets(patternSize = 16)
+__constant__ int8_t c_ring[16][2] = {{0, 3},  {1, 3},  {2, 2},   {3, 1},   {3, 0},  {3, -1},
+                                     {2, -2}, {1, -3}, {0, -3},  {-1, -3}, {-2, -2}, {-3, -1},
+                                     {-3, 0}, {-3, 1}, {-2, 2},  {-1, 3}};
+
+__device__ __forceinline__ bool run9(unsigned m16) {
+    unsigned m = m16 | (m16 << 16);   // circular
+    unsigned r = m & (m >> 1);        // 2 consecutive
+    r &= r >> 2;                      // 4
+    r &= r >> 4;                      // 8
+    r &= m >> 8;                      // 9
+    return (r & 0xFFFFu) != 0;
+}
+
+__global__ __launch_bounds__(256) void fast_score_kernel(const uint8_t* __restrict__ img, int w,
+                                                         int h, int pitch, int threshold,
+                                                         int want_score,
+                                                         uint16_t* __restrict__ cs) {
+    __shared__ uint8_t T[FT_IH][FT_IW + 2];
+    const int x0 = blockIdx.x * FT_TX, y0 = blockIdx.y * FT_TY;
+    const int tid = threadIdx.x;
+    for (int k = tid; k < FT_IH * FT_IW; k += 256) {
+        int r = k / FT_IW, c = k - r * FT_IW;
+        int y = y0 - 3 + r, x = x0 - 3 + c;
+        T[r][c] = ((unsigned)y < (unsigned)h && (unsigned)x < (unsigned)w) ? img[(size_t)y * pitch + x] : 0;
+    }
+    __syncthreads();
+    const int c = tid & 63;
+    const int x = x0 + c;
+    if (x >= w) return;
+    for (int i = 0; i < FT_TY / 4; i++) {
+        const int r = (tid >> 6) * (FT_TY / 4) + i;
+        const int y = y0 + r;
+        if (y >= h) break;
+        uint16_t out = 0;
+        if (x >= 3 && x < w - 3 && y >= 3 && y < h - 3) {
+            const int v = T[r + 3][c + 3];
+            int ring[16];
+            unsigned bright = 0, dark = 0;
+#pragma unroll
+            for (int k = 0; k < 16; k++) {
+                ring[k] = T[r + 3 + c_ring[k][1]][c + 3 + c_ring[k][0]];
+                bright |= (unsigned)(ring[k] > v + threshold) << k;
+                dark |= (unsigned)(ring[k] < v - threshold) << k;
+            }
+            if (run9(bright) || run9(dark)) {
+                int score = 0;
+                if (want_score) {
+                    int d[25];
+#pragma unroll
+                    for (int k = 0; k < 25; k++) d[k] = v - ring[k & 15];
+                    int a0 = threshold;
+#pragma unroll
+                    for (int k = 0; k < 16; k += 2) {
+                        int a = min(d[k + 1], d[k + 2]);
+                        a = min(a, d[k + 3]);
+                        a = min(a, d[k + 4]);
+                        a = min(a, d[k + 5]);
+                        a = min(a, d[k + 6]);
+                        a = min(a, d[k + 7]);
+                        a = min(a, d[k + 8]);
+                        a0 = max(a0, min(a, d[k]));
+                        a0 = max(a0, min(a, d[k + 9]));
+                    }
+                    int b0 = -a0;
+#pragma unroll
+                    for (int k = 0; k < 16; k += 2) {
+                        int b = max(d[k + 1], d[k + 2]);
+                        b = max(b, d[k + 3]);
+                        b = max(b, d[k + 4]);
+                        b = max(b, d[k + 5]);
+                        b = max(b, d[k + 6]);
+                        b = max(b, d[k + 7]);
+                        b = max(b, d[k + 8]);
+                        b0 = min(b0, max(b, d[k]));
+                        b0 = min(b0, max(b, d[k + 9]));
+                    }
+                    score = (-b0 - 1) & 0xFF;
+                }
+                out = (uint16_t)(0x100 | score);
+            }
+        }
+        cs[(size_t)y * w + x] = out;
+    }
+}
+
+__device__ __forceinline__ bool fast_keep(const uint16_t* __restrict__ cs, int w, int x, int y,
+                                          int nonmax, const uint8_t* __restrict__ mask) {
+    const uint16_t* p = cs + (size_t)y * w + x;
+    unsigned v = p[0];
+    if (!(v & 0x100)) return false;
+    if (nonmax) {
+        int s = v & 0xFF;
+        // neighbours exist: corners lie in 3..dim-4
+        if (!(s > (p[-1] & 0xFF) && s > (p[1] & 0xFF) && s > (p[-w - 1] & 0xFF) &&
+              s > (p[-w] & 0xFF) && s > (p[-w + 1] & 0xFF) && s > (p[w - 1] & 0xFF) &&
+              s > (p[w] & 0xFF) && s > (p[w + 1] & 0xFF)))
+            return false;
+    }
+    if (mask && mask[(size_t)y * w + x] == 0) return false;
+    return true;
+}
+
+__global__ __launch_bounds__(256) void fast_count_kernel(const uint16_t* __restrict__ cs, int w,
+                                                         int h, int nonmax,
+                                                         const uint8_t* __restrict__ mask,
+                                                         int* __restrict__ rowcnt) {
+    const int y = blockIdx.x;
+    __shared__ int wsum[4];
+    int cnt = 0;
+    if (y >= 3 && y < h - 3)
+        for (int x = 3 + threadIdx.x; x < w - 3; x += 256) cnt += fast_keep(cs, w, x, y, nonmax, mask);
+    for (int o = 32; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o);
+    if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = cnt;
+    __syncthreads();
+    if (threadIdx.x == 0) rowcnt[y] = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+}
+
+__global__ __launch_bounds__(256) void fast_write_kernel(const uint16_t* __restrict__ cs, int w,
+                                                         int h, int nonmax,
+                                                         const uint8_t* __restrict__ mask,
+                                                         const int* __restrict__ rowcnt,
+                                                         svo_keypoint* __restrict__ out, int cap,
+                                                         int* __restrict__ n_out) {
+    const int y = blockIdx.x;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    __shared__ int wsum[4];
+    __shared__ int base_s;
+    // exclusive offset of this row: sum of the counts of rows above
+    int s = 0;
+    for (int r = tid; r < y; r += 256) s += rowcnt[r];
+    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+    if (lane == 0) wsum[wv] = s;
+    __syncthreads();
+    if (tid == 0) {
+        base_s = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+        if (y == h - 1) *n_out = base_s + rowcnt[y];
+    }
+    __syncthreads();
+    if (y < 3 || y >= h - 3 || rowcnt[y] == 0) return;
+    int base = base_s;
+    for (int x0 = 0; x0 < w; x0 += 256) {
+        const int x = x0 + tid;
+        const bool keep = x >= 3 && x < w - 3 && fast_keep(cs, w, x, y, nonmax, mask);
+        const unsigned long long bal = __ballot(keep);
+        const int rank = __popcll(bal & ((1ull << lane) - 1ull));
+        __syncthreads();
+        if (lane == 0) wsum[wv] = __popcll(bal);
+        __syncthreads();
+        int off = base;
+        for (int k = 0; k < wv; k++) off += wsum[k];
+        if (keep) {
+            const int idx = off + rank;
+            if (idx < cap) {
+                svo_keypoint kp;
+                kp.x = (float)x;
+                kp.y = (float)y;
+                kp.response = (float)(cs[(size_t)y * w + x] & 0xFF);
+                out[idx] = kp;
+            }
+        }
+        base += wsum[0] + wsum[1] + wsum[2] + wsum[3];
+    }
+}
+
+__global__ __launch_bounds__(64) void mask_boxes_kernel(int w, int h, const float* __restrict__ pts,
+                                                        int n, float half,
+                                                        uint8_t* __restrict__ mask) {
+    const int i = blockIdx.x;
+    if (i >= n) return;
+    const float px = pts[2 * i], py = pts[2 * i + 1];
+    // cv::rectangle(Point2f -> Point via cvRound, FILLED, inclusive, clipped)
+    int xa = (int)__builtin_rintf(px - half), ya = (int)__builtin_rintf(py - half);
+    int xb = (int)__builtin_rintf(px + half), yb = (int)__builtin_rintf(py + half);
+    int xl = min(xa, xb), xr = max(xa, xb), yt = min(ya, yb), yd = max(ya, yb);
+    xl = max(xl, 0);
+    yt = max(yt, 0);
+    xr = min(xr, w - 1);
+    yd = min(yd, h - 1);
+    const int bw = xr - xl + 1, bh = yd - yt + 1;
+    if (bw <= 0 || bh <= 0) return;
+    for (int k = threadIdx.x; k < bw * bh; k += 64) {
+        int r = k / bw, c = k - r * bw;
+        mask[(size_t)(yt + r) * w + (xl + c)] = 0;
+    }
+}
+
+}  // namespace
+
+hipError_t launch_fast_score(const ImgLevel& L, int threshold, int nonmax, uint16_t* cs,
+                             hipStream_t st) {
+    dim3 grid((L.w + FT_TX - 1) / FT_TX, (L.h + FT_TY - 1) / FT_TY);
+    hipLaunchKernelGGL(fast_score_kernel, grid, dim3(256), 0, st, L.data, L.w, L.h, L.pitch,
+                       threshold, nonmax, cs);
+    return hipGetLastError();
+}
+
+hipError_t launch_fast_collect(const ImgLevel& L, const uint16_t* cs, int nonmax,
+                               const uint8_t* mask, int* rowcnt, svo_keypoint* out, int cap,
+                               int* n_out, hipStream_t st) {
+    hipLaunchKernelGGL(fast_count_kernel, dim3(L.h), dim3(256), 0, st, cs, L.w, L.h, nonmax, mask,
+                       rowcnt);
+    hipLaunchKernelGGL(fast_write_kernel, dim3(L.h), dim3(256), 0, st, cs, L.w, L.h, nonmax, mask,
+                       rowcnt, out, cap, n_out);
+    return hipGetLastError();
+}
+
+hipError_t launch_mask_boxes(int w, int h, const float* pts, int n, float half, uint8_t* mask,
+                             hipStream_t st) {
+    hipError_t e = hipMemsetAsync(mask, 255, (size_t)w * h, st);
+    if (e != hipSuccess) return e;
+    if (n > 0) hipLaunchKernelGGL(mask_boxes_kernel, dim3(n), dim3(64), 0, st, w, h, pts, n, half, mask);
+    return hipGetLastError();
+}
+
+}  // namespace svo

@@ -1,0 +1,230 @@
+// Small dense double-precision linear algebra for the pose solvers
+// (host now; written __host__ __device__ so the minimal solvers can move onto
+// the GPU). Fixed maximum sizes, no allocation.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+
+namespace svo {
+namespace la {
+
+#define SVO_HD __host__ __device__ inline
+
+// Cyclic Jacobi eigen-decomposition of a symmetric n x n (n <= 12) matrix A
+// (row-major, destroyed). Eigenvalues descending in w; eigenvector i in row i of V.
+SVO_HD void sym_eig(double* A, int n, double* w, double* V) {
+    double Q[144];
+    for (int i = 0; i < n * n; i++) Q[i] = 0;
+    for (int i = 0; i < n; i++) Q[i * n + i] = 1;
+    for (int sweep = 0; sweep < 60; sweep++) {
+        double off = 0, tot = 0;
+        for (int p = 0; p < n; p++)
+            for (int q = 0; q < n; q++) {
+                double v = A[p * n + q] * A[p * n + q];
+                tot += v;
+                if (p != q) off += v;
+            }
+        if (off == 0 || off <= 1e-32 * tot) break;
+        for (int p = 0; p < n - 1; p++)
+            for (int q = p + 1; q < n; q++) {
+                const double apq = A[p * n + q];
+                if (apq == 0) continue;
+                const double theta = (A[q * n + q] - A[p * n + p]) / (2 * apq);
+                const double t = (theta >= 0 ? 1.0 : -1.0) / (fabs(theta) + sqrt(theta * theta + 1));
+                const double c = 1 / sqrt(t * t + 1), s = t * c;
+                for (int k = 0; k < n; k++) {
+                    const double a = A[k * n + p], b = A[k * n + q];
+                    A[k * n + p] = c * a - s * b;
+                    A[k * n + q] = s * a + c * b;
+                }
+                for (int k = 0; k < n; k++) {
+                    const double a = A[p * n + k], b = A[q * n + k];
+                    A[p * n + k] = c * a - s * b;
+                    A[q * n + k] = s * a + c * b;
+                }
+                for (int k = 0; k < n; k++) {
+                    const double a = Q[k * n + p], b = Q[k * n + q];
+                    Q[k * n + p] = c * a - s * b;
+                    Q[k * n + q] = s * a + c * b;
+                }
+            }
+    }
+    int order[12];
+    for (int i = 0; i < n; i++) order[i] = i;
+    for (int i = 1; i < n; i++) {  // insertion sort, descending
+        int v = order[i], j = i - 1;
+        while (j >= 0 && A[order[j] * n + order[j]] < A[v * n + v]) {
+            order[j + 1] = order[j];
+            j--;
+        }
+        order[j + 1] = v;
+    }
+    for (int i = 0; i < n; i++) {
+        w[i] = A[order[i] * n + order[i]];
+        for (int k = 0; k < n; k++) V[i * n + k] = Q[k * n + order[i]];
+    }
+}
+
+// One-sided Jacobi SVD of a (m x n, m <= 12, n <= 12): a = U diag(s) V^T,
+// s descending; U is m x n (columns), Vt is n x n (rows).
+SVO_HD void svd(const double* a, int m, int n, double* s, double* U, double* Vt) {
+    double W[144], V[144];
+    for (int i = 0; i < m * n; i++) W[i] = a[i];
+    for (int i = 0; i < n * n; i++) V[i] = 0;
+    for (int i = 0; i < n; i++) V[i * n + i] = 1;
+    for (int sweep = 0; sweep < 60; sweep++) {
+        bool rotated = false;
+        for (int p = 0; p < n - 1; p++)
+            for (int q = p + 1; q < n; q++) {
+                double al = 0, be = 0, ga = 0;
+                for (int k = 0; k < m; k++) {
+                    al += W[k * n + p] * W[k * n + p];
+                    be += W[k * n + q] * W[k * n + q];
+                    ga += W[k * n + p] * W[k * n + q];
+                }
+                if (ga == 0 || fabs(ga) <= 1e-15 * sqrt(al * be)) continue;
+                rotated = true;
+                const double z = (be - al) / (2 * ga);
+                const double t = (z >= 0 ? 1.0 : -1.0) / (fabs(z) + sqrt(1 + z * z));
+                const double c = 1 / sqrt(1 + t * t), sn = c * t;
+                for (int k = 0; k < m; k++) {
+                    const double x = W[k * n + p], y = W[k * n + q];
+                    W[k * n + p] = c * x - sn * y;
+                    W[k * n + q] = sn * x + c * y;
+                }
+                for (int k = 0; k < n; k++) {
+                    const double x = V[k * n + p], y = V[k * n + q];
+                    V[k * n + p] = c * x - sn * y;
+                    V[k * n + q] = sn * x + c * y;
+                }
+            }
+        if (!rotated) break;
+    }
+    double nrm[12];
+    int order[12];
+    for (int j = 0; j < n; j++) {
+        double acc = 0;
+        for (int k = 0; k < m; k++) acc += W[k * n + j] * W[k * n + j];
+        nrm[j] = sqrt(acc);
+        order[j] = j;
+    }
+    for (int i = 1; i < n; i++) {
+        int v = order[i], j = i - 1;
+        while (j >= 0 && nrm[order[j]] < nrm[v]) {
+            order[j + 1] = order[j];
+            j--;
+        }
+        order[j + 1] = v;
+    }
+    for (int i = 0; i < n; i++) {
+        const int c = order[i];
+        s[i] = nrm[c];
+        for (int k = 0; k < n; k++) Vt[i * n + k] = V[k * n + c];
+        if (U)
+            for (int k = 0; k < m; k++) U[k * n + i] = nrm[c] > 0 ? W[k * n + c] / nrm[c] : 0;
+    }
+}
+
+// Least squares x = pinv(A) b (m x n, m <= 12, n <= 12), as cv::solve(DECOMP_SVD).
+SVO_HD void lstsq(const double* A, int m, int n, const double* b, double* x) {
+    double s[12], U[144], Vt[144];
+    svd(A, m, n, s, U, Vt);
+    const double tol = s[0] * (m > n ? m : n) * 2.220446049250313e-16;
+    for (int j = 0; j < n; j++) x[j] = 0;
+    for (int i = 0; i < n; i++) {
+        if (!(s[i] > tol)) continue;
+        double ub = 0;
+        for (int k = 0; k < m; k++) ub += U[k * n + i] * b[k];
+        ub /= s[i];
+        for (int j = 0; j < n; j++) x[j] += ub * Vt[i * n + j];
+    }
+}
+
+// Pseudo-inverse of a 3x3 matrix.
+SVO_HD void pinv3(const double* A, double* Ai) {
+    double s[3], U[9], Vt[9];
+    svd(A, 3, 3, s, U, Vt);
+    const double tol = s[0] * 3 * 2.220446049250313e-16;
+    for (int i = 0; i < 3; i++)
+        for (int j = 0; j < 3; j++) {
+            double acc = 0;
+            for (int k = 0; k < 3; k++)
+                if (s[k] > tol) acc += Vt[k * 3 + i] * U[j * 3 + k] / s[k];
+            Ai[i * 3 + j] = acc;
+        }
+}
+
+// Nearest rotation (polar factor with det = +1) of a 3x3 matrix.
+SVO_HD void nearest_rotation(const double* M, double* R) {
+    double s[3], U[9], Vt[9];
+    svd(M, 3, 3, s, U, Vt);
+    double sg = 1.0;
+    for (int pass = 0; pass < 2; pass++) {
+        for (int i = 0; i < 3; i++)
+            for (int j = 0; j < 3; j++)
+                R[i * 3 + j] = U[i * 3 + 0] * Vt[0 * 3 + j] + U[i * 3 + 1] * Vt[1 * 3 + j] + sg * U[i * 3 + 2] * Vt[2 * 3 + j];
+        const double det = R[0] * (R[4] * R[8] - R[5] * R[7]) - R[1] * (R[3] * R[8] - R[5] * R[6]) +
+                           R[2] * (R[3] * R[7] - R[4] * R[6]);
+        if (det > 0) break;
+        sg = -1.0;
+    }
+}
+
+// Rodrigues vector -> matrix (cv::Rodrigues formula order).
+SVO_HD void rodrigues(const double* rv, double* R) {
+    double rx = rv[0], ry = rv[1], rz = rv[2];
+    const double th = sqrt(rx * rx + ry * ry + rz * rz);
+    if (th < 2.220446049250313e-16) {
+        for (int i = 0; i < 9; i++) R[i] = (i % 4 == 0) ? 1.0 : 0.0;
+        return;
+    }
+    const double c = cos(th), s = sin(th), c1 = 1. - c, it = th ? 1. / th : 0.;
+    rx *= it;
+    ry *= it;
+    rz *= it;
+    const double rrt[9] = {rx * rx, rx * ry, rx * rz, rx * ry, ry * ry, ry * rz, rx * rz, ry * rz, rz * rz};
+    const double rxm[9] = {0, -rz, ry, rz, 0, -rx, -ry, rx, 0};
+    for (int i = 0; i < 9; i++) R[i] = (c * ((i % 4 == 0) ? 1.0 : 0.0) + c1 * rrt[i]) + s * rxm[i];
+}
+
+// Rodrigues matrix -> vector (re-orthonormalised through the SVD first).
+SVO_HD void rodrigues_inv(const double* Rin, double* rv) {
+    double R[9];
+    nearest_rotation(Rin, R);
+    double rx = R[7] - R[5], ry = R[2] - R[6], rz = R[3] - R[1];
+    const double s = sqrt((rx * rx + ry * ry + rz * rz) * 0.25);
+    double c = (R[0] + R[4] + R[8] - 1) * 0.5;
+    c = c > 1. ? 1. : c < -1. ? -1. : c;
+    double th = acos(c);
+    if (s < 1e-5) {
+        if (c > 0) {
+            rx = ry = rz = 0;
+        } else {
+            double t = (R[0] + 1) * 0.5;
+            rx = sqrt(t > 0 ? t : 0.);
+            t = (R[4] + 1) * 0.5;
+            ry = sqrt(t > 0 ? t : 0.) * (R[1] < 0 ? -1. : 1.);
+            t = (R[8] + 1) * 0.5;
+            rz = sqrt(t > 0 ? t : 0.) * (R[2] < 0 ? -1. : 1.);
+            if (fabs(rx) < fabs(ry) && fabs(rx) < fabs(rz) && (R[5] > 0) != (ry * rz > 0)) rz = -rz;
+            th /= sqrt(rx * rx + ry * ry + rz * rz);
+            rx *= th;
+            ry *= th;
+            rz *= th;
+        }
+    } else {
+        double vth = 1 / (2 * s);
+        vth *= th;
+        rx *= vth;
+        ry *= vth;
+        rz *= vth;
+    }
+    rv[0] = rx;
+    rv[1] = ry;
+    rv[2] = rz;
+}
+
+}  // namespace la
+}  // namespace svo

@@ -1,0 +1,82 @@
+// Grayscale pyramid build (pyrDown chain) for gfx950.
+//
+// Replaces the pyramid OpenCV builds inside every cv::calcOpticalFlowPyrLK call
+// at R:src/tracking.cpp:101-105 and :160-165 (lkpyramid.cpp buildOpticalFlowPyramid
+// -> pyramids.cpp pyrDown_): dst = ((w+1)/2, (h+1)/2), separable [1 4 6 4 1]^2,
+// (sum + 128) >> 8, BORDER_REFLECT_101. Bit-exact (integer arithmetic).
+//
+// Unlike the reference, which rebuilds both pyramids on every LK call, a frame's
+// pyramid is built once, kept in HBM and shared by the temporal and stereo LK
+// calls. HBM roofline: reads w*h, writes w*h/4 bytes per level.
+#include "common.hpp"
+
+namespace svo {
+
+__device__ __forceinline__ int refl101(int p, int len) {
+    if ((unsigned)p < (unsigned)len) return p;
+    if (len == 1) return 0;
+    do {
+        p = p < 0 ? -p : 2 * len - 2 - p;
+    } while ((unsigned)p >= (unsigned)len);
+    return p;
+}
+
+constexpr int PD_TX = 64;   // output tile width
+constexpr int PD_TY = 16;   // output tile height
+constexpr int PD_IW = 2 * PD_TX + 4;  // 132 input columns
+constexpr int PD_IH = 2 * PD_TY + 4;  // 36 input rows
+
+__global__ __launch_bounds__(256) void pyr_down_kernel(const uint8_t* __restrict__ src, int sw,
+                                                       int sh, int sp, uint8_t* __restrict__ dst,
+                                                       int dw, int dh, int dp) {
+    __shared__ uint8_t T[PD_IH][PD_IW + 4];
+    __shared__ int H[PD_IH][PD_TX + 1];
+    const int x0 = blockIdx.x * PD_TX, y0 = blockIdx.y * PD_TY;
+    const int sx0 = 2 * x0 - 2, sy0 = 2 * y0 - 2;
+    const int tid = threadIdx.x;
+    const bool interior = sx0 >= 0 && sy0 >= 0 && sx0 + PD_IW <= sw && sy0 + PD_IH <= sh;
+    if (interior) {
+        for (int k = tid; k < PD_IH * PD_IW; k += 256) {
+            int r = k / PD_IW, c = k - r * PD_IW;
+            T[r][c] = src[(size_t)(sy0 + r) * sp + (sx0 + c)];
+        }
+    } else {
+        for (int k = tid; k < PD_IH * PD_IW; k += 256) {
+            int r = k / PD_IW, c = k - r * PD_IW;
+            T[r][c] = src[(size_t)refl101(sy0 + r, sh) * sp + refl101(sx0 + c, sw)];
+        }
+    }
+    __syncthreads();
+    for (int k = tid; k < PD_IH * PD_TX; k += 256) {
+        int r = k >> 6, c = k & 63;
+        const uint8_t* t = &T[r][2 * c];
+        H[r][c] = t[0] + 4 * t[1] + 6 * t[2] + 4 * t[3] + t[4];
+    }
+    __syncthreads();
+    const int c = tid & 63;
+    const int x = x0 + c;
+    if (x >= dw) return;
+#pragma unroll
+    for (int i = 0; i < PD_TY / 4; i++) {
+        int r = (tid >> 6) * (PD_TY / 4) + i;
+        int y = y0 + r;
+        if (y < dh) {
+            int s = H[2 * r][c] + 4 * H[2 * r + 1][c] + 6 * H[2 * r + 2][c] + 4 * H[2 * r + 3][c] +
+                    H[2 * r + 4][c];
+            dst[(size_t)y * dp + x] = (uint8_t)((s + 128) >> 8);
+        }
+    }
+}
+
+hipError_t launch_pyramid(const svo_image* img, int first_level, hipStream_t st) {
+    for (int l = first_level < 1 ? 1 : first_level; l < img->nlevels; l++) {
+        const ImgLevel& s = img->desc.lv[l - 1];
+        const ImgLevel& d = img->desc.lv[l];
+        dim3 grid((d.w + PD_TX - 1) / PD_TX, (d.h + PD_TY - 1) / PD_TY);
+        hipLaunchKernelGGL(pyr_down_kernel, grid, dim3(256), 0, st, s.data, s.w, s.h, s.pitch,
+                           const_cast<uint8_t*>(d.data), d.w, d.h, d.pitch);
+    }
+    return hipGetLastError();
+}
+
+}  // namespace svo

@@ -1,0 +1,81 @@
+// Deterministic synthetic input for tests and bench only: a
+// canvas of random rectangles (box-blurred) seen by a pinhole camera that only
+// rotates, so frame-to-frame motion is the homography K R K^-1 and a map point
+// at ANY depth along a canvas ray reprojects exactly (no stereo needed to make
+// consistent 3D points). The reference reads KITTI PNGs instead
+// (R:include/async_image_loader.h:57-69); KITTI is not available here.
+#include <cmath>
+#include <cstring>
+#include <vector>
+
+#include "svo_gpu.h"
+
+namespace {
+
+inline uint64_t splitmix(uint64_t& s) {
+    uint64_t z = (s += 0x9E3779B97F4A7C15ULL);
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+    return z ^ (z >> 31);
+}
+inline uint64_t hash3(uint64_t seed, uint64_t a, uint64_t b) {
+    uint64_t s = seed ^ (a * 0x9E3779B97F4A7C15ULL) ^ (b * 0xC2B2AE3D27D4EB4FULL);
+    return splitmix(s);
+}
+
+}  // namespace
+
+extern "C" int svo_synth_canvas(uint64_t seed, int cw, int ch, int n_rect, uint8_t* canvas) {
+    if (cw <= 0 || ch <= 0 || !canvas || n_rect < 0) return SVO_ERR_ARG;
+    std::vector<uint8_t> tmp((size_t)cw * ch, 128);
+    uint64_t s = seed * 2 + 1;
+    for (int r = 0; r < n_rect; r++) {
+        int x = (int)(splitmix(s) % (uint64_t)cw), y = (int)(splitmix(s) % (uint64_t)ch);
+        int w = 4 + (int)(splitmix(s) % 61), h = 4 + (int)(splitmix(s) % 61);
+        uint8_t v = (uint8_t)(splitmix(s) & 0xFF);
+        for (int yy = y; yy < y + h && yy < ch; yy++)
+            std::memset(&tmp[(size_t)yy * cw + x], v, (size_t)((x + w <= cw ? w : cw - x)));
+    }
+    // 3x3 box blur, replicate border
+    for (int y = 0; y < ch; y++)
+        for (int x = 0; x < cw; x++) {
+            int acc = 0;
+            for (int dy = -1; dy <= 1; dy++) {
+                int yy = y + dy < 0 ? 0 : y + dy >= ch ? ch - 1 : y + dy;
+                for (int dx = -1; dx <= 1; dx++) {
+                    int xx = x + dx < 0 ? 0 : x + dx >= cw ? cw - 1 : x + dx;
+                    acc += tmp[(size_t)yy * cw + xx];
+                }
+            }
+            canvas[(size_t)y * cw + x] = (uint8_t)((acc + 4) / 9);
+        }
+    return SVO_OK;
+}
+
+extern "C" int svo_synth_frame(const uint8_t* canvas, int cw, int ch, int margin_x, int margin_y,
+                               const double R[9], const double K[9], uint64_t noise_seed, int noise,
+                               uint8_t* frame, int w, int h) {
+    if (!canvas || !R || !K || !frame || w <= 0 || h <= 0) return SVO_ERR_ARG;
+    const double fx = K[0], fy = K[4], cx = K[2], cy = K[5];
+    for (int y = 0; y < h; y++)
+        for (int x = 0; x < w; x++) {
+            // camera ray, rotated to the world (canvas) frame: R^T K^-1 p
+            const double dx = (x - cx) / fx, dy = (y - cy) / fy;
+            const double wx = R[0] * dx + R[3] * dy + R[6];
+            const double wy = R[1] * dx + R[4] * dy + R[7];
+            const double wz = R[2] * dx + R[5] * dy + R[8];
+            double u = fx * wx / wz + cx + margin_x, v = fy * wy / wz + cy + margin_y;
+            if (!(wz > 0)) u = v = -1;
+            u = u < 0 ? 0 : u > cw - 1.001 ? cw - 1.001 : u;
+            v = v < 0 ? 0 : v > ch - 1.001 ? ch - 1.001 : v;
+            const int iu = (int)u, iv = (int)v;
+            const double a = u - iu, b = v - iv;
+            const uint8_t* c0 = canvas + (size_t)iv * cw + iu;
+            const uint8_t* c1 = c0 + cw;
+            double val = (1 - a) * (1 - b) * c0[0] + a * (1 - b) * c0[1] + (1 - a) * b * c1[0] + a * b * c1[1];
+            if (noise > 0) val += (int)(hash3(noise_seed, (uint64_t)x, (uint64_t)y) % (uint64_t)(2 * noise + 1)) - noise;
+            int iv8 = (int)std::floor(val + 0.5);
+            frame[(size_t)y * w + x] = (uint8_t)(iv8 < 0 ? 0 : iv8 > 255 ? 255 : iv8);
+        }
+    return SVO_OK;
+}

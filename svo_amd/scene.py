@@ -1,0 +1,94 @@
+"""Deterministic synthetic scenes for the parity tests and the bench.
+
+The reference reads KITTI sequence 00 (R:configs/config.yaml:2-4); KITTI is not
+available here, so frames are rendered from a textured canvas (random
+rectangles, 3x3 box blur, +-3 noise) by a pinhole camera that only rotates.
+Per frame the camera turns so that the image moves by about (+1.37, -0.82) px
+and rolls 0.25 deg (ping-pong over `period` frames so the view stays on the
+canvas): frame-to-frame motion is the homography K R K^-1, the same order of
+motion as the survey's similarity warp, and a 3D point placed at ANY depth on
+a canvas ray reprojects exactly -- which gives consistent PnP inputs without
+stereo triangulation.
+"""
+from __future__ import annotations
+
+import math
+
+import numpy as np
+
+from . import synth_canvas, synth_frame
+
+KITTI_W, KITTI_H = 1241, 376
+# R:configs/config.yaml:8-11 (fx, fy, cx, cy), held as float32 like the
+# reference's cv::Matx33f K (R:include/tracking.h:55)
+KITTI_FX, KITTI_FY, KITTI_CX, KITTI_CY = 718.8560, 718.8560, 607.1928, 185.2157
+
+
+def intrinsics(w: int, h: int) -> np.ndarray:
+    """Camera matrix for a w x h synthetic frame: KITTI's, scaled; float32-rounded."""
+    sx, sy = w / KITTI_W, h / KITTI_H
+    K = np.array([[KITTI_FX * sx, 0, KITTI_CX * sx], [0, KITTI_FY * sx, KITTI_CY * sy], [0, 0, 1]],
+                 np.float32)
+    return K.astype(np.float64)
+
+
+def rot(axis: str, a: float) -> np.ndarray:
+    c, s = math.cos(a), math.sin(a)
+    if axis == "x":
+        return np.array([[1, 0, 0], [0, c, -s], [0, s, c]])
+    if axis == "y":
+        return np.array([[c, 0, s], [0, 1, 0], [-s, 0, c]])
+    return np.array([[c, -s, 0], [s, c, 0], [0, 0, 1]])
+
+
+class Scene:
+    """A synthetic sequence: canvas + per-frame camera rotation."""
+
+    def __init__(self, w: int, h: int, seed: int = 0, period: int = 16, noise: int = 3,
+                 shift=(1.37, -0.82), roll_deg: float = 0.25, density: float = 1 / 250.0):
+        self.w, self.h, self.seed, self.period, self.noise = w, h, seed, period, noise
+        self.K = intrinsics(w, h)
+        fx, fy = self.K[0, 0], self.K[1, 1]
+        self.yaw_rate = math.atan(shift[0] / fx)
+        self.pitch_rate = math.atan(-shift[1] / fy)
+        self.roll_rate = math.radians(roll_deg)
+        diag = math.hypot(w, h) / 2
+        span = period * max(abs(shift[0]), abs(shift[1])) + diag * math.sin(period * self.roll_rate) + 16
+        self.margin = int(math.ceil(span)) + 8
+        self.cw, self.ch = w + 2 * self.margin, h + 2 * self.margin
+        n_rect = int(self.cw * self.ch * density)
+        self.canvas = synth_canvas(seed, self.cw, self.ch, n_rect)
+
+    def phase(self, t: int) -> float:
+        p = self.period
+        m = t % (2 * p)
+        return float(m if m <= p else 2 * p - m)
+
+    def R(self, t: int) -> np.ndarray:
+        """World -> camera rotation of frame t."""
+        s = self.phase(t)
+        return rot("z", s * self.roll_rate) @ rot("x", s * self.pitch_rate) @ rot("y", s * self.yaw_rate)
+
+    def frame(self, t: int) -> np.ndarray:
+        return synth_frame(self.canvas, (self.margin, self.margin), self.R(t), self.K,
+                           (self.seed << 20) + t + 1, self.noise, self.w, self.h)
+
+    def depth(self, cu: np.ndarray, cv: np.ndarray) -> np.ndarray:
+        """Smooth positive depth field over canvas coordinates (metres)."""
+        return 12.0 + 5.0 * np.sin(cu / 97.0 + self.seed) + 4.0 * np.cos(cv / 61.0 - 0.5 * self.seed)
+
+    def map_points(self, pts: np.ndarray, t: int) -> np.ndarray:
+        """World points (float64, (n,3)) of pixels `pts` observed in frame t."""
+        pts = np.asarray(pts, np.float64).reshape(-1, 2)
+        Ki = np.linalg.inv(self.K)
+        rays = (Ki @ np.c_[pts, np.ones(len(pts))].T)          # camera rays
+        rw = self.R(t).T @ rays                                 # world rays
+        cu = self.K[0, 0] * rw[0] / rw[2] + self.K[0, 2]
+        cv = self.K[1, 1] * rw[1] / rw[2] + self.K[1, 2]
+        rho = self.depth(cu, cv)
+        return (rw / rw[2] * rho).T.copy()
+
+    def project(self, X: np.ndarray, t: int) -> np.ndarray:
+        Xc = (self.R(t) @ np.asarray(X, np.float64).T)
+        uv = self.K @ Xc
+        return (uv[:2] / uv[2]).T

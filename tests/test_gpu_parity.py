@@ -1,0 +1,252 @@
+"""GPU-vs-oracle parity of every HIP kernel on the hot path.
+
+All calls go through the C ABI (libsvo_gpu.so via svo_amd's ctypes layer).
+Bar: bit-exact for the integer work (pyramid, FAST score map, keypoint lists,
+masks, bucket selection) and for the fixed-point LK / double PnP residuals
+against the oracle's EXACT accumulation mode; LK additionally within 0.1 px of
+the oracle's restatement of OpenCV's own (SSE) float accumulation order.
+"""
+import numpy as np
+import pytest
+
+import oracle as O
+import svo_amd as S
+from svo_amd.scene import Scene
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    return S.Context(0)
+
+
+def frames(w, h, seed=0, t0=0, t1=1):
+    sc = Scene(w, h, seed=seed)
+    return sc, sc.frame(t0), sc.frame(t1)
+
+
+# ------------------------------------------------------------------ pyramid
+@pytest.mark.parametrize("wh", [(1241, 376), (160, 120), (161, 121), (97, 33), (1920, 1080), (7, 5), (1, 1), (2, 3)])
+def test_pyramid_bit_exact(ctx, wh):
+    w, h = wh
+    rng = np.random.default_rng(w * 1000 + h)
+    img = rng.integers(0, 256, (h, w), dtype=np.uint8)
+    g = ctx.image(img, max_levels=4)
+    lvl = img
+    for l in range(5):
+        got = g.level(l)
+        assert got.shape == lvl.shape
+        assert np.array_equal(got, lvl), f"level {l} differs"
+        lvl = O.pyr_down(lvl)
+
+
+# ------------------------------------------------------------------ FAST
+@pytest.mark.parametrize("wh,seed", [((1241, 376), 0), ((160, 120), 3), ((64, 48), 5), ((3840, 2160), 1)])
+def test_fast_score_map_bit_exact(ctx, wh, seed):
+    sc, A, _ = frames(*wh, seed=seed)
+    g = ctx.image(A, 0)
+    for t in (0, 7, 20, 60):
+        s, c = ctx.fast_score_map(g, t)
+        so, co = O.fast_score(A, t)
+        assert np.array_equal(c, co), f"corner map differs at t={t}"
+        assert np.array_equal(s, so), f"score map differs at t={t}"
+
+
+@pytest.mark.parametrize("nonmax", [True, False])
+@pytest.mark.parametrize("wh,seed", [((1241, 376), 0), ((160, 120), 2), ((1920, 1080), 4)])
+def test_fast_keypoints_identical(ctx, wh, seed, nonmax):
+    sc, A, _ = frames(*wh, seed=seed)
+    g = ctx.image(A, 0)
+    det = S.FastFeatureDetector.create(ctx, 20, nonmax)
+    got = det.detect(g)
+    ref = O.fast(A, 20, nonmax)
+    assert got.shape == ref.shape
+    assert np.array_equal(got, ref)
+
+
+def test_fast_with_mask_identical(ctx):
+    sc, A, _ = frames(1241, 376, seed=0)
+    g = ctx.image(A, 0)
+    prev = O.fast(A, 20, True)[::3, :2] + np.float32(0.37)
+    m_gpu = ctx.mask_boxes(1241, 376, prev, 10.0)
+    m_ref = O.mask_boxes(1241, 376, prev, 10.0)
+    assert np.array_equal(m_gpu, m_ref)
+    got = ctx.fast_detect(g, 20, True, m_gpu)
+    ref = O.fast(A, 20, True, m_ref)
+    assert np.array_equal(got, ref)
+    assert len(ref) < len(O.fast(A, 20, True))
+
+
+def test_mask_boxes_edges(ctx):
+    pts = np.array([[0.5, 0.5], [10.5, 10.5], [-3.0, 5.0], [63.4, 47.6], [30.5, 20.5], [100, 100]], np.float32)
+    assert np.array_equal(ctx.mask_boxes(64, 48, pts, 10.0), O.mask_boxes(64, 48, pts, 10.0))
+
+
+def test_fast_threshold_extremes(ctx):
+    sc, A, _ = frames(160, 120, seed=9)
+    g = ctx.image(A, 0)
+    for t in (0, 1, 254, 255, 300, -5):
+        assert np.array_equal(ctx.fast_detect(g, t, True), O.fast(A, max(0, min(255, t)), True))
+
+
+# ------------------------------------------------------------------ bucket
+@pytest.mark.parametrize("B,k", [(50, 4), (37, 1), (64, 7), (100, 2)])
+def test_bucket_identical(ctx, B, k):
+    sc, A, _ = frames(1241, 376, seed=1)
+    kp = O.fast(A, 20, True)[:, :2]
+    ages = np.arange(len(kp), dtype=np.int32) % 5
+    for a in (None, ages):
+        gx, ga = ctx.bucket_features(kp, 1241, 376, B, k, a)
+        rx, ra = O.bucket(kp, 1241, 376, B, k, a)
+        assert np.array_equal(gx, rx)
+        assert np.array_equal(ga, ra)
+
+
+def test_bucket_empty(ctx):
+    gx, ga = ctx.bucket_features(np.zeros((0, 2), np.float32), 640, 480, 50, 4)
+    assert len(gx) == 0
+
+
+# ------------------------------------------------------------------ LK
+def _lk_pair(ctx, w, h, seed, npts, win, ml, crit, flags, t1=1):
+    sc, A, B = frames(w, h, seed=seed, t1=t1)
+    pts = O.fast(A, 20, True)[:npts, :2]
+    ga, gb = ctx.image(A, 6), ctx.image(B, 6)
+    got = ctx.calc_optical_flow_pyr_lk(ga, gb, pts, win_size=win, max_level=ml, criteria=crit, flags=flags)
+    ref = O.lk(A, B, pts, win, ml, crit, flags, acc=O.ACC_EXACT)
+    sse = O.lk(A, B, pts, win, ml, crit, flags, acc=O.ACC_SSE)
+    return sc, pts, got, ref, sse
+
+
+TEMPORAL = dict(win=(21, 21), ml=3, crit=(3, 50, 1e-3), flags=S.LK_GET_MIN_EIGENVALS)  # R:src/tracking.cpp:160-165
+STEREO = dict(win=(11, 11), ml=3, crit=(3, 30, 1e-3), flags=0)                        # R:src/tracking.cpp:101-105
+
+
+@pytest.mark.parametrize("cfg", [TEMPORAL, STEREO], ids=["temporal21", "stereo11"])
+@pytest.mark.parametrize("wh,seed,n", [((1241, 376), 0, 2000), ((160, 120), 1, 300), ((1920, 1080), 2, 4000)])
+def test_lk_bit_exact(ctx, cfg, wh, seed, n):
+    sc, pts, got, ref, sse = _lk_pair(ctx, *wh, seed, n, cfg["win"], cfg["ml"], cfg["crit"], cfg["flags"])
+    gn, gs, ge = got
+    rn, rs, re_, _ = ref
+    assert np.array_equal(gs, rs), f"status differs at {np.nonzero(gs != rs)[0][:10]}"
+    assert np.array_equal(gn.view(np.uint32), rn.view(np.uint32)), \
+        f"max |d| {np.abs(gn - rn).max()} at {np.argmax(np.abs(gn - rn).max(1))}"
+    assert np.array_equal(ge.view(np.uint32), re_.view(np.uint32))
+    # OpenCV's own float accumulation order (SSE path) is within 0.1 px
+    sn, ss, _, _ = sse
+    ok = (gs == 1) & (ss == 1)
+    assert np.abs(gn[ok] - sn[ok]).max() <= 0.1
+    assert (gs != ss).mean() < 0.002
+
+
+def test_lk_iteration_count_matches_oracle(ctx):
+    sc, A, B = frames(1241, 376, seed=0)
+    pts = O.fast(A, 20, True)[:1000, :2]
+    ga, gb = ctx.image(A, 4), ctx.image(B, 4)
+    ctx.calc_optical_flow_pyr_lk(ga, gb, pts, win_size=(21, 21), max_level=3, criteria=(3, 50, 1e-3),
+                                 flags=S.LK_GET_MIN_EIGENVALS)
+    _, _, _, it = O.lk(A, B, pts, (21, 21), 3, (3, 50, 1e-3), O.LK_GET_MIN_EIGENVALS)
+    assert ctx.lk_last_iterations() == int(it.sum())
+
+
+def test_lk_borders_and_out_of_image(ctx):
+    sc, A, B = frames(320, 240, seed=4)
+    rng = np.random.default_rng(0)
+    pts = np.concatenate([
+        rng.uniform(-40, 360, (400, 2)),                       # includes far outside
+        np.array([[0, 0], [319, 239], [-21, 5], [5, -21], [-20.5, 3], [339.9, 120], [160, 259.5]]),
+    ]).astype(np.float32)
+    ga, gb = ctx.image(A, 4), ctx.image(B, 4)
+    for cfg in (TEMPORAL, STEREO):
+        gn, gs, ge = ctx.calc_optical_flow_pyr_lk(ga, gb, pts, win_size=cfg["win"], max_level=cfg["ml"],
+                                                  criteria=cfg["crit"], flags=cfg["flags"])
+        rn, rs, re_, _ = O.lk(A, B, pts, cfg["win"], cfg["ml"], cfg["crit"], cfg["flags"])
+        assert np.array_equal(gs, rs)
+        assert np.array_equal(gn.view(np.uint32), rn.view(np.uint32))
+        assert np.array_equal(ge.view(np.uint32), re_.view(np.uint32))
+
+
+def test_lk_initial_flow_and_criteria(ctx):
+    sc, A, B = frames(640, 376, seed=6)
+    pts = O.fast(A, 20, True)[:500, :2]
+    guess = pts + np.float32(1.0)
+    ga, gb = ctx.image(A, 4), ctx.image(B, 4)
+    for crit in [(1, 5, 0.0), (2, 0, 0.5), (3, 200, 1e-6), (3, 10, 20.0)]:
+        for flags in (S.LK_USE_INITIAL_FLOW, S.LK_USE_INITIAL_FLOW | S.LK_GET_MIN_EIGENVALS):
+            gn, gs, ge = ctx.calc_optical_flow_pyr_lk(ga, gb, pts, next_pts=guess, win_size=(15, 9), max_level=2,
+                                                      criteria=crit, flags=flags, min_eig_threshold=1e-3)
+            rn, rs, re_, _ = O.lk(A, B, pts, (15, 9), 2, crit, flags, 1e-3, next_pts=guess)
+            assert np.array_equal(gs, rs)
+            assert np.array_equal(gn.view(np.uint32), rn.view(np.uint32))
+            assert np.array_equal(ge.view(np.uint32), re_.view(np.uint32))
+
+
+def test_lk_small_image_clamps_levels(ctx):
+    sc, A, B = frames(64, 48, seed=7)
+    pts = O.fast(A, 10, True)[:50, :2]
+    ga, gb = ctx.image(A, 5), ctx.image(B, 5)
+    gn, gs, ge = ctx.calc_optical_flow_pyr_lk(ga, gb, pts, win_size=(21, 21), max_level=5, criteria=(3, 30, 0.01))
+    rn, rs, re_, _ = O.lk(A, B, pts, (21, 21), 5, (3, 30, 0.01), 0)
+    assert np.array_equal(gs, rs)
+    assert np.array_equal(gn.view(np.uint32), rn.view(np.uint32))
+
+
+def test_lk_empty_and_bad_args(ctx):
+    sc, A, B = frames(64, 48)
+    ga, gb = ctx.image(A, 2), ctx.image(B, 2)
+    n, s, e = ctx.calc_optical_flow_pyr_lk(ga, gb, np.zeros((0, 2), np.float32))
+    assert len(n) == 0
+    with pytest.raises(S.SvoError):
+        ctx.calc_optical_flow_pyr_lk(ga, gb, np.ones((3, 2), np.float32), win_size=(2, 2))
+    with pytest.raises(S.SvoError):
+        ctx.calc_optical_flow_pyr_lk(ga, gb, np.ones((3, 2), np.float32), max_level=-1)
+
+
+# ------------------------------------------------------------------ PnP
+def _pnp_problem(n=2000, seed=0, outlier_frac=0.1):
+    sc = Scene(1241, 376, seed=seed)
+    rng = np.random.default_rng(seed)
+    pts0 = np.c_[rng.uniform(20, 1220, n), rng.uniform(20, 356, n)]
+    X = sc.map_points(pts0, 0)
+    uv = sc.project(X, 3) + rng.normal(0, 0.3, (n, 2))
+    out = rng.random(n) < outlier_frac
+    uv[out] += rng.uniform(60, 200, (out.sum(), 2)) * rng.choice([-1, 1], (out.sum(), 2))
+    return sc, X, uv.astype(np.float32), out
+
+
+def test_pnp_residuals_bit_exact(ctx):
+    sc, X, uv, _ = _pnp_problem()
+    rng = np.random.default_rng(1)
+    hyps = []
+    for _ in range(100):
+        rv = rng.normal(0, 0.01, 3)
+        R = O.rodrigues(rv)
+        t = rng.normal(0, 0.05, 3)
+        hyps.append(np.r_[R.ravel(), t])
+    hyps = np.array(hyps)
+    ge, gm, gc = ctx.pnp_residuals(X, uv, hyps, sc.K, 64.0)
+    re_, rm, rc = O.pnp_residuals(X, uv, hyps, sc.K, 64.0)
+    assert np.array_equal(ge.view(np.uint32), re_.view(np.uint32))
+    assert np.array_equal(gm, rm)
+    assert np.array_equal(gc, rc)
+
+
+def test_pnp_ransac_inliers_identical(ctx):
+    for seed in range(3):
+        sc, X, uv, out = _pnp_problem(seed=seed)
+        ok, rv, tv, inl = ctx.solve_pnp_ransac(X, uv, sc.K)
+        rc, rv_o, tv_o, inl_o, _ = O.solve_pnp_ransac(X, uv, sc.K)
+        assert ok and rc == 1
+        assert np.array_equal(inl, inl_o)
+        assert not np.isin(np.nonzero(out)[0], inl).any()
+        np.testing.assert_allclose(rv, rv_o, atol=1e-7)
+        np.testing.assert_allclose(tv, tv_o, atol=1e-6)
+        # the recovered pose is the true one (pure rotation, t = 0)
+        Rt = sc.R(3)
+        np.testing.assert_allclose(O.rodrigues(rv), Rt, atol=2e-3)
+
+
+def test_pnp_ransac_too_few_points(ctx):
+    with pytest.raises(S.SvoError):
+        ctx.solve_pnp_ransac(np.zeros((3, 3)), np.zeros((3, 2), np.float32), np.eye(3))
