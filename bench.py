@@ -1,0 +1,244 @@
+#!/usr/bin/env python3
+"""Benchmark: the reference's per-frame tracking step on MI355X.
+
+Metric (BASELINE.json): frames/sec @1241x376, 2000 feats; LK iters/sec; achieved
+HBM GB/s. A "step" = one frame of every sequence in the batch through
+pyramid(frame t) -> temporal LK (21x21, maxLevel 3, 50 it, MIN_EIGENVALS) ->
+status compaction -> solvePnPRansac (100 it, 8 px, 0.999: host EPnP + GPU
+scoring) -> outlier removal -> mask + FAST(20, NMS) -> top-up to 2000 features
+(R:src/tracking.cpp:240-269, keyframe-every-frame upper bound). Frames are
+synthetic KITTI-sized renders (svo_amd/scene.py), uploaded to HBM before the
+timed region. Multi-GPU: one process per GPU, each advancing its own batch of
+independent sequences (weak scaling, no collective on the data path).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--seq S] [--config kitti|1080p|4k]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+CONFIGS = {
+    # name: (W, H, n_features, max_level, workload label)   -- BASELINE.json configs[1..3]
+    "kitti": (1241, 376, 2000, 3, "1241x376 KITTI-size synthetic, 2000 feats, 3-level (maxLevel 3) pyr-LK 21x21"),
+    "1080p": (1920, 1080, 8000, 4, "1920x1080 synthetic, 8000 feats, maxLevel 4 pyr-LK 21x21"),
+    "4k": (3840, 2160, 16000, 3, "3840x2160 synthetic, 16000 feats, 21x21 LK, maxLevel 3"),
+}
+HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (guides/MI355X_MICROARCH.md)
+
+
+def lk_bytes_per_feature(levels: int, win: int = 21) -> int:
+    """B_lk per feature = L((win+3)^2 + (win+1)^2) + 21."""
+    return levels * ((win + 3) ** 2 + (win + 1) ** 2) + 21
+
+
+def frame_bytes(W: int, H: int, n: int, max_level: int, win: int = 21) -> int:
+    """B = B_pyr + B_fast + B_lk per frame."""
+    sizes = [(W, H)]
+    for _ in range(max_level):
+        w, h = sizes[-1]
+        sizes.append(((w + 1) // 2, (h + 1) // 2))
+    L = max_level + 1
+    b_pyr = sum(w * h for w, h in sizes[:-1]) + sum(w * h for w, h in sizes[1:])
+    return b_pyr + W * H + n * lk_bytes_per_feature(L, win)
+
+
+def dist_setup():
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist  # plumbing only: barrier + max over ranks
+        dist.init_process_group("gloo")
+    return world, rank, local, dist
+
+
+def barrier(dist):
+    if dist is not None:
+        dist.barrier()
+
+
+def allreduce_max(dist, v: float) -> float:
+    if dist is None:
+        return v
+    import torch
+    t = torch.tensor([v], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def allreduce_sum(dist, v: float) -> float:
+    if dist is None:
+        return v
+    import torch
+    t = torch.tensor([v], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    return float(t.item())
+
+
+def pmc_traffic(kernel_prefix: str):
+    """Per-launch HBM bytes of a kernel from a committed rocprofv3 PMC summary
+    (profiles/pmc_summary.json, written by tools/pmc_summary.py), or None."""
+    path = os.path.join(ROOT, "profiles", "pmc_summary.json")
+    try:
+        with open(path) as f:
+            d = json.load(f)
+        for k, v in d.get("kernels", {}).items():
+            if k.startswith(kernel_prefix):
+                return v.get("hbm_bytes_per_launch")
+    except Exception:
+        return None
+    return None
+
+
+def cpu_baseline(cfg_name: str, seconds: float):
+    """The oracle (CPU restatement of the reference's OpenCV path) timed on this
+    host on a bounded sample of the same workload: one sequence, frames until
+    `seconds` of CPU work; LK parallel over points (OpenMP), rest single-thread."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from oracle_loop import OracleLoop  # noqa: E402  (oracle: cpu_baseline leg only)
+    from svo_amd.scene import Scene
+    W, H, N, _, _ = CONFIGS[cfg_name]
+    sc = Scene(W, H, seed=101)
+    frames = [sc.frame(t) for t in range(64)]
+    loop = OracleLoop(sc, N, depth_seed=101).init(0)
+    loop.img = frames[0]
+    t0 = time.perf_counter()
+    n = 0
+    while time.perf_counter() - t0 < seconds and n < 63:
+        loop.step(n + 1, frames[n + 1])
+        n += 1
+    dt = time.perf_counter() - t0
+    cores = int(os.environ.get("OMP_NUM_THREADS", "0")) or (os.cpu_count() or 1)
+    return {"value": round(n / dt, 3), "unit": "frames/s", "cores": cores, "kind": "port",
+            "sample": f"{n} frames of one {W}x{H} sequence, {N} feats, {dt:.1f} s; oracle/ C restatement "
+                      f"of the OpenCV path (LK OpenMP over {cores} threads, FAST/PnP single-thread)"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--seq", type=int, default=64, help="independent sequences per GPU (batched launches)")
+    ap.add_argument("--config", default="kitti", choices=sorted(CONFIGS))
+    ap.add_argument("--threads", type=int, default=0, help="host RANSAC threads (0 = auto)")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-single", action="store_true")
+    args = ap.parse_args()
+
+    world, rank, local, dist = dist_setup()
+    import svo_amd as S
+    from svo_amd.scene import Scene
+
+    W, H, N, ML, label = CONFIGS[args.config]
+    Sq, K, Wm = args.seq, args.steps, args.warmup
+    T = Wm + K + 1
+    ctx = S.Context(local)
+    seeds = [rank * Sq + s + 1 for s in range(Sq)]
+    scenes = [Scene(W, H, seed=sd) for sd in seeds]
+    cfg = S.FrontendConfig(W, H, scenes[0].K, n_seq=Sq, n_frames=T, n_features=N, max_level=ML,
+                           host_threads=args.threads, timing=1)
+    fe = S.Frontend(ctx, cfg)
+    for s, sc in enumerate(scenes):
+        for t in range(T):
+            fe.set_frame(s, t, sc.frame(t), sc.R(t), depth_seed=sc.seed)
+    fe.init(0)
+    for t in range(1, Wm + 1):
+        fe.step(t)
+    fe.reset_times()
+    tot = {"lk_iterations": 0, "tracked": 0, "inliers": 0, "added": 0, "hypotheses": 0}
+    lk_units = 0
+    feats_prev = None
+    barrier(dist)
+    t0 = time.perf_counter()
+    for t in range(Wm + 1, Wm + K + 1):
+        st = fe.step(t).as_dict()
+        for k in tot:
+            tot[k] += st[k]
+        lk_units += st["tracked"] if feats_prev is None else feats_prev
+        feats_prev = st["features"]
+    barrier(dist)
+    dt = time.perf_counter() - t0
+    dt_max = allreduce_max(dist, dt)
+    frames = Sq * K * world
+    fps = frames / dt_max
+    lk_iters_total = allreduce_sum(dist, float(tot["lk_iterations"]))
+    phases = fe.phase_times()
+
+    if rank != 0:
+        return
+    # roofline of the dominant kernel (by device time): LK
+    lk_ms, lk_n = phases["lk"]
+    L = ML + 1
+    units_per_launch = lk_units / max(lk_n, 1)
+    bytes_per_launch = units_per_launch * lk_bytes_per_feature(L)
+    lk_avg_s = lk_ms / max(lk_n, 1) / 1e3
+    achieved = bytes_per_launch / lk_avg_s / 1e9 if lk_avg_s > 0 else 0.0
+    traffic = pmc_traffic("_ZN3svo12_GLOBAL__N_19lk_kernel")
+    dominant = max(phases, key=lambda k: phases[k][0])
+    single = None
+    if not args.no_single:
+        fe1 = S.Frontend(ctx, S.FrontendConfig(W, H, scenes[0].K, n_seq=1, n_frames=T, n_features=N, max_level=ML))
+        for t in range(T):
+            fe1.set_frame(0, t, scenes[0].frame(t), scenes[0].R(t), depth_seed=scenes[0].seed)
+        fe1.init(0)
+        for t in range(1, Wm + 1):
+            fe1.step(t)
+        t1 = time.perf_counter()
+        for t in range(Wm + 1, Wm + K + 1):
+            fe1.step(t)
+        single = K / (time.perf_counter() - t1)
+        fe1.close()
+    out = {
+        "metric": "frames/sec @1241x376, 2000 feats; LK iters/sec; achieved HBM GB/s",
+        "value": round(fps, 2),
+        "unit": "frames/s",
+        "n_gpus": world,
+        "steps": K,
+        "warmup": Wm,
+        "ms_per_step": round(dt_max / K * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u8/int32 fixed-point (LK sums exact int, solve f32), f64 PnP",
+        "data": "synthetic (rendered KITTI-size frames, seeded; no dataset on the box)",
+        "config": {"workload": label, "sequences_per_gpu": Sq, "global_batch": Sq * world,
+                   "features": N, "win": 21, "max_level": ML, "parallelism": f"{world} x independent sequences"},
+        "lk_iters_per_s": round(lk_iters_total / dt_max, 1),
+        "achieved_GBps_algorithmic": round(frames * frame_bytes(W, H, N, ML) / dt_max / 1e9, 2),
+        "single_stream_fps": round(single, 2) if single else None,
+        "phase_ms_per_step": {k: round(v[0] / K, 4) for k, v in phases.items()},
+        "stats_per_step": {k: round(v / K, 1) for k, v in tot.items()},
+        "roofline": {
+            "kernel": "lk_kernel (temporal LK, all levels, one wave per feature)",
+            "dominant_phase": dominant,
+            "bound": "hbm",
+            "achieved": round(achieved, 2),
+            "peak": HBM_PEAK_GBPS,
+            "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBPS, 4),
+            "traffic": traffic,
+            "algorithmic_bytes_per_launch": int(bytes_per_launch),
+            "units_per_launch": round(units_per_launch, 1),
+            "bytes_per_unit": lk_bytes_per_feature(L),
+            "avg_launch_us": round(lk_avg_s * 1e6, 3),
+        },
+    }
+    if not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(args.config, args.cpu_seconds)
+    print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -140,6 +140,70 @@ int svo_solve_pnp_ransac(svo_ctx* ctx, const double* obj_xyz, const float* img_x
                          double confidence, double rvec[3], double tvec[3], int* inliers,
                          int* n_inliers);
 
+/* ------------------------------------------------------------ batched front end
+ * The reference's per-frame loop (Tracking::startStereo, R:src/tracking.cpp:232-276:
+ * trackFrames -> calculatePose -> keyframe extractFeatures) for n_seq independent
+ * camera sequences advanced in lockstep: every kernel launch covers the whole
+ * batch, all state (pyramids, features, map points) stays in HBM, and only the
+ * RANSAC minimal solver (EPnP) runs on the host between GPU scoring launches.
+ * Map points of new features come from the synthetic scene's depth (stand-in for
+ * triangulateNewMapPoints, which needs a stereo pair: DESIGN.md). */
+typedef struct svo_frontend svo_frontend;
+
+typedef struct svo_frontend_config {
+    int width, height;      /* frame size */
+    int n_seq;              /* sequences per batch */
+    int n_frames;           /* frames kept resident per sequence */
+    int n_features;         /* features kept per frame (top-up target), e.g. 2000 */
+    int max_level;          /* LK maxLevel, R:src/tracking.cpp:163 -> 3 */
+    int win;                /* LK window, :163 -> 21 */
+    int lk_max_count;       /* :157 -> 50 */
+    double lk_epsilon;      /* :157 -> 1e-3 */
+    double min_eig;         /* OpenCV default 1e-4 */
+    int lk_flags;           /* :164 -> SVO_LK_GET_MIN_EIGENVALS */
+    int fast_threshold;     /* R:configs/config.yaml:30 -> 20 */
+    int fast_nonmax;        /* R:include/config_reader.h:37 -> 1 */
+    float mask_half;        /* R:src/tracking.cpp:78 -> 10 */
+    int bucket_size;        /* 0 = no bucketing (the reference never calls it) */
+    int per_bucket;
+    int pnp_iterations;     /* R:src/tracking.cpp:195 -> 100 */
+    float pnp_reproj;       /* -> 8.0 */
+    double pnp_confidence;  /* -> 0.999 */
+    double K[9];            /* camera matrix (float-rounded, as the Matx33f K) */
+    int host_threads;       /* RANSAC host threads; 0 = auto */
+    int timing;             /* 1 = record per-phase HIP events */
+} svo_frontend_config;
+
+typedef struct svo_frontend_stats {
+    int64_t lk_iterations;  /* GN iterations this step (all sequences, levels) */
+    int64_t tracked;        /* features with status 1 after LK */
+    int64_t inliers;        /* PnP inliers kept */
+    int64_t added;          /* new features from the keyframe top-up */
+    int64_t features;       /* features after the step */
+    int64_t hypotheses;     /* RANSAC hypotheses scored on the GPU */
+} svo_frontend_stats;
+
+int svo_frontend_create(svo_ctx* ctx, const svo_frontend_config* cfg, svo_frontend** out);
+void svo_frontend_destroy(svo_frontend* fe);
+/* Frame t of sequence seq: level 0 upload (H2D, untimed) + world->camera
+ * rotation of the synthetic scene and its depth seed (for new map points). */
+int svo_frontend_set_frame(svo_frontend* fe, int seq, int t, const uint8_t* gray, int stride,
+                           const double R[9], int depth_seed);
+/* Build every resident frame's pyramid now (else each step builds its own). */
+int svo_frontend_prebuild_pyramids(svo_frontend* fe);
+/* First keyframe: FAST (+bucket) on frame t0 of every sequence, map points. */
+int svo_frontend_init(svo_frontend* fe, int t0);
+/* One step: frame t-1 -> t for every sequence (pyramid of t, temporal LK,
+ * compaction, PnP RANSAC, outlier removal, masked FAST top-up). */
+int svo_frontend_step(svo_frontend* fe, int t, svo_frontend_stats* stats);
+int svo_frontend_pose(const svo_frontend* fe, int seq, double rvec[3], double tvec[3]);
+int svo_frontend_features(svo_frontend* fe, int seq, float* xy, int cap, int* n);
+/* Accumulated per-phase device time (ms) and launch counts since create/reset:
+ * phases: 0 pyramid, 1 lk, 2 compact, 3 gather, 4 pnp_score, 5 mask, 6 fast,
+ * 7 bucket, 8 append. Returns the number of phases. */
+int svo_frontend_phase_times(const svo_frontend* fe, double* ms, int64_t* launches, int cap);
+void svo_frontend_reset_times(svo_frontend* fe);
+
 /* ------------------------------------------------------------ synthetic input
  * Deterministic synthetic KITTI-like frames: a textured canvas
  * of random rectangles, box-blurred, seen through a rotating pinhole camera

@@ -306,8 +306,6 @@ int svo_oracle_lk(const uint8_t* prev, const uint8_t* next, int w, int h, int st
     svo_oracle_build_pyramid(prev, w, h, stride, win_w, win_h, ml, pp);
     svo_oracle_build_pyramid(next, w, h, stride, win_w, win_h, ml, np);
 
-    int16_t* IWin = (int16_t*)malloc(sizeof(int16_t) * (size_t)win_w * win_h);
-    int16_t* dIWin = (int16_t*)malloc(sizeof(int16_t) * 2 * (size_t)win_w * win_h);
     size_t off = total;
     for (int level = ml; level >= 0; level--) {
         off -= (size_t)lw[level] * lh[level];
@@ -315,11 +313,20 @@ int svo_oracle_lk(const uint8_t* prev, const uint8_t* next, int w, int h, int st
         make_padded(&I, pp + off, lw[level], lh[level], win_w, win_h);
         make_padded(&J, np + off, lw[level], lh[level], win_w, win_h);
         make_deriv(&I, pp + off);
-        for (int i = 0; i < npts; i++)
-            track_point(&I, &J, i, prev_xy, next_xy, status, err, win_w, win_h, max_count, epsilon,
-                        level, ml, flags, (float)min_eig_threshold, acc_mode, IWin, dIWin, iters_out);
+        /* cv::parallel_for_ over points (LKTrackerInvoker): points are independent */
+#pragma omp parallel
+        {
+            int16_t* IWin = (int16_t*)malloc(sizeof(int16_t) * (size_t)win_w * win_h);
+            int16_t* dIWin = (int16_t*)malloc(sizeof(int16_t) * 2 * (size_t)win_w * win_h);
+#pragma omp for schedule(dynamic, 64)
+            for (int i = 0; i < npts; i++)
+                track_point(&I, &J, i, prev_xy, next_xy, status, err, win_w, win_h, max_count, epsilon,
+                            level, ml, flags, (float)min_eig_threshold, acc_mode, IWin, dIWin, iters_out);
+            free(IWin);
+            free(dIWin);
+        }
         free(I.img); free(I.der); free(J.img);
     }
-    free(IWin); free(dIWin); free(pp); free(np);
+    free(pp); free(np);
     return ml;
 }

@@ -32,7 +32,7 @@ import numpy as np
 __all__ = [
     "SvoError", "lib", "Context", "Image", "FastFeatureDetector",
     "TERM_COUNT", "TERM_EPS", "LK_USE_INITIAL_FLOW", "LK_GET_MIN_EIGENVALS",
-    "synth_canvas", "synth_frame", "lib_path",
+    "synth_canvas", "synth_frame", "lib_path", "Frontend", "FrontendConfig", "FrontendStats",
 ]
 
 TERM_COUNT = 1
@@ -85,6 +85,16 @@ _SIGS = [
                                     _f32p, _u8p, _i32p]),
     ("svo_solve_pnp_ransac", C.c_int, [_vp, _f64p, _f32p, C.c_int, _f64p, C.c_int, C.c_float,
                                        C.c_double, _f64p, _f64p, _i32p, _i32p]),
+    ("svo_frontend_create", C.c_int, [_vp, _vp, C.POINTER(_vp)]),
+    ("svo_frontend_destroy", None, [_vp]),
+    ("svo_frontend_set_frame", C.c_int, [_vp, C.c_int, C.c_int, _u8p, C.c_int, _f64p, C.c_int]),
+    ("svo_frontend_prebuild_pyramids", C.c_int, [_vp]),
+    ("svo_frontend_init", C.c_int, [_vp, C.c_int]),
+    ("svo_frontend_step", C.c_int, [_vp, C.c_int, _vp]),
+    ("svo_frontend_pose", C.c_int, [_vp, C.c_int, _f64p, _f64p]),
+    ("svo_frontend_features", C.c_int, [_vp, C.c_int, _f32p, C.c_int, _i32p]),
+    ("svo_frontend_phase_times", C.c_int, [_vp, _f64p, C.POINTER(C.c_int64), C.c_int]),
+    ("svo_frontend_reset_times", None, [_vp]),
     ("svo_synth_canvas", C.c_int, [C.c_uint64, C.c_int, C.c_int, C.c_int, _u8p]),
     ("svo_synth_frame", C.c_int, [_u8p, C.c_int, C.c_int, C.c_int, C.c_int, _f64p, _f64p,
                                   C.c_uint64, C.c_int, _u8p, C.c_int, C.c_int]),
@@ -292,6 +302,107 @@ class Context:
                                                     float(confidence), _p(rvec, _f64p), _p(tvec, _f64p),
                                                     _p(inl, _i32p), C.byref(ninl)))
         return rc == 1, rvec, tvec, inl[: ninl.value].copy()
+
+
+class FrontendConfig(C.Structure):
+    """svo_frontend_config (include/svo_gpu.h); defaults = the reference's
+    temporal-tracking call (R:src/tracking.cpp:157-165), FAST params
+    (R:configs/config.yaml:29-32) and solvePnPRansac args (:191-196)."""
+    _fields_ = [
+        ("width", C.c_int), ("height", C.c_int), ("n_seq", C.c_int), ("n_frames", C.c_int),
+        ("n_features", C.c_int), ("max_level", C.c_int), ("win", C.c_int), ("lk_max_count", C.c_int),
+        ("lk_epsilon", C.c_double), ("min_eig", C.c_double), ("lk_flags", C.c_int),
+        ("fast_threshold", C.c_int), ("fast_nonmax", C.c_int), ("mask_half", C.c_float),
+        ("bucket_size", C.c_int), ("per_bucket", C.c_int), ("pnp_iterations", C.c_int),
+        ("pnp_reproj", C.c_float), ("pnp_confidence", C.c_double), ("K", C.c_double * 9),
+        ("host_threads", C.c_int), ("timing", C.c_int),
+    ]
+
+    def __init__(self, width, height, K, n_seq=1, n_frames=2, n_features=2000, **kw):
+        super().__init__()
+        d = dict(max_level=3, win=21, lk_max_count=50, lk_epsilon=1e-3, min_eig=1e-4,
+                 lk_flags=LK_GET_MIN_EIGENVALS, fast_threshold=20, fast_nonmax=1, mask_half=10.0,
+                 bucket_size=0, per_bucket=0, pnp_iterations=100, pnp_reproj=8.0, pnp_confidence=0.999,
+                 host_threads=0, timing=0)
+        d.update(kw)
+        self.width, self.height, self.n_seq, self.n_frames, self.n_features = width, height, n_seq, n_frames, n_features
+        for k, v in d.items():
+            setattr(self, k, v)
+        self.K[:] = [float(x) for x in np.asarray(K, np.float64).ravel()]
+
+
+class FrontendStats(C.Structure):
+    _fields_ = [("lk_iterations", C.c_int64), ("tracked", C.c_int64), ("inliers", C.c_int64),
+                ("added", C.c_int64), ("features", C.c_int64), ("hypotheses", C.c_int64)]
+
+    def as_dict(self):
+        return {k: int(getattr(self, k)) for k, _ in self._fields_}
+
+
+PHASES = ["pyramid", "lk", "compact", "gather", "pnp_score", "mask", "fast", "bucket", "append"]
+
+
+class Frontend:
+    """Batched tracking loop of Tracking::startStereo (R:src/tracking.cpp:232-276) over
+    n_seq independent sequences (svo_frontend_*)."""
+
+    def __init__(self, ctx: Context, cfg: FrontendConfig):
+        self.ctx, self.cfg = ctx, cfg
+        h = _vp()
+        ctx._check(lib().svo_frontend_create(ctx.handle, C.byref(cfg), C.byref(h)))
+        self.handle = h
+
+    def set_frame(self, seq, t, gray, R=None, depth_seed=0):
+        gray = _c(gray, np.uint8)
+        Rp = None
+        if R is not None:
+            R = _c(R, np.float64).reshape(9)
+            Rp = _p(R, _f64p)
+        self.ctx._check(lib().svo_frontend_set_frame(self.handle, seq, t, _p(gray, _u8p), gray.shape[1], Rp,
+                                                     int(depth_seed)))
+
+    def prebuild_pyramids(self):
+        self.ctx._check(lib().svo_frontend_prebuild_pyramids(self.handle))
+
+    def init(self, t0=0):
+        self.ctx._check(lib().svo_frontend_init(self.handle, t0))
+
+    def step(self, t) -> FrontendStats:
+        st = FrontendStats()
+        self.ctx._check(lib().svo_frontend_step(self.handle, t, C.byref(st)))
+        return st
+
+    def pose(self, seq):
+        r = np.zeros(3)
+        t = np.zeros(3)
+        self.ctx._check(lib().svo_frontend_pose(self.handle, seq, _p(r, _f64p), _p(t, _f64p)))
+        return r, t
+
+    def features(self, seq, cap=1 << 16):
+        xy = np.empty((cap, 2), np.float32)
+        n = C.c_int()
+        self.ctx._check(lib().svo_frontend_features(self.handle, seq, _p(xy, _f32p), cap, C.byref(n)))
+        return xy[: min(n.value, cap)].copy()
+
+    def phase_times(self):
+        ms = np.zeros(16)
+        n = np.zeros(16, np.int64)
+        k = lib().svo_frontend_phase_times(self.handle, _p(ms, _f64p), n.ctypes.data_as(C.POINTER(C.c_int64)), 16)
+        return {PHASES[i]: (float(ms[i]), int(n[i])) for i in range(k)}
+
+    def reset_times(self):
+        lib().svo_frontend_reset_times(self.handle)
+
+    def close(self):
+        if getattr(self, "handle", None):
+            lib().svo_frontend_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 class FastFeatureDetector:

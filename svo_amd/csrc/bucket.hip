@@ -24,13 +24,17 @@ __device__ __forceinline__ int bucket_of(float x, float y, int B, int nw) {
     return hi * nw + wi;
 }
 
-__global__ __launch_bounds__(1024) void bucket_kernel(const float* __restrict__ xy,
-                                                      const int* __restrict__ ages, int n, int B,
-                                                      int nh, int nw, int k,
-                                                      float* __restrict__ xy_out,
-                                                      int* __restrict__ ages_out, int cap,
-                                                      int* __restrict__ n_out,
-                                                      int* __restrict__ scr) {
+__global__ __launch_bounds__(1024) void bucket_kernel(BucketBatch Bt, int B, int nh, int nw, int k) {
+    const int seq = blockIdx.x;
+    const int n = Bt.in_counts ? min(Bt.in_counts[seq], Bt.in_cap) : Bt.n;
+    const int E = Bt.in_elem;
+    const float* __restrict__ xy = Bt.xy + (size_t)seq * Bt.in_cap * E;
+    const int* __restrict__ ages = Bt.ages ? Bt.ages + (size_t)seq * Bt.in_cap : nullptr;
+    float* __restrict__ xy_out = Bt.xy_out + 2 * (size_t)seq * Bt.out_cap;
+    int* __restrict__ ages_out = Bt.ages_out ? Bt.ages_out + (size_t)seq * Bt.out_cap : nullptr;
+    const int cap = Bt.out_cap;
+    int* __restrict__ n_out = Bt.n_out + seq;
+    int* __restrict__ scr = Bt.scr + (size_t)seq * Bt.scr_stride;
     const int nb = (nh + 1) * (nw + 1);
     const int npos = (nh + 1) * (nw + 1);
     int* cnt = scr;             // nb
@@ -47,7 +51,7 @@ __global__ __launch_bounds__(1024) void bucket_kernel(const float* __restrict__ 
             const int i = c0 + lane;
             int b = -1;
             if (i < n) {
-                b = bucket_of(xy[2 * i], xy[2 * i + 1], B, nw);
+                b = bucket_of(xy[E * i], xy[E * i + 1], B, nw);
                 if (b < 0 || b >= nb) b = -2;  // out of range: undefined in the reference, dropped
             }
             unsigned long long active = __ballot(b >= 0);
@@ -71,7 +75,7 @@ __global__ __launch_bounds__(1024) void bucket_kernel(const float* __restrict__ 
     for (int i = tid; i < n; i += 1024) {
         const int r = rank[i];
         if (r < 0) continue;
-        const int b = bucket_of(xy[2 * i], xy[2 * i + 1], B, nw);
+        const int b = bucket_of(xy[E * i], xy[E * i + 1], B, nw);
         const int m = cnt[b];
         if (r < k && !(r == 0 && m > k)) slot[(size_t)b * k + r] = i;
         if (m > k && r == m - 1) slot[(size_t)b * k] = i;
@@ -115,8 +119,8 @@ __global__ __launch_bounds__(1024) void bucket_kernel(const float* __restrict__ 
             const int o = off[q] + s;
             if (o >= cap) break;
             const int i = slot[(size_t)b * k + s];
-            xy_out[2 * o] = xy[2 * i];
-            xy_out[2 * o + 1] = xy[2 * i + 1];
+            xy_out[2 * o] = xy[E * i];
+            xy_out[2 * o + 1] = xy[E * i + 1];
             if (ages_out) ages_out[o] = ages ? ages[i] : 0;
         }
     }
@@ -124,12 +128,15 @@ __global__ __launch_bounds__(1024) void bucket_kernel(const float* __restrict__ 
 
 }  // namespace
 
-hipError_t launch_bucket(const float* xy, const int* ages, int n, int img_w, int img_h, int bucket,
-                         int per_bucket, float* xy_out, int* ages_out, int cap, int* n_out,
-                         int* scr, hipStream_t st) {
+size_t bucket_scratch_ints(int img_w, int img_h, int bucket, int per_bucket, int n) {
+    const size_t nb = (size_t)(img_h / bucket + 1) * (img_w / bucket + 1);
+    return nb + nb * per_bucket + (size_t)n + nb + 1;
+}
+
+hipError_t launch_bucket(const BucketBatch& b, int nseq, int img_w, int img_h, int bucket, int per_bucket,
+                         hipStream_t st) {
     const int nh = img_h / bucket, nw = img_w / bucket;
-    hipLaunchKernelGGL(bucket_kernel, dim3(1), dim3(1024), 0, st, xy, ages, n, bucket, nh, nw,
-                       per_bucket, xy_out, ages_out, cap, n_out, scr);
+    hipLaunchKernelGGL(bucket_kernel, dim3(nseq), dim3(1024), 0, st, b, bucket, nh, nw, per_bucket);
     return hipGetLastError();
 }
 

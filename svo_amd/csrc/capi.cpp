@@ -56,6 +56,15 @@ void* pinned(svo_ctx* ctx, size_t bytes) {
     return ctx->pinned;
 }
 
+// Upload one pyramid descriptor to device scratch slot 3's head (single-image calls).
+static PyrDesc* stage_desc(svo_ctx* ctx, const svo_image* img, void* dst) {
+    PyrDesc* h = (PyrDesc*)pinned(ctx, sizeof(PyrDesc));
+    if (!h || hipStreamSynchronize(ctx->stream) != hipSuccess) return nullptr;
+    *h = img->desc;
+    if (hipMemcpyAsync(dst, h, sizeof(PyrDesc), hipMemcpyHostToDevice, ctx->stream) != hipSuccess) return nullptr;
+    return (PyrDesc*)dst;
+}
+
 }  // namespace svo
 
 using namespace svo;
@@ -182,9 +191,12 @@ int svo_fast_score_map(svo_ctx* ctx, const svo_image* img, int threshold, uint8_
     threshold = threshold < 0 ? 0 : threshold > 255 ? 255 : threshold;
     const ImgLevel& L = img->desc.lv[0];
     size_t npx = (size_t)L.w * L.h;
-    uint16_t* cs = (uint16_t*)scratch(ctx, 0, npx * 2);
+    uint16_t* cs = (uint16_t*)scratch(ctx, 0, npx * 2 + 1024);
     if (!cs) return set_error(ctx, SVO_ERR_HIP, "scratch alloc");
-    SVO_HIP(ctx, launch_fast_score(L, threshold, 1, cs, ctx->stream));
+    PyrDesc* dd = stage_desc(ctx, img, (char*)cs + ((npx * 2 + 255) & ~(size_t)255));
+    if (!dd) return set_error(ctx, SVO_ERR_HIP, "desc staging");
+    FastBatch b{dd, cs, nullptr, nullptr, nullptr, nullptr, npx, 0};
+    SVO_HIP(ctx, launch_fast_score(b, 1, L.w, L.h, threshold, 1, ctx->stream));
     std::vector<uint16_t> h(npx);
     SVO_HIP(ctx, hipMemcpyAsync(h.data(), cs, npx * 2, hipMemcpyDeviceToHost, ctx->stream));
     SVO_HIP(ctx, hipStreamSynchronize(ctx->stream));
@@ -202,7 +214,7 @@ int svo_fast_detect(svo_ctx* ctx, const svo_image* img, int threshold, int nonma
     threshold = threshold < 0 ? 0 : threshold > 255 ? 255 : threshold;
     const ImgLevel& L = img->desc.lv[0];
     size_t npx = (size_t)L.w * L.h;
-    uint16_t* cs = (uint16_t*)scratch(ctx, 0, npx * 2);
+    uint16_t* cs = (uint16_t*)scratch(ctx, 0, npx * 2 + 1024);
     int* rowcnt = (int*)scratch(ctx, 1, sizeof(int) * ((size_t)L.h + 16));
     uint8_t* dmask = mask ? (uint8_t*)scratch(ctx, 2, npx) : nullptr;
     int kcap = cap > 0 ? cap : 1;
@@ -210,8 +222,11 @@ int svo_fast_detect(svo_ctx* ctx, const svo_image* img, int threshold, int nonma
     int* dn = (int*)((char*)dout + sizeof(svo_keypoint) * (size_t)kcap);
     if (!cs || !rowcnt || (mask && !dmask) || !dout) return set_error(ctx, SVO_ERR_HIP, "scratch alloc");
     if (mask) SVO_HIP(ctx, hipMemcpyAsync(dmask, mask, npx, hipMemcpyHostToDevice, ctx->stream));
-    SVO_HIP(ctx, launch_fast_score(L, threshold, nonmax ? 1 : 0, cs, ctx->stream));
-    SVO_HIP(ctx, launch_fast_collect(L, cs, nonmax ? 1 : 0, dmask, rowcnt, dout, cap, dn, ctx->stream));
+    PyrDesc* dd = stage_desc(ctx, img, (char*)cs + ((npx * 2 + 255) & ~(size_t)255));
+    if (!dd) return set_error(ctx, SVO_ERR_HIP, "desc staging");
+    FastBatch b{dd, cs, dmask, rowcnt, dout, dn, npx, cap};
+    SVO_HIP(ctx, launch_fast_score(b, 1, L.w, L.h, threshold, nonmax ? 1 : 0, ctx->stream));
+    SVO_HIP(ctx, launch_fast_collect(b, 1, L.w, L.h, nonmax ? 1 : 0, ctx->stream));
     int n = 0;
     SVO_HIP(ctx, hipMemcpyAsync(&n, dn, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
     SVO_HIP(ctx, hipStreamSynchronize(ctx->stream));
@@ -230,7 +245,7 @@ int svo_mask_boxes(svo_ctx* ctx, int w, int h, const float* pts_xy, int n, float
     float* dpts = (float*)scratch(ctx, 4, sizeof(float) * 2 * (size_t)(n > 0 ? n : 1));
     if (!dmask || !dpts) return set_error(ctx, SVO_ERR_HIP, "scratch alloc");
     if (n > 0) SVO_HIP(ctx, hipMemcpyAsync(dpts, pts_xy, sizeof(float) * 2 * n, hipMemcpyHostToDevice, ctx->stream));
-    SVO_HIP(ctx, launch_mask_boxes(w, h, dpts, n, half, dmask, ctx->stream));
+    SVO_HIP(ctx, launch_mask_boxes(w, h, dpts, nullptr, n, n, 1, half, dmask, ctx->stream));
     SVO_HIP(ctx, hipMemcpyAsync(mask, dmask, npx, hipMemcpyDeviceToHost, ctx->stream));
     SVO_HIP(ctx, hipStreamSynchronize(ctx->stream));
     return SVO_OK;
@@ -245,8 +260,8 @@ int svo_bucket_features(svo_ctx* ctx, const float* xy, const int* ages, int n, i
         return set_error(ctx, SVO_ERR_ARG, "svo_bucket_features: bad arguments");
     const int nh = img_h / bucket_size, nw = img_w / bucket_size;
     if (nw <= 0) return set_error(ctx, SVO_ERR_ARG, "svo_bucket_features: bucket wider than image");
-    const size_t nb = (size_t)(nh + 1) * (nw + 1);
-    size_t scr_ints = nb + nb * per_bucket + (size_t)n + nb + 1;
+    (void)nh;
+    size_t scr_ints = bucket_scratch_ints(img_w, img_h, bucket_size, per_bucket, n);
     int* scr = (int*)scratch(ctx, 5, sizeof(int) * scr_ints);
     int ncap = cap > 0 ? cap : 1;
     char* io = (char*)scratch(ctx, 6, sizeof(float) * 2 * ((size_t)n + ncap) + sizeof(int) * ((size_t)n + ncap) + 256);
@@ -260,8 +275,8 @@ int svo_bucket_features(svo_ctx* ctx, const float* xy, const int* ages, int n, i
         SVO_HIP(ctx, hipMemcpyAsync(dxy, xy, sizeof(float) * 2 * n, hipMemcpyHostToDevice, ctx->stream));
         if (ages) SVO_HIP(ctx, hipMemcpyAsync(dages, ages, sizeof(int) * n, hipMemcpyHostToDevice, ctx->stream));
     }
-    SVO_HIP(ctx, launch_bucket(dxy, ages ? dages : nullptr, n, img_w, img_h, bucket_size, per_bucket,
-                               dxy_out, dages_out, cap, dn, scr, ctx->stream));
+    BucketBatch bb{dxy, 2, n, nullptr, n, ages ? dages : nullptr, dxy_out, dages_out, cap, dn, scr, scr_ints};
+    SVO_HIP(ctx, launch_bucket(bb, 1, img_w, img_h, bucket_size, per_bucket, ctx->stream));
     int tot = 0;
     SVO_HIP(ctx, hipMemcpyAsync(&tot, dn, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
     SVO_HIP(ctx, hipStreamSynchronize(ctx->stream));
@@ -307,9 +322,11 @@ int svo_calc_optical_flow_pyr_lk(svo_ctx* ctx, const svo_image* prev, const svo_
     p.flags = flags;
     p.min_eig = (float)min_eig_threshold;
     p.want_err = err ? 1 : 0;
-    size_t bytes = (size_t)n * (8 + 8 + 1 + 4 + 4) + 256;
+    size_t bytes = (size_t)n * (8 + 8 + 1 + 4 + 4) + 2 * sizeof(PyrDesc) + 512;
     char* d = (char*)scratch(ctx, 7, bytes);
     if (!d) return set_error(ctx, SVO_ERR_HIP, "scratch alloc");
+    PyrDesc* ddesc = (PyrDesc*)d;
+    d += (2 * sizeof(PyrDesc) + 255) & ~(size_t)255;
     float* dprev = (float*)d;
     float* dnext = dprev + 2 * (size_t)n;
     float* derr = dnext + 2 * (size_t)n;
@@ -318,8 +335,14 @@ int svo_calc_optical_flow_pyr_lk(svo_ctx* ctx, const svo_image* prev, const svo_
     SVO_HIP(ctx, hipMemcpyAsync(dprev, prev_xy, sizeof(float) * 2 * n, hipMemcpyHostToDevice, ctx->stream));
     if (flags & SVO_LK_USE_INITIAL_FLOW)
         SVO_HIP(ctx, hipMemcpyAsync(dnext, next_xy, sizeof(float) * 2 * n, hipMemcpyHostToDevice, ctx->stream));
-    SVO_HIP(ctx, launch_lk(prev->desc, next->desc, dprev, dnext, dst, err ? derr : nullptr, diters, n, p,
-                           ctx->stream));
+    PyrDesc* hdesc = (PyrDesc*)pinned(ctx, 2 * sizeof(PyrDesc));
+    if (!hdesc) return set_error(ctx, SVO_ERR_HIP, "pinned alloc");
+    SVO_HIP(ctx, hipStreamSynchronize(ctx->stream));  // pinned staging is reused
+    hdesc[0] = prev->desc;
+    hdesc[1] = next->desc;
+    SVO_HIP(ctx, hipMemcpyAsync(ddesc, hdesc, 2 * sizeof(PyrDesc), hipMemcpyHostToDevice, ctx->stream));
+    LKBatch b{ddesc, ddesc + 1, dprev, dnext, dst, err ? derr : nullptr, diters, nullptr, n, n};
+    SVO_HIP(ctx, launch_lk(b, 1, n, p, ctx->stream));
     std::vector<int> it(n);
     SVO_HIP(ctx, hipMemcpyAsync(next_xy, dnext, sizeof(float) * 2 * n, hipMemcpyDeviceToHost, ctx->stream));
     SVO_HIP(ctx, hipMemcpyAsync(status, dst, n, hipMemcpyDeviceToHost, ctx->stream));
@@ -360,8 +383,8 @@ int svo_pnp_residuals(svo_ctx* ctx, const float* obj_xyz, const float* img_xy, i
     SVO_HIP(ctx, hipMemcpyAsync(dh, hyp_Rt, sizeof(double) * 12 * m, hipMemcpyHostToDevice, ctx->stream));
     SVO_HIP(ctx, hipMemcpyAsync(dobj, obj_xyz, sizeof(float) * 3 * n, hipMemcpyHostToDevice, ctx->stream));
     SVO_HIP(ctx, hipMemcpyAsync(dimg, img_xy, sizeof(float) * 2 * n, hipMemcpyHostToDevice, ctx->stream));
-    SVO_HIP(ctx, launch_pnp_residuals(dobj, dimg, n, dh, m, K[0], K[4], K[2], K[5], thresh2, derr, dbits,
-                                      dcnt, ctx->stream));
+    PnpBatch b{dobj, dimg, nullptr, n, n, dh, m, derr, dbits, words, dcnt};
+    SVO_HIP(ctx, launch_pnp_residuals(b, 1, n, K[0], K[4], K[2], K[5], thresh2, ctx->stream));
     std::vector<uint32_t> bits((size_t)words * m);
     SVO_HIP(ctx, hipMemcpyAsync(bits.data(), dbits, sizeof(uint32_t) * bits.size(), hipMemcpyDeviceToHost, ctx->stream));
     if (counts) SVO_HIP(ctx, hipMemcpyAsync(counts, dcnt, sizeof(int) * m, hipMemcpyDeviceToHost, ctx->stream));

@@ -72,13 +72,28 @@ void* pinned(svo_ctx* ctx, size_t bytes);
 
 // Kernel launchers (implemented in the .hip files).
 hipError_t launch_pyramid(const svo_image* img, int first_level, hipStream_t st);
-hipError_t launch_fast_score(const ImgLevel& L, int threshold, int nonmax, uint16_t* cs,
+hipError_t launch_pyramid_batched(const PyrDesc* d_descs, int nseq, int w, int h, int nlevels,
+                                  hipStream_t st);
+
+// Batched FAST: sequence z reads level 0 of descs[z]; per-sequence slices of
+// cs/mask (npx each), rowcnt (h each), out (cap each), n_out (1 each).
+struct FastBatch {
+    const PyrDesc* descs;
+    uint16_t* cs;
+    const uint8_t* mask;  // nullable
+    int* rowcnt;
+    svo_keypoint* out;
+    int* n_out;
+    size_t npx;
+    int cap;
+};
+hipError_t launch_fast_score(const FastBatch& b, int nseq, int w, int h, int threshold, int nonmax,
                              hipStream_t st);
-hipError_t launch_fast_collect(const ImgLevel& L, const uint16_t* cs, int nonmax,
-                               const uint8_t* mask, int* rowcnt, svo_keypoint* out, int cap,
-                               int* n_out, hipStream_t st);
-hipError_t launch_mask_boxes(int w, int h, const float* pts, int n, float half, uint8_t* mask,
-                             hipStream_t st);
+hipError_t launch_fast_collect(const FastBatch& b, int nseq, int w, int h, int nonmax, hipStream_t st);
+// Masks for nseq sequences (w*h each): 255 + filled boxes around counts[s] (or n)
+// points of pts + s*pts_stride.
+hipError_t launch_mask_boxes(int w, int h, const float* pts, const int* counts, int n, int pts_stride,
+                             int nseq, float half, uint8_t* mask, hipStream_t st);
 
 struct LKParams {
     int win_w, win_h;
@@ -89,19 +104,58 @@ struct LKParams {
     float min_eig;
     int want_err;
 };
-// Single-sequence LK over device arrays.
-hipError_t launch_lk(const PyrDesc& prev, const PyrDesc& next, const float* prev_xy, float* next_xy,
-                     uint8_t* status, float* err, int* iters, int n, const LKParams& p,
-                     hipStream_t st);
+// Batched LK: blockIdx.y = sequence; sequence s owns points [s*cap, s*cap + n_s)
+// of every array, n_s = counts[s] (device) or n when counts is null.
+struct LKBatch {
+    const PyrDesc* prev;  // [nseq] device
+    const PyrDesc* next;  // [nseq] device
+    const float* prev_xy;
+    float* next_xy;
+    uint8_t* status;
+    float* err;   // nullable
+    int* iters;   // nullable
+    const int* counts;  // nullable
+    int n, cap;
+};
+hipError_t launch_lk(const LKBatch& b, int nseq, int max_n, const LKParams& p, hipStream_t st);
 bool lk_supported(int win_w, int win_h);
 
-hipError_t launch_pnp_residuals(const float* obj, const float* img, int n, const double* hyp,
-                                int m, double fx, double fy, double cx, double cy, float thresh2,
-                                float* err, uint32_t* bits, int* counts, hipStream_t st);
+// Batched residual scoring: blockIdx.z = sequence, blockIdx.y = hypothesis.
+// Sequence s: obj/img points [s*cap, s*cap + n_s), hypotheses [s*m, s*m + m),
+// err rows of cap floats, bits rows of words_cap words, cnt per hypothesis.
+struct PnpBatch {
+    const float* obj;
+    const float* img;
+    const int* counts;  // nullable -> n
+    int n, cap;
+    const double* hyp;
+    int m;
+    float* err;      // nullable
+    uint32_t* bits;  // nullable
+    int words_cap;
+    int* cnt;        // nullable
+};
+hipError_t launch_pnp_residuals(const PnpBatch& b, int nseq, int max_n, double fx, double fy, double cx,
+                                double cy, float thresh2, hipStream_t st);
 
-hipError_t launch_bucket(const float* xy, const int* ages, int n, int img_w, int img_h,
-                         int bucket, int per_bucket, float* xy_out, int* ages_out, int cap,
-                         int* n_out, int* scratch_counts, hipStream_t st);
+// Batched bucket selection: blockIdx.x = sequence. Input points are in_elem
+// floats apart (2 = xy pairs, 3 = svo_keypoint), in_cap per sequence.
+struct BucketBatch {
+    const float* xy;
+    int in_elem, in_cap;
+    const int* in_counts;  // nullable -> n
+    int n;
+    const int* ages;  // nullable
+    float* xy_out;
+    int* ages_out;  // nullable
+    int out_cap;
+    int* n_out;
+    int* scr;
+    size_t scr_stride;
+};
+size_t bucket_scratch_ints(int img_w, int img_h, int bucket, int per_bucket, int n);
+hipError_t launch_bucket(const BucketBatch& b, int nseq, int img_w, int img_h, int bucket, int per_bucket,
+                         hipStream_t st);
 
 }  // namespace svo
 

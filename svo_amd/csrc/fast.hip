@@ -39,10 +39,12 @@ __device__ __forceinline__ bool run9(unsigned m16) {
     return (r & 0xFFFFu) != 0;
 }
 
-__global__ __launch_bounds__(256) void fast_score_kernel(const uint8_t* __restrict__ img, int w,
-                                                         int h, int pitch, int threshold,
-                                                         int want_score,
-                                                         uint16_t* __restrict__ cs) {
+__global__ __launch_bounds__(256) void fast_score_kernel(FastBatch B, int threshold,
+                                                         int want_score) {
+    const ImgLevel L = B.descs[blockIdx.z].lv[0];
+    const uint8_t* __restrict__ img = L.data;
+    const int w = L.w, h = L.h, pitch = L.pitch;
+    uint16_t* __restrict__ cs = B.cs + (size_t)blockIdx.z * B.npx;
     __shared__ uint8_t T[FT_IH][FT_IW + 2];
     const int x0 = blockIdx.x * FT_TX, y0 = blockIdx.y * FT_TY;
     const int tid = threadIdx.x;
@@ -128,11 +130,11 @@ __device__ __forceinline__ bool fast_keep(const uint16_t* __restrict__ cs, int w
     return true;
 }
 
-__global__ __launch_bounds__(256) void fast_count_kernel(const uint16_t* __restrict__ cs, int w,
-                                                         int h, int nonmax,
-                                                         const uint8_t* __restrict__ mask,
-                                                         int* __restrict__ rowcnt) {
+__global__ __launch_bounds__(256) void fast_count_kernel(FastBatch B, int w, int h, int nonmax) {
     const int y = blockIdx.x;
+    const uint16_t* __restrict__ cs = B.cs + (size_t)blockIdx.y * B.npx;
+    const uint8_t* __restrict__ mask = B.mask ? B.mask + (size_t)blockIdx.y * B.npx : nullptr;
+    int* __restrict__ rowcnt = B.rowcnt + (size_t)blockIdx.y * h;
     __shared__ int wsum[4];
     int cnt = 0;
     if (y >= 3 && y < h - 3)
@@ -143,13 +145,14 @@ __global__ __launch_bounds__(256) void fast_count_kernel(const uint16_t* __restr
     if (threadIdx.x == 0) rowcnt[y] = wsum[0] + wsum[1] + wsum[2] + wsum[3];
 }
 
-__global__ __launch_bounds__(256) void fast_write_kernel(const uint16_t* __restrict__ cs, int w,
-                                                         int h, int nonmax,
-                                                         const uint8_t* __restrict__ mask,
-                                                         const int* __restrict__ rowcnt,
-                                                         svo_keypoint* __restrict__ out, int cap,
-                                                         int* __restrict__ n_out) {
+__global__ __launch_bounds__(256) void fast_write_kernel(FastBatch B, int w, int h, int nonmax) {
     const int y = blockIdx.x;
+    const uint16_t* __restrict__ cs = B.cs + (size_t)blockIdx.y * B.npx;
+    const uint8_t* __restrict__ mask = B.mask ? B.mask + (size_t)blockIdx.y * B.npx : nullptr;
+    const int* __restrict__ rowcnt = B.rowcnt + (size_t)blockIdx.y * h;
+    svo_keypoint* __restrict__ out = B.out + (size_t)blockIdx.y * B.cap;
+    const int cap = B.cap;
+    int* __restrict__ n_out = B.n_out + blockIdx.y;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     __shared__ int wsum[4];
     __shared__ int base_s;
@@ -190,11 +193,15 @@ __global__ __launch_bounds__(256) void fast_write_kernel(const uint16_t* __restr
     }
 }
 
-__global__ __launch_bounds__(64) void mask_boxes_kernel(int w, int h, const float* __restrict__ pts,
-                                                        int n, float half,
-                                                        uint8_t* __restrict__ mask) {
+__global__ __launch_bounds__(64) void mask_boxes_kernel(int w, int h, const float* __restrict__ pts_all,
+                                                        const int* __restrict__ counts, int n0,
+                                                        int pts_stride, float half,
+                                                        uint8_t* __restrict__ mask_all) {
     const int i = blockIdx.x;
+    const int n = counts ? counts[blockIdx.y] : n0;
     if (i >= n) return;
+    const float* __restrict__ pts = pts_all + 2 * (size_t)blockIdx.y * pts_stride;
+    uint8_t* __restrict__ mask = mask_all + (size_t)blockIdx.y * w * h;
     const float px = pts[2 * i], py = pts[2 * i + 1];
     // cv::rectangle(Point2f -> Point via cvRound, FILLED, inclusive, clipped)
     int xa = (int)__builtin_rintf(px - half), ya = (int)__builtin_rintf(py - half);
@@ -214,29 +221,25 @@ __global__ __launch_bounds__(64) void mask_boxes_kernel(int w, int h, const floa
 
 }  // namespace
 
-hipError_t launch_fast_score(const ImgLevel& L, int threshold, int nonmax, uint16_t* cs,
+hipError_t launch_fast_score(const FastBatch& b, int nseq, int w, int h, int threshold, int nonmax,
                              hipStream_t st) {
-    dim3 grid((L.w + FT_TX - 1) / FT_TX, (L.h + FT_TY - 1) / FT_TY);
-    hipLaunchKernelGGL(fast_score_kernel, grid, dim3(256), 0, st, L.data, L.w, L.h, L.pitch,
-                       threshold, nonmax, cs);
+    dim3 grid((w + FT_TX - 1) / FT_TX, (h + FT_TY - 1) / FT_TY, nseq);
+    hipLaunchKernelGGL(fast_score_kernel, grid, dim3(256), 0, st, b, threshold, nonmax);
     return hipGetLastError();
 }
 
-hipError_t launch_fast_collect(const ImgLevel& L, const uint16_t* cs, int nonmax,
-                               const uint8_t* mask, int* rowcnt, svo_keypoint* out, int cap,
-                               int* n_out, hipStream_t st) {
-    hipLaunchKernelGGL(fast_count_kernel, dim3(L.h), dim3(256), 0, st, cs, L.w, L.h, nonmax, mask,
-                       rowcnt);
-    hipLaunchKernelGGL(fast_write_kernel, dim3(L.h), dim3(256), 0, st, cs, L.w, L.h, nonmax, mask,
-                       rowcnt, out, cap, n_out);
+hipError_t launch_fast_collect(const FastBatch& b, int nseq, int w, int h, int nonmax, hipStream_t st) {
+    hipLaunchKernelGGL(fast_count_kernel, dim3(h, nseq), dim3(256), 0, st, b, w, h, nonmax);
+    hipLaunchKernelGGL(fast_write_kernel, dim3(h, nseq), dim3(256), 0, st, b, w, h, nonmax);
     return hipGetLastError();
 }
 
-hipError_t launch_mask_boxes(int w, int h, const float* pts, int n, float half, uint8_t* mask,
-                             hipStream_t st) {
-    hipError_t e = hipMemsetAsync(mask, 255, (size_t)w * h, st);
+hipError_t launch_mask_boxes(int w, int h, const float* pts, const int* counts, int n, int pts_stride,
+                             int nseq, float half, uint8_t* mask, hipStream_t st) {
+    hipError_t e = hipMemsetAsync(mask, 255, (size_t)w * h * nseq, st);
     if (e != hipSuccess) return e;
-    if (n > 0) hipLaunchKernelGGL(mask_boxes_kernel, dim3(n), dim3(64), 0, st, w, h, pts, n, half, mask);
+    if (n > 0) hipLaunchKernelGGL(mask_boxes_kernel, dim3(n, nseq), dim3(64), 0, st, w, h, pts, counts, n,
+                                  pts_stride, half, mask);
     return hipGetLastError();
 }
 

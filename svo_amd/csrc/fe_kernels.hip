@@ -1,0 +1,148 @@
+// Batched device-side glue of the tracking loop (R:src/tracking.cpp:240-269):
+// stable compaction of tracked / inlier features, map-point gather for PnP,
+// and keyframe top-up with new map points. One launch covers every sequence of
+// the batch (blockIdx = sequence), so a frame step costs the same number of
+// launches for 1 or 512 sequences.
+#include "frontend.hpp"
+
+namespace svo {
+
+namespace {
+
+// Stable order-preserving compaction of features [0, n_in[s]) of sequence s
+// (one 1024-thread block per sequence). keep = status[i] (u8) or bit i of bits.
+__global__ __launch_bounds__(1024) void compact_kernel(CompactBatch B) {
+    const int s = blockIdx.x;
+    const int n = B.n_in[s];
+    const size_t o = (size_t)s * B.cap;
+    __shared__ int wsum[16];
+    __shared__ int base_s;
+    __shared__ long long it_s;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    if (tid == 0) {
+        base_s = 0;
+        it_s = 0;
+    }
+    __syncthreads();
+    long long it = 0;
+    for (int c0 = 0; c0 < n; c0 += 1024) {
+        const int i = c0 + tid;
+        bool keep = false;
+        if (i < n) {
+            keep = B.status ? B.status[o + i] != 0 : ((B.bits[(size_t)s * B.words_cap + (i >> 5)] >> (i & 31)) & 1u);
+            if (B.iters) it += B.iters[o + i];
+        }
+        const unsigned long long bal = __ballot(keep);
+        if (lane == 0) wsum[wv] = __popcll(bal);
+        __syncthreads();
+        int off = base_s;
+        for (int k = 0; k < wv; k++) off += wsum[k];
+        if (keep) {
+            const int d = off + __popcll(bal & ((1ull << lane) - 1ull));
+            B.xy_out[2 * (o + d)] = B.xy_in[2 * (o + i)];
+            B.xy_out[2 * (o + d) + 1] = B.xy_in[2 * (o + i) + 1];
+            B.mid_out[o + d] = B.mid_in[o + i];
+        }
+        __syncthreads();
+        if (tid == 0) {
+            int tot = 0;
+            for (int k = 0; k < 16; k++) tot += wsum[k];
+            base_s += tot;
+        }
+        __syncthreads();
+    }
+    if (B.iters) {
+        for (int off = 32; off > 0; off >>= 1) it += __shfl_xor(it, off);
+        if (lane == 0) atomicAdd((unsigned long long*)&it_s, (unsigned long long)it);
+    }
+    __syncthreads();
+    if (tid == 0) {
+        B.n_out[s] = base_s;
+        if (B.iters_sum) B.iters_sum[s] = it_s;
+    }
+}
+
+// obj[s][i] = (float) map[s][mid[s][i]]  (solvePnPRansac converts Point3d to CV_32F)
+__global__ __launch_bounds__(256) void gather_kernel(const int* __restrict__ n, const int* __restrict__ mid,
+                                                     const double* __restrict__ map, int cap, int map_cap,
+                                                     float* __restrict__ obj) {
+    const int s = blockIdx.y;
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= n[s]) return;
+    const size_t o = (size_t)s * cap + i;
+    const double* X = map + 3 * ((size_t)s * map_cap + mid[o]);
+    obj[3 * o] = (float)X[0];
+    obj[3 * o + 1] = (float)X[1];
+    obj[3 * o + 2] = (float)X[2];
+}
+
+// Keyframe top-up: append the first (n_target - n) candidates (bucketed FAST
+// output, raster/bucket order) as new features with new map points. The map
+// point stands in for triangulateNewMapPoints (R:src/tracking.cpp:120-152):
+// the synthetic scene gives the depth of every pixel ray (scene.py).
+__global__ __launch_bounds__(256) void append_kernel(AppendBatch B) {
+    const int s = blockIdx.x;
+    __shared__ int take_s, n0_s, m0_s;
+    if (threadIdx.x == 0) {
+        const int n0 = B.n[s];
+        const int cand = min(B.cand_n[s], B.cand_cap);
+        int take = min(max(B.n_target - n0, 0), cand);
+        take = min(take, B.cap - n0);
+        take = min(take, B.map_cap - B.map_n[s]);
+        take = max(take, 0);
+        take_s = take;
+        n0_s = n0;
+        m0_s = B.map_n[s];
+    }
+    __syncthreads();
+    const int take = take_s, n0 = n0_s, m0 = m0_s;
+    const double* R = B.rot + 9 * (size_t)s;  // world -> camera of this frame
+    const double fx = B.K[0], fy = B.K[4], cx = B.K[2], cy = B.K[5];
+    const double seed = (double)B.depth_seed[s];
+    for (int j = threadIdx.x; j < take; j += 256) {
+        const float* c = B.cand + (size_t)B.cand_elem * ((size_t)s * B.cand_cap + j);
+        const float x = c[0], y = c[1];
+        const size_t o = (size_t)s * B.cap + n0 + j;
+        B.xy[2 * o] = x;
+        B.xy[2 * o + 1] = y;
+        B.mid[o] = m0 + j;
+        const double rx = (x - cx) / fx, ry = (y - cy) / fy;
+        const double wx = R[0] * rx + R[3] * ry + R[6];
+        const double wy = R[1] * rx + R[4] * ry + R[7];
+        const double wz = R[2] * rx + R[5] * ry + R[8];
+        const double cu = fx * wx / wz + cx, cv = fy * wy / wz + cy;
+        const double rho = 12.0 + 5.0 * sin(cu / 97.0 + seed) + 4.0 * cos(cv / 61.0 - 0.5 * seed);
+        double* X = B.map + 3 * ((size_t)s * B.map_cap + m0 + j);
+        X[0] = wx / wz * rho;
+        X[1] = wy / wz * rho;
+        X[2] = rho;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        B.n[s] = n0 + take;
+        B.map_n[s] = m0 + take;
+        if (B.added) B.added[s] = take;
+    }
+}
+
+}  // namespace
+
+hipError_t launch_compact(const CompactBatch& b, int nseq, hipStream_t st) {
+    hipLaunchKernelGGL(compact_kernel, dim3(nseq), dim3(1024), 0, st, b);
+    return hipGetLastError();
+}
+
+hipError_t launch_gather(const int* n, const int* mid, const double* map, int cap, int map_cap, float* obj,
+                         int nseq, int max_n, hipStream_t st) {
+    if (max_n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(gather_kernel, dim3((max_n + 255) / 256, nseq), dim3(256), 0, st, n, mid, map, cap,
+                       map_cap, obj);
+    return hipGetLastError();
+}
+
+hipError_t launch_append(const AppendBatch& b, int nseq, hipStream_t st) {
+    hipLaunchKernelGGL(append_kernel, dim3(nseq), dim3(256), 0, st, b);
+    return hipGetLastError();
+}
+
+}  // namespace svo

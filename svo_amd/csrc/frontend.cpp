@@ -1,0 +1,622 @@
+// Batched, device-resident tracking front end: the per-frame loop of
+// Tracking::startStereo (R:src/tracking.cpp:232-276) for n_seq independent
+// sequences advanced in lockstep.
+//
+//   step(t), for every sequence s at once:
+//     pyramid(frame t)                                   [pyramid.hip]
+//     temporal LK  frame t-1 -> t (21x21, L3, 50 it)     [lk.hip]        trackFrames :154-179
+//     mask of boxes around frame t-1's features          [fast.hip]      extractFeatures :76-79
+//     FAST(t=20, NMS) on frame t with that mask          [fast.hip]      :82
+//     bucket selection (optional)                        [bucket.hip]    bucket.cpp (dead code)
+//     keep status==1 (stable compaction), gather map pts [frontend.hip]  :169-175, :182-187
+//     RANSAC: host EPnP chunks <-> GPU scoring launches  [pose.cpp, pnp.hip] calculatePose :191-196
+//     drop outliers (stable compaction)                  [frontend.hip]  :218-229
+//     keyframe top-up to n_features with new map points  [frontend.hip]  :247-255
+//
+// FAST and the bucket run on the GPU while the host builds RANSAC hypotheses.
+#include <algorithm>
+#include <atomic>
+#include <condition_variable>
+#include <cstring>
+#include <functional>
+#include <mutex>
+#include <thread>
+#include <vector>
+
+#include "frontend.hpp"
+#include "pose.hpp"
+
+namespace svo {
+
+namespace {
+
+// Minimal persistent pool for the per-sequence host work (RANSAC).
+class Pool {
+   public:
+    explicit Pool(int n) {
+        for (int i = 0; i < n; i++) th_.emplace_back([this] { loop(); });
+    }
+    ~Pool() {
+        {
+            std::lock_guard<std::mutex> g(mu_);
+            stop_ = true;
+        }
+        cv_.notify_all();
+        for (auto& t : th_) t.join();
+    }
+    int size() const { return (int)th_.size(); }
+    void run(int n, const std::function<void(int)>& fn) {
+        if (th_.empty() || n <= 1) {
+            for (int i = 0; i < n; i++) fn(i);
+            return;
+        }
+        {
+            std::lock_guard<std::mutex> g(mu_);
+            fn_ = &fn;
+            n_ = n;
+            next_.store(0);
+            pending_ = (int)th_.size();
+            gen_++;
+        }
+        cv_.notify_all();
+        work();
+        std::unique_lock<std::mutex> lk(mu_);
+        done_cv_.wait(lk, [this] { return pending_ == 0; });
+        fn_ = nullptr;
+    }
+
+   private:
+    void work() {
+        for (;;) {
+            int i = next_.fetch_add(1);
+            if (i >= n_) break;
+            (*fn_)(i);
+        }
+    }
+    void loop() {
+        uint64_t seen = 0;
+        for (;;) {
+            {
+                std::unique_lock<std::mutex> lk(mu_);
+                cv_.wait(lk, [&] { return stop_ || gen_ != seen; });
+                if (stop_) return;
+                seen = gen_;
+            }
+            work();
+            std::lock_guard<std::mutex> g(mu_);
+            if (--pending_ == 0) done_cv_.notify_all();
+        }
+    }
+    std::vector<std::thread> th_;
+    std::mutex mu_;
+    std::condition_variable cv_, done_cv_;
+    const std::function<void(int)>* fn_ = nullptr;
+    std::atomic<int> next_{0};
+    int n_ = 0, pending_ = 0;
+    uint64_t gen_ = 0;
+    bool stop_ = false;
+};
+
+constexpr int kPhases = 9;
+enum Phase { PH_PYR, PH_LK, PH_COMPACT, PH_GATHER, PH_PNP, PH_MASK, PH_FAST, PH_BUCKET, PH_APPEND };
+
+}  // namespace
+
+}  // namespace svo
+
+using namespace svo;
+
+struct svo_frontend {
+    svo_ctx* ctx = nullptr;
+    svo_frontend_config cfg{};
+    int S = 0, T = 0, CAP = 0, MAPCAP = 0, WORDS = 0, KCAP = 0, BCAP = 0;
+    int W = 0, H = 0, nlev = 0, ml = 0;
+    size_t npx = 0, bscr = 0;
+    std::vector<svo_image*> frames;  // [s*T + t]
+    std::vector<double> rot_host;    // [s*T + t][9]
+    std::vector<int> seed_host;      // [s]
+    std::vector<PyrDesc> desc_host;  // [t*S + s]
+    PyrDesc* d_desc = nullptr;       // [t][s]
+    // device state (one allocation)
+    void* dmem = nullptr;
+    float *xyA, *next_xy, *xyB, *obj, *kps, *cand;
+    int *midA, *midB, *nA, *nB, *iters, *kn, *bn, *map_n, *rowcnt, *scr, *cnt, *added, *seed_d;
+    long long* itsum;
+    uint8_t *status, *mask;
+    uint16_t* cs;
+    uint32_t *bits_all, *bits_best;
+    double *map, *hyps, *rot_d;
+    // host mirrors (pinned)
+    void* hmem = nullptr;
+    int *h_nB, *h_nA, *h_cnt, *h_added;
+    long long* h_itsum;
+    float *h_xyB, *h_obj;
+    double* h_hyps;
+    uint32_t *h_bits, *h_best;
+    std::vector<RansacSeq> rs;
+    std::vector<double> pose;  // [s][6]
+    Pool* pool = nullptr;
+    // timing
+    hipEvent_t ev[2 * kPhases * 4];
+    double phase_ms[kPhases] = {0};
+    int64_t phase_n[kPhases] = {0};
+    std::vector<std::pair<int, int>> pending;  // (phase, event pair index)
+    int ev_used = 0;
+};
+
+namespace {
+
+void ph_begin(svo_frontend* fe, int ph, int* slot) {
+    *slot = -1;
+    if (!fe->cfg.timing || fe->ev_used + 2 > (int)(sizeof(fe->ev) / sizeof(fe->ev[0]))) return;
+    *slot = fe->ev_used;
+    fe->ev_used += 2;
+    (void)hipEventRecord(fe->ev[*slot], fe->ctx->stream);
+    fe->pending.push_back({ph, *slot});
+}
+void ph_end(svo_frontend* fe, int slot) {
+    if (slot >= 0) (void)hipEventRecord(fe->ev[slot + 1], fe->ctx->stream);
+}
+// after a stream sync: fold the recorded event pairs into the phase totals
+void ph_collect(svo_frontend* fe) {
+    for (auto& p : fe->pending) {
+        float ms = 0.f;
+        if (hipEventElapsedTime(&ms, fe->ev[p.second], fe->ev[p.second + 1]) == hipSuccess) {
+            fe->phase_ms[p.first] += ms;
+            fe->phase_n[p.first] += 1;
+        }
+    }
+    fe->pending.clear();
+    fe->ev_used = 0;
+}
+
+template <class T>
+T* carve(char*& p, size_t count) {
+    p = (char*)(((uintptr_t)p + 255) & ~(uintptr_t)255);
+    T* r = (T*)p;
+    p += sizeof(T) * count;
+    return r;
+}
+
+int fe_fast_and_bucket(svo_frontend* fe, const PyrDesc* descs_cur, bool use_mask) {
+    svo_ctx* ctx = fe->ctx;
+    hipStream_t st = ctx->stream;
+    int slot;
+    FastBatch fb{descs_cur, fe->cs, use_mask ? fe->mask : nullptr, fe->rowcnt, (svo_keypoint*)fe->kps,
+                 fe->kn, fe->npx, fe->KCAP};
+    ph_begin(fe, PH_FAST, &slot);
+    SVO_HIP(ctx, launch_fast_score(fb, fe->S, fe->W, fe->H, fe->cfg.fast_threshold, fe->cfg.fast_nonmax, st));
+    SVO_HIP(ctx, launch_fast_collect(fb, fe->S, fe->W, fe->H, fe->cfg.fast_nonmax, st));
+    ph_end(fe, slot);
+    if (fe->cfg.bucket_size > 0) {
+        ph_begin(fe, PH_BUCKET, &slot);
+        BucketBatch bb{fe->kps, 3, fe->KCAP, fe->kn, 0, nullptr, fe->cand, nullptr, fe->BCAP, fe->bn, fe->scr,
+                       fe->bscr};
+        SVO_HIP(ctx, launch_bucket(bb, fe->S, fe->W, fe->H, fe->cfg.bucket_size, fe->cfg.per_bucket, st));
+        ph_end(fe, slot);
+    }
+    return SVO_OK;
+}
+
+int fe_append(svo_frontend* fe, int t) {
+    svo_ctx* ctx = fe->ctx;
+    int slot;
+    AppendBatch ab;
+    ab.n = fe->nA;
+    ab.xy = fe->xyA;
+    ab.mid = fe->midA;
+    ab.cap = fe->CAP;
+    ab.n_target = fe->cfg.n_features;
+    const bool bucketed = fe->cfg.bucket_size > 0;
+    ab.cand = bucketed ? fe->cand : fe->kps;
+    ab.cand_elem = bucketed ? 2 : 3;
+    ab.cand_cap = bucketed ? fe->BCAP : fe->KCAP;
+    ab.cand_n = bucketed ? fe->bn : fe->kn;
+    ab.map = fe->map;
+    ab.map_n = fe->map_n;
+    ab.map_cap = fe->MAPCAP;
+    ab.rot = fe->rot_d + 9 * (size_t)(t % fe->T) * fe->S;
+    ab.depth_seed = fe->seed_d;
+    ab.added = fe->added;
+    std::memcpy(ab.K, fe->cfg.K, sizeof(ab.K));
+    ph_begin(fe, PH_APPEND, &slot);
+    SVO_HIP(ctx, launch_append(ab, fe->S, ctx->stream));
+    ph_end(fe, slot);
+    return SVO_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int svo_frontend_create(svo_ctx* ctx, const svo_frontend_config* cfg, svo_frontend** out) {
+    if (!ctx || !cfg || !out) return SVO_ERR_ARG;
+    const svo_frontend_config& c = *cfg;
+    if (c.width <= 0 || c.height <= 0 || c.n_seq <= 0 || c.n_frames < 2 || c.n_features <= 0 || c.max_level < 0 ||
+        !lk_supported(c.win, c.win) || c.pnp_iterations <= 0 || !(c.pnp_confidence > 0 && c.pnp_confidence < 1) ||
+        (c.bucket_size > 0 && (c.per_bucket <= 0 || c.width / c.bucket_size <= 0)))
+        return set_error(ctx, SVO_ERR_ARG, "svo_frontend_create: bad config");
+    svo_frontend* fe = new svo_frontend();
+    fe->ctx = ctx;
+    fe->cfg = c;
+    fe->S = c.n_seq;
+    fe->T = c.n_frames;
+    fe->W = c.width;
+    fe->H = c.height;
+    fe->CAP = (c.n_features + 63) & ~63;
+    fe->WORDS = (fe->CAP + 31) / 32;
+    fe->KCAP = std::max(4 * fe->CAP, 8192);
+    fe->BCAP = ((c.bucket_size > 0) ? (c.height / c.bucket_size + 1) * (c.width / c.bucket_size + 1) * c.per_bucket
+                                    : 1) + 64;
+    fe->MAPCAP = fe->CAP * (c.n_frames + 2);
+    fe->npx = (size_t)c.width * c.height;
+    fe->ml = lk_levels_for_window(c.width, c.height, c.win, c.win, c.max_level);
+    fe->nlev = fe->ml + 1;
+    fe->bscr = c.bucket_size > 0 ? bucket_scratch_ints(c.width, c.height, c.bucket_size, c.per_bucket, fe->KCAP) : 1;
+    const int S = fe->S, CAP = fe->CAP;
+    // frames
+    fe->frames.assign((size_t)S * fe->T, nullptr);
+    for (auto& f : fe->frames) {
+        int rc = svo_image_create(ctx, c.width, c.height, fe->ml, &f);
+        if (rc) {
+            svo_frontend_destroy(fe);
+            return rc;
+        }
+    }
+    fe->desc_host.resize((size_t)fe->T * S);
+    for (int t = 0; t < fe->T; t++)
+        for (int s = 0; s < S; s++) fe->desc_host[(size_t)t * S + s] = fe->frames[(size_t)s * fe->T + t]->desc;
+    fe->rot_host.assign((size_t)fe->T * S * 9, 0.0);
+    for (size_t i = 0; i < fe->rot_host.size(); i += 9) fe->rot_host[i] = fe->rot_host[i + 4] = fe->rot_host[i + 8] = 1;
+    fe->seed_host.assign(S, 0);
+    // device state
+    size_t bytes = 0;
+    {
+        char* p = nullptr;
+        auto add = [&](size_t b) { p = (char*)(((uintptr_t)p + 255) & ~(uintptr_t)255) + b; };
+        add(sizeof(PyrDesc) * fe->T * S);
+        add(sizeof(float) * 2 * S * CAP * 3);  // xyA next_xy xyB
+        add(sizeof(float) * 3 * S * CAP);      // obj
+        add(sizeof(float) * 3 * (size_t)S * fe->KCAP);
+        add(sizeof(float) * 2 * (size_t)S * fe->BCAP);
+        add(sizeof(int) * S * CAP * 3);  // midA midB iters
+        add(sizeof(int) * S * 16);       // counts
+        add(sizeof(int) * (size_t)S * c.height);
+        add(sizeof(int) * fe->bscr * S);
+        add(sizeof(int) * S * kRansacChunk);
+        add(sizeof(long long) * S);
+        add(S * (size_t)CAP);          // status
+        add(fe->npx * S);              // mask
+        add(2 * fe->npx * S);          // cs
+        add(sizeof(uint32_t) * (size_t)S * kRansacChunk * fe->WORDS);
+        add(sizeof(uint32_t) * (size_t)S * fe->WORDS);
+        add(sizeof(double) * 3 * (size_t)S * fe->MAPCAP);
+        add(sizeof(double) * 12 * (size_t)S * kRansacChunk);
+        add(sizeof(double) * 9 * (size_t)S * fe->T);
+        add(4096);
+        bytes = (size_t)p;
+    }
+    if (hipMalloc(&fe->dmem, bytes) != hipSuccess) {
+        svo_frontend_destroy(fe);
+        return set_error(ctx, SVO_ERR_HIP, "svo_frontend_create: hipMalloc(%zu)", bytes);
+    }
+    {
+        char* p = (char*)fe->dmem;
+        fe->d_desc = carve<PyrDesc>(p, (size_t)fe->T * S);
+        fe->xyA = carve<float>(p, 2 * (size_t)S * CAP);
+        fe->next_xy = carve<float>(p, 2 * (size_t)S * CAP);
+        fe->xyB = carve<float>(p, 2 * (size_t)S * CAP);
+        fe->obj = carve<float>(p, 3 * (size_t)S * CAP);
+        fe->kps = carve<float>(p, 3 * (size_t)S * fe->KCAP);
+        fe->cand = carve<float>(p, 2 * (size_t)S * fe->BCAP);
+        fe->midA = carve<int>(p, (size_t)S * CAP);
+        fe->midB = carve<int>(p, (size_t)S * CAP);
+        fe->iters = carve<int>(p, (size_t)S * CAP);
+        fe->nA = carve<int>(p, S);
+        fe->nB = carve<int>(p, S);
+        fe->kn = carve<int>(p, S);
+        fe->bn = carve<int>(p, S);
+        fe->map_n = carve<int>(p, S);
+        fe->added = carve<int>(p, S);
+        fe->seed_d = carve<int>(p, S);
+        fe->rowcnt = carve<int>(p, (size_t)S * c.height);
+        fe->scr = carve<int>(p, fe->bscr * S);
+        fe->cnt = carve<int>(p, (size_t)S * kRansacChunk);
+        fe->itsum = carve<long long>(p, S);
+        fe->status = carve<uint8_t>(p, (size_t)S * CAP);
+        fe->mask = carve<uint8_t>(p, fe->npx * S);
+        fe->cs = carve<uint16_t>(p, fe->npx * S);
+        fe->bits_all = carve<uint32_t>(p, (size_t)S * kRansacChunk * fe->WORDS);
+        fe->bits_best = carve<uint32_t>(p, (size_t)S * fe->WORDS);
+        fe->map = carve<double>(p, 3 * (size_t)S * fe->MAPCAP);
+        fe->hyps = carve<double>(p, 12 * (size_t)S * kRansacChunk);
+        fe->rot_d = carve<double>(p, 9 * (size_t)S * fe->T);
+    }
+    (void)hipMemsetAsync(fe->dmem, 0, bytes, ctx->stream);
+    // host mirrors
+    size_t hbytes = 0;
+    {
+        char* p = nullptr;
+        auto add = [&](size_t b) { p = (char*)(((uintptr_t)p + 255) & ~(uintptr_t)255) + b; };
+        add(sizeof(int) * S * 4);
+        add(sizeof(long long) * S);
+        add(sizeof(float) * 5 * (size_t)S * CAP);
+        add(sizeof(double) * 12 * (size_t)S * kRansacChunk);
+        add(sizeof(int) * (size_t)S * kRansacChunk);
+        add(sizeof(uint32_t) * (size_t)S * kRansacChunk * fe->WORDS);
+        add(sizeof(uint32_t) * (size_t)S * fe->WORDS);
+        add(4096);
+        hbytes = (size_t)p;
+    }
+    if (hipHostMalloc(&fe->hmem, hbytes, hipHostMallocDefault) != hipSuccess) {
+        svo_frontend_destroy(fe);
+        return set_error(ctx, SVO_ERR_HIP, "svo_frontend_create: hipHostMalloc");
+    }
+    {
+        char* p = (char*)fe->hmem;
+        fe->h_nB = carve<int>(p, S);
+        fe->h_nA = carve<int>(p, S);
+        fe->h_cnt = carve<int>(p, (size_t)S * kRansacChunk);
+        fe->h_added = carve<int>(p, S);
+        fe->h_itsum = carve<long long>(p, S);
+        fe->h_xyB = carve<float>(p, 2 * (size_t)S * CAP);
+        fe->h_obj = carve<float>(p, 3 * (size_t)S * CAP);
+        fe->h_hyps = carve<double>(p, 12 * (size_t)S * kRansacChunk);
+        fe->h_bits = carve<uint32_t>(p, (size_t)S * kRansacChunk * fe->WORDS);
+        fe->h_best = carve<uint32_t>(p, (size_t)S * fe->WORDS);
+        std::memset(fe->h_nA, 0, sizeof(int) * S);
+    }
+    fe->rs.resize(S);
+    fe->pose.assign((size_t)S * 6, 0.0);
+    int nt = c.host_threads > 0 ? c.host_threads : (int)std::thread::hardware_concurrency();
+    nt = std::max(1, std::min({nt, S, 16}));
+    fe->pool = new Pool(nt - 1);
+    for (auto& e : fe->ev) (void)hipEventCreate(&e);
+    SVO_HIP(ctx, hipMemcpyAsync(fe->d_desc, fe->desc_host.data(), sizeof(PyrDesc) * fe->desc_host.size(),
+                                hipMemcpyHostToDevice, ctx->stream));
+    SVO_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    *out = fe;
+    return SVO_OK;
+}
+
+void svo_frontend_destroy(svo_frontend* fe) {
+    if (!fe) return;
+    if (fe->ctx) (void)hipStreamSynchronize(fe->ctx->stream);
+    delete fe->pool;
+    for (auto* f : fe->frames)
+        if (f) svo_image_destroy(fe->ctx, f);
+    if (fe->dmem) (void)hipFree(fe->dmem);
+    if (fe->hmem) (void)hipHostFree(fe->hmem);
+    for (auto& e : fe->ev)
+        if (e) (void)hipEventDestroy(e);
+    delete fe;
+}
+
+int svo_frontend_set_frame(svo_frontend* fe, int seq, int t, const uint8_t* gray, int stride, const double R[9],
+                           int depth_seed) {
+    if (!fe || seq < 0 || seq >= fe->S || t < 0 || t >= fe->T || !gray || stride < fe->W) return SVO_ERR_ARG;
+    svo_ctx* ctx = fe->ctx;
+    svo_image* im = fe->frames[(size_t)seq * fe->T + t];
+    SVO_HIP(ctx, hipMemcpy2DAsync(const_cast<uint8_t*>(im->desc.lv[0].data), im->desc.lv[0].pitch, gray, stride,
+                                  fe->W, fe->H, hipMemcpyHostToDevice, ctx->stream));
+    if (R) {
+        std::memcpy(&fe->rot_host[9 * ((size_t)t * fe->S + seq)], R, sizeof(double) * 9);
+        SVO_HIP(ctx, hipMemcpyAsync(fe->rot_d + 9 * ((size_t)t * fe->S + seq), R, sizeof(double) * 9,
+                                    hipMemcpyHostToDevice, ctx->stream));
+    }
+    fe->seed_host[seq] = depth_seed;
+    SVO_HIP(ctx, hipMemcpyAsync(fe->seed_d + seq, &fe->seed_host[seq], sizeof(int), hipMemcpyHostToDevice,
+                                ctx->stream));
+    SVO_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    return SVO_OK;
+}
+
+int svo_frontend_prebuild_pyramids(svo_frontend* fe) {
+    if (!fe) return SVO_ERR_ARG;
+    for (int t = 0; t < fe->T; t++)
+        SVO_HIP(fe->ctx, launch_pyramid_batched(fe->d_desc + (size_t)t * fe->S, fe->S, fe->W, fe->H, fe->nlev,
+                                                fe->ctx->stream));
+    SVO_HIP(fe->ctx, hipStreamSynchronize(fe->ctx->stream));
+    return SVO_OK;
+}
+
+int svo_frontend_init(svo_frontend* fe, int t0) {
+    if (!fe || t0 < 0) return SVO_ERR_ARG;
+    svo_ctx* ctx = fe->ctx;
+    const int S = fe->S;
+    const PyrDesc* dcur = fe->d_desc + (size_t)(t0 % fe->T) * S;
+    SVO_HIP(ctx, launch_pyramid_batched(dcur, S, fe->W, fe->H, fe->nlev, ctx->stream));
+    SVO_HIP(ctx, hipMemsetAsync(fe->nA, 0, sizeof(int) * S, ctx->stream));
+    SVO_HIP(ctx, hipMemsetAsync(fe->map_n, 0, sizeof(int) * S, ctx->stream));
+    int rc = fe_fast_and_bucket(fe, dcur, false);
+    if (rc) return rc;
+    rc = fe_append(fe, t0);
+    if (rc) return rc;
+    SVO_HIP(ctx, hipMemcpyAsync(fe->h_nA, fe->nA, sizeof(int) * S, hipMemcpyDeviceToHost, ctx->stream));
+    SVO_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    ph_collect(fe);
+    std::fill(fe->pose.begin(), fe->pose.end(), 0.0);
+    return SVO_OK;
+}
+
+int svo_frontend_step(svo_frontend* fe, int t, svo_frontend_stats* stats) {
+    if (!fe || t < 1) return SVO_ERR_ARG;
+    svo_ctx* ctx = fe->ctx;
+    hipStream_t st = ctx->stream;
+    const int S = fe->S, CAP = fe->CAP;
+    const svo_frontend_config& c = fe->cfg;
+    const PyrDesc* dprev = fe->d_desc + (size_t)((t - 1) % fe->T) * S;
+    const PyrDesc* dcur = fe->d_desc + (size_t)(t % fe->T) * S;
+    int slot;
+    int max_prev = 0;
+    for (int s = 0; s < S; s++) max_prev = std::max(max_prev, fe->h_nA[s]);
+
+    // 1. pyramid of frame t
+    ph_begin(fe, PH_PYR, &slot);
+    SVO_HIP(ctx, launch_pyramid_batched(dcur, S, fe->W, fe->H, fe->nlev, st));
+    ph_end(fe, slot);
+    // 2. temporal LK (trackFrames)
+    LKParams lp;
+    lp.win_w = lp.win_h = c.win;
+    lp.max_level = fe->ml;
+    lp.max_count = std::min(std::max(c.lk_max_count, 0), 100);
+    const double eps = std::min(std::max(c.lk_epsilon, 0.0), 10.0);
+    lp.eps2 = eps * eps;
+    lp.flags = c.lk_flags & ~SVO_LK_USE_INITIAL_FLOW;
+    lp.min_eig = (float)c.min_eig;
+    lp.want_err = 0;
+    LKBatch lb{dprev, dcur, fe->xyA, fe->next_xy, fe->status, nullptr, fe->iters, fe->nA, 0, CAP};
+    ph_begin(fe, PH_LK, &slot);
+    SVO_HIP(ctx, launch_lk(lb, S, max_prev, lp, st));
+    ph_end(fe, slot);
+    // 3. mask around frame t-1's features (the reference masks with prevFrame's
+    //    features, R:src/tracking.cpp:77) + FAST/bucket on frame t: independent
+    //    of the pose, so the GPU runs them while the host solves RANSAC
+    ph_begin(fe, PH_MASK, &slot);
+    SVO_HIP(ctx, launch_mask_boxes(fe->W, fe->H, fe->xyA, fe->nA, max_prev, CAP, S, c.mask_half, fe->mask, st));
+    ph_end(fe, slot);
+    // 4. keep status == 1 (+ sum LK iterations), gather map points
+    CompactBatch cb{fe->nA, fe->status, nullptr, 0, fe->next_xy, fe->midA, fe->iters, fe->itsum,
+                    fe->xyB, fe->midB, fe->nB, CAP};
+    ph_begin(fe, PH_COMPACT, &slot);
+    SVO_HIP(ctx, launch_compact(cb, S, st));
+    ph_end(fe, slot);
+    ph_begin(fe, PH_GATHER, &slot);
+    SVO_HIP(ctx, launch_gather(fe->nB, fe->midB, fe->map, CAP, fe->MAPCAP, fe->obj, S, max_prev, st));
+    ph_end(fe, slot);
+    SVO_HIP(ctx, hipMemcpyAsync(fe->h_nB, fe->nB, sizeof(int) * S, hipMemcpyDeviceToHost, st));
+    SVO_HIP(ctx, hipMemcpyAsync(fe->h_itsum, fe->itsum, sizeof(long long) * S, hipMemcpyDeviceToHost, st));
+    SVO_HIP(ctx, hipMemcpyAsync(fe->h_xyB, fe->xyB, sizeof(float) * 2 * S * (size_t)CAP, hipMemcpyDeviceToHost, st));
+    SVO_HIP(ctx, hipMemcpyAsync(fe->h_obj, fe->obj, sizeof(float) * 3 * S * (size_t)CAP, hipMemcpyDeviceToHost, st));
+    hipEvent_t ready;
+    SVO_HIP(ctx, hipEventCreateWithFlags(&ready, hipEventDisableTiming));
+    SVO_HIP(ctx, hipEventRecord(ready, st));
+    int rc = fe_fast_and_bucket(fe, dcur, true);
+    if (rc) return rc;
+    SVO_HIP(ctx, hipEventSynchronize(ready));
+    (void)hipEventDestroy(ready);
+
+    // 5. calculatePose: RANSAC per sequence, hypotheses scored on the GPU
+    int max_b = 0;
+    for (int s = 0; s < S; s++) {
+        fe->rs[s].begin(fe->h_obj + 3 * (size_t)s * CAP, fe->h_xyB + 2 * (size_t)s * CAP, fe->h_nB[s],
+                        c.pnp_iterations);
+        max_b = std::max(max_b, fe->h_nB[s]);
+    }
+    const float thr = (float)((double)c.pnp_reproj * (double)c.pnp_reproj);
+    int64_t nhyp = 0;
+    for (;;) {
+        std::vector<int> ms(S, 0);
+        fe->pool->run(S, [&](int s) { ms[s] = fe->rs[s].gen_chunk(c.K); });
+        int mmax = 0;
+        for (int s = 0; s < S; s++) mmax = std::max(mmax, ms[s]);
+        if (mmax == 0) break;
+        for (int s = 0; s < S; s++) {
+            double* dst = fe->h_hyps + 12 * (size_t)s * kRansacChunk;
+            std::memcpy(dst, fe->rs[s].hyp, sizeof(double) * 12 * ms[s]);
+            for (int j = ms[s]; j < mmax; j++) std::memset(dst + 12 * j, 0, sizeof(double) * 12);
+            nhyp += ms[s];
+        }
+        SVO_HIP(ctx, hipMemcpyAsync(fe->hyps, fe->h_hyps, sizeof(double) * 12 * S * kRansacChunk,
+                                    hipMemcpyHostToDevice, st));
+        PnpBatch pb{fe->obj, fe->xyB, fe->nB, 0, CAP, fe->hyps, kRansacChunk, nullptr, fe->bits_all, fe->WORDS,
+                    fe->cnt};
+        pb.m = mmax;  // rows beyond a sequence's own m are ignored by consume()
+        // hypotheses live at stride kRansacChunk: score with m = kRansacChunk rows
+        pb.m = kRansacChunk;
+        ph_begin(fe, PH_PNP, &slot);
+        SVO_HIP(ctx, launch_pnp_residuals(pb, S, max_b, c.K[0], c.K[4], c.K[2], c.K[5], thr, st));
+        ph_end(fe, slot);
+        SVO_HIP(ctx, hipMemcpyAsync(fe->h_cnt, fe->cnt, sizeof(int) * S * kRansacChunk, hipMemcpyDeviceToHost, st));
+        SVO_HIP(ctx, hipMemcpyAsync(fe->h_bits, fe->bits_all, sizeof(uint32_t) * S * kRansacChunk * fe->WORDS,
+                                    hipMemcpyDeviceToHost, st));
+        SVO_HIP(ctx, hipStreamSynchronize(st));
+        fe->pool->run(S, [&](int s) {
+            if (ms[s] > 0)
+                fe->rs[s].consume(fe->h_cnt + (size_t)s * kRansacChunk,
+                                  fe->h_bits + (size_t)s * kRansacChunk * fe->WORDS, fe->WORDS, c.pnp_confidence);
+        });
+    }
+    fe->pool->run(S, [&](int s) {
+        RansacSeq& r = fe->rs[s];
+        r.finish(c.K);
+        uint32_t* b = fe->h_best + (size_t)s * fe->WORDS;
+        std::memset(b, 0, sizeof(uint32_t) * fe->WORDS);
+        if (r.ok) {
+            for (int i : r.inliers) b[i >> 5] |= 1u << (i & 31);
+            std::memcpy(&fe->pose[6 * (size_t)s], r.rvec, sizeof(r.rvec));
+            std::memcpy(&fe->pose[6 * (size_t)s + 3], r.tvec, sizeof(r.tvec));
+        } else if (r.n < 4) {
+            // solvePnPRansac would throw (CV_Assert npoints >= 4); keep the frame's
+            // features untouched instead of aborting the batch
+            for (int i = 0; i < r.n; i++) b[i >> 5] |= 1u << (i & 31);
+        }
+    });
+    // 6. drop outliers (R:src/tracking.cpp:218-229), top up to n_features
+    SVO_HIP(ctx, hipMemcpyAsync(fe->bits_best, fe->h_best, sizeof(uint32_t) * S * fe->WORDS, hipMemcpyHostToDevice,
+                                st));
+    CompactBatch cb2{fe->nB, nullptr, fe->bits_best, fe->WORDS, fe->xyB, fe->midB, nullptr, nullptr,
+                     fe->xyA, fe->midA, fe->nA, CAP};
+    ph_begin(fe, PH_COMPACT, &slot);
+    SVO_HIP(ctx, launch_compact(cb2, S, st));
+    ph_end(fe, slot);
+    int64_t inl = 0;
+    for (int s = 0; s < S; s++) inl += fe->rs[s].ok ? (int64_t)fe->rs[s].inliers.size() : fe->rs[s].n;
+    rc = fe_append(fe, t);
+    if (rc) return rc;
+    SVO_HIP(ctx, hipMemcpyAsync(fe->h_nA, fe->nA, sizeof(int) * S, hipMemcpyDeviceToHost, st));
+    SVO_HIP(ctx, hipMemcpyAsync(fe->h_added, fe->added, sizeof(int) * S, hipMemcpyDeviceToHost, st));
+    SVO_HIP(ctx, hipStreamSynchronize(st));
+    ph_collect(fe);
+    if (stats) {
+        std::memset(stats, 0, sizeof(*stats));
+        for (int s = 0; s < S; s++) {
+            stats->lk_iterations += fe->h_itsum[s];
+            stats->tracked += fe->h_nB[s];
+            stats->added += fe->h_added[s];
+            stats->features += fe->h_nA[s];
+        }
+        stats->inliers = inl;
+        stats->hypotheses = nhyp;
+    }
+    return SVO_OK;
+}
+
+int svo_frontend_pose(const svo_frontend* fe, int seq, double rvec[3], double tvec[3]) {
+    if (!fe || seq < 0 || seq >= fe->S) return SVO_ERR_ARG;
+    std::memcpy(rvec, &fe->pose[6 * (size_t)seq], sizeof(double) * 3);
+    std::memcpy(tvec, &fe->pose[6 * (size_t)seq + 3], sizeof(double) * 3);
+    return SVO_OK;
+}
+
+int svo_frontend_features(svo_frontend* fe, int seq, float* xy, int cap, int* n) {
+    if (!fe || seq < 0 || seq >= fe->S) return SVO_ERR_ARG;
+    svo_ctx* ctx = fe->ctx;
+    int cnt = 0;
+    SVO_HIP(ctx, hipMemcpyAsync(&cnt, fe->nA + seq, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
+    SVO_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    const int k = std::min(cnt, cap);
+    if (k > 0 && xy)
+        SVO_HIP(ctx, hipMemcpy(xy, fe->xyA + 2 * (size_t)seq * fe->CAP, sizeof(float) * 2 * k, hipMemcpyDeviceToHost));
+    if (n) *n = cnt;
+    return SVO_OK;
+}
+
+int svo_frontend_phase_times(const svo_frontend* fe, double* ms, int64_t* launches, int cap) {
+    if (!fe) return SVO_ERR_ARG;
+    for (int i = 0; i < kPhases && i < cap; i++) {
+        if (ms) ms[i] = fe->phase_ms[i];
+        if (launches) launches[i] = fe->phase_n[i];
+    }
+    return kPhases;
+}
+
+void svo_frontend_reset_times(svo_frontend* fe) {
+    if (!fe) return;
+    for (int i = 0; i < kPhases; i++) {
+        fe->phase_ms[i] = 0;
+        fe->phase_n[i] = 0;
+    }
+}
+
+}  // extern "C"

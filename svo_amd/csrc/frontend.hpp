@@ -1,0 +1,44 @@
+// Batched tracking front end (device-resident state + launch helpers).
+#pragma once
+
+#include "common.hpp"
+
+namespace svo {
+
+struct CompactBatch {
+    const int* n_in;
+    const uint8_t* status;  // either status (u8 per point) ...
+    const uint32_t* bits;   // ... or a bitmask (words_cap words per sequence)
+    int words_cap;
+    const float* xy_in;
+    const int* mid_in;
+    const int* iters;        // nullable: per-point LK iterations to sum
+    long long* iters_sum;    // nullable: per-sequence sum
+    float* xy_out;
+    int* mid_out;
+    int* n_out;
+    int cap;
+};
+hipError_t launch_compact(const CompactBatch& b, int nseq, hipStream_t st);
+hipError_t launch_gather(const int* n, const int* mid, const double* map, int cap, int map_cap, float* obj,
+                         int nseq, int max_n, hipStream_t st);
+
+struct AppendBatch {
+    int* n;             // features per sequence (in/out)
+    float* xy;          // [s][cap] xy
+    int* mid;           // [s][cap]
+    int cap, n_target;
+    const float* cand;  // candidates, cand_elem floats each, cand_cap per sequence
+    int cand_elem, cand_cap;
+    const int* cand_n;
+    double* map;        // [s][map_cap] xyz
+    int* map_n;
+    int map_cap;
+    const double* rot;  // [s] 3x3 world->camera of this frame
+    const int* depth_seed;
+    int* added;         // nullable
+    double K[9];
+};
+hipError_t launch_append(const AppendBatch& b, int nseq, hipStream_t st);
+
+}  // namespace svo

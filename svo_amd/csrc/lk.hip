@@ -81,7 +81,7 @@ __device__ __forceinline__ double wave_sum_exact(int v) {
 
 struct LKDev {
     int win_w, win_h, groups;      // strip map: groups = lanes/win_w, RPG rows each
-    int tile_w, tile_h, grid_w, grid_h;
+    int tile_w, tile_h, jr_w, jr_h;
     int tile_bytes, lds_wave;      // per-wave LDS carve
     int max_level, max_count;
     double eps2;
@@ -89,28 +89,82 @@ struct LKDev {
     float min_eig;
 };
 
-template <int RPG>
-__global__ __launch_bounds__(256) void lk_kernel(PyrDesc prev, PyrDesc next,
-                                                 const float* __restrict__ prev_xy,
-                                                 float* __restrict__ next_xy,
-                                                 uint8_t* __restrict__ status,
-                                                 float* __restrict__ err, int* __restrict__ iters,
-                                                 int n, LKDev p) {
+constexpr int JM = 3;  // margin (px) of the staged next-image region around the window
+
+typedef const __attribute__((address_space(1))) uint8_t* gu8;  // global (not flat) loads
+typedef short s16x2 __attribute__((ext_vector_type(2)));
+
+// v_dot2_i32_i16: both operands signed 16-bit -- OpenCV's rounded bilinear weights
+// can be -1 (iw11 = 2^14 - iw00 - iw01 - iw10), pixels 0..255 and Scharr values
+// |v| <= 4080 fit, and every partial sum fits int32.
+__device__ __forceinline__ int sdot2(unsigned a, unsigned b, int c) {
+    return __builtin_amdgcn_sdot2(__builtin_bit_cast(s16x2, a), __builtin_bit_cast(s16x2, b), c, false);
+}
+__device__ __forceinline__ unsigned pack16(int lo, int hi) {
+    return ((unsigned)lo & 0xFFFFu) | ((unsigned)hi << 16);
+}
+
+// Cooperative copy of the rw x rh prev-image region at (x0, y0) into LDS bytes
+// (row pitch rw); REFLECT_101 outside the image, as OpenCV's padded pyramid.
+__device__ __forceinline__ void stage_bytes(uint8_t* dst, const ImgLevel& L, int x0, int y0, int rw,
+                                            int rh, int lr, int lc, int rpp) {
+    if (lr >= rpp) return;
+    gu8 src = (gu8)L.data;
+    const bool inside = x0 >= 0 && y0 >= 0 && x0 + rw <= L.w && y0 + rh <= L.h;
+    if (inside) {
+        gu8 q = src + (size_t)(y0 + lr) * L.pitch + (x0 + lc);
+        const size_t step = (size_t)rpp * L.pitch;
+        for (int r = lr; r < rh; r += rpp, q += step) dst[r * rw + lc] = *q;
+    } else {
+        const int sx = refl101(x0 + lc, L.w);
+        for (int r = lr; r < rh; r += rpp) dst[r * rw + lc] = src[(size_t)refl101(y0 + r, L.h) * L.pitch + sx];
+    }
+}
+
+// Next-image region at (x0, y0) as horizontal pixel pairs: entry (r, e) =
+// J(x0+e, y0+r) | J(x0+e+1, y0+r) << 16, ready for one v_dot2_u32_u16 per row.
+__device__ __forceinline__ void stage_pairs(unsigned* dst, const ImgLevel& L, int x0, int y0, int rw,
+                                            int rh, int lr, int lc, int rpp) {
+    if (lr >= rpp) return;
+    gu8 src = (gu8)L.data;
+    const bool inside = x0 >= 0 && y0 >= 0 && x0 + rw + 1 <= L.w && y0 + rh <= L.h;
+    if (inside) {
+        gu8 q = src + (size_t)(y0 + lr) * L.pitch + (x0 + lc);
+        const size_t step = (size_t)rpp * L.pitch;
+        for (int r = lr; r < rh; r += rpp, q += step) dst[r * rw + lc] = (unsigned)q[0] | ((unsigned)q[1] << 16);
+    } else {
+        const int sx0 = refl101(x0 + lc, L.w), sx1 = refl101(x0 + lc + 1, L.w);
+        for (int r = lr; r < rh; r += rpp) {
+            gu8 row = src + (size_t)refl101(y0 + r, L.h) * L.pitch;
+            dst[r * rw + lc] = (unsigned)row[sx0] | ((unsigned)row[sx1] << 16);
+        }
+    }
+}
+
+template <int RPG, bool FULL>
+__global__ __launch_bounds__(256) void lk_kernel(LKBatch B, LKDev p) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     const int lane = threadIdx.x & 63;
     const int wid = threadIdx.x >> 6;
+    const int seq = blockIdx.y;
+    const int n = B.counts ? B.counts[seq] : B.n;
     const int pt = blockIdx.x * 4 + wid;
     if (pt >= n) return;
+    const size_t base = (size_t)seq * B.cap;
+    const float* __restrict__ prev_xy = B.prev_xy + 2 * base;
+    float* __restrict__ next_xy = B.next_xy + 2 * base;
+    const PyrDesc& prev = B.prev[seq];
+    const PyrDesc& next = B.next[seq];
     uint8_t* tile = lds + wid * p.lds_wave;
-    int* grid = reinterpret_cast<int*>(tile + p.tile_bytes);
+    unsigned* jreg = reinterpret_cast<unsigned*>(tile + p.tile_bytes);
 
     const int win_w = p.win_w, win_h = p.win_h;
     const int sc = lane % win_w;
     const int sg = lane / win_w;
     const bool strip = sg < p.groups;
     const int r0 = sg * RPG;
-    const int tile_rows_per_pass = 64 / p.tile_w;
-    const int tl_r = lane / p.tile_w, tl_c = lane - (lane / p.tile_w) * p.tile_w;
+    const int t_rpp = 64 / p.tile_w, t_lr = lane / p.tile_w, t_lc = lane - t_lr * p.tile_w;
+    const int j_rpp = 64 / p.jr_w, j_lr = lane / p.jr_w, j_lc = lane - j_lr * p.jr_w;
 
     const float halfWx = (win_w - 1) * 0.5f, halfWy = (win_h - 1) * 0.5f;
     const float px = uni_f(prev_xy[2 * pt]), py = uni_f(prev_xy[2 * pt + 1]);
@@ -155,69 +209,82 @@ __global__ __launch_bounds__(256) void lk_kernel(PyrDesc prev, PyrDesc next,
             continue;
         }
         float a = prevx - ipx, b = prevy - ipy;
-        int iw00 = uround((1.f - a) * (1.f - b) * (1 << W_BITS));
-        int iw01 = uround(a * (1.f - b) * (1 << W_BITS));
-        int iw10 = uround((1.f - a) * b * (1 << W_BITS));
-        int iw11 = (1 << W_BITS) - iw00 - iw01 - iw10;
+        const int iw00 = uround((1.f - a) * (1.f - b) * (1 << W_BITS));
+        const int iw01 = uround(a * (1.f - b) * (1 << W_BITS));
+        const int iw10 = uround((1.f - a) * b * (1 << W_BITS));
+        const int iw11 = (1 << W_BITS) - iw00 - iw01 - iw10;
+        const unsigned IW0 = pack16(iw00, iw01), IW1 = pack16(iw10, iw11);
 
-        // ---- stage the previous-image patch (rows ipy-1.., cols ipx-1..) ----
-        {
-            const int ty0 = ipy - 1, tx0 = ipx - 1;
-            const bool inside = tx0 >= 0 && ty0 >= 0 && tx0 + p.tile_w <= I.w && ty0 + p.tile_h <= I.h;
-            if (tl_r < tile_rows_per_pass) {
-                for (int r = tl_r; r < p.tile_h; r += tile_rows_per_pass) {
-                    int sy = ty0 + r, sx = tx0 + tl_c;
-                    if (!inside) {
-                        sy = refl101(sy, I.h);
-                        sx = refl101(sx, I.w);
-                    }
-                    tile[r * p.tile_w + tl_c] = I.data[(size_t)sy * I.pitch + sx];
-                }
-            }
-        }
-        wave_lds_sync();
-        // ---- Scharr derivative at the (win+1)^2 grid points, zero outside ----
-        for (int k = lane; k < p.grid_w * p.grid_h; k += 64) {
-            int gr = k / p.grid_w, gc = k - gr * p.grid_w;
-            int X = ipx + gc, Y = ipy + gr;
-            int v = 0;
-            if (X >= 0 && X < I.w && Y >= 0 && Y < I.h) {
-                const uint8_t* t0 = tile + gr * p.tile_w + gc;   // row Y-1, col X-1
-                const uint8_t* t1 = t0 + p.tile_w;
-                const uint8_t* t2 = t1 + p.tile_w;
-                int tl = t0[0], tm = t0[1], tr = t0[2];
-                int ml = t1[0], mr = t1[2];
-                int bl = t2[0], bm = t2[1], br = t2[2];
-                int ix = (3 * (tr + br) + 10 * mr) - (3 * (tl + bl) + 10 * ml);
-                int iy = 3 * ((br - tr) + (bl - tl)) + 10 * (bm - tm);
-                v = (int)(((unsigned)iy << 16) | ((unsigned)ix & 0xFFFFu));
-            }
-            grid[k] = v;
-        }
+        // ---- stage the prev patch (rows ipy-1.., cols ipx-1..) and the next-image
+        //      region around the initial window: one load burst, one LDS sync ----
+        int jx0 = uni_i(ufloor(nextx - halfWx)) - JM, jy0 = uni_i(ufloor(nexty - halfWy)) - JM;
+        stage_bytes(tile, I, ipx - 1, ipy - 1, p.tile_w, p.tile_h, t_lr, t_lc, t_rpp);
+        stage_pairs(jreg, J, jx0, jy0, p.jr_w, p.jr_h, j_lr, j_lc, j_rpp);
         wave_lds_sync();
 
-        // ---- per-lane strip: I (x32) and (Ix, Iy) at its window pixels ----
-        int ival[RPG], gxy[RPG];
+        // ---- per-lane strip (column sc, rows r0..): Scharr at grid columns sc and
+        //      sc+1 from tile columns sc..sc+3 (sliding over rows), zero outside the
+        //      image; bilinear I (x32), Ix, Iy at the strip pixels ----
+        int ival[RPG], gix[RPG], giy[RPG];
         int a11 = 0, a12 = 0, a22 = 0;
+        {
+            const bool full_in = ipx >= 0 && ipy >= 0 && ipx + win_w < I.w && ipy + win_h < I.h;
+            const int X0 = ipx + sc;  // image x of grid column sc
+            const bool cin0 = X0 >= 0 && X0 < I.w, cin1 = X0 + 1 >= 0 && X0 + 1 < I.w;
+            const uint8_t* tp = tile + r0 * p.tile_w + sc;
+            int ra[4], rb[4], rc[4];   // tile rows k-2, k-1, k (cols sc..sc+3)
+            int gxa0 = 0, gxa1 = 0, gya0 = 0, gya1 = 0;  // grid row (k-3)
 #pragma unroll
-        for (int j = 0; j < RPG; j++) {
-            ival[j] = 0;
-            gxy[j] = 0;
-            const int r = r0 + j;
-            if (strip && r < win_h) {
-                const uint8_t* t = tile + (r + 1) * p.tile_w + (sc + 1);
-                ival[j] = descale(t[0] * iw00 + t[1] * iw01 + t[p.tile_w] * iw10 + t[p.tile_w + 1] * iw11,
-                                  W_BITS - 5);
-                const int* g = grid + r * p.grid_w + sc;
-                int g00 = g[0], g01 = g[1], g10 = g[p.grid_w], g11 = g[p.grid_w + 1];
-                int ix = descale((int)(short)g00 * iw00 + (int)(short)g01 * iw01 + (int)(short)g10 * iw10 +
-                                     (int)(short)g11 * iw11, W_BITS);
-                int iy = descale((g00 >> 16) * iw00 + (g01 >> 16) * iw01 + (g10 >> 16) * iw10 +
-                                     (g11 >> 16) * iw11, W_BITS);
-                gxy[j] = (int)(((unsigned)iy << 16) | ((unsigned)ix & 0xFFFFu));
-                a11 += ix * ix;
-                a12 += ix * iy;
-                a22 += iy * iy;
+            for (int k = 0; k < RPG + 3; k++) {
+#pragma unroll
+                for (int x = 0; x < 4; x++) {
+                    ra[x] = rb[x];
+                    rb[x] = rc[x];
+                    rc[x] = (strip && (FULL || r0 + k <= win_h + 2)) ? tp[k * p.tile_w + x] : 0;
+                }
+                if (k < 2) continue;
+                // grid row g = r0 + k - 2 from tile rows k-2, k-1, k
+                const int v00 = 3 * (ra[0] + rc[0]) + 10 * rb[0], v01 = 3 * (ra[1] + rc[1]) + 10 * rb[1];
+                const int v02 = 3 * (ra[2] + rc[2]) + 10 * rb[2], v03 = 3 * (ra[3] + rc[3]) + 10 * rb[3];
+                const int d0 = rc[0] - ra[0], d1 = rc[1] - ra[1], d2 = rc[2] - ra[2], d3 = rc[3] - ra[3];
+                int gx0 = v02 - v00, gx1 = v03 - v01;
+                int gy0 = 3 * (d2 + d0) + 10 * d1, gy1 = 3 * (d3 + d1) + 10 * d2;
+                if (!full_in) {
+                    const int Y = ipy + r0 + k - 2;
+                    const bool rin = Y >= 0 && Y < I.h;
+                    if (!(rin && cin0)) gx0 = gy0 = 0;
+                    if (!(rin && cin1)) gx1 = gy1 = 0;
+                }
+                if (k >= 3) {
+                    // window row j = k - 3: grid rows j (held) and j+1 (just computed)
+                    const int j = k - 3;
+                    if (j < RPG && (FULL || (strip && r0 + j < win_h))) {
+                        const unsigned P0 = pack16(gxa0, gxa1), P1 = pack16(gx0, gx1);
+                        const unsigned Q0 = pack16(gya0, gya1), Q1 = pack16(gy0, gy1);
+                        const int ix = sdot2(P0, IW0, sdot2(P1, IW1, 1 << (W_BITS - 1))) >> W_BITS;
+                        const int iy = sdot2(Q0, IW0, sdot2(Q1, IW1, 1 << (W_BITS - 1))) >> W_BITS;
+                        // I at tile rows r0+j+1 (= ra) and r0+j+2 (= rb), cols sc+1, sc+2
+                        const unsigned T0 = (unsigned)ra[1] | ((unsigned)ra[2] << 16);
+                        const unsigned T1 = (unsigned)rb[1] | ((unsigned)rb[2] << 16);
+                        ival[j] = sdot2(T0, IW0, sdot2(T1, IW1, 1 << (W_BITS - 6))) >> (W_BITS - 5);
+                        gix[j] = ix;
+                        giy[j] = iy;
+                        a11 += ix * ix;
+                        a12 += ix * iy;
+                        a22 += iy * iy;
+                    } else if (j < RPG) {
+                        ival[j] = gix[j] = giy[j] = 0;
+                    }
+                }
+                gxa0 = gx0;
+                gxa1 = gx1;
+                gya0 = gy0;
+                gya1 = gy1;
+            }
+            if (!strip) {
+#pragma unroll
+                for (int j = 0; j < RPG; j++) ival[j] = gix[j] = giy[j] = 0;
+                a11 = a12 = a22 = 0;
             }
         }
         const float A11 = (float)wave_sum_exact(a11) * FLT_SCALE;
@@ -230,6 +297,7 @@ __global__ __launch_bounds__(256) void lk_kernel(PyrDesc prev, PyrDesc next,
         if (p.want_err && (p.flags & SVO_LK_GET_MIN_EIGENVALS)) errv = minEig;
         if (minEig < p.min_eig || D < FLT_EPSILON) {
             if (level == 0) st = 0;
+            wave_lds_sync();
             continue;
         }
         D = 1.f / D;
@@ -244,39 +312,34 @@ __global__ __launch_bounds__(256) void lk_kernel(PyrDesc prev, PyrDesc next,
                 break;
             }
             itcount++;
+            if (inx < jx0 || inx > jx0 + 2 * JM || iny < jy0 || iny > jy0 + 2 * JM) {
+                // the window left the staged region: re-stage around it
+                jx0 = inx - JM;
+                jy0 = iny - JM;
+                wave_lds_sync();
+                stage_pairs(jreg, J, jx0, jy0, p.jr_w, p.jr_h, j_lr, j_lc, j_rpp);
+                wave_lds_sync();
+            }
             a = nextx - inx;
             b = nexty - iny;
-            int w00 = uround((1.f - a) * (1.f - b) * (1 << W_BITS));
-            int w01 = uround(a * (1.f - b) * (1 << W_BITS));
-            int w10 = uround((1.f - a) * b * (1 << W_BITS));
-            int w11 = (1 << W_BITS) - w00 - w01 - w10;
+            const int w00 = uround((1.f - a) * (1.f - b) * (1 << W_BITS));
+            const int w01 = uround(a * (1.f - b) * (1 << W_BITS));
+            const int w10 = uround((1.f - a) * b * (1 << W_BITS));
+            const int w11 = (1 << W_BITS) - w00 - w01 - w10;
+            const unsigned W0 = pack16(w00, w01), W1 = pack16(w10, w11);
             int b1 = 0, b2 = 0;
             if (strip) {
-                const bool inside = inx >= 0 && iny >= 0 && inx + win_w < J.w && iny + win_h < J.h;
-                int c0 = inx + sc, c1 = c0 + 1;
-                if (!inside) {
-                    c0 = refl101(c0, J.w);
-                    c1 = refl101(c1, J.w);
-                }
-                int jv[RPG + 1][2];
-#pragma unroll
-                for (int k = 0; k <= RPG; k++) {
-                    jv[k][0] = jv[k][1] = 0;
-                    if (r0 + k <= win_h) {
-                        int y = iny + r0 + k;
-                        if (!inside) y = refl101(y, J.h);
-                        const uint8_t* row = J.data + (size_t)y * J.pitch;
-                        jv[k][0] = row[c0];
-                        jv[k][1] = row[c1];
-                    }
-                }
+                const unsigned* jp = jreg + (iny - jy0 + r0) * p.jr_w + (inx - jx0 + sc);
+                unsigned p0 = jp[0];
 #pragma unroll
                 for (int k = 0; k < RPG; k++) {
-                    if (r0 + k < win_h) {
-                        int diff = descale(jv[k][0] * w00 + jv[k][1] * w01 + jv[k + 1][0] * w10 +
-                                               jv[k + 1][1] * w11, W_BITS - 5) - ival[k];
-                        b1 += diff * (int)(short)gxy[k];
-                        b2 += diff * (gxy[k] >> 16);
+                    if (FULL || r0 + k < win_h) {
+                        const unsigned p1 = jp[(k + 1) * p.jr_w];
+                        const int jv = sdot2(p0, W0, sdot2(p1, W1, 1 << (W_BITS - 6))) >> (W_BITS - 5);
+                        const int diff = jv - ival[k];
+                        b1 += diff * gix[k];
+                        b2 += diff * giy[k];
+                        p0 = p1;
                     }
                 }
             }
@@ -305,21 +368,28 @@ __global__ __launch_bounds__(256) void lk_kernel(PyrDesc prev, PyrDesc next,
                 st = 0;
                 continue;
             }
+            if (ix0 < jx0 || ix0 > jx0 + 2 * JM || iy0 < jy0 || iy0 > jy0 + 2 * JM) {
+                jx0 = ix0 - JM;
+                jy0 = iy0 - JM;
+                wave_lds_sync();
+                stage_pairs(jreg, J, jx0, jy0, p.jr_w, p.jr_h, j_lr, j_lc, j_rpp);
+                wave_lds_sync();
+            }
             float aa = npx - ix0, bb = npy - iy0;
-            int w00 = uround((1.f - aa) * (1.f - bb) * (1 << W_BITS));
-            int w01 = uround(aa * (1.f - bb) * (1 << W_BITS));
-            int w10 = uround((1.f - aa) * bb * (1 << W_BITS));
-            int w11 = (1 << W_BITS) - w00 - w01 - w10;
+            const int w00 = uround((1.f - aa) * (1.f - bb) * (1 << W_BITS));
+            const int w01 = uround(aa * (1.f - bb) * (1 << W_BITS));
+            const int w10 = uround((1.f - aa) * bb * (1 << W_BITS));
+            const int w11 = (1 << W_BITS) - w00 - w01 - w10;
+            const unsigned W0 = pack16(w00, w01), W1 = pack16(w10, w11);
             int sad = 0;
             if (strip) {
-                int c0 = refl101(ix0 + sc, J.w), c1 = refl101(ix0 + sc + 1, J.w);
+                const unsigned* jp = jreg + (iy0 - jy0 + r0) * p.jr_w + (ix0 - jx0 + sc);
 #pragma unroll
                 for (int k = 0; k < RPG; k++) {
-                    if (r0 + k < win_h) {
-                        const uint8_t* ra = J.data + (size_t)refl101(iy0 + r0 + k, J.h) * J.pitch;
-                        const uint8_t* rb = J.data + (size_t)refl101(iy0 + r0 + k + 1, J.h) * J.pitch;
-                        int diff = descale(ra[c0] * w00 + ra[c1] * w01 + rb[c0] * w10 + rb[c1] * w11,
-                                           W_BITS - 5) - ival[k];
+                    if (FULL || r0 + k < win_h) {
+                        const int jv = sdot2(jp[k * p.jr_w], W0, sdot2(jp[(k + 1) * p.jr_w], W1,
+                                                                       1 << (W_BITS - 6))) >> (W_BITS - 5);
+                        const int diff = jv - ival[k];
                         sad += diff < 0 ? -diff : diff;
                     }
                 }
@@ -327,39 +397,38 @@ __global__ __launch_bounds__(256) void lk_kernel(PyrDesc prev, PyrDesc next,
             // |diff| sums stay < 2^24 for windows <= 2048 px: exact in float
             errv = (float)wave_sum_exact(sad) * 1.f / (float)(32 * win_w * win_h);
         }
+        wave_lds_sync();  // this level's LDS reads finish before the next level's staging
     }
     if (lane == 0) {
         next_xy[2 * pt] = nx;
         next_xy[2 * pt + 1] = ny;
-        status[pt] = (uint8_t)st;
-        if (err) err[pt] = errv;
-        if (iters) iters[pt] = itcount;
+        B.status[base + pt] = (uint8_t)st;
+        if (B.err) B.err[base + pt] = errv;
+        if (B.iters) B.iters[base + pt] = itcount;
     }
 }
 
 template <int RPG>
-hipError_t launch_rpg(const PyrDesc& prev, const PyrDesc& next, const float* prev_xy, float* next_xy,
-                      uint8_t* status, float* err, int* iters, int n, const LKDev& d,
-                      hipStream_t st) {
-    dim3 grid((n + 3) / 4);
-    hipLaunchKernelGGL(lk_kernel<RPG>, grid, dim3(256), 4 * d.lds_wave, st, prev, next, prev_xy,
-                       next_xy, status, err, iters, n, d);
+hipError_t launch_rpg(const LKBatch& b, int nseq, int max_n, const LKDev& d, hipStream_t st) {
+    dim3 grid((max_n + 3) / 4, nseq);
+    if (d.groups * RPG == d.win_h)
+        hipLaunchKernelGGL((lk_kernel<RPG, true>), grid, dim3(256), 4 * d.lds_wave, st, b, d);
+    else
+        hipLaunchKernelGGL((lk_kernel<RPG, false>), grid, dim3(256), 4 * d.lds_wave, st, b, d);
     return hipGetLastError();
 }
 
 }  // namespace
 
 bool lk_supported(int win_w, int win_h) {
-    if (win_w < 3 || win_h < 3 || win_w + 3 > 64) return false;
+    if (win_w < 3 || win_h < 3 || win_w + 2 * JM > 64 || win_w + 3 > 64) return false;
     int groups = 64 / win_w;
     int rpg = (win_h + groups - 1) / groups;
     return rpg <= 32 && win_w * win_h <= 2048;
 }
 
-hipError_t launch_lk(const PyrDesc& prev, const PyrDesc& next, const float* prev_xy, float* next_xy,
-                     uint8_t* status, float* err, int* iters, int n, const LKParams& lp,
-                     hipStream_t st) {
-    if (n <= 0) return hipSuccess;
+hipError_t launch_lk(const LKBatch& b, int nseq, int max_n, const LKParams& lp, hipStream_t st) {
+    if (max_n <= 0 || nseq <= 0) return hipSuccess;
     LKDev d;
     d.win_w = lp.win_w;
     d.win_h = lp.win_h;
@@ -367,10 +436,10 @@ hipError_t launch_lk(const PyrDesc& prev, const PyrDesc& next, const float* prev
     int rpg = (lp.win_h + d.groups - 1) / d.groups;
     d.tile_w = lp.win_w + 3;
     d.tile_h = lp.win_h + 3;
-    d.grid_w = lp.win_w + 1;
-    d.grid_h = lp.win_h + 1;
+    d.jr_w = lp.win_w + 2 * JM;       // pair entries per row (cover win_w + 2JM + 1 pixels)
+    d.jr_h = lp.win_h + 1 + 2 * JM;
     d.tile_bytes = (d.tile_w * d.tile_h + 15) & ~15;
-    d.lds_wave = d.tile_bytes + ((d.grid_w * d.grid_h * 4 + 15) & ~15);
+    d.lds_wave = d.tile_bytes + ((d.jr_w * d.jr_h * 4 + 15) & ~15);
     d.max_level = lp.max_level;
     d.max_count = lp.max_count;
     d.eps2 = lp.eps2;
@@ -378,7 +447,7 @@ hipError_t launch_lk(const PyrDesc& prev, const PyrDesc& next, const float* prev
     d.want_err = lp.want_err;
     d.min_eig = lp.min_eig;
 #define SVO_LK_CASE(R) \
-    case R: return launch_rpg<R>(prev, next, prev_xy, next_xy, status, err, iters, n, d, st);
+    case R: return launch_rpg<R>(b, nseq, max_n, d, st);
     switch (rpg) {
         SVO_LK_CASE(1) SVO_LK_CASE(2) SVO_LK_CASE(3) SVO_LK_CASE(4) SVO_LK_CASE(5) SVO_LK_CASE(6)
         SVO_LK_CASE(7) SVO_LK_CASE(8) SVO_LK_CASE(9) SVO_LK_CASE(10) SVO_LK_CASE(11) SVO_LK_CASE(12)
@@ -388,9 +457,9 @@ hipError_t launch_lk(const PyrDesc& prev, const PyrDesc& next, const float* prev
     }
 #undef SVO_LK_CASE
     // uncommon strip heights: round up to the next instantiated size
-    if (rpg <= 13) return launch_rpg<14>(prev, next, prev_xy, next_xy, status, err, iters, n, d, st);
-    if (rpg <= 16) return launch_rpg<16>(prev, next, prev_xy, next_xy, status, err, iters, n, d, st);
-    return launch_rpg<32>(prev, next, prev_xy, next_xy, status, err, iters, n, d, st);
+    if (rpg <= 13) return launch_rpg<14>(b, nseq, max_n, d, st);
+    if (rpg <= 16) return launch_rpg<16>(b, nseq, max_n, d, st);
+    return launch_rpg<32>(b, nseq, max_n, d, st);
 }
 
 }  // namespace svo

@@ -16,17 +16,16 @@ namespace svo {
 
 namespace {
 
-__global__ __launch_bounds__(256) void pnp_residual_kernel(const float* __restrict__ obj,
-                                                           const float* __restrict__ img, int n,
-                                                           const double* __restrict__ hyp,
-                                                           double fx, double fy, double cx,
-                                                           double cy, float thresh2,
-                                                           float* __restrict__ err,
-                                                           uint32_t* __restrict__ bits,
-                                                           int* __restrict__ counts) {
+__global__ __launch_bounds__(256) void pnp_residual_kernel(PnpBatch B, double fx, double fy, double cx,
+                                                           double cy, float thresh2) {
+    const int seq = blockIdx.z;
     const int h = blockIdx.y;
+    const int n = B.counts ? B.counts[seq] : B.n;
+    if ((int)blockIdx.x * 256 >= n) return;
     const int i = blockIdx.x * 256 + threadIdx.x;
-    const double* R = hyp + 12 * h;  // uniform -> scalar loads
+    const float* __restrict__ obj = B.obj + 3 * (size_t)seq * B.cap;
+    const float* __restrict__ img = B.img + 2 * (size_t)seq * B.cap;
+    const double* R = B.hyp + 12 * ((size_t)seq * B.m + h);  // uniform -> scalar loads
     bool inl = false;
     if (i < n) {
         const double X = obj[3 * i], Y = obj[3 * i + 1], Z = obj[3 * i + 2];
@@ -41,33 +40,32 @@ __global__ __launch_bounds__(256) void pnp_residual_kernel(const float* __restri
         float s = 0.f;
         s += dx * dx;
         s += dy * dy;
-        if (err) err[(size_t)h * n + i] = s;
+        if (B.err) B.err[((size_t)seq * B.m + h) * B.cap + i] = s;
         inl = s <= thresh2;
     }
     const unsigned long long bal = __ballot(inl);
     const int lane = threadIdx.x & 63;
     const int words = (n + 31) >> 5;
     const int w0 = (blockIdx.x * 256 + (threadIdx.x & ~63)) >> 5;
-    if (bits) {
-        if (lane == 0 && w0 < words) bits[(size_t)h * words + w0] = (uint32_t)bal;
-        if (lane == 1 && w0 + 1 < words) bits[(size_t)h * words + w0 + 1] = (uint32_t)(bal >> 32);
+    if (B.bits) {
+        uint32_t* bits = B.bits + ((size_t)seq * B.m + h) * B.words_cap;
+        if (lane == 0 && w0 < words) bits[w0] = (uint32_t)bal;
+        if (lane == 1 && w0 + 1 < words) bits[w0 + 1] = (uint32_t)(bal >> 32);
     }
-    if (counts && lane == 0 && bal) atomicAdd(&counts[h], __popcll(bal));
+    if (B.cnt && lane == 0 && bal) atomicAdd(&B.cnt[(size_t)seq * B.m + h], __popcll(bal));
 }
 
 }  // namespace
 
-hipError_t launch_pnp_residuals(const float* obj, const float* img, int n, const double* hyp,
-                                int m, double fx, double fy, double cx, double cy, float thresh2,
-                                float* err, uint32_t* bits, int* counts, hipStream_t st) {
-    if (n <= 0 || m <= 0) return hipSuccess;
-    if (counts) {
-        hipError_t e = hipMemsetAsync(counts, 0, sizeof(int) * (size_t)m, st);
+hipError_t launch_pnp_residuals(const PnpBatch& b, int nseq, int max_n, double fx, double fy, double cx,
+                                double cy, float thresh2, hipStream_t st) {
+    if (max_n <= 0 || b.m <= 0 || nseq <= 0) return hipSuccess;
+    if (b.cnt) {
+        hipError_t e = hipMemsetAsync(b.cnt, 0, sizeof(int) * (size_t)b.m * nseq, st);
         if (e != hipSuccess) return e;
     }
-    dim3 grid((n + 255) / 256, m);
-    hipLaunchKernelGGL(pnp_residual_kernel, grid, dim3(256), 0, st, obj, img, n, hyp, fx, fy, cx, cy,
-                       thresh2, err, bits, counts);
+    dim3 grid((max_n + 255) / 256, b.m, nseq);
+    hipLaunchKernelGGL(pnp_residual_kernel, grid, dim3(256), 0, st, b, fx, fy, cx, cy, thresh2);
     return hipGetLastError();
 }
 

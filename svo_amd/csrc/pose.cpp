@@ -19,19 +19,12 @@
 
 #include "common.hpp"
 #include "linalg.hpp"
+#include "pose.hpp"
 
 namespace svo {
 
 namespace {
 
-struct Rng {  // cv::RNG
-    uint64_t state;
-    uint32_t next() {
-        state = (uint64_t)(uint32_t)state * 4164903690U + (uint32_t)(state >> 32);
-        return (uint32_t)state;
-    }
-    int uniform(int a, int b) { return a == b ? a : (int)(next() % (unsigned)(b - a) + a); }
-};
 
 inline double dot3(const double* a, const double* b) { return a[0] * b[0] + a[1] * b[1] + a[2] * b[2]; }
 
@@ -484,97 +477,96 @@ void final_fit(const float* obj, const float* img, const std::vector<int>& inl, 
 
 }  // namespace
 
-// Device-resident RANSAC scorer used by both the C ABI and the Tracking loop:
-// obj/img already on the device (dobj, dimg) and on the host (obj, img).
-int ransac_pnp(svo_ctx* ctx, const float* obj, const float* img, const float* dobj, const float* dimg,
-               int n, const double K[9], int iterations, float reproj_err, double confidence,
-               double rvec[3], double tvec[3], std::vector<int>& inliers, int* hyps_out) {
-    const int modelPoints = 5;
+// ---- resumable per-sequence RANSAC (batched GPU scoring between chunks) ----
+void RansacSeq::begin(const float* o, const float* im, int npts, int iterations) {
+    obj = o;
+    img = im;
+    n = npts;
+    rng = 0xFFFFFFFFFFFFFFFFULL;
+    niters = iterations > 1 ? iterations : 1;
+    iter = 0;
+    maxGood = 0;
+    nh = 0;
+    m = 0;
+    best.assign((size_t)(n + 31) / 32, 0u);
+    for (int i = 0; i < 9; i++) bestR[i] = (i % 4 == 0) ? 1.0 : 0.0;
+    direct = n <= 5;
+    done = n < 4;
+    ok = false;
+}
+
+int RansacSeq::gen_chunk(const double K[9]) {
+    m = 0;
+    if (done || direct) return 0;
+    const int want = (niters - iter) < kRansacChunk ? (niters - iter) : kRansacChunk;
+    Rng r{rng};
+    for (int j = 0; j < want; j++) {
+        int idx[5];
+        for (int i = 0; i < 5; i++) {
+            int v;
+            bool dup;
+            do {
+                v = r.uniform(0, n);
+                dup = false;
+                for (int k = 0; k < i; k++) dup |= idx[k] == v;
+            } while (dup);
+            idx[i] = v;
+        }
+        double Rj[9], tj[3], rv[3];
+        valid[j] = epnp_pixels(obj, img, idx, 5, K, Rj, tj);
+        double* hp = hyp + 12 * j;
+        if (valid[j]) {
+            la::rodrigues_inv(Rj, rv);  // the model is stored as (rvec, tvec)
+            la::rodrigues(rv, hp);
+            std::memcpy(hp + 9, tj, sizeof(tj));
+        } else {
+            for (int k = 0; k < 12; k++) hp[k] = 0;
+        }
+    }
+    rng = r.state;
+    m = want;
+    nh += want;
+    return want;
+}
+
+void RansacSeq::consume(const int* counts, const uint32_t* bits, int words_cap, double confidence) {
+    const int words = (n + 31) / 32;
+    for (int j = 0; j < m && iter < niters; j++, iter++) {
+        const int good = valid[j] ? counts[j] : 0;
+        if (good > (maxGood > 4 ? maxGood : 4)) {
+            std::memcpy(best.data(), bits + (size_t)words_cap * j, sizeof(uint32_t) * words);
+            std::memcpy(bestR, hyp + 12 * j, sizeof(double) * 9);
+            maxGood = good;
+            niters = update_num_iters(confidence, (double)(n - good) / n, 5, niters);
+        }
+    }
+    m = 0;
+    if (iter >= niters) done = true;
+}
+
+void RansacSeq::finish(const double K[9]) {
     inliers.clear();
-    if (n < 4) return set_error(ctx, SVO_ERR_ARG, "solvePnPRansac: npoints >= 4 required (CV_Assert)");
-    double R[9], t[3];
-    if (n <= modelPoints) {
-        // model_points == npoints: one solvePnP (EPnP; OpenCV uses P3P for n == 4)
-        if (!epnp_pixels(obj, img, nullptr, n, K, R, t)) return 0;
+    ok = false;
+    if (n < 4) return;
+    if (direct) {
+        double R[9], t[3];
+        if (!epnp_pixels(obj, img, nullptr, n, K, R, t)) return;
         la::rodrigues_inv(R, rvec);
         std::memcpy(tvec, t, sizeof(t));
         for (int i = 0; i < n; i++) inliers.push_back(i);
-        if (hyps_out) *hyps_out = 1;
-        return 1;
+        for (int i = 0; i < n; i++) best[i >> 5] |= 1u << (i & 31);
+        maxGood = n;
+        ok = true;
+        return;
     }
-    const float thr = (float)((double)reproj_err * (double)reproj_err);
-    const int words = (n + 31) / 32;
-    constexpr int kChunk = 16;
-    double* dh = (double*)scratch(ctx, 6, sizeof(double) * 12 * kChunk + sizeof(int) * kChunk +
-                                                sizeof(uint32_t) * (size_t)words * kChunk + 256);
-    if (!dh) return set_error(ctx, SVO_ERR_HIP, "scratch alloc");
-    int* dcnt = (int*)(dh + 12 * kChunk);
-    uint32_t* dbits = (uint32_t*)(dcnt + kChunk);
-    double* hh = (double*)pinned(ctx, sizeof(double) * 12 * kChunk + sizeof(int) * kChunk +
-                                          sizeof(uint32_t) * (size_t)words * kChunk + 256);
-    if (!hh) return set_error(ctx, SVO_ERR_HIP, "pinned alloc");
-    int* hcnt = (int*)(hh + 12 * kChunk);
-    uint32_t* hbits = (uint32_t*)(hcnt + kChunk);
-
-    Rng rng{0xFFFFFFFFFFFFFFFFULL};
-    int niters = iterations > 1 ? iterations : 1;
-    int maxGood = 0, nh = 0;
-    std::vector<uint32_t> best((size_t)words, 0);
-    double bestR[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1};
-    int iter = 0;
-    while (iter < niters) {
-        const int m = (niters - iter) < kChunk ? (niters - iter) : kChunk;
-        bool valid[kChunk];
-        for (int j = 0; j < m; j++) {
-            int idx[5];
-            for (int i = 0; i < modelPoints; i++) {
-                int v;
-                bool dup;
-                do {
-                    v = rng.uniform(0, n);
-                    dup = false;
-                    for (int k = 0; k < i; k++) dup |= idx[k] == v;
-                } while (dup);
-                idx[i] = v;
-            }
-            double Rj[9], tj[3], rv[3];
-            valid[j] = epnp_pixels(obj, img, idx, modelPoints, K, Rj, tj);
-            double* hyp = hh + 12 * j;
-            if (valid[j]) {
-                la::rodrigues_inv(Rj, rv);  // the model is stored as (rvec, tvec)
-                la::rodrigues(rv, hyp);
-                std::memcpy(hyp + 9, tj, sizeof(tj));
-            } else {
-                for (int k = 0; k < 12; k++) hyp[k] = 0;
-            }
-        }
-        nh += m;
-        SVO_HIP(ctx, hipMemcpyAsync(dh, hh, sizeof(double) * 12 * m, hipMemcpyHostToDevice, ctx->stream));
-        SVO_HIP(ctx, launch_pnp_residuals(dobj, dimg, n, dh, m, K[0], K[4], K[2], K[5], thr, nullptr, dbits,
-                                          dcnt, ctx->stream));
-        SVO_HIP(ctx, hipMemcpyAsync(hcnt, dcnt, sizeof(int) * m, hipMemcpyDeviceToHost, ctx->stream));
-        SVO_HIP(ctx, hipMemcpyAsync(hbits, dbits, sizeof(uint32_t) * (size_t)words * m, hipMemcpyDeviceToHost,
-                                    ctx->stream));
-        SVO_HIP(ctx, hipStreamSynchronize(ctx->stream));
-        for (int j = 0; j < m && iter < niters; j++, iter++) {
-            const int good = valid[j] ? hcnt[j] : 0;
-            if (good > (maxGood > modelPoints - 1 ? maxGood : modelPoints - 1)) {
-                std::memcpy(best.data(), hbits + (size_t)words * j, sizeof(uint32_t) * words);
-                std::memcpy(bestR, hh + 12 * j, sizeof(double) * 9);
-                maxGood = good;
-                niters = update_num_iters(confidence, (double)(n - good) / n, modelPoints, niters);
-            }
-        }
-    }
-    if (hyps_out) *hyps_out = nh;
-    if (maxGood <= 0) return 0;
+    if (maxGood <= 0) return;
     for (int i = 0; i < n; i++)
         if ((best[i >> 5] >> (i & 31)) & 1) inliers.push_back(i);
     double Rf[9], tf[3];
     final_fit(obj, img, inliers, K, bestR, Rf, tf);
     la::rodrigues_inv(Rf, rvec);
     std::memcpy(tvec, tf, sizeof(tf));
-    return 1;
+    ok = true;
 }
 
 }  // namespace svo
@@ -589,18 +581,48 @@ extern "C" int svo_solve_pnp_ransac(svo_ctx* ctx, const double* obj_xyz, const f
     if (!(confidence > 0 && confidence < 1)) return set_error(ctx, SVO_ERR_ARG, "confidence in (0,1)");
     std::vector<float> obj(3 * (size_t)n);
     for (size_t i = 0; i < obj.size(); i++) obj[i] = (float)obj_xyz[i];  // Point3d -> CV_32F
-    float* d = (float*)scratch(ctx, 5, sizeof(float) * 5 * (size_t)n + 64);
-    if (!d) return set_error(ctx, SVO_ERR_HIP, "scratch alloc");
-    SVO_HIP(ctx, hipMemcpyAsync(d, obj.data(), sizeof(float) * 3 * n, hipMemcpyHostToDevice, ctx->stream));
-    SVO_HIP(ctx, hipMemcpyAsync(d + 3 * (size_t)n, img_xy, sizeof(float) * 2 * n, hipMemcpyHostToDevice,
-                                ctx->stream));
-    std::vector<int> inl;
-    int hyps = 0;
-    int r = ransac_pnp(ctx, obj.data(), img_xy, d, d + 3 * (size_t)n, n, K, iterations, reproj_err, confidence,
-                       rvec, tvec, inl, &hyps);
-    if (r < 0) return r;
+    const int words = (n + 31) / 32;
+    const size_t dbytes = sizeof(float) * 5 * (size_t)n + sizeof(double) * 12 * kRansacChunk +
+                          sizeof(int) * kRansacChunk + sizeof(uint32_t) * (size_t)words * kRansacChunk + 1024;
+    char* d = (char*)scratch(ctx, 5, dbytes);
+    char* h = (char*)pinned(ctx, sizeof(int) * kRansacChunk + sizeof(uint32_t) * (size_t)words * kRansacChunk +
+                                     sizeof(double) * 12 * kRansacChunk + 256);
+    if (!d || !h) return set_error(ctx, SVO_ERR_HIP, "scratch alloc");
+    double* dh = (double*)d;
+    int* dcnt = (int*)(dh + 12 * kRansacChunk);
+    uint32_t* dbits = (uint32_t*)(dcnt + kRansacChunk);
+    float* dobj = (float*)(dbits + (size_t)words * kRansacChunk);
+    float* dimg = dobj + 3 * (size_t)n;
+    double* hh = (double*)h;
+    int* hcnt = (int*)(hh + 12 * kRansacChunk);
+    uint32_t* hbits = (uint32_t*)(hcnt + kRansacChunk);
+    SVO_HIP(ctx, hipMemcpyAsync(dobj, obj.data(), sizeof(float) * 3 * n, hipMemcpyHostToDevice, ctx->stream));
+    SVO_HIP(ctx, hipMemcpyAsync(dimg, img_xy, sizeof(float) * 2 * n, hipMemcpyHostToDevice, ctx->stream));
+    const float thr = (float)((double)reproj_err * (double)reproj_err);
+    RansacSeq rs;
+    rs.begin(obj.data(), img_xy, n, iterations);
+    while (!rs.done && !rs.direct) {
+        const int m = rs.gen_chunk(K);
+        if (m == 0) break;
+        std::memcpy(hh, rs.hyp, sizeof(double) * 12 * m);
+        SVO_HIP(ctx, hipMemcpyAsync(dh, hh, sizeof(double) * 12 * m, hipMemcpyHostToDevice, ctx->stream));
+        PnpBatch b{dobj, dimg, nullptr, n, n, dh, m, nullptr, dbits, words, dcnt};
+        SVO_HIP(ctx, launch_pnp_residuals(b, 1, n, K[0], K[4], K[2], K[5], thr, ctx->stream));
+        SVO_HIP(ctx, hipMemcpyAsync(hcnt, dcnt, sizeof(int) * m, hipMemcpyDeviceToHost, ctx->stream));
+        SVO_HIP(ctx, hipMemcpyAsync(hbits, dbits, sizeof(uint32_t) * (size_t)words * m, hipMemcpyDeviceToHost,
+                                    ctx->stream));
+        SVO_HIP(ctx, hipStreamSynchronize(ctx->stream));
+        rs.consume(hcnt, hbits, words, confidence);
+    }
+    rs.finish(K);
+    if (!rs.ok) {
+        if (n_inliers) *n_inliers = 0;
+        return 0;
+    }
+    std::memcpy(rvec, rs.rvec, sizeof(rs.rvec));
+    std::memcpy(tvec, rs.tvec, sizeof(rs.tvec));
     if (inliers)
-        for (size_t i = 0; i < inl.size(); i++) inliers[i] = inl[i];
-    if (n_inliers) *n_inliers = (int)inl.size();
-    return r;
+        for (size_t i = 0; i < rs.inliers.size(); i++) inliers[i] = rs.inliers[i];
+    if (n_inliers) *n_inliers = (int)rs.inliers.size();
+    return 1;
 }

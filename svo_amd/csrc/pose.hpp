@@ -1,0 +1,43 @@
+// Host side of the pose update (solvePnPRansac with GPU hypothesis scoring).
+#pragma once
+
+#include <cstdint>
+#include <vector>
+
+namespace svo {
+
+struct Rng {  // cv::RNG (core/include/opencv2/core/operations.hpp): multiply-with-carry
+    uint64_t state;
+    uint32_t next() {
+        state = (uint64_t)(uint32_t)state * 4164903690U + (uint32_t)(state >> 32);
+        return (uint32_t)state;
+    }
+    int uniform(int a, int b) { return a == b ? a : (int)(next() % (unsigned)(b - a) + a); }
+};
+
+constexpr int kRansacChunk = 16;  // hypotheses generated per scoring launch
+
+// RANSACPointSetRegistrator::run for PnP (5-point EPnP kernel), split so the
+// hypotheses of many sequences are scored by one batched kernel launch:
+//   begin -> { gen_chunk -> [GPU: score m hypotheses] -> consume } until done -> finish
+struct RansacSeq {
+    const float* obj = nullptr;  // n x 3 (float, as OpenCV converts Point3d)
+    const float* img = nullptr;  // n x 2
+    int n = 0;
+    uint64_t rng = 0;
+    int niters = 0, iter = 0, maxGood = 0, nh = 0, m = 0;
+    bool done = true, direct = false, ok = false;
+    bool valid[kRansacChunk];
+    double hyp[12 * kRansacChunk];
+    std::vector<uint32_t> best;
+    double bestR[9];
+    std::vector<int> inliers;
+    double rvec[3] = {0, 0, 0}, tvec[3] = {0, 0, 0};
+
+    void begin(const float* obj, const float* img, int n, int iterations);
+    int gen_chunk(const double K[9]);  // fills hyp[0..m) (R row-major + t); returns m
+    void consume(const int* counts, const uint32_t* bits, int words_cap, double confidence);
+    void finish(const double K[9]);    // final SQPnP-objective fit on the inliers
+};
+
+}  // namespace svo

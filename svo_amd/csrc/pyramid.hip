@@ -26,9 +26,9 @@ constexpr int PD_TY = 16;   // output tile height
 constexpr int PD_IW = 2 * PD_TX + 4;  // 132 input columns
 constexpr int PD_IH = 2 * PD_TY + 4;  // 36 input rows
 
-__global__ __launch_bounds__(256) void pyr_down_kernel(const uint8_t* __restrict__ src, int sw,
-                                                       int sh, int sp, uint8_t* __restrict__ dst,
-                                                       int dw, int dh, int dp) {
+__device__ __forceinline__ void pyr_down_tile(const uint8_t* __restrict__ src, int sw, int sh,
+                                              int sp, uint8_t* __restrict__ dst, int dw, int dh,
+                                              int dp) {
     __shared__ uint8_t T[PD_IH][PD_IW + 4];
     __shared__ int H[PD_IH][PD_TX + 1];
     const int x0 = blockIdx.x * PD_TX, y0 = blockIdx.y * PD_TY;
@@ -66,6 +66,35 @@ __global__ __launch_bounds__(256) void pyr_down_kernel(const uint8_t* __restrict
             dst[(size_t)y * dp + x] = (uint8_t)((s + 128) >> 8);
         }
     }
+}
+
+__global__ __launch_bounds__(256) void pyr_down_kernel(const uint8_t* __restrict__ src, int sw,
+                                                       int sh, int sp, uint8_t* __restrict__ dst,
+                                                       int dw, int dh, int dp) {
+    pyr_down_tile(src, sw, sh, sp, dst, dw, dh, dp);
+}
+
+// Batched form: blockIdx.z = sequence, level l of descs[z] from level l-1.
+__global__ __launch_bounds__(256) void pyr_down_batched_kernel(const PyrDesc* __restrict__ descs,
+                                                               int level) {
+    const PyrDesc& P = descs[blockIdx.z];
+    const ImgLevel& s = P.lv[level - 1];
+    const ImgLevel& d = P.lv[level];
+    if ((int)blockIdx.x * PD_TX >= d.w || (int)blockIdx.y * PD_TY >= d.h) return;
+    // same body as pyr_down_kernel (inlined call keeps one copy of the math)
+    pyr_down_tile(s.data, s.w, s.h, s.pitch, const_cast<uint8_t*>(d.data), d.w, d.h, d.pitch);
+}
+
+hipError_t launch_pyramid_batched(const PyrDesc* d_descs, int nseq, int w, int h, int nlevels,
+                                  hipStream_t st) {
+    int lw = w, lh = h;
+    for (int l = 1; l < nlevels; l++) {
+        lw = (lw + 1) / 2;
+        lh = (lh + 1) / 2;
+        dim3 grid((lw + PD_TX - 1) / PD_TX, (lh + PD_TY - 1) / PD_TY, nseq);
+        hipLaunchKernelGGL(pyr_down_batched_kernel, grid, dim3(256), 0, st, d_descs, l);
+    }
+    return hipGetLastError();
 }
 
 hipError_t launch_pyramid(const svo_image* img, int first_level, hipStream_t st) {

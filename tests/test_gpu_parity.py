@@ -250,3 +250,24 @@ def test_pnp_ransac_inliers_identical(ctx):
 def test_pnp_ransac_too_few_points(ctx):
     with pytest.raises(S.SvoError):
         ctx.solve_pnp_ransac(np.zeros((3, 3)), np.zeros((3, 2), np.float32), np.eye(3))
+
+
+def test_lk_negative_bilinear_weight_case(ctx):
+    """OpenCV's rounded weights can make iw11 = 2^14 - iw00 - iw01 - iw10 = -1
+    (fractional offsets (0.00706080, 0.00132304) or (0.0000501, 0.2830146)):
+    the fixed-point dot products must be signed."""
+    sc, A, B = frames(640, 376, seed=3)
+    base = np.floor(O.fast(A, 20, True)[:300, :2])
+    fr = np.array([[0.0070608025416731834, 0.0013230398762971163], [5.0094684411305934e-05, 0.28301456570625305]],
+                  np.float32)
+    pts = np.concatenate([base + fr[0], base + fr[1]]).astype(np.float32)
+    guess = (pts + np.float32(1.0)).astype(np.float32)   # same fractions at the first J sample
+    ga, gb = ctx.image(A, 4), ctx.image(B, 4)
+    for cfg in (TEMPORAL, STEREO):
+        for ml, flags, nxt in ((cfg["ml"], cfg["flags"], None), (0, cfg["flags"] | S.LK_USE_INITIAL_FLOW, guess)):
+            gn, gs, ge = ctx.calc_optical_flow_pyr_lk(ga, gb, pts, next_pts=nxt, win_size=cfg["win"], max_level=ml,
+                                                      criteria=cfg["crit"], flags=flags)
+            rn, rs, re_, _ = O.lk(A, B, pts, cfg["win"], ml, cfg["crit"], flags, next_pts=nxt)
+            assert np.array_equal(gs, rs)
+            assert np.array_equal(gn.view(np.uint32), rn.view(np.uint32))
+            assert np.array_equal(ge.view(np.uint32), re_.view(np.uint32))

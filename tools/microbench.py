@@ -1,0 +1,56 @@
+#!/usr/bin/env python3
+"""Kernel micro-benchmarks through the C ABI (for rocprofv3 runs).
+
+    python tools/microbench.py lk --points 128000 --reps 5
+    python tools/microbench.py pyr --reps 20
+    python tools/microbench.py fast --reps 20
+"""
+import argparse
+import os
+import sys
+import time
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import svo_amd as S  # noqa: E402
+from svo_amd.scene import Scene  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("what", choices=["lk", "pyr", "fast", "stereo"])
+    ap.add_argument("--points", type=int, default=128000)
+    ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--w", type=int, default=1241)
+    ap.add_argument("--h", type=int, default=376)
+    args = ap.parse_args()
+    ctx = S.Context(0)
+    sc = Scene(args.w, args.h, seed=0)
+    A, B = sc.frame(0), sc.frame(1)
+    ga, gb = ctx.image(A, 4), ctx.image(B, 4)
+    if args.what in ("lk", "stereo"):
+        kp = ctx.fast_detect(ga, 20, True)[:, :2]
+        reps = -(-args.points // len(kp))
+        rng = np.random.default_rng(0)
+        pts = np.concatenate([kp + rng.uniform(-0.5, 0.5, kp.shape).astype(np.float32) * (i > 0)
+                              for i in range(reps)])[: args.points]
+        win, crit, flags = ((21, 21), (3, 50, 1e-3), S.LK_GET_MIN_EIGENVALS) if args.what == "lk" else \
+            ((11, 11), (3, 30, 1e-3), 0)
+        for r in range(args.reps):
+            t = time.perf_counter()
+            ctx.calc_optical_flow_pyr_lk(ga, gb, pts, win_size=win, max_level=3, criteria=crit, flags=flags)
+            dt = time.perf_counter() - t
+            print(f"{args.what} {len(pts)} pts: {dt*1e3:.3f} ms (host incl. copies), iters {ctx.lk_last_iterations()}")
+    elif args.what == "pyr":
+        for r in range(args.reps):
+            ga.upload(A)
+        print("pyr done")
+    elif args.what == "fast":
+        for r in range(args.reps):
+            kp = ctx.fast_detect(ga, 20, True)
+        print("fast", len(kp))
+
+
+if __name__ == "__main__":
+    main()
