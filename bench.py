@@ -157,7 +157,8 @@ def main():
     for t in range(1, Wm + 1):
         fe.step(t)
     fe.reset_times()
-    tot = {"lk_iterations": 0, "tracked": 0, "inliers": 0, "added": 0, "hypotheses": 0}
+    tot = {"lk_iterations": 0, "tracked": 0, "inliers": 0, "added": 0, "hypotheses": 0,
+           "host_ms_hyp": 0.0, "host_ms_fit": 0.0, "host_ms_wait": 0.0}
     lk_units = 0
     feats_prev = None
     barrier(dist)
@@ -219,7 +220,7 @@ def main():
         "achieved_GBps_algorithmic": round(frames * frame_bytes(W, H, N, ML) / dt_max / 1e9, 2),
         "single_stream_fps": round(single, 2) if single else None,
         "phase_ms_per_step": {k: round(v[0] / K, 4) for k, v in phases.items()},
-        "stats_per_step": {k: round(v / K, 1) for k, v in tot.items()},
+        "stats_per_step": {k: round(v / K, 3) for k, v in tot.items()},
         "roofline": {
             "kernel": "lk_kernel (temporal LK, all levels, one wave per feature)",
             "dominant_phase": dominant,

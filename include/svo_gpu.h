@@ -181,6 +181,9 @@ typedef struct svo_frontend_stats {
     int64_t added;          /* new features from the keyframe top-up */
     int64_t features;       /* features after the step */
     int64_t hypotheses;     /* RANSAC hypotheses scored on the GPU */
+    double host_ms_hyp;     /* host wall time generating hypotheses (EPnP) */
+    double host_ms_fit;     /* host wall time in the final fits */
+    double host_ms_wait;    /* host wall time blocked on the GPU */
 } svo_frontend_stats;
 
 int svo_frontend_create(svo_ctx* ctx, const svo_frontend_config* cfg, svo_frontend** out);

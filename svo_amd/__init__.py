@@ -333,10 +333,12 @@ class FrontendConfig(C.Structure):
 
 class FrontendStats(C.Structure):
     _fields_ = [("lk_iterations", C.c_int64), ("tracked", C.c_int64), ("inliers", C.c_int64),
-                ("added", C.c_int64), ("features", C.c_int64), ("hypotheses", C.c_int64)]
+                ("added", C.c_int64), ("features", C.c_int64), ("hypotheses", C.c_int64),
+                ("host_ms_hyp", C.c_double), ("host_ms_fit", C.c_double), ("host_ms_wait", C.c_double)]
 
     def as_dict(self):
-        return {k: int(getattr(self, k)) for k, _ in self._fields_}
+        return {k: (float(getattr(self, k)) if k.startswith("host_") else int(getattr(self, k)))
+                for k, _ in self._fields_}
 
 
 PHASES = ["pyramid", "lk", "compact", "gather", "pnp_score", "mask", "fast", "bucket", "append"]

@@ -213,20 +213,23 @@ int svo_fast_detect(svo_ctx* ctx, const svo_image* img, int threshold, int nonma
         return set_error(ctx, SVO_ERR_ARG, "svo_fast_detect: bad arguments");
     threshold = threshold < 0 ? 0 : threshold > 255 ? 255 : threshold;
     const ImgLevel& L = img->desc.lv[0];
-    size_t npx = (size_t)L.w * L.h;
-    uint16_t* cs = (uint16_t*)scratch(ctx, 0, npx * 2 + 1024);
-    int* rowcnt = (int*)scratch(ctx, 1, sizeof(int) * ((size_t)L.h + 16));
+    const size_t npx = (size_t)L.w * L.h;
+    const int nseg = (L.w + 63) / 64;
+    const int kcap = cap > 0 ? cap : 1;
+    const size_t bbytes = sizeof(unsigned long long) * (size_t)L.h * nseg;
+    char* d = (char*)scratch(ctx, 0, bbytes + sizeof(int) * 2 * ((size_t)L.h + 64) + 1024);
     uint8_t* dmask = mask ? (uint8_t*)scratch(ctx, 2, npx) : nullptr;
-    int kcap = cap > 0 ? cap : 1;
     svo_keypoint* dout = (svo_keypoint*)scratch(ctx, 3, sizeof(svo_keypoint) * (size_t)kcap + 64);
+    if (!d || (mask && !dmask) || !dout) return set_error(ctx, SVO_ERR_HIP, "scratch alloc");
     int* dn = (int*)((char*)dout + sizeof(svo_keypoint) * (size_t)kcap);
-    if (!cs || !rowcnt || (mask && !dmask) || !dout) return set_error(ctx, SVO_ERR_HIP, "scratch alloc");
-    if (mask) SVO_HIP(ctx, hipMemcpyAsync(dmask, mask, npx, hipMemcpyHostToDevice, ctx->stream));
-    PyrDesc* dd = stage_desc(ctx, img, (char*)cs + ((npx * 2 + 255) & ~(size_t)255));
+    PyrDesc* dd = stage_desc(ctx, img, d);
     if (!dd) return set_error(ctx, SVO_ERR_HIP, "desc staging");
-    FastBatch b{dd, cs, dmask, rowcnt, dout, dn, npx, cap};
-    SVO_HIP(ctx, launch_fast_score(b, 1, L.w, L.h, threshold, nonmax ? 1 : 0, ctx->stream));
-    SVO_HIP(ctx, launch_fast_collect(b, 1, L.w, L.h, nonmax ? 1 : 0, ctx->stream));
+    unsigned long long* bits = (unsigned long long*)(d + 256);
+    int* rowcnt = (int*)((char*)bits + ((bbytes + 255) & ~(size_t)255));
+    int* rowoff = rowcnt + L.h + 64;
+    if (mask) SVO_HIP(ctx, hipMemcpyAsync(dmask, mask, npx, hipMemcpyHostToDevice, ctx->stream));
+    FastDetBatch b{dd, dmask, bits, rowcnt, rowoff, dout, dn, npx, nseg, cap};
+    SVO_HIP(ctx, launch_fast_detect(b, 1, L.w, L.h, threshold, nonmax ? 1 : 0, ctx->stream));
     int n = 0;
     SVO_HIP(ctx, hipMemcpyAsync(&n, dn, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
     SVO_HIP(ctx, hipStreamSynchronize(ctx->stream));
@@ -322,11 +325,17 @@ int svo_calc_optical_flow_pyr_lk(svo_ctx* ctx, const svo_image* prev, const svo_
     p.flags = flags;
     p.min_eig = (float)min_eig_threshold;
     p.want_err = err ? 1 : 0;
-    size_t bytes = (size_t)n * (8 + 8 + 1 + 4 + 4) + 2 * sizeof(PyrDesc) + 512;
+    // derivative pyramid of prev (calcSharrDeriv per level), then LK
+    size_t doff[kMaxLevels];
+    int dpitch[kMaxLevels];
+    const size_t dbytes = deriv_layout(prev->w, prev->h, ml + 1, doff, dpitch);
+    size_t bytes = (size_t)n * (8 + 8 + 1 + 4 + 4) + 2 * sizeof(PyrDesc) + sizeof(DerivDesc) + dbytes + 2048;
     char* d = (char*)scratch(ctx, 7, bytes);
     if (!d) return set_error(ctx, SVO_ERR_HIP, "scratch alloc");
     PyrDesc* ddesc = (PyrDesc*)d;
-    d += (2 * sizeof(PyrDesc) + 255) & ~(size_t)255;
+    DerivDesc* dder = (DerivDesc*)(d + 2 * sizeof(PyrDesc));
+    char* dbase = (char*)(((uintptr_t)(d + 2 * sizeof(PyrDesc) + sizeof(DerivDesc)) + 255) & ~(uintptr_t)255);
+    d = dbase + ((dbytes + 255) & ~(size_t)255);
     float* dprev = (float*)d;
     float* dnext = dprev + 2 * (size_t)n;
     float* derr = dnext + 2 * (size_t)n;
@@ -335,13 +344,22 @@ int svo_calc_optical_flow_pyr_lk(svo_ctx* ctx, const svo_image* prev, const svo_
     SVO_HIP(ctx, hipMemcpyAsync(dprev, prev_xy, sizeof(float) * 2 * n, hipMemcpyHostToDevice, ctx->stream));
     if (flags & SVO_LK_USE_INITIAL_FLOW)
         SVO_HIP(ctx, hipMemcpyAsync(dnext, next_xy, sizeof(float) * 2 * n, hipMemcpyHostToDevice, ctx->stream));
-    PyrDesc* hdesc = (PyrDesc*)pinned(ctx, 2 * sizeof(PyrDesc));
-    if (!hdesc) return set_error(ctx, SVO_ERR_HIP, "pinned alloc");
+    struct Staged {
+        PyrDesc pd[2];
+        DerivDesc dd;
+    };
+    Staged* hs = (Staged*)pinned(ctx, sizeof(Staged));
+    if (!hs) return set_error(ctx, SVO_ERR_HIP, "pinned alloc");
     SVO_HIP(ctx, hipStreamSynchronize(ctx->stream));  // pinned staging is reused
-    hdesc[0] = prev->desc;
-    hdesc[1] = next->desc;
-    SVO_HIP(ctx, hipMemcpyAsync(ddesc, hdesc, 2 * sizeof(PyrDesc), hipMemcpyHostToDevice, ctx->stream));
-    LKBatch b{ddesc, ddesc + 1, dprev, dnext, dst, err ? derr : nullptr, diters, nullptr, n, n};
+    hs->pd[0] = prev->desc;
+    hs->pd[1] = next->desc;
+    for (int l = 0; l < kMaxLevels; l++) {
+        hs->dd.data[l] = l <= ml ? (uint32_t*)(dbase + doff[l]) : nullptr;
+        hs->dd.pitch[l] = l <= ml ? dpitch[l] : 0;
+    }
+    SVO_HIP(ctx, hipMemcpyAsync(ddesc, hs, sizeof(Staged), hipMemcpyHostToDevice, ctx->stream));
+    SVO_HIP(ctx, launch_scharr(ddesc, dder, 1, prev->w, prev->h, ml + 1, ctx->stream));
+    LKBatch b{ddesc, ddesc + 1, dder, dprev, dnext, dst, err ? derr : nullptr, diters, nullptr, n, n};
     SVO_HIP(ctx, launch_lk(b, 1, n, p, ctx->stream));
     std::vector<int> it(n);
     SVO_HIP(ctx, hipMemcpyAsync(next_xy, dnext, sizeof(float) * 2 * n, hipMemcpyDeviceToHost, ctx->stream));

@@ -90,10 +90,35 @@ struct FastBatch {
 hipError_t launch_fast_score(const FastBatch& b, int nseq, int w, int h, int threshold, int nonmax,
                              hipStream_t st);
 hipError_t launch_fast_collect(const FastBatch& b, int nseq, int w, int h, int nonmax, hipStream_t st);
+
+// Fused detection path: detect (score + NMS + mask -> 64-bit keep masks per row
+// segment + row counts), scan (row offsets), emit (raster-order keypoints).
+struct FastDetBatch {
+    const PyrDesc* descs;
+    const uint8_t* mask;        // nullable, npx per sequence
+    unsigned long long* bits;   // [s][h][nseg]
+    int* rowcnt;                // [s][h]
+    int* rowoff;                // [s][h]
+    svo_keypoint* out;          // [s][cap]
+    int* n_out;                 // [s]
+    size_t npx;
+    int nseg, cap;
+};
+hipError_t launch_fast_detect(const FastDetBatch& b, int nseq, int w, int h, int threshold, int nonmax,
+                              hipStream_t st);
 // Masks for nseq sequences (w*h each): 255 + filled boxes around counts[s] (or n)
 // points of pts + s*pts_stride.
 hipError_t launch_mask_boxes(int w, int h, const float* pts, const int* counts, int n, int pts_stride,
                              int nseq, float half, uint8_t* mask, hipStream_t st);
+
+// Scharr derivative pyramid of one image (packed int16 Ix | Iy << 16 per pixel).
+struct DerivDesc {
+    uint32_t* data[kMaxLevels];
+    int pitch[kMaxLevels];  // elements
+};
+size_t deriv_layout(int w, int h, int nlevels, size_t* off, int* pitch);
+hipError_t launch_scharr(const PyrDesc* d_pyrs, const DerivDesc* d_ders, int nseq, int w, int h, int nlevels,
+                         hipStream_t st);
 
 struct LKParams {
     int win_w, win_h;
@@ -107,8 +132,9 @@ struct LKParams {
 // Batched LK: blockIdx.y = sequence; sequence s owns points [s*cap, s*cap + n_s)
 // of every array, n_s = counts[s] (device) or n when counts is null.
 struct LKBatch {
-    const PyrDesc* prev;  // [nseq] device
-    const PyrDesc* next;  // [nseq] device
+    const PyrDesc* prev;     // [nseq] device
+    const PyrDesc* next;     // [nseq] device
+    const DerivDesc* dprev;  // [nseq] device: Scharr pyramid of prev (launch_scharr)
     const float* prev_xy;
     float* next_xy;
     uint8_t* status;

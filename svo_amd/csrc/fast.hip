@@ -39,6 +39,40 @@ __device__ __forceinline__ bool run9(unsigned m16) {
     return (r & 0xFFFFu) != 0;
 }
 
+// cornerScore<16> (fast_score.cpp) of the pixel with value v and ring values.
+__device__ __forceinline__ int corner_score16(int v, const int* ring, int threshold) {
+    int d[25];
+#pragma unroll
+    for (int k = 0; k < 25; k++) d[k] = v - ring[k & 15];
+    int a0 = threshold;
+#pragma unroll
+    for (int k = 0; k < 16; k += 2) {
+        int a = min(d[k + 1], d[k + 2]);
+        a = min(a, d[k + 3]);
+        a = min(a, d[k + 4]);
+        a = min(a, d[k + 5]);
+        a = min(a, d[k + 6]);
+        a = min(a, d[k + 7]);
+        a = min(a, d[k + 8]);
+        a0 = max(a0, min(a, d[k]));
+        a0 = max(a0, min(a, d[k + 9]));
+    }
+    int b0 = -a0;
+#pragma unroll
+    for (int k = 0; k < 16; k += 2) {
+        int b = max(d[k + 1], d[k + 2]);
+        b = max(b, d[k + 3]);
+        b = max(b, d[k + 4]);
+        b = max(b, d[k + 5]);
+        b = max(b, d[k + 6]);
+        b = max(b, d[k + 7]);
+        b = max(b, d[k + 8]);
+        b0 = min(b0, max(b, d[k]));
+        b0 = min(b0, max(b, d[k + 9]));
+    }
+    return (-b0 - 1) & 0xFF;  // (uchar) cast in FAST_t
+}
+
 __global__ __launch_bounds__(256) void fast_score_kernel(FastBatch B, int threshold,
                                                          int want_score) {
     const ImgLevel L = B.descs[blockIdx.z].lv[0];
@@ -73,39 +107,7 @@ __global__ __launch_bounds__(256) void fast_score_kernel(FastBatch B, int thresh
                 dark |= (unsigned)(ring[k] < v - threshold) << k;
             }
             if (run9(bright) || run9(dark)) {
-                int score = 0;
-                if (want_score) {
-                    int d[25];
-#pragma unroll
-                    for (int k = 0; k < 25; k++) d[k] = v - ring[k & 15];
-                    int a0 = threshold;
-#pragma unroll
-                    for (int k = 0; k < 16; k += 2) {
-                        int a = min(d[k + 1], d[k + 2]);
-                        a = min(a, d[k + 3]);
-                        a = min(a, d[k + 4]);
-                        a = min(a, d[k + 5]);
-                        a = min(a, d[k + 6]);
-                        a = min(a, d[k + 7]);
-                        a = min(a, d[k + 8]);
-                        a0 = max(a0, min(a, d[k]));
-                        a0 = max(a0, min(a, d[k + 9]));
-                    }
-                    int b0 = -a0;
-#pragma unroll
-                    for (int k = 0; k < 16; k += 2) {
-                        int b = max(d[k + 1], d[k + 2]);
-                        b = max(b, d[k + 3]);
-                        b = max(b, d[k + 4]);
-                        b = max(b, d[k + 5]);
-                        b = max(b, d[k + 6]);
-                        b = max(b, d[k + 7]);
-                        b = max(b, d[k + 8]);
-                        b0 = min(b0, max(b, d[k]));
-                        b0 = min(b0, max(b, d[k + 9]));
-                    }
-                    score = (-b0 - 1) & 0xFF;
-                }
+                const int score = want_score ? corner_score16(v, ring, threshold) : 0;
                 out = (uint16_t)(0x100 | score);
             }
         }
@@ -193,6 +195,150 @@ __global__ __launch_bounds__(256) void fast_write_kernel(FastBatch B, int w, int
     }
 }
 
+// ---- fused detection: FAST-9 + score + NMS + mask for a 64x16 tile (scores
+// of a 1-pixel halo recomputed), one 64-bit keep mask per (row, 64-px segment)
+// and per-row counts (integer atomics) ----
+constexpr int FD_TX = 64, FD_TY = 16;
+constexpr int FD_SW = FD_TX + 2, FD_SH = FD_TY + 2;  // score region (halo 1)
+constexpr int FD_IW = FD_TX + 8, FD_IH = FD_TY + 8;  // image region (halo 4)
+
+__global__ __launch_bounds__(256) void fast_detect_kernel(FastDetBatch B, int threshold, int nonmax) {
+    const ImgLevel L = B.descs[blockIdx.z].lv[0];
+    const int w = L.w, h = L.h;
+    const int x0 = blockIdx.x * FD_TX, y0 = blockIdx.y * FD_TY;
+    const size_t seq = blockIdx.z;
+    __shared__ uint8_t T[FD_IH][FD_IW];
+    __shared__ uint16_t SC[FD_SH][FD_SW + 2];  // bit 8: corner, low byte: score
+    const int tid = threadIdx.x;
+    const bool inside = x0 >= 4 && y0 >= 4 && x0 - 4 + FD_IW <= w && y0 - 4 + FD_IH <= h;
+    if (inside) {
+        for (int k = tid; k < FD_IH * (FD_IW / 4); k += 256) {
+            const int r = k / (FD_IW / 4), c4 = k - r * (FD_IW / 4);
+            const uint8_t* src = L.data + (size_t)(y0 - 4 + r) * L.pitch + (x0 - 4 + 4 * c4);
+            // x0 - 4 is a multiple of 4 and pitch is a multiple of 64: aligned dword
+            *reinterpret_cast<uint32_t*>(&T[r][4 * c4]) = *reinterpret_cast<const uint32_t*>(src);
+        }
+    } else {
+        for (int k = tid; k < FD_IH * FD_IW; k += 256) {
+            const int r = k / FD_IW, c = k - r * FD_IW;
+            const int y = y0 - 4 + r, x = x0 - 4 + c;
+            T[r][c] = ((unsigned)y < (unsigned)h && (unsigned)x < (unsigned)w) ? L.data[(size_t)y * L.pitch + x] : 0;
+        }
+    }
+    __syncthreads();
+    for (int k = tid; k < FD_SH * FD_SW; k += 256) {
+        const int r = k / FD_SW, c = k - r * FD_SW;
+        const int y = y0 - 1 + r, x = x0 - 1 + c;
+        uint16_t out = 0;
+        if (x >= 3 && x < w - 3 && y >= 3 && y < h - 3) {
+            const int ty = r + 3, tx = c + 3;  // image-tile coords of (x, y)
+            const int v = T[ty][tx];
+            int ring[16];
+            unsigned bright = 0, dark = 0;
+#pragma unroll
+            for (int q = 0; q < 16; q++) {
+                ring[q] = T[ty + c_ring[q][1]][tx + c_ring[q][0]];
+                bright |= (unsigned)(ring[q] > v + threshold) << q;
+                dark |= (unsigned)(ring[q] < v - threshold) << q;
+            }
+            if (run9(bright) || run9(dark)) out = (uint16_t)(0x100 | (nonmax ? corner_score16(v, ring, threshold) : 0));
+        }
+        SC[r][c] = out;
+    }
+    __syncthreads();
+    const int lane = tid & 63, wv = tid >> 6;
+    const int x = x0 + lane;
+    const uint8_t* __restrict__ mask = B.mask ? B.mask + seq * B.npx : nullptr;
+#pragma unroll
+    for (int i = 0; i < FD_TY / 4; i++) {
+        const int r = wv * (FD_TY / 4) + i;
+        const int y = y0 + r;
+        if (y >= h) break;
+        const int c = lane + 1, rr = r + 1;
+        const unsigned v = SC[rr][c];
+        bool keep = (v & 0x100) != 0 && x < w;
+        if (keep && nonmax) {
+            const int s = v & 0xFF;
+            keep = s > (SC[rr][c - 1] & 0xFF) && s > (SC[rr][c + 1] & 0xFF) && s > (SC[rr - 1][c - 1] & 0xFF) &&
+                   s > (SC[rr - 1][c] & 0xFF) && s > (SC[rr - 1][c + 1] & 0xFF) && s > (SC[rr + 1][c - 1] & 0xFF) &&
+                   s > (SC[rr + 1][c] & 0xFF) && s > (SC[rr + 1][c + 1] & 0xFF);
+        }
+        if (keep && mask && mask[(size_t)y * w + x] == 0) keep = false;
+        const unsigned long long bal = __ballot(keep);
+        if (lane == 0) {
+            B.bits[(seq * h + y) * B.nseg + blockIdx.x] = bal;
+            if (bal) atomicAdd(&B.rowcnt[seq * h + y], __popcll(bal));
+        }
+    }
+}
+
+// exclusive scan of the per-row counts of one sequence (one block per sequence)
+__global__ __launch_bounds__(1024) void fast_scan_kernel(FastDetBatch B, int h) {
+    const size_t seq = blockIdx.x;
+    const int* __restrict__ cnt = B.rowcnt + seq * h;
+    int* __restrict__ off = B.rowoff + seq * h;
+    __shared__ int part[1024];
+    __shared__ int carry;
+    const int tid = threadIdx.x;
+    if (tid == 0) carry = 0;
+    __syncthreads();
+    for (int y0 = 0; y0 < h; y0 += 1024) {
+        const int y = y0 + tid;
+        const int v = y < h ? cnt[y] : 0;
+        part[tid] = v;
+        __syncthreads();
+        for (int o = 1; o < 1024; o <<= 1) {
+            const int t = tid >= o ? part[tid - o] : 0;
+            __syncthreads();
+            part[tid] += t;
+            __syncthreads();
+        }
+        if (y < h) off[y] = carry + part[tid] - v;
+        __syncthreads();
+        if (tid == 0) carry += part[1023];
+        __syncthreads();
+    }
+    if (tid == 0) B.n_out[seq] = carry;
+}
+
+// raster-order write of one row's keypoints (one wave per row); the FAST
+// score of a kept corner is recomputed from the image (few pixels)
+__global__ __launch_bounds__(64) void fast_emit_kernel(FastDetBatch B, int threshold, int nonmax) {
+    const int y = blockIdx.x;
+    const size_t seq = blockIdx.y;
+    const ImgLevel L = B.descs[seq].lv[0];
+    const int h = L.h;
+    if (B.rowcnt[seq * h + y] == 0) return;
+    const int lane = threadIdx.x;
+    int off = B.rowoff[seq * h + y];
+    const unsigned long long* bits = B.bits + (seq * h + y) * B.nseg;
+    svo_keypoint* __restrict__ out = B.out + seq * B.cap;
+    for (int sgi = 0; sgi < B.nseg; sgi++) {
+        const unsigned long long m = bits[sgi];
+        if (!m) continue;
+        if ((m >> lane) & 1ull) {
+            const int idx = off + __popcll(m & ((1ull << lane) - 1ull));
+            if (idx < B.cap) {
+                const int x = sgi * 64 + lane;
+                float resp = 0.f;
+                if (nonmax) {
+                    const uint8_t* p = L.data + (size_t)y * L.pitch + x;
+                    int ring[16];
+#pragma unroll
+                    for (int q = 0; q < 16; q++) ring[q] = p[c_ring[q][1] * L.pitch + c_ring[q][0]];
+                    resp = (float)corner_score16(p[0], ring, threshold);
+                }
+                svo_keypoint kp;
+                kp.x = (float)x;
+                kp.y = (float)y;
+                kp.response = resp;
+                out[idx] = kp;
+            }
+        }
+        off += __popcll(m);
+    }
+}
+
 __global__ __launch_bounds__(64) void mask_boxes_kernel(int w, int h, const float* __restrict__ pts_all,
                                                         const int* __restrict__ counts, int n0,
                                                         int pts_stride, float half,
@@ -231,6 +377,17 @@ hipError_t launch_fast_score(const FastBatch& b, int nseq, int w, int h, int thr
 hipError_t launch_fast_collect(const FastBatch& b, int nseq, int w, int h, int nonmax, hipStream_t st) {
     hipLaunchKernelGGL(fast_count_kernel, dim3(h, nseq), dim3(256), 0, st, b, w, h, nonmax);
     hipLaunchKernelGGL(fast_write_kernel, dim3(h, nseq), dim3(256), 0, st, b, w, h, nonmax);
+    return hipGetLastError();
+}
+
+hipError_t launch_fast_detect(const FastDetBatch& b, int nseq, int w, int h, int threshold, int nonmax,
+                              hipStream_t st) {
+    hipError_t e = hipMemsetAsync(b.rowcnt, 0, sizeof(int) * (size_t)h * nseq, st);
+    if (e != hipSuccess) return e;
+    dim3 grid((w + FD_TX - 1) / FD_TX, (h + FD_TY - 1) / FD_TY, nseq);
+    hipLaunchKernelGGL(fast_detect_kernel, grid, dim3(256), 0, st, b, threshold, nonmax);
+    hipLaunchKernelGGL(fast_scan_kernel, dim3(nseq), dim3(1024), 0, st, b, h);
+    hipLaunchKernelGGL(fast_emit_kernel, dim3(h, nseq), dim3(64), 0, st, b, threshold, nonmax);
     return hipGetLastError();
 }
 

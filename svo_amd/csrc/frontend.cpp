@@ -15,6 +15,7 @@
 //
 // FAST and the bucket run on the GPU while the host builds RANSAC hypotheses.
 #include <algorithm>
+#include <chrono>
 #include <atomic>
 #include <condition_variable>
 #include <cstring>
@@ -117,13 +118,15 @@ struct svo_frontend {
     std::vector<int> seed_host;      // [s]
     std::vector<PyrDesc> desc_host;  // [t*S + s]
     PyrDesc* d_desc = nullptr;       // [t][s]
+    void* dermem = nullptr;          // Scharr pyramids, ping-pong [2][s]
+    DerivDesc* d_der = nullptr;      // [2][s]
     // device state (one allocation)
     void* dmem = nullptr;
     float *xyA, *next_xy, *xyB, *obj, *kps, *cand;
-    int *midA, *midB, *nA, *nB, *iters, *kn, *bn, *map_n, *rowcnt, *scr, *cnt, *added, *seed_d;
+    int *midA, *midB, *nA, *nB, *iters, *kn, *bn, *map_n, *rowcnt, *rowoff, *scr, *cnt, *added, *seed_d;
+    unsigned long long* fbits;
     long long* itsum;
     uint8_t *status, *mask;
-    uint16_t* cs;
     uint32_t *bits_all, *bits_best;
     double *map, *hyps, *rot_d;
     // host mirrors (pinned)
@@ -182,11 +185,10 @@ int fe_fast_and_bucket(svo_frontend* fe, const PyrDesc* descs_cur, bool use_mask
     svo_ctx* ctx = fe->ctx;
     hipStream_t st = ctx->stream;
     int slot;
-    FastBatch fb{descs_cur, fe->cs, use_mask ? fe->mask : nullptr, fe->rowcnt, (svo_keypoint*)fe->kps,
-                 fe->kn, fe->npx, fe->KCAP};
+    FastDetBatch fb{descs_cur, use_mask ? fe->mask : nullptr, fe->fbits, fe->rowcnt, fe->rowoff,
+                    (svo_keypoint*)fe->kps, fe->kn, fe->npx, (fe->W + 63) / 64, fe->KCAP};
     ph_begin(fe, PH_FAST, &slot);
-    SVO_HIP(ctx, launch_fast_score(fb, fe->S, fe->W, fe->H, fe->cfg.fast_threshold, fe->cfg.fast_nonmax, st));
-    SVO_HIP(ctx, launch_fast_collect(fb, fe->S, fe->W, fe->H, fe->cfg.fast_nonmax, st));
+    SVO_HIP(ctx, launch_fast_detect(fb, fe->S, fe->W, fe->H, fe->cfg.fast_threshold, fe->cfg.fast_nonmax, st));
     ph_end(fe, slot);
     if (fe->cfg.bucket_size > 0) {
         ph_begin(fe, PH_BUCKET, &slot);
@@ -287,7 +289,8 @@ int svo_frontend_create(svo_ctx* ctx, const svo_frontend_config* cfg, svo_fronte
         add(sizeof(long long) * S);
         add(S * (size_t)CAP);          // status
         add(fe->npx * S);              // mask
-        add(2 * fe->npx * S);          // cs
+        add(sizeof(unsigned long long) * (size_t)S * c.height * ((c.width + 63) / 64));  // FAST keep bits
+        add(sizeof(int) * (size_t)S * c.height);  // rowoff
         add(sizeof(uint32_t) * (size_t)S * kRansacChunk * fe->WORDS);
         add(sizeof(uint32_t) * (size_t)S * fe->WORDS);
         add(sizeof(double) * 3 * (size_t)S * fe->MAPCAP);
@@ -325,7 +328,8 @@ int svo_frontend_create(svo_ctx* ctx, const svo_frontend_config* cfg, svo_fronte
         fe->itsum = carve<long long>(p, S);
         fe->status = carve<uint8_t>(p, (size_t)S * CAP);
         fe->mask = carve<uint8_t>(p, fe->npx * S);
-        fe->cs = carve<uint16_t>(p, fe->npx * S);
+        fe->fbits = carve<unsigned long long>(p, (size_t)S * c.height * ((c.width + 63) / 64));
+        fe->rowoff = carve<int>(p, (size_t)S * c.height);
         fe->bits_all = carve<uint32_t>(p, (size_t)S * kRansacChunk * fe->WORDS);
         fe->bits_best = carve<uint32_t>(p, (size_t)S * fe->WORDS);
         fe->map = carve<double>(p, 3 * (size_t)S * fe->MAPCAP);
@@ -366,6 +370,27 @@ int svo_frontend_create(svo_ctx* ctx, const svo_frontend_config* cfg, svo_fronte
         fe->h_best = carve<uint32_t>(p, (size_t)S * fe->WORDS);
         std::memset(fe->h_nA, 0, sizeof(int) * S);
     }
+    // derivative pyramids of the last two frames of every sequence (ping-pong)
+    {
+        size_t doff[kMaxLevels];
+        int dpitch[kMaxLevels];
+        const size_t dbytes = (deriv_layout(c.width, c.height, fe->nlev, doff, dpitch) + 255) & ~(size_t)255;
+        if (hipMalloc(&fe->dermem, dbytes * 2 * S + 256 + sizeof(DerivDesc) * 2 * S) != hipSuccess) {
+            svo_frontend_destroy(fe);
+            return set_error(ctx, SVO_ERR_HIP, "svo_frontend_create: deriv alloc");
+        }
+        std::vector<DerivDesc> hd(2 * (size_t)S);
+        char* base = (char*)fe->dermem + ((sizeof(DerivDesc) * 2 * S + 255) & ~(size_t)255);
+        for (int k = 0; k < 2 * S; k++)
+            for (int l = 0; l < kMaxLevels; l++) {
+                hd[k].data[l] = l < fe->nlev ? (uint32_t*)(base + dbytes * k + doff[l]) : nullptr;
+                hd[k].pitch[l] = l < fe->nlev ? dpitch[l] : 0;
+            }
+        fe->d_der = (DerivDesc*)fe->dermem;
+        SVO_HIP(ctx, hipMemcpyAsync(fe->d_der, hd.data(), sizeof(DerivDesc) * hd.size(), hipMemcpyHostToDevice,
+                                    ctx->stream));
+        SVO_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    }
     fe->rs.resize(S);
     fe->pose.assign((size_t)S * 6, 0.0);
     int nt = c.host_threads > 0 ? c.host_threads : (int)std::thread::hardware_concurrency();
@@ -386,6 +411,7 @@ void svo_frontend_destroy(svo_frontend* fe) {
     for (auto* f : fe->frames)
         if (f) svo_image_destroy(fe->ctx, f);
     if (fe->dmem) (void)hipFree(fe->dmem);
+    if (fe->dermem) (void)hipFree(fe->dermem);
     if (fe->hmem) (void)hipHostFree(fe->hmem);
     for (auto& e : fe->ev)
         if (e) (void)hipEventDestroy(e);
@@ -426,6 +452,7 @@ int svo_frontend_init(svo_frontend* fe, int t0) {
     const int S = fe->S;
     const PyrDesc* dcur = fe->d_desc + (size_t)(t0 % fe->T) * S;
     SVO_HIP(ctx, launch_pyramid_batched(dcur, S, fe->W, fe->H, fe->nlev, ctx->stream));
+    SVO_HIP(ctx, launch_scharr(dcur, fe->d_der + (size_t)(t0 & 1) * S, S, fe->W, fe->H, fe->nlev, ctx->stream));
     SVO_HIP(ctx, hipMemsetAsync(fe->nA, 0, sizeof(int) * S, ctx->stream));
     SVO_HIP(ctx, hipMemsetAsync(fe->map_n, 0, sizeof(int) * S, ctx->stream));
     int rc = fe_fast_and_bucket(fe, dcur, false);
@@ -451,9 +478,11 @@ int svo_frontend_step(svo_frontend* fe, int t, svo_frontend_stats* stats) {
     int max_prev = 0;
     for (int s = 0; s < S; s++) max_prev = std::max(max_prev, fe->h_nA[s]);
 
-    // 1. pyramid of frame t
+    // 1. pyramid of frame t and its Scharr derivative pyramid (used when frame
+    //    t is the prev image of the next step; OpenCV recomputes it per call)
     ph_begin(fe, PH_PYR, &slot);
     SVO_HIP(ctx, launch_pyramid_batched(dcur, S, fe->W, fe->H, fe->nlev, st));
+    SVO_HIP(ctx, launch_scharr(dcur, fe->d_der + (size_t)(t & 1) * S, S, fe->W, fe->H, fe->nlev, st));
     ph_end(fe, slot);
     // 2. temporal LK (trackFrames)
     LKParams lp;
@@ -465,7 +494,8 @@ int svo_frontend_step(svo_frontend* fe, int t, svo_frontend_stats* stats) {
     lp.flags = c.lk_flags & ~SVO_LK_USE_INITIAL_FLOW;
     lp.min_eig = (float)c.min_eig;
     lp.want_err = 0;
-    LKBatch lb{dprev, dcur, fe->xyA, fe->next_xy, fe->status, nullptr, fe->iters, fe->nA, 0, CAP};
+    LKBatch lb{dprev, dcur, fe->d_der + (size_t)((t - 1) & 1) * S, fe->xyA, fe->next_xy, fe->status, nullptr,
+               fe->iters, fe->nA, 0, CAP};
     ph_begin(fe, PH_LK, &slot);
     SVO_HIP(ctx, launch_lk(lb, S, max_prev, lp, st));
     ph_end(fe, slot);
@@ -493,8 +523,15 @@ int svo_frontend_step(svo_frontend* fe, int t, svo_frontend_stats* stats) {
     SVO_HIP(ctx, hipEventRecord(ready, st));
     int rc = fe_fast_and_bucket(fe, dcur, true);
     if (rc) return rc;
+    using clk = std::chrono::steady_clock;
+    auto ms_since = [](clk::time_point t0) {
+        return std::chrono::duration<double, std::milli>(clk::now() - t0).count();
+    };
+    double ms_hyp = 0, ms_fit = 0, ms_wait = 0;
+    auto tw = clk::now();
     SVO_HIP(ctx, hipEventSynchronize(ready));
     (void)hipEventDestroy(ready);
+    ms_wait += ms_since(tw);
 
     // 5. calculatePose: RANSAC per sequence, hypotheses scored on the GPU
     int max_b = 0;
@@ -507,7 +544,9 @@ int svo_frontend_step(svo_frontend* fe, int t, svo_frontend_stats* stats) {
     int64_t nhyp = 0;
     for (;;) {
         std::vector<int> ms(S, 0);
+        auto th = clk::now();
         fe->pool->run(S, [&](int s) { ms[s] = fe->rs[s].gen_chunk(c.K); });
+        ms_hyp += ms_since(th);
         int mmax = 0;
         for (int s = 0; s < S; s++) mmax = std::max(mmax, ms[s]);
         if (mmax == 0) break;
@@ -530,13 +569,16 @@ int svo_frontend_step(svo_frontend* fe, int t, svo_frontend_stats* stats) {
         SVO_HIP(ctx, hipMemcpyAsync(fe->h_cnt, fe->cnt, sizeof(int) * S * kRansacChunk, hipMemcpyDeviceToHost, st));
         SVO_HIP(ctx, hipMemcpyAsync(fe->h_bits, fe->bits_all, sizeof(uint32_t) * S * kRansacChunk * fe->WORDS,
                                     hipMemcpyDeviceToHost, st));
+        tw = clk::now();
         SVO_HIP(ctx, hipStreamSynchronize(st));
+        ms_wait += ms_since(tw);
         fe->pool->run(S, [&](int s) {
             if (ms[s] > 0)
                 fe->rs[s].consume(fe->h_cnt + (size_t)s * kRansacChunk,
                                   fe->h_bits + (size_t)s * kRansacChunk * fe->WORDS, fe->WORDS, c.pnp_confidence);
         });
     }
+    auto tf = clk::now();
     fe->pool->run(S, [&](int s) {
         RansacSeq& r = fe->rs[s];
         r.finish(c.K);
@@ -552,6 +594,7 @@ int svo_frontend_step(svo_frontend* fe, int t, svo_frontend_stats* stats) {
             for (int i = 0; i < r.n; i++) b[i >> 5] |= 1u << (i & 31);
         }
     });
+    ms_fit += ms_since(tf);
     // 6. drop outliers (R:src/tracking.cpp:218-229), top up to n_features
     SVO_HIP(ctx, hipMemcpyAsync(fe->bits_best, fe->h_best, sizeof(uint32_t) * S * fe->WORDS, hipMemcpyHostToDevice,
                                 st));
@@ -566,7 +609,9 @@ int svo_frontend_step(svo_frontend* fe, int t, svo_frontend_stats* stats) {
     if (rc) return rc;
     SVO_HIP(ctx, hipMemcpyAsync(fe->h_nA, fe->nA, sizeof(int) * S, hipMemcpyDeviceToHost, st));
     SVO_HIP(ctx, hipMemcpyAsync(fe->h_added, fe->added, sizeof(int) * S, hipMemcpyDeviceToHost, st));
+    tw = clk::now();
     SVO_HIP(ctx, hipStreamSynchronize(st));
+    ms_wait += ms_since(tw);
     ph_collect(fe);
     if (stats) {
         std::memset(stats, 0, sizeof(*stats));
@@ -578,6 +623,9 @@ int svo_frontend_step(svo_frontend* fe, int t, svo_frontend_stats* stats) {
         }
         stats->inliers = inl;
         stats->hypotheses = nhyp;
+        stats->host_ms_hyp = ms_hyp;
+        stats->host_ms_fit = ms_fit;
+        stats->host_ms_wait = ms_wait;
     }
     return SVO_OK;
 }

@@ -81,8 +81,8 @@ __device__ __forceinline__ double wave_sum_exact(int v) {
 
 struct LKDev {
     int win_w, win_h, groups;      // strip map: groups = lanes/win_w, RPG rows each
-    int tile_w, tile_h, jr_w, jr_h;
-    int tile_bytes, lds_wave;      // per-wave LDS carve
+    int ip_w, ip_h, jr_w, jr_h;    // staged prev / next pair regions (entries x rows)
+    int ip_bytes, lds_wave;        // per-wave LDS carve
     int max_level, max_count;
     double eps2;
     int flags, want_err;
@@ -92,6 +92,7 @@ struct LKDev {
 constexpr int JM = 3;  // margin (px) of the staged next-image region around the window
 
 typedef const __attribute__((address_space(1))) uint8_t* gu8;  // global (not flat) loads
+typedef const __attribute__((address_space(1))) uint32_t* gu32;
 typedef short s16x2 __attribute__((ext_vector_type(2)));
 
 // v_dot2_i32_i16: both operands signed 16-bit -- OpenCV's rounded bilinear weights
@@ -104,25 +105,9 @@ __device__ __forceinline__ unsigned pack16(int lo, int hi) {
     return ((unsigned)lo & 0xFFFFu) | ((unsigned)hi << 16);
 }
 
-// Cooperative copy of the rw x rh prev-image region at (x0, y0) into LDS bytes
-// (row pitch rw); REFLECT_101 outside the image, as OpenCV's padded pyramid.
-__device__ __forceinline__ void stage_bytes(uint8_t* dst, const ImgLevel& L, int x0, int y0, int rw,
-                                            int rh, int lr, int lc, int rpp) {
-    if (lr >= rpp) return;
-    gu8 src = (gu8)L.data;
-    const bool inside = x0 >= 0 && y0 >= 0 && x0 + rw <= L.w && y0 + rh <= L.h;
-    if (inside) {
-        gu8 q = src + (size_t)(y0 + lr) * L.pitch + (x0 + lc);
-        const size_t step = (size_t)rpp * L.pitch;
-        for (int r = lr; r < rh; r += rpp, q += step) dst[r * rw + lc] = *q;
-    } else {
-        const int sx = refl101(x0 + lc, L.w);
-        for (int r = lr; r < rh; r += rpp) dst[r * rw + lc] = src[(size_t)refl101(y0 + r, L.h) * L.pitch + sx];
-    }
-}
-
-// Next-image region at (x0, y0) as horizontal pixel pairs: entry (r, e) =
-// J(x0+e, y0+r) | J(x0+e+1, y0+r) << 16, ready for one v_dot2_u32_u16 per row.
+// Image region at (x0, y0) as horizontal pixel pairs: entry (r, e) =
+// L(x0+e, y0+r) | L(x0+e+1, y0+r) << 16, ready for one v_dot2_i32_i16 per row;
+// REFLECT_101 outside the image, as OpenCV's padded pyramid levels.
 __device__ __forceinline__ void stage_pairs(unsigned* dst, const ImgLevel& L, int x0, int y0, int rw,
                                             int rh, int lr, int lc, int rpp) {
     if (lr >= rpp) return;
@@ -155,15 +140,16 @@ __global__ __launch_bounds__(256) void lk_kernel(LKBatch B, LKDev p) {
     float* __restrict__ next_xy = B.next_xy + 2 * base;
     const PyrDesc& prev = B.prev[seq];
     const PyrDesc& next = B.next[seq];
-    uint8_t* tile = lds + wid * p.lds_wave;
-    unsigned* jreg = reinterpret_cast<unsigned*>(tile + p.tile_bytes);
+    const DerivDesc& dprev = B.dprev[seq];
+    unsigned* ipair = reinterpret_cast<unsigned*>(lds + wid * p.lds_wave);
+    unsigned* jreg = reinterpret_cast<unsigned*>(lds + wid * p.lds_wave + p.ip_bytes);
 
     const int win_w = p.win_w, win_h = p.win_h;
     const int sc = lane % win_w;
     const int sg = lane / win_w;
     const bool strip = sg < p.groups;
     const int r0 = sg * RPG;
-    const int t_rpp = 64 / p.tile_w, t_lr = lane / p.tile_w, t_lc = lane - t_lr * p.tile_w;
+    const int i_rpp = 64 / p.ip_w, i_lr = lane / p.ip_w, i_lc = lane - i_lr * p.ip_w;
     const int j_rpp = 64 / p.jr_w, j_lr = lane / p.jr_w, j_lc = lane - j_lr * p.jr_w;
 
     const float halfWx = (win_w - 1) * 0.5f, halfWy = (win_h - 1) * 0.5f;
@@ -215,76 +201,70 @@ __global__ __launch_bounds__(256) void lk_kernel(LKBatch B, LKDev p) {
         const int iw11 = (1 << W_BITS) - iw00 - iw01 - iw10;
         const unsigned IW0 = pack16(iw00, iw01), IW1 = pack16(iw10, iw11);
 
-        // ---- stage the prev patch (rows ipy-1.., cols ipx-1..) and the next-image
-        //      region around the initial window: one load burst, one LDS sync ----
+        // ---- stage the prev window (+1 row/col, as pixel pairs) and the next-image
+        //      region around the initial window: one load burst, one LDS sync.
+        //      The Scharr derivative comes from the precomputed derivative pyramid
+        //      (zero outside the image, as OpenCV's zero-padded derivative level). ----
         int jx0 = uni_i(ufloor(nextx - halfWx)) - JM, jy0 = uni_i(ufloor(nexty - halfWy)) - JM;
-        stage_bytes(tile, I, ipx - 1, ipy - 1, p.tile_w, p.tile_h, t_lr, t_lc, t_rpp);
+        stage_pairs(ipair, I, ipx, ipy, p.ip_w, p.ip_h, i_lr, i_lc, i_rpp);
         stage_pairs(jreg, J, jx0, jy0, p.jr_w, p.jr_h, j_lr, j_lc, j_rpp);
+        uint32_t dv[RPG + 1][2];
+        {
+            const int dpitch = dprev.pitch[level];
+            gu32 dsrc = (gu32)dprev.data[level];
+            const bool full_in = ipx >= 0 && ipy >= 0 && ipx + win_w < I.w && ipy + win_h < I.h;
+            const int X = ipx + sc;
+            if (full_in) {
+                gu32 q = dsrc + (size_t)(ipy + r0) * dpitch + X;
+#pragma unroll
+                for (int k = 0; k <= RPG; k++) {
+                    dv[k][0] = dv[k][1] = 0;
+                    if (strip && (FULL || r0 + k <= win_h)) {
+                        dv[k][0] = q[(size_t)k * dpitch];
+                        dv[k][1] = q[(size_t)k * dpitch + 1];
+                    }
+                }
+            } else {
+                const bool c0 = X >= 0 && X < I.w, c1 = X + 1 >= 0 && X + 1 < I.w;
+#pragma unroll
+                for (int k = 0; k <= RPG; k++) {
+                    dv[k][0] = dv[k][1] = 0;
+                    const int Y = ipy + r0 + k;
+                    if (strip && (FULL || r0 + k <= win_h) && Y >= 0 && Y < I.h) {
+                        gu32 q = dsrc + (size_t)Y * dpitch + X;
+                        if (c0) dv[k][0] = q[0];
+                        if (c1) dv[k][1] = q[1];
+                    }
+                }
+            }
+        }
         wave_lds_sync();
 
-        // ---- per-lane strip (column sc, rows r0..): Scharr at grid columns sc and
-        //      sc+1 from tile columns sc..sc+3 (sliding over rows), zero outside the
-        //      image; bilinear I (x32), Ix, Iy at the strip pixels ----
+        // ---- per-lane strip: bilinear I (x32), Ix, Iy at its window pixels ----
         int ival[RPG], gix[RPG], giy[RPG];
         int a11 = 0, a12 = 0, a22 = 0;
         {
-            const bool full_in = ipx >= 0 && ipy >= 0 && ipx + win_w < I.w && ipy + win_h < I.h;
-            const int X0 = ipx + sc;  // image x of grid column sc
-            const bool cin0 = X0 >= 0 && X0 < I.w, cin1 = X0 + 1 >= 0 && X0 + 1 < I.w;
-            const uint8_t* tp = tile + r0 * p.tile_w + sc;
-            int ra[4], rb[4], rc[4];   // tile rows k-2, k-1, k (cols sc..sc+3)
-            int gxa0 = 0, gxa1 = 0, gya0 = 0, gya1 = 0;  // grid row (k-3)
+            const unsigned* ip = ipair + r0 * p.ip_w + sc;
+            unsigned P0 = strip ? ip[0] : 0u;
 #pragma unroll
-            for (int k = 0; k < RPG + 3; k++) {
-#pragma unroll
-                for (int x = 0; x < 4; x++) {
-                    ra[x] = rb[x];
-                    rb[x] = rc[x];
-                    rc[x] = (strip && (FULL || r0 + k <= win_h + 2)) ? tp[k * p.tile_w + x] : 0;
+            for (int j = 0; j < RPG; j++) {
+                ival[j] = gix[j] = giy[j] = 0;
+                if (strip && (FULL || r0 + j < win_h)) {
+                    const unsigned P1 = ip[(j + 1) * p.ip_w];
+                    ival[j] = sdot2(P0, IW0, sdot2(P1, IW1, 1 << (W_BITS - 6))) >> (W_BITS - 5);
+                    P0 = P1;
+                    const unsigned X0 = __builtin_amdgcn_perm(dv[j][1], dv[j][0], 0x05040100u);
+                    const unsigned X1 = __builtin_amdgcn_perm(dv[j + 1][1], dv[j + 1][0], 0x05040100u);
+                    const unsigned Y0 = __builtin_amdgcn_perm(dv[j][1], dv[j][0], 0x07060302u);
+                    const unsigned Y1 = __builtin_amdgcn_perm(dv[j + 1][1], dv[j + 1][0], 0x07060302u);
+                    const int ix = sdot2(X0, IW0, sdot2(X1, IW1, 1 << (W_BITS - 1))) >> W_BITS;
+                    const int iy = sdot2(Y0, IW0, sdot2(Y1, IW1, 1 << (W_BITS - 1))) >> W_BITS;
+                    gix[j] = ix;
+                    giy[j] = iy;
+                    a11 += ix * ix;
+                    a12 += ix * iy;
+                    a22 += iy * iy;
                 }
-                if (k < 2) continue;
-                // grid row g = r0 + k - 2 from tile rows k-2, k-1, k
-                const int v00 = 3 * (ra[0] + rc[0]) + 10 * rb[0], v01 = 3 * (ra[1] + rc[1]) + 10 * rb[1];
-                const int v02 = 3 * (ra[2] + rc[2]) + 10 * rb[2], v03 = 3 * (ra[3] + rc[3]) + 10 * rb[3];
-                const int d0 = rc[0] - ra[0], d1 = rc[1] - ra[1], d2 = rc[2] - ra[2], d3 = rc[3] - ra[3];
-                int gx0 = v02 - v00, gx1 = v03 - v01;
-                int gy0 = 3 * (d2 + d0) + 10 * d1, gy1 = 3 * (d3 + d1) + 10 * d2;
-                if (!full_in) {
-                    const int Y = ipy + r0 + k - 2;
-                    const bool rin = Y >= 0 && Y < I.h;
-                    if (!(rin && cin0)) gx0 = gy0 = 0;
-                    if (!(rin && cin1)) gx1 = gy1 = 0;
-                }
-                if (k >= 3) {
-                    // window row j = k - 3: grid rows j (held) and j+1 (just computed)
-                    const int j = k - 3;
-                    if (j < RPG && (FULL || (strip && r0 + j < win_h))) {
-                        const unsigned P0 = pack16(gxa0, gxa1), P1 = pack16(gx0, gx1);
-                        const unsigned Q0 = pack16(gya0, gya1), Q1 = pack16(gy0, gy1);
-                        const int ix = sdot2(P0, IW0, sdot2(P1, IW1, 1 << (W_BITS - 1))) >> W_BITS;
-                        const int iy = sdot2(Q0, IW0, sdot2(Q1, IW1, 1 << (W_BITS - 1))) >> W_BITS;
-                        // I at tile rows r0+j+1 (= ra) and r0+j+2 (= rb), cols sc+1, sc+2
-                        const unsigned T0 = (unsigned)ra[1] | ((unsigned)ra[2] << 16);
-                        const unsigned T1 = (unsigned)rb[1] | ((unsigned)rb[2] << 16);
-                        ival[j] = sdot2(T0, IW0, sdot2(T1, IW1, 1 << (W_BITS - 6))) >> (W_BITS - 5);
-                        gix[j] = ix;
-                        giy[j] = iy;
-                        a11 += ix * ix;
-                        a12 += ix * iy;
-                        a22 += iy * iy;
-                    } else if (j < RPG) {
-                        ival[j] = gix[j] = giy[j] = 0;
-                    }
-                }
-                gxa0 = gx0;
-                gxa1 = gx1;
-                gya0 = gy0;
-                gya1 = gy1;
-            }
-            if (!strip) {
-#pragma unroll
-                for (int j = 0; j < RPG; j++) ival[j] = gix[j] = giy[j] = 0;
-                a11 = a12 = a22 = 0;
             }
         }
         const float A11 = (float)wave_sum_exact(a11) * FLT_SCALE;
@@ -434,12 +414,12 @@ hipError_t launch_lk(const LKBatch& b, int nseq, int max_n, const LKParams& lp, 
     d.win_h = lp.win_h;
     d.groups = 64 / lp.win_w;
     int rpg = (lp.win_h + d.groups - 1) / d.groups;
-    d.tile_w = lp.win_w + 3;
-    d.tile_h = lp.win_h + 3;
-    d.jr_w = lp.win_w + 2 * JM;       // pair entries per row (cover win_w + 2JM + 1 pixels)
+    d.ip_w = lp.win_w;                // prev window: win_w pairs x (win_h + 1) rows
+    d.ip_h = lp.win_h + 1;
+    d.jr_w = lp.win_w + 2 * JM;       // next region: pair entries per row (win_w + 2JM + 1 pixels)
     d.jr_h = lp.win_h + 1 + 2 * JM;
-    d.tile_bytes = (d.tile_w * d.tile_h + 15) & ~15;
-    d.lds_wave = d.tile_bytes + ((d.jr_w * d.jr_h * 4 + 15) & ~15);
+    d.ip_bytes = (d.ip_w * d.ip_h * 4 + 15) & ~15;
+    d.lds_wave = d.ip_bytes + ((d.jr_w * d.jr_h * 4 + 15) & ~15);
     d.max_level = lp.max_level;
     d.max_count = lp.max_count;
     d.eps2 = lp.eps2;

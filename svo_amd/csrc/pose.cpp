@@ -336,43 +336,53 @@ struct SqpnpCost {
     double P[27];  // t = P vec(R)
 };
 
+// Omega = sum_i (B_i + P)^T A_i (B_i + P) with A_i = I - v v^T / v^T v,
+// B_i vec(R) = R p_i, P = -Q^-1 S: expanded through the sufficient statistics
+// Q = sum A_i, S = sum A_i B_i, M = sum B_i^T A_i B_i as Omega = M - S^T Q^-1 S
+// (one pass, ~130 flops per point).
 void sqpnp_cost(const std::vector<double>& pw, const std::vector<double>& q, SqpnpCost& c) {
     const int n = (int)q.size() / 2;
-    double Q[9] = {0}, S[27] = {0};
-    std::vector<double> A(9 * (size_t)n);
+    static const int IDX[3][3] = {{0, 1, 2}, {1, 3, 4}, {2, 4, 5}};  // unique entries of a sym 3x3
+    double Qs[6] = {0}, T[6][3] = {{0}}, U[6][6] = {{0}};
     for (int i = 0; i < n; i++) {
-        const double v[3] = {q[2 * i], q[2 * i + 1], 1.0};
-        const double nn = v[0] * v[0] + v[1] * v[1] + 1.0;
-        double* Ai = &A[9 * (size_t)i];
-        for (int a = 0; a < 3; a++)
-            for (int b = 0; b < 3; b++) Ai[3 * a + b] = (a == b ? 1.0 : 0.0) - v[a] * v[b] / nn;
-        for (int k = 0; k < 9; k++) Q[k] += Ai[k];
-        for (int a = 0; a < 3; a++)
-            for (int col = 0; col < 9; col++) S[9 * a + col] += Ai[3 * a + col / 3] * pw[3 * i + col % 3];
+        const double x = q[2 * i], y = q[2 * i + 1];
+        const double in = 1.0 / (x * x + y * y + 1.0);
+        const double As[6] = {1.0 - x * x * in, -x * y * in, -x * in, 1.0 - y * y * in, -y * in, 1.0 - in};
+        const double* p = &pw[3 * (size_t)i];
+        const double pp[6] = {p[0] * p[0], p[0] * p[1], p[0] * p[2], p[1] * p[1], p[1] * p[2], p[2] * p[2]};
+        for (int u = 0; u < 6; u++) {
+            Qs[u] += As[u];
+            T[u][0] += As[u] * p[0];
+            T[u][1] += As[u] * p[1];
+            T[u][2] += As[u] * p[2];
+            for (int v = 0; v < 6; v++) U[u][v] += As[u] * pp[v];
+        }
     }
-    double Qi[9];
+    double Q[9], S[27], Qi[9];
+    for (int a = 0; a < 3; a++)
+        for (int b = 0; b < 3; b++) Q[3 * a + b] = Qs[IDX[a][b]];
+    for (int a = 0; a < 3; a++)
+        for (int r = 0; r < 3; r++)
+            for (int j = 0; j < 3; j++) S[9 * a + 3 * r + j] = T[IDX[a][r]][j];
     la::pinv3(Q, Qi);
     for (int a = 0; a < 3; a++)
         for (int col = 0; col < 9; col++)
             c.P[9 * a + col] = -(Qi[3 * a] * S[col] + Qi[3 * a + 1] * S[9 + col] + Qi[3 * a + 2] * S[18 + col]);
-    std::memset(c.Om, 0, sizeof(c.Om));
-    for (int i = 0; i < n; i++) {
-        const double* Ai = &A[9 * (size_t)i];
-        double G[27];
-        for (int a = 0; a < 3; a++)
-            for (int col = 0; col < 9; col++) {
-                double s = Ai[3 * a + col / 3] * pw[3 * i + col % 3];
-                for (int k = 0; k < 3; k++) s += Ai[3 * a + k] * c.P[9 * k + col];
-                G[9 * a + col] = s;
-            }
-        for (int r = 0; r < 9; r++)
-            for (int col = r; col < 9; col++) {
-                const double s = G[r] * G[col] + G[9 + r] * G[9 + col] + G[18 + r] * G[18 + col];
-                c.Om[9 * r + col] += s;
-            }
-    }
-    for (int r = 0; r < 9; r++)
-        for (int col = 0; col < r; col++) c.Om[9 * r + col] = c.Om[9 * col + r];
+    for (int r = 0; r < 3; r++)
+        for (int j = 0; j < 3; j++)
+            for (int s2 = 0; s2 < 3; s2++)
+                for (int k = 0; k < 3; k++) {
+                    // M[(r,j),(s,k)] = sum A_rs p_j p_k ; minus (S^T Qi S) = + S^T P
+                    const double m = U[IDX[r][s2]][IDX[j][k]];
+                    const int R = 3 * r + j, Cc = 3 * s2 + k;
+                    double stp = S[R] * c.P[Cc] + S[9 + R] * c.P[9 + Cc] + S[18 + R] * c.P[18 + Cc];
+                    c.Om[9 * R + Cc] = m + stp;
+                }
+    for (int r = 0; r < 9; r++)  // symmetrise
+        for (int col = 0; col < r; col++) {
+            const double v = 0.5 * (c.Om[9 * r + col] + c.Om[9 * col + r]);
+            c.Om[9 * r + col] = c.Om[9 * col + r] = v;
+        }
 }
 
 double quad(const double* Om, const double* r) {
@@ -488,6 +498,7 @@ void RansacSeq::begin(const float* o, const float* im, int npts, int iterations)
     maxGood = 0;
     nh = 0;
     m = 0;
+    rounds = 0;
     best.assign((size_t)(n + 31) / 32, 0u);
     for (int i = 0; i < 9; i++) bestR[i] = (i % 4 == 0) ? 1.0 : 0.0;
     direct = n <= 5;
@@ -498,7 +509,11 @@ void RansacSeq::begin(const float* o, const float* im, int npts, int iterations)
 int RansacSeq::gen_chunk(const double K[9]) {
     m = 0;
     if (done || direct) return 0;
-    const int want = (niters - iter) < kRansacChunk ? (niters - iter) : kRansacChunk;
+    // chunk schedule 2, 8, 16, 16, ...: clean data stops after the first
+    // hypothesis (niters -> 0), so the first round stays small
+    const int sched = rounds == 0 ? 2 : rounds == 1 ? 8 : kRansacChunk;
+    const int want = (niters - iter) < sched ? (niters - iter) : sched;
+    rounds++;
     Rng r{rng};
     for (int j = 0; j < want; j++) {
         int idx[5];

@@ -25,7 +25,7 @@ struct RansacSeq {
     const float* img = nullptr;  // n x 2
     int n = 0;
     uint64_t rng = 0;
-    int niters = 0, iter = 0, maxGood = 0, nh = 0, m = 0;
+    int niters = 0, iter = 0, maxGood = 0, nh = 0, m = 0, rounds = 0;
     bool done = true, direct = false, ok = false;
     bool valid[kRansacChunk];
     double hyp[12 * kRansacChunk];
