@@ -62,6 +62,11 @@ def dist_setup():
     return world, rank, local, dist
 
 
+def sequence_seeds(rank: int, per_gpu: int):
+    """Seeds of the independent sequences this rank owns (disjoint across ranks)."""
+    return [rank * per_gpu + s + 1 for s in range(per_gpu)]
+
+
 def barrier(dist):
     if dist is not None:
         dist.barrier()
@@ -145,7 +150,7 @@ def main():
     Sq, K, Wm = args.seq, args.steps, args.warmup
     T = Wm + K + 1
     ctx = S.Context(local)
-    seeds = [rank * Sq + s + 1 for s in range(Sq)]
+    seeds = sequence_seeds(rank, Sq)
     scenes = [Scene(W, H, seed=sd) for sd in seeds]
     cfg = S.FrontendConfig(W, H, scenes[0].K, n_seq=Sq, n_frames=T, n_features=N, max_level=ML,
                            host_threads=args.threads, timing=1)

@@ -271,3 +271,28 @@ def test_lk_negative_bilinear_weight_case(ctx):
             assert np.array_equal(gs, rs)
             assert np.array_equal(gn.view(np.uint32), rn.view(np.uint32))
             assert np.array_equal(ge.view(np.uint32), re_.view(np.uint32))
+
+
+# ------------------------------------------------------------------ committed golden fixtures
+def test_gpu_matches_committed_golden(ctx):
+    import os
+    g = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "small_160x120.npz"))
+    A, B = g["A"], g["B"]
+    ga, gb = ctx.image(A, 4), ctx.image(B, 4)
+    for l in range(1, 4):
+        if f"pyr{l}" in g:
+            assert np.array_equal(ga.level(l), g[f"pyr{l}"])
+    assert np.array_equal(ctx.fast_detect(ga, 20, True), g["kp_nms"])
+    assert np.array_equal(ctx.fast_detect(ga, 20, False), g["kp_all"])
+    assert np.array_equal(ctx.fast_detect(ga, 20, True, g["mask"]), g["kp_mask"])
+    n, s, e = ctx.calc_optical_flow_pyr_lk(ga, gb, g["pts"], win_size=(21, 21), max_level=3,
+                                          criteria=(3, 50, 1e-3), flags=S.LK_GET_MIN_EIGENVALS)
+    assert np.array_equal(n, g["t_next"]) and np.array_equal(s, g["t_status"]) and np.array_equal(e, g["t_err"])
+    n, s, e = ctx.calc_optical_flow_pyr_lk(ga, gb, g["pts"], win_size=(11, 11), max_level=3,
+                                          criteria=(3, 30, 1e-3), flags=0)
+    assert np.array_equal(n, g["s_next"]) and np.array_equal(s, g["s_status"]) and np.array_equal(e, g["s_err"])
+    bx, _ = ctx.bucket_features(g["kp_all"][:, :2], 160, 120, 50, 2)
+    assert np.array_equal(bx, g["bucket_xy"])
+    ok, rv, tv, inl = ctx.solve_pnp_ransac(g["X"], g["t_next"], g["K"])
+    assert ok and np.array_equal(inl, g["pnp_inliers"])
+    assert np.allclose(rv, g["pnp_rvec"], atol=1e-7) and np.allclose(tv, g["pnp_tvec"], atol=1e-6)
