@@ -19,6 +19,8 @@
  *     cv::solvePnPRansac, R:src/tracking.cpp:191-196)
  *   cv::solvePnPRansac(..., SOLVEPNP_SQPNP)                      svo_solve_pnp_ransac
  *     R:src/tracking.cpp:191-196
+ *   cv::triangulatePoints + convertPointsFromHomogeneous          svo_triangulate_points
+ *     R:src/tracking.cpp:125-131
  *
  * Conventions (no exceptions cross this ABI; no torch types):
  *   - Host memory is caller-owned. Device memory is owned by the context.
@@ -140,6 +142,16 @@ int svo_solve_pnp_ransac(svo_ctx* ctx, const double* obj_xyz, const float* img_x
                          double confidence, double rvec[3], double tvec[3], int* inliers,
                          int* n_inliers);
 
+/* ------------------------------------------------------------ triangulation
+ * cv::triangulatePoints(P1, P2, pts1, pts2, points4D) then
+ * cv::convertPointsFromHomogeneous (R:src/tracking.cpp:125-131). P1, P2: 3x4
+ * row-major float (cv::Matx34f). Per point the DLT null vector of the 4x4
+ * system, unit length with w >= 0 (OpenCV's sign is arbitrary and cancels),
+ * rounded to float -> xyzw (4n, may be NULL); xyz = xyzw[0:3] * (1/w) in float
+ * (3n, may be NULL). */
+int svo_triangulate_points(svo_ctx* ctx, const float P1[12], const float P2[12], const float* pts1,
+                           const float* pts2, int n, float* xyzw, float* xyz);
+
 /* ------------------------------------------------------------ batched front end
  * The reference's per-frame loop (Tracking::startStereo, R:src/tracking.cpp:232-276:
  * trackFrames -> calculatePose -> keyframe extractFeatures) for n_seq independent
@@ -219,6 +231,14 @@ int svo_synth_canvas(uint64_t seed, int cw, int ch, int n_rect, uint8_t* canvas)
 int svo_synth_frame(const uint8_t* canvas, int cw, int ch, int margin_x, int margin_y,
                     const double R[9], const double K[9], uint64_t noise_seed, int noise,
                     uint8_t* frame, int w, int h);
+
+/* Right view of a rectified stereo pair of the same synthetic scene: the
+ * canvas surface sits at depth rho(u, v) = 12 + 5 sin(u/97 + seed) +
+ * 4 cos(v/61 - seed/2) (world z; the field the frontend's map points use) and
+ * the right camera is the left one shifted by the baseline (fx * b = bf). */
+int svo_synth_frame_right(const uint8_t* canvas, int cw, int ch, int margin_x, int margin_y,
+                          const double R[9], const double K[9], double bf, int depth_seed,
+                          uint64_t noise_seed, int noise, uint8_t* frame, int w, int h);
 
 #ifdef __cplusplus
 }

@@ -32,7 +32,7 @@ import numpy as np
 __all__ = [
     "SvoError", "lib", "Context", "Image", "FastFeatureDetector",
     "TERM_COUNT", "TERM_EPS", "LK_USE_INITIAL_FLOW", "LK_GET_MIN_EIGENVALS",
-    "synth_canvas", "synth_frame", "lib_path", "Frontend", "FrontendConfig", "FrontendStats",
+    "synth_canvas", "synth_frame", "synth_frame_right", "lib_path", "Frontend", "FrontendConfig", "FrontendStats",
 ]
 
 TERM_COUNT = 1
@@ -85,6 +85,7 @@ _SIGS = [
                                     _f32p, _u8p, _i32p]),
     ("svo_solve_pnp_ransac", C.c_int, [_vp, _f64p, _f32p, C.c_int, _f64p, C.c_int, C.c_float,
                                        C.c_double, _f64p, _f64p, _i32p, _i32p]),
+    ("svo_triangulate_points", C.c_int, [_vp, _f32p, _f32p, _f32p, _f32p, C.c_int, _f32p, _f32p]),
     ("svo_frontend_create", C.c_int, [_vp, _vp, C.POINTER(_vp)]),
     ("svo_frontend_destroy", None, [_vp]),
     ("svo_frontend_set_frame", C.c_int, [_vp, C.c_int, C.c_int, _u8p, C.c_int, _f64p, C.c_int]),
@@ -98,6 +99,8 @@ _SIGS = [
     ("svo_synth_canvas", C.c_int, [C.c_uint64, C.c_int, C.c_int, C.c_int, _u8p]),
     ("svo_synth_frame", C.c_int, [_u8p, C.c_int, C.c_int, C.c_int, C.c_int, _f64p, _f64p,
                                   C.c_uint64, C.c_int, _u8p, C.c_int, C.c_int]),
+    ("svo_synth_frame_right", C.c_int, [_u8p, C.c_int, C.c_int, C.c_int, C.c_int, _f64p, _f64p,
+                                        C.c_double, C.c_int, C.c_uint64, C.c_int, _u8p, C.c_int, C.c_int]),
 ]
 
 SYMBOLS = [s[0] for s in _SIGS]
@@ -286,6 +289,21 @@ class Context:
                                             _p(mask, _u8p), _p(counts, _i32p)))
         return err, mask, counts
 
+    def triangulate_points(self, P1, P2, pts1, pts2):
+        """cv::triangulatePoints + convertPointsFromHomogeneous -> (xyzw (n,4), xyz (n,3)) float32."""
+        P1 = _c(P1, np.float32).reshape(12)
+        P2 = _c(P2, np.float32).reshape(12)
+        pts1 = _c(pts1, np.float32).reshape(-1, 2)
+        pts2 = _c(pts2, np.float32).reshape(-1, 2)
+        n = len(pts1)
+        if len(pts2) != n:
+            raise ValueError("pts1 and pts2 differ in length")
+        h = np.empty((n, 4), np.float32)
+        x = np.empty((n, 3), np.float32)
+        self._check(lib().svo_triangulate_points(self.handle, _p(P1, _f32p), _p(P2, _f32p), _p(pts1, _f32p),
+                                                 _p(pts2, _f32p), n, _p(h, _f32p), _p(x, _f32p)))
+        return h, x
+
     def solve_pnp_ransac(self, obj, img_pts, K, iterations: int = 100, reproj_err: float = 8.0,
                          confidence: float = 0.999):
         """cv::solvePnPRansac(..., SOLVEPNP_SQPNP) -> (ok, rvec, tvec, inliers)."""
@@ -440,4 +458,18 @@ def synth_frame(canvas: np.ndarray, margin: tuple, R, K, noise_seed: int, noise:
     if lib().svo_synth_frame(_p(canvas, _u8p), cw, ch, int(margin[0]), int(margin[1]), _p(R, _f64p),
                              _p(K, _f64p), noise_seed, noise, _p(out, _u8p), w, h) != 0:
         raise SvoError("svo_synth_frame failed")
+    return out
+
+
+def synth_frame_right(canvas: np.ndarray, margin: tuple, R, K, bf: float, depth_seed: int, noise_seed: int,
+                      noise: int, w: int, h: int) -> np.ndarray:
+    canvas = _c(canvas, np.uint8)
+    R = _c(R, np.float64).reshape(9)
+    K = _c(K, np.float64).reshape(9)
+    out = np.empty((h, w), np.uint8)
+    ch, cw = canvas.shape
+    if lib().svo_synth_frame_right(_p(canvas, _u8p), cw, ch, int(margin[0]), int(margin[1]), _p(R, _f64p),
+                                   _p(K, _f64p), float(bf), int(depth_seed), noise_seed, noise, _p(out, _u8p),
+                                   w, h) != 0:
+        raise SvoError("svo_synth_frame_right failed")
     return out

@@ -414,4 +414,28 @@ int svo_pnp_residuals(svo_ctx* ctx, const float* obj_xyz, const float* img_xy, i
     return SVO_OK;
 }
 
+int svo_triangulate_points(svo_ctx* ctx, const float P1[12], const float P2[12], const float* pts1,
+                           const float* pts2, int n, float* xyzw, float* xyz) {
+    if (!ctx || !P1 || !P2 || n < 0 || (n > 0 && (!pts1 || !pts2)))
+        return set_error(ctx, SVO_ERR_ARG, "svo_triangulate_points: bad arguments");
+    if (n == 0) return SVO_OK;
+    const size_t bytes = sizeof(float) * (24 + 4 * (size_t)n + 7 * (size_t)n) + 1024;
+    float* d = (float*)scratch(ctx, 6, bytes);
+    if (!d) return set_error(ctx, SVO_ERR_HIP, "scratch alloc");
+    float* dP = d;
+    float* dp1 = dP + 24;
+    float* dp2 = dp1 + 2 * (size_t)n;
+    float* dh = dp2 + 2 * (size_t)n;
+    float* dx = dh + 4 * (size_t)n;
+    SVO_HIP(ctx, hipMemcpyAsync(dP, P1, sizeof(float) * 12, hipMemcpyHostToDevice, ctx->stream));
+    SVO_HIP(ctx, hipMemcpyAsync(dP + 12, P2, sizeof(float) * 12, hipMemcpyHostToDevice, ctx->stream));
+    SVO_HIP(ctx, hipMemcpyAsync(dp1, pts1, sizeof(float) * 2 * n, hipMemcpyHostToDevice, ctx->stream));
+    SVO_HIP(ctx, hipMemcpyAsync(dp2, pts2, sizeof(float) * 2 * n, hipMemcpyHostToDevice, ctx->stream));
+    SVO_HIP(ctx, launch_triangulate(dP, dp1, dp2, n, dh, dx, ctx->stream));
+    if (xyzw) SVO_HIP(ctx, hipMemcpyAsync(xyzw, dh, sizeof(float) * 4 * n, hipMemcpyDeviceToHost, ctx->stream));
+    if (xyz) SVO_HIP(ctx, hipMemcpyAsync(xyz, dx, sizeof(float) * 3 * n, hipMemcpyDeviceToHost, ctx->stream));
+    SVO_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    return SVO_OK;
+}
+
 }  // extern "C"

@@ -179,6 +179,8 @@ struct BucketBatch {
     int* scr;
     size_t scr_stride;
 };
+hipError_t launch_triangulate(const float* d_P, const float* d_p1, const float* d_p2, int n, float* d_xyzw,
+                              float* d_xyz, hipStream_t st);
 size_t bucket_scratch_ints(int img_w, int img_h, int bucket, int per_bucket, int n);
 hipError_t launch_bucket(const BucketBatch& b, int nseq, int img_w, int img_h, int bucket, int per_bucket,
                          hipStream_t st);

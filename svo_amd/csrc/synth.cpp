@@ -79,3 +79,44 @@ extern "C" int svo_synth_frame(const uint8_t* canvas, int cw, int ch, int margin
         }
     return SVO_OK;
 }
+
+// Right image of a rectified stereo rig (baseline along camera x, fx*b = bf):
+// the canvas points now sit at the depth field rho(cu, cv) (world z, the same
+// field the map points use), so the right view of right pixel (xr, y) is the
+// left view of the pixel xl solving xl = xr + bf / z(xl, y), with z the
+// camera-frame depth of the surface point seen at left pixel (xl, y).
+// Fixed-point iteration (a contraction: |d(bf/z)/dx| << 1 for this field).
+extern "C" int svo_synth_frame_right(const uint8_t* canvas, int cw, int ch, int margin_x, int margin_y,
+                                     const double R[9], const double K[9], double bf, int depth_seed,
+                                     uint64_t noise_seed, int noise, uint8_t* frame, int w, int h) {
+    if (!canvas || !R || !K || !frame || w <= 0 || h <= 0) return SVO_ERR_ARG;
+    const double fx = K[0], fy = K[4], cx = K[2], cy = K[5];
+    const double seed = (double)depth_seed;
+    for (int y = 0; y < h; y++)
+        for (int x = 0; x < w; x++) {
+            double xl = x, u = -1, v = -1;
+            for (int it = 0; it < 12; it++) {
+                const double dx = (xl - cx) / fx, dy = (y - cy) / fy;
+                const double wx = R[0] * dx + R[3] * dy + R[6];
+                const double wy = R[1] * dx + R[4] * dy + R[7];
+                const double wz = R[2] * dx + R[5] * dy + R[8];
+                if (!(wz > 0)) break;
+                const double cu = fx * wx / wz + cx, cv = fy * wy / wz + cy;
+                const double rho = 12.0 + 5.0 * std::sin(cu / 97.0 + seed) + 4.0 * std::cos(cv / 61.0 - 0.5 * seed);
+                u = cu + margin_x;
+                v = cv + margin_y;
+                xl = x + bf * wz / rho;  // camera-frame depth of the surface point = rho / wz
+            }
+            u = u < 0 ? 0 : u > cw - 1.001 ? cw - 1.001 : u;
+            v = v < 0 ? 0 : v > ch - 1.001 ? ch - 1.001 : v;
+            const int iu = (int)u, iv = (int)v;
+            const double a = u - iu, b = v - iv;
+            const uint8_t* c0 = canvas + (size_t)iv * cw + iu;
+            const uint8_t* c1 = c0 + cw;
+            double val = (1 - a) * (1 - b) * c0[0] + a * (1 - b) * c0[1] + (1 - a) * b * c1[0] + a * b * c1[1];
+            if (noise > 0) val += (int)(hash3(noise_seed, (uint64_t)x, (uint64_t)y) % (uint64_t)(2 * noise + 1)) - noise;
+            int iv8 = (int)std::floor(val + 0.5);
+            frame[(size_t)y * w + x] = (uint8_t)(iv8 < 0 ? 0 : iv8 > 255 ? 255 : iv8);
+        }
+    return SVO_OK;
+}

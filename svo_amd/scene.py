@@ -16,12 +16,16 @@ import math
 
 import numpy as np
 
-from . import synth_canvas, synth_frame
+from . import synth_canvas, synth_frame, synth_frame_right
 
 KITTI_W, KITTI_H = 1241, 376
 # R:configs/config.yaml:8-11 (fx, fy, cx, cy), held as float32 like the
 # reference's cv::Matx33f K (R:include/tracking.h:55)
 KITTI_FX, KITTI_FY, KITTI_CX, KITTI_CY = 718.8560, 718.8560, 607.1928, 185.2157
+# fx * baseline of the synthetic stereo rig. KITTI's is 386.1448 (P1[0,3]); a
+# quarter of it keeps the disparities of the 3-21 m depth field (5-32 px) in
+# the range an 11x11, maxLevel-3 LK recovers, as on KITTI's far field.
+STEREO_BF = 386.1448 / 4
 
 
 def intrinsics(w: int, h: int) -> np.ndarray:
@@ -72,6 +76,19 @@ class Scene:
     def frame(self, t: int) -> np.ndarray:
         return synth_frame(self.canvas, (self.margin, self.margin), self.R(t), self.K,
                            (self.seed << 20) + t + 1, self.noise, self.w, self.h)
+
+    def right(self, t: int, bf: float = STEREO_BF) -> np.ndarray:
+        """Right image of the rectified stereo pair at frame t (depth field surface)."""
+        return synth_frame_right(self.canvas, (self.margin, self.margin), self.R(t), self.K, bf, self.seed,
+                                 (self.seed << 20) + t + (1 << 19), self.noise, self.w, self.h)
+
+    def projections(self, bf: float = STEREO_BF):
+        """KITTI-style calib rows P0 (left) and P1 (right) as float32 3x4 (R:src/main.cpp:25-32)."""
+        P0 = np.zeros((3, 4), np.float32)
+        P0[:, :3] = self.K
+        P1 = P0.copy()
+        P1[0, 3] = -bf
+        return P0, P1
 
     def depth(self, cu: np.ndarray, cv: np.ndarray) -> np.ndarray:
         """Smooth positive depth field over canvas coordinates (metres)."""

@@ -57,6 +57,7 @@ def load():
             "svo_oracle_solve_pnp_ransac": (C.c_int, [_f64p, _f32p, C.c_int, _f64p, C.c_int, C.c_float,
                                                       C.c_double, _f64p, _f64p, _u8p, _i32p, _i32p]),
             "svo_oracle_get_subset": (C.c_int, [_u64p, C.c_int, C.c_int, _i32p]),
+            "svo_oracle_triangulate": (None, [_f32p, _f32p, _f32p, _f32p, C.c_int, _f32p, _f32p]),
         }
         for k, (r, a) in sig.items():
             f = getattr(L, k)
@@ -221,6 +222,20 @@ def solve_pnp_ransac(obj, img, K, iterations=100, reproj=8.0, confidence=0.999):
 
 def update_num_iters(p, ep, model_points, max_iters):
     return load().svo_oracle_ransac_update_num_iters(p, ep, model_points, max_iters)
+
+
+def triangulate(P1, P2, pts1, pts2):
+    """cv::triangulatePoints + convertPointsFromHomogeneous -> (xyzw (n,4), xyz (n,3)) float32."""
+    P1 = _c(P1, np.float32).reshape(12)
+    P2 = _c(P2, np.float32).reshape(12)
+    pts1 = _c(pts1, np.float32).reshape(-1, 2)
+    pts2 = _c(pts2, np.float32).reshape(-1, 2)
+    n = len(pts1)
+    h = np.empty((n, 4), np.float32)
+    x = np.empty((n, 3), np.float32)
+    load().svo_oracle_triangulate(_p(P1, _f32p), _p(P2, _f32p), _p(pts1, _f32p), _p(pts2, _f32p), n,
+                                  _p(h, _f32p), _p(x, _f32p))
+    return h, x
 
 
 def rng_sequence(n, state=0xFFFFFFFFFFFFFFFF):

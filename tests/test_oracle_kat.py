@@ -280,3 +280,27 @@ def test_oracle_matches_committed_golden():
     rc, rv, tv, inl, _ = O.solve_pnp_ransac(g["X"], g["t_next"], g["K"])
     assert np.array_equal(inl, g["pnp_inliers"])
     assert np.allclose(rv, g["pnp_rvec"], atol=1e-9) and np.allclose(tv, g["pnp_tvec"], atol=1e-9)
+
+
+# ------------------------------------------------------------------ triangulation (cv::triangulatePoints)
+def test_kat_triangulate_exact_projections():
+    """Points projected exactly by P0 = K[I|0] and P1 = K[I|(-b,0,0)] triangulate back."""
+    K = np.array([[718.856, 0, 607.1928], [0, 718.856, 185.2157], [0, 0, 1]])
+    P0 = np.zeros((3, 4)); P0[:, :3] = K
+    P1 = P0.copy(); P1[0, 3] = -386.1448
+    P0, P1 = P0.astype(np.float32), P1.astype(np.float32)
+    rng = np.random.default_rng(0)
+    X = np.c_[rng.uniform(-5, 5, 50), rng.uniform(-2, 2, 50), rng.uniform(4, 40, 50)]
+    Xh = np.c_[X, np.ones(50)]
+    p1 = (P0.astype(np.float64) @ Xh.T); p1 = (p1[:2] / p1[2]).T.astype(np.float32)
+    p2 = (P1.astype(np.float64) @ Xh.T); p2 = (p2[:2] / p2[2]).T.astype(np.float32)
+    h, x = O.triangulate(P0, P1, p1, p2)
+    assert np.all(h[:, 3] >= 0)
+    assert np.allclose(np.linalg.norm(h, axis=1), 1, atol=1e-6)
+    rel = np.abs(x - X).max(1) / X[:, 2]
+    assert rel.max() < 2e-4, rel.max()     # float pixel rounding only
+    # behind-camera point keeps z < 0 (the reference filters on z > 0)
+    Xb = np.array([[0.5, 0.2, -8.0, 1.0]])
+    q1 = P0.astype(np.float64) @ Xb.T; q2 = P1.astype(np.float64) @ Xb.T
+    _, xb = O.triangulate(P0, P1, (q1[:2] / q1[2]).T, (q2[:2] / q2[2]).T)
+    assert xb[0, 2] < 0 and abs(xb[0, 2] + 8.0) < 1e-3
