@@ -152,6 +152,28 @@ int svo_solve_pnp_ransac(svo_ctx* ctx, const double* obj_xyz, const float* img_x
 int svo_triangulate_points(svo_ctx* ctx, const float P1[12], const float P2[12], const float* pts1,
                            const float* pts2, int n, float* xyzw, float* xyz);
 
+/* ------------------------------------------------------------ reprojection cost (§8 a11)
+ * The north star's "ceres reprojection cost": Ceres is linked by the reference
+ * but never called (R:CMakeLists.txt:22,33), so there is no
+ * reference implementation; pinned by finite differences.
+ * P problems of up to max_n points each (obj: P*max_n*3 doubles, img:
+ * P*max_n*2 floats, counts: P or NULL = max_n each), poses: P x 12 doubles
+ * ([R|t], world -> camera, R row-major). Per point: r = pi(K (R X + t)) - u and
+ * J = dr/dxi (2x6 row-major) for T <- exp(xi^) T, xi = (rho, phi). normal:
+ * P x 28 = H (upper triangle of sum w J^T J, row-major, 21), g (sum w J^T r,
+ * 6), cost (sum of rho(|r|)); w, rho: Huber with delta > 0, else least
+ * squares. Points behind the camera contribute 0. Outputs may be NULL;
+ * results are deterministic (fixed reduction order). */
+int svo_reprojection_jacobians(svo_ctx* ctx, const double* obj_xyz, const float* img_xy, const int* counts,
+                               int n_problems, int max_n, const double* poses, const double K[9],
+                               double huber_delta, double* res, double* jac, double* normal);
+/* Host Levenberg-Marquardt over SE(3) (motion-only bundle adjustment), one
+ * batched GPU evaluation per iteration for all P problems. poses: in/out.
+ * costs (P, final cost) and iterations may be NULL. */
+int svo_refine_poses(svo_ctx* ctx, const double* obj_xyz, const float* img_xy, const int* counts, int n_problems,
+                     int max_n, const double K[9], double huber_delta, int max_iterations, double* poses,
+                     double* costs, int* iterations);
+
 /* ------------------------------------------------------------ batched front end
  * The reference's per-frame loop (Tracking::startStereo, R:src/tracking.cpp:232-276:
  * trackFrames -> calculatePose -> keyframe extractFeatures) for n_seq independent

@@ -86,6 +86,10 @@ _SIGS = [
     ("svo_solve_pnp_ransac", C.c_int, [_vp, _f64p, _f32p, C.c_int, _f64p, C.c_int, C.c_float,
                                        C.c_double, _f64p, _f64p, _i32p, _i32p]),
     ("svo_triangulate_points", C.c_int, [_vp, _f32p, _f32p, _f32p, _f32p, C.c_int, _f32p, _f32p]),
+    ("svo_reprojection_jacobians", C.c_int, [_vp, _f64p, _f32p, _i32p, C.c_int, C.c_int, _f64p, _f64p,
+                                             C.c_double, _f64p, _f64p, _f64p]),
+    ("svo_refine_poses", C.c_int, [_vp, _f64p, _f32p, _i32p, C.c_int, C.c_int, _f64p, C.c_double, C.c_int,
+                                   _f64p, _f64p, _i32p]),
     ("svo_frontend_create", C.c_int, [_vp, _vp, C.POINTER(_vp)]),
     ("svo_frontend_destroy", None, [_vp]),
     ("svo_frontend_set_frame", C.c_int, [_vp, C.c_int, C.c_int, _u8p, C.c_int, _f64p, C.c_int]),
@@ -303,6 +307,43 @@ class Context:
         self._check(lib().svo_triangulate_points(self.handle, _p(P1, _f32p), _p(P2, _f32p), _p(pts1, _f32p),
                                                  _p(pts2, _f32p), n, _p(h, _f32p), _p(x, _f32p)))
         return h, x
+
+    def reprojection_jacobians(self, obj, img_pts, poses, K, counts=None, huber_delta: float = 0.0):
+        """obj (P, n, 3) f64, img (P, n, 2) f32, poses (P, 12) -> (res (P,n,2), jac (P,n,2,6), normal (P,28))."""
+        obj = _c(obj, np.float64)
+        if obj.ndim == 2:
+            obj = obj[None]
+        P, n = obj.shape[0], obj.shape[1]
+        img_pts = _c(img_pts, np.float32).reshape(P, n, 2)
+        poses = _c(poses, np.float64).reshape(P, 12)
+        K = _c(K, np.float64).reshape(9)
+        cnt = _c(counts, np.int32).reshape(P) if counts is not None else None
+        res = np.empty((P, n, 2), np.float64)
+        jac = np.empty((P, n, 2, 6), np.float64)
+        ne = np.empty((P, 28), np.float64)
+        self._check(lib().svo_reprojection_jacobians(self.handle, _p(obj, _f64p), _p(img_pts, _f32p),
+                                                     _p(cnt, _i32p) if cnt is not None else None, P, n,
+                                                     _p(poses, _f64p), _p(K, _f64p), float(huber_delta),
+                                                     _p(res, _f64p), _p(jac, _f64p), _p(ne, _f64p)))
+        return res, jac, ne
+
+    def refine_poses(self, obj, img_pts, poses, K, counts=None, huber_delta: float = 0.0, max_iterations: int = 20):
+        """Motion-only LM over SE(3) -> (poses (P,12), costs (P,), iterations)."""
+        obj = _c(obj, np.float64)
+        if obj.ndim == 2:
+            obj = obj[None]
+        P, n = obj.shape[0], obj.shape[1]
+        img_pts = _c(img_pts, np.float32).reshape(P, n, 2)
+        poses = np.array(poses, np.float64).reshape(P, 12)
+        K = _c(K, np.float64).reshape(9)
+        cnt = _c(counts, np.int32).reshape(P) if counts is not None else None
+        costs = np.empty(P, np.float64)
+        it = C.c_int()
+        self._check(lib().svo_refine_poses(self.handle, _p(obj, _f64p), _p(img_pts, _f32p),
+                                           _p(cnt, _i32p) if cnt is not None else None, P, n, _p(K, _f64p),
+                                           float(huber_delta), int(max_iterations), _p(poses, _f64p),
+                                           _p(costs, _f64p), C.byref(it)))
+        return poses, costs, it.value
 
     def solve_pnp_ransac(self, obj, img_pts, K, iterations: int = 100, reproj_err: float = 8.0,
                          confidence: float = 0.999):

@@ -181,6 +181,10 @@ struct BucketBatch {
 };
 hipError_t launch_triangulate(const float* d_P, const float* d_p1, const float* d_p2, int n, float* d_xyzw,
                               float* d_xyz, hipStream_t st);
+size_t reproj_partial_doubles(int n_problems, int max_n);
+hipError_t launch_reproj(const double* d_obj, const float* d_img, const int* d_counts, int n_problems, int cap,
+                         int max_n, const double* d_poses, const double K[9], double delta, double* d_res,
+                         double* d_jac, double* d_partial, double* d_normal, hipStream_t st);
 size_t bucket_scratch_ints(int img_w, int img_h, int bucket, int per_bucket, int n);
 hipError_t launch_bucket(const BucketBatch& b, int nseq, int img_w, int img_h, int bucket, int per_bucket,
                          hipStream_t st);
