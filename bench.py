@@ -136,6 +136,7 @@ def main():
     ap.add_argument("--seq", type=int, default=64, help="independent sequences per GPU (batched launches)")
     ap.add_argument("--config", default="kitti", choices=sorted(CONFIGS))
     ap.add_argument("--threads", type=int, default=0, help="host RANSAC threads (0 = auto)")
+    ap.add_argument("--groups", type=int, default=0, help="pipeline slices of the batch (0 = auto)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-single", action="store_true")
@@ -152,7 +153,7 @@ def main():
     seeds = sequence_seeds(rank, Sq)
     scenes = [Scene(W, H, seed=sd) for sd in seeds]
     cfg = S.FrontendConfig(W, H, scenes[0].K, n_seq=Sq, n_frames=T, n_features=N, max_level=ML,
-                           host_threads=args.threads, timing=1)
+                           host_threads=args.threads, timing=1, groups=args.groups)
     fe = S.Frontend(ctx, cfg)
     for s, sc in enumerate(scenes):
         for t in range(T):
@@ -219,7 +220,8 @@ def main():
         "dtype": "u8/int32 fixed-point (LK sums exact int, solve f32), f64 PnP",
         "data": "synthetic (rendered KITTI-size frames, seeded; no dataset on the box)",
         "config": {"workload": label, "sequences_per_gpu": Sq, "global_batch": Sq * world,
-                   "features": N, "win": 21, "max_level": ML, "parallelism": f"{world} x independent sequences"},
+                   "features": N, "win": 21, "max_level": ML, "parallelism": f"{world} x independent sequences",
+                   "groups": args.groups},
         "lk_iters_per_s": round(lk_iters_total / dt_max, 1),
         "achieved_GBps_algorithmic": round(frames * frame_bytes(W, H, N, ML) / dt_max / 1e9, 2),
         "single_stream_fps": round(single, 2) if single else None,

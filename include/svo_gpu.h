@@ -206,6 +206,9 @@ typedef struct svo_frontend_config {
     double K[9];            /* camera matrix (float-rounded, as the Matx33f K) */
     int host_threads;       /* RANSAC host threads; 0 = auto */
     int timing;             /* 1 = record per-phase HIP events */
+    int groups;             /* pipeline groups: the batch is split into this many
+                               slices whose LK / RANSAC overlap (host RANSAC of one
+                               slice while the GPU tracks the next); 0 = auto */
 } svo_frontend_config;
 
 typedef struct svo_frontend_stats {
@@ -233,7 +236,7 @@ int svo_frontend_init(svo_frontend* fe, int t0);
 /* One step: frame t-1 -> t for every sequence (pyramid of t, temporal LK,
  * compaction, PnP RANSAC, outlier removal, masked FAST top-up). */
 int svo_frontend_step(svo_frontend* fe, int t, svo_frontend_stats* stats);
-int svo_frontend_pose(const svo_frontend* fe, int seq, double rvec[3], double tvec[3]);
+int svo_frontend_pose(svo_frontend* fe, int seq, double rvec[3], double tvec[3]);
 int svo_frontend_features(svo_frontend* fe, int seq, float* xy, int cap, int* n);
 /* Accumulated per-phase device time (ms) and launch counts since create/reset:
  * phases: 0 pyramid, 1 lk, 2 compact, 3 gather, 4 pnp_score, 5 mask, 6 fast,

@@ -374,7 +374,7 @@ class FrontendConfig(C.Structure):
         ("fast_threshold", C.c_int), ("fast_nonmax", C.c_int), ("mask_half", C.c_float),
         ("bucket_size", C.c_int), ("per_bucket", C.c_int), ("pnp_iterations", C.c_int),
         ("pnp_reproj", C.c_float), ("pnp_confidence", C.c_double), ("K", C.c_double * 9),
-        ("host_threads", C.c_int), ("timing", C.c_int),
+        ("host_threads", C.c_int), ("timing", C.c_int), ("groups", C.c_int),
     ]
 
     def __init__(self, width, height, K, n_seq=1, n_frames=2, n_features=2000, **kw):
@@ -382,7 +382,7 @@ class FrontendConfig(C.Structure):
         d = dict(max_level=3, win=21, lk_max_count=50, lk_epsilon=1e-3, min_eig=1e-4,
                  lk_flags=LK_GET_MIN_EIGENVALS, fast_threshold=20, fast_nonmax=1, mask_half=10.0,
                  bucket_size=0, per_bucket=0, pnp_iterations=100, pnp_reproj=8.0, pnp_confidence=0.999,
-                 host_threads=0, timing=0)
+                 host_threads=0, timing=0, groups=0)
         d.update(kw)
         self.width, self.height, self.n_seq, self.n_frames, self.n_features = width, height, n_seq, n_frames, n_features
         for k, v in d.items():

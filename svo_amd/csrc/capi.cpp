@@ -1,6 +1,7 @@
 // C ABI of libsvo_gpu.so: context, device images, and the host-pointer entry
 // points that mirror the reference's OpenCV calls (see include/svo_gpu.h for
 // the reference file:line each one replaces).
+#include <cstdlib>
 #include <cstdarg>
 #include <cstring>
 #include <vector>
@@ -133,6 +134,7 @@ int svo_image_create(svo_ctx* ctx, int w, int h, int max_levels, svo_image** out
         lw = (lw + 1) / 2;
         lh = (lh + 1) / 2;
     }
+    total += 256;  // over-read slack: the LK stager loads whole aligned dwords past a row's end
     if (hipMalloc(&im->base, total) != hipSuccess) {
         delete im;
         return set_error(ctx, SVO_ERR_HIP, "svo_image_create: hipMalloc(%zu) failed", total);
@@ -325,6 +327,9 @@ int svo_calc_optical_flow_pyr_lk(svo_ctx* ctx, const svo_image* prev, const svo_
     p.flags = flags;
     p.min_eig = (float)min_eig_threshold;
     p.want_err = err ? 1 : 0;
+    // test hook: SVO_LK_GENERIC=1 routes every window through the runtime-size kernel
+    const char* gen = std::getenv("SVO_LK_GENERIC");
+    p.generic = gen && gen[0] == '1' ? 1 : 0;
     // derivative pyramid of prev (calcSharrDeriv per level), then LK
     size_t doff[kMaxLevels];
     int dpitch[kMaxLevels];

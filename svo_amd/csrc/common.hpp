@@ -128,6 +128,7 @@ struct LKParams {
     int flags;
     float min_eig;
     int want_err;
+    int generic = 0;  // 1: always use the runtime-window kernel (tests compare both)
 };
 // Batched LK: blockIdx.y = sequence; sequence s owns points [s*cap, s*cap + n_s)
 // of every array, n_s = counts[s] (device) or n when counts is null.
@@ -185,6 +186,8 @@ size_t reproj_partial_doubles(int n_problems, int max_n);
 hipError_t launch_reproj(const double* d_obj, const float* d_img, const int* d_counts, int n_problems, int cap,
                          int max_n, const double* d_poses, const double K[9], double delta, double* d_res,
                          double* d_jac, double* d_partial, double* d_normal, hipStream_t st);
+hipError_t launch_suffstats(const float* obj, const float* img, const int* counts, int cap, const uint32_t* bits,
+                            int words_cap, int nseq, const double K[9], double* out, hipStream_t st);
 size_t bucket_scratch_ints(int img_w, int img_h, int bucket, int per_bucket, int n);
 hipError_t launch_bucket(const BucketBatch& b, int nseq, int img_w, int img_h, int bucket, int per_bucket,
                          hipStream_t st);

@@ -128,19 +128,28 @@ struct svo_frontend {
     long long* itsum;
     uint8_t *status, *mask;
     uint32_t *bits_all, *bits_best;
-    double *map, *hyps, *rot_d;
+    double *map, *hyps, *rot_d, *stats;
     // host mirrors (pinned)
     void* hmem = nullptr;
     int *h_nB, *h_nA, *h_cnt, *h_added;
     long long* h_itsum;
     float *h_xyB, *h_obj;
-    double* h_hyps;
+    double *h_hyps, *h_stats;
     uint32_t *h_bits, *h_best;
     std::vector<RansacSeq> rs;
     std::vector<double> pose;  // [s][6]
+    bool fits_pending = false;
+    int pyr_ready = -1;  // frame index whose pyramid + Scharr were built ahead
     Pool* pool = nullptr;
+    // pipeline: slices of the batch [g0[g], g0[g] + gn[g]) on their own streams
+    int G = 1;
+    std::vector<int> g0, gn;
+    std::vector<hipStream_t> gst;     // per slice (high priority)
+    hipStream_t st_fast = nullptr;    // mask + FAST + bucket (low priority)
+    // [0] pyramid done, [1] FAST done, [2 + 2g] LK done, [3 + 2g] D2H done, [2 + 2G + g] stats D2H done
+    std::vector<hipEvent_t> ev_sync;
     // timing
-    hipEvent_t ev[2 * kPhases * 4];
+    hipEvent_t ev[256];
     double phase_ms[kPhases] = {0};
     int64_t phase_n[kPhases] = {0};
     std::vector<std::pair<int, int>> pending;  // (phase, event pair index)
@@ -149,16 +158,16 @@ struct svo_frontend {
 
 namespace {
 
-void ph_begin(svo_frontend* fe, int ph, int* slot) {
+void ph_begin(svo_frontend* fe, int ph, hipStream_t st, int* slot) {
     *slot = -1;
     if (!fe->cfg.timing || fe->ev_used + 2 > (int)(sizeof(fe->ev) / sizeof(fe->ev[0]))) return;
     *slot = fe->ev_used;
     fe->ev_used += 2;
-    (void)hipEventRecord(fe->ev[*slot], fe->ctx->stream);
+    (void)hipEventRecord(fe->ev[*slot], st);
     fe->pending.push_back({ph, *slot});
 }
-void ph_end(svo_frontend* fe, int slot) {
-    if (slot >= 0) (void)hipEventRecord(fe->ev[slot + 1], fe->ctx->stream);
+void ph_end(svo_frontend* fe, hipStream_t st, int slot) {
+    if (slot >= 0) (void)hipEventRecord(fe->ev[slot + 1], st);
 }
 // after a stream sync: fold the recorded event pairs into the phase totals
 void ph_collect(svo_frontend* fe) {
@@ -181,50 +190,68 @@ T* carve(char*& p, size_t count) {
     return r;
 }
 
-int fe_fast_and_bucket(svo_frontend* fe, const PyrDesc* descs_cur, bool use_mask) {
+int fe_fast_and_bucket(svo_frontend* fe, const PyrDesc* descs_cur, bool use_mask, hipStream_t st) {
     svo_ctx* ctx = fe->ctx;
-    hipStream_t st = ctx->stream;
     int slot;
     FastDetBatch fb{descs_cur, use_mask ? fe->mask : nullptr, fe->fbits, fe->rowcnt, fe->rowoff,
                     (svo_keypoint*)fe->kps, fe->kn, fe->npx, (fe->W + 63) / 64, fe->KCAP};
-    ph_begin(fe, PH_FAST, &slot);
+    ph_begin(fe, PH_FAST, st, &slot);
     SVO_HIP(ctx, launch_fast_detect(fb, fe->S, fe->W, fe->H, fe->cfg.fast_threshold, fe->cfg.fast_nonmax, st));
-    ph_end(fe, slot);
+    ph_end(fe, st, slot);
     if (fe->cfg.bucket_size > 0) {
-        ph_begin(fe, PH_BUCKET, &slot);
+        ph_begin(fe, PH_BUCKET, st, &slot);
         BucketBatch bb{fe->kps, 3, fe->KCAP, fe->kn, 0, nullptr, fe->cand, nullptr, fe->BCAP, fe->bn, fe->scr,
                        fe->bscr};
         SVO_HIP(ctx, launch_bucket(bb, fe->S, fe->W, fe->H, fe->cfg.bucket_size, fe->cfg.per_bucket, st));
-        ph_end(fe, slot);
+        ph_end(fe, st, slot);
     }
     return SVO_OK;
 }
 
-int fe_append(svo_frontend* fe, int t) {
+// keyframe top-up of sequences [g0, g0 + n)
+int fe_append(svo_frontend* fe, int t, int g0, int n, hipStream_t st) {
     svo_ctx* ctx = fe->ctx;
     int slot;
     AppendBatch ab;
-    ab.n = fe->nA;
-    ab.xy = fe->xyA;
-    ab.mid = fe->midA;
+    ab.n = fe->nA + g0;
+    ab.xy = fe->xyA + 2 * (size_t)g0 * fe->CAP;
+    ab.mid = fe->midA + (size_t)g0 * fe->CAP;
     ab.cap = fe->CAP;
     ab.n_target = fe->cfg.n_features;
     const bool bucketed = fe->cfg.bucket_size > 0;
-    ab.cand = bucketed ? fe->cand : fe->kps;
+    ab.cand = bucketed ? fe->cand + 2 * (size_t)g0 * fe->BCAP : fe->kps + 3 * (size_t)g0 * fe->KCAP;
     ab.cand_elem = bucketed ? 2 : 3;
     ab.cand_cap = bucketed ? fe->BCAP : fe->KCAP;
-    ab.cand_n = bucketed ? fe->bn : fe->kn;
-    ab.map = fe->map;
-    ab.map_n = fe->map_n;
+    ab.cand_n = (bucketed ? fe->bn : fe->kn) + g0;
+    ab.map = fe->map + 3 * (size_t)g0 * fe->MAPCAP;
+    ab.map_n = fe->map_n + g0;
     ab.map_cap = fe->MAPCAP;
-    ab.rot = fe->rot_d + 9 * (size_t)(t % fe->T) * fe->S;
-    ab.depth_seed = fe->seed_d;
-    ab.added = fe->added;
+    ab.rot = fe->rot_d + 9 * ((size_t)(t % fe->T) * fe->S + g0);
+    ab.depth_seed = fe->seed_d + g0;
+    ab.added = fe->added + g0;
     std::memcpy(ab.K, fe->cfg.K, sizeof(ab.K));
-    ph_begin(fe, PH_APPEND, &slot);
-    SVO_HIP(ctx, launch_append(ab, fe->S, ctx->stream));
-    ph_end(fe, slot);
+    ph_begin(fe, PH_APPEND, st, &slot);
+    SVO_HIP(ctx, launch_append(ab, n, st));
+    ph_end(fe, st, slot);
     return SVO_OK;
+}
+
+// Final SQPnP-objective fits of the last step (from the GPU sufficient
+// statistics in h_stats): refine the reported poses only, so they are run
+// lazily -- at the next step while the GPU tracks, or when a pose is read.
+double fe_finish_fits(svo_frontend* fe) {
+    if (!fe->fits_pending) return 0.0;
+    auto t0 = std::chrono::steady_clock::now();
+    fe->pool->run(fe->S, [&](int s) {
+        RansacSeq& r = fe->rs[s];
+        r.fit(fe->cfg.K, fe->h_stats + 60 * (size_t)s);
+        if (r.ok) {
+            std::memcpy(&fe->pose[6 * (size_t)s], r.rvec, sizeof(r.rvec));
+            std::memcpy(&fe->pose[6 * (size_t)s + 3], r.tvec, sizeof(r.tvec));
+        }
+    });
+    fe->fits_pending = false;
+    return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
 }
 
 }  // namespace
@@ -296,6 +323,7 @@ int svo_frontend_create(svo_ctx* ctx, const svo_frontend_config* cfg, svo_fronte
         add(sizeof(double) * 3 * (size_t)S * fe->MAPCAP);
         add(sizeof(double) * 12 * (size_t)S * kRansacChunk);
         add(sizeof(double) * 9 * (size_t)S * fe->T);
+        add(sizeof(double) * 60 * (size_t)S);
         add(4096);
         bytes = (size_t)p;
     }
@@ -335,6 +363,7 @@ int svo_frontend_create(svo_ctx* ctx, const svo_frontend_config* cfg, svo_fronte
         fe->map = carve<double>(p, 3 * (size_t)S * fe->MAPCAP);
         fe->hyps = carve<double>(p, 12 * (size_t)S * kRansacChunk);
         fe->rot_d = carve<double>(p, 9 * (size_t)S * fe->T);
+        fe->stats = carve<double>(p, 60 * (size_t)S);
     }
     (void)hipMemsetAsync(fe->dmem, 0, bytes, ctx->stream);
     // host mirrors
@@ -349,6 +378,7 @@ int svo_frontend_create(svo_ctx* ctx, const svo_frontend_config* cfg, svo_fronte
         add(sizeof(int) * (size_t)S * kRansacChunk);
         add(sizeof(uint32_t) * (size_t)S * kRansacChunk * fe->WORDS);
         add(sizeof(uint32_t) * (size_t)S * fe->WORDS);
+        add(sizeof(double) * 60 * (size_t)S);
         add(4096);
         hbytes = (size_t)p;
     }
@@ -368,6 +398,7 @@ int svo_frontend_create(svo_ctx* ctx, const svo_frontend_config* cfg, svo_fronte
         fe->h_hyps = carve<double>(p, 12 * (size_t)S * kRansacChunk);
         fe->h_bits = carve<uint32_t>(p, (size_t)S * kRansacChunk * fe->WORDS);
         fe->h_best = carve<uint32_t>(p, (size_t)S * fe->WORDS);
+        fe->h_stats = carve<double>(p, 60 * (size_t)S);
         std::memset(fe->h_nA, 0, sizeof(int) * S);
     }
     // derivative pyramids of the last two frames of every sequence (ping-pong)
@@ -397,6 +428,34 @@ int svo_frontend_create(svo_ctx* ctx, const svo_frontend_config* cfg, svo_fronte
     nt = std::max(1, std::min({nt, S, 16}));
     fe->pool = new Pool(nt - 1);
     for (auto& e : fe->ev) (void)hipEventCreate(&e);
+    // pipeline slices: contiguous, near-equal sequence ranges
+    {
+        // slices > 1 only pay off when the host RANSAC outweighs the LK tail
+        // they hide; measured on MI355X one slice is fastest
+        int G = c.groups > 0 ? c.groups : 1;
+        G = std::max(1, std::min(G, S));
+        fe->G = G;
+        fe->g0.resize(G);
+        fe->gn.resize(G);
+        for (int g = 0; g < G; g++) {
+            fe->g0[g] = (int)((int64_t)S * g / G);
+            fe->gn[g] = (int)((int64_t)S * (g + 1) / G) - fe->g0[g];
+        }
+        int least = 0, greatest = 0;
+        (void)hipDeviceGetStreamPriorityRange(&least, &greatest);
+        fe->gst.assign(G, nullptr);
+        for (auto& g : fe->gst)
+            if (hipStreamCreateWithPriority(&g, hipStreamNonBlocking, greatest) != hipSuccess) {
+                svo_frontend_destroy(fe);
+                return set_error(ctx, SVO_ERR_HIP, "svo_frontend_create: stream");
+            }
+        if (hipStreamCreateWithPriority(&fe->st_fast, hipStreamNonBlocking, least) != hipSuccess) {
+            svo_frontend_destroy(fe);
+            return set_error(ctx, SVO_ERR_HIP, "svo_frontend_create: stream");
+        }
+        fe->ev_sync.assign(2 + 3 * G, nullptr);
+        for (auto& e : fe->ev_sync) (void)hipEventCreateWithFlags(&e, hipEventDisableTiming);
+    }
     SVO_HIP(ctx, hipMemcpyAsync(fe->d_desc, fe->desc_host.data(), sizeof(PyrDesc) * fe->desc_host.size(),
                                 hipMemcpyHostToDevice, ctx->stream));
     SVO_HIP(ctx, hipStreamSynchronize(ctx->stream));
@@ -415,6 +474,17 @@ void svo_frontend_destroy(svo_frontend* fe) {
     if (fe->hmem) (void)hipHostFree(fe->hmem);
     for (auto& e : fe->ev)
         if (e) (void)hipEventDestroy(e);
+    for (auto& g : fe->gst)
+        if (g) {
+            (void)hipStreamSynchronize(g);
+            (void)hipStreamDestroy(g);
+        }
+    if (fe->st_fast) {
+        (void)hipStreamSynchronize(fe->st_fast);
+        (void)hipStreamDestroy(fe->st_fast);
+    }
+    for (auto& e : fe->ev_sync)
+        if (e) (void)hipEventDestroy(e);
     delete fe;
 }
 
@@ -423,6 +493,7 @@ int svo_frontend_set_frame(svo_frontend* fe, int seq, int t, const uint8_t* gray
     if (!fe || seq < 0 || seq >= fe->S || t < 0 || t >= fe->T || !gray || stride < fe->W) return SVO_ERR_ARG;
     svo_ctx* ctx = fe->ctx;
     svo_image* im = fe->frames[(size_t)seq * fe->T + t];
+    if (fe->pyr_ready >= 0 && fe->pyr_ready % fe->T == t) fe->pyr_ready = -1;  // built from the old image
     SVO_HIP(ctx, hipMemcpy2DAsync(const_cast<uint8_t*>(im->desc.lv[0].data), im->desc.lv[0].pitch, gray, stride,
                                   fe->W, fe->H, hipMemcpyHostToDevice, ctx->stream));
     if (R) {
@@ -448,6 +519,8 @@ int svo_frontend_prebuild_pyramids(svo_frontend* fe) {
 
 int svo_frontend_init(svo_frontend* fe, int t0) {
     if (!fe || t0 < 0) return SVO_ERR_ARG;
+    fe->pyr_ready = -1;
+    fe->fits_pending = false;
     svo_ctx* ctx = fe->ctx;
     const int S = fe->S;
     const PyrDesc* dcur = fe->d_desc + (size_t)(t0 % fe->T) * S;
@@ -455,9 +528,9 @@ int svo_frontend_init(svo_frontend* fe, int t0) {
     SVO_HIP(ctx, launch_scharr(dcur, fe->d_der + (size_t)(t0 & 1) * S, S, fe->W, fe->H, fe->nlev, ctx->stream));
     SVO_HIP(ctx, hipMemsetAsync(fe->nA, 0, sizeof(int) * S, ctx->stream));
     SVO_HIP(ctx, hipMemsetAsync(fe->map_n, 0, sizeof(int) * S, ctx->stream));
-    int rc = fe_fast_and_bucket(fe, dcur, false);
+    int rc = fe_fast_and_bucket(fe, dcur, false, ctx->stream);
     if (rc) return rc;
-    rc = fe_append(fe, t0);
+    rc = fe_append(fe, t0, 0, S, ctx->stream);
     if (rc) return rc;
     SVO_HIP(ctx, hipMemcpyAsync(fe->h_nA, fe->nA, sizeof(int) * S, hipMemcpyDeviceToHost, ctx->stream));
     SVO_HIP(ctx, hipStreamSynchronize(ctx->stream));
@@ -469,22 +542,29 @@ int svo_frontend_init(svo_frontend* fe, int t0) {
 int svo_frontend_step(svo_frontend* fe, int t, svo_frontend_stats* stats) {
     if (!fe || t < 1) return SVO_ERR_ARG;
     svo_ctx* ctx = fe->ctx;
-    hipStream_t st = ctx->stream;
-    const int S = fe->S, CAP = fe->CAP;
+    hipStream_t st0 = ctx->stream;
+    const int S = fe->S, CAP = fe->CAP, G = fe->G;
     const svo_frontend_config& c = fe->cfg;
     const PyrDesc* dprev = fe->d_desc + (size_t)((t - 1) % fe->T) * S;
     const PyrDesc* dcur = fe->d_desc + (size_t)(t % fe->T) * S;
+    hipEvent_t ev_pyr = fe->ev_sync[0], ev_fast = fe->ev_sync[1];
     int slot;
     int max_prev = 0;
     for (int s = 0; s < S; s++) max_prev = std::max(max_prev, fe->h_nA[s]);
 
     // 1. pyramid of frame t and its Scharr derivative pyramid (used when frame
     //    t is the prev image of the next step; OpenCV recomputes it per call)
-    ph_begin(fe, PH_PYR, &slot);
-    SVO_HIP(ctx, launch_pyramid_batched(dcur, S, fe->W, fe->H, fe->nlev, st));
-    SVO_HIP(ctx, launch_scharr(dcur, fe->d_der + (size_t)(t & 1) * S, S, fe->W, fe->H, fe->nlev, st));
-    ph_end(fe, slot);
-    // 2. temporal LK (trackFrames)
+    if (fe->pyr_ready != t) {
+        ph_begin(fe, PH_PYR, st0, &slot);
+        SVO_HIP(ctx, launch_pyramid_batched(dcur, S, fe->W, fe->H, fe->nlev, st0));
+        SVO_HIP(ctx, launch_scharr(dcur, fe->d_der + (size_t)(t & 1) * S, S, fe->W, fe->H, fe->nlev, st0));
+        ph_end(fe, st0, slot);
+    }
+    SVO_HIP(ctx, hipEventRecord(ev_pyr, st0));
+
+    // 3. per slice: temporal LK (trackFrames), keep status == 1, gather map
+    //    points, D2H. Slice g's LK starts after slice g-1's so that slice 0's
+    //    results reach the host first and its RANSAC overlaps slice 1's LK.
     LKParams lp;
     lp.win_w = lp.win_h = c.win;
     lp.max_level = fe->ml;
@@ -494,123 +574,183 @@ int svo_frontend_step(svo_frontend* fe, int t, svo_frontend_stats* stats) {
     lp.flags = c.lk_flags & ~SVO_LK_USE_INITIAL_FLOW;
     lp.min_eig = (float)c.min_eig;
     lp.want_err = 0;
-    LKBatch lb{dprev, dcur, fe->d_der + (size_t)((t - 1) & 1) * S, fe->xyA, fe->next_xy, fe->status, nullptr,
-               fe->iters, fe->nA, 0, CAP};
-    ph_begin(fe, PH_LK, &slot);
-    SVO_HIP(ctx, launch_lk(lb, S, max_prev, lp, st));
-    ph_end(fe, slot);
-    // 3. mask around frame t-1's features (the reference masks with prevFrame's
-    //    features, R:src/tracking.cpp:77) + FAST/bucket on frame t: independent
-    //    of the pose, so the GPU runs them while the host solves RANSAC
-    ph_begin(fe, PH_MASK, &slot);
-    SVO_HIP(ctx, launch_mask_boxes(fe->W, fe->H, fe->xyA, fe->nA, max_prev, CAP, S, c.mask_half, fe->mask, st));
-    ph_end(fe, slot);
-    // 4. keep status == 1 (+ sum LK iterations), gather map points
-    CompactBatch cb{fe->nA, fe->status, nullptr, 0, fe->next_xy, fe->midA, fe->iters, fe->itsum,
-                    fe->xyB, fe->midB, fe->nB, CAP};
-    ph_begin(fe, PH_COMPACT, &slot);
-    SVO_HIP(ctx, launch_compact(cb, S, st));
-    ph_end(fe, slot);
-    ph_begin(fe, PH_GATHER, &slot);
-    SVO_HIP(ctx, launch_gather(fe->nB, fe->midB, fe->map, CAP, fe->MAPCAP, fe->obj, S, max_prev, st));
-    ph_end(fe, slot);
-    SVO_HIP(ctx, hipMemcpyAsync(fe->h_nB, fe->nB, sizeof(int) * S, hipMemcpyDeviceToHost, st));
-    SVO_HIP(ctx, hipMemcpyAsync(fe->h_itsum, fe->itsum, sizeof(long long) * S, hipMemcpyDeviceToHost, st));
-    SVO_HIP(ctx, hipMemcpyAsync(fe->h_xyB, fe->xyB, sizeof(float) * 2 * S * (size_t)CAP, hipMemcpyDeviceToHost, st));
-    SVO_HIP(ctx, hipMemcpyAsync(fe->h_obj, fe->obj, sizeof(float) * 3 * S * (size_t)CAP, hipMemcpyDeviceToHost, st));
-    hipEvent_t ready;
-    SVO_HIP(ctx, hipEventCreateWithFlags(&ready, hipEventDisableTiming));
-    SVO_HIP(ctx, hipEventRecord(ready, st));
-    int rc = fe_fast_and_bucket(fe, dcur, true);
+    for (int g = 0; g < G; g++) {
+        const int a = fe->g0[g], n = fe->gn[g];
+        hipStream_t sg = fe->gst[g];
+        int mp = 0;
+        for (int s = a; s < a + n; s++) mp = std::max(mp, fe->h_nA[s]);
+        SVO_HIP(ctx, hipStreamWaitEvent(sg, ev_pyr, 0));
+        if (g > 0) SVO_HIP(ctx, hipStreamWaitEvent(sg, fe->ev_sync[2 + 2 * (g - 1)], 0));
+        LKBatch lb{dprev + a, dcur + a, fe->d_der + (size_t)((t - 1) & 1) * S + a, fe->xyA + 2 * (size_t)a * CAP,
+                   fe->next_xy + 2 * (size_t)a * CAP, fe->status + (size_t)a * CAP, nullptr,
+                   fe->iters + (size_t)a * CAP, fe->nA + a, 0, CAP};
+        ph_begin(fe, PH_LK, sg, &slot);
+        SVO_HIP(ctx, launch_lk(lb, n, mp, lp, sg));
+        ph_end(fe, sg, slot);
+        SVO_HIP(ctx, hipEventRecord(fe->ev_sync[2 + 2 * g], sg));
+    }
+    // 3b'. build frame t+1's pyramid + Scharr ahead, once every LK of this step is
+    //      done (the Scharr ping-pong buffer it writes is the one LK reads): it
+    //      runs while the host solves RANSAC. Used if the next step is t+1.
+    fe->pyr_ready = -1;
+    {
+        const int tn = t + 1;
+        const PyrDesc* dnext = fe->d_desc + (size_t)(tn % fe->T) * S;
+        SVO_HIP(ctx, hipStreamWaitEvent(st0, fe->ev_sync[2 + 2 * (G - 1)], 0));
+        ph_begin(fe, PH_PYR, st0, &slot);
+        SVO_HIP(ctx, launch_pyramid_batched(dnext, S, fe->W, fe->H, fe->nlev, st0));
+        SVO_HIP(ctx, launch_scharr(dnext, fe->d_der + (size_t)(tn & 1) * S, S, fe->W, fe->H, fe->nlev, st0));
+        ph_end(fe, st0, slot);
+        fe->pyr_ready = tn;
+    }
+    // 3a. the previous step's final pose fits, deferred to here: the host does
+    //     them while the GPU tracks this frame (before this step's D2H copies
+    //     are queued: the fits read the previous frame's host mirrors)
+    double ms_fit = fe_finish_fits(fe);
+    for (int g = 0; g < G; g++) {
+        const int a = fe->g0[g], n = fe->gn[g];
+        hipStream_t sg = fe->gst[g];
+        int mp = 0;
+        for (int s = a; s < a + n; s++) mp = std::max(mp, fe->h_nA[s]);
+        CompactBatch cb{fe->nA + a, fe->status + (size_t)a * CAP, nullptr, 0, fe->next_xy + 2 * (size_t)a * CAP,
+                        fe->midA + (size_t)a * CAP, fe->iters + (size_t)a * CAP, fe->itsum + a,
+                        fe->xyB + 2 * (size_t)a * CAP, fe->midB + (size_t)a * CAP, fe->nB + a, CAP};
+        ph_begin(fe, PH_COMPACT, sg, &slot);
+        SVO_HIP(ctx, launch_compact(cb, n, sg));
+        ph_end(fe, sg, slot);
+        ph_begin(fe, PH_GATHER, sg, &slot);
+        SVO_HIP(ctx, launch_gather(fe->nB + a, fe->midB + (size_t)a * CAP, fe->map + 3 * (size_t)a * fe->MAPCAP, CAP,
+                                   fe->MAPCAP, fe->obj + 3 * (size_t)a * CAP, n, mp, sg));
+        ph_end(fe, sg, slot);
+        SVO_HIP(ctx, hipMemcpyAsync(fe->h_nB + a, fe->nB + a, sizeof(int) * n, hipMemcpyDeviceToHost, sg));
+        SVO_HIP(ctx, hipMemcpyAsync(fe->h_itsum + a, fe->itsum + a, sizeof(long long) * n, hipMemcpyDeviceToHost, sg));
+        SVO_HIP(ctx, hipMemcpyAsync(fe->h_xyB + 2 * (size_t)a * CAP, fe->xyB + 2 * (size_t)a * CAP,
+                                    sizeof(float) * 2 * n * (size_t)CAP, hipMemcpyDeviceToHost, sg));
+        SVO_HIP(ctx, hipMemcpyAsync(fe->h_obj + 3 * (size_t)a * CAP, fe->obj + 3 * (size_t)a * CAP,
+                                    sizeof(float) * 3 * n * (size_t)CAP, hipMemcpyDeviceToHost, sg));
+        SVO_HIP(ctx, hipEventRecord(fe->ev_sync[3 + 2 * g], sg));
+    }
+
+    // 3b. mask around frame t-1's features (the reference masks with prevFrame's
+    //     features, R:src/tracking.cpp:77) + FAST/bucket on frame t, whole batch,
+    //     on its own stream after the last LK: independent of the pose, it fills
+    //     the GPU while the host solves RANSAC (and does not slow LK down)
+    hipStream_t sf = fe->st_fast;
+    SVO_HIP(ctx, hipStreamWaitEvent(sf, fe->ev_sync[2 + 2 * (G - 1)], 0));
+    ph_begin(fe, PH_MASK, sf, &slot);
+    SVO_HIP(ctx, launch_mask_boxes(fe->W, fe->H, fe->xyA, fe->nA, max_prev, CAP, S, c.mask_half, fe->mask, sf));
+    ph_end(fe, sf, slot);
+    int rc = fe_fast_and_bucket(fe, dcur, true, sf);
     if (rc) return rc;
+    SVO_HIP(ctx, hipEventRecord(ev_fast, sf));
+
+
     using clk = std::chrono::steady_clock;
     auto ms_since = [](clk::time_point t0) {
         return std::chrono::duration<double, std::milli>(clk::now() - t0).count();
     };
-    double ms_hyp = 0, ms_fit = 0, ms_wait = 0;
-    auto tw = clk::now();
-    SVO_HIP(ctx, hipEventSynchronize(ready));
-    (void)hipEventDestroy(ready);
-    ms_wait += ms_since(tw);
-
-    // 5. calculatePose: RANSAC per sequence, hypotheses scored on the GPU
-    int max_b = 0;
-    for (int s = 0; s < S; s++) {
-        fe->rs[s].begin(fe->h_obj + 3 * (size_t)s * CAP, fe->h_xyB + 2 * (size_t)s * CAP, fe->h_nB[s],
-                        c.pnp_iterations);
-        max_b = std::max(max_b, fe->h_nB[s]);
-    }
+    double ms_hyp = 0, ms_wait = 0;
     const float thr = (float)((double)c.pnp_reproj * (double)c.pnp_reproj);
-    int64_t nhyp = 0;
-    for (;;) {
-        std::vector<int> ms(S, 0);
-        auto th = clk::now();
-        fe->pool->run(S, [&](int s) { ms[s] = fe->rs[s].gen_chunk(c.K); });
-        ms_hyp += ms_since(th);
-        int mmax = 0;
-        for (int s = 0; s < S; s++) mmax = std::max(mmax, ms[s]);
-        if (mmax == 0) break;
-        for (int s = 0; s < S; s++) {
-            double* dst = fe->h_hyps + 12 * (size_t)s * kRansacChunk;
-            std::memcpy(dst, fe->rs[s].hyp, sizeof(double) * 12 * ms[s]);
-            for (int j = ms[s]; j < mmax; j++) std::memset(dst + 12 * j, 0, sizeof(double) * 12);
-            nhyp += ms[s];
-        }
-        SVO_HIP(ctx, hipMemcpyAsync(fe->hyps, fe->h_hyps, sizeof(double) * 12 * S * kRansacChunk,
-                                    hipMemcpyHostToDevice, st));
-        PnpBatch pb{fe->obj, fe->xyB, fe->nB, 0, CAP, fe->hyps, kRansacChunk, nullptr, fe->bits_all, fe->WORDS,
-                    fe->cnt};
-        pb.m = mmax;  // rows beyond a sequence's own m are ignored by consume()
-        // hypotheses live at stride kRansacChunk: score with m = kRansacChunk rows
-        pb.m = kRansacChunk;
-        ph_begin(fe, PH_PNP, &slot);
-        SVO_HIP(ctx, launch_pnp_residuals(pb, S, max_b, c.K[0], c.K[4], c.K[2], c.K[5], thr, st));
-        ph_end(fe, slot);
-        SVO_HIP(ctx, hipMemcpyAsync(fe->h_cnt, fe->cnt, sizeof(int) * S * kRansacChunk, hipMemcpyDeviceToHost, st));
-        SVO_HIP(ctx, hipMemcpyAsync(fe->h_bits, fe->bits_all, sizeof(uint32_t) * S * kRansacChunk * fe->WORDS,
-                                    hipMemcpyDeviceToHost, st));
-        tw = clk::now();
-        SVO_HIP(ctx, hipStreamSynchronize(st));
+    int64_t nhyp = 0, inl = 0;
+    std::vector<int> ms(S, 0);
+
+    // 4. per slice, in order: calculatePose (RANSAC per sequence, hypotheses
+    //    scored on the GPU), drop outliers (R:src/tracking.cpp:218-229), top up
+    for (int g = 0; g < G; g++) {
+        const int a = fe->g0[g], n = fe->gn[g];
+        hipStream_t sg = fe->gst[g];
+        auto tw = clk::now();
+        SVO_HIP(ctx, hipEventSynchronize(fe->ev_sync[3 + 2 * g]));
         ms_wait += ms_since(tw);
-        fe->pool->run(S, [&](int s) {
-            if (ms[s] > 0)
-                fe->rs[s].consume(fe->h_cnt + (size_t)s * kRansacChunk,
-                                  fe->h_bits + (size_t)s * kRansacChunk * fe->WORDS, fe->WORDS, c.pnp_confidence);
-        });
-    }
-    auto tf = clk::now();
-    fe->pool->run(S, [&](int s) {
-        RansacSeq& r = fe->rs[s];
-        r.finish(c.K);
-        uint32_t* b = fe->h_best + (size_t)s * fe->WORDS;
-        std::memset(b, 0, sizeof(uint32_t) * fe->WORDS);
-        if (r.ok) {
-            for (int i : r.inliers) b[i >> 5] |= 1u << (i & 31);
-            std::memcpy(&fe->pose[6 * (size_t)s], r.rvec, sizeof(r.rvec));
-            std::memcpy(&fe->pose[6 * (size_t)s + 3], r.tvec, sizeof(r.tvec));
-        } else if (r.n < 4) {
-            // solvePnPRansac would throw (CV_Assert npoints >= 4); keep the frame's
-            // features untouched instead of aborting the batch
-            for (int i = 0; i < r.n; i++) b[i >> 5] |= 1u << (i & 31);
+        int max_b = 0;
+        for (int s = a; s < a + n; s++) {
+            fe->rs[s].begin(fe->h_obj + 3 * (size_t)s * CAP, fe->h_xyB + 2 * (size_t)s * CAP, fe->h_nB[s],
+                            c.pnp_iterations);
+            max_b = std::max(max_b, fe->h_nB[s]);
         }
-    });
-    ms_fit += ms_since(tf);
-    // 6. drop outliers (R:src/tracking.cpp:218-229), top up to n_features
-    SVO_HIP(ctx, hipMemcpyAsync(fe->bits_best, fe->h_best, sizeof(uint32_t) * S * fe->WORDS, hipMemcpyHostToDevice,
-                                st));
-    CompactBatch cb2{fe->nB, nullptr, fe->bits_best, fe->WORDS, fe->xyB, fe->midB, nullptr, nullptr,
-                     fe->xyA, fe->midA, fe->nA, CAP};
-    ph_begin(fe, PH_COMPACT, &slot);
-    SVO_HIP(ctx, launch_compact(cb2, S, st));
-    ph_end(fe, slot);
-    int64_t inl = 0;
-    for (int s = 0; s < S; s++) inl += fe->rs[s].ok ? (int64_t)fe->rs[s].inliers.size() : fe->rs[s].n;
-    rc = fe_append(fe, t);
-    if (rc) return rc;
-    SVO_HIP(ctx, hipMemcpyAsync(fe->h_nA, fe->nA, sizeof(int) * S, hipMemcpyDeviceToHost, st));
-    SVO_HIP(ctx, hipMemcpyAsync(fe->h_added, fe->added, sizeof(int) * S, hipMemcpyDeviceToHost, st));
-    tw = clk::now();
-    SVO_HIP(ctx, hipStreamSynchronize(st));
+        for (;;) {
+            auto th = clk::now();
+            fe->pool->run(n, [&](int i) { ms[a + i] = fe->rs[a + i].gen_chunk(c.K); });
+            ms_hyp += ms_since(th);
+            int mmax = 0;
+            for (int s = a; s < a + n; s++) mmax = std::max(mmax, ms[s]);
+            if (mmax == 0) break;
+            for (int s = a; s < a + n; s++) {
+                double* dst = fe->h_hyps + 12 * (size_t)s * kRansacChunk;
+                std::memcpy(dst, fe->rs[s].hyp, sizeof(double) * 12 * ms[s]);
+                for (int j = ms[s]; j < mmax; j++) std::memset(dst + 12 * j, 0, sizeof(double) * 12);
+                nhyp += ms[s];
+            }
+            SVO_HIP(ctx, hipMemcpyAsync(fe->hyps + 12 * (size_t)a * kRansacChunk, fe->h_hyps + 12 * (size_t)a * kRansacChunk,
+                                        sizeof(double) * 12 * n * kRansacChunk, hipMemcpyHostToDevice, sg));
+            // hypotheses live at stride kRansacChunk: score all kRansacChunk rows
+            // (rows beyond a sequence's own count are ignored by consume())
+            PnpBatch pb{fe->obj + 3 * (size_t)a * CAP, fe->xyB + 2 * (size_t)a * CAP, fe->nB + a, 0, CAP,
+                        fe->hyps + 12 * (size_t)a * kRansacChunk, kRansacChunk, nullptr,
+                        fe->bits_all + (size_t)a * kRansacChunk * fe->WORDS, fe->WORDS, fe->cnt + (size_t)a * kRansacChunk};
+            ph_begin(fe, PH_PNP, sg, &slot);
+            SVO_HIP(ctx, launch_pnp_residuals(pb, n, max_b, c.K[0], c.K[4], c.K[2], c.K[5], thr, sg));
+            ph_end(fe, sg, slot);
+            SVO_HIP(ctx, hipMemcpyAsync(fe->h_cnt + (size_t)a * kRansacChunk, fe->cnt + (size_t)a * kRansacChunk,
+                                        sizeof(int) * n * kRansacChunk, hipMemcpyDeviceToHost, sg));
+            SVO_HIP(ctx, hipMemcpyAsync(fe->h_bits + (size_t)a * kRansacChunk * fe->WORDS,
+                                        fe->bits_all + (size_t)a * kRansacChunk * fe->WORDS,
+                                        sizeof(uint32_t) * n * kRansacChunk * fe->WORDS, hipMemcpyDeviceToHost, sg));
+            tw = clk::now();
+            SVO_HIP(ctx, hipStreamSynchronize(sg));
+            ms_wait += ms_since(tw);
+            fe->pool->run(n, [&](int i) {
+                const int s = a + i;
+                if (ms[s] > 0)
+                    fe->rs[s].consume(fe->h_cnt + (size_t)s * kRansacChunk,
+                                      fe->h_bits + (size_t)s * kRansacChunk * fe->WORDS, fe->WORDS, c.pnp_confidence);
+            });
+        }
+        // the RANSAC inlier set is the output (R:src/tracking.cpp:218-229); the final
+        // SQPnP-objective fit only refines the pose, from statistics summed on the GPU
+        auto tf = clk::now();
+        fe->pool->run(n, [&](int i) {
+            const int s = a + i;
+            RansacSeq& r = fe->rs[s];
+            r.select(c.K);
+            uint32_t* b = fe->h_best + (size_t)s * fe->WORDS;
+            std::memset(b, 0, sizeof(uint32_t) * fe->WORDS);
+            if (r.ok) {
+                for (int k : r.inliers) b[k >> 5] |= 1u << (k & 31);
+            } else if (r.n < 4) {
+                // solvePnPRansac would throw (CV_Assert npoints >= 4); keep the frame's
+                // features untouched instead of aborting the batch
+                for (int k = 0; k < r.n; k++) b[k >> 5] |= 1u << (k & 31);
+            }
+        });
+        ms_fit += ms_since(tf);
+        for (int s = a; s < a + n; s++) inl += fe->rs[s].ok ? (int64_t)fe->rs[s].inliers.size() : fe->rs[s].n;
+        SVO_HIP(ctx, hipMemcpyAsync(fe->bits_best + (size_t)a * fe->WORDS, fe->h_best + (size_t)a * fe->WORDS,
+                                    sizeof(uint32_t) * n * fe->WORDS, hipMemcpyHostToDevice, sg));
+        SVO_HIP(ctx, launch_suffstats(fe->obj + 3 * (size_t)a * CAP, fe->xyB + 2 * (size_t)a * CAP, fe->nB + a, CAP,
+                                      fe->bits_best + (size_t)a * fe->WORDS, fe->WORDS, n, c.K,
+                                      fe->stats + 60 * (size_t)a, sg));
+        SVO_HIP(ctx, hipMemcpyAsync(fe->h_stats + 60 * (size_t)a, fe->stats + 60 * (size_t)a, sizeof(double) * 60 * n,
+                                    hipMemcpyDeviceToHost, sg));
+        SVO_HIP(ctx, hipEventRecord(fe->ev_sync[2 + 2 * G + g], sg));
+        // the mask (reads xyA) and FAST (writes kps) must be done before xyA is rewritten / kps read
+        SVO_HIP(ctx, hipStreamWaitEvent(sg, ev_fast, 0));
+        CompactBatch cb2{fe->nB + a, nullptr, fe->bits_best + (size_t)a * fe->WORDS, fe->WORDS,
+                         fe->xyB + 2 * (size_t)a * CAP, fe->midB + (size_t)a * CAP, nullptr, nullptr,
+                         fe->xyA + 2 * (size_t)a * CAP, fe->midA + (size_t)a * CAP, fe->nA + a, CAP};
+        ph_begin(fe, PH_COMPACT, sg, &slot);
+        SVO_HIP(ctx, launch_compact(cb2, n, sg));
+        ph_end(fe, sg, slot);
+        rc = fe_append(fe, t, a, n, sg);
+        if (rc) return rc;
+        SVO_HIP(ctx, hipMemcpyAsync(fe->h_nA + a, fe->nA + a, sizeof(int) * n, hipMemcpyDeviceToHost, sg));
+        SVO_HIP(ctx, hipMemcpyAsync(fe->h_added + a, fe->added + a, sizeof(int) * n, hipMemcpyDeviceToHost, sg));
+    }
+    fe->fits_pending = true;  // statistics land with the stream syncs below
+    auto tw = clk::now();
+    for (int g = 0; g < G; g++) SVO_HIP(ctx, hipStreamSynchronize(fe->gst[g]));
+    SVO_HIP(ctx, hipStreamSynchronize(sf));
+    SVO_HIP(ctx, hipStreamSynchronize(st0));
     ms_wait += ms_since(tw);
     ph_collect(fe);
     if (stats) {
@@ -630,8 +770,9 @@ int svo_frontend_step(svo_frontend* fe, int t, svo_frontend_stats* stats) {
     return SVO_OK;
 }
 
-int svo_frontend_pose(const svo_frontend* fe, int seq, double rvec[3], double tvec[3]) {
+int svo_frontend_pose(svo_frontend* fe, int seq, double rvec[3], double tvec[3]) {
     if (!fe || seq < 0 || seq >= fe->S) return SVO_ERR_ARG;
+    fe_finish_fits(fe);
     std::memcpy(rvec, &fe->pose[6 * (size_t)seq], sizeof(double) * 3);
     std::memcpy(tvec, &fe->pose[6 * (size_t)seq + 3], sizeof(double) * 3);
     return SVO_OK;

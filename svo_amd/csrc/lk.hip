@@ -28,6 +28,7 @@
 #include "common.hpp"
 
 #include <cfloat>
+#include <cstdlib>
 
 namespace svo {
 
@@ -388,6 +389,408 @@ __global__ __launch_bounds__(256) void lk_kernel(LKBatch B, LKDev p) {
     }
 }
 
+// ---------------------------------------------------------------------------
+// Specialised kernel for compile-time window sizes (the reference's 21x21 and
+// 11x11, plus 15x15 / 31x31). Same semantics and lane map as lk_kernel; the
+// differences are all instruction count:
+//  * staging loads whole aligned dwords (4 pixels) per lane and builds the 4
+//    pixel pairs with v_perm from its dword and the next lane's (ds_bpermute),
+//    one ds_write_b128 per lane: 1 VMEM instruction per 4 pairs instead of 8;
+//  * LDS strides are compile-time (ds_read2 with immediate offsets);
+//  * two window rows are processed per packed op: the J-I differences of a row
+//    pair are packed to int16x2 (v_perm + v_pk_sub_i16) and multiplied into the
+//    normal equations with one v_dot2_i32_i16 per sum (b1, b2, A11, A12, A22),
+//    replacing two quarter-rate v_mul_lo_u32 per pixel and sum.
+// All values fit int16 (|J - I| <= 8160, |Ix|, |Iy| <= 4080) and the per-lane
+// int32 sums cannot overflow (7 rows x 2 x 8160 x 4080 < 2^31), so the sums are
+// the same exact integers as before: bit-identical results.
+constexpr int ru4(int v) { return (v + 3) & ~3; }
+
+template <int WW, int WH>
+struct Shape {
+    static constexpr int G = 64 / WW;               // row groups of the strip map
+    static constexpr int RPG = (WH + G - 1) / G;     // rows per group
+    static constexpr bool FULL = G * RPG == WH;
+    static constexpr int NP = (RPG + 1) / 2;        // packed row pairs per lane
+    static constexpr int IPW = ru4(WW + 3), IPH = WH + 1;           // I pairs: entries x rows
+    static constexpr int JRW = ru4(WW + 2 * JM + 3), JRH = WH + 1 + 2 * JM;
+    static constexpr int IBYTES = IPW * IPH * 4, JBYTES = JRW * JRH * 4;
+    static constexpr int WAVE_BYTES = IBYTES + JBYTES;
+};
+
+__device__ __forceinline__ unsigned lo16x2(int lo, int hi) {  // (lo & 0xffff) | (hi << 16) in one v_perm
+    return __builtin_amdgcn_perm((unsigned)hi, (unsigned)lo, 0x05040100u);
+}
+template <int CTRL, int ROW_MASK, bool BC>
+__device__ __forceinline__ int dpp_add(int v) {
+    return v + __builtin_amdgcn_update_dpp(0, v, CTRL, ROW_MASK, 0xf, BC);
+}
+
+// Exact wave sums of two int32 values whose per-lane magnitude is below 2^31/8
+// (true for b1, b2, A11, A12, A22: <= RPG * 2 * 8160 * 4080): the first three
+// DPP steps (8-lane partial sums) run in int32, then each partial is split into
+// 16-bit halves for the last three steps, all four chains interleaved so that
+// no DPP read waits on the write before it (no s_nop padding).
+__device__ __forceinline__ void wave_sum_exact2(int x, int y, double& sx, double& sy) {
+    x = dpp_add<0xb1, 0xf, true>(x);
+    y = dpp_add<0xb1, 0xf, true>(y);
+    x = dpp_add<0x4e, 0xf, true>(x);
+    y = dpp_add<0x4e, 0xf, true>(y);
+    x = dpp_add<0x114, 0xf, true>(x);
+    y = dpp_add<0x114, 0xf, true>(y);
+    int xh = x >> 16, xl = x & 0xFFFF, yh = y >> 16, yl = y & 0xFFFF;
+    xh = dpp_add<0x118, 0xf, true>(xh);
+    xl = dpp_add<0x118, 0xf, true>(xl);
+    yh = dpp_add<0x118, 0xf, true>(yh);
+    yl = dpp_add<0x118, 0xf, true>(yl);
+    xh = dpp_add<0x142, 0xa, false>(xh);
+    xl = dpp_add<0x142, 0xa, false>(xl);
+    yh = dpp_add<0x142, 0xa, false>(yh);
+    yl = dpp_add<0x142, 0xa, false>(yl);
+    xh = dpp_add<0x143, 0xc, false>(xh);
+    xl = dpp_add<0x143, 0xc, false>(xl);
+    yh = dpp_add<0x143, 0xc, false>(yh);
+    yl = dpp_add<0x143, 0xc, false>(yl);
+    const long long tx = (long long)__builtin_amdgcn_readlane(xh, 63) * 65536 + __builtin_amdgcn_readlane(xl, 63);
+    const long long ty = (long long)__builtin_amdgcn_readlane(yh, 63) * 65536 + __builtin_amdgcn_readlane(yl, 63);
+    sx = (double)tx;
+    sy = (double)ty;
+}
+
+// v_dot2_i32_i16 in its VOP3P form with a register accumulator: the compiler
+// otherwise picks v_dot2c (accumulator = destination) plus a v_mov of the
+// rounding constant for every use.
+__device__ __forceinline__ int sdot2_r(unsigned a, unsigned b, int c) {
+    int d;
+    asm("v_dot2_i32_i16 %0, %1, %2, %3" : "=v"(d) : "v"(a), "v"(b), "v"(c));
+    return d;
+}
+__device__ __forceinline__ unsigned pk_sub16(unsigned a, unsigned b) {
+    return __builtin_bit_cast(unsigned, __builtin_bit_cast(s16x2, a) - __builtin_bit_cast(s16x2, b));
+}
+
+// Stage rows [0, H) x pair entries [0, W) of the region whose pixel origin is
+// (xa, y0), xa a multiple of 4: entry (r, e) = L(xa+e, y0+r) | L(xa+e+1, y0+r) << 16.
+// REFLECT_101 outside the image (slow path, border windows only).
+template <int W, int H>
+__device__ __forceinline__ void stage_aligned(unsigned* dst, const ImgLevel& L, int xa, int y0, int lane) {
+    constexpr int LPR = W / 4 + 1;   // lanes per row: W/4 dwords + the one holding the last pair's right pixel
+    constexpr int RPP = 64 / LPR;    // rows per pass
+    const int lr = lane / LPR, d = lane - lr * LPR;
+    gu8 src = (gu8)L.data;
+    const bool inside = xa >= 0 && y0 >= 0 && xa + W + 1 <= L.w && y0 + H <= L.h;
+    if (inside) {
+        // dword loads may run past the row end (never past the allocation: 256 B slack)
+        gu32 q = (gu32)(src + (size_t)(y0 + lr) * L.pitch + xa) + d;
+        const size_t step = (size_t)RPP * L.pitch / 4;
+#pragma unroll
+        for (int r = 0; r < H; r += RPP, q += step) {
+            const bool act = lr < RPP && r + lr < H;
+            const unsigned v = act ? q[0] : 0u;
+            const unsigned nv = (unsigned)__builtin_amdgcn_ds_bpermute((lane + 1) << 2, (int)v);
+            if (act && d < W / 4) {
+                uint4 o;
+                o.x = __builtin_amdgcn_perm(nv, v, 0x0c010c00u);
+                o.y = __builtin_amdgcn_perm(nv, v, 0x0c020c01u);
+                o.z = __builtin_amdgcn_perm(nv, v, 0x0c030c02u);
+                o.w = __builtin_amdgcn_perm(nv, v, 0x0c040c03u);
+                *reinterpret_cast<uint4*>(dst + (r + lr) * W + 4 * d) = o;
+            }
+        }
+    } else {
+        for (int k = lane; k < W * H; k += 64) {
+            const int r = k / W, e = k - r * W;
+            gu8 row = src + (size_t)refl101(y0 + r, L.h) * L.pitch;
+            dst[k] = (unsigned)row[refl101(xa + e, L.w)] | ((unsigned)row[refl101(xa + e + 1, L.w)] << 16);
+        }
+    }
+}
+
+template <int WW, int WH, int MINW>
+__global__ __launch_bounds__(256, MINW) void lk_fast_kernel(LKBatch B, LKDev p) {
+    using S = Shape<WW, WH>;
+    constexpr int RPG = S::RPG, NP = S::NP;
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    const int lane = threadIdx.x & 63;
+    const int wid = threadIdx.x >> 6;
+    const int seq = blockIdx.y;
+    const int n = B.counts ? B.counts[seq] : B.n;
+    const int pt = blockIdx.x * 4 + wid;
+    if (pt >= n) return;
+    const size_t base = (size_t)seq * B.cap;
+    const float* __restrict__ prev_xy = B.prev_xy + 2 * base;
+    float* __restrict__ next_xy = B.next_xy + 2 * base;
+    const PyrDesc& prev = B.prev[seq];
+    const PyrDesc& next = B.next[seq];
+    const DerivDesc& dprev = B.dprev[seq];
+    unsigned* ipair = reinterpret_cast<unsigned*>(lds + wid * S::WAVE_BYTES);
+    unsigned* jreg = reinterpret_cast<unsigned*>(lds + wid * S::WAVE_BYTES + S::IBYTES);
+
+    const int sc = lane % WW;
+    const int sg = lane / WW;
+    const bool strip = sg < S::G;
+    // lanes outside the strip map (and rows past the window) run the same code on
+    // in-range addresses; their derivatives are zeroed, so they add nothing
+    const int r0 = (strip ? sg : 0) * RPG;
+    const int rnd_i = 1 << (W_BITS - 6), rnd_d = 1 << (W_BITS - 1);
+
+    constexpr float halfWx = (WW - 1) * 0.5f, halfWy = (WH - 1) * 0.5f;
+    const float px = uni_f(prev_xy[2 * pt]), py = uni_f(prev_xy[2 * pt + 1]);
+    float nx = 0.f, ny = 0.f;
+    if (p.flags & SVO_LK_USE_INITIAL_FLOW) {
+        nx = uni_f(next_xy[2 * pt]);
+        ny = uni_f(next_xy[2 * pt + 1]);
+    }
+    int st = 1;
+    float errv = 0.f;
+    int itcount = 0;
+    const int max_level = p.max_level;
+
+    for (int level = max_level; level >= 0; level--) {
+        const ImgLevel I = prev.lv[level];
+        const ImgLevel J = next.lv[level];
+        const float lscale = (float)(1. / (1 << level));
+        float prevx = px * lscale, prevy = py * lscale;
+        float nextx, nexty;
+        if (level == max_level) {
+            if (p.flags & SVO_LK_USE_INITIAL_FLOW) {
+                nextx = nx * lscale;
+                nexty = ny * lscale;
+            } else {
+                nextx = prevx;
+                nexty = prevy;
+            }
+        } else {
+            nextx = nx * 2.f;
+            nexty = ny * 2.f;
+        }
+        nx = nextx;
+        ny = nexty;
+        prevx -= halfWx;
+        prevy -= halfWy;
+        const int ipx = uni_i(ufloor(prevx)), ipy = uni_i(ufloor(prevy));
+        if (ipx < -WW || ipx >= I.w || ipy < -WH || ipy >= I.h) {
+            if (level == 0) {
+                st = 0;
+                errv = 0.f;
+            }
+            continue;
+        }
+        float a = prevx - ipx, b = prevy - ipy;
+        const int iw00 = uround((1.f - a) * (1.f - b) * (1 << W_BITS));
+        const int iw01 = uround(a * (1.f - b) * (1 << W_BITS));
+        const int iw10 = uround((1.f - a) * b * (1 << W_BITS));
+        const int iw11 = (1 << W_BITS) - iw00 - iw01 - iw10;
+        const unsigned IW0 = pack16(iw00, iw01), IW1 = pack16(iw10, iw11);
+
+        const int ixa = ipx & ~3;
+        int jx0 = uni_i(ufloor(nextx - halfWx)) - JM, jy0 = uni_i(ufloor(nexty - halfWy)) - JM;
+        int jxa = jx0 & ~3;
+        stage_aligned<S::IPW, S::IPH>(ipair, I, ixa, ipy, lane);
+        stage_aligned<S::JRW, S::JRH>(jreg, J, jxa, jy0, lane);
+        uint32_t dv[RPG + 1][2];
+        {
+            const int dpitch = dprev.pitch[level];
+            gu32 dsrc = (gu32)dprev.data[level];
+            const bool full_in = ipx >= 0 && ipy >= 0 && ipx + WW < I.w && ipy + WH < I.h;
+            const int X = ipx + sc;
+            if (full_in) {
+                gu32 q = dsrc + (size_t)(ipy + r0) * dpitch + X;
+#pragma unroll
+                for (int k = 0; k <= RPG; k++) {
+                    const int kk = (S::FULL || r0 + k <= WH) ? k : 0;  // stay inside the window
+                    dv[k][0] = q[(size_t)kk * dpitch];
+                    dv[k][1] = q[(size_t)kk * dpitch + 1];
+                }
+            } else {
+                const bool c0 = X >= 0 && X < I.w, c1 = X + 1 >= 0 && X + 1 < I.w;
+#pragma unroll
+                for (int k = 0; k <= RPG; k++) {
+                    dv[k][0] = dv[k][1] = 0;
+                    const int Y = ipy + r0 + k;
+                    if ((S::FULL || r0 + k <= WH) && Y >= 0 && Y < I.h) {
+                        gu32 q = dsrc + (size_t)Y * dpitch + X;
+                        if (c0) dv[k][0] = q[0];
+                        if (c1) dv[k][1] = q[1];
+                    }
+                }
+            }
+        }
+        wave_lds_sync();
+
+        // ---- I (x32), Ix, Iy at the lane's RPG window pixels, packed by row pairs ----
+        unsigned I2[NP], GX2[NP], GY2[NP];
+        int a11 = 0, a12 = 0, a22 = 0;
+        {
+            const unsigned* ip = ipair + r0 * S::IPW + (ipx - ixa) + sc;
+            int iv[2 * NP], gx[2 * NP], gy[2 * NP];
+#pragma unroll
+            for (int j = 0; j < 2 * NP; j++) iv[j] = gx[j] = gy[j] = 0;
+            unsigned P0 = ip[0];
+#pragma unroll
+            for (int j = 0; j < RPG; j++) {
+                const bool valid = strip && (S::FULL || r0 + j < WH);
+                const unsigned P1 = ip[(S::FULL || r0 + j < WH ? j + 1 : 0) * S::IPW];
+                iv[j] = sdot2(P0, IW0, sdot2_r(P1, IW1, rnd_i)) >> (W_BITS - 5);
+                P0 = P1;
+                const unsigned X0 = __builtin_amdgcn_perm(dv[j][1], dv[j][0], 0x05040100u);
+                const unsigned X1 = __builtin_amdgcn_perm(dv[j + 1][1], dv[j + 1][0], 0x05040100u);
+                const unsigned Y0 = __builtin_amdgcn_perm(dv[j][1], dv[j][0], 0x07060302u);
+                const unsigned Y1 = __builtin_amdgcn_perm(dv[j + 1][1], dv[j + 1][0], 0x07060302u);
+                gx[j] = valid ? sdot2(X0, IW0, sdot2_r(X1, IW1, rnd_d)) >> W_BITS : 0;
+                gy[j] = valid ? sdot2(Y0, IW0, sdot2_r(Y1, IW1, rnd_d)) >> W_BITS : 0;
+            }
+#pragma unroll
+            for (int m = 0; m < NP; m++) {
+                I2[m] = lo16x2(iv[2 * m], iv[2 * m + 1]);
+                GX2[m] = lo16x2(gx[2 * m], gx[2 * m + 1]);
+                GY2[m] = lo16x2(gy[2 * m], gy[2 * m + 1]);
+                a11 = sdot2(GX2[m], GX2[m], a11);
+                a12 = sdot2(GX2[m], GY2[m], a12);
+                a22 = sdot2(GY2[m], GY2[m], a22);
+            }
+        }
+        double s11, s12, s22, s_unused;
+        wave_sum_exact2(a11, a12, s11, s12);
+        wave_sum_exact2(a22, 0, s22, s_unused);
+        const float A11 = (float)s11 * FLT_SCALE;
+        const float A12 = (float)s12 * FLT_SCALE;
+        const float A22 = (float)s22 * FLT_SCALE;
+
+        float D = A11 * A22 - A12 * A12;
+        float minEig = (A22 + A11 - sqrtf((A11 - A22) * (A11 - A22) + 4.f * A12 * A12)) / (float)(2 * WW * WH);
+        if (p.want_err && (p.flags & SVO_LK_GET_MIN_EIGENVALS)) errv = minEig;
+        if (minEig < p.min_eig || D < FLT_EPSILON) {
+            if (level == 0) st = 0;
+            wave_lds_sync();
+            continue;
+        }
+        D = 1.f / D;
+
+        nextx -= halfWx;
+        nexty -= halfWy;
+        float pdx = 0.f, pdy = 0.f;
+        for (int j = 0; j < p.max_count; j++) {
+            const int inx = uni_i(ufloor(nextx)), iny = uni_i(ufloor(nexty));
+            if (inx < -WW || inx >= J.w || iny < -WH || iny >= J.h) {
+                if (level == 0) st = 0;
+                break;
+            }
+            itcount++;
+            if (inx < jx0 || inx > jx0 + 2 * JM || iny < jy0 || iny > jy0 + 2 * JM) {
+                jx0 = inx - JM;
+                jy0 = iny - JM;
+                jxa = jx0 & ~3;
+                wave_lds_sync();
+                stage_aligned<S::JRW, S::JRH>(jreg, J, jxa, jy0, lane);
+                wave_lds_sync();
+            }
+            a = nextx - inx;
+            b = nexty - iny;
+            const int w00 = uround((1.f - a) * (1.f - b) * (1 << W_BITS));
+            const int w01 = uround(a * (1.f - b) * (1 << W_BITS));
+            const int w10 = uround((1.f - a) * b * (1 << W_BITS));
+            const int w11 = (1 << W_BITS) - w00 - w01 - w10;
+            const unsigned W0 = pack16(w00, w01), W1 = pack16(w10, w11);
+            int b1 = 0, b2 = 0;
+            {
+                const unsigned* jp = jreg + (iny - jy0 + r0) * S::JRW + (inx - jxa + sc);
+                unsigned q[RPG + 1];
+#pragma unroll
+                for (int k = 0; k <= RPG; k++) q[k] = jp[k * S::JRW];
+                int jv[2 * NP];
+#pragma unroll
+                for (int k = 0; k < 2 * NP; k++)
+                    jv[k] = k < RPG ? sdot2(q[k], W0, sdot2_r(q[k + 1], W1, rnd_i)) >> (W_BITS - 5) : 0;
+#pragma unroll
+                for (int m = 0; m < NP; m++) {
+                    const unsigned d2 = pk_sub16(lo16x2(jv[2 * m], jv[2 * m + 1]), I2[m]);
+                    b1 = sdot2(d2, GX2[m], b1);
+                    b2 = sdot2(d2, GY2[m], b2);
+                }
+            }
+            double sb1, sb2;
+            wave_sum_exact2(b1, b2, sb1, sb2);
+            const float fb1 = (float)sb1 * FLT_SCALE;
+            const float fb2 = (float)sb2 * FLT_SCALE;
+            const float dx = (A12 * fb2 - A22 * fb1) * D;
+            const float dy = (A12 * fb1 - A11 * fb2) * D;
+            nextx += dx;
+            nexty += dy;
+            nx = nextx + halfWx;
+            ny = nexty + halfWy;
+            if ((double)dx * dx + (double)dy * dy <= p.eps2) break;
+            if (j > 0 && (double)fabsf(dx + pdx) < 0.01 && (double)fabsf(dy + pdy) < 0.01) {
+                nx -= dx * 0.5f;
+                ny -= dy * 0.5f;
+                break;
+            }
+            pdx = dx;
+            pdy = dy;
+        }
+
+        if (st && p.want_err && level == 0 && !(p.flags & SVO_LK_GET_MIN_EIGENVALS)) {
+            const float npx = nx - halfWx, npy = ny - halfWy;
+            const int ix0 = uni_i(ufloor(npx)), iy0 = uni_i(ufloor(npy));
+            if (ix0 < -WW || ix0 >= J.w || iy0 < -WH || iy0 >= J.h) {
+                st = 0;
+                continue;
+            }
+            if (ix0 < jx0 || ix0 > jx0 + 2 * JM || iy0 < jy0 || iy0 > jy0 + 2 * JM) {
+                jx0 = ix0 - JM;
+                jy0 = iy0 - JM;
+                jxa = jx0 & ~3;
+                wave_lds_sync();
+                stage_aligned<S::JRW, S::JRH>(jreg, J, jxa, jy0, lane);
+                wave_lds_sync();
+            }
+            float aa = npx - ix0, bb = npy - iy0;
+            const int w00 = uround((1.f - aa) * (1.f - bb) * (1 << W_BITS));
+            const int w01 = uround(aa * (1.f - bb) * (1 << W_BITS));
+            const int w10 = uround((1.f - aa) * bb * (1 << W_BITS));
+            const int w11 = (1 << W_BITS) - w00 - w01 - w10;
+            const unsigned W0 = pack16(w00, w01), W1 = pack16(w10, w11);
+            int sad = 0;
+            {
+                const unsigned* jp = jreg + (iy0 - jy0 + r0) * S::JRW + (ix0 - jxa + sc);
+#pragma unroll
+                for (int k = 0; k < RPG; k++) {
+                    const int jv = sdot2(jp[k * S::JRW], W0, sdot2_r(jp[(k + 1) * S::JRW], W1, rnd_i)) >>
+                                   (W_BITS - 5);
+                    const unsigned pr = I2[k >> 1];
+                    const int iv = (k & 1) ? ((int)pr >> 16) : (int)(short)(pr & 0xFFFFu);
+                    const int diff = jv - iv;
+                    if (strip && (S::FULL || r0 + k < WH)) sad += diff < 0 ? -diff : diff;
+                }
+            }
+            errv = (float)wave_sum_exact(sad) * 1.f / (float)(32 * WW * WH);
+        }
+        wave_lds_sync();
+    }
+    if (lane == 0) {
+        next_xy[2 * pt] = nx;
+        next_xy[2 * pt + 1] = ny;
+        B.status[base + pt] = (uint8_t)st;
+        if (B.err) B.err[base + pt] = errv;
+        if (B.iters) B.iters[base + pt] = itcount;
+    }
+}
+
+template <int WW, int WH>
+hipError_t launch_fast(const LKBatch& b, int nseq, int max_n, const LKDev& d, hipStream_t st) {
+    dim3 grid((max_n + 3) / 4, nseq);
+    constexpr int lds_bytes = 4 * Shape<WW, WH>::WAVE_BYTES;
+    const char* v = std::getenv("SVO_LK_MINW");
+    const int minw = v ? std::atoi(v) : 1;
+    if (minw >= 8)
+        hipLaunchKernelGGL((lk_fast_kernel<WW, WH, 8>), grid, dim3(256), lds_bytes, st, b, d);
+    else if (minw >= 2)
+        hipLaunchKernelGGL((lk_fast_kernel<WW, WH, 2>), grid, dim3(256), lds_bytes, st, b, d);
+    else
+        hipLaunchKernelGGL((lk_fast_kernel<WW, WH, 1>), grid, dim3(256), lds_bytes, st, b, d);
+    return hipGetLastError();
+}
+
 template <int RPG>
 hipError_t launch_rpg(const LKBatch& b, int nseq, int max_n, const LKDev& d, hipStream_t st) {
     dim3 grid((max_n + 3) / 4, nseq);
@@ -426,6 +829,12 @@ hipError_t launch_lk(const LKBatch& b, int nseq, int max_n, const LKParams& lp, 
     d.flags = lp.flags;
     d.want_err = lp.want_err;
     d.min_eig = lp.min_eig;
+    if (!lp.generic) {
+        if (lp.win_w == 21 && lp.win_h == 21) return launch_fast<21, 21>(b, nseq, max_n, d, st);
+        if (lp.win_w == 11 && lp.win_h == 11) return launch_fast<11, 11>(b, nseq, max_n, d, st);
+        if (lp.win_w == 15 && lp.win_h == 15) return launch_fast<15, 15>(b, nseq, max_n, d, st);
+        if (lp.win_w == 31 && lp.win_h == 31) return launch_fast<31, 31>(b, nseq, max_n, d, st);
+    }
 #define SVO_LK_CASE(R) \
     case R: return launch_rpg<R>(b, nseq, max_n, d, st);
     switch (rpg) {

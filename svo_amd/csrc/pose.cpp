@@ -62,7 +62,7 @@ class EPnP {
                 for (int q = 0; q < 12; q++) MtM[p * 12 + q] += r1[p] * r1[q] + r2[p] * r2[q];
         }
         double ev[12], ut[144];
-        la::sym_eig(MtM, 12, ev, ut);
+        la::sym_eig_ql(MtM, 12, ev, ut);
         double L[60], rho[6];
         make_L(ut, L);
         const int pairs[6][2] = {{0, 1}, {0, 2}, {0, 3}, {1, 2}, {1, 3}, {2, 3}};
@@ -340,15 +340,18 @@ struct SqpnpCost {
 // B_i vec(R) = R p_i, P = -Q^-1 S: expanded through the sufficient statistics
 // Q = sum A_i, S = sum A_i B_i, M = sum B_i^T A_i B_i as Omega = M - S^T Q^-1 S
 // (one pass, ~130 flops per point).
-void sqpnp_cost(const std::vector<double>& pw, const std::vector<double>& q, SqpnpCost& c) {
-    const int n = (int)q.size() / 2;
-    static const int IDX[3][3] = {{0, 1, 2}, {1, 3, 4}, {2, 4, 5}};  // unique entries of a sym 3x3
+}  // namespace
+
+// The 60 sufficient statistics of one point set: Q = sum A_i (6 unique),
+// T[u][j] = sum A_i,u p_j (18), U[u][v] = sum A_i,u (p p^T)_v (36); A_i as
+// symmetric 6-vectors. Host twin of pnp.hip's suffstats kernel.
+void sqpnp_sums(const double* pw, const double* q, int n, double* sums) {
     double Qs[6] = {0}, T[6][3] = {{0}}, U[6][6] = {{0}};
     for (int i = 0; i < n; i++) {
         const double x = q[2 * i], y = q[2 * i + 1];
         const double in = 1.0 / (x * x + y * y + 1.0);
         const double As[6] = {1.0 - x * x * in, -x * y * in, -x * in, 1.0 - y * y * in, -y * in, 1.0 - in};
-        const double* p = &pw[3 * (size_t)i];
+        const double* p = pw + 3 * (size_t)i;
         const double pp[6] = {p[0] * p[0], p[0] * p[1], p[0] * p[2], p[1] * p[1], p[1] * p[2], p[2] * p[2]};
         for (int u = 0; u < 6; u++) {
             Qs[u] += As[u];
@@ -358,12 +361,27 @@ void sqpnp_cost(const std::vector<double>& pw, const std::vector<double>& q, Sqp
             for (int v = 0; v < 6; v++) U[u][v] += As[u] * pp[v];
         }
     }
+    std::memcpy(sums, Qs, sizeof(Qs));
+    std::memcpy(sums + 6, T, sizeof(T));
+    std::memcpy(sums + 24, U, sizeof(U));
+}
+
+namespace {
+
+// Omega = sum_i (B_i + P)^T A_i (B_i + P) with A_i = I - v v^T / v^T v,
+// B_i vec(R) = R p_i, P = -Q^-1 S, assembled from the sufficient statistics
+// as Omega = M - S^T Q^-1 S.
+void sqpnp_assemble(const double* sums, SqpnpCost& c) {
+    static const int IDX[3][3] = {{0, 1, 2}, {1, 3, 4}, {2, 4, 5}};  // unique entries of a sym 3x3
+    const double* Qs = sums;
+    auto T = [&](int u, int j) { return sums[6 + 3 * u + j]; };
+    auto U = [&](int u, int v) { return sums[24 + 6 * u + v]; };
     double Q[9], S[27], Qi[9];
     for (int a = 0; a < 3; a++)
         for (int b = 0; b < 3; b++) Q[3 * a + b] = Qs[IDX[a][b]];
     for (int a = 0; a < 3; a++)
         for (int r = 0; r < 3; r++)
-            for (int j = 0; j < 3; j++) S[9 * a + 3 * r + j] = T[IDX[a][r]][j];
+            for (int j = 0; j < 3; j++) S[9 * a + 3 * r + j] = T(IDX[a][r], j);
     la::pinv3(Q, Qi);
     for (int a = 0; a < 3; a++)
         for (int col = 0; col < 9; col++)
@@ -373,7 +391,7 @@ void sqpnp_cost(const std::vector<double>& pw, const std::vector<double>& q, Sqp
             for (int s2 = 0; s2 < 3; s2++)
                 for (int k = 0; k < 3; k++) {
                     // M[(r,j),(s,k)] = sum A_rs p_j p_k ; minus (S^T Qi S) = + S^T P
-                    const double m = U[IDX[r][s2]][IDX[j][k]];
+                    const double m = U(IDX[r][s2], IDX[j][k]);
                     const int R = 3 * r + j, Cc = 3 * s2 + k;
                     double stp = S[R] * c.P[Cc] + S[9 + R] * c.P[9 + Cc] + S[18 + R] * c.P[18 + Cc];
                     c.Om[9 * R + Cc] = m + stp;
@@ -433,23 +451,17 @@ double refine_so3(const double* Om, double* R) {
     return quad(Om, R);
 }
 
-void final_fit(const float* obj, const float* img, const std::vector<int>& inl, const double K[9],
-               const double R0[9], double R[9], double t[3]) {
+// Minimiser of r^T Omega r over SO(3): Gauss-Newton from the RANSAC rotation
+// and from the nearest rotations of Omega's two smallest eigenvectors (both
+// signs); the lowest-cost start whose solution puts at least half the inliers
+// in front of the camera wins (SQPnP's cheirality test).
+void fit_from_cost(const SqpnpCost& c, const float* obj, const std::vector<int>& inl, const double R0[9],
+                   double R[9], double t[3]) {
     const int n = (int)inl.size();
-    std::vector<double> pw(3 * (size_t)n), q(2 * (size_t)n);
-    const double ifx = 1. / K[0], ify = 1. / K[4];
-    for (int k = 0; k < n; k++) {
-        const int i = inl[k];
-        for (int j = 0; j < 3; j++) pw[3 * k + j] = obj[3 * i + j];
-        q[2 * k] = ((double)img[2 * i] - K[2]) * ifx;
-        q[2 * k + 1] = ((double)img[2 * i + 1] - K[5]) * ify;
-    }
-    SqpnpCost c;
-    sqpnp_cost(pw, q, c);
     double Oc[81], ev[9], evec[81];
     std::memcpy(Oc, c.Om, sizeof(Oc));
-    la::sym_eig(Oc, 9, ev, evec);
-    double starts[5][9];
+    la::sym_eig_ql(Oc, 9, ev, evec);
+    double starts[5][9], Es[5], ts[5][3];
     std::memcpy(starts[0], R0, sizeof(double) * 9);
     for (int s = 0; s < 4; s++) {
         const double* e = evec + 9 * (8 - (s >> 1));
@@ -457,31 +469,34 @@ void final_fit(const float* obj, const float* img, const std::vector<int>& inl, 
         for (int k = 0; k < 9; k++) M[k] = ((s & 1) ? -1.0 : 1.0) * e[k];
         la::nearest_rotation(M, starts[s + 1]);
     }
-    double best = DBL_MAX;
-    for (auto& st : starts) {
-        double cand[9];
-        std::memcpy(cand, st, sizeof(cand));
-        const double E = refine_so3(c.Om, cand);
-        double tc[3];
+    for (int s = 0; s < 5; s++) {
+        Es[s] = refine_so3(c.Om, starts[s]);
         for (int a = 0; a < 3; a++) {
-            tc[a] = 0;
-            for (int col = 0; col < 9; col++) tc[a] += c.P[9 * a + col] * cand[col];
-        }
-        int pos = 0;
-        for (int k = 0; k < n; k++) pos += dot3(cand + 6, &pw[3 * (size_t)k]) + tc[2] > 0;
-        if (2 * pos < n) continue;
-        if (E < best) {
-            best = E;
-            std::memcpy(R, cand, sizeof(cand));
-            std::memcpy(t, tc, sizeof(tc));
+            ts[s][a] = 0;
+            for (int col = 0; col < 9; col++) ts[s][a] += c.P[9 * a + col] * starts[s][col];
         }
     }
-    if (best == DBL_MAX) {
-        std::memcpy(R, R0, sizeof(double) * 9);
-        for (int a = 0; a < 3; a++) {
-            t[a] = 0;
-            for (int col = 0; col < 9; col++) t[a] += c.P[9 * a + col] * R0[col];
+    // candidates in cost order (ties: start order), first cheirality pass wins
+    int ord[5] = {0, 1, 2, 3, 4};
+    for (int i = 1; i < 5; i++)
+        for (int j = i; j > 0 && Es[ord[j]] < Es[ord[j - 1]]; j--) std::swap(ord[j], ord[j - 1]);
+    for (int k = 0; k < 5; k++) {
+        const int s = ord[k];
+        const double* cand = starts[s];
+        int pos = 0;
+        for (int i : inl) {
+            const double p[3] = {obj[3 * i], obj[3 * i + 1], obj[3 * i + 2]};
+            pos += dot3(cand + 6, p) + ts[s][2] > 0;
         }
+        if (2 * pos < n) continue;
+        std::memcpy(R, cand, sizeof(double) * 9);
+        std::memcpy(t, ts[s], sizeof(double) * 3);
+        return;
+    }
+    std::memcpy(R, R0, sizeof(double) * 9);
+    for (int a = 0; a < 3; a++) {
+        t[a] = 0;
+        for (int col = 0; col < 9; col++) t[a] += c.P[9 * a + col] * R0[col];
     }
 }
 
@@ -509,9 +524,10 @@ void RansacSeq::begin(const float* o, const float* im, int npts, int iterations)
 int RansacSeq::gen_chunk(const double K[9]) {
     m = 0;
     if (done || direct) return 0;
-    // chunk schedule 2, 8, 16, 16, ...: clean data stops after the first
-    // hypothesis (niters -> 0), so the first round stays small
-    const int sched = rounds == 0 ? 2 : rounds == 1 ? 8 : kRansacChunk;
+    // chunk schedule 3, 8, 16, 16, ...: at the tracker's inlier ratios (> 98 %)
+    // RANSACUpdateNumIters brings niters down to 2-3 after the first accepted
+    // hypothesis, so one round usually suffices
+    const int sched = rounds == 0 ? 3 : rounds == 1 ? 8 : kRansacChunk;
     const int want = (niters - iter) < sched ? (niters - iter) : sched;
     rounds++;
     Rng r{rng};
@@ -559,9 +575,10 @@ void RansacSeq::consume(const int* counts, const uint32_t* bits, int words_cap, 
     if (iter >= niters) done = true;
 }
 
-void RansacSeq::finish(const double K[9]) {
+void RansacSeq::select(const double K[9]) {
     inliers.clear();
     ok = false;
+    fitted = false;
     if (n < 4) return;
     if (direct) {
         double R[9], t[3];
@@ -572,16 +589,51 @@ void RansacSeq::finish(const double K[9]) {
         for (int i = 0; i < n; i++) best[i >> 5] |= 1u << (i & 31);
         maxGood = n;
         ok = true;
+        fitted = true;
         return;
     }
     if (maxGood <= 0) return;
     for (int i = 0; i < n; i++)
         if ((best[i >> 5] >> (i & 31)) & 1) inliers.push_back(i);
+    ok = true;
+}
+
+// Normalised image coordinates and world points of the inliers (as doubles).
+static void inlier_arrays(const float* obj, const float* img, const std::vector<int>& inl, const double K[9],
+                          std::vector<double>& pw, std::vector<double>& q) {
+    const int n = (int)inl.size();
+    pw.resize(3 * (size_t)n);
+    q.resize(2 * (size_t)n);
+    const double ifx = 1. / K[0], ify = 1. / K[4];
+    for (int k = 0; k < n; k++) {
+        const int i = inl[k];
+        for (int j = 0; j < 3; j++) pw[3 * k + j] = obj[3 * i + j];
+        q[2 * k] = ((double)img[2 * i] - K[2]) * ifx;
+        q[2 * k + 1] = ((double)img[2 * i + 1] - K[5]) * ify;
+    }
+}
+
+void RansacSeq::fit(const double K[9], const double* sums) {
+    if (!ok || fitted) return;
+    double own[60];
+    if (!sums) {
+        std::vector<double> pw, q;
+        inlier_arrays(obj, img, inliers, K, pw, q);
+        sqpnp_sums(pw.data(), q.data(), (int)inliers.size(), own);
+        sums = own;
+    }
+    SqpnpCost c;
+    sqpnp_assemble(sums, c);
     double Rf[9], tf[3];
-    final_fit(obj, img, inliers, K, bestR, Rf, tf);
+    fit_from_cost(c, obj, inliers, bestR, Rf, tf);
     la::rodrigues_inv(Rf, rvec);
     std::memcpy(tvec, tf, sizeof(tf));
-    ok = true;
+    fitted = true;
+}
+
+void RansacSeq::finish(const double K[9]) {
+    select(K);
+    fit(K, nullptr);
 }
 
 }  // namespace svo

@@ -26,7 +26,7 @@ struct RansacSeq {
     int n = 0;
     uint64_t rng = 0;
     int niters = 0, iter = 0, maxGood = 0, nh = 0, m = 0, rounds = 0;
-    bool done = true, direct = false, ok = false;
+    bool done = true, direct = false, ok = false, fitted = false;
     bool valid[kRansacChunk];
     double hyp[12 * kRansacChunk];
     std::vector<uint32_t> best;
@@ -37,7 +37,14 @@ struct RansacSeq {
     void begin(const float* obj, const float* img, int n, int iterations);
     int gen_chunk(const double K[9]);  // fills hyp[0..m) (R row-major + t); returns m
     void consume(const int* counts, const uint32_t* bits, int words_cap, double confidence);
-    void finish(const double K[9]);    // final SQPnP-objective fit on the inliers
+    void select(const double K[9]);    // inlier set of the best model (the output inliers)
+    // final SQPnP-objective fit on the inliers; sums = their 60 sufficient
+    // statistics (sqpnp_sums / the suffstats kernel) or null to compute here
+    void fit(const double K[9], const double* sums);
+    void finish(const double K[9]);    // select + fit
 };
+
+// Sufficient statistics of the SQPnP cost over n points (60 doubles).
+void sqpnp_sums(const double* pw, const double* q, int n, double* sums);
 
 }  // namespace svo

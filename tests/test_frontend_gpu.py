@@ -47,12 +47,14 @@ def test_frontend_matches_oracle_loop(bucket):
         np.testing.assert_allclose(O.rodrigues(rv), sc.R(t), atol=3e-3)
 
 
-def test_frontend_batch_independence():
-    """A sequence's result does not depend on the batch it runs in."""
+@pytest.mark.parametrize("groups", [1, 2, 3])
+def test_frontend_batch_independence(groups):
+    """A sequence's result does not depend on the batch it runs in, nor on the
+    pipeline slicing of the batch (slices overlap LK and host RANSAC)."""
     ctx = S.Context(0)
     W, H, N, T = 1241, 376, 2000, 4
     scenes = [Scene(W, H, seed=s) for s in range(3)]
-    feb = make_frontend(ctx, scenes, T, N)
+    feb = make_frontend(ctx, scenes, T, N, groups=groups)
     feb.init(0)
     solo = [make_frontend(ctx, [sc], T, N) for sc in scenes]
     for f in solo:

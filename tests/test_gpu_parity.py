@@ -123,9 +123,17 @@ TEMPORAL = dict(win=(21, 21), ml=3, crit=(3, 50, 1e-3), flags=S.LK_GET_MIN_EIGEN
 STEREO = dict(win=(11, 11), ml=3, crit=(3, 30, 1e-3), flags=0)                        # R:src/tracking.cpp:101-105
 
 
+@pytest.fixture(params=["fixed-window", "generic"])
+def lk_kernel(request, monkeypatch):
+    """Both LK kernels: the compile-time-window one (21x21, 11x11, 15x15, 31x31)
+    and the runtime-window one every other size uses (SVO_LK_GENERIC=1)."""
+    monkeypatch.setenv("SVO_LK_GENERIC", "1" if request.param == "generic" else "0")
+    return request.param
+
+
 @pytest.mark.parametrize("cfg", [TEMPORAL, STEREO], ids=["temporal21", "stereo11"])
 @pytest.mark.parametrize("wh,seed,n", [((1241, 376), 0, 2000), ((160, 120), 1, 300), ((1920, 1080), 2, 4000)])
-def test_lk_bit_exact(ctx, cfg, wh, seed, n):
+def test_lk_bit_exact(ctx, cfg, wh, seed, n, lk_kernel):
     sc, pts, got, ref, sse = _lk_pair(ctx, *wh, seed, n, cfg["win"], cfg["ml"], cfg["crit"], cfg["flags"])
     gn, gs, ge = got
     rn, rs, re_, _ = ref
@@ -140,7 +148,7 @@ def test_lk_bit_exact(ctx, cfg, wh, seed, n):
     assert (gs != ss).mean() < 0.002
 
 
-def test_lk_iteration_count_matches_oracle(ctx):
+def test_lk_iteration_count_matches_oracle(ctx, lk_kernel):
     sc, A, B = frames(1241, 376, seed=0)
     pts = O.fast(A, 20, True)[:1000, :2]
     ga, gb = ctx.image(A, 4), ctx.image(B, 4)
@@ -150,7 +158,7 @@ def test_lk_iteration_count_matches_oracle(ctx):
     assert ctx.lk_last_iterations() == int(it.sum())
 
 
-def test_lk_borders_and_out_of_image(ctx):
+def test_lk_borders_and_out_of_image(ctx, lk_kernel):
     sc, A, B = frames(320, 240, seed=4)
     rng = np.random.default_rng(0)
     pts = np.concatenate([
@@ -252,7 +260,7 @@ def test_pnp_ransac_too_few_points(ctx):
         ctx.solve_pnp_ransac(np.zeros((3, 3)), np.zeros((3, 2), np.float32), np.eye(3))
 
 
-def test_lk_negative_bilinear_weight_case(ctx):
+def test_lk_negative_bilinear_weight_case(ctx, lk_kernel):
     """OpenCV's rounded weights can make iw11 = 2^14 - iw00 - iw01 - iw10 = -1
     (fractional offsets (0.00706080, 0.00132304) or (0.0000501, 0.2830146)):
     the fixed-point dot products must be signed."""
@@ -296,3 +304,17 @@ def test_gpu_matches_committed_golden(ctx):
     ok, rv, tv, inl = ctx.solve_pnp_ransac(g["X"], g["t_next"], g["K"])
     assert ok and np.array_equal(inl, g["pnp_inliers"])
     assert np.allclose(rv, g["pnp_rvec"], atol=1e-7) and np.allclose(tv, g["pnp_tvec"], atol=1e-6)
+
+
+@pytest.mark.parametrize("win", [(15, 15), (31, 31)])
+def test_lk_other_fixed_windows(ctx, win, lk_kernel):
+    sc, A, B = frames(640, 480, seed=9)
+    pts = O.fast(A, 20, True)[:800, :2]
+    ga, gb = ctx.image(A, 4), ctx.image(B, 4)
+    for flags in (0, S.LK_GET_MIN_EIGENVALS):
+        gn, gs, ge = ctx.calc_optical_flow_pyr_lk(ga, gb, pts, win_size=win, max_level=3, criteria=(3, 30, 1e-3),
+                                                  flags=flags)
+        rn, rs, re_, _ = O.lk(A, B, pts, win, 3, (3, 30, 1e-3), flags)
+        assert np.array_equal(gs, rs)
+        assert np.array_equal(gn.view(np.uint32), rn.view(np.uint32))
+        assert np.array_equal(ge.view(np.uint32), re_.view(np.uint32))
