@@ -405,6 +405,7 @@ __global__ __launch_bounds__(256) void lk_kernel(LKBatch B, LKDev p) {
 // int32 sums cannot overflow (7 rows x 2 x 8160 x 4080 < 2^31), so the sums are
 // the same exact integers as before: bit-identical results.
 constexpr int ru4(int v) { return (v + 3) & ~3; }
+typedef uint32_t u32x2a4 __attribute__((ext_vector_type(2), aligned(4)));
 
 template <int WW, int WH>
 struct Shape {
@@ -549,7 +550,7 @@ __global__ __launch_bounds__(256, MINW) void lk_fast_kernel(LKBatch B, LKDev p) 
     for (int level = max_level; level >= 0; level--) {
         const ImgLevel I = prev.lv[level];
         const ImgLevel J = next.lv[level];
-        const float lscale = (float)(1. / (1 << level));
+        const float lscale = __builtin_amdgcn_ldexpf(1.f, -level);  // == (float)(1. / (1 << level))
         float prevx = px * lscale, prevy = py * lscale;
         float nextx, nexty;
         if (level == max_level) {
@@ -588,7 +589,7 @@ __global__ __launch_bounds__(256, MINW) void lk_fast_kernel(LKBatch B, LKDev p) 
         int jxa = jx0 & ~3;
         stage_aligned<S::IPW, S::IPH>(ipair, I, ixa, ipy, lane);
         stage_aligned<S::JRW, S::JRH>(jreg, J, jxa, jy0, lane);
-        uint32_t dv[RPG + 1][2];
+        u32x2a4 dv[RPG + 1];  // (Ix|Iy) at columns X, X+1 of each row: one dwordx2 load
         {
             const int dpitch = dprev.pitch[level];
             gu32 dsrc = (gu32)dprev.data[level];
@@ -599,19 +600,18 @@ __global__ __launch_bounds__(256, MINW) void lk_fast_kernel(LKBatch B, LKDev p) 
 #pragma unroll
                 for (int k = 0; k <= RPG; k++) {
                     const int kk = (S::FULL || r0 + k <= WH) ? k : 0;  // stay inside the window
-                    dv[k][0] = q[(size_t)kk * dpitch];
-                    dv[k][1] = q[(size_t)kk * dpitch + 1];
+                    dv[k] = *(const __attribute__((address_space(1))) u32x2a4*)(q + (size_t)kk * dpitch);
                 }
             } else {
                 const bool c0 = X >= 0 && X < I.w, c1 = X + 1 >= 0 && X + 1 < I.w;
 #pragma unroll
                 for (int k = 0; k <= RPG; k++) {
-                    dv[k][0] = dv[k][1] = 0;
+                    dv[k] = u32x2a4{0u, 0u};
                     const int Y = ipy + r0 + k;
                     if ((S::FULL || r0 + k <= WH) && Y >= 0 && Y < I.h) {
                         gu32 q = dsrc + (size_t)Y * dpitch + X;
-                        if (c0) dv[k][0] = q[0];
-                        if (c1) dv[k][1] = q[1];
+                        if (c0) dv[k].x = q[0];
+                        if (c1) dv[k].y = q[1];
                     }
                 }
             }
@@ -633,10 +633,10 @@ __global__ __launch_bounds__(256, MINW) void lk_fast_kernel(LKBatch B, LKDev p) 
                 const unsigned P1 = ip[(S::FULL || r0 + j < WH ? j + 1 : 0) * S::IPW];
                 iv[j] = sdot2(P0, IW0, sdot2_r(P1, IW1, rnd_i)) >> (W_BITS - 5);
                 P0 = P1;
-                const unsigned X0 = __builtin_amdgcn_perm(dv[j][1], dv[j][0], 0x05040100u);
-                const unsigned X1 = __builtin_amdgcn_perm(dv[j + 1][1], dv[j + 1][0], 0x05040100u);
-                const unsigned Y0 = __builtin_amdgcn_perm(dv[j][1], dv[j][0], 0x07060302u);
-                const unsigned Y1 = __builtin_amdgcn_perm(dv[j + 1][1], dv[j + 1][0], 0x07060302u);
+                const unsigned X0 = __builtin_amdgcn_perm(dv[j].y, dv[j].x, 0x05040100u);
+                const unsigned X1 = __builtin_amdgcn_perm(dv[j + 1].y, dv[j + 1].x, 0x05040100u);
+                const unsigned Y0 = __builtin_amdgcn_perm(dv[j].y, dv[j].x, 0x07060302u);
+                const unsigned Y1 = __builtin_amdgcn_perm(dv[j + 1].y, dv[j + 1].x, 0x07060302u);
                 gx[j] = valid ? sdot2(X0, IW0, sdot2_r(X1, IW1, rnd_d)) >> W_BITS : 0;
                 gy[j] = valid ? sdot2(Y0, IW0, sdot2_r(Y1, IW1, rnd_d)) >> W_BITS : 0;
             }
@@ -780,14 +780,9 @@ template <int WW, int WH>
 hipError_t launch_fast(const LKBatch& b, int nseq, int max_n, const LKDev& d, hipStream_t st) {
     dim3 grid((max_n + 3) / 4, nseq);
     constexpr int lds_bytes = 4 * Shape<WW, WH>::WAVE_BYTES;
-    const char* v = std::getenv("SVO_LK_MINW");
-    const int minw = v ? std::atoi(v) : 1;
-    if (minw >= 8)
-        hipLaunchKernelGGL((lk_fast_kernel<WW, WH, 8>), grid, dim3(256), lds_bytes, st, b, d);
-    else if (minw >= 2)
-        hipLaunchKernelGGL((lk_fast_kernel<WW, WH, 2>), grid, dim3(256), lds_bytes, st, b, d);
-    else
-        hipLaunchKernelGGL((lk_fast_kernel<WW, WH, 1>), grid, dim3(256), lds_bytes, st, b, d);
+    // occupancy is limited by LDS (7 blocks/CU) and ~70 VGPRs alike; capping the
+    // VGPRs lower spills (measured: launch bounds 6/7/8 waves all slower)
+    hipLaunchKernelGGL((lk_fast_kernel<WW, WH, 1>), grid, dim3(256), lds_bytes, st, b, d);
     return hipGetLastError();
 }
 

@@ -24,6 +24,7 @@ def main():
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--w", type=int, default=1241)
     ap.add_argument("--h", type=int, default=376)
+    ap.add_argument("--count", type=int, default=0, help="override the LK iteration cap")
     args = ap.parse_args()
     ctx = S.Context(0)
     sc = Scene(args.w, args.h, seed=0)
@@ -37,6 +38,8 @@ def main():
                               for i in range(reps)])[: args.points]
         win, crit, flags = ((21, 21), (3, 50, 1e-3), S.LK_GET_MIN_EIGENVALS) if args.what == "lk" else \
             ((11, 11), (3, 30, 1e-3), 0)
+        if args.count:
+            crit = (crit[0], args.count, crit[2])
         for r in range(args.reps):
             t = time.perf_counter()
             ctx.calc_optical_flow_pyr_lk(ga, gb, pts, win_size=win, max_level=3, criteria=crit, flags=flags)
