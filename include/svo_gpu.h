@@ -236,12 +236,15 @@ int svo_frontend_init(svo_frontend* fe, int t0);
 /* One step: frame t-1 -> t for every sequence (pyramid of t, temporal LK,
  * compaction, PnP RANSAC, outlier removal, masked FAST top-up). */
 int svo_frontend_step(svo_frontend* fe, int t, svo_frontend_stats* stats);
+/* Wait for every stream of the front end (a step returns with the next frame's
+ * pyramid and the pose statistics still running) and finish the pose fits. */
+int svo_frontend_synchronize(svo_frontend* fe);
 int svo_frontend_pose(svo_frontend* fe, int seq, double rvec[3], double tvec[3]);
 int svo_frontend_features(svo_frontend* fe, int seq, float* xy, int cap, int* n);
 /* Accumulated per-phase device time (ms) and launch counts since create/reset:
  * phases: 0 pyramid, 1 lk, 2 compact, 3 gather, 4 pnp_score, 5 mask, 6 fast,
  * 7 bucket, 8 append. Returns the number of phases. */
-int svo_frontend_phase_times(const svo_frontend* fe, double* ms, int64_t* launches, int cap);
+int svo_frontend_phase_times(svo_frontend* fe, double* ms, int64_t* launches, int cap);
 void svo_frontend_reset_times(svo_frontend* fe);
 
 /* ------------------------------------------------------------ synthetic input

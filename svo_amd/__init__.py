@@ -96,6 +96,7 @@ _SIGS = [
     ("svo_frontend_prebuild_pyramids", C.c_int, [_vp]),
     ("svo_frontend_init", C.c_int, [_vp, C.c_int]),
     ("svo_frontend_step", C.c_int, [_vp, C.c_int, _vp]),
+    ("svo_frontend_synchronize", C.c_int, [_vp]),
     ("svo_frontend_pose", C.c_int, [_vp, C.c_int, _f64p, _f64p]),
     ("svo_frontend_features", C.c_int, [_vp, C.c_int, _f32p, C.c_int, _i32p]),
     ("svo_frontend_phase_times", C.c_int, [_vp, _f64p, C.POINTER(C.c_int64), C.c_int]),
@@ -432,6 +433,10 @@ class Frontend:
         st = FrontendStats()
         self.ctx._check(lib().svo_frontend_step(self.handle, t, C.byref(st)))
         return st
+
+    def synchronize(self):
+        """Wait for all of the front end's streams and finish the pose fits."""
+        self.ctx._check(lib().svo_frontend_synchronize(self.handle))
 
     def pose(self, seq):
         r = np.zeros(3)

@@ -81,6 +81,10 @@ int svo_ctx_create(int device, svo_ctx** out) {
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return SVO_ERR_NODEVICE;
     if (device < 0 || device >= ndev) return SVO_ERR_ARG;
     if (hipSetDevice(device) != hipSuccess) return SVO_ERR_HIP;
+    // spin-wait host synchronisation: the front end syncs a few times per frame
+    // and a sleeping wake-up costs tens of microseconds (fails harmlessly if the
+    // device was already initialised with other flags)
+    (void)hipSetDeviceFlags(hipDeviceScheduleSpin);
     svo_ctx* c = new svo_ctx();
     c->device = device;
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {

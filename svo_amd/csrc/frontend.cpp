@@ -15,6 +15,8 @@
 //
 // FAST and the bucket run on the GPU while the host builds RANSAC hypotheses.
 #include <algorithm>
+#include <cstdio>
+#include <cstdlib>
 #include <chrono>
 #include <atomic>
 #include <condition_variable>
@@ -140,6 +142,7 @@ struct svo_frontend {
     std::vector<double> pose;  // [s][6]
     bool fits_pending = false;
     int pyr_ready = -1;  // frame index whose pyramid + Scharr were built ahead
+    hipEvent_t ev_stats = nullptr;  // SQPnP statistics of the last step on the host
     Pool* pool = nullptr;
     // pipeline: slices of the batch [g0[g], g0[g] + gn[g]) on their own streams
     int G = 1;
@@ -158,29 +161,42 @@ struct svo_frontend {
 
 namespace {
 
+// Phase timing: event pairs from a ring; a pair is folded into the totals once
+// its end event has completed (work that runs into the next step is collected
+// then), so timing never adds a synchronisation.
+constexpr int kEvRing = (int)(sizeof(((svo_frontend*)nullptr)->ev) / sizeof(hipEvent_t));
+
+void ph_fold(svo_frontend* fe, bool wait) {
+    std::vector<std::pair<int, int>> keep;
+    for (auto& p : fe->pending) {
+        if (wait) (void)hipEventSynchronize(fe->ev[p.second + 1]);
+        float ms = 0.f;
+        const hipError_t e = hipEventElapsedTime(&ms, fe->ev[p.second], fe->ev[p.second + 1]);
+        if (e == hipSuccess) {
+            fe->phase_ms[p.first] += ms;
+            fe->phase_n[p.first] += 1;
+        } else if (e == hipErrorNotReady) {
+            keep.push_back(p);
+        }
+    }
+    fe->pending.swap(keep);
+}
+
 void ph_begin(svo_frontend* fe, int ph, hipStream_t st, int* slot) {
     *slot = -1;
-    if (!fe->cfg.timing || fe->ev_used + 2 > (int)(sizeof(fe->ev) / sizeof(fe->ev[0]))) return;
-    *slot = fe->ev_used;
-    fe->ev_used += 2;
-    (void)hipEventRecord(fe->ev[*slot], st);
-    fe->pending.push_back({ph, *slot});
+    if (!fe->cfg.timing) return;
+    const int sl = fe->ev_used;
+    for (auto& p : fe->pending)  // ring wrapped onto a pair still in flight
+        if (p.second == sl) ph_fold(fe, true);
+    fe->ev_used = (fe->ev_used + 2) % kEvRing;
+    *slot = sl;
+    (void)hipEventRecord(fe->ev[sl], st);
+    fe->pending.push_back({ph, sl});
 }
 void ph_end(svo_frontend* fe, hipStream_t st, int slot) {
     if (slot >= 0) (void)hipEventRecord(fe->ev[slot + 1], st);
 }
-// after a stream sync: fold the recorded event pairs into the phase totals
-void ph_collect(svo_frontend* fe) {
-    for (auto& p : fe->pending) {
-        float ms = 0.f;
-        if (hipEventElapsedTime(&ms, fe->ev[p.second], fe->ev[p.second + 1]) == hipSuccess) {
-            fe->phase_ms[p.first] += ms;
-            fe->phase_n[p.first] += 1;
-        }
-    }
-    fe->pending.clear();
-    fe->ev_used = 0;
-}
+void ph_collect(svo_frontend* fe) { ph_fold(fe, false); }
 
 template <class T>
 T* carve(char*& p, size_t count) {
@@ -242,6 +258,7 @@ int fe_append(svo_frontend* fe, int t, int g0, int n, hipStream_t st) {
 double fe_finish_fits(svo_frontend* fe) {
     if (!fe->fits_pending) return 0.0;
     auto t0 = std::chrono::steady_clock::now();
+    (void)hipEventSynchronize(fe->ev_stats);
     fe->pool->run(fe->S, [&](int s) {
         RansacSeq& r = fe->rs[s];
         r.fit(fe->cfg.K, fe->h_stats + 60 * (size_t)s);
@@ -455,6 +472,7 @@ int svo_frontend_create(svo_ctx* ctx, const svo_frontend_config* cfg, svo_fronte
         }
         fe->ev_sync.assign(2 + 3 * G, nullptr);
         for (auto& e : fe->ev_sync) (void)hipEventCreateWithFlags(&e, hipEventDisableTiming);
+        (void)hipEventCreateWithFlags(&fe->ev_stats, hipEventDisableTiming);
     }
     SVO_HIP(ctx, hipMemcpyAsync(fe->d_desc, fe->desc_host.data(), sizeof(PyrDesc) * fe->desc_host.size(),
                                 hipMemcpyHostToDevice, ctx->stream));
@@ -485,6 +503,7 @@ void svo_frontend_destroy(svo_frontend* fe) {
     }
     for (auto& e : fe->ev_sync)
         if (e) (void)hipEventDestroy(e);
+    if (fe->ev_stats) (void)hipEventDestroy(fe->ev_stats);
     delete fe;
 }
 
@@ -541,6 +560,18 @@ int svo_frontend_init(svo_frontend* fe, int t0) {
 
 int svo_frontend_step(svo_frontend* fe, int t, svo_frontend_stats* stats) {
     if (!fe || t < 1) return SVO_ERR_ARG;
+    // host-side step trace (SVO_FE_TRACE=1): label + microseconds since step start
+    static const bool trace_on = [] {
+        const char* e = std::getenv("SVO_FE_TRACE");
+        return e && e[0] == '1';
+    }();
+    const auto trace_t0 = std::chrono::steady_clock::now();
+    std::vector<std::pair<const char*, double>> trace;
+    auto TP = [&](const char* label) {
+        if (trace_on)
+            trace.push_back({label, std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() -
+                                                                               trace_t0).count()});
+    };
     svo_ctx* ctx = fe->ctx;
     hipStream_t st0 = ctx->stream;
     const int S = fe->S, CAP = fe->CAP, G = fe->G;
@@ -603,15 +634,19 @@ int svo_frontend_step(svo_frontend* fe, int t, svo_frontend_stats* stats) {
         ph_end(fe, st0, slot);
         fe->pyr_ready = tn;
     }
+    TP("lk+pyr enqueued");
     // 3a. the previous step's final pose fits, deferred to here: the host does
     //     them while the GPU tracks this frame (before this step's D2H copies
     //     are queued: the fits read the previous frame's host mirrors)
     double ms_fit = fe_finish_fits(fe);
+    TP("fits done");
     for (int g = 0; g < G; g++) {
         const int a = fe->g0[g], n = fe->gn[g];
         hipStream_t sg = fe->gst[g];
         int mp = 0;
         for (int s = a; s < a + n; s++) mp = std::max(mp, fe->h_nA[s]);
+        // the previous step's statistics kernel still reads xyB / obj
+        SVO_HIP(ctx, hipStreamWaitEvent(sg, fe->ev_stats, 0));
         CompactBatch cb{fe->nA + a, fe->status + (size_t)a * CAP, nullptr, 0, fe->next_xy + 2 * (size_t)a * CAP,
                         fe->midA + (size_t)a * CAP, fe->iters + (size_t)a * CAP, fe->itsum + a,
                         fe->xyB + 2 * (size_t)a * CAP, fe->midB + (size_t)a * CAP, fe->nB + a, CAP};
@@ -659,8 +694,10 @@ int svo_frontend_step(svo_frontend* fe, int t, svo_frontend_stats* stats) {
     for (int g = 0; g < G; g++) {
         const int a = fe->g0[g], n = fe->gn[g];
         hipStream_t sg = fe->gst[g];
+        TP("ransac begin");
         auto tw = clk::now();
         SVO_HIP(ctx, hipEventSynchronize(fe->ev_sync[3 + 2 * g]));
+        TP("lk results on host");
         ms_wait += ms_since(tw);
         int max_b = 0;
         for (int s = a; s < a + n; s++) {
@@ -669,8 +706,13 @@ int svo_frontend_step(svo_frontend* fe, int t, svo_frontend_stats* stats) {
             max_b = std::max(max_b, fe->h_nB[s]);
         }
         for (;;) {
+            // sequences still sampling (no pool dispatch once all are done)
+            bool any = false;
+            for (int s = a; s < a + n; s++) any |= !fe->rs[s].done && !fe->rs[s].direct;
+            if (!any) break;
             auto th = clk::now();
             fe->pool->run(n, [&](int i) { ms[a + i] = fe->rs[a + i].gen_chunk(c.K); });
+            TP("hyps generated");
             ms_hyp += ms_since(th);
             int mmax = 0;
             for (int s = a; s < a + n; s++) mmax = std::max(mmax, ms[s]);
@@ -697,42 +739,46 @@ int svo_frontend_step(svo_frontend* fe, int t, svo_frontend_stats* stats) {
                                         fe->bits_all + (size_t)a * kRansacChunk * fe->WORDS,
                                         sizeof(uint32_t) * n * kRansacChunk * fe->WORDS, hipMemcpyDeviceToHost, sg));
             tw = clk::now();
+            TP("scoring enqueued");
             SVO_HIP(ctx, hipStreamSynchronize(sg));
             ms_wait += ms_since(tw);
-            fe->pool->run(n, [&](int i) {
-                const int s = a + i;
+            TP("scores on host");
+            // consume is a few compares per hypothesis: cheaper here than a pool dispatch
+            for (int s = a; s < a + n; s++)
                 if (ms[s] > 0)
                     fe->rs[s].consume(fe->h_cnt + (size_t)s * kRansacChunk,
                                       fe->h_bits + (size_t)s * kRansacChunk * fe->WORDS, fe->WORDS, c.pnp_confidence);
-            });
         }
         // the RANSAC inlier set is the output (R:src/tracking.cpp:218-229); the final
         // SQPnP-objective fit only refines the pose, from statistics summed on the GPU
+        TP("consumed");
         auto tf = clk::now();
-        fe->pool->run(n, [&](int i) {
-            const int s = a + i;
+        for (int s = a; s < a + n; s++) {
             RansacSeq& r = fe->rs[s];
-            r.select(c.K);
+            r.select(c.K, false);
             uint32_t* b = fe->h_best + (size_t)s * fe->WORDS;
             std::memset(b, 0, sizeof(uint32_t) * fe->WORDS);
             if (r.ok) {
-                for (int k : r.inliers) b[k >> 5] |= 1u << (k & 31);
+                std::memcpy(b, r.best.data(), sizeof(uint32_t) * r.best.size());
             } else if (r.n < 4) {
                 // solvePnPRansac would throw (CV_Assert npoints >= 4); keep the frame's
                 // features untouched instead of aborting the batch
                 for (int k = 0; k < r.n; k++) b[k >> 5] |= 1u << (k & 31);
             }
-        });
+            inl += r.ok ? (int64_t)r.maxGood : r.n;
+        }
         ms_fit += ms_since(tf);
-        for (int s = a; s < a + n; s++) inl += fe->rs[s].ok ? (int64_t)fe->rs[s].inliers.size() : fe->rs[s].n;
         SVO_HIP(ctx, hipMemcpyAsync(fe->bits_best + (size_t)a * fe->WORDS, fe->h_best + (size_t)a * fe->WORDS,
                                     sizeof(uint32_t) * n * fe->WORDS, hipMemcpyHostToDevice, sg));
+        // the SQPnP statistics only feed the pose fits, which run during the next
+        // step: off the critical path, on the FAST stream
+        SVO_HIP(ctx, hipEventRecord(fe->ev_sync[2 + 2 * G + g], sg));
+        SVO_HIP(ctx, hipStreamWaitEvent(sf, fe->ev_sync[2 + 2 * G + g], 0));
         SVO_HIP(ctx, launch_suffstats(fe->obj + 3 * (size_t)a * CAP, fe->xyB + 2 * (size_t)a * CAP, fe->nB + a, CAP,
                                       fe->bits_best + (size_t)a * fe->WORDS, fe->WORDS, n, c.K,
-                                      fe->stats + 60 * (size_t)a, sg));
+                                      fe->stats + 60 * (size_t)a, sf));
         SVO_HIP(ctx, hipMemcpyAsync(fe->h_stats + 60 * (size_t)a, fe->stats + 60 * (size_t)a, sizeof(double) * 60 * n,
-                                    hipMemcpyDeviceToHost, sg));
-        SVO_HIP(ctx, hipEventRecord(fe->ev_sync[2 + 2 * G + g], sg));
+                                    hipMemcpyDeviceToHost, sf));
         // the mask (reads xyA) and FAST (writes kps) must be done before xyA is rewritten / kps read
         SVO_HIP(ctx, hipStreamWaitEvent(sg, ev_fast, 0));
         CompactBatch cb2{fe->nB + a, nullptr, fe->bits_best + (size_t)a * fe->WORDS, fe->WORDS,
@@ -747,12 +793,18 @@ int svo_frontend_step(svo_frontend* fe, int t, svo_frontend_stats* stats) {
         SVO_HIP(ctx, hipMemcpyAsync(fe->h_added + a, fe->added + a, sizeof(int) * n, hipMemcpyDeviceToHost, sg));
     }
     fe->fits_pending = true;  // statistics land with the stream syncs below
+    SVO_HIP(ctx, hipEventRecord(fe->ev_stats, sf));
+    TP("tail enqueued");
+    // only the slices' streams: the statistics (FAST stream) and the next
+    // frame's pyramid (main stream) keep running into the next step
     auto tw = clk::now();
     for (int g = 0; g < G; g++) SVO_HIP(ctx, hipStreamSynchronize(fe->gst[g]));
-    SVO_HIP(ctx, hipStreamSynchronize(sf));
-    SVO_HIP(ctx, hipStreamSynchronize(st0));
     ms_wait += ms_since(tw);
+    TP("synced");
     ph_collect(fe);
+    if (trace_on) {
+        for (auto& e : trace) std::fprintf(stderr, "[fe t=%d] %8.1f us  %s\n", t, e.second, e.first);
+    }
     if (stats) {
         std::memset(stats, 0, sizeof(*stats));
         for (int s = 0; s < S; s++) {
@@ -767,6 +819,16 @@ int svo_frontend_step(svo_frontend* fe, int t, svo_frontend_stats* stats) {
         stats->host_ms_fit = ms_fit;
         stats->host_ms_wait = ms_wait;
     }
+    return SVO_OK;
+}
+
+int svo_frontend_synchronize(svo_frontend* fe) {
+    if (!fe) return SVO_ERR_ARG;
+    svo_ctx* ctx = fe->ctx;
+    for (auto& g : fe->gst) SVO_HIP(ctx, hipStreamSynchronize(g));
+    if (fe->st_fast) SVO_HIP(ctx, hipStreamSynchronize(fe->st_fast));
+    SVO_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    fe_finish_fits(fe);
     return SVO_OK;
 }
 
@@ -791,8 +853,9 @@ int svo_frontend_features(svo_frontend* fe, int seq, float* xy, int cap, int* n)
     return SVO_OK;
 }
 
-int svo_frontend_phase_times(const svo_frontend* fe, double* ms, int64_t* launches, int cap) {
+int svo_frontend_phase_times(svo_frontend* fe, double* ms, int64_t* launches, int cap) {
     if (!fe) return SVO_ERR_ARG;
+    ph_fold(fe, true);
     for (int i = 0; i < kPhases && i < cap; i++) {
         if (ms) ms[i] = fe->phase_ms[i];
         if (launches) launches[i] = fe->phase_n[i];
@@ -802,6 +865,7 @@ int svo_frontend_phase_times(const svo_frontend* fe, double* ms, int64_t* launch
 
 void svo_frontend_reset_times(svo_frontend* fe) {
     if (!fe) return;
+    ph_fold(fe, true);
     for (int i = 0; i < kPhases; i++) {
         fe->phase_ms[i] = 0;
         fe->phase_n[i] = 0;

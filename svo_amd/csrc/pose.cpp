@@ -524,10 +524,10 @@ void RansacSeq::begin(const float* o, const float* im, int npts, int iterations)
 int RansacSeq::gen_chunk(const double K[9]) {
     m = 0;
     if (done || direct) return 0;
-    // chunk schedule 3, 8, 16, 16, ...: at the tracker's inlier ratios (> 98 %)
-    // RANSACUpdateNumIters brings niters down to 2-3 after the first accepted
-    // hypothesis, so one round usually suffices
-    const int sched = rounds == 0 ? 3 : rounds == 1 ? 8 : kRansacChunk;
+    // chunk schedule 2, 8, 16, 16, ...: below ~1 % outliers RANSACUpdateNumIters
+    // (p 0.999, 5 points) brings niters down to 2 after the first accepted
+    // hypothesis, so one round suffices; above, round 2 covers up to 10
+    const int sched = rounds == 0 ? 2 : rounds == 1 ? 8 : kRansacChunk;
     const int want = (niters - iter) < sched ? (niters - iter) : sched;
     rounds++;
     Rng r{rng};
@@ -575,7 +575,7 @@ void RansacSeq::consume(const int* counts, const uint32_t* bits, int words_cap, 
     if (iter >= niters) done = true;
 }
 
-void RansacSeq::select(const double K[9]) {
+void RansacSeq::select(const double K[9], bool list) {
     inliers.clear();
     ok = false;
     fitted = false;
@@ -593,8 +593,9 @@ void RansacSeq::select(const double K[9]) {
         return;
     }
     if (maxGood <= 0) return;
-    for (int i = 0; i < n; i++)
-        if ((best[i >> 5] >> (i & 31)) & 1) inliers.push_back(i);
+    if (list)
+        for (int i = 0; i < n; i++)
+            if ((best[i >> 5] >> (i & 31)) & 1) inliers.push_back(i);
     ok = true;
 }
 
@@ -615,6 +616,9 @@ static void inlier_arrays(const float* obj, const float* img, const std::vector<
 
 void RansacSeq::fit(const double K[9], const double* sums) {
     if (!ok || fitted) return;
+    if (inliers.empty())  // select(..., false) left the list to here
+        for (int i = 0; i < n; i++)
+            if ((best[i >> 5] >> (i & 31)) & 1) inliers.push_back(i);
     double own[60];
     if (!sums) {
         std::vector<double> pw, q;

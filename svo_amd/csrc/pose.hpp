@@ -37,7 +37,9 @@ struct RansacSeq {
     void begin(const float* obj, const float* img, int n, int iterations);
     int gen_chunk(const double K[9]);  // fills hyp[0..m) (R row-major + t); returns m
     void consume(const int* counts, const uint32_t* bits, int words_cap, double confidence);
-    void select(const double K[9]);    // inlier set of the best model (the output inliers)
+    // inlier set of the best model (the output): `best` bits, and the index list
+    // too unless list = false (fit() then builds it)
+    void select(const double K[9], bool list = true);
     // final SQPnP-objective fit on the inliers; sums = their 60 sufficient
     // statistics (sqpnp_sums / the suffstats kernel) or null to compute here
     void fit(const double K[9], const double* sums);

@@ -1,0 +1,23 @@
+#!/usr/bin/env python3
+"""Print one frontend step's GPU timeline from a rocprofv3 --kernel-trace
+--memory-copy-trace CSV pair (tools/gpu_trace.sh)."""
+import csv
+import re
+import sys
+
+d = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/tr_g1"
+rows = []
+for r in csv.DictReader(open(f"{d}/run_kernel_trace.csv")):
+    n = r["Kernel_Name"]
+    m = re.search(r"([a-z_]+kernel)", n)
+    short = m.group(1) if m else n.split("(")[0][-32:]
+    rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), "K:" + short, r.get("Queue_Id", "")))
+for r in csv.DictReader(open(f"{d}/run_memory_copy_trace.csv")):
+    rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), "C:" + r["Direction"][:24], r.get("Queue_Id", "")))
+rows.sort()
+lk = [x for x in rows if "lk_fast" in x[2] or x[2] == "K:lk_kernel"]
+t0, tp = lk[-1][0], lk[-2][0]
+print(f"step period {(t0 - tp) / 1e3:.1f} us")
+for a, b, n, q in rows:
+    if tp <= a < t0:
+        print(f"{(a - tp) / 1e3:8.1f} {(b - tp) / 1e3:8.1f} {(b - a) / 1e3:7.1f} q{q} {n}")
