@@ -416,8 +416,14 @@ struct Shape {
     static constexpr int IPW = ru4(WW + 3), IPH = WH + 1;           // I pairs: entries x rows
     static constexpr int JRW = ru4(WW + 2 * JM + 3), JRH = WH + 1 + 2 * JM;
     static constexpr int IBYTES = IPW * IPH * 4, JBYTES = JRW * JRH * 4;
-    static constexpr int WAVE_BYTES = IBYTES + JBYTES;
+    static constexpr int WAVE_BYTES = IBYTES + JBYTES + 16;  // + a sink for the stager's spare lanes
 };
+
+// v_perm selector picking bytes sh, sh+1 of the 8-byte pair {hi:lo} into the
+// 16-bit lanes of a pixel pair (p[sh] | p[sh+1] << 16).
+__device__ __forceinline__ unsigned pair_sel(unsigned sh) {
+    return sh | 0x0c00u | ((sh + 1) << 16) | 0x0c000000u;
+}
 
 __device__ __forceinline__ unsigned lo16x2(int lo, int hi) {  // (lo & 0xffff) | (hi << 16) in one v_perm
     return __builtin_amdgcn_perm((unsigned)hi, (unsigned)lo, 0x05040100u);
@@ -507,6 +513,45 @@ __device__ __forceinline__ void stage_aligned(unsigned* dst, const ImgLevel& L, 
     }
 }
 
+// Branch-free form of stage_aligned (no exec-mask branches, which cost ~5 SALU
+// each): every lane loads a valid dword (rows past the region re-read the last
+// row, so they carry the same bytes as that row's owner) and every lane writes:
+// lanes without a complete set of pairs write to `sink`. A scheduling barrier
+// per pass keeps the compiler from hoisting all loads (register pressure).
+template <int W, int H>
+__device__ __forceinline__ void stage_bf(unsigned* dst, unsigned* sink, const ImgLevel& L, int xa, int y0,
+                                         int lane) {
+    constexpr int LPR = W / 4 + 1, RPP = 64 / LPR, NP = (H + RPP - 1) / RPP;
+    const int lr = lane / LPR, d = lane - lr * LPR;
+    const bool inside = xa >= 0 && y0 >= 0 && xa + W + 1 <= L.w && y0 + H <= L.h;
+    if (inside) {
+        gu8 src = (gu8)L.data + xa + 4 * d;
+        unsigned* dpl = (d < W / 4 && lr < RPP) ? dst + 4 * d : sink;
+        const int dstride = (d < W / 4 && lr < RPP) ? W : 0;
+#pragma unroll
+        for (int q = 0; q < NP; q++) {
+            int r = q * RPP + lr;
+            r = r < H ? r : H - 1;
+            const unsigned v = *(gu32)(src + (size_t)(y0 + r) * L.pitch);
+            const unsigned nv = (unsigned)__builtin_amdgcn_ds_bpermute((lane + 1) << 2, (int)v);
+            uint4 o;
+            o.x = __builtin_amdgcn_perm(nv, v, 0x0c010c00u);
+            o.y = __builtin_amdgcn_perm(nv, v, 0x0c020c01u);
+            o.z = __builtin_amdgcn_perm(nv, v, 0x0c030c02u);
+            o.w = __builtin_amdgcn_perm(nv, v, 0x0c040c03u);
+            *reinterpret_cast<uint4*>(dpl + r * dstride) = o;
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    } else {
+        gu8 src = (gu8)L.data;
+        for (int k = lane; k < W * H; k += 64) {
+            const int r = k / W, e = k - r * W;
+            gu8 row = src + (size_t)refl101(y0 + r, L.h) * L.pitch;
+            dst[k] = (unsigned)row[refl101(xa + e, L.w)] | ((unsigned)row[refl101(xa + e + 1, L.w)] << 16);
+        }
+    }
+}
+
 template <int WW, int WH, int MINW>
 __global__ __launch_bounds__(256, MINW) void lk_fast_kernel(LKBatch B, LKDev p) {
     using S = Shape<WW, WH>;
@@ -526,6 +571,7 @@ __global__ __launch_bounds__(256, MINW) void lk_fast_kernel(LKBatch B, LKDev p) 
     const DerivDesc& dprev = B.dprev[seq];
     unsigned* ipair = reinterpret_cast<unsigned*>(lds + wid * S::WAVE_BYTES);
     unsigned* jreg = reinterpret_cast<unsigned*>(lds + wid * S::WAVE_BYTES + S::IBYTES);
+    unsigned* sink = reinterpret_cast<unsigned*>(lds + wid * S::WAVE_BYTES + S::IBYTES + S::JBYTES);
 
     const int sc = lane % WW;
     const int sg = lane / WW;
@@ -587,8 +633,8 @@ __global__ __launch_bounds__(256, MINW) void lk_fast_kernel(LKBatch B, LKDev p) 
         const int ixa = ipx & ~3;
         int jx0 = uni_i(ufloor(nextx - halfWx)) - JM, jy0 = uni_i(ufloor(nexty - halfWy)) - JM;
         int jxa = jx0 & ~3;
-        stage_aligned<S::IPW, S::IPH>(ipair, I, ixa, ipy, lane);
-        stage_aligned<S::JRW, S::JRH>(jreg, J, jxa, jy0, lane);
+        stage_bf<S::IPW, S::IPH>(ipair, sink, I, ixa, ipy, lane);
+        stage_bf<S::JRW, S::JRH>(jreg, sink, J, jxa, jy0, lane);
         u32x2a4 dv[RPG + 1];  // (Ix|Iy) at columns X, X+1 of each row: one dwordx2 load
         {
             const int dpitch = dprev.pitch[level];
@@ -682,7 +728,7 @@ __global__ __launch_bounds__(256, MINW) void lk_fast_kernel(LKBatch B, LKDev p) 
                 jy0 = iny - JM;
                 jxa = jx0 & ~3;
                 wave_lds_sync();
-                stage_aligned<S::JRW, S::JRH>(jreg, J, jxa, jy0, lane);
+                stage_bf<S::JRW, S::JRH>(jreg, sink, J, jxa, jy0, lane);
                 wave_lds_sync();
             }
             a = nextx - inx;
@@ -741,7 +787,7 @@ __global__ __launch_bounds__(256, MINW) void lk_fast_kernel(LKBatch B, LKDev p) 
                 jy0 = iy0 - JM;
                 jxa = jx0 & ~3;
                 wave_lds_sync();
-                stage_aligned<S::JRW, S::JRH>(jreg, J, jxa, jy0, lane);
+                stage_bf<S::JRW, S::JRH>(jreg, sink, J, jxa, jy0, lane);
                 wave_lds_sync();
             }
             float aa = npx - ix0, bb = npy - iy0;
