@@ -108,24 +108,37 @@ def pmc_traffic(kernel_prefix: str):  # substring of the demangled kernel name
 def cpu_baseline(cfg_name: str, seconds: float):
     """The oracle (CPU restatement of the reference's OpenCV path) timed on this
     host on a bounded sample of the same workload: one sequence, frames until
-    `seconds` of CPU work; LK parallel over points (OpenMP), rest single-thread."""
+    `seconds` of CPU work, twice: LK over all host threads (OpenMP, as OpenCV's
+    parallel_for_) and single-threaded; FAST and PnP are
+    single-threaded in both, as in OpenCV."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
-    from oracle_loop import OracleLoop  # noqa: E402  (oracle: cpu_baseline leg only)
+    import oracle as O  # noqa: E402  (oracle: cpu_baseline leg only)
+    from oracle_loop import OracleLoop  # noqa: E402
     from svo_amd.scene import Scene
     W, H, N, _, _ = CONFIGS[cfg_name]
-    sc = Scene(W, H, seed=101)
-    loop = OracleLoop(sc, N, depth_seed=101).init(0)
-    dt, n = 0.0, 0
-    while dt < seconds and n < 5000:
-        frame = sc.frame(n + 1)  # rendered outside the timed region
-        t0 = time.perf_counter()
-        loop.step(n + 1, frame)
-        dt += time.perf_counter() - t0
-        n += 1
     cores = int(os.environ.get("OMP_NUM_THREADS", "0")) or (os.cpu_count() or 1)
+
+    def run(threads, secs):
+        O.set_threads(threads)
+        sc = Scene(W, H, seed=101)
+        loop = OracleLoop(sc, N, depth_seed=101).init(0)
+        dt, n = 0.0, 0
+        while dt < secs and n < 5000:
+            frame = sc.frame(n + 1)  # rendered outside the timed region
+            t0 = time.perf_counter()
+            loop.step(n + 1, frame)
+            dt += time.perf_counter() - t0
+            n += 1
+        return n, dt
+
+    n, dt = run(cores, seconds)
+    n1, dt1 = run(1, seconds)
+    O.set_threads(cores)
     return {"value": round(n / dt, 3), "unit": "frames/s", "cores": cores, "kind": "port",
             "sample": f"{n} frames of one {W}x{H} sequence, {N} feats, {dt:.1f} s; oracle/ C restatement "
-                      f"of the OpenCV path (LK OpenMP over {cores} threads, FAST/PnP single-thread)"}
+                      f"of the OpenCV path (LK OpenMP over {cores} threads, FAST/PnP single-thread)",
+            "single_thread": {"value": round(n1 / dt1, 3), "cores": 1,
+                              "sample": f"{n1} frames, {dt1:.1f} s, everything on one thread"}}
 
 
 def main():
@@ -192,7 +205,7 @@ def main():
     bytes_per_launch = units_per_launch * lk_bytes_per_feature(L)
     lk_avg_s = lk_ms / max(lk_n, 1) / 1e3
     achieved = bytes_per_launch / lk_avg_s / 1e9 if lk_avg_s > 0 else 0.0
-    traffic = pmc_traffic("lk_kernel")
+    traffic = pmc_traffic("lk_fast_kernel<21, 21") or pmc_traffic("lk_kernel")
     dominant = max(phases, key=lambda k: phases[k][0])
     single = None
     if not args.no_single:
@@ -230,7 +243,7 @@ def main():
         "phase_ms_per_step": {k: round(v[0] / K, 4) for k, v in phases.items()},
         "stats_per_step": {k: round(v / K, 3) for k, v in tot.items()},
         "roofline": {
-            "kernel": "lk_kernel (temporal LK, all levels, one wave per feature)",
+            "kernel": "lk_fast_kernel<21,21> (temporal LK, all levels, one wave per feature)",
             "dominant_phase": dominant,
             "bound": "hbm",
             "achieved": round(achieved, 2),

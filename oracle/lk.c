@@ -330,3 +330,10 @@ int svo_oracle_lk(const uint8_t* prev, const uint8_t* next, int w, int h, int st
     free(pp); free(np);
     return ml;
 }
+
+/* Host threads of the LK point loop (OpenMP; OpenCV's parallel_for_). */
+#include <omp.h>
+void svo_oracle_set_threads(int n)
+{
+    omp_set_num_threads(n > 0 ? n : 1);
+}

@@ -150,6 +150,9 @@ int svo_oracle_solve_pnp_ransac(const double* obj_xyz_d, const float* img_xy, in
  * checkSubset): draws `k` distinct indices in [0,count). Returns 1 if found. */
 int svo_oracle_get_subset(uint64_t* rng_state, int count, int k, int* idx);
 
+/* Threads for the LK point loop (OpenMP, like OpenCV's parallel_for_). */
+void svo_oracle_set_threads(int n);
+
 /* cv::triangulatePoints + cv::convertPointsFromHomogeneous (triangulate.c). */
 void svo_oracle_triangulate(const float P1[12], const float P2[12], const float* pts1, const float* pts2,
                             int n, float* xyzw, float* xyz);

@@ -58,6 +58,7 @@ def load():
                                                       C.c_double, _f64p, _f64p, _u8p, _i32p, _i32p]),
             "svo_oracle_get_subset": (C.c_int, [_u64p, C.c_int, C.c_int, _i32p]),
             "svo_oracle_triangulate": (None, [_f32p, _f32p, _f32p, _f32p, C.c_int, _f32p, _f32p]),
+            "svo_oracle_set_threads": (None, [C.c_int]),
         }
         for k, (r, a) in sig.items():
             f = getattr(L, k)
@@ -222,6 +223,11 @@ def solve_pnp_ransac(obj, img, K, iterations=100, reproj=8.0, confidence=0.999):
 
 def update_num_iters(p, ep, model_points, max_iters):
     return load().svo_oracle_ransac_update_num_iters(p, ep, model_points, max_iters)
+
+
+def set_threads(n: int):
+    """Threads of the oracle's LK point loop (OpenMP)."""
+    load().svo_oracle_set_threads(int(n))
 
 
 def triangulate(P1, P2, pts1, pts2):
