@@ -150,6 +150,8 @@ def main():
     ap.add_argument("--config", default="kitti", choices=sorted(CONFIGS))
     ap.add_argument("--threads", type=int, default=0, help="host RANSAC threads (0 = auto)")
     ap.add_argument("--groups", type=int, default=0, help="pipeline slices of the batch (0 = auto)")
+    ap.add_argument("--timing", type=int, default=2, choices=(0, 1, 2),
+                    help="phase events: 1 all phases, 2 only LK/pyramid/FAST (lighter host tail)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-single", action="store_true")
@@ -166,7 +168,7 @@ def main():
     seeds = sequence_seeds(rank, Sq)
     scenes = [Scene(W, H, seed=sd) for sd in seeds]
     cfg = S.FrontendConfig(W, H, scenes[0].K, n_seq=Sq, n_frames=T, n_features=N, max_level=ML,
-                           host_threads=args.threads, timing=1, groups=args.groups)
+                           host_threads=args.threads, timing=args.timing, groups=args.groups)
     fe = S.Frontend(ctx, cfg)
     for s, sc in enumerate(scenes):
         for t in range(T):

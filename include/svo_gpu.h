@@ -205,7 +205,7 @@ typedef struct svo_frontend_config {
     double pnp_confidence;  /* -> 0.999 */
     double K[9];            /* camera matrix (float-rounded, as the Matx33f K) */
     int host_threads;       /* RANSAC host threads; 0 = auto */
-    int timing;             /* 1 = record per-phase HIP events */
+    int timing;             /* 1 = per-phase HIP events; 2 = only LK, pyramid, FAST */
     int groups;             /* pipeline groups: the batch is split into this many
                                slices whose LK / RANSAC overlap (host RANSAC of one
                                slice while the GPU tracks the next); 0 = auto */

@@ -103,7 +103,19 @@ struct FastDetBatch {
     int* n_out;                 // [s]
     size_t npx;
     int nseg, cap;
+    // alternatively (mask null): boxes of +-box_half around box_counts[s] points
+    // of box_pts + 2*s*box_stride, rasterised per tile inside the kernel
+    const float* box_pts = nullptr;
+    const int* box_counts = nullptr;
+    int box_stride = 0;
+    float box_half = 0.f;
+    // scratch for binning the box centres by 16-row band: [s][box_stride] float2
+    // and [s][nbands + 1] band offsets (launch_fast_detect fills them)
+    float* box_binned = nullptr;
+    int* box_band = nullptr;
 };
+// ints of band-offset scratch per sequence for an image of height h
+inline int fast_box_bands(int h) { return (h + 15) / 16 + 1; }
 hipError_t launch_fast_detect(const FastDetBatch& b, int nseq, int w, int h, int threshold, int nonmax,
                               hipStream_t st);
 // Masks for nseq sequences (w*h each): 255 + filled boxes around counts[s] (or n)
@@ -117,6 +129,12 @@ struct DerivDesc {
     int pitch[kMaxLevels];  // elements
 };
 size_t deriv_layout(int w, int h, int nlevels, size_t* off, int* pitch);
+// one level's derivative (level dims lw x lh)
+hipError_t launch_scharr_level(const PyrDesc* d_pyrs, const DerivDesc* d_ders, int nseq, int lw, int lh, int level,
+                               hipStream_t st);
+// pyramid levels 1.. and derivative levels 0.. in one pass per level (pyramid.hip)
+hipError_t launch_pyramid_scharr_batched(const PyrDesc* d_descs, const DerivDesc* d_ders, int nseq, int w, int h,
+                                         int nlevels, hipStream_t st);
 hipError_t launch_scharr(const PyrDesc* d_pyrs, const DerivDesc* d_ders, int nseq, int w, int h, int nlevels,
                          hipStream_t st);
 
@@ -161,6 +179,7 @@ struct PnpBatch {
     uint32_t* bits;  // nullable
     int words_cap;
     int* cnt;        // nullable
+    int mstride = 0; // hypothesis-row stride of hyp/err/bits/cnt per sequence (0: m)
 };
 hipError_t launch_pnp_residuals(const PnpBatch& b, int nseq, int max_n, double fx, double fy, double cx,
                                 double cy, float thresh2, hipStream_t st);

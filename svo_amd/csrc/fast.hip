@@ -226,24 +226,89 @@ __global__ __launch_bounds__(256) void fast_detect_kernel(FastDetBatch B, int th
         }
     }
     __syncthreads();
-    for (int k = tid; k < FD_SH * FD_SW; k += 256) {
+    // phase A: segment test for every score-region pixel; corners are queued
+    // (wave-aggregated LDS append) so that the expensive cornerScore runs only on
+    // them with full waves instead of in nearly every (divergent) wave
+    __shared__ uint16_t CQ[FD_SH * FD_SW];
+    __shared__ int ncq;
+    if (tid == 0) ncq = 0;
+    __syncthreads();
+    for (int base = 0; base < FD_SH * FD_SW; base += 256) {
+        const int k = base + tid;
         const int r = k / FD_SW, c = k - r * FD_SW;
         const int y = y0 - 1 + r, x = x0 - 1 + c;
-        uint16_t out = 0;
-        if (x >= 3 && x < w - 3 && y >= 3 && y < h - 3) {
+        bool corner = false;
+        if (k < FD_SH * FD_SW && x >= 3 && x < w - 3 && y >= 3 && y < h - 3) {
             const int ty = r + 3, tx = c + 3;  // image-tile coords of (x, y)
             const int v = T[ty][tx];
-            int ring[16];
             unsigned bright = 0, dark = 0;
 #pragma unroll
             for (int q = 0; q < 16; q++) {
-                ring[q] = T[ty + c_ring[q][1]][tx + c_ring[q][0]];
-                bright |= (unsigned)(ring[q] > v + threshold) << q;
-                dark |= (unsigned)(ring[q] < v - threshold) << q;
+                const int rv = T[ty + c_ring[q][1]][tx + c_ring[q][0]];
+                bright |= (unsigned)(rv > v + threshold) << q;
+                dark |= (unsigned)(rv < v - threshold) << q;
             }
-            if (run9(bright) || run9(dark)) out = (uint16_t)(0x100 | (nonmax ? corner_score16(v, ring, threshold) : 0));
+            corner = run9(bright) || run9(dark);
         }
-        SC[r][c] = out;
+        if (k < FD_SH * FD_SW) SC[r][c] = corner ? 0x100 : 0;
+        if (nonmax) {
+            const unsigned long long bal = __ballot(corner);
+            if (bal) {
+                int qb = 0;
+                if ((tid & 63) == 0) qb = atomicAdd(&ncq, __popcll(bal));
+                qb = __builtin_amdgcn_readfirstlane(qb);
+                if (corner) {
+                    const int pos = qb + __popcll(bal & ((1ull << (tid & 63)) - 1ull));
+                    CQ[pos] = (uint16_t)k;
+                }
+            }
+        }
+    }
+    __syncthreads();
+    // phase B: cornerScore of the queued corners, dense
+    if (nonmax) {
+        const int nq = ncq;
+        for (int i = tid; i < nq; i += 256) {
+            const int k = CQ[i];
+            const int r = k / FD_SW, c = k - r * FD_SW;
+            const int ty = r + 3, tx = c + 3;
+            const int v = T[ty][tx];
+            int ring[16];
+#pragma unroll
+            for (int q = 0; q < 16; q++) ring[q] = T[ty + c_ring[q][1]][tx + c_ring[q][0]];
+            SC[r][c] = (uint16_t)(0x100 | corner_score16(v, ring, threshold));
+        }
+    }
+    // tile mask from the previous frame's feature boxes (R:src/tracking.cpp:76-79,
+    // cv::rectangle FILLED with cvRound corners, clipped): one bit per pixel of
+    // the 64x16 tile, cleared by every box that overlaps it -- no W x H mask in HBM
+    __shared__ unsigned long long TM[FD_TY];
+    const bool boxes = B.box_pts != nullptr;
+    if (boxes) {
+        if (tid < FD_TY) TM[tid] = ~0ull;
+        __syncthreads();
+        // only the bands whose box centres can reach this tile
+        const int nb = (h + 15) / 16;
+        const int* __restrict__ band = B.box_band + seq * (size_t)(nb + 1);
+        const int b0 = max(0, (int)floorf((y0 - B.box_half - 1.f) / 16.f));
+        const int b1 = min(nb - 1, (int)floorf((y0 + FD_TY + B.box_half + 1.f) / 16.f));
+        const int i0 = band[b0], i1 = band[b1 + 1];
+        const float* __restrict__ pts = B.box_binned + 2 * seq * (size_t)B.box_stride;
+        for (int i = i0 + tid; i < i1; i += 256) {
+            const float px = pts[2 * i], py = pts[2 * i + 1];
+            const int xa = (int)__builtin_rintf(px - B.box_half), ya = (int)__builtin_rintf(py - B.box_half);
+            const int xb = (int)__builtin_rintf(px + B.box_half), yb = (int)__builtin_rintf(py + B.box_half);
+            int xl = min(xa, xb), xr = max(xa, xb), yt = min(ya, yb), yd = max(ya, yb);
+            xl = max(xl, max(0, x0));
+            xr = min(xr, min(w - 1, x0 + FD_TX - 1));
+            yt = max(yt, max(0, y0));
+            yd = min(yd, min(h - 1, y0 + FD_TY - 1));
+            if (xl > xr || yt > yd) continue;
+            const int c0 = xl - x0, c1 = xr - x0;  // 0..63
+            const unsigned long long span =
+                (c1 - c0 == 63) ? ~0ull : (((1ull << (c1 - c0 + 1)) - 1ull) << c0);
+            for (int y = yt; y <= yd; y++) atomicAnd(&TM[y - y0], ~span);
+        }
     }
     __syncthreads();
     const int lane = tid & 63, wv = tid >> 6;
@@ -264,11 +329,48 @@ __global__ __launch_bounds__(256) void fast_detect_kernel(FastDetBatch B, int th
                    s > (SC[rr + 1][c] & 0xFF) && s > (SC[rr + 1][c + 1] & 0xFF);
         }
         if (keep && mask && mask[(size_t)y * w + x] == 0) keep = false;
+        if (boxes && !((TM[r] >> lane) & 1ull)) keep = false;
         const unsigned long long bal = __ballot(keep);
         if (lane == 0) {
             B.bits[(seq * h + y) * B.nseg + blockIdx.x] = bal;
             if (bal) atomicAdd(&B.rowcnt[seq * h + y], __popcll(bal));
         }
+    }
+}
+
+// Box centres of one sequence binned by 16-row band (counting sort; order within
+// a band is irrelevant: the mask is an AND of boxes). One block per sequence.
+__global__ __launch_bounds__(256) void box_bin_kernel(FastDetBatch B, int h) {
+    const size_t seq = blockIdx.x;
+    const int nb = (h + 15) / 16;
+    __shared__ int cnt[1024], cur[1024];
+    const int n = B.box_counts[seq];
+    const float* __restrict__ pts = B.box_pts + 2 * seq * (size_t)B.box_stride;
+    float* __restrict__ outp = B.box_binned + 2 * seq * (size_t)B.box_stride;
+    int* __restrict__ band = B.box_band + seq * (size_t)(nb + 1);
+    for (int b = threadIdx.x; b < nb; b += 256) cnt[b] = 0;
+    __syncthreads();
+    auto band_of = [&](float y) {
+        int b = (int)floorf(y / 16.f);
+        return b < 0 ? 0 : b >= nb ? nb - 1 : b;
+    };
+    for (int i = threadIdx.x; i < n; i += 256) atomicAdd(&cnt[band_of(pts[2 * i + 1])], 1);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int acc = 0;
+        for (int b = 0; b < nb; b++) {
+            band[b] = acc;
+            cur[b] = acc;
+            acc += cnt[b];
+        }
+        band[nb] = acc;
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < n; i += 256) {
+        const float x = pts[2 * i], y = pts[2 * i + 1];
+        const int pos = atomicAdd(&cur[band_of(y)], 1);
+        outp[2 * pos] = x;
+        outp[2 * pos + 1] = y;
     }
 }
 
@@ -384,6 +486,10 @@ hipError_t launch_fast_detect(const FastDetBatch& b, int nseq, int w, int h, int
                               hipStream_t st) {
     hipError_t e = hipMemsetAsync(b.rowcnt, 0, sizeof(int) * (size_t)h * nseq, st);
     if (e != hipSuccess) return e;
+    if (b.box_pts) {
+        if ((h + 15) / 16 > 1024) return hipErrorInvalidValue;
+        hipLaunchKernelGGL(box_bin_kernel, dim3(nseq), dim3(256), 0, st, b, h);
+    }
     dim3 grid((w + FD_TX - 1) / FD_TX, (h + FD_TY - 1) / FD_TY, nseq);
     hipLaunchKernelGGL(fast_detect_kernel, grid, dim3(256), 0, st, b, threshold, nonmax);
     hipLaunchKernelGGL(fast_scan_kernel, dim3(nseq), dim3(1024), 0, st, b, h);

@@ -124,7 +124,8 @@ struct svo_frontend {
     DerivDesc* d_der = nullptr;      // [2][s]
     // device state (one allocation)
     void* dmem = nullptr;
-    float *xyA, *next_xy, *xyB, *obj, *kps, *cand;
+    float *xyA, *next_xy, *xyB, *obj, *kps, *cand, *box_binned;
+    int* box_band;
     int *midA, *midB, *nA, *nB, *iters, *kn, *bn, *map_n, *rowcnt, *rowoff, *scr, *cnt, *added, *seed_d;
     unsigned long long* fbits;
     long long* itsum;
@@ -141,6 +142,7 @@ struct svo_frontend {
     std::vector<RansacSeq> rs;
     std::vector<double> pose;  // [s][6]
     bool fits_pending = false;
+    bool stats_pending = false;
     int pyr_ready = -1;  // frame index whose pyramid + Scharr were built ahead
     hipEvent_t ev_stats = nullptr;  // SQPnP statistics of the last step on the host
     Pool* pool = nullptr;
@@ -185,6 +187,8 @@ void ph_fold(svo_frontend* fe, bool wait) {
 void ph_begin(svo_frontend* fe, int ph, hipStream_t st, int* slot) {
     *slot = -1;
     if (!fe->cfg.timing) return;
+    // timing 2: only the big phases (each event pair costs a few us of host time)
+    if (fe->cfg.timing == 2 && ph != PH_LK && ph != PH_PYR && ph != PH_FAST) return;
     const int sl = fe->ev_used;
     for (auto& p : fe->pending)  // ring wrapped onto a pair still in flight
         if (p.second == sl) ph_fold(fe, true);
@@ -209,8 +213,16 @@ T* carve(char*& p, size_t count) {
 int fe_fast_and_bucket(svo_frontend* fe, const PyrDesc* descs_cur, bool use_mask, hipStream_t st) {
     svo_ctx* ctx = fe->ctx;
     int slot;
-    FastDetBatch fb{descs_cur, use_mask ? fe->mask : nullptr, fe->fbits, fe->rowcnt, fe->rowoff,
+    FastDetBatch fb{descs_cur, nullptr, fe->fbits, fe->rowcnt, fe->rowoff,
                     (svo_keypoint*)fe->kps, fe->kn, fe->npx, (fe->W + 63) / 64, fe->KCAP};
+    if (use_mask) {  // boxes around the previous frame's features, rasterised per FAST tile
+        fb.box_pts = fe->xyA;
+        fb.box_counts = fe->nA;
+        fb.box_stride = fe->CAP;
+        fb.box_half = fe->cfg.mask_half;
+        fb.box_binned = fe->box_binned;
+        fb.box_band = fe->box_band;
+    }
     ph_begin(fe, PH_FAST, st, &slot);
     SVO_HIP(ctx, launch_fast_detect(fb, fe->S, fe->W, fe->H, fe->cfg.fast_threshold, fe->cfg.fast_nonmax, st));
     ph_end(fe, st, slot);
@@ -249,6 +261,20 @@ int fe_append(svo_frontend* fe, int t, int g0, int n, hipStream_t st) {
     ph_begin(fe, PH_APPEND, st, &slot);
     SVO_HIP(ctx, launch_append(ab, n, st));
     ph_end(fe, st, slot);
+    return SVO_OK;
+}
+
+// Queue the SQPnP sufficient statistics of the last step's RANSAC inliers (the
+// bits are on the device since that step) on the FAST stream, then their D2H.
+int fe_queue_stats(svo_frontend* fe) {
+    if (!fe->stats_pending) return SVO_OK;
+    svo_ctx* ctx = fe->ctx;
+    hipStream_t sf = fe->st_fast;
+    SVO_HIP(ctx, launch_suffstats(fe->obj, fe->xyB, fe->nB, fe->CAP, fe->bits_best, fe->WORDS, fe->S, fe->cfg.K,
+                                  fe->stats, sf));
+    SVO_HIP(ctx, hipMemcpyAsync(fe->h_stats, fe->stats, sizeof(double) * 60 * fe->S, hipMemcpyDeviceToHost, sf));
+    SVO_HIP(ctx, hipEventRecord(fe->ev_stats, sf));
+    fe->stats_pending = false;
     return SVO_OK;
 }
 
@@ -341,6 +367,8 @@ int svo_frontend_create(svo_ctx* ctx, const svo_frontend_config* cfg, svo_fronte
         add(sizeof(double) * 12 * (size_t)S * kRansacChunk);
         add(sizeof(double) * 9 * (size_t)S * fe->T);
         add(sizeof(double) * 60 * (size_t)S);
+        add(sizeof(float) * 2 * (size_t)S * CAP);               // box centres binned by band
+        add(sizeof(int) * (size_t)S * fast_box_bands(c.height));
         add(4096);
         bytes = (size_t)p;
     }
@@ -381,6 +409,8 @@ int svo_frontend_create(svo_ctx* ctx, const svo_frontend_config* cfg, svo_fronte
         fe->hyps = carve<double>(p, 12 * (size_t)S * kRansacChunk);
         fe->rot_d = carve<double>(p, 9 * (size_t)S * fe->T);
         fe->stats = carve<double>(p, 60 * (size_t)S);
+        fe->box_binned = carve<float>(p, 2 * (size_t)S * CAP);
+        fe->box_band = carve<int>(p, (size_t)S * fast_box_bands(c.height));
     }
     (void)hipMemsetAsync(fe->dmem, 0, bytes, ctx->stream);
     // host mirrors
@@ -540,11 +570,12 @@ int svo_frontend_init(svo_frontend* fe, int t0) {
     if (!fe || t0 < 0) return SVO_ERR_ARG;
     fe->pyr_ready = -1;
     fe->fits_pending = false;
+    fe->stats_pending = false;
     svo_ctx* ctx = fe->ctx;
     const int S = fe->S;
     const PyrDesc* dcur = fe->d_desc + (size_t)(t0 % fe->T) * S;
-    SVO_HIP(ctx, launch_pyramid_batched(dcur, S, fe->W, fe->H, fe->nlev, ctx->stream));
-    SVO_HIP(ctx, launch_scharr(dcur, fe->d_der + (size_t)(t0 & 1) * S, S, fe->W, fe->H, fe->nlev, ctx->stream));
+    SVO_HIP(ctx, launch_pyramid_scharr_batched(dcur, fe->d_der + (size_t)(t0 & 1) * S, S, fe->W, fe->H, fe->nlev,
+                                               ctx->stream));
     SVO_HIP(ctx, hipMemsetAsync(fe->nA, 0, sizeof(int) * S, ctx->stream));
     SVO_HIP(ctx, hipMemsetAsync(fe->map_n, 0, sizeof(int) * S, ctx->stream));
     int rc = fe_fast_and_bucket(fe, dcur, false, ctx->stream);
@@ -587,8 +618,8 @@ int svo_frontend_step(svo_frontend* fe, int t, svo_frontend_stats* stats) {
     //    t is the prev image of the next step; OpenCV recomputes it per call)
     if (fe->pyr_ready != t) {
         ph_begin(fe, PH_PYR, st0, &slot);
-        SVO_HIP(ctx, launch_pyramid_batched(dcur, S, fe->W, fe->H, fe->nlev, st0));
-        SVO_HIP(ctx, launch_scharr(dcur, fe->d_der + (size_t)(t & 1) * S, S, fe->W, fe->H, fe->nlev, st0));
+        SVO_HIP(ctx, launch_pyramid_scharr_batched(dcur, fe->d_der + (size_t)(t & 1) * S, S, fe->W, fe->H, fe->nlev,
+                                                   st0));
         ph_end(fe, st0, slot);
     }
     SVO_HIP(ctx, hipEventRecord(ev_pyr, st0));
@@ -629,12 +660,15 @@ int svo_frontend_step(svo_frontend* fe, int t, svo_frontend_stats* stats) {
         const PyrDesc* dnext = fe->d_desc + (size_t)(tn % fe->T) * S;
         SVO_HIP(ctx, hipStreamWaitEvent(st0, fe->ev_sync[2 + 2 * (G - 1)], 0));
         ph_begin(fe, PH_PYR, st0, &slot);
-        SVO_HIP(ctx, launch_pyramid_batched(dnext, S, fe->W, fe->H, fe->nlev, st0));
-        SVO_HIP(ctx, launch_scharr(dnext, fe->d_der + (size_t)(tn & 1) * S, S, fe->W, fe->H, fe->nlev, st0));
+        SVO_HIP(ctx, launch_pyramid_scharr_batched(dnext, fe->d_der + (size_t)(tn & 1) * S, S, fe->W, fe->H,
+                                                   fe->nlev, st0));
         ph_end(fe, st0, slot);
         fe->pyr_ready = tn;
     }
     TP("lk+pyr enqueued");
+    // 3a'. the previous step's SQPnP statistics (runs beside LK)
+    int rq = fe_queue_stats(fe);
+    if (rq) return rq;
     // 3a. the previous step's final pose fits, deferred to here: the host does
     //     them while the GPU tracks this frame (before this step's D2H copies
     //     are queued: the fits read the previous frame's host mirrors)
@@ -672,9 +706,6 @@ int svo_frontend_step(svo_frontend* fe, int t, svo_frontend_stats* stats) {
     //     the GPU while the host solves RANSAC (and does not slow LK down)
     hipStream_t sf = fe->st_fast;
     SVO_HIP(ctx, hipStreamWaitEvent(sf, fe->ev_sync[2 + 2 * (G - 1)], 0));
-    ph_begin(fe, PH_MASK, sf, &slot);
-    SVO_HIP(ctx, launch_mask_boxes(fe->W, fe->H, fe->xyA, fe->nA, max_prev, CAP, S, c.mask_half, fe->mask, sf));
-    ph_end(fe, sf, slot);
     int rc = fe_fast_and_bucket(fe, dcur, true, sf);
     if (rc) return rc;
     SVO_HIP(ctx, hipEventRecord(ev_fast, sf));
@@ -725,20 +756,21 @@ int svo_frontend_step(svo_frontend* fe, int t, svo_frontend_stats* stats) {
             }
             SVO_HIP(ctx, hipMemcpyAsync(fe->hyps + 12 * (size_t)a * kRansacChunk, fe->h_hyps + 12 * (size_t)a * kRansacChunk,
                                         sizeof(double) * 12 * n * kRansacChunk, hipMemcpyHostToDevice, sg));
-            // hypotheses live at stride kRansacChunk: score all kRansacChunk rows
-            // (rows beyond a sequence's own count are ignored by consume())
+            // hypotheses live at stride kRansacChunk; score (and copy back) only the
+            // mmax rows of this round (rows beyond a sequence's own count are ignored)
             PnpBatch pb{fe->obj + 3 * (size_t)a * CAP, fe->xyB + 2 * (size_t)a * CAP, fe->nB + a, 0, CAP,
-                        fe->hyps + 12 * (size_t)a * kRansacChunk, kRansacChunk, nullptr,
+                        fe->hyps + 12 * (size_t)a * kRansacChunk, mmax, nullptr,
                         fe->bits_all + (size_t)a * kRansacChunk * fe->WORDS, fe->WORDS, fe->cnt + (size_t)a * kRansacChunk};
+            pb.mstride = kRansacChunk;
             ph_begin(fe, PH_PNP, sg, &slot);
             SVO_HIP(ctx, launch_pnp_residuals(pb, n, max_b, c.K[0], c.K[4], c.K[2], c.K[5], thr, sg));
             ph_end(fe, sg, slot);
             SVO_HIP(ctx, hipMemcpyAsync(fe->h_cnt + (size_t)a * kRansacChunk, fe->cnt + (size_t)a * kRansacChunk,
                                         sizeof(int) * n * kRansacChunk, hipMemcpyDeviceToHost, sg));
-            SVO_HIP(ctx, hipMemcpyAsync(fe->h_bits + (size_t)a * kRansacChunk * fe->WORDS,
-                                        fe->bits_all + (size_t)a * kRansacChunk * fe->WORDS,
-                                        sizeof(uint32_t) * n * kRansacChunk * fe->WORDS, hipMemcpyDeviceToHost, sg));
-            tw = clk::now();
+            const size_t rowb = sizeof(uint32_t) * (size_t)kRansacChunk * fe->WORDS;
+            SVO_HIP(ctx, hipMemcpy2DAsync(fe->h_bits + (size_t)a * kRansacChunk * fe->WORDS, rowb,
+                                          fe->bits_all + (size_t)a * kRansacChunk * fe->WORDS, rowb,
+                                          sizeof(uint32_t) * (size_t)mmax * fe->WORDS, n, hipMemcpyDeviceToHost, sg));
             TP("scoring enqueued");
             SVO_HIP(ctx, hipStreamSynchronize(sg));
             ms_wait += ms_since(tw);
@@ -771,14 +803,8 @@ int svo_frontend_step(svo_frontend* fe, int t, svo_frontend_stats* stats) {
         SVO_HIP(ctx, hipMemcpyAsync(fe->bits_best + (size_t)a * fe->WORDS, fe->h_best + (size_t)a * fe->WORDS,
                                     sizeof(uint32_t) * n * fe->WORDS, hipMemcpyHostToDevice, sg));
         // the SQPnP statistics only feed the pose fits, which run during the next
-        // step: off the critical path, on the FAST stream
-        SVO_HIP(ctx, hipEventRecord(fe->ev_sync[2 + 2 * G + g], sg));
-        SVO_HIP(ctx, hipStreamWaitEvent(sf, fe->ev_sync[2 + 2 * G + g], 0));
-        SVO_HIP(ctx, launch_suffstats(fe->obj + 3 * (size_t)a * CAP, fe->xyB + 2 * (size_t)a * CAP, fe->nB + a, CAP,
-                                      fe->bits_best + (size_t)a * fe->WORDS, fe->WORDS, n, c.K,
-                                      fe->stats + 60 * (size_t)a, sf));
-        SVO_HIP(ctx, hipMemcpyAsync(fe->h_stats + 60 * (size_t)a, fe->stats + 60 * (size_t)a, sizeof(double) * 60 * n,
-                                    hipMemcpyDeviceToHost, sf));
+        // step's LK: they are queued then (fe_queue_stats), off the critical path
+        fe->stats_pending = true;
         // the mask (reads xyA) and FAST (writes kps) must be done before xyA is rewritten / kps read
         SVO_HIP(ctx, hipStreamWaitEvent(sg, ev_fast, 0));
         CompactBatch cb2{fe->nB + a, nullptr, fe->bits_best + (size_t)a * fe->WORDS, fe->WORDS,
@@ -793,7 +819,6 @@ int svo_frontend_step(svo_frontend* fe, int t, svo_frontend_stats* stats) {
         SVO_HIP(ctx, hipMemcpyAsync(fe->h_added + a, fe->added + a, sizeof(int) * n, hipMemcpyDeviceToHost, sg));
     }
     fe->fits_pending = true;  // statistics land with the stream syncs below
-    SVO_HIP(ctx, hipEventRecord(fe->ev_stats, sf));
     TP("tail enqueued");
     // only the slices' streams: the statistics (FAST stream) and the next
     // frame's pyramid (main stream) keep running into the next step
@@ -825,6 +850,8 @@ int svo_frontend_step(svo_frontend* fe, int t, svo_frontend_stats* stats) {
 int svo_frontend_synchronize(svo_frontend* fe) {
     if (!fe) return SVO_ERR_ARG;
     svo_ctx* ctx = fe->ctx;
+    int rq = fe_queue_stats(fe);
+    if (rq) return rq;
     for (auto& g : fe->gst) SVO_HIP(ctx, hipStreamSynchronize(g));
     if (fe->st_fast) SVO_HIP(ctx, hipStreamSynchronize(fe->st_fast));
     SVO_HIP(ctx, hipStreamSynchronize(ctx->stream));
@@ -834,6 +861,8 @@ int svo_frontend_synchronize(svo_frontend* fe) {
 
 int svo_frontend_pose(svo_frontend* fe, int seq, double rvec[3], double tvec[3]) {
     if (!fe || seq < 0 || seq >= fe->S) return SVO_ERR_ARG;
+    int rq = fe_queue_stats(fe);
+    if (rq) return rq;
     fe_finish_fits(fe);
     std::memcpy(rvec, &fe->pose[6 * (size_t)seq], sizeof(double) * 3);
     std::memcpy(tvec, &fe->pose[6 * (size_t)seq + 3], sizeof(double) * 3);

@@ -25,7 +25,8 @@ __global__ __launch_bounds__(256) void pnp_residual_kernel(PnpBatch B, double fx
     const int i = blockIdx.x * 256 + threadIdx.x;
     const float* __restrict__ obj = B.obj + 3 * (size_t)seq * B.cap;
     const float* __restrict__ img = B.img + 2 * (size_t)seq * B.cap;
-    const double* R = B.hyp + 12 * ((size_t)seq * B.m + h);  // uniform -> scalar loads
+    const int ms = B.mstride ? B.mstride : B.m;
+    const double* R = B.hyp + 12 * ((size_t)seq * ms + h);  // uniform -> scalar loads
     bool inl = false;
     if (i < n) {
         const double X = obj[3 * i], Y = obj[3 * i + 1], Z = obj[3 * i + 2];
@@ -40,7 +41,7 @@ __global__ __launch_bounds__(256) void pnp_residual_kernel(PnpBatch B, double fx
         float s = 0.f;
         s += dx * dx;
         s += dy * dy;
-        if (B.err) B.err[((size_t)seq * B.m + h) * B.cap + i] = s;
+        if (B.err) B.err[((size_t)seq * ms + h) * B.cap + i] = s;
         inl = s <= thresh2;
     }
     const unsigned long long bal = __ballot(inl);
@@ -48,11 +49,11 @@ __global__ __launch_bounds__(256) void pnp_residual_kernel(PnpBatch B, double fx
     const int words = (n + 31) >> 5;
     const int w0 = (blockIdx.x * 256 + (threadIdx.x & ~63)) >> 5;
     if (B.bits) {
-        uint32_t* bits = B.bits + ((size_t)seq * B.m + h) * B.words_cap;
+        uint32_t* bits = B.bits + ((size_t)seq * ms + h) * B.words_cap;
         if (lane == 0 && w0 < words) bits[w0] = (uint32_t)bal;
         if (lane == 1 && w0 + 1 < words) bits[w0 + 1] = (uint32_t)(bal >> 32);
     }
-    if (B.cnt && lane == 0 && bal) atomicAdd(&B.cnt[(size_t)seq * B.m + h], __popcll(bal));
+    if (B.cnt && lane == 0 && bal) atomicAdd(&B.cnt[(size_t)seq * ms + h], __popcll(bal));
 }
 
 }  // namespace
@@ -61,7 +62,8 @@ hipError_t launch_pnp_residuals(const PnpBatch& b, int nseq, int max_n, double f
                                 double cy, float thresh2, hipStream_t st) {
     if (max_n <= 0 || b.m <= 0 || nseq <= 0) return hipSuccess;
     if (b.cnt) {
-        hipError_t e = hipMemsetAsync(b.cnt, 0, sizeof(int) * (size_t)b.m * nseq, st);
+        const int ms = b.mstride ? b.mstride : b.m;
+        hipError_t e = hipMemsetAsync(b.cnt, 0, sizeof(int) * (size_t)ms * nseq, st);
         if (e != hipSuccess) return e;
     }
     dim3 grid((max_n + 255) / 256, b.m, nseq);

@@ -109,3 +109,109 @@ hipError_t launch_pyramid(const svo_image* img, int first_level, hipStream_t st)
 }
 
 }  // namespace svo
+
+// ---------------------------------------------------------------------------
+// Fused pyrDown + Scharr: one pass over level l writes level l+1 of the image
+// pyramid and level l of the derivative pyramid (scharr.hip's packed layout).
+// A block owns a 64x16 tile of level l+1, i.e. the 128x32 pixels of level l
+// under it; the staged 136x36 level-l tile (dword loads; REFLECT_101 at the
+// borders, which both operators use) feeds both outputs, so level l is read
+// once instead of twice. Bit-exact integer arithmetic as the separate kernels.
+namespace svo {
+
+namespace {
+
+constexpr int FS_IW = 2 * PD_TX + 8;  // 136 staged columns: sx0 - 2 .. sx0 + 133 (dword aligned)
+constexpr int FS_IH = PD_IH;          // 36 rows
+
+__global__ __launch_bounds__(256) void pyr_scharr_kernel(const PyrDesc* __restrict__ descs,
+                                                         const DerivDesc* __restrict__ ders, int level) {
+    const PyrDesc& P = descs[blockIdx.z];
+    const ImgLevel& s = P.lv[level];
+    const ImgLevel& d = P.lv[level + 1];
+    const int x0 = blockIdx.x * PD_TX, y0 = blockIdx.y * PD_TY;
+    const int sx0 = 2 * x0 - 2, sy0 = 2 * y0 - 2;
+    const int xa = sx0 - 2;  // multiple of 4 (x0 is a multiple of 64)
+    __shared__ __attribute__((aligned(16))) uint8_t T[FS_IH][FS_IW];
+    __shared__ int H[PD_IH][PD_TX + 1];
+    const int tid = threadIdx.x;
+    const int sw = s.w, sh = s.h;
+    const bool interior = xa >= 0 && sy0 >= 0 && xa + FS_IW <= sw && sy0 + FS_IH <= sh;
+    if (interior) {
+        constexpr int DW = FS_IW / 4;  // 34 dwords per row
+        for (int k = tid; k < FS_IH * DW; k += 256) {
+            const int r = k / DW, c4 = k - r * DW;
+            *reinterpret_cast<uint32_t*>(&T[r][4 * c4]) =
+                *reinterpret_cast<const uint32_t*>(s.data + (size_t)(sy0 + r) * s.pitch + xa + 4 * c4);
+        }
+    } else {
+        for (int k = tid; k < FS_IH * FS_IW; k += 256) {
+            const int r = k / FS_IW, c = k - r * FS_IW;
+            T[r][c] = s.data[(size_t)refl101(sy0 + r, sh) * s.pitch + refl101(xa + c, sw)];
+        }
+    }
+    __syncthreads();
+    // ---- pyrDown: T column 2 + j holds level-l column sx0 + j ----
+    for (int k = tid; k < PD_IH * PD_TX; k += 256) {
+        const int r = k >> 6, c = k & 63;
+        const uint8_t* t = &T[r][2 * c + 2];
+        H[r][c] = t[0] + 4 * t[1] + 6 * t[2] + 4 * t[3] + t[4];
+    }
+    // ---- Scharr of level l pixels (2x0 + i, 2y0 + j), i < 128, j < 32: T[2 + j][4 + i] ----
+    {
+        uint32_t* __restrict__ out = ders[blockIdx.z].data[level];
+        const int op = ders[blockIdx.z].pitch[level];
+        const int i = tid & 127, j0 = (tid >> 7) * 16;
+        const int x = 2 * x0 + i;
+        if (x < sw) {
+            const int tc = 4 + i;
+            int tl = T[1 + j0][tc - 1], tm = T[1 + j0][tc], tr = T[1 + j0][tc + 1];
+            int ml = T[2 + j0][tc - 1], mm = T[2 + j0][tc], mr = T[2 + j0][tc + 1];
+#pragma unroll 4
+            for (int jj = 0; jj < 16; jj++) {
+                const int y = 2 * y0 + j0 + jj;
+                const int br = T[3 + j0 + jj][tc + 1], bm = T[3 + j0 + jj][tc], bl = T[3 + j0 + jj][tc - 1];
+                if (y < sh) {
+                    const int ix = (3 * (tr + br) + 10 * mr) - (3 * (tl + bl) + 10 * ml);
+                    const int iy = 3 * ((br - tr) + (bl - tl)) + 10 * (bm - tm);
+                    out[(size_t)y * op + x] = ((unsigned)iy << 16) | ((unsigned)ix & 0xFFFFu);
+                }
+                tl = ml; tm = mm; tr = mr;
+                ml = bl; mm = bm; mr = br;
+            }
+        }
+    }
+    __syncthreads();
+    const int c = tid & 63;
+    const int x = x0 + c;
+    if (x >= d.w) return;
+    uint8_t* __restrict__ dst = const_cast<uint8_t*>(d.data);
+#pragma unroll
+    for (int i = 0; i < PD_TY / 4; i++) {
+        const int r = (tid >> 6) * (PD_TY / 4) + i;
+        const int y = y0 + r;
+        if (y < d.h) {
+            const int sum = H[2 * r][c] + 4 * H[2 * r + 1][c] + 6 * H[2 * r + 2][c] + 4 * H[2 * r + 3][c] +
+                            H[2 * r + 4][c];
+            dst[(size_t)y * d.pitch + x] = (uint8_t)((sum + 128) >> 8);
+        }
+    }
+}
+
+}  // namespace
+
+hipError_t launch_pyramid_scharr_batched(const PyrDesc* d_descs, const DerivDesc* d_ders, int nseq, int w, int h,
+                                         int nlevels, hipStream_t st) {
+    int lw = w, lh = h;
+    for (int l = 0; l + 1 < nlevels; l++) {
+        const int nw = (lw + 1) / 2, nh = (lh + 1) / 2;
+        dim3 grid((nw + PD_TX - 1) / PD_TX, (nh + PD_TY - 1) / PD_TY, nseq);
+        hipLaunchKernelGGL(pyr_scharr_kernel, grid, dim3(256), 0, st, d_descs, d_ders, l);
+        lw = nw;
+        lh = nh;
+    }
+    // the coarsest level's derivative (no pyrDown after it)
+    return launch_scharr_level(d_descs, d_ders, nseq, lw, lh, nlevels - 1, st);
+}
+
+}  // namespace svo

@@ -79,6 +79,13 @@ hipError_t launch_scharr(const PyrDesc* d_pyrs, const DerivDesc* d_ders, int nse
     return hipGetLastError();
 }
 
+hipError_t launch_scharr_level(const PyrDesc* d_pyrs, const DerivDesc* d_ders, int nseq, int lw, int lh, int level,
+                               hipStream_t st) {
+    dim3 grid((lw + SC_TX - 1) / SC_TX, (lh + SC_TY - 1) / SC_TY, nseq);
+    hipLaunchKernelGGL(scharr_kernel, grid, dim3(256), 0, st, d_pyrs, d_ders, level);
+    return hipGetLastError();
+}
+
 size_t deriv_layout(int w, int h, int nlevels, size_t* off, int* pitch) {
     size_t total = 0;
     int lw = w, lh = h;
