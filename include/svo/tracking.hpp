@@ -22,7 +22,7 @@ struct Config {
     double fx = 0, fy = 0, cx = 0, cy = 0, bf = 0;
     int start_frame = 0, end_frame = 0;
     bool show_gt = false;
-    bool use_orb = false;  // ORB is not built (§8f-4): Tracking throws if set
+    bool use_orb = false;  // R:configs/config.yaml:20 ships 1; svo_orb_detect then replaces FAST
     struct {
         int nfeatures = 500;
         float scale_factor = 1.2f;
@@ -94,6 +94,9 @@ public:
     Tracking& operator=(const Tracking&) = delete;
 
     void startStereo();
+
+    // pyrDown levels kept per device image: maxLevel of both LK calls (R:src/tracking.cpp:104,163)
+    static constexpr int kImageLevels = 3;
 
     // startStereo split into its two parts, for callers that drive frames one
     // at a time: the first keyframe, then one loop iteration per call. Both

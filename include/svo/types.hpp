@@ -50,12 +50,16 @@ public:
     GrayImage() = default;
     GrayImage(int w, int h);
     static GrayImage copyFrom(const uint8_t* data, int w, int h, int stride);
+    // The loader's imread + cvtColor(COLOR_BGR2GRAY) (R:include/async_image_loader.h:63-69)
+    // done on the device: the grey image is born device-resident (svo_image_upload_bgr,
+    // pyramid of max_level levels) and its host pixels are downloaded on first data().
+    static GrayImage fromBGR(svo_ctx* ctx, const uint8_t* bgr, int w, int h, int stride, int max_level);
 
     int cols() const { return b_ ? b_->w : 0; }
     int rows() const { return b_ ? b_->h : 0; }
     bool empty() const { return !b_ || b_->w == 0; }
-    uint8_t* data() { return b_ ? b_->px.data() : nullptr; }
-    const uint8_t* data() const { return b_ ? b_->px.data() : nullptr; }
+    uint8_t* data() { return b_ ? b_->host() : nullptr; }
+    const uint8_t* data() const { return b_ ? b_->host() : nullptr; }
 
     // Device image with >= max_level pyrDown levels (uploaded once per image).
     svo_image* device(svo_ctx* ctx, int max_level) const;
@@ -65,10 +69,12 @@ public:
 private:
     struct Body {
         std::vector<uint8_t> px;
+        bool px_valid = true;  // false while only the device copy holds the pixels
         int w = 0, h = 0;
         svo_ctx* ctx = nullptr;
         svo_image* dev = nullptr;
         int levels = -1;
+        uint8_t* host();
         ~Body();
     };
     std::shared_ptr<Body> b_;

@@ -79,6 +79,12 @@ int svo_image_create(svo_ctx* ctx, int w, int h, int max_levels, svo_image** out
 void svo_image_destroy(svo_ctx* ctx, svo_image* img);
 /* H2D copy of level 0 (row stride in bytes) and pyramid build. */
 int svo_image_upload(svo_ctx* ctx, svo_image* img, const uint8_t* gray, int stride);
+/* Colour ingest (R:include/async_image_loader.h:63-69, imread + cvtColor(
+ * COLOR_BGR2GRAY)): H2D of a host 8UC3 BGR image (row stride in bytes >= 3w)
+ * through a pinned double buffer, grey conversion written straight into level
+ * 0 (OpenCV's fixed-point weights, bit-exact), then the pyramid build. Returns
+ * once the copy is queued: `bgr` may be reused immediately. */
+int svo_image_upload_bgr(svo_ctx* ctx, svo_image* img, const uint8_t* bgr, int stride);
 /* Rebuild levels 1..max_levels from the device-resident level 0. */
 int svo_image_build_pyramid(svo_ctx* ctx, svo_image* img);
 int svo_image_level_size(const svo_image* img, int level, int* w, int* h);
@@ -95,6 +101,30 @@ int svo_fast_detect(svo_ctx* ctx, const svo_image* img, int threshold, int nonma
  * and corner flag, both W*H u8. */
 int svo_fast_score_map(svo_ctx* ctx, const svo_image* img, int threshold,
                        uint8_t* score, uint8_t* corner);
+/* ------------------------------------------------------------ ORB (detect only)
+ * The reference's shipped default detector (use_orb: 1, R:configs/config.yaml:20-27):
+ * cv::ORB::create(nfeatures, scaleFactor, nlevels, edgeThreshold, firstLevel, WTA_K,
+ * scoreType, patchSize, fastThreshold) at R:src/tracking.cpp:33-50, used through
+ * detect(img, keypoints, mask) at :82. Keypoints in OpenCV's order (level by level,
+ * retainBest's order within a level), pt scaled to level 0; response = Harris (or
+ * FAST) score; octave optional (may be NULL). Angles are not computed (the
+ * reference keeps positions only, R:src/tracking.cpp:85). firstLevel must be 0. */
+#define SVO_ORB_HARRIS_SCORE 0
+#define SVO_ORB_FAST_SCORE 1
+typedef struct svo_orb_params {
+    int nfeatures;        /* R:configs/config.yaml:22 (150) */
+    float scale_factor;   /* 1.2 */
+    int nlevels;          /* 8 (<= 8) */
+    int edge_threshold;   /* the reference passes patch_size (31) */
+    int first_level;      /* 0 */
+    int wta_k;            /* 4 (descriptors only; unused by detect) */
+    int score_type;       /* SVO_ORB_HARRIS_SCORE */
+    int patch_size;       /* 31 */
+    int fast_threshold;   /* 20 */
+} svo_orb_params;
+int svo_orb_detect(svo_ctx* ctx, const svo_image* img, const svo_orb_params* params,
+                   const uint8_t* mask, svo_keypoint* out, int* octave, int cap, int* n_out);
+
 /* R:src/tracking.cpp:76-79: W*H mask of 255 with a filled box of +-half around
  * each point (cvRound corners, inclusive, clipped). Host output. */
 int svo_mask_boxes(svo_ctx* ctx, int w, int h, const float* pts_xy, int n, float half,
@@ -229,6 +259,9 @@ void svo_frontend_destroy(svo_frontend* fe);
  * rotation of the synthetic scene and its depth seed (for new map points). */
 int svo_frontend_set_frame(svo_frontend* fe, int seq, int t, const uint8_t* gray, int stride,
                            const double R[9], int depth_seed);
+/* Same from a BGR 8UC3 frame (svo_image_upload_bgr's conversion). */
+int svo_frontend_set_frame_bgr(svo_frontend* fe, int seq, int t, const uint8_t* bgr, int stride,
+                               const double R[9], int depth_seed);
 /* Build every resident frame's pyramid now (else each step builds its own). */
 int svo_frontend_prebuild_pyramids(svo_frontend* fe);
 /* First keyframe: FAST (+bucket) on frame t0 of every sequence, map points. */

@@ -25,6 +25,13 @@ typedef struct svo_tracking_config {
     float y_threshold;       /* R:configs/config.yaml:16 -> 40 */
     int features_to_track;   /* R:configs/config.yaml:17 -> 70 */
     int device;
+    /* detector choice, R:configs/config.yaml:20-27 (use_orb: 1 ships) */
+    int use_orb;
+    int orb_nfeatures;       /* 150 */
+    float orb_scale_factor;  /* 1.2 */
+    int orb_pyr_levels;      /* 8 */
+    int orb_patch_size;      /* 31 (also the edge threshold) */
+    int orb_fast_threshold;  /* 20 */
 } svo_tracking_config;
 
 /* calib: P0 then P1, 3x4 row-major floats (R:src/main.cpp:25-32). */
@@ -34,6 +41,10 @@ const char* svo_tracking_last_error(const svo_tracking* tr);
 /* Queue one rectified stereo pair (8-bit gray, w x h, row stride in bytes). */
 int svo_tracking_push_stereo(svo_tracking* tr, const uint8_t* left, const uint8_t* right, int w, int h,
                              int stride);
+/* Same from colour frames (8UC3 BGR, row stride in bytes >= 3w): the loader's
+ * cvtColor(COLOR_BGR2GRAY) runs on the device as the frame is uploaded. */
+int svo_tracking_push_stereo_bgr(svo_tracking* tr, const uint8_t* left, const uint8_t* right, int w, int h,
+                                 int stride);
 /* First call: the initial keyframe (extractFeatures + triangulateNewMapPoints);
  * later calls: one iteration of startStereo's loop. Returns 1 if a frame was
  * processed, 0 if no frame was queued, < 0 on error (message in last_error). */

@@ -18,10 +18,12 @@
  *   exact correspondences + far outliers, bucket selection on hand-listed points.
  *
  * Reference call sites each oracle entry point restates:
+ *   svo_oracle_bgr2gray       <- cv::cvtColor(COLOR_BGR2GRAY), R:include/async_image_loader.h:68-69
  *   svo_oracle_build_pyramid  <- cv::buildOpticalFlowPyramid inside
  *                                cv::calcOpticalFlowPyrLK, R:src/tracking.cpp:101,160
  *   svo_oracle_lk             <- cv::calcOpticalFlowPyrLK,  R:src/tracking.cpp:101-105,160-165
  *   svo_oracle_fast           <- cv::FastFeatureDetector::detect, R:src/tracking.cpp:54-57,82
+ *   svo_oracle_orb_detect     <- cv::ORB::detect (use_orb: 1), R:src/tracking.cpp:33-50,82
  *   svo_oracle_mask_boxes     <- cv::rectangle(mask,...,FILLED), R:src/tracking.cpp:76-79
  *   svo_oracle_bucket         <- FeatureSet::bucketingFeatures, R:src/bucket.cpp:24-106
  *   svo_oracle_pnp_*          <- cv::solvePnPRansac(...,SOLVEPNP_SQPNP), R:src/tracking.cpp:191-196
@@ -34,6 +36,12 @@
 #ifdef __cplusplus
 extern "C" {
 #endif
+
+/* ---------------------------------------------------------------- ingest */
+
+/* cv::cvtColor(COLOR_BGR2GRAY) on 8UC3 (R:include/async_image_loader.h:68-69):
+ * gray is w*h, row stride w. */
+void svo_oracle_bgr2gray(const uint8_t* bgr, int w, int h, int stride, uint8_t* gray);
 
 /* ---------------------------------------------------------------- pyramid */
 
@@ -100,6 +108,22 @@ void svo_oracle_fast_score(const uint8_t* img, int w, int h, int stride, int thr
  * p+(h,h), 0, FILLED) for every point (Point2f -> Point via cvRound). */
 void svo_oracle_mask_boxes(int w, int h, const float* pts_xy, int n, float half,
                            uint8_t* mask);
+
+/* ---------------------------------------------------------------- ORB (orb.cpp) */
+
+/* imgproc resize(src, dst, (dw, dh), 0, 0, INTER_LINEAR_EXACT) on 8UC1. */
+void svo_oracle_resize_linear_exact(const uint8_t* src, int sw, int sh, int sstride, uint8_t* dst, int dw, int dh,
+                                    int dstride);
+/* ORB level geometry: sizes, float scales and nfeaturesPerLevel. */
+void svo_oracle_orb_level_info(int w, int h, float scale_factor, int nlevels, int nfeatures, int* lw, int* lh,
+                               float* lscale, int* nper);
+/* cv::ORB::create(nfeatures, scale_factor, nlevels, edge_threshold, 0, 4,
+ * harris_score ? HARRIS_SCORE : FAST_SCORE, patch_size, fast_threshold)
+ * ->detect(img, kps, mask). Writes up to cap (x, y, response) triples and
+ * octaves (may be NULL); returns the keypoint count. */
+int svo_oracle_orb_detect(const uint8_t* img, int w, int h, int stride, const uint8_t* mask, int nfeatures,
+                          float scale_factor, int nlevels, int edge_threshold, int patch_size, int fast_threshold,
+                          int harris_score, float* kp_xyr, int* octave, int cap);
 
 /* ---------------------------------------------------------------- bucket */
 

@@ -69,10 +69,12 @@ _SIGS = [
     ("svo_image_create", C.c_int, [_vp, C.c_int, C.c_int, C.c_int, C.POINTER(_vp)]),
     ("svo_image_destroy", None, [_vp, _vp]),
     ("svo_image_upload", C.c_int, [_vp, _vp, _u8p, C.c_int]),
+    ("svo_image_upload_bgr", C.c_int, [_vp, _vp, _u8p, C.c_int]),
     ("svo_image_build_pyramid", C.c_int, [_vp, _vp]),
     ("svo_image_level_size", C.c_int, [_vp, C.c_int, _i32p, _i32p]),
     ("svo_image_download_level", C.c_int, [_vp, _vp, C.c_int, _u8p, C.c_int]),
     ("svo_fast_detect", C.c_int, [_vp, _vp, C.c_int, C.c_int, _u8p, _f32p, C.c_int, _i32p]),
+    ("svo_orb_detect", C.c_int, [_vp, _vp, _vp, _u8p, _f32p, _i32p, C.c_int, _i32p]),
     ("svo_fast_score_map", C.c_int, [_vp, _vp, C.c_int, _u8p, _u8p]),
     ("svo_mask_boxes", C.c_int, [_vp, C.c_int, C.c_int, _f32p, C.c_int, C.c_float, _u8p]),
     ("svo_bucket_features", C.c_int, [_vp, _f32p, _i32p, C.c_int, C.c_int, C.c_int, C.c_int,
@@ -93,6 +95,7 @@ _SIGS = [
     ("svo_frontend_create", C.c_int, [_vp, _vp, C.POINTER(_vp)]),
     ("svo_frontend_destroy", None, [_vp]),
     ("svo_frontend_set_frame", C.c_int, [_vp, C.c_int, C.c_int, _u8p, C.c_int, _f64p, C.c_int]),
+    ("svo_frontend_set_frame_bgr", C.c_int, [_vp, C.c_int, C.c_int, _u8p, C.c_int, _f64p, C.c_int]),
     ("svo_frontend_prebuild_pyramids", C.c_int, [_vp]),
     ("svo_frontend_init", C.c_int, [_vp, C.c_int]),
     ("svo_frontend_step", C.c_int, [_vp, C.c_int, _vp]),
@@ -155,6 +158,12 @@ class Image:
         assert gray.shape == (self.h, self.w)
         self.ctx._check(lib().svo_image_upload(self.ctx.handle, self.handle, _p(gray, _u8p), self.w))
 
+    def upload_bgr(self, bgr: np.ndarray):
+        """H2D of an (h, w, 3) BGR image, grey conversion on the device (cvtColor BGR2GRAY)."""
+        bgr = _c(bgr, np.uint8)
+        assert bgr.shape == (self.h, self.w, 3)
+        self.ctx._check(lib().svo_image_upload_bgr(self.ctx.handle, self.handle, _p(bgr, _u8p), 3 * self.w))
+
     def close(self):
         if self.handle:
             lib().svo_image_destroy(self.ctx.handle, self.handle)
@@ -165,6 +174,24 @@ class Image:
             self.close()
         except Exception:
             pass
+
+
+class OrbParams(C.Structure):
+    """svo_orb_params; defaults = the reference's ORB (R:configs/config.yaml:20-27,
+    R:src/tracking.cpp:33-50: edgeThreshold = patch_size, firstLevel 0, WTA_K 4, HARRIS)."""
+    _fields_ = [("nfeatures", C.c_int), ("scale_factor", C.c_float), ("nlevels", C.c_int),
+                ("edge_threshold", C.c_int), ("first_level", C.c_int), ("wta_k", C.c_int),
+                ("score_type", C.c_int), ("patch_size", C.c_int), ("fast_threshold", C.c_int)]
+
+    HARRIS, FAST = 0, 1
+
+    def __init__(self, nfeatures=150, scale_factor=1.2, nlevels=8, patch_size=31, fast_threshold=20,
+                 edge_threshold=None, score_type=0):
+        super().__init__()
+        self.nfeatures, self.scale_factor, self.nlevels = nfeatures, scale_factor, nlevels
+        self.edge_threshold = patch_size if edge_threshold is None else edge_threshold
+        self.first_level, self.wta_k, self.score_type = 0, 4, score_type
+        self.patch_size, self.fast_threshold = patch_size, fast_threshold
 
 
 class Context:
@@ -204,6 +231,17 @@ class Context:
         img.upload(gray)
         return img
 
+    def image_bgr(self, bgr: np.ndarray, max_levels: int = 4) -> Image:
+        """Device image from an (h, w, 3) BGR frame (svo_image_upload_bgr)."""
+        bgr = _c(bgr, np.uint8)
+        h, w, c = bgr.shape
+        assert c == 3
+        hd = _vp()
+        self._check(lib().svo_image_create(self.handle, w, h, max_levels, C.byref(hd)))
+        img = Image(self, hd, w, h, max_levels)
+        img.upload_bgr(bgr)
+        return img
+
     # ---------------------------------------------------------------- FAST
     def fast_detect(self, img: Image, threshold: int = 20, nonmax: bool = True, mask=None,
                     cap: int = 1 << 20) -> np.ndarray:
@@ -218,6 +256,22 @@ class Context:
         self._check(lib().svo_fast_detect(self.handle, img.handle, int(threshold), int(bool(nonmax)), mp,
                                           _p(out, _f32p), cap, C.byref(n)))
         return out[: min(n.value, cap)].copy()
+
+    def orb_detect(self, img: Image, params: "OrbParams" = None, mask=None, cap: int = 1 << 16):
+        """cv::ORB::detect -> (float32 (n, 3) x, y, response; int32 (n,) octave)."""
+        params = params or OrbParams()
+        out = np.empty((cap, 3), np.float32)
+        octv = np.empty(cap, np.int32)
+        n = C.c_int()
+        mp = None
+        if mask is not None:
+            mask = _c(mask, np.uint8)
+            assert mask.shape == (img.h, img.w)
+            mp = _p(mask, _u8p)
+        self._check(lib().svo_orb_detect(self.handle, img.handle, C.byref(params), mp, _p(out, _f32p),
+                                         _p(octv, _i32p), cap, C.byref(n)))
+        k = min(n.value, cap)
+        return out[:k].copy(), octv[:k].copy()
 
     def fast_score_map(self, img: Image, threshold: int = 20):
         score = np.empty((img.h, img.w), np.uint8)
@@ -415,11 +469,16 @@ class Frontend:
         self.handle = h
 
     def set_frame(self, seq, t, gray, R=None, depth_seed=0):
+        """Frame t of sequence seq: (h, w) grey, or (h, w, 3) BGR converted on the device."""
         gray = _c(gray, np.uint8)
         Rp = None
         if R is not None:
             R = _c(R, np.float64).reshape(9)
             Rp = _p(R, _f64p)
+        if gray.ndim == 3:
+            self.ctx._check(lib().svo_frontend_set_frame_bgr(self.handle, seq, t, _p(gray, _u8p), 3 * gray.shape[1],
+                                                             Rp, int(depth_seed)))
+            return
         self.ctx._check(lib().svo_frontend_set_frame(self.handle, seq, t, _p(gray, _u8p), gray.shape[1], Rp,
                                                      int(depth_seed)))
 

@@ -57,6 +57,30 @@ void* pinned(svo_ctx* ctx, size_t bytes) {
     return ctx->pinned;
 }
 
+int ingest_bgr(svo_ctx* ctx, const uint8_t* bgr, int stride, int w, int h, uint8_t* level0, int pitch) {
+    const int bp = (3 * w + 63) & ~63;
+    const size_t bytes = (size_t)bp * h;
+    const int i = ctx->ingest_next;
+    ctx->ingest_next ^= 1;
+    if (!ctx->ingest_ev[i]) SVO_HIP(ctx, hipEventCreateWithFlags(&ctx->ingest_ev[i], hipEventDisableTiming));
+    else SVO_HIP(ctx, hipEventSynchronize(ctx->ingest_ev[i]));  // buffer i's previous H2D is done
+    if (ctx->ingest_bytes[i] < bytes) {
+        if (ctx->ingest_host[i]) (void)hipHostFree(ctx->ingest_host[i]);
+        ctx->ingest_host[i] = nullptr;
+        ctx->ingest_bytes[i] = 0;
+        SVO_HIP(ctx, hipHostMalloc(&ctx->ingest_host[i], bytes, hipHostMallocDefault));
+        ctx->ingest_bytes[i] = bytes;
+    }
+    uint8_t* hb = (uint8_t*)ctx->ingest_host[i];
+    for (int y = 0; y < h; y++) std::memcpy(hb + (size_t)y * bp, bgr + (size_t)y * stride, (size_t)3 * w);
+    uint8_t* dev = (uint8_t*)scratch(ctx, 8 + i, bytes);
+    if (!dev) return set_error(ctx, SVO_ERR_HIP, "ingest: scratch alloc failed");
+    SVO_HIP(ctx, hipMemcpyAsync(dev, hb, bytes, hipMemcpyHostToDevice, ctx->stream));
+    SVO_HIP(ctx, hipEventRecord(ctx->ingest_ev[i], ctx->stream));
+    SVO_HIP(ctx, launch_bgr_to_gray(dev, bp, level0, pitch, w, h, ctx->stream));
+    return SVO_OK;
+}
+
 // Upload one pyramid descriptor to device scratch slot 3's head (single-image calls).
 static PyrDesc* stage_desc(svo_ctx* ctx, const svo_image* img, void* dst) {
     PyrDesc* h = (PyrDesc*)pinned(ctx, sizeof(PyrDesc));
@@ -102,6 +126,10 @@ void svo_ctx_destroy(svo_ctx* ctx) {
     for (auto& s : ctx->s)
         if (s.p) (void)hipFree(s.p);
     if (ctx->pinned) (void)hipHostFree(ctx->pinned);
+    for (int i = 0; i < 2; i++) {
+        if (ctx->ingest_host[i]) (void)hipHostFree(ctx->ingest_host[i]);
+        if (ctx->ingest_ev[i]) (void)hipEventDestroy(ctx->ingest_ev[i]);
+    }
     (void)hipStreamDestroy(ctx->stream);
     delete ctx;
 }
@@ -169,6 +197,15 @@ int svo_image_upload(svo_ctx* ctx, svo_image* img, const uint8_t* gray, int stri
     const ImgLevel& L = img->desc.lv[0];
     SVO_HIP(ctx, hipMemcpy2DAsync(const_cast<uint8_t*>(L.data), L.pitch, gray, stride, L.w, L.h,
                                   hipMemcpyHostToDevice, ctx->stream));
+    return svo_image_build_pyramid(ctx, img);
+}
+
+int svo_image_upload_bgr(svo_ctx* ctx, svo_image* img, const uint8_t* bgr, int stride) {
+    if (!ctx || !img || !bgr || stride < 3 * img->w)
+        return set_error(ctx, SVO_ERR_ARG, "svo_image_upload_bgr: bad arguments");
+    const ImgLevel& L = img->desc.lv[0];
+    int rc = ingest_bgr(ctx, bgr, stride, L.w, L.h, const_cast<uint8_t*>(L.data), L.pitch);
+    if (rc) return rc;
     return svo_image_build_pyramid(ctx, img);
 }
 

@@ -58,9 +58,15 @@ struct svo_ctx {
     hipStream_t stream = nullptr;
     std::string err;
     int64_t lk_iters = 0;
-    svo_scratch s[8];
+    svo_scratch s[12];
     void* pinned = nullptr;
     size_t pinned_bytes = 0;
+    // colour ingest: pinned double buffer (host copy of frame k+1 overlaps the
+    // H2D of frame k), reused once its event shows the H2D is done
+    void* ingest_host[2] = {nullptr, nullptr};
+    size_t ingest_bytes[2] = {0, 0};
+    hipEvent_t ingest_ev[2] = {nullptr, nullptr};
+    int ingest_next = 0;
 };
 
 namespace svo {
@@ -72,6 +78,11 @@ void* pinned(svo_ctx* ctx, size_t bytes);
 
 // Kernel launchers (implemented in the .hip files).
 hipError_t launch_pyramid(const svo_image* img, int first_level, hipStream_t st);
+hipError_t launch_bgr_to_gray(const uint8_t* bgr, int bpitch, uint8_t* dst, int pitch, int w, int h,
+                              hipStream_t st);
+// H2D of a host BGR image through the context's pinned double buffer and its
+// grey conversion into `level0` (w x h, row pitch `pitch`), on ctx->stream.
+int ingest_bgr(svo_ctx* ctx, const uint8_t* bgr, int stride, int w, int h, uint8_t* level0, int pitch);
 hipError_t launch_pyramid_batched(const PyrDesc* d_descs, int nseq, int w, int h, int nlevels,
                                   hipStream_t st);
 

@@ -537,14 +537,21 @@ void svo_frontend_destroy(svo_frontend* fe) {
     delete fe;
 }
 
-int svo_frontend_set_frame(svo_frontend* fe, int seq, int t, const uint8_t* gray, int stride, const double R[9],
-                           int depth_seed) {
-    if (!fe || seq < 0 || seq >= fe->S || t < 0 || t >= fe->T || !gray || stride < fe->W) return SVO_ERR_ARG;
+static int fe_set_frame(svo_frontend* fe, int seq, int t, const uint8_t* px, int stride, bool bgr,
+                        const double R[9], int depth_seed) {
+    if (!fe || seq < 0 || seq >= fe->S || t < 0 || t >= fe->T || !px || stride < (bgr ? 3 : 1) * fe->W)
+        return SVO_ERR_ARG;
     svo_ctx* ctx = fe->ctx;
     svo_image* im = fe->frames[(size_t)seq * fe->T + t];
     if (fe->pyr_ready >= 0 && fe->pyr_ready % fe->T == t) fe->pyr_ready = -1;  // built from the old image
-    SVO_HIP(ctx, hipMemcpy2DAsync(const_cast<uint8_t*>(im->desc.lv[0].data), im->desc.lv[0].pitch, gray, stride,
-                                  fe->W, fe->H, hipMemcpyHostToDevice, ctx->stream));
+    uint8_t* l0 = const_cast<uint8_t*>(im->desc.lv[0].data);
+    if (bgr) {
+        int rc = ingest_bgr(ctx, px, stride, fe->W, fe->H, l0, im->desc.lv[0].pitch);
+        if (rc) return rc;
+    } else {
+        SVO_HIP(ctx, hipMemcpy2DAsync(l0, im->desc.lv[0].pitch, px, stride, fe->W, fe->H, hipMemcpyHostToDevice,
+                                      ctx->stream));
+    }
     if (R) {
         std::memcpy(&fe->rot_host[9 * ((size_t)t * fe->S + seq)], R, sizeof(double) * 9);
         SVO_HIP(ctx, hipMemcpyAsync(fe->rot_d + 9 * ((size_t)t * fe->S + seq), R, sizeof(double) * 9,
@@ -555,6 +562,16 @@ int svo_frontend_set_frame(svo_frontend* fe, int seq, int t, const uint8_t* gray
                                 ctx->stream));
     SVO_HIP(ctx, hipStreamSynchronize(ctx->stream));
     return SVO_OK;
+}
+
+int svo_frontend_set_frame(svo_frontend* fe, int seq, int t, const uint8_t* gray, int stride, const double R[9],
+                           int depth_seed) {
+    return fe_set_frame(fe, seq, t, gray, stride, false, R, depth_seed);
+}
+
+int svo_frontend_set_frame_bgr(svo_frontend* fe, int seq, int t, const uint8_t* bgr, int stride,
+                               const double R[9], int depth_seed) {
+    return fe_set_frame(fe, seq, t, bgr, stride, true, R, depth_seed);
 }
 
 int svo_frontend_prebuild_pyramids(svo_frontend* fe) {

@@ -16,7 +16,7 @@ namespace svo {
 
 namespace {
 
-constexpr int kMaxLevel = 3;  // maxLevel of both LK calls, R:src/tracking.cpp:104,163
+constexpr int kMaxLevel = Tracking::kImageLevels;  // maxLevel of both LK calls, R:src/tracking.cpp:104,163
 
 [[noreturn]] void fail(svo_ctx* ctx, const char* what) {
     throw std::runtime_error(std::string(what) + ": " + (ctx ? svo_last_error(ctx) : "no context"));
@@ -64,7 +64,6 @@ Tracking::Tracking(const Config& config, Map& map, const std::vector<float>& c, 
     : prevFrame(nullptr), currFrame(nullptr), lastFrameID(0), mImageLoader(source), mConfig(config), mMap(map),
       inlierRatio(0) {
     if (c.size() < 24) throw std::invalid_argument("Tracking: calib_data needs P0 and P1 (24 floats)");
-    if (config.use_orb) throw std::invalid_argument("Tracking: the ORB detector is not built (FAST only)");
     for (int i = 0; i < 12; i++) {
         mProjectionMatrixLeft[i] = c[i];
         mProjectionMatrixRight[i] = c[12 + i];
@@ -113,9 +112,22 @@ void Tracking::extractFeatures(StereoFrame* frame) {
     std::vector<svo_keypoint> keypoints(1 << 15);
     int n = 0;
     for (;;) {
-        if (svo_fast_detect(mGpu, dimg, mConfig.fast_params.threshold, mConfig.fast_params.nonMaxSuppression ? 1 : 0,
-                            mask.data(), keypoints.data(), (int)keypoints.size(), &n) != SVO_OK)
+        if (mConfig.use_orb) {
+            // R:src/tracking.cpp:33-50: ORB(nfeatures, scale_factor, pyr_levels,
+            // edge_threshold = patch_size, first_level 0, WTA_K 4, HARRIS_SCORE,
+            // patch_size, fast_treshold)
+            svo_orb_params op{mConfig.orb_params.nfeatures, mConfig.orb_params.scale_factor,
+                              mConfig.orb_params.pyr_levels, mConfig.orb_params.patch_size, 0, 4,
+                              SVO_ORB_HARRIS_SCORE, mConfig.orb_params.patch_size,
+                              mConfig.orb_params.fast_treshold};
+            if (svo_orb_detect(mGpu, dimg, &op, mask.data(), keypoints.data(), nullptr, (int)keypoints.size(), &n) !=
+                SVO_OK)
+                fail(mGpu, "svo_orb_detect");
+        } else if (svo_fast_detect(mGpu, dimg, mConfig.fast_params.threshold,
+                                   mConfig.fast_params.nonMaxSuppression ? 1 : 0, mask.data(), keypoints.data(),
+                                   (int)keypoints.size(), &n) != SVO_OK) {
             fail(mGpu, "svo_fast_detect");
+        }
         if (n <= (int)keypoints.size()) break;
         keypoints.resize((size_t)n);
     }

@@ -40,6 +40,14 @@ int svo_tracking_create(const svo_tracking_config* cfg, const float calib[24], s
     tr->config.tracking.features_to_track = cfg->features_to_track;
     tr->config.device = cfg->device;
     tr->config.verbose = false;
+    tr->config.use_orb = cfg->use_orb != 0;
+    if (cfg->use_orb) {
+        tr->config.orb_params.nfeatures = cfg->orb_nfeatures;
+        tr->config.orb_params.scale_factor = cfg->orb_scale_factor;
+        tr->config.orb_params.pyr_levels = cfg->orb_pyr_levels;
+        tr->config.orb_params.patch_size = cfg->orb_patch_size;
+        tr->config.orb_params.fast_treshold = cfg->orb_fast_threshold;
+    }
     try {
         tr->tracking = std::make_unique<svo::Tracking>(tr->config, tr->map, std::vector<float>(calib, calib + 24),
                                                        tr->source);
@@ -63,6 +71,21 @@ int svo_tracking_push_stereo(svo_tracking* tr, const uint8_t* left, const uint8_
                              int stride) {
     if (!tr || !left || !right || w <= 0 || h <= 0 || stride < w) return -1;
     tr->source.push(svo::GrayImage::copyFrom(left, w, h, stride), svo::GrayImage::copyFrom(right, w, h, stride));
+    return 0;
+}
+
+int svo_tracking_push_stereo_bgr(svo_tracking* tr, const uint8_t* left, const uint8_t* right, int w, int h,
+                                 int stride) {
+    if (!tr || !left || !right || w <= 0 || h <= 0 || stride < 3 * w) return -1;
+    try {
+        svo_ctx* ctx = tr->tracking->context();
+        const int lv = svo::Tracking::kImageLevels;
+        tr->source.push(svo::GrayImage::fromBGR(ctx, left, w, h, stride, lv),
+                        svo::GrayImage::fromBGR(ctx, right, w, h, stride, lv));
+    } catch (const std::exception& e) {
+        tr->err = e.what();
+        return -2;
+    }
     return 0;
 }
 

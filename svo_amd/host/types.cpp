@@ -53,14 +53,48 @@ GrayImage GrayImage::copyFrom(const uint8_t* data, int w, int h, int stride) {
     return im;
 }
 
+GrayImage GrayImage::fromBGR(svo_ctx* ctx, const uint8_t* bgr, int w, int h, int stride, int max_level) {
+    if (!ctx || !bgr || w <= 0 || h <= 0 || stride < 3 * w) throw std::invalid_argument("GrayImage::fromBGR");
+    GrayImage im;
+    im.b_ = std::make_shared<Body>();
+    Body& b = *im.b_;
+    b.w = w;
+    b.h = h;
+    b.px_valid = false;
+    svo_image* d = nullptr;
+    int rc = svo_image_create(ctx, w, h, max_level, &d);
+    if (rc == SVO_OK) rc = svo_image_upload_bgr(ctx, d, bgr, stride);
+    if (rc != SVO_OK) {
+        if (d) svo_image_destroy(ctx, d);
+        throw std::runtime_error(std::string("svo_image_upload_bgr: ") + svo_last_error(ctx));
+    }
+    b.dev = d;
+    b.ctx = ctx;
+    b.levels = max_level;
+    return im;
+}
+
+uint8_t* GrayImage::Body::host() {
+    if (!px_valid) {
+        px.resize((size_t)w * h);
+        if (!dev || svo_image_download_level(ctx, dev, 0, px.data(), w) != SVO_OK)
+            throw std::runtime_error("GrayImage: device pixels unavailable");
+        px_valid = true;
+    }
+    return px.data();
+}
+
 svo_image* GrayImage::device(svo_ctx* ctx, int max_level) const {
     if (empty()) throw std::invalid_argument("GrayImage::device: empty image");
     Body& b = *b_;
-    if (b.dev && (b.ctx != ctx || b.levels < max_level)) releaseDevice();
+    if (b.dev && (b.ctx != ctx || b.levels < max_level)) {
+        b.host();  // keep the pixels of a device-born image before dropping the device copy
+        releaseDevice();
+    }
     if (!b.dev) {
         svo_image* im = nullptr;
         int rc = svo_image_create(ctx, b.w, b.h, max_level, &im);
-        if (rc == SVO_OK) rc = svo_image_upload(ctx, im, b.px.data(), b.w);
+        if (rc == SVO_OK) rc = svo_image_upload(ctx, im, b.host(), b.w);
         if (rc != SVO_OK) {
             if (im) svo_image_destroy(ctx, im);
             throw std::runtime_error(std::string("svo_image_upload: ") + svo_last_error(ctx));

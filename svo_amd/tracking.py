@@ -26,7 +26,9 @@ _vp = C.c_void_p
 
 class TrackingConfig(C.Structure):
     _fields_ = [("fast_threshold", C.c_int), ("fast_nonmax", C.c_int), ("y_threshold", C.c_float),
-                ("features_to_track", C.c_int), ("device", C.c_int)]
+                ("features_to_track", C.c_int), ("device", C.c_int),
+                ("use_orb", C.c_int), ("orb_nfeatures", C.c_int), ("orb_scale_factor", C.c_float),
+                ("orb_pyr_levels", C.c_int), ("orb_patch_size", C.c_int), ("orb_fast_threshold", C.c_int)]
 
 
 _SIGS = [
@@ -34,6 +36,7 @@ _SIGS = [
     ("svo_tracking_destroy", None, [_vp]),
     ("svo_tracking_last_error", C.c_char_p, [_vp]),
     ("svo_tracking_push_stereo", C.c_int, [_vp, _u8p, _u8p, C.c_int, C.c_int, C.c_int]),
+    ("svo_tracking_push_stereo_bgr", C.c_int, [_vp, _u8p, _u8p, C.c_int, C.c_int, C.c_int]),
     ("svo_tracking_step", C.c_int, [_vp]),
     ("svo_tracking_frame_info", C.c_int, [_vp, _i64p, _i32p, _i64p, _i64p, _f64p, _f64p]),
     ("svo_tracking_features", C.c_int, [_vp, _f32p, _f64p, _i64p, C.c_int, _i32p]),
@@ -74,10 +77,14 @@ class Tracking:
     """The reference's Tracking (stereo, FAST) on the GPU path, one frame per step()."""
 
     def __init__(self, calib, fast_threshold=20, fast_nonmax=True, y_threshold=40.0, features_to_track=70,
-                 device=0):
+                 device=0, use_orb=False, orb_nfeatures=150, orb_scale_factor=1.2, orb_pyr_levels=8,
+                 orb_patch_size=31, orb_fast_threshold=20):
+        """Defaults: R:configs/config.yaml (its ORB block; use_orb=True is what it ships)."""
         calib = np.ascontiguousarray(calib, np.float32).reshape(24)
         cfg = TrackingConfig(int(fast_threshold), int(bool(fast_nonmax)), float(y_threshold),
-                             int(features_to_track), int(device))
+                             int(features_to_track), int(device), int(bool(use_orb)), int(orb_nfeatures),
+                             float(orb_scale_factor), int(orb_pyr_levels), int(orb_patch_size),
+                             int(orb_fast_threshold))
         h = _vp()
         rc = lib().svo_tracking_create(C.byref(cfg), calib.ctypes.data_as(_f32p), C.byref(h))
         if rc != 0:
@@ -104,6 +111,17 @@ class Tracking:
         if lib().svo_tracking_push_stereo(self.handle, left.ctypes.data_as(_u8p), right.ctypes.data_as(_u8p),
                                           w, h, w) != 0:
             raise SvoError("svo_tracking_push_stereo failed")
+
+    def push_bgr(self, left: np.ndarray, right: np.ndarray):
+        """Queue a colour (h, w, 3) BGR pair; grey conversion happens on the device."""
+        left = np.ascontiguousarray(left, np.uint8)
+        right = np.ascontiguousarray(right, np.uint8)
+        h, w, c = left.shape
+        if right.shape != left.shape or c != 3:
+            raise ValueError("need two (h, w, 3) BGR images of one size")
+        if lib().svo_tracking_push_stereo_bgr(self.handle, left.ctypes.data_as(_u8p), right.ctypes.data_as(_u8p),
+                                              w, h, 3 * w) != 0:
+            raise SvoError("svo_tracking_push_stereo_bgr: " + lib().svo_tracking_last_error(self.handle).decode())
 
     def step(self) -> bool:
         rc = lib().svo_tracking_step(self.handle)

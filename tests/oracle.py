@@ -59,6 +59,13 @@ def load():
             "svo_oracle_get_subset": (C.c_int, [_u64p, C.c_int, C.c_int, _i32p]),
             "svo_oracle_triangulate": (None, [_f32p, _f32p, _f32p, _f32p, C.c_int, _f32p, _f32p]),
             "svo_oracle_set_threads": (None, [C.c_int]),
+            "svo_oracle_bgr2gray": (None, [_u8p, C.c_int, C.c_int, C.c_int, _u8p]),
+            "svo_oracle_resize_linear_exact": (None, [_u8p, C.c_int, C.c_int, C.c_int, _u8p, C.c_int, C.c_int,
+                                                       C.c_int]),
+            "svo_oracle_orb_level_info": (None, [C.c_int, C.c_int, C.c_float, C.c_int, C.c_int, _i32p, _i32p,
+                                                  _f32p, _i32p]),
+            "svo_oracle_orb_detect": (C.c_int, [_u8p, C.c_int, C.c_int, C.c_int, _u8p, C.c_int, C.c_float, C.c_int,
+                                                C.c_int, C.c_int, C.c_int, C.c_int, _f32p, _i32p, C.c_int]),
         }
         for k, (r, a) in sig.items():
             f = getattr(L, k)
@@ -223,6 +230,47 @@ def solve_pnp_ransac(obj, img, K, iterations=100, reproj=8.0, confidence=0.999):
 
 def update_num_iters(p, ep, model_points, max_iters):
     return load().svo_oracle_ransac_update_num_iters(p, ep, model_points, max_iters)
+
+
+def bgr2gray(bgr):
+    bgr = _c(bgr, np.uint8)
+    h, w, _ = bgr.shape
+    out = np.empty((h, w), np.uint8)
+    load().svo_oracle_bgr2gray(_p(bgr, _u8p), w, h, 3 * w, _p(out, _u8p))
+    return out
+
+
+def resize_linear_exact(img, dw, dh):
+    img = _c(img, np.uint8)
+    h, w = img.shape
+    out = np.empty((dh, dw), np.uint8)
+    load().svo_oracle_resize_linear_exact(_p(img, _u8p), w, h, w, _p(out, _u8p), dw, dh, dw)
+    return out
+
+
+def orb_level_info(w, h, scale_factor=1.2, nlevels=8, nfeatures=150):
+    lw, lh, nper = (np.zeros(nlevels, np.int32) for _ in range(3))
+    ls = np.zeros(nlevels, np.float32)
+    load().svo_oracle_orb_level_info(w, h, scale_factor, nlevels, nfeatures, _p(lw, _i32p), _p(lh, _i32p),
+                                     _p(ls, _f32p), _p(nper, _i32p))
+    return lw, lh, ls, nper
+
+
+def orb_detect(img, mask=None, nfeatures=150, scale_factor=1.2, nlevels=8, edge_threshold=31, patch_size=31,
+               fast_threshold=20, harris=True, cap=1 << 16):
+    img = _c(img, np.uint8)
+    h, w = img.shape
+    out = np.empty((cap, 3), np.float32)
+    octv = np.empty(cap, np.int32)
+    mp = None
+    if mask is not None:
+        mask = _c(mask, np.uint8)
+        mp = _p(mask, _u8p)
+    n = load().svo_oracle_orb_detect(_p(img, _u8p), w, h, w, mp, nfeatures, scale_factor, nlevels, edge_threshold,
+                                     patch_size, fast_threshold, int(bool(harris)), _p(out, _f32p),
+                                     _p(octv, _i32p), cap)
+    k = min(n, cap)
+    return out[:k].copy(), octv[:k].copy()
 
 
 def set_threads(n: int):

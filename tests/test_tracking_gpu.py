@@ -47,22 +47,41 @@ def test_triangulate_matches_oracle_and_truth(ctx):
     assert h0.shape == (0, 4) and x0.shape == (0, 3)
 
 
-@pytest.mark.parametrize("features_to_track", [70, 1 << 30])
-def test_tracking_mirror_stagewise_parity(features_to_track):
-    """70 = the reference config (keyframe only at frame 0 here); 2^30 makes
+def _colour(g, t):
+    """A BGR frame built around a grey frame (the channels differ, so the device
+    conversion's weights matter); the test's grey frame is the oracle's conversion."""
+    b = g
+    gg = np.roll(g, 1, axis=1)  # same for every frame: the scene's motion is unchanged
+    r = 255 - g
+    return np.ascontiguousarray(np.stack([b, gg, r], axis=2))
+
+
+@pytest.mark.parametrize("detector,features_to_track,colour", [
+    ("fast", 70, False), ("fast", 1 << 30, False), ("orb", 70, False), ("orb", 1 << 30, True)])
+def test_tracking_mirror_stagewise_parity(detector, features_to_track, colour):
+    """70 = the reference config (keyframe only at frame 0 here for FAST); 2^30 makes
     every other frame a keyframe (R:src/tracking.cpp:68-69), exercising the
-    detect/stereo/triangulate path mid-sequence."""
+    detect/stereo/triangulate path mid-sequence. "orb" is the detector the reference
+    ships (use_orb: 1, 150 features: keyframes recur as tracks are lost); colour
+    frames go through the device BGR->grey ingest (R:include/async_image_loader.h:68-69)."""
     sc = Scene(1241, 376, seed=33)
     P0, P1 = sc.projections()
     K = sc.K
-    tr = Tracking(np.r_[P0.ravel(), P1.ravel()], features_to_track=features_to_track)
+    tr = Tracking(np.r_[P0.ravel(), P1.ravel()], features_to_track=features_to_track, use_orb=detector == "orb")
     T = 6
-    frames = [(sc.frame(t), sc.right(t)) for t in range(T)]
+    if colour:
+        bgr = [(_colour(sc.frame(t), t), _colour(sc.right(t), t)) for t in range(T)]
+        frames = [(O.bgr2gray(a), O.bgr2gray(b)) for a, b in bgr]
+    else:
+        frames = [(sc.frame(t), sc.right(t)) for t in range(T)]
     prev_xy = None
     n_kf = 0
     for t in range(T):
         L, Rimg = frames[t]
-        tr.push(L, Rimg)
+        if colour:
+            tr.push_bgr(*bgr[t])
+        else:
+            tr.push(L, Rimg)
         assert tr.step()
         info = tr.frame_info()
         assert info["id"] == t
@@ -99,7 +118,10 @@ def test_tracking_mirror_stagewise_parity(features_to_track):
             mask_pts, kps = tr.trace("mask_pts"), tr.trace("kps")
             assert np.array_equal(mask_pts, prev_xy if t > 0 else np.zeros((0, 2), np.float32))
             mask = O.mask_boxes(L.shape[1], L.shape[0], mask_pts, 10.0) if t > 0 else None
-            okp = O.fast(L, 20, True, mask)[:, :2]
+            if detector == "orb":
+                okp = O.orb_detect(L, mask)[0][:, :2]
+            else:
+                okp = O.fast(L, 20, True, mask)[:, :2]
             assert np.array_equal(kps, okp)
             sr, ss = tr.trace("stereo_right"), tr.trace("stereo_status")
             on, ost, _, _ = O.lk(L, Rimg, kps, (11, 11), 3, (3, 30, 1e-3), 0)
@@ -119,7 +141,10 @@ def test_tracking_mirror_stagewise_parity(features_to_track):
         else:
             assert len(xy) == len(keep_tracked)
         prev_xy = xy
-    assert n_kf == (1 if features_to_track == 70 else 3)
+    if detector == "fast":
+        assert n_kf == (1 if features_to_track == 70 else 3)
+    else:
+        assert n_kf >= (1 if features_to_track == 70 else 3)
     tr.close()
 
 
