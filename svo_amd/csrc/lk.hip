@@ -48,9 +48,8 @@ __device__ __forceinline__ int refl101(int p, int len) {
     return p;
 }
 
-__device__ __forceinline__ int ufloor(float v) {  // cvFloor
-    int i = (int)v;
-    return i - (i > v);
+__device__ __forceinline__ int ufloor(float v) {  // cvFloor (identical for |v| < 2^31)
+    return (int)__builtin_floorf(v);
 }
 __device__ __forceinline__ int uround(float v) { return (int)__builtin_rintf(v); }  // cvRound
 __device__ __forceinline__ float uni_f(float v) {
@@ -406,6 +405,9 @@ __global__ __launch_bounds__(256) void lk_kernel(LKBatch B, LKDev p) {
 // the same exact integers as before: bit-identical results.
 constexpr int ru4(int v) { return (v + 3) & ~3; }
 typedef uint32_t u32x2a4 __attribute__((ext_vector_type(2), aligned(4)));
+typedef uint16_t u16a1 __attribute__((aligned(1)));
+typedef const __attribute__((address_space(1))) u16a1* gu16u;  // unaligned 2-byte global loads
+typedef const __attribute__((address_space(4))) PyrDesc* cpyr;  // scalar (s_load) descriptor reads
 
 template <int WW, int WH>
 struct Shape {
@@ -433,12 +435,21 @@ __device__ __forceinline__ int dpp_add(int v) {
     return v + __builtin_amdgcn_update_dpp(0, v, CTRL, ROW_MASK, 0xf, BC);
 }
 
-// Exact wave sums of two int32 values whose per-lane magnitude is below 2^31/8
+// Exact wave sums of int32 values whose per-lane magnitude is below 2^31/8
 // (true for b1, b2, A11, A12, A22: <= RPG * 2 * 8160 * 4080): the first three
 // DPP steps (8-lane partial sums) run in int32, then each partial is split into
-// 16-bit halves for the last three steps, all four chains interleaved so that
-// no DPP read waits on the write before it (no s_nop padding).
-__device__ __forceinline__ void wave_sum_exact2(int x, int y, double& sx, double& sy) {
+// 16-bit halves for the last three steps, all chains interleaved so that no
+// DPP read waits on the write before it (no s_nop padding). The results are
+// the FLT_SCALE'd floats: hi * 65536 is exact in float (|hi| < 2^24) and the one
+// addition rounds the exact total once -- the same float as
+// (float)(double)(int64 total), without the int64 / double detour.
+__device__ __forceinline__ float halves_to_float(int hi_lane, int lo_lane) {
+    const float h = (float)__builtin_amdgcn_readlane(hi_lane, 63);
+    const float l = (float)__builtin_amdgcn_readlane(lo_lane, 63);
+    return (h * 65536.f + l) * FLT_SCALE;
+}
+
+__device__ __forceinline__ void wave_sum_f2(int x, int y, float& fx, float& fy) {
     x = dpp_add<0xb1, 0xf, true>(x);
     y = dpp_add<0xb1, 0xf, true>(y);
     x = dpp_add<0x4e, 0xf, true>(x);
@@ -458,10 +469,43 @@ __device__ __forceinline__ void wave_sum_exact2(int x, int y, double& sx, double
     xl = dpp_add<0x143, 0xc, false>(xl);
     yh = dpp_add<0x143, 0xc, false>(yh);
     yl = dpp_add<0x143, 0xc, false>(yl);
-    const long long tx = (long long)__builtin_amdgcn_readlane(xh, 63) * 65536 + __builtin_amdgcn_readlane(xl, 63);
-    const long long ty = (long long)__builtin_amdgcn_readlane(yh, 63) * 65536 + __builtin_amdgcn_readlane(yl, 63);
-    sx = (double)tx;
-    sy = (double)ty;
+    fx = halves_to_float(xh, xl);
+    fy = halves_to_float(yh, yl);
+}
+
+// three chains: the normal matrix (A11, A12, A22) in one pass
+__device__ __forceinline__ void wave_sum_f3(int x, int y, int z, float& fx, float& fy, float& fz) {
+    x = dpp_add<0xb1, 0xf, true>(x);
+    y = dpp_add<0xb1, 0xf, true>(y);
+    z = dpp_add<0xb1, 0xf, true>(z);
+    x = dpp_add<0x4e, 0xf, true>(x);
+    y = dpp_add<0x4e, 0xf, true>(y);
+    z = dpp_add<0x4e, 0xf, true>(z);
+    x = dpp_add<0x114, 0xf, true>(x);
+    y = dpp_add<0x114, 0xf, true>(y);
+    z = dpp_add<0x114, 0xf, true>(z);
+    int xh = x >> 16, xl = x & 0xFFFF, yh = y >> 16, yl = y & 0xFFFF, zh = z >> 16, zl = z & 0xFFFF;
+    xh = dpp_add<0x118, 0xf, true>(xh);
+    xl = dpp_add<0x118, 0xf, true>(xl);
+    yh = dpp_add<0x118, 0xf, true>(yh);
+    yl = dpp_add<0x118, 0xf, true>(yl);
+    zh = dpp_add<0x118, 0xf, true>(zh);
+    zl = dpp_add<0x118, 0xf, true>(zl);
+    xh = dpp_add<0x142, 0xa, false>(xh);
+    xl = dpp_add<0x142, 0xa, false>(xl);
+    yh = dpp_add<0x142, 0xa, false>(yh);
+    yl = dpp_add<0x142, 0xa, false>(yl);
+    zh = dpp_add<0x142, 0xa, false>(zh);
+    zl = dpp_add<0x142, 0xa, false>(zl);
+    xh = dpp_add<0x143, 0xc, false>(xh);
+    xl = dpp_add<0x143, 0xc, false>(xl);
+    yh = dpp_add<0x143, 0xc, false>(yh);
+    yl = dpp_add<0x143, 0xc, false>(yl);
+    zh = dpp_add<0x143, 0xc, false>(zh);
+    zl = dpp_add<0x143, 0xc, false>(zl);
+    fx = halves_to_float(xh, xl);
+    fy = halves_to_float(yh, yl);
+    fz = halves_to_float(zh, zl);
 }
 
 // v_dot2_i32_i16 in its VOP3P form with a register accumulator: the compiler
@@ -566,8 +610,9 @@ __global__ __launch_bounds__(256, MINW) void lk_fast_kernel(LKBatch B, LKDev p) 
     const size_t base = (size_t)seq * B.cap;
     const float* __restrict__ prev_xy = B.prev_xy + 2 * base;
     float* __restrict__ next_xy = B.next_xy + 2 * base;
-    const PyrDesc& prev = B.prev[seq];
-    const PyrDesc& next = B.next[seq];
+    // descriptors through the scalar cache (uniform per wave)
+    const cpyr prev = (cpyr)B.prev + seq;
+    const cpyr next = (cpyr)B.next + seq;
     const DerivDesc& dprev = B.dprev[seq];
     unsigned* ipair = reinterpret_cast<unsigned*>(lds + wid * S::WAVE_BYTES);
     unsigned* jreg = reinterpret_cast<unsigned*>(lds + wid * S::WAVE_BYTES + S::IBYTES);
@@ -594,8 +639,8 @@ __global__ __launch_bounds__(256, MINW) void lk_fast_kernel(LKBatch B, LKDev p) 
     const int max_level = p.max_level;
 
     for (int level = max_level; level >= 0; level--) {
-        const ImgLevel I = prev.lv[level];
-        const ImgLevel J = next.lv[level];
+        const ImgLevel I{prev->lv[level].data, prev->lv[level].w, prev->lv[level].h, prev->lv[level].pitch};
+        const ImgLevel J{next->lv[level].data, next->lv[level].w, next->lv[level].h, next->lv[level].pitch};
         const float lscale = __builtin_amdgcn_ldexpf(1.f, -level);  // == (float)(1. / (1 << level))
         float prevx = px * lscale, prevy = py * lscale;
         float nextx, nexty;
@@ -633,22 +678,28 @@ __global__ __launch_bounds__(256, MINW) void lk_fast_kernel(LKBatch B, LKDev p) 
         const int ixa = ipx & ~3;
         int jx0 = uni_i(ufloor(nextx - halfWx)) - JM, jy0 = uni_i(ufloor(nexty - halfWy)) - JM;
         int jxa = jx0 & ~3;
-        stage_bf<S::IPW, S::IPH>(ipair, sink, I, ixa, ipy, lane);
+        // window (and its +1 bilinear row/column) inside the level: I pairs and
+        // derivative pairs come straight from HBM; else REFLECT_101 staging / zeros
+        const bool full_in = ipx >= 0 && ipy >= 0 && ipx + WW < I.w && ipy + WH < I.h;
         stage_bf<S::JRW, S::JRH>(jreg, sink, J, jxa, jy0, lane);
-        u32x2a4 dv[RPG + 1];  // (Ix|Iy) at columns X, X+1 of each row: one dwordx2 load
+        unsigned P[RPG + 1];   // I(x, y) | I(x + 1, y) << 16 at the lane's column, rows r0 .. r0 + RPG
+        u32x2a4 dv[RPG + 1];   // (Ix|Iy) at columns X, X+1 of each row: one dwordx2 load
         {
             const int dpitch = dprev.pitch[level];
             gu32 dsrc = (gu32)dprev.data[level];
-            const bool full_in = ipx >= 0 && ipy >= 0 && ipx + WW < I.w && ipy + WH < I.h;
             const int X = ipx + sc;
             if (full_in) {
+                gu8 ib = (gu8)I.data + (size_t)(ipy + r0) * I.pitch + X;
                 gu32 q = dsrc + (size_t)(ipy + r0) * dpitch + X;
 #pragma unroll
                 for (int k = 0; k <= RPG; k++) {
                     const int kk = (S::FULL || r0 + k <= WH) ? k : 0;  // stay inside the window
+                    const unsigned v = *(gu16u)(ib + (size_t)kk * I.pitch);
+                    P[k] = __builtin_amdgcn_perm(0u, v, 0x0c010c00u);
                     dv[k] = *(const __attribute__((address_space(1))) u32x2a4*)(q + (size_t)kk * dpitch);
                 }
             } else {
+                stage_bf<S::IPW, S::IPH>(ipair, sink, I, ixa, ipy, lane);
                 const bool c0 = X >= 0 && X < I.w, c1 = X + 1 >= 0 && X + 1 < I.w;
 #pragma unroll
                 for (int k = 0; k <= RPG; k++) {
@@ -660,31 +711,41 @@ __global__ __launch_bounds__(256, MINW) void lk_fast_kernel(LKBatch B, LKDev p) 
                         if (c1) dv[k].y = q[1];
                     }
                 }
+                wave_lds_sync();
+                const unsigned* ip = ipair + r0 * S::IPW + (ipx - ixa) + sc;
+#pragma unroll
+                for (int k = 0; k <= RPG; k++) P[k] = ip[(S::FULL || r0 + k <= WH ? k : 0) * S::IPW];
             }
         }
         wave_lds_sync();
 
         // ---- I (x32), Ix, Iy at the lane's RPG window pixels, packed by row pairs ----
+        // Lanes outside the strip map get zero derivative weights (their Ix, Iy
+        // come out 0: rnd_d >> W_BITS == 0), so no branch per row.
         unsigned I2[NP], GX2[NP], GY2[NP];
         int a11 = 0, a12 = 0, a22 = 0;
         {
-            const unsigned* ip = ipair + r0 * S::IPW + (ipx - ixa) + sc;
+            const unsigned GW0 = strip ? IW0 : 0u, GW1 = strip ? IW1 : 0u;
             int iv[2 * NP], gx[2 * NP], gy[2 * NP];
 #pragma unroll
             for (int j = 0; j < 2 * NP; j++) iv[j] = gx[j] = gy[j] = 0;
-            unsigned P0 = ip[0];
 #pragma unroll
             for (int j = 0; j < RPG; j++) {
-                const bool valid = strip && (S::FULL || r0 + j < WH);
-                const unsigned P1 = ip[(S::FULL || r0 + j < WH ? j + 1 : 0) * S::IPW];
-                iv[j] = sdot2(P0, IW0, sdot2_r(P1, IW1, rnd_i)) >> (W_BITS - 5);
-                P0 = P1;
+                iv[j] = sdot2(P[j], IW0, sdot2_r(P[j + 1], IW1, rnd_i)) >> (W_BITS - 5);
                 const unsigned X0 = __builtin_amdgcn_perm(dv[j].y, dv[j].x, 0x05040100u);
                 const unsigned X1 = __builtin_amdgcn_perm(dv[j + 1].y, dv[j + 1].x, 0x05040100u);
                 const unsigned Y0 = __builtin_amdgcn_perm(dv[j].y, dv[j].x, 0x07060302u);
                 const unsigned Y1 = __builtin_amdgcn_perm(dv[j + 1].y, dv[j + 1].x, 0x07060302u);
-                gx[j] = valid ? sdot2(X0, IW0, sdot2_r(X1, IW1, rnd_d)) >> W_BITS : 0;
-                gy[j] = valid ? sdot2(Y0, IW0, sdot2_r(Y1, IW1, rnd_d)) >> W_BITS : 0;
+                const int gxr = sdot2(X0, GW0, sdot2_r(X1, GW1, rnd_d)) >> W_BITS;
+                const int gyr = sdot2(Y0, GW0, sdot2_r(Y1, GW1, rnd_d)) >> W_BITS;
+                if (S::FULL) {
+                    gx[j] = gxr;
+                    gy[j] = gyr;
+                } else {
+                    const int keep = -(int)(r0 + j < WH);
+                    gx[j] = gxr & keep;
+                    gy[j] = gyr & keep;
+                }
             }
 #pragma unroll
             for (int m = 0; m < NP; m++) {
@@ -696,12 +757,8 @@ __global__ __launch_bounds__(256, MINW) void lk_fast_kernel(LKBatch B, LKDev p) 
                 a22 = sdot2(GY2[m], GY2[m], a22);
             }
         }
-        double s11, s12, s22, s_unused;
-        wave_sum_exact2(a11, a12, s11, s12);
-        wave_sum_exact2(a22, 0, s22, s_unused);
-        const float A11 = (float)s11 * FLT_SCALE;
-        const float A12 = (float)s12 * FLT_SCALE;
-        const float A22 = (float)s22 * FLT_SCALE;
+        float A11, A12, A22;
+        wave_sum_f3(a11, a12, a22, A11, A12, A22);
 
         float D = A11 * A22 - A12 * A12;
         float minEig = (A22 + A11 - sqrtf((A11 - A22) * (A11 - A22) + 4.f * A12 * A12)) / (float)(2 * WW * WH);
@@ -716,21 +773,26 @@ __global__ __launch_bounds__(256, MINW) void lk_fast_kernel(LKBatch B, LKDev p) 
         nextx -= halfWx;
         nexty -= halfWy;
         float pdx = 0.f, pdy = 0.f;
+        // every top-left position of the staged region passes the image-bound test
+        bool jsafe = jx0 >= -WW && jx0 + 2 * JM < J.w && jy0 >= -WH && jy0 + 2 * JM < J.h;
         for (int j = 0; j < p.max_count; j++) {
             const int inx = uni_i(ufloor(nextx)), iny = uni_i(ufloor(nexty));
-            if (inx < -WW || inx >= J.w || iny < -WH || iny >= J.h) {
-                if (level == 0) st = 0;
-                break;
+            if (!(jsafe && (unsigned)(inx - jx0) <= 2u * JM && (unsigned)(iny - jy0) <= 2u * JM)) {
+                if (inx < -WW || inx >= J.w || iny < -WH || iny >= J.h) {
+                    if (level == 0) st = 0;
+                    break;
+                }
+                if (inx < jx0 || inx > jx0 + 2 * JM || iny < jy0 || iny > jy0 + 2 * JM) {
+                    jx0 = inx - JM;
+                    jy0 = iny - JM;
+                    jxa = jx0 & ~3;
+                    jsafe = jx0 >= -WW && jx0 + 2 * JM < J.w && jy0 >= -WH && jy0 + 2 * JM < J.h;
+                    wave_lds_sync();
+                    stage_bf<S::JRW, S::JRH>(jreg, sink, J, jxa, jy0, lane);
+                    wave_lds_sync();
+                }
             }
             itcount++;
-            if (inx < jx0 || inx > jx0 + 2 * JM || iny < jy0 || iny > jy0 + 2 * JM) {
-                jx0 = inx - JM;
-                jy0 = iny - JM;
-                jxa = jx0 & ~3;
-                wave_lds_sync();
-                stage_bf<S::JRW, S::JRH>(jreg, sink, J, jxa, jy0, lane);
-                wave_lds_sync();
-            }
             a = nextx - inx;
             b = nexty - iny;
             const int w00 = uround((1.f - a) * (1.f - b) * (1 << W_BITS));
@@ -755,10 +817,8 @@ __global__ __launch_bounds__(256, MINW) void lk_fast_kernel(LKBatch B, LKDev p) 
                     b2 = sdot2(d2, GY2[m], b2);
                 }
             }
-            double sb1, sb2;
-            wave_sum_exact2(b1, b2, sb1, sb2);
-            const float fb1 = (float)sb1 * FLT_SCALE;
-            const float fb2 = (float)sb2 * FLT_SCALE;
+            float fb1, fb2;
+            wave_sum_f2(b1, b2, fb1, fb2);
             const float dx = (A12 * fb2 - A22 * fb1) * D;
             const float dy = (A12 * fb1 - A11 * fb2) * D;
             nextx += dx;
