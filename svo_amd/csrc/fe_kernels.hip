@@ -125,7 +125,56 @@ __global__ __launch_bounds__(256) void append_kernel(AppendBatch B) {
     }
 }
 
+// RANSAC subset prefetch: the draws of RANSACPointSetRegistrator::getSubset
+// (cv::RNG(-1) MWC, uniform(0, n) = next() % n, redraw duplicates) depend only
+// on n, so the device replays them for the first `nh` hypotheses of every
+// sequence and gathers the drawn points: per hypothesis obj[5][3] then
+// img[5][2] floats. One block per sequence: lane 0 draws, the block gathers.
+__global__ __launch_bounds__(256) void ransac_sample_kernel(const int* __restrict__ counts, const float* __restrict__ obj,
+                                                            const float* __restrict__ img, int cap, int nh,
+                                                            float* __restrict__ samp) {
+    __shared__ int idx[5 * 64];
+    const int s = blockIdx.x;
+    const int n = counts[s];
+    if (n <= 5 || nh > 64) return;  // n <= 5: solved directly from all points, on the host
+    if (threadIdx.x == 0) {
+        uint64_t st = ~0ull;
+        for (int j = 0; j < nh; j++)
+            for (int i = 0; i < 5; i++) {
+                int v;
+                bool dup;
+                do {
+                    st = (uint64_t)(uint32_t)st * 4164903690u + (uint32_t)(st >> 32);
+                    v = (int)((uint32_t)st % (unsigned)n);
+                    dup = false;
+                    for (int k = 0; k < i; k++) dup |= idx[5 * j + k] == v;
+                } while (dup);
+                idx[5 * j + i] = v;
+            }
+    }
+    __syncthreads();
+    const float* o = obj + (size_t)3 * cap * s;
+    const float* im = img + (size_t)2 * cap * s;
+    float* dst = samp + (size_t)25 * nh * s;
+    for (int k = threadIdx.x; k < 5 * nh; k += blockDim.x) {
+        const int j = k / 5, i = k - 5 * j, p = idx[k];
+        float* h = dst + 25 * j;
+        h[3 * i] = o[3 * p];
+        h[3 * i + 1] = o[3 * p + 1];
+        h[3 * i + 2] = o[3 * p + 2];
+        h[15 + 2 * i] = im[2 * p];
+        h[15 + 2 * i + 1] = im[2 * p + 1];
+    }
+}
+
 }  // namespace
+
+hipError_t launch_ransac_samples(const int* counts, const float* obj, const float* img, int cap, int nh, int nseq,
+                                 float* samp, hipStream_t st) {
+    if (nh <= 0 || nh > 64) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(ransac_sample_kernel, dim3(nseq), dim3(256), 0, st, counts, obj, img, cap, nh, samp);
+    return hipGetLastError();
+}
 
 hipError_t launch_compact(const CompactBatch& b, int nseq, hipStream_t st) {
     hipLaunchKernelGGL(compact_kernel, dim3(nseq), dim3(1024), 0, st, b);

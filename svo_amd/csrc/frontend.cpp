@@ -132,11 +132,12 @@ struct svo_frontend {
     uint8_t *status, *mask;
     uint32_t *bits_all, *bits_best;
     double *map, *hyps, *rot_d, *stats;
+    float* samp;  // [s][kRansacPrefetch][kSampleFloats] RANSAC subsets gathered on the device
     // host mirrors (pinned)
     void* hmem = nullptr;
     int *h_nB, *h_nA, *h_cnt, *h_added;
     long long* h_itsum;
-    float *h_xyB, *h_obj;
+    float *h_xyB, *h_obj, *h_samp;
     double *h_hyps, *h_stats;
     uint32_t *h_bits, *h_best;
     std::vector<RansacSeq> rs;
@@ -145,6 +146,12 @@ struct svo_frontend {
     bool stats_pending = false;
     int pyr_ready = -1;  // frame index whose pyramid + Scharr were built ahead
     hipEvent_t ev_stats = nullptr;  // SQPnP statistics of the last step on the host
+    // full copies of the tracked points / map points (h_xyB, h_obj): needed only by
+    // the final fits, RANSAC past the prefetched subsets and the n <= 5 solve, so
+    // they travel on their own stream once requested
+    hipStream_t st_copy = nullptr;
+    hipEvent_t ev_gathered = nullptr, ev_full = nullptr;
+    bool full_queued = false;
     Pool* pool = nullptr;
     // pipeline: slices of the batch [g0[g], g0[g] + gn[g]) on their own streams
     int G = 1;
@@ -264,6 +271,20 @@ int fe_append(svo_frontend* fe, int t, int g0, int n, hipStream_t st) {
     return SVO_OK;
 }
 
+// Full D2H of the step's tracked points and map points (after ev_gathered), on
+// the copy stream; queued once per step, when first needed or at the step's end.
+int fe_queue_full(svo_frontend* fe) {
+    if (fe->full_queued) return SVO_OK;
+    svo_ctx* ctx = fe->ctx;
+    const size_t S = fe->S, CAP = fe->CAP;
+    SVO_HIP(ctx, hipStreamWaitEvent(fe->st_copy, fe->ev_gathered, 0));
+    SVO_HIP(ctx, hipMemcpyAsync(fe->h_xyB, fe->xyB, sizeof(float) * 2 * S * CAP, hipMemcpyDeviceToHost, fe->st_copy));
+    SVO_HIP(ctx, hipMemcpyAsync(fe->h_obj, fe->obj, sizeof(float) * 3 * S * CAP, hipMemcpyDeviceToHost, fe->st_copy));
+    SVO_HIP(ctx, hipEventRecord(fe->ev_full, fe->st_copy));
+    fe->full_queued = true;
+    return SVO_OK;
+}
+
 // Queue the SQPnP sufficient statistics of the last step's RANSAC inliers (the
 // bits are on the device since that step) on the FAST stream, then their D2H.
 int fe_queue_stats(svo_frontend* fe) {
@@ -285,6 +306,7 @@ double fe_finish_fits(svo_frontend* fe) {
     if (!fe->fits_pending) return 0.0;
     auto t0 = std::chrono::steady_clock::now();
     (void)hipEventSynchronize(fe->ev_stats);
+    if (fe->full_queued) (void)hipEventSynchronize(fe->ev_full);  // cheirality test reads h_obj
     fe->pool->run(fe->S, [&](int s) {
         RansacSeq& r = fe->rs[s];
         r.fit(fe->cfg.K, fe->h_stats + 60 * (size_t)s);
@@ -368,6 +390,7 @@ int svo_frontend_create(svo_ctx* ctx, const svo_frontend_config* cfg, svo_fronte
         add(sizeof(double) * 9 * (size_t)S * fe->T);
         add(sizeof(double) * 60 * (size_t)S);
         add(sizeof(float) * 2 * (size_t)S * CAP);               // box centres binned by band
+        add(sizeof(float) * kSampleFloats * kRansacPrefetch * (size_t)S);
         add(sizeof(int) * (size_t)S * fast_box_bands(c.height));
         add(4096);
         bytes = (size_t)p;
@@ -411,6 +434,7 @@ int svo_frontend_create(svo_ctx* ctx, const svo_frontend_config* cfg, svo_fronte
         fe->stats = carve<double>(p, 60 * (size_t)S);
         fe->box_binned = carve<float>(p, 2 * (size_t)S * CAP);
         fe->box_band = carve<int>(p, (size_t)S * fast_box_bands(c.height));
+        fe->samp = carve<float>(p, (size_t)kSampleFloats * kRansacPrefetch * S);
     }
     (void)hipMemsetAsync(fe->dmem, 0, bytes, ctx->stream);
     // host mirrors
@@ -426,6 +450,7 @@ int svo_frontend_create(svo_ctx* ctx, const svo_frontend_config* cfg, svo_fronte
         add(sizeof(uint32_t) * (size_t)S * kRansacChunk * fe->WORDS);
         add(sizeof(uint32_t) * (size_t)S * fe->WORDS);
         add(sizeof(double) * 60 * (size_t)S);
+        add(sizeof(float) * kSampleFloats * kRansacPrefetch * (size_t)S);
         add(4096);
         hbytes = (size_t)p;
     }
@@ -446,6 +471,7 @@ int svo_frontend_create(svo_ctx* ctx, const svo_frontend_config* cfg, svo_fronte
         fe->h_bits = carve<uint32_t>(p, (size_t)S * kRansacChunk * fe->WORDS);
         fe->h_best = carve<uint32_t>(p, (size_t)S * fe->WORDS);
         fe->h_stats = carve<double>(p, 60 * (size_t)S);
+        fe->h_samp = carve<float>(p, (size_t)kSampleFloats * kRansacPrefetch * S);
         std::memset(fe->h_nA, 0, sizeof(int) * S);
     }
     // derivative pyramids of the last two frames of every sequence (ping-pong)
@@ -503,6 +529,12 @@ int svo_frontend_create(svo_ctx* ctx, const svo_frontend_config* cfg, svo_fronte
         fe->ev_sync.assign(2 + 3 * G, nullptr);
         for (auto& e : fe->ev_sync) (void)hipEventCreateWithFlags(&e, hipEventDisableTiming);
         (void)hipEventCreateWithFlags(&fe->ev_stats, hipEventDisableTiming);
+        (void)hipEventCreateWithFlags(&fe->ev_gathered, hipEventDisableTiming);
+        (void)hipEventCreateWithFlags(&fe->ev_full, hipEventDisableTiming);
+        if (hipStreamCreateWithFlags(&fe->st_copy, hipStreamNonBlocking) != hipSuccess) {
+            svo_frontend_destroy(fe);
+            return set_error(ctx, SVO_ERR_HIP, "svo_frontend_create: stream");
+        }
     }
     SVO_HIP(ctx, hipMemcpyAsync(fe->d_desc, fe->desc_host.data(), sizeof(PyrDesc) * fe->desc_host.size(),
                                 hipMemcpyHostToDevice, ctx->stream));
@@ -534,6 +566,12 @@ void svo_frontend_destroy(svo_frontend* fe) {
     for (auto& e : fe->ev_sync)
         if (e) (void)hipEventDestroy(e);
     if (fe->ev_stats) (void)hipEventDestroy(fe->ev_stats);
+    if (fe->st_copy) {
+        (void)hipStreamSynchronize(fe->st_copy);
+        (void)hipStreamDestroy(fe->st_copy);
+    }
+    if (fe->ev_gathered) (void)hipEventDestroy(fe->ev_gathered);
+    if (fe->ev_full) (void)hipEventDestroy(fe->ev_full);
     delete fe;
 }
 
@@ -631,6 +669,13 @@ int svo_frontend_step(svo_frontend* fe, int t, svo_frontend_stats* stats) {
     int max_prev = 0;
     for (int s = 0; s < S; s++) max_prev = std::max(max_prev, fe->h_nA[s]);
 
+    // 0. the previous step's SQPnP statistics, queued before this step's big
+    //    launches so that the low-priority stream gets CUs before LK fills them
+    //    (the fits wait for it; the compaction below overwrites its inputs)
+    {
+        int rq = fe_queue_stats(fe);
+        if (rq) return rq;
+    }
     // 1. pyramid of frame t and its Scharr derivative pyramid (used when frame
     //    t is the prev image of the next step; OpenCV recomputes it per call)
     if (fe->pyr_ready != t) {
@@ -683,21 +728,21 @@ int svo_frontend_step(svo_frontend* fe, int t, svo_frontend_stats* stats) {
         fe->pyr_ready = tn;
     }
     TP("lk+pyr enqueued");
-    // 3a'. the previous step's SQPnP statistics (runs beside LK)
-    int rq = fe_queue_stats(fe);
-    if (rq) return rq;
     // 3a. the previous step's final pose fits, deferred to here: the host does
     //     them while the GPU tracks this frame (before this step's D2H copies
     //     are queued: the fits read the previous frame's host mirrors)
     double ms_fit = fe_finish_fits(fe);
     TP("fits done");
+    const bool prev_full = fe->full_queued;  // the compacts below wait for it
+    fe->full_queued = false;
     for (int g = 0; g < G; g++) {
         const int a = fe->g0[g], n = fe->gn[g];
         hipStream_t sg = fe->gst[g];
         int mp = 0;
         for (int s = a; s < a + n; s++) mp = std::max(mp, fe->h_nA[s]);
-        // the previous step's statistics kernel still reads xyB / obj
+        // the previous step's statistics kernel and full copy still read xyB / obj
         SVO_HIP(ctx, hipStreamWaitEvent(sg, fe->ev_stats, 0));
+        if (prev_full) SVO_HIP(ctx, hipStreamWaitEvent(sg, fe->ev_full, 0));
         CompactBatch cb{fe->nA + a, fe->status + (size_t)a * CAP, nullptr, 0, fe->next_xy + 2 * (size_t)a * CAP,
                         fe->midA + (size_t)a * CAP, fe->iters + (size_t)a * CAP, fe->itsum + a,
                         fe->xyB + 2 * (size_t)a * CAP, fe->midB + (size_t)a * CAP, fe->nB + a, CAP};
@@ -708,14 +753,20 @@ int svo_frontend_step(svo_frontend* fe, int t, svo_frontend_stats* stats) {
         SVO_HIP(ctx, launch_gather(fe->nB + a, fe->midB + (size_t)a * CAP, fe->map + 3 * (size_t)a * fe->MAPCAP, CAP,
                                    fe->MAPCAP, fe->obj + 3 * (size_t)a * CAP, n, mp, sg));
         ph_end(fe, sg, slot);
+        // the RANSAC subsets of the first hypotheses, gathered here: the host needs
+        // ~100 B per hypothesis instead of the whole point set
+        const size_t sfl = (size_t)kSampleFloats * kRansacPrefetch;
+        SVO_HIP(ctx, launch_ransac_samples(fe->nB + a, fe->obj + 3 * (size_t)a * CAP, fe->xyB + 2 * (size_t)a * CAP,
+                                           CAP, kRansacPrefetch, n, fe->samp + sfl * a, sg));
         SVO_HIP(ctx, hipMemcpyAsync(fe->h_nB + a, fe->nB + a, sizeof(int) * n, hipMemcpyDeviceToHost, sg));
         SVO_HIP(ctx, hipMemcpyAsync(fe->h_itsum + a, fe->itsum + a, sizeof(long long) * n, hipMemcpyDeviceToHost, sg));
-        SVO_HIP(ctx, hipMemcpyAsync(fe->h_xyB + 2 * (size_t)a * CAP, fe->xyB + 2 * (size_t)a * CAP,
-                                    sizeof(float) * 2 * n * (size_t)CAP, hipMemcpyDeviceToHost, sg));
-        SVO_HIP(ctx, hipMemcpyAsync(fe->h_obj + 3 * (size_t)a * CAP, fe->obj + 3 * (size_t)a * CAP,
-                                    sizeof(float) * 3 * n * (size_t)CAP, hipMemcpyDeviceToHost, sg));
+        SVO_HIP(ctx, hipMemcpyAsync(fe->h_samp + sfl * a, fe->samp + sfl * a, sizeof(float) * sfl * n,
+                                    hipMemcpyDeviceToHost, sg));
         SVO_HIP(ctx, hipEventRecord(fe->ev_sync[3 + 2 * g], sg));
     }
+    // every slice's points are gathered once the last slice's copies are queued
+    // (slices run in order on their streams; the full copy waits for the last)
+    SVO_HIP(ctx, hipEventRecord(fe->ev_gathered, fe->gst[G - 1]));
 
     // 3b. mask around frame t-1's features (the reference masks with prevFrame's
     //     features, R:src/tracking.cpp:77) + FAST/bucket on frame t, whole batch,
@@ -748,16 +799,40 @@ int svo_frontend_step(svo_frontend* fe, int t, svo_frontend_stats* stats) {
         TP("lk results on host");
         ms_wait += ms_since(tw);
         int max_b = 0;
+        bool need_full = false;
         for (int s = a; s < a + n; s++) {
-            fe->rs[s].begin(fe->h_obj + 3 * (size_t)s * CAP, fe->h_xyB + 2 * (size_t)s * CAP, fe->h_nB[s],
-                            c.pnp_iterations);
+            RansacSeq& r = fe->rs[s];
+            r.begin(fe->h_obj + 3 * (size_t)s * CAP, fe->h_xyB + 2 * (size_t)s * CAP, fe->h_nB[s], c.pnp_iterations);
+            r.samp = fe->h_samp + (size_t)kSampleFloats * kRansacPrefetch * s;
+            r.nsamp = kRansacPrefetch;
+            need_full |= r.direct && !r.done;  // n <= 5: EPnP on all points
             max_b = std::max(max_b, fe->h_nB[s]);
+        }
+        bool have_full = false;
+        auto ensure_full = [&]() -> int {
+            if (have_full) return SVO_OK;
+            int rf = fe_queue_full(fe);
+            if (rf) return rf;
+            SVO_HIP(ctx, hipEventSynchronize(fe->ev_full));
+            have_full = true;
+            return SVO_OK;
+        };
+        if (need_full) {
+            int rf = ensure_full();
+            if (rf) return rf;
         }
         for (;;) {
             // sequences still sampling (no pool dispatch once all are done)
             bool any = false;
-            for (int s = a; s < a + n; s++) any |= !fe->rs[s].done && !fe->rs[s].direct;
+            for (int s = a; s < a + n; s++) {
+                any |= !fe->rs[s].done && !fe->rs[s].direct;
+                need_full |= fe->rs[s].next_end() > fe->rs[s].nsamp;
+            }
             if (!any) break;
+            if (need_full) {  // past the prefetched subsets (> 26 hypotheses): rare
+                int rf = ensure_full();
+                if (rf) return rf;
+            }
             auto th = clk::now();
             fe->pool->run(n, [&](int i) { ms[a + i] = fe->rs[a + i].gen_chunk(c.K); });
             TP("hyps generated");
@@ -836,6 +911,8 @@ int svo_frontend_step(svo_frontend* fe, int t, svo_frontend_stats* stats) {
         SVO_HIP(ctx, hipMemcpyAsync(fe->h_added + a, fe->added + a, sizeof(int) * n, hipMemcpyDeviceToHost, sg));
     }
     fe->fits_pending = true;  // statistics land with the stream syncs below
+    rc = fe_queue_full(fe);    // for the fits (cheirality test), off the critical path
+    if (rc) return rc;
     TP("tail enqueued");
     // only the slices' streams: the statistics (FAST stream) and the next
     // frame's pyramid (main stream) keep running into the next step

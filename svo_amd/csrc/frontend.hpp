@@ -23,6 +23,12 @@ hipError_t launch_compact(const CompactBatch& b, int nseq, hipStream_t st);
 hipError_t launch_gather(const int* n, const int* mid, const double* map, int cap, int map_cap, float* obj,
                          int nseq, int max_n, hipStream_t st);
 
+// The 5-point subsets of the first nh (<= 64) RANSAC hypotheses of every
+// sequence (cv::RNG(-1) draws over counts[s] points), gathered as obj[5][3] +
+// img[5][2] floats per hypothesis into samp[s][nh][25].
+hipError_t launch_ransac_samples(const int* counts, const float* obj, const float* img, int cap, int nh, int nseq,
+                                 float* samp, hipStream_t st);
+
 struct AppendBatch {
     int* n;             // features per sequence (in/out)
     float* xy;          // [s][cap] xy

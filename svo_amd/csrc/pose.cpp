@@ -227,15 +227,27 @@ void RansacSeq::begin(const float* o, const float* im, int npts, int iterations)
     direct = n <= 5;
     done = n < 4;
     ok = false;
+    samp = nullptr;
+    nsamp = 0;
+}
+
+static int chunk_size(int rounds) {
+    // chunk schedule 2, 8, 16, 16, ...: below ~1 % outliers RANSACUpdateNumIters
+    // (p 0.999, 5 points) brings niters down to 2 after the first accepted
+    // hypothesis, so one round suffices; above, round 2 covers up to 10
+    return rounds == 0 ? 2 : rounds == 1 ? 8 : kRansacChunk;
+}
+
+int RansacSeq::next_end() const {
+    if (done || direct) return nh;
+    const int sched = chunk_size(rounds);
+    return nh + ((niters - iter) < sched ? (niters - iter) : sched);
 }
 
 int RansacSeq::gen_chunk(const double K[9]) {
     m = 0;
     if (done || direct) return 0;
-    // chunk schedule 2, 8, 16, 16, ...: below ~1 % outliers RANSACUpdateNumIters
-    // (p 0.999, 5 points) brings niters down to 2 after the first accepted
-    // hypothesis, so one round suffices; above, round 2 covers up to 10
-    const int sched = rounds == 0 ? 2 : rounds == 1 ? 8 : kRansacChunk;
+    const int sched = chunk_size(rounds);
     const int want = (niters - iter) < sched ? (niters - iter) : sched;
     rounds++;
     Rng r{rng};
@@ -252,7 +264,13 @@ int RansacSeq::gen_chunk(const double K[9]) {
             idx[i] = v;
         }
         double Rj[9], tj[3], rv[3];
-        valid[j] = epnp_pixels(obj, img, idx, 5, K, Rj, tj);
+        const int h = nh + j;
+        if (h < nsamp) {  // the same 5 points, gathered on the device in draw order
+            const float* sp = samp + (size_t)kSampleFloats * h;
+            valid[j] = epnp_pixels(sp, sp + 15, nullptr, 5, K, Rj, tj);
+        } else {
+            valid[j] = epnp_pixels(obj, img, idx, 5, K, Rj, tj);
+        }
         double* hp = hyp + 12 * j;
         if (valid[j]) {
             la::rodrigues_inv(Rj, rv);  // the model is stored as (rvec, tvec)

@@ -16,6 +16,10 @@ struct Rng {  // cv::RNG (core/include/opencv2/core/operations.hpp): multiply-wi
 };
 
 constexpr int kRansacChunk = 16;  // hypotheses generated per scoring launch
+// hypotheses whose 5-point subsets the device gathers ahead of the host RANSAC
+// (chunk schedule 2 + 8 + 16): the host then needs no full copy of the points
+constexpr int kRansacPrefetch = 26;
+constexpr int kSampleFloats = 25;  // 5 points x (obj xyz, pixel xy)
 
 // RANSACPointSetRegistrator::run for PnP (5-point EPnP kernel), split so the
 // hypotheses of many sequences are scored by one batched kernel launch:
@@ -23,6 +27,11 @@ constexpr int kRansacChunk = 16;  // hypotheses generated per scoring launch
 struct RansacSeq {
     const float* obj = nullptr;  // n x 3 (float, as OpenCV converts Point3d)
     const float* img = nullptr;  // n x 2
+    // optional: the subsets of hypotheses [0, nsamp) gathered by the device, in
+    // draw order (kSampleFloats per hypothesis); obj / img are then only read
+    // for hypotheses past nsamp, the n <= 5 direct solve and the final fit
+    const float* samp = nullptr;
+    int nsamp = 0;
     int n = 0;
     uint64_t rng = 0;
     int niters = 0, iter = 0, maxGood = 0, nh = 0, m = 0, rounds = 0;
@@ -36,6 +45,9 @@ struct RansacSeq {
 
     void begin(const float* obj, const float* img, int n, int iterations);
     int gen_chunk(const double K[9]);  // fills hyp[0..m) (R row-major + t); returns m
+    // hypotheses generated once the next gen_chunk has run (for deciding whether
+    // the full point arrays must be on the host first)
+    int next_end() const;
     void consume(const int* counts, const uint32_t* bits, int words_cap, double confidence);
     // inlier set of the best model (the output): `best` bits, and the index list
     // too unless list = false (fit() then builds it)
