@@ -226,20 +226,50 @@ __global__ __launch_bounds__(256) void fast_detect_kernel(FastDetBatch B, int th
         }
     }
     __syncthreads();
-    // phase A: segment test for every score-region pixel; corners are queued
-    // (wave-aggregated LDS append) so that the expensive cornerScore runs only on
-    // them with full waves instead of in nearly every (divergent) wave
-    __shared__ uint16_t CQ[FD_SH * FD_SW];
-    __shared__ int ncq;
-    if (tid == 0) ncq = 0;
+    // phase A0: OpenCV FAST_t's first pre-test as a necessary condition: a 9-arc
+    // of the 16-ring holds one pixel of each antipodal pair, so a corner has
+    // (b0 | b8) & (b4 | b12) for "brighter" or the same for "darker" on the
+    // compass pixels. Only survivors (a small fraction: flat areas and straight
+    // edges fail) are queued for the full 16-pixel test, which then runs with
+    // full waves (phase A1); corners are queued again for the score (phase B).
+    constexpr int NSC = FD_SH * FD_SW;
+    __shared__ uint16_t CQ[NSC], CQ1[NSC];
+    __shared__ int ncq, ncq1;
+    if (tid == 0) ncq = ncq1 = 0;
     __syncthreads();
-    for (int base = 0; base < FD_SH * FD_SW; base += 256) {
+    for (int base = 0; base < NSC; base += 256) {
         const int k = base + tid;
         const int r = k / FD_SW, c = k - r * FD_SW;
         const int y = y0 - 1 + r, x = x0 - 1 + c;
+        bool cand = false;
+        if (k < NSC && x >= 3 && x < w - 3 && y >= 3 && y < h - 3) {
+            const int ty = r + 3, tx = c + 3;
+            const int v = T[ty][tx], hi = v + threshold, lo = v - threshold;
+            const int p0 = T[ty + 3][tx], p8 = T[ty - 3][tx], p4 = T[ty][tx + 3], p12 = T[ty][tx - 3];
+            const bool bright = (p0 > hi || p8 > hi) && (p4 > hi || p12 > hi);
+            const bool dark = (p0 < lo || p8 < lo) && (p4 < lo || p12 < lo);
+            cand = bright || dark;
+        }
+        if (k < NSC) SC[r][c] = 0;
+        const unsigned long long bal = __ballot(cand);
+        if (bal) {
+            int qb = 0;
+            if ((tid & 63) == 0) qb = atomicAdd(&ncq1, __popcll(bal));
+            qb = __builtin_amdgcn_readfirstlane(qb);
+            if (cand) CQ1[qb + __popcll(bal & ((1ull << (tid & 63)) - 1ull))] = (uint16_t)k;
+        }
+    }
+    __syncthreads();
+    // phase A1: full segment test of the candidates
+    const int nq1 = ncq1;
+    for (int base = 0; base < nq1; base += 256) {
+        const int i = base + tid;
         bool corner = false;
-        if (k < FD_SH * FD_SW && x >= 3 && x < w - 3 && y >= 3 && y < h - 3) {
-            const int ty = r + 3, tx = c + 3;  // image-tile coords of (x, y)
+        int k = 0;
+        if (i < nq1) {
+            k = CQ1[i];
+            const int r = k / FD_SW, c = k - r * FD_SW;
+            const int ty = r + 3, tx = c + 3;
             const int v = T[ty][tx];
             unsigned bright = 0, dark = 0;
 #pragma unroll
@@ -249,18 +279,18 @@ __global__ __launch_bounds__(256) void fast_detect_kernel(FastDetBatch B, int th
                 dark |= (unsigned)(rv < v - threshold) << q;
             }
             corner = run9(bright) || run9(dark);
+            if (corner) {
+                const int r2 = k / FD_SW, c2 = k - r2 * FD_SW;
+                SC[r2][c2] = 0x100;
+            }
         }
-        if (k < FD_SH * FD_SW) SC[r][c] = corner ? 0x100 : 0;
         if (nonmax) {
             const unsigned long long bal = __ballot(corner);
             if (bal) {
                 int qb = 0;
                 if ((tid & 63) == 0) qb = atomicAdd(&ncq, __popcll(bal));
                 qb = __builtin_amdgcn_readfirstlane(qb);
-                if (corner) {
-                    const int pos = qb + __popcll(bal & ((1ull << (tid & 63)) - 1ull));
-                    CQ[pos] = (uint16_t)k;
-                }
+                if (corner) CQ[qb + __popcll(bal & ((1ull << (tid & 63)) - 1ull))] = (uint16_t)k;
             }
         }
     }
@@ -314,27 +344,40 @@ __global__ __launch_bounds__(256) void fast_detect_kernel(FastDetBatch B, int th
     const int lane = tid & 63, wv = tid >> 6;
     const int x = x0 + lane;
     const uint8_t* __restrict__ mask = B.mask ? B.mask + seq * B.npx : nullptr;
+    // per row: the keep bits of the tile's 64 columns; one wave then writes all
+    // rows' bit words and count atomics with single vector instructions
+    __shared__ unsigned long long RB[FD_TY];
 #pragma unroll
     for (int i = 0; i < FD_TY / 4; i++) {
         const int r = wv * (FD_TY / 4) + i;
         const int y = y0 + r;
-        if (y >= h) break;
         const int c = lane + 1, rr = r + 1;
         const unsigned v = SC[rr][c];
-        bool keep = (v & 0x100) != 0 && x < w;
-        if (keep && nonmax) {
-            const int s = v & 0xFF;
-            keep = s > (SC[rr][c - 1] & 0xFF) && s > (SC[rr][c + 1] & 0xFF) && s > (SC[rr - 1][c - 1] & 0xFF) &&
-                   s > (SC[rr - 1][c] & 0xFF) && s > (SC[rr - 1][c + 1] & 0xFF) && s > (SC[rr + 1][c - 1] & 0xFF) &&
-                   s > (SC[rr + 1][c] & 0xFF) && s > (SC[rr + 1][c + 1] & 0xFF);
+        bool keep = (v & 0x100) != 0 && x < w && y < h;
+        if (nonmax) {
+            // strict maximum over the 8 neighbours' score bytes (non-corners score 0),
+            // branch-free: byte reads of the low halves + max3
+            auto sb = [&](int y2, int x2) { return (int)reinterpret_cast<const uint8_t*>(&SC[y2][x2])[0]; };
+            int m = max(max(sb(rr, c - 1), sb(rr, c + 1)), sb(rr - 1, c - 1));
+            m = max(max(m, sb(rr - 1, c)), sb(rr - 1, c + 1));
+            m = max(max(m, sb(rr + 1, c - 1)), sb(rr + 1, c));
+            m = max(m, sb(rr + 1, c + 1));
+            keep = keep && (int)(v & 0xFF) > m;
         }
-        if (keep && mask && mask[(size_t)y * w + x] == 0) keep = false;
-        if (boxes && !((TM[r] >> lane) & 1ull)) keep = false;
+        if (mask) {  // host mask (svo_fast_detect): runByPixelsMask
+            const int yy = y < h ? y : h - 1, xx = x < w ? x : w - 1;
+            keep = keep && mask[(size_t)yy * w + xx] != 0;
+        }
+        if (boxes) keep = keep && ((TM[r] >> lane) & 1ull);
         const unsigned long long bal = __ballot(keep);
-        if (lane == 0) {
-            B.bits[(seq * h + y) * B.nseg + blockIdx.x] = bal;
-            if (bal) atomicAdd(&B.rowcnt[seq * h + y], __popcll(bal));
-        }
+        if (lane == 0) RB[r] = bal;
+    }
+    __syncthreads();
+    if (tid < FD_TY && y0 + tid < h) {
+        const unsigned long long bal = RB[tid];
+        const size_t row = seq * h + y0 + tid;
+        B.bits[row * B.nseg + blockIdx.x] = bal;
+        if (bal) atomicAdd(&B.rowcnt[row], __popcll(bal));
     }
 }
 
@@ -486,14 +529,21 @@ hipError_t launch_fast_detect(const FastDetBatch& b, int nseq, int w, int h, int
                               hipStream_t st) {
     hipError_t e = hipMemsetAsync(b.rowcnt, 0, sizeof(int) * (size_t)h * nseq, st);
     if (e != hipSuccess) return e;
-    if (b.box_pts) {
-        if ((h + 15) / 16 > 1024) return hipErrorInvalidValue;
-        hipLaunchKernelGGL(box_bin_kernel, dim3(nseq), dim3(256), 0, st, b, h);
+    if (b.box_pts && !b.box_prebinned) {
+        e = launch_box_bin(b, nseq, h, st);
+        if (e != hipSuccess) return e;
     }
     dim3 grid((w + FD_TX - 1) / FD_TX, (h + FD_TY - 1) / FD_TY, nseq);
     hipLaunchKernelGGL(fast_detect_kernel, grid, dim3(256), 0, st, b, threshold, nonmax);
     hipLaunchKernelGGL(fast_scan_kernel, dim3(nseq), dim3(1024), 0, st, b, h);
     hipLaunchKernelGGL(fast_emit_kernel, dim3(h, nseq), dim3(64), 0, st, b, threshold, nonmax);
+    return hipGetLastError();
+}
+
+hipError_t launch_box_bin(const FastDetBatch& b, int nseq, int h, hipStream_t st) {
+    if (!b.box_pts) return hipSuccess;
+    if ((h + 15) / 16 > 1024) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(box_bin_kernel, dim3(nseq), dim3(256), 0, st, b, h);
     return hipGetLastError();
 }
 

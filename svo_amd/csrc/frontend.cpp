@@ -33,16 +33,25 @@ namespace svo {
 
 namespace {
 
-// Minimal persistent pool for the per-sequence host work (RANSAC).
+// Persistent pool for the per-sequence host work (RANSAC hypotheses, pose fits).
+// It runs a couple of times per step, microseconds apart: workers busy-poll a
+// generation counter for a while after each job (spin_us, SVO_POOL_SPIN_US)
+// before sleeping on a condition variable, so a dispatch normally costs no
+// futex wake-up. The caller works too and spins on a counter of finished TASKS
+// (a worker that wakes late with nothing left to take is not waited for).
+// Tasks are claimed by CAS on (generation << 32 | index), so a worker still
+// holding an old generation can never take (or skip) a task of a newer job.
 class Pool {
    public:
     explicit Pool(int n) {
+        const char* e = std::getenv("SVO_POOL_SPIN_US");
+        spin_us_ = e ? std::atof(e) : 3000.0;
         for (int i = 0; i < n; i++) th_.emplace_back([this] { loop(); });
     }
     ~Pool() {
         {
             std::lock_guard<std::mutex> g(mu_);
-            stop_ = true;
+            stop_.store(true);
         }
         cv_.notify_all();
         for (auto& t : th_) t.join();
@@ -53,51 +62,69 @@ class Pool {
             for (int i = 0; i < n; i++) fn(i);
             return;
         }
+        const uint64_t g = gen_.load(std::memory_order_relaxed) + 1;
+        fn_ = &fn;
+        n_.store(n, std::memory_order_relaxed);
+        done_.store(0, std::memory_order_relaxed);
+        next_.store(g << 32, std::memory_order_release);  // publishes fn_ / n_ to claimers
         {
-            std::lock_guard<std::mutex> g(mu_);
-            fn_ = &fn;
-            n_ = n;
-            next_.store(0);
-            pending_ = (int)th_.size();
-            gen_++;
+            std::lock_guard<std::mutex> lk(mu_);
+            gen_.store(g, std::memory_order_release);
         }
-        cv_.notify_all();
-        work();
-        std::unique_lock<std::mutex> lk(mu_);
-        done_cv_.wait(lk, [this] { return pending_ == 0; });
-        fn_ = nullptr;
+        if (sleeping_.load(std::memory_order_acquire) > 0) cv_.notify_all();
+        work(g);
+        while (done_.load(std::memory_order_acquire) < n) pause();
     }
 
    private:
-    void work() {
+    static void pause() {
+#if defined(__x86_64__)
+        __builtin_ia32_pause();
+#endif
+    }
+    void work(uint64_t g) {
         for (;;) {
-            int i = next_.fetch_add(1);
-            if (i >= n_) break;
-            (*fn_)(i);
+            uint64_t v = next_.load(std::memory_order_acquire);
+            if ((v >> 32) != g || (int)(v & 0xffffffffu) >= n_.load(std::memory_order_relaxed)) return;
+            if (!next_.compare_exchange_weak(v, v + 1, std::memory_order_acq_rel)) continue;
+            (*fn_)((int)(v & 0xffffffffu));
+            done_.fetch_add(1, std::memory_order_acq_rel);
         }
     }
     void loop() {
         uint64_t seen = 0;
         for (;;) {
-            {
-                std::unique_lock<std::mutex> lk(mu_);
-                cv_.wait(lk, [&] { return stop_ || gen_ != seen; });
-                if (stop_) return;
-                seen = gen_;
+            const auto t0 = std::chrono::steady_clock::now();
+            int k = 0;
+            while (gen_.load(std::memory_order_acquire) == seen && !stop_.load(std::memory_order_relaxed)) {
+                pause();
+                if (++k == 256) {
+                    k = 0;
+                    if (std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count() >
+                        spin_us_)
+                        break;
+                }
             }
-            work();
-            std::lock_guard<std::mutex> g(mu_);
-            if (--pending_ == 0) done_cv_.notify_all();
+            if (gen_.load(std::memory_order_acquire) == seen && !stop_.load()) {
+                std::unique_lock<std::mutex> lk(mu_);
+                sleeping_.fetch_add(1);
+                cv_.wait(lk, [&] { return stop_.load() || gen_.load() != seen; });
+                sleeping_.fetch_sub(1);
+            }
+            if (stop_.load()) return;
+            seen = gen_.load(std::memory_order_acquire);
+            work(seen);
         }
     }
     std::vector<std::thread> th_;
     std::mutex mu_;
-    std::condition_variable cv_, done_cv_;
+    std::condition_variable cv_;
     const std::function<void(int)>* fn_ = nullptr;
-    std::atomic<int> next_{0};
-    int n_ = 0, pending_ = 0;
-    uint64_t gen_ = 0;
-    bool stop_ = false;
+    std::atomic<int> n_{0};
+    std::atomic<uint64_t> next_{0}, gen_{0};
+    std::atomic<int> done_{0}, sleeping_{0};
+    std::atomic<bool> stop_{false};
+    double spin_us_ = 3000.0;
 };
 
 constexpr int kPhases = 9;
@@ -141,6 +168,7 @@ struct svo_frontend {
     double *h_hyps, *h_stats;
     uint32_t *h_bits, *h_best;
     std::vector<RansacSeq> rs;
+    std::vector<int> pred_iters;  // [s] RANSAC hypotheses the last frame's outlier ratio implies
     std::vector<double> pose;  // [s][6]
     bool fits_pending = false;
     bool stats_pending = false;
@@ -217,9 +245,7 @@ T* carve(char*& p, size_t count) {
     return r;
 }
 
-int fe_fast_and_bucket(svo_frontend* fe, const PyrDesc* descs_cur, bool use_mask, hipStream_t st) {
-    svo_ctx* ctx = fe->ctx;
-    int slot;
+FastDetBatch fe_fast_batch(svo_frontend* fe, const PyrDesc* descs_cur, bool use_mask) {
     FastDetBatch fb{descs_cur, nullptr, fe->fbits, fe->rowcnt, fe->rowoff,
                     (svo_keypoint*)fe->kps, fe->kn, fe->npx, (fe->W + 63) / 64, fe->KCAP};
     if (use_mask) {  // boxes around the previous frame's features, rasterised per FAST tile
@@ -230,6 +256,15 @@ int fe_fast_and_bucket(svo_frontend* fe, const PyrDesc* descs_cur, bool use_mask
         fb.box_binned = fe->box_binned;
         fb.box_band = fe->box_band;
     }
+    return fb;
+}
+
+int fe_fast_and_bucket(svo_frontend* fe, const PyrDesc* descs_cur, bool use_mask, hipStream_t st,
+                       bool prebinned = false) {
+    svo_ctx* ctx = fe->ctx;
+    int slot;
+    FastDetBatch fb = fe_fast_batch(fe, descs_cur, use_mask);
+    fb.box_prebinned = prebinned;
     ph_begin(fe, PH_FAST, st, &slot);
     SVO_HIP(ctx, launch_fast_detect(fb, fe->S, fe->W, fe->H, fe->cfg.fast_threshold, fe->cfg.fast_nonmax, st));
     ph_end(fe, st, slot);
@@ -496,6 +531,7 @@ int svo_frontend_create(svo_ctx* ctx, const svo_frontend_config* cfg, svo_fronte
         SVO_HIP(ctx, hipStreamSynchronize(ctx->stream));
     }
     fe->rs.resize(S);
+    fe->pred_iters.assign(S, 0);
     fe->pose.assign((size_t)S * 6, 0.0);
     int nt = c.host_threads > 0 ? c.host_threads : (int)std::thread::hardware_concurrency();
     nt = std::max(1, std::min({nt, S, 16}));
@@ -675,6 +711,9 @@ int svo_frontend_step(svo_frontend* fe, int t, svo_frontend_stats* stats) {
     {
         int rq = fe_queue_stats(fe);
         if (rq) return rq;
+        // the FAST mask's box centres (frame t-1's features) binned by band, also
+        // ahead: only FAST itself waits for LK
+        SVO_HIP(ctx, launch_box_bin(fe_fast_batch(fe, dcur, true), S, fe->H, fe->st_fast));
     }
     // 1. pyramid of frame t and its Scharr derivative pyramid (used when frame
     //    t is the prev image of the next step; OpenCV recomputes it per call)
@@ -774,7 +813,7 @@ int svo_frontend_step(svo_frontend* fe, int t, svo_frontend_stats* stats) {
     //     the GPU while the host solves RANSAC (and does not slow LK down)
     hipStream_t sf = fe->st_fast;
     SVO_HIP(ctx, hipStreamWaitEvent(sf, fe->ev_sync[2 + 2 * (G - 1)], 0));
-    int rc = fe_fast_and_bucket(fe, dcur, true, sf);
+    int rc = fe_fast_and_bucket(fe, dcur, true, sf, true);
     if (rc) return rc;
     SVO_HIP(ctx, hipEventRecord(ev_fast, sf));
 
@@ -805,6 +844,9 @@ int svo_frontend_step(svo_frontend* fe, int t, svo_frontend_stats* stats) {
             r.begin(fe->h_obj + 3 * (size_t)s * CAP, fe->h_xyB + 2 * (size_t)s * CAP, fe->h_nB[s], c.pnp_iterations);
             r.samp = fe->h_samp + (size_t)kSampleFloats * kRansacPrefetch * s;
             r.nsamp = kRansacPrefetch;
+            // first chunk sized by the hypotheses the previous frame's outlier ratio
+            // implies (a prediction only: a short chunk costs one more scoring round)
+            r.first_chunk = std::max(2, fe->pred_iters[s]);
             need_full |= r.direct && !r.done;  // n <= 5: EPnP on all points
             max_b = std::max(max_b, fe->h_nB[s]);
         }
@@ -890,6 +932,11 @@ int svo_frontend_step(svo_frontend* fe, int t, svo_frontend_stats* stats) {
                 for (int k = 0; k < r.n; k++) b[k >> 5] |= 1u << (k & 31);
             }
             inl += r.ok ? (int64_t)r.maxGood : r.n;
+            fe->pred_iters[s] = (r.ok && r.n > 0)
+                                    ? std::max(1, RansacSeq::predict_iters(c.pnp_confidence,
+                                                                           (double)(r.n - r.maxGood) / r.n,
+                                                                           c.pnp_iterations))
+                                    : 0;
         }
         ms_fit += ms_since(tf);
         SVO_HIP(ctx, hipMemcpyAsync(fe->bits_best + (size_t)a * fe->WORDS, fe->h_best + (size_t)a * fe->WORDS,

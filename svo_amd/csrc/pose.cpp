@@ -231,23 +231,29 @@ void RansacSeq::begin(const float* o, const float* im, int npts, int iterations)
     nsamp = 0;
 }
 
-static int chunk_size(int rounds) {
-    // chunk schedule 2, 8, 16, 16, ...: below ~1 % outliers RANSACUpdateNumIters
-    // (p 0.999, 5 points) brings niters down to 2 after the first accepted
-    // hypothesis, so one round suffices; above, round 2 covers up to 10
-    return rounds == 0 ? 2 : rounds == 1 ? 8 : kRansacChunk;
+// chunk schedule first, 8, 16, 16, ...: first defaults to 2 (below ~1 % outliers
+// RANSACUpdateNumIters (p 0.999, 5 points) brings niters down to 2 after the first
+// accepted hypothesis, below ~0.6 % to 1, so one round suffices); above, round 2
+// covers up to 10
+static int chunk_size(int rounds, int first) {
+    if (rounds == 0) return first > 0 ? (first < kRansacChunk ? first : kRansacChunk) : 2;
+    return rounds == 1 ? 8 : kRansacChunk;
+}
+
+int RansacSeq::predict_iters(double confidence, double ep, int max_iters) {
+    return update_num_iters(confidence, ep, 5, max_iters);
 }
 
 int RansacSeq::next_end() const {
     if (done || direct) return nh;
-    const int sched = chunk_size(rounds);
+    const int sched = chunk_size(rounds, first_chunk);
     return nh + ((niters - iter) < sched ? (niters - iter) : sched);
 }
 
 int RansacSeq::gen_chunk(const double K[9]) {
     m = 0;
     if (done || direct) return 0;
-    const int sched = chunk_size(rounds);
+    const int sched = chunk_size(rounds, first_chunk);
     const int want = (niters - iter) < sched ? (niters - iter) : sched;
     rounds++;
     Rng r{rng};

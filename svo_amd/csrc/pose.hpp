@@ -35,6 +35,9 @@ struct RansacSeq {
     int n = 0;
     uint64_t rng = 0;
     int niters = 0, iter = 0, maxGood = 0, nh = 0, m = 0, rounds = 0;
+    // size of the first hypothesis chunk (a scheduling choice only: the draws and
+    // the accept replay are the same for any chunking). 0: the default 2.
+    int first_chunk = 0;
     bool done = true, direct = false, ok = false, fitted = false;
     bool valid[kRansacChunk];
     double hyp[12 * kRansacChunk];
@@ -44,6 +47,9 @@ struct RansacSeq {
     double rvec[3] = {0, 0, 0}, tvec[3] = {0, 0, 0};
 
     void begin(const float* obj, const float* img, int n, int iterations);
+    // RANSACUpdateNumIters' niters for outlier ratio ep: a prediction of how many
+    // hypotheses this sequence needs, from its previous frame
+    static int predict_iters(double confidence, double ep, int max_iters);
     int gen_chunk(const double K[9]);  // fills hyp[0..m) (R row-major + t); returns m
     // hypotheses generated once the next gen_chunk has run (for deciding whether
     // the full point arrays must be on the host first)
