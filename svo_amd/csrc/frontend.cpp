@@ -167,6 +167,14 @@ struct svo_frontend {
     float *h_xyB, *h_obj, *h_samp;
     double *h_hyps, *h_stats;
     uint32_t *h_bits, *h_best;
+    // host-coherent buffers the scoring kernel reads / writes directly (zero-copy:
+    // no H2D of the hypotheses, no D2H of bits / counts, no count memset)
+    void* zmem = nullptr;
+    double* z_hyps = nullptr;     // [s][kRansacChunk][12]
+    uint32_t* z_bits = nullptr;   // [s][kRansacChunk][WORDS]
+    int* z_wcnt = nullptr;        // [s][kRansacChunk][WS] inliers per wave of 64 points
+    int WS = 0;
+    bool zero_copy = true;
     std::vector<RansacSeq> rs;
     std::vector<int> pred_iters;  // [s] RANSAC hypotheses the last frame's outlier ratio implies
     std::vector<double> pose;  // [s][6]
@@ -509,6 +517,26 @@ int svo_frontend_create(svo_ctx* ctx, const svo_frontend_config* cfg, svo_fronte
         fe->h_samp = carve<float>(p, (size_t)kSampleFloats * kRansacPrefetch * S);
         std::memset(fe->h_nA, 0, sizeof(int) * S);
     }
+    // zero-copy scoring buffers (coherent: the kernel's writes are visible to the
+    // host once the stream is synchronised)
+    {
+        const char* e = std::getenv("SVO_FE_ZEROCOPY");
+        fe->zero_copy = !(e && e[0] == '0');
+        fe->WS = (CAP + 63) / 64;
+        const size_t zb = ((sizeof(double) * 12 * (size_t)S * kRansacChunk + 255) & ~(size_t)255) +
+                          ((sizeof(uint32_t) * (size_t)S * kRansacChunk * fe->WORDS + 255) & ~(size_t)255) +
+                          sizeof(int) * (size_t)S * kRansacChunk * fe->WS;
+        if (fe->zero_copy && hipHostMalloc(&fe->zmem, zb, hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess) {
+            fe->zmem = nullptr;
+            fe->zero_copy = false;
+        }
+        if (fe->zero_copy) {
+            char* p = (char*)fe->zmem;
+            fe->z_hyps = carve<double>(p, 12 * (size_t)S * kRansacChunk);
+            fe->z_bits = carve<uint32_t>(p, (size_t)S * kRansacChunk * fe->WORDS);
+            fe->z_wcnt = carve<int>(p, (size_t)S * kRansacChunk * fe->WS);
+        }
+    }
     // derivative pyramids of the last two frames of every sequence (ping-pong)
     {
         size_t doff[kMaxLevels];
@@ -588,6 +616,7 @@ void svo_frontend_destroy(svo_frontend* fe) {
     if (fe->dmem) (void)hipFree(fe->dmem);
     if (fe->dermem) (void)hipFree(fe->dermem);
     if (fe->hmem) (void)hipHostFree(fe->hmem);
+    if (fe->zmem) (void)hipHostFree(fe->zmem);
     for (auto& e : fe->ev)
         if (e) (void)hipEventDestroy(e);
     for (auto& g : fe->gst)
@@ -882,38 +911,63 @@ int svo_frontend_step(svo_frontend* fe, int t, svo_frontend_stats* stats) {
             int mmax = 0;
             for (int s = a; s < a + n; s++) mmax = std::max(mmax, ms[s]);
             if (mmax == 0) break;
+            const bool zc = fe->zero_copy;
+            double* hyp_host = zc ? fe->z_hyps : fe->h_hyps;
             for (int s = a; s < a + n; s++) {
-                double* dst = fe->h_hyps + 12 * (size_t)s * kRansacChunk;
+                double* dst = hyp_host + 12 * (size_t)s * kRansacChunk;
                 std::memcpy(dst, fe->rs[s].hyp, sizeof(double) * 12 * ms[s]);
                 for (int j = ms[s]; j < mmax; j++) std::memset(dst + 12 * j, 0, sizeof(double) * 12);
                 nhyp += ms[s];
             }
-            SVO_HIP(ctx, hipMemcpyAsync(fe->hyps + 12 * (size_t)a * kRansacChunk, fe->h_hyps + 12 * (size_t)a * kRansacChunk,
-                                        sizeof(double) * 12 * n * kRansacChunk, hipMemcpyHostToDevice, sg));
             // hypotheses live at stride kRansacChunk; score (and copy back) only the
             // mmax rows of this round (rows beyond a sequence's own count are ignored)
             PnpBatch pb{fe->obj + 3 * (size_t)a * CAP, fe->xyB + 2 * (size_t)a * CAP, fe->nB + a, 0, CAP,
                         fe->hyps + 12 * (size_t)a * kRansacChunk, mmax, nullptr,
                         fe->bits_all + (size_t)a * kRansacChunk * fe->WORDS, fe->WORDS, fe->cnt + (size_t)a * kRansacChunk};
             pb.mstride = kRansacChunk;
+            if (zc) {  // the kernel reads the hypotheses and writes bits / per-wave counts in host memory
+                pb.hyp = fe->z_hyps + 12 * (size_t)a * kRansacChunk;
+                pb.bits = fe->z_bits + (size_t)a * kRansacChunk * fe->WORDS;
+                pb.cnt = nullptr;
+                pb.wave_cnt = fe->z_wcnt + (size_t)a * kRansacChunk * fe->WS;
+                pb.wave_stride = fe->WS;
+            } else {
+                SVO_HIP(ctx, hipMemcpyAsync(fe->hyps + 12 * (size_t)a * kRansacChunk,
+                                            fe->h_hyps + 12 * (size_t)a * kRansacChunk,
+                                            sizeof(double) * 12 * n * kRansacChunk, hipMemcpyHostToDevice, sg));
+            }
             ph_begin(fe, PH_PNP, sg, &slot);
             SVO_HIP(ctx, launch_pnp_residuals(pb, n, max_b, c.K[0], c.K[4], c.K[2], c.K[5], thr, sg));
             ph_end(fe, sg, slot);
-            SVO_HIP(ctx, hipMemcpyAsync(fe->h_cnt + (size_t)a * kRansacChunk, fe->cnt + (size_t)a * kRansacChunk,
-                                        sizeof(int) * n * kRansacChunk, hipMemcpyDeviceToHost, sg));
-            const size_t rowb = sizeof(uint32_t) * (size_t)kRansacChunk * fe->WORDS;
-            SVO_HIP(ctx, hipMemcpy2DAsync(fe->h_bits + (size_t)a * kRansacChunk * fe->WORDS, rowb,
-                                          fe->bits_all + (size_t)a * kRansacChunk * fe->WORDS, rowb,
-                                          sizeof(uint32_t) * (size_t)mmax * fe->WORDS, n, hipMemcpyDeviceToHost, sg));
+            if (!zc) {
+                SVO_HIP(ctx, hipMemcpyAsync(fe->h_cnt + (size_t)a * kRansacChunk, fe->cnt + (size_t)a * kRansacChunk,
+                                            sizeof(int) * n * kRansacChunk, hipMemcpyDeviceToHost, sg));
+                const size_t rowb = sizeof(uint32_t) * (size_t)kRansacChunk * fe->WORDS;
+                SVO_HIP(ctx, hipMemcpy2DAsync(fe->h_bits + (size_t)a * kRansacChunk * fe->WORDS, rowb,
+                                              fe->bits_all + (size_t)a * kRansacChunk * fe->WORDS, rowb,
+                                              sizeof(uint32_t) * (size_t)mmax * fe->WORDS, n, hipMemcpyDeviceToHost,
+                                              sg));
+            }
             TP("scoring enqueued");
             SVO_HIP(ctx, hipStreamSynchronize(sg));
             ms_wait += ms_since(tw);
             TP("scores on host");
             // consume is a few compares per hypothesis: cheaper here than a pool dispatch
-            for (int s = a; s < a + n; s++)
-                if (ms[s] > 0)
-                    fe->rs[s].consume(fe->h_cnt + (size_t)s * kRansacChunk,
-                                      fe->h_bits + (size_t)s * kRansacChunk * fe->WORDS, fe->WORDS, c.pnp_confidence);
+            for (int s = a; s < a + n; s++) {
+                if (ms[s] <= 0) continue;
+                int* cnts = fe->h_cnt + (size_t)s * kRansacChunk;
+                const uint32_t* bits = (zc ? fe->z_bits : fe->h_bits) + (size_t)s * kRansacChunk * fe->WORDS;
+                if (zc) {  // inlier counts = sum of the waves that hold points
+                    const int nw = (fe->h_nB[s] + 63) / 64;
+                    for (int j = 0; j < ms[s]; j++) {
+                        const int* wc = fe->z_wcnt + ((size_t)s * kRansacChunk + j) * fe->WS;
+                        int t = 0;
+                        for (int w = 0; w < nw; w++) t += wc[w];
+                        cnts[j] = t;
+                    }
+                }
+                fe->rs[s].consume(cnts, bits, fe->WORDS, c.pnp_confidence);
+            }
         }
         // the RANSAC inlier set is the output (R:src/tracking.cpp:218-229); the final
         // SQPnP-objective fit only refines the pose, from statistics summed on the GPU

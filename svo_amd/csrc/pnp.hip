@@ -54,6 +54,8 @@ __global__ __launch_bounds__(256) void pnp_residual_kernel(PnpBatch B, double fx
         if (lane == 1 && w0 + 1 < words) bits[w0 + 1] = (uint32_t)(bal >> 32);
     }
     if (B.cnt && lane == 0 && bal) atomicAdd(&B.cnt[(size_t)seq * ms + h], __popcll(bal));
+    if (B.wave_cnt && lane == 0)
+        B.wave_cnt[((size_t)seq * ms + h) * B.wave_stride + (blockIdx.x * 256 + threadIdx.x) / 64] = __popcll(bal);
 }
 
 }  // namespace
