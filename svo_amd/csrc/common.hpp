@@ -161,6 +161,7 @@ struct LKParams {
     float min_eig;
     int want_err;
     int generic = 0;  // 1: always use the runtime-window kernel (tests compare both)
+    int quad = 1;     // 21x21: two features per wave (lk_dual_kernel); 0: one per wave
 };
 // Batched LK: blockIdx.y = sequence; sequence s owns points [s*cap, s*cap + n_s)
 // of every array, n_s = counts[s] (device) or n when counts is null.

@@ -766,6 +766,13 @@ int svo_frontend_step(svo_frontend* fe, int t, svo_frontend_stats* stats) {
     lp.flags = c.lk_flags & ~SVO_LK_USE_INITIAL_FLOW;
     lp.min_eig = (float)c.min_eig;
     lp.want_err = 0;
+    {
+        static const bool quad_off = [] {
+            const char* e = std::getenv("SVO_LK_QUAD");
+            return e && e[0] == '0';
+        }();
+        lp.quad = quad_off ? 0 : 1;
+    }
     for (int g = 0; g < G; g++) {
         const int a = fe->g0[g], n = fe->gn[g];
         hipStream_t sg = fe->gst[g];
