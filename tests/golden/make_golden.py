@@ -42,6 +42,20 @@ def main():
                         bucket_xy=bx, X=X, K=sc.K, pnp_rvec=rv, pnp_tvec=tv, pnp_inliers=inl)
     print("wrote small_160x120.npz:", len(kp_nms), "kps,", int(t_s.sum()), "tracked,", len(inl), "inliers")
 
+    # colour ingest + ORB: a BGR frame whose channels differ,
+    # its grey conversion, and ORB(150 and 500 features) with and without a box mask
+    sc2 = Scene(320, 240, seed=12)
+    g0 = sc2.frame(0)
+    bgr = np.ascontiguousarray(np.stack([g0, np.roll(g0, 3, axis=1), 255 - g0], axis=2))
+    gray = O.bgr2gray(bgr)
+    kq = O.fast(gray, 20, True)[::5, :2]
+    omask = O.mask_boxes(320, 240, kq, 10.0)
+    orb150, oct150 = O.orb_detect(gray, None, nfeatures=150)
+    orb500m, oct500m = O.orb_detect(gray, omask, nfeatures=500)
+    np.savez_compressed(os.path.join(HERE, "orb_ingest_320x240.npz"), bgr=bgr, gray=gray, mask=omask,
+                        orb150=orb150, oct150=oct150, orb500m=orb500m, oct500m=oct500m)
+    print("wrote orb_ingest_320x240.npz:", len(orb150), "/", len(orb500m), "ORB keypoints")
+
 
 if __name__ == "__main__":
     main()

@@ -149,3 +149,30 @@ def test_gpu_orb_rejects_unsupported(ctx):
     p = S.OrbParams(nlevels=9)
     with pytest.raises(S.SvoError):
         ctx.orb_detect(g, p)
+
+
+# ------------------------------------------------------------------ committed fixture
+def _fixture():
+    import os
+    return np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "orb_ingest_320x240.npz"))
+
+
+def test_oracle_matches_committed_orb_ingest_fixture():
+    g = _fixture()
+    assert np.array_equal(O.bgr2gray(g["bgr"]), g["gray"])
+    k, o = O.orb_detect(g["gray"], None, nfeatures=150)
+    assert np.array_equal(k, g["orb150"]) and np.array_equal(o, g["oct150"])
+    k, o = O.orb_detect(g["gray"], g["mask"], nfeatures=500)
+    assert np.array_equal(k, g["orb500m"]) and np.array_equal(o, g["oct500m"])
+
+
+@pytest.mark.gpu
+def test_gpu_matches_committed_orb_ingest_fixture(ctx):
+    import svo_amd as S
+    g = _fixture()
+    img = ctx.image_bgr(g["bgr"], max_levels=3)
+    assert np.array_equal(img.level(0), g["gray"])
+    k, o = ctx.orb_detect(img, S.OrbParams(nfeatures=150))
+    assert np.array_equal(k, g["orb150"]) and np.array_equal(o, g["oct150"])
+    k, o = ctx.orb_detect(img, S.OrbParams(nfeatures=500), g["mask"])
+    assert np.array_equal(k, g["orb500m"]) and np.array_equal(o, g["oct500m"])
