@@ -120,18 +120,20 @@ struct FastDetBatch {
     const int* box_counts = nullptr;
     int box_stride = 0;
     float box_half = 0.f;
-    // scratch for binning the box centres by 16-row band: [s][box_stride] float2
-    // and [s][nbands + 1] band offsets (launch_fast_detect fills them)
+    // scratch for binning the box centres by (16-row band, 64-column tile) cell:
+    // [s][box_stride] float2 and [s][fast_box_cells(w, h)] offsets
     float* box_binned = nullptr;
     int* box_band = nullptr;
     bool box_prebinned = false;  // launch_box_bin already ran (e.g. ahead, off the critical path)
 };
 // ints of band-offset scratch per sequence for an image of height h
-inline int fast_box_bands(int h) { return (h + 15) / 16 + 1; }
+// Box centres are binned by cell: 16-row band x 64-column tile (the FAST tile
+// grid), cell-major per band; [s][cells + 1] offsets.
+inline int fast_box_cells(int w, int h) { return ((h + 15) / 16) * ((w + 63) / 64) + 1; }
 hipError_t launch_fast_detect(const FastDetBatch& b, int nseq, int w, int h, int threshold, int nonmax,
                               hipStream_t st);
 // The band binning of the box centres alone (needs only box_pts / box_counts).
-hipError_t launch_box_bin(const FastDetBatch& b, int nseq, int h, hipStream_t st);
+hipError_t launch_box_bin(const FastDetBatch& b, int nseq, int w, int h, hipStream_t st);
 // Masks for nseq sequences (w*h each): 255 + filled boxes around counts[s] (or n)
 // points of pts + s*pts_stride.
 hipError_t launch_mask_boxes(int w, int h, const float* pts, const int* counts, int n, int pts_stride,

@@ -317,14 +317,16 @@ __global__ __launch_bounds__(256) void fast_detect_kernel(FastDetBatch B, int th
     if (boxes) {
         if (tid < FD_TY) TM[tid] = ~0ull;
         __syncthreads();
-        // only the bands whose box centres can reach this tile
-        const int nb = (h + 15) / 16;
-        const int* __restrict__ band = B.box_band + seq * (size_t)(nb + 1);
+        // only the cells (16-row band x 64-column tile) whose box centres can reach this tile
+        const int nb = (h + 15) / 16, nc = (w + 63) / 64;
+        const int* __restrict__ cells = B.box_band + seq * (size_t)(nb * nc + 1);
         const int b0 = max(0, (int)floorf((y0 - B.box_half - 1.f) / 16.f));
         const int b1 = min(nb - 1, (int)floorf((y0 + FD_TY + B.box_half + 1.f) / 16.f));
-        const int i0 = band[b0], i1 = band[b1 + 1];
+        const int cb0 = max(0, (int)floorf((x0 - B.box_half - 1.f) / 64.f));
+        const int cb1 = min(nc - 1, (int)floorf((x0 + FD_TX + B.box_half + 1.f) / 64.f));
         const float* __restrict__ pts = B.box_binned + 2 * seq * (size_t)B.box_stride;
-        for (int i = i0 + tid; i < i1; i += 256) {
+        for (int bq = b0; bq <= b1; bq++)
+        for (int i = cells[bq * nc + cb0] + tid, i1 = cells[bq * nc + cb1 + 1]; i < i1; i += 256) {
             const float px = pts[2 * i], py = pts[2 * i + 1];
             const int xa = (int)__builtin_rintf(px - B.box_half), ya = (int)__builtin_rintf(py - B.box_half);
             const int xb = (int)__builtin_rintf(px + B.box_half), yb = (int)__builtin_rintf(py + B.box_half);
@@ -381,37 +383,57 @@ __global__ __launch_bounds__(256) void fast_detect_kernel(FastDetBatch B, int th
     }
 }
 
-// Box centres of one sequence binned by 16-row band (counting sort; order within
-// a band is irrelevant: the mask is an AND of boxes). One block per sequence.
-__global__ __launch_bounds__(256) void box_bin_kernel(FastDetBatch B, int h) {
+// Box centres of one sequence binned by cell (16-row band x 64-column tile):
+// counting sort, one block per sequence; order within a cell is irrelevant
+// (the mask is an AND of boxes).
+constexpr int kMaxBoxCells = 12288;
+__global__ __launch_bounds__(256) void box_bin_kernel(FastDetBatch B, int w, int h) {
     const size_t seq = blockIdx.x;
-    const int nb = (h + 15) / 16;
-    __shared__ int cnt[1024], cur[1024];
+    const int nb = (h + 15) / 16, nc = (w + 63) / 64, ncell = nb * nc;
+    extern __shared__ int box_lds[];  // [256] chunk totals + [ncell] counts (sized at launch)
+    int* part = box_lds;
+    int* cnt = box_lds + 256;
     const int n = B.box_counts[seq];
     const float* __restrict__ pts = B.box_pts + 2 * seq * (size_t)B.box_stride;
     float* __restrict__ outp = B.box_binned + 2 * seq * (size_t)B.box_stride;
-    int* __restrict__ band = B.box_band + seq * (size_t)(nb + 1);
-    for (int b = threadIdx.x; b < nb; b += 256) cnt[b] = 0;
+    int* __restrict__ cells = B.box_band + seq * (size_t)(ncell + 1);
+    for (int c = threadIdx.x; c < ncell; c += 256) cnt[c] = 0;
     __syncthreads();
-    auto band_of = [&](float y) {
-        int b = (int)floorf(y / 16.f);
-        return b < 0 ? 0 : b >= nb ? nb - 1 : b;
+    auto cell_of = [&](float x, float y) {
+        int b = (int)floorf(y / 16.f), t = (int)floorf(x / 64.f);
+        b = b < 0 ? 0 : b >= nb ? nb - 1 : b;
+        t = t < 0 ? 0 : t >= nc ? nc - 1 : t;
+        return b * nc + t;
     };
-    for (int i = threadIdx.x; i < n; i += 256) atomicAdd(&cnt[band_of(pts[2 * i + 1])], 1);
+    for (int i = threadIdx.x; i < n; i += 256) atomicAdd(&cnt[cell_of(pts[2 * i], pts[2 * i + 1])], 1);
+    __syncthreads();
+    // exclusive scan: each thread a contiguous chunk, then the chunk totals
+    const int chunk = (ncell + 255) / 256, c0 = threadIdx.x * chunk, c1 = min(ncell, c0 + chunk);
+    int acc = 0;
+    for (int c = c0; c < c1; c++) acc += cnt[c];
+    part[threadIdx.x] = acc;
     __syncthreads();
     if (threadIdx.x == 0) {
-        int acc = 0;
-        for (int b = 0; b < nb; b++) {
-            band[b] = acc;
-            cur[b] = acc;
-            acc += cnt[b];
+        int run = 0;
+        for (int k = 0; k < 256; k++) {
+            const int v = part[k];
+            part[k] = run;
+            run += v;
         }
-        band[nb] = acc;
+        cells[ncell] = run;
+    }
+    __syncthreads();
+    int run = part[threadIdx.x];
+    for (int c = c0; c < c1; c++) {
+        const int v = cnt[c];
+        cells[c] = run;
+        cnt[c] = run;  // becomes the running cursor
+        run += v;
     }
     __syncthreads();
     for (int i = threadIdx.x; i < n; i += 256) {
         const float x = pts[2 * i], y = pts[2 * i + 1];
-        const int pos = atomicAdd(&cur[band_of(y)], 1);
+        const int pos = atomicAdd(&cnt[cell_of(x, y)], 1);
         outp[2 * pos] = x;
         outp[2 * pos + 1] = y;
     }
@@ -530,7 +552,7 @@ hipError_t launch_fast_detect(const FastDetBatch& b, int nseq, int w, int h, int
     hipError_t e = hipMemsetAsync(b.rowcnt, 0, sizeof(int) * (size_t)h * nseq, st);
     if (e != hipSuccess) return e;
     if (b.box_pts && !b.box_prebinned) {
-        e = launch_box_bin(b, nseq, h, st);
+        e = launch_box_bin(b, nseq, w, h, st);
         if (e != hipSuccess) return e;
     }
     dim3 grid((w + FD_TX - 1) / FD_TX, (h + FD_TY - 1) / FD_TY, nseq);
@@ -540,10 +562,13 @@ hipError_t launch_fast_detect(const FastDetBatch& b, int nseq, int w, int h, int
     return hipGetLastError();
 }
 
-hipError_t launch_box_bin(const FastDetBatch& b, int nseq, int h, hipStream_t st) {
+hipError_t launch_box_bin(const FastDetBatch& b, int nseq, int w, int h, hipStream_t st) {
     if (!b.box_pts) return hipSuccess;
-    if ((h + 15) / 16 > 1024) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(box_bin_kernel, dim3(nseq), dim3(256), 0, st, b, h);
+    if (fast_box_cells(w, h) - 1 > kMaxBoxCells) return hipErrorInvalidValue;
+    // LDS sized to the cell grid (2 KB at KITTI size): the kernel runs beside LK
+    // and must fit next to its blocks
+    const size_t lds = sizeof(int) * (256 + (size_t)fast_box_cells(w, h));
+    hipLaunchKernelGGL(box_bin_kernel, dim3(nseq), dim3(256), lds, st, b, w, h);
     return hipGetLastError();
 }
 

@@ -160,6 +160,14 @@ struct svo_frontend {
     uint32_t *bits_all, *bits_best;
     double *map, *hyps, *rot_d, *stats;
     float* samp;  // [s][kRansacPrefetch][kSampleFloats] RANSAC subsets gathered on the device
+    // the tracked-point arrays of a step (xyB, obj, nB) and its inlier bits are
+    // double-buffered by step parity: the side work of step t (SQPnP statistics,
+    // full copy to the host) reads them while step t+1 already runs
+    float *xyB_b[2], *obj_b[2];
+    int* nB_b[2];
+    uint32_t* bits_best_b[2];
+    int front_t = -1;  // step whose first half (LK .. FAST) is already enqueued
+    std::vector<hipEvent_t> ev_tail;  // [g] end of a step's tail on slice g
     // host mirrors (pinned)
     void* hmem = nullptr;
     int *h_nB, *h_nA, *h_cnt, *h_added;
@@ -180,6 +188,7 @@ struct svo_frontend {
     std::vector<double> pose;  // [s][6]
     bool fits_pending = false;
     bool stats_pending = false;
+    bool boxes_binned = false;  // box_bin already queued for the next step's FAST
     int pyr_ready = -1;  // frame index whose pyramid + Scharr were built ahead
     hipEvent_t ev_stats = nullptr;  // SQPnP statistics of the last step on the host
     // full copies of the tracked points / map points (h_xyB, h_obj): needed only by
@@ -434,7 +443,11 @@ int svo_frontend_create(svo_ctx* ctx, const svo_frontend_config* cfg, svo_fronte
         add(sizeof(double) * 60 * (size_t)S);
         add(sizeof(float) * 2 * (size_t)S * CAP);               // box centres binned by band
         add(sizeof(float) * kSampleFloats * kRansacPrefetch * (size_t)S);
-        add(sizeof(int) * (size_t)S * fast_box_bands(c.height));
+        add(sizeof(int) * (size_t)S * fast_box_cells(c.width, c.height));
+        add(sizeof(float) * 2 * (size_t)S * CAP);               // second xyB
+        add(sizeof(float) * 3 * (size_t)S * CAP);               // second obj
+        add(sizeof(int) * S);                                   // second nB
+        add(sizeof(uint32_t) * (size_t)S * fe->WORDS);          // second bits_best
         add(4096);
         bytes = (size_t)p;
     }
@@ -476,8 +489,16 @@ int svo_frontend_create(svo_ctx* ctx, const svo_frontend_config* cfg, svo_fronte
         fe->rot_d = carve<double>(p, 9 * (size_t)S * fe->T);
         fe->stats = carve<double>(p, 60 * (size_t)S);
         fe->box_binned = carve<float>(p, 2 * (size_t)S * CAP);
-        fe->box_band = carve<int>(p, (size_t)S * fast_box_bands(c.height));
+        fe->box_band = carve<int>(p, (size_t)S * fast_box_cells(c.width, c.height));
         fe->samp = carve<float>(p, (size_t)kSampleFloats * kRansacPrefetch * S);
+        fe->xyB_b[0] = fe->xyB;
+        fe->obj_b[0] = fe->obj;
+        fe->nB_b[0] = fe->nB;
+        fe->bits_best_b[0] = fe->bits_best;
+        fe->xyB_b[1] = carve<float>(p, 2 * (size_t)S * CAP);
+        fe->obj_b[1] = carve<float>(p, 3 * (size_t)S * CAP);
+        fe->nB_b[1] = carve<int>(p, S);
+        fe->bits_best_b[1] = carve<uint32_t>(p, (size_t)S * fe->WORDS);
     }
     (void)hipMemsetAsync(fe->dmem, 0, bytes, ctx->stream);
     // host mirrors
@@ -594,6 +615,8 @@ int svo_frontend_create(svo_ctx* ctx, const svo_frontend_config* cfg, svo_fronte
         for (auto& e : fe->ev_sync) (void)hipEventCreateWithFlags(&e, hipEventDisableTiming);
         (void)hipEventCreateWithFlags(&fe->ev_stats, hipEventDisableTiming);
         (void)hipEventCreateWithFlags(&fe->ev_gathered, hipEventDisableTiming);
+        fe->ev_tail.assign(G, nullptr);
+        for (auto& e : fe->ev_tail) (void)hipEventCreateWithFlags(&e, hipEventDisableTiming);
         (void)hipEventCreateWithFlags(&fe->ev_full, hipEventDisableTiming);
         if (hipStreamCreateWithFlags(&fe->st_copy, hipStreamNonBlocking) != hipSuccess) {
             svo_frontend_destroy(fe);
@@ -636,8 +659,24 @@ void svo_frontend_destroy(svo_frontend* fe) {
         (void)hipStreamDestroy(fe->st_copy);
     }
     if (fe->ev_gathered) (void)hipEventDestroy(fe->ev_gathered);
+    for (auto& e : fe->ev_tail)
+        if (e) (void)hipEventDestroy(e);
     if (fe->ev_full) (void)hipEventDestroy(fe->ev_full);
     delete fe;
+}
+
+// Drop a prefetched first half (its inputs are about to change): let every
+// stream finish and forget it; the frame pyramids built ahead go too.
+static int fe_drain(svo_frontend* fe) {
+    svo_ctx* ctx = fe->ctx;
+    if (fe->front_t < 0) return SVO_OK;
+    for (auto& g : fe->gst) SVO_HIP(ctx, hipStreamSynchronize(g));
+    if (fe->st_fast) SVO_HIP(ctx, hipStreamSynchronize(fe->st_fast));
+    if (fe->st_copy) SVO_HIP(ctx, hipStreamSynchronize(fe->st_copy));
+    SVO_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    fe->front_t = -1;
+    fe->pyr_ready = -1;
+    return SVO_OK;
 }
 
 static int fe_set_frame(svo_frontend* fe, int seq, int t, const uint8_t* px, int stride, bool bgr,
@@ -645,6 +684,8 @@ static int fe_set_frame(svo_frontend* fe, int seq, int t, const uint8_t* px, int
     if (!fe || seq < 0 || seq >= fe->S || t < 0 || t >= fe->T || !px || stride < (bgr ? 3 : 1) * fe->W)
         return SVO_ERR_ARG;
     svo_ctx* ctx = fe->ctx;
+    int rd = fe_drain(fe);
+    if (rd) return rd;
     svo_image* im = fe->frames[(size_t)seq * fe->T + t];
     if (fe->pyr_ready >= 0 && fe->pyr_ready % fe->T == t) fe->pyr_ready = -1;  // built from the old image
     uint8_t* l0 = const_cast<uint8_t*>(im->desc.lv[0].data);
@@ -688,9 +729,12 @@ int svo_frontend_prebuild_pyramids(svo_frontend* fe) {
 
 int svo_frontend_init(svo_frontend* fe, int t0) {
     if (!fe || t0 < 0) return SVO_ERR_ARG;
+    int rd = fe_drain(fe);
+    if (rd) return rd;
     fe->pyr_ready = -1;
     fe->fits_pending = false;
     fe->stats_pending = false;
+    fe->boxes_binned = false;
     svo_ctx* ctx = fe->ctx;
     const int S = fe->S;
     const PyrDesc* dcur = fe->d_desc + (size_t)(t0 % fe->T) * S;
@@ -709,20 +753,12 @@ int svo_frontend_init(svo_frontend* fe, int t0) {
     return SVO_OK;
 }
 
-int svo_frontend_step(svo_frontend* fe, int t, svo_frontend_stats* stats) {
-    if (!fe || t < 1) return SVO_ERR_ARG;
-    // host-side step trace (SVO_FE_TRACE=1): label + microseconds since step start
-    static const bool trace_on = [] {
-        const char* e = std::getenv("SVO_FE_TRACE");
-        return e && e[0] == '1';
-    }();
-    const auto trace_t0 = std::chrono::steady_clock::now();
-    std::vector<std::pair<const char*, double>> trace;
-    auto TP = [&](const char* label) {
-        if (trace_on)
-            trace.push_back({label, std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() -
-                                                                               trace_t0).count()});
-    };
+// First half of a step (enqueue only, no host waits): the previous step's side
+// work if still pending, the pyramid of frame t if not built ahead, temporal LK,
+// frame t+1's pyramid, compaction / gather / RANSAC subsets and their D2H, FAST.
+// svo_frontend_step enqueues the next step's first half right after its own
+// tail, so the GPU goes on with LK while the caller is between steps.
+static int fe_front(svo_frontend* fe, int t) {
     svo_ctx* ctx = fe->ctx;
     hipStream_t st0 = ctx->stream;
     const int S = fe->S, CAP = fe->CAP, G = fe->G;
@@ -731,18 +767,21 @@ int svo_frontend_step(svo_frontend* fe, int t, svo_frontend_stats* stats) {
     const PyrDesc* dcur = fe->d_desc + (size_t)(t % fe->T) * S;
     hipEvent_t ev_pyr = fe->ev_sync[0], ev_fast = fe->ev_sync[1];
     int slot;
-    int max_prev = 0;
-    for (int s = 0; s < S; s++) max_prev = std::max(max_prev, fe->h_nA[s]);
-
-    // 0. the previous step's SQPnP statistics, queued before this step's big
-    //    launches so that the low-priority stream gets CUs before LK fills them
-    //    (the fits wait for it; the compaction below overwrites its inputs)
+    // this step's parity buffers (the previous step's stay with its side work)
+    fe->xyB = fe->xyB_b[t & 1];
+    fe->obj = fe->obj_b[t & 1];
+    fe->nB = fe->nB_b[t & 1];
+    fe->bits_best = fe->bits_best_b[t & 1];
+    // 0. the previous step's SQPnP statistics and the binning of the FAST mask's
+    //    box centres (frame t-1's features) normally went out at the end of that
+    //    step, ahead of this step's LK (a kernel queued beside LK waits for it:
+    //    LK leaves no registers free); only after init / a reset are they queued here
     {
         int rq = fe_queue_stats(fe);
         if (rq) return rq;
-        // the FAST mask's box centres (frame t-1's features) binned by band, also
-        // ahead: only FAST itself waits for LK
-        SVO_HIP(ctx, launch_box_bin(fe_fast_batch(fe, dcur, true), S, fe->H, fe->st_fast));
+        if (!fe->boxes_binned)
+            SVO_HIP(ctx, launch_box_bin(fe_fast_batch(fe, dcur, true), S, fe->W, fe->H, fe->st_fast));
+        fe->boxes_binned = false;
     }
     // 1. pyramid of frame t and its Scharr derivative pyramid (used when frame
     //    t is the prev image of the next step; OpenCV recomputes it per call)
@@ -776,8 +815,7 @@ int svo_frontend_step(svo_frontend* fe, int t, svo_frontend_stats* stats) {
     for (int g = 0; g < G; g++) {
         const int a = fe->g0[g], n = fe->gn[g];
         hipStream_t sg = fe->gst[g];
-        int mp = 0;
-        for (int s = a; s < a + n; s++) mp = std::max(mp, fe->h_nA[s]);
+        const int mp = CAP;  // grid bound: the host counts of the previous tail may not be back yet
         SVO_HIP(ctx, hipStreamWaitEvent(sg, ev_pyr, 0));
         if (g > 0) SVO_HIP(ctx, hipStreamWaitEvent(sg, fe->ev_sync[2 + 2 * (g - 1)], 0));
         LKBatch lb{dprev + a, dcur + a, fe->d_der + (size_t)((t - 1) & 1) * S + a, fe->xyA + 2 * (size_t)a * CAP,
@@ -802,22 +840,10 @@ int svo_frontend_step(svo_frontend* fe, int t, svo_frontend_stats* stats) {
         ph_end(fe, st0, slot);
         fe->pyr_ready = tn;
     }
-    TP("lk+pyr enqueued");
-    // 3a. the previous step's final pose fits, deferred to here: the host does
-    //     them while the GPU tracks this frame (before this step's D2H copies
-    //     are queued: the fits read the previous frame's host mirrors)
-    double ms_fit = fe_finish_fits(fe);
-    TP("fits done");
-    const bool prev_full = fe->full_queued;  // the compacts below wait for it
-    fe->full_queued = false;
     for (int g = 0; g < G; g++) {
         const int a = fe->g0[g], n = fe->gn[g];
         hipStream_t sg = fe->gst[g];
-        int mp = 0;
-        for (int s = a; s < a + n; s++) mp = std::max(mp, fe->h_nA[s]);
-        // the previous step's statistics kernel and full copy still read xyB / obj
-        SVO_HIP(ctx, hipStreamWaitEvent(sg, fe->ev_stats, 0));
-        if (prev_full) SVO_HIP(ctx, hipStreamWaitEvent(sg, fe->ev_full, 0));
+        const int mp = CAP;  // grid bound (the kernels read the device counts)
         CompactBatch cb{fe->nA + a, fe->status + (size_t)a * CAP, nullptr, 0, fe->next_xy + 2 * (size_t)a * CAP,
                         fe->midA + (size_t)a * CAP, fe->iters + (size_t)a * CAP, fe->itsum + a,
                         fe->xyB + 2 * (size_t)a * CAP, fe->midB + (size_t)a * CAP, fe->nB + a, CAP};
@@ -853,6 +879,44 @@ int svo_frontend_step(svo_frontend* fe, int t, svo_frontend_stats* stats) {
     if (rc) return rc;
     SVO_HIP(ctx, hipEventRecord(ev_fast, sf));
 
+
+    return SVO_OK;
+}
+
+int svo_frontend_step(svo_frontend* fe, int t, svo_frontend_stats* stats) {
+    if (!fe || t < 1) return SVO_ERR_ARG;
+    // host-side step trace (SVO_FE_TRACE=1): label + microseconds since step start
+    static const bool trace_on = [] {
+        const char* e = std::getenv("SVO_FE_TRACE");
+        return e && e[0] == '1';
+    }();
+    const auto trace_t0 = std::chrono::steady_clock::now();
+    std::vector<std::pair<const char*, double>> trace;
+    auto TP = [&](const char* label) {
+        if (trace_on)
+            trace.push_back({label, std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() -
+                                                                               trace_t0).count()});
+    };
+    svo_ctx* ctx = fe->ctx;
+    const int S = fe->S, CAP = fe->CAP, G = fe->G;
+    const svo_frontend_config& c = fe->cfg;
+    int slot;
+
+    if (fe->front_t != t) {
+        int rf = fe_front(fe, t);
+        if (rf) return rf;
+    }
+    fe->front_t = -1;
+    TP("front enqueued");
+    // the previous step's final pose fits, deferred to here: the host does them
+    // while the GPU tracks this frame
+    double ms_fit = fe_finish_fits(fe);
+    TP("fits done");
+    fe->full_queued = false;
+    hipEvent_t ev_fast = fe->ev_sync[1];
+    hipStream_t sf = fe->st_fast;
+    int rc = SVO_OK;
+    const PyrDesc* dcur = fe->d_desc + (size_t)(t % fe->T) * S;
 
     using clk = std::chrono::steady_clock;
     auto ms_since = [](clk::time_point t0) {
@@ -1021,11 +1085,38 @@ int svo_frontend_step(svo_frontend* fe, int t, svo_frontend_stats* stats) {
     fe->fits_pending = true;  // statistics land with the stream syncs below
     rc = fe_queue_full(fe);    // for the fits (cheirality test), off the critical path
     if (rc) return rc;
+    // the next step's side work, queued now (before its LK): the SQPnP statistics
+    // of these inliers and the binning of these features as next frame's mask boxes
+    for (int g = 0; g < G; g++) {
+        SVO_HIP(ctx, hipEventRecord(fe->ev_tail[g], fe->gst[g]));
+        SVO_HIP(ctx, hipStreamWaitEvent(sf, fe->ev_tail[g], 0));
+    }
+    rc = fe_queue_stats(fe);
+    if (rc) return rc;
+    SVO_HIP(ctx, launch_box_bin(fe_fast_batch(fe, dcur, true), S, fe->W, fe->H, sf));
+    fe->boxes_binned = true;
     TP("tail enqueued");
-    // only the slices' streams: the statistics (FAST stream) and the next
-    // frame's pyramid (main stream) keep running into the next step
+    // this step's counts, before the next step's first half re-fills the mirrors
+    int64_t lk_its = 0, tracked = 0;
+    for (int s = 0; s < S; s++) {
+        lk_its += fe->h_itsum[s];
+        tracked += fe->h_nB[s];
+    }
+    // the next step's first half goes out now, behind this step's tail, so the
+    // GPU moves on to its LK while the host returns to the caller
+    static const bool prefetch = [] {
+        const char* e = std::getenv("SVO_FE_PREFETCH");
+        return !(e && e[0] == '0');
+    }();
+    if (prefetch && t + 1 < fe->T) {
+        rc = fe_front(fe, t + 1);
+        if (rc) return rc;
+        fe->front_t = t + 1;
+    }
+    // wait for this step's tail only (the statistics, the next frame's pyramid and
+    // the prefetched first half keep running into the next step)
     auto tw = clk::now();
-    for (int g = 0; g < G; g++) SVO_HIP(ctx, hipStreamSynchronize(fe->gst[g]));
+    for (int g = 0; g < G; g++) SVO_HIP(ctx, hipEventSynchronize(fe->ev_tail[g]));
     ms_wait += ms_since(tw);
     TP("synced");
     ph_collect(fe);
@@ -1034,9 +1125,9 @@ int svo_frontend_step(svo_frontend* fe, int t, svo_frontend_stats* stats) {
     }
     if (stats) {
         std::memset(stats, 0, sizeof(*stats));
+        stats->lk_iterations = lk_its;
+        stats->tracked = tracked;
         for (int s = 0; s < S; s++) {
-            stats->lk_iterations += fe->h_itsum[s];
-            stats->tracked += fe->h_nB[s];
             stats->added += fe->h_added[s];
             stats->features += fe->h_nA[s];
         }
