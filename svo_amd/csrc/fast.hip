@@ -198,7 +198,7 @@ __global__ __launch_bounds__(256) void fast_write_kernel(FastBatch B, int w, int
 // ---- fused detection: FAST-9 + score + NMS + mask for a 64x16 tile (scores
 // of a 1-pixel halo recomputed), one 64-bit keep mask per (row, 64-px segment)
 // and per-row counts (integer atomics) ----
-constexpr int FD_TX = 64, FD_TY = 16;
+constexpr int FD_TX = 64, FD_TY = 32;
 constexpr int FD_SW = FD_TX + 2, FD_SH = FD_TY + 2;  // score region (halo 1)
 constexpr int FD_IW = FD_TX + 8, FD_IH = FD_TY + 8;  // image region (halo 4)
 
