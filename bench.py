@@ -207,7 +207,11 @@ def main():
     bytes_per_launch = units_per_launch * lk_bytes_per_feature(L)
     lk_avg_s = lk_ms / max(lk_n, 1) / 1e3
     achieved = bytes_per_launch / lk_avg_s / 1e9 if lk_avg_s > 0 else 0.0
-    traffic = pmc_traffic("lk_fast_kernel<21, 21") or pmc_traffic("lk_kernel")
+    # the 21x21 temporal call runs lk_dual_kernel (two features per wave) unless
+    # SVO_LK_QUAD=0 selects the one-feature-per-wave lk_fast_kernel
+    dual = os.environ.get("SVO_LK_QUAD", "1")[:1] != "0"
+    lk_name = "lk_dual_kernel<21, 21" if dual else "lk_fast_kernel<21, 21"
+    traffic = pmc_traffic(lk_name)
     dominant = max(phases, key=lambda k: phases[k][0])
     single = None
     if not args.no_single:
@@ -245,7 +249,8 @@ def main():
         "phase_ms_per_step": {k: round(v[0] / K, 4) for k, v in phases.items()},
         "stats_per_step": {k: round(v / K, 3) for k, v in tot.items()},
         "roofline": {
-            "kernel": "lk_fast_kernel<21,21> (temporal LK, all levels, one wave per feature)",
+            "kernel": (lk_name + "> (temporal LK, all levels, two features per wave)") if dual else
+                      (lk_name + "> (temporal LK, all levels, one wave per feature)"),
             "dominant_phase": dominant,
             "bound": "hbm",
             "achieved": round(achieved, 2),
