@@ -156,9 +156,9 @@ int svo_image_create(svo_ctx* ctx, int w, int h, int max_levels, svo_image** out
     size_t total = 0;
     int lw = w, lh = h;
     for (int l = 0; l < im->nlevels; l++) {
-        int pitch = (lw + 63) & ~63;
-        off[l] = total;
-        total += (size_t)pitch * lh;
+        int pitch = (lw + 2 * kPyrPad + 63) & ~63;
+        off[l] = total + (size_t)kPyrPad * pitch + kPyrPad;
+        total += (size_t)pitch * (lh + 2 * kPyrPad);
         total = (total + 255) & ~(size_t)255;
         im->desc.lv[l].w = lw;
         im->desc.lv[l].h = lh;
@@ -407,6 +407,7 @@ int svo_calc_optical_flow_pyr_lk(svo_ctx* ctx, const svo_image* prev, const svo_
         hs->dd.pitch[l] = l <= ml ? dpitch[l] : 0;
     }
     SVO_HIP(ctx, hipMemcpyAsync(ddesc, hs, sizeof(Staged), hipMemcpyHostToDevice, ctx->stream));
+    SVO_HIP(ctx, hipMemsetAsync(dbase, 0, dbytes, ctx->stream));  // the zero borders
     SVO_HIP(ctx, launch_scharr(ddesc, dder, 1, prev->w, prev->h, ml + 1, ctx->stream));
     LKBatch b{ddesc, ddesc + 1, dder, dprev, dnext, dst, err ? derr : nullptr, diters, nullptr, n, n};
     SVO_HIP(ctx, launch_lk(b, 1, n, p, ctx->stream));

@@ -13,7 +13,16 @@ namespace svo {
 
 constexpr int kMaxLevels = 8;  // pyramid levels kept per image (0..7)
 
-// One pyramid level in HBM: tightly pitched u8 rows (pitch multiple of 64 B).
+// Every pyramid level is stored with a kPyrPad-pixel REFLECT_101 border on all
+// four sides (OpenCV pads its LK pyramid levels the same way, by the window
+// size) and every derivative level with a kDerPad-element zero border (OpenCV's
+// zero-padded derivative levels): the LK kernels read windows and staged
+// regions reaching up to win + margin pixels outside a level without any
+// border test. `data` points at pixel (0, 0) of the interior.
+constexpr int kPyrPad = 32;
+constexpr int kDerPad = 32;
+
+// One pyramid level in HBM: u8 rows (pitch multiple of 64 B), padded as above.
 struct ImgLevel {
     const uint8_t* data;
     int w, h, pitch;
@@ -144,7 +153,11 @@ struct DerivDesc {
     uint32_t* data[kMaxLevels];
     int pitch[kMaxLevels];  // elements
 };
+// off[l] = element-0 offset (bytes) of level l's interior from the buffer start;
+// the buffer must be zeroed once (the borders are never written).
 size_t deriv_layout(int w, int h, int nlevels, size_t* off, int* pitch);
+// REFLECT_101 border of levels [0, nlevels) of nseq pyramids (after they are built)
+hipError_t launch_pyramid_pad(const PyrDesc* d_descs, int nseq, int w, int h, int nlevels, hipStream_t st);
 // one level's derivative (level dims lw x lh)
 hipError_t launch_scharr_level(const PyrDesc* d_pyrs, const DerivDesc* d_ders, int nseq, int lw, int lh, int level,
                                hipStream_t st);

@@ -575,6 +575,7 @@ int svo_frontend_create(svo_ctx* ctx, const svo_frontend_config* cfg, svo_fronte
                 hd[k].pitch[l] = l < fe->nlev ? dpitch[l] : 0;
             }
         fe->d_der = (DerivDesc*)fe->dermem;
+        SVO_HIP(ctx, hipMemsetAsync(base, 0, dbytes * 2 * S, ctx->stream));  // zero borders, never rewritten
         SVO_HIP(ctx, hipMemcpyAsync(fe->d_der, hd.data(), sizeof(DerivDesc) * hd.size(), hipMemcpyHostToDevice,
                                     ctx->stream));
         SVO_HIP(ctx, hipStreamSynchronize(ctx->stream));

@@ -966,22 +966,6 @@ __device__ __forceinline__ void half_sum_f3(int x, int y, int z, float& fx, floa
     fz = halves_lane_float(zh, zl);
 }
 
-// I pair (I(x, y) | I(x + 1, y) << 16) / derivative pair at one window row:
-// REFLECT_101 for the image, zeros for the derivative outside the level.
-__device__ __forceinline__ unsigned pair_border(const ImgLevel& L, int x, int y) {
-    gu8 row = (gu8)L.data + (size_t)refl101(y, L.h) * L.pitch;
-    return (unsigned)row[refl101(x, L.w)] | ((unsigned)row[refl101(x + 1, L.w)] << 16);
-}
-__device__ __forceinline__ u32x2a4 deriv_border(gu32 dsrc, int dpitch, int w, int h, int x, int y) {
-    u32x2a4 v{0u, 0u};
-    if (y >= 0 && y < h) {
-        gu32 q = dsrc + (size_t)y * dpitch;
-        if (x >= 0 && x < w) v.x = q[x];
-        if (x + 1 >= 0 && x + 1 < w) v.y = q[x + 1];
-    }
-    return v;
-}
-
 // 7 rows of one strip: I (x32) / Ix / Iy at the strip's pixels packed by row
 // pairs (4 pairs, the last closed by a zero row), accumulated into the A sums.
 template <int NR>
@@ -1013,9 +997,65 @@ __device__ __forceinline__ void strip_setup(const unsigned* P, const u32x2a4* D,
     }
 }
 
+// A level's global loads of a wave are issued back to back (both features'
+// next-image staging dwords, both strips' prev pairs and derivative pairs), then
+// consumed. Staging: lanes own (row, dword) slots, LPR lanes per row (the last
+// one supplies the right pixel of the row's last pair), RPP rows per pass.
+template <int JRW, int JRH>
+struct DualStageLoads {
+    static constexpr int LPR = JRW / 4 + 1, RPP = 64 / LPR, NPS = (JRH + RPP - 1) / RPP;
+    unsigned v[2][NPS];
+};
+
+// The staged region (pixel columns xa .. xa + 4 * (JRW / 4 + 1) - 1 read as
+// dwords, rows y0 .. y0 + JRH - 1) lies inside the padded level.
+template <int JRW, int JRH>
+__device__ __forceinline__ bool region_in_pad(const ImgLevel& L, int xa, int y0) {
+    return xa >= -kPyrPad && y0 >= -kPyrPad && xa + 4 * (JRW / 4 + 1) <= L.w + kPyrPad &&
+           y0 + JRH <= L.h + kPyrPad;
+}
+
+// One staged dword -> four pixel pairs (this lane's dword and the next lane's).
+__device__ __forceinline__ void stage_write(unsigned* dst, unsigned v, int lane) {
+    const unsigned nv = (unsigned)__builtin_amdgcn_ds_bpermute((lane + 1) << 2, (int)v);
+    uint4 o;
+    o.x = __builtin_amdgcn_perm(nv, v, 0x0c010c00u);
+    o.y = __builtin_amdgcn_perm(nv, v, 0x0c020c01u);
+    o.z = __builtin_amdgcn_perm(nv, v, 0x0c030c02u);
+    o.w = __builtin_amdgcn_perm(nv, v, 0x0c040c03u);
+    *reinterpret_cast<uint4*>(dst) = o;
+}
+
+// stage_bf for padded levels (the region is known to lie inside the padding)
+template <int W, int H>
+__device__ __forceinline__ void stage_padded(unsigned* dst, unsigned* sink, const ImgLevel& L, int xa, int y0,
+                                             int lane) {
+    constexpr int LPR = W / 4 + 1, RPP = 64 / LPR, NP = (H + RPP - 1) / RPP;
+    const int lr = lane / LPR, d = lane - lr * LPR;
+    gu8 src = (gu8)L.data + xa + 4 * d;
+    const bool wr = d < W / 4 && lr < RPP;
+    unsigned* dpl = wr ? dst + 4 * d : sink;
+    const int dstride = wr ? W : 0;
+    unsigned v[NP];
+#pragma unroll
+    for (int q = 0; q < NP; q++) {
+        int r = q * RPP + lr;
+        r = r < H ? r : H - 1;
+        v[q] = *(gu32)(src + (ptrdiff_t)(y0 + r) * L.pitch);
+    }
+#pragma unroll
+    for (int q = 0; q < NP; q++) {
+        int r = q * RPP + lr;
+        r = r < H ? r : H - 1;
+        stage_write(dpl + r * dstride, v[q], lane);
+    }
+}
+
 template <int WW, int WH, int MINW>
 __global__ __launch_bounds__(64, MINW) void lk_dual_kernel(LKBatch B, LKDev p) {
     using Q = DualShape<WW, WH>;
+    // window + staging margin + dword alignment stay inside the level padding
+    static_assert(WW + JM + 3 <= kPyrPad && WW + 1 <= kDerPad, "padding too small for the window");
     constexpr int JRW = Q::JRW, JRH = Q::JRH;
     constexpr int NR = 7, NP = 4;
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
@@ -1096,43 +1136,68 @@ __global__ __launch_bounds__(64, MINW) void lk_dual_kernel(LKBatch B, LKDev p) {
 
         int jx0 = ufloor(nextx - halfWx) - JM, jy0 = ufloor(nexty - halfWy) - JM;
         int jxa = jx0 & ~3;
-#pragma unroll
-        for (int f = 0; f < 2; f++) {
-            if (__builtin_amdgcn_readlane((int)lact, 32 * f))
-                stage_bf<JRW, JRH>(jregs + f * (Q::JBYTES / 4), sink, J, __builtin_amdgcn_readlane(jxa, 32 * f),
-                                   __builtin_amdgcn_readlane(jy0, 32 * f), lane);
-        }
         unsigned I2A[NP], GXA[NP], GYA[NP], I2B[NP], GXB[NP], GYB[NP];
         int a11 = 0, a12 = 0, a22 = 0;
         {
-            const int dpitch = dprev.pitch[level];
-            gu32 dsrc = (gu32)dprev.data[level];
-            const bool full_in = ipx >= 0 && ipy >= 0 && ipx + WW < I.w && ipy + WH < I.h;
-            // one strip at a time (loads of both in flight at once cost ~50 VGPRs)
-            auto strip = [&](int cx, int ry, unsigned GW0, unsigned GW1, unsigned* I2, unsigned* GX, unsigned* GY) {
-                unsigned P[NR + 1];
-                u32x2a4 D[NR + 1];
-                const int x = ipx + cx, y = ipy + ry;
-                if (full_in) {
-                    gu8 ia = (gu8)I.data + (size_t)y * I.pitch + x;
-                    gu32 qa = dsrc + (size_t)y * dpitch + x;
+            // Levels carry kPyrPad-pixel REFLECT_101 borders and the derivative
+            // levels kDerPad-element zero borders, so every read below is
+            // branch-free. An inactive half (or one whose region lies beyond the
+            // padding: its first bounds test deactivates it) stages and reads at
+            // the level origin; its results are never used.
+            using SL = DualStageLoads<JRW, JRH>;
+            const int lr = lane / SL::LPR, d = lane - lr * SL::LPR;
+            int xs[2], ys[2];
 #pragma unroll
-                    for (int k = 0; k <= NR; k++) {
-                        P[k] = __builtin_amdgcn_perm(0u, (unsigned)*(gu16u)(ia + (size_t)k * I.pitch), 0x0c010c00u);
-                        D[k] = *(const __attribute__((address_space(1))) u32x2a4*)(qa + (size_t)k * dpitch);
-                    }
-                } else {
+            for (int f = 0; f < 2; f++) {
+                const int xa = __builtin_amdgcn_readlane(jxa, 32 * f), y0 = __builtin_amdgcn_readlane(jy0, 32 * f);
+                const bool ok = __builtin_amdgcn_readlane((int)lact, 32 * f) && region_in_pad<JRW, JRH>(J, xa, y0);
+                xs[f] = ok ? xa : 0;
+                ys[f] = ok ? y0 : 0;
+            }
+            SL ld;
 #pragma unroll
-                    for (int k = 0; k <= NR; k++) {
-                        P[k] = pair_border(I, x, y + k);
-                        D[k] = deriv_border(dsrc, dpitch, I.w, I.h, x, y + k);
-                    }
+            for (int f = 0; f < 2; f++) {
+                gu8 src = (gu8)J.data + xs[f] + 4 * d;
+#pragma unroll
+                for (int q = 0; q < SL::NPS; q++) {
+                    int r = q * SL::RPP + lr;
+                    r = r < JRH ? r : JRH - 1;
+                    ld.v[f][q] = *(gu32)(src + (ptrdiff_t)(ys[f] + r) * J.pitch);
                 }
-                strip_setup<NR>(P, D, IW0, IW1, GW0, GW1, I2, GX, GY, a11, a12, a22);
-            };
-            strip(cA, rA, IW0, IW1, I2A, GXA, GYA);
-            __builtin_amdgcn_sched_barrier(0);
-            strip(cB, rB, hasB ? IW0 : 0u, hasB ? IW1 : 0u, I2B, GXB, GYB);
+            }
+            unsigned PA[NR + 1], PB[NR + 1];
+            u32x2a4 DA[NR + 1], DB[NR + 1];
+            {
+                const int dpitch = dprev.pitch[level];
+                gu32 dsrc = (gu32)dprev.data[level];
+                const int sx = inb ? ipx : 0, sy = inb ? ipy : 0;
+                const int xA = sx + cA, yA = sy + rA, xB = sx + cB, yB = sy + rB;
+                gu8 ia = (gu8)I.data + (ptrdiff_t)yA * I.pitch + xA;
+                gu8 ib = (gu8)I.data + (ptrdiff_t)yB * I.pitch + xB;
+                gu32 qa = dsrc + (ptrdiff_t)yA * dpitch + xA;
+                gu32 qb = dsrc + (ptrdiff_t)yB * dpitch + xB;
+#pragma unroll
+                for (int k = 0; k <= NR; k++) {
+                    PA[k] = __builtin_amdgcn_perm(0u, (unsigned)*(gu16u)(ia + (ptrdiff_t)k * I.pitch), 0x0c010c00u);
+                    DA[k] = *(const __attribute__((address_space(1))) u32x2a4*)(qa + (ptrdiff_t)k * dpitch);
+                    PB[k] = __builtin_amdgcn_perm(0u, (unsigned)*(gu16u)(ib + (ptrdiff_t)k * I.pitch), 0x0c010c00u);
+                    DB[k] = *(const __attribute__((address_space(1))) u32x2a4*)(qb + (ptrdiff_t)k * dpitch);
+                }
+            }
+            const bool wr = d < JRW / 4 && lr < SL::RPP;
+#pragma unroll
+            for (int f = 0; f < 2; f++) {
+                unsigned* dpl = wr ? jregs + f * (Q::JBYTES / 4) + 4 * d : sink;
+                const int dstride = wr ? JRW : 0;
+#pragma unroll
+                for (int q = 0; q < SL::NPS; q++) {
+                    int r = q * SL::RPP + lr;
+                    r = r < JRH ? r : JRH - 1;
+                    stage_write(dpl + r * dstride, ld.v[f][q], lane);
+                }
+            }
+            strip_setup<NR>(PA, DA, IW0, IW1, IW0, IW1, I2A, GXA, GYA, a11, a12, a22);
+            strip_setup<NR>(PB, DB, IW0, IW1, hasB ? IW0 : 0u, hasB ? IW1 : 0u, I2B, GXB, GYB, a11, a12, a22);
         }
         wave_lds_sync();
         float A11, A12, A22;
@@ -1170,8 +1235,9 @@ __global__ __launch_bounds__(64, MINW) void lk_dual_kernel(LKBatch B, LKDev p) {
                 while (nb) {
                     const int f = (int)(__builtin_ctzll(nb) >> 5);
                     nb &= nb - 1;
-                    stage_bf<JRW, JRH>(jregs + f * (Q::JBYTES / 4), sink, J, __builtin_amdgcn_readlane(jxa, 32 * f),
-                                       __builtin_amdgcn_readlane(jy0, 32 * f), lane);
+                    stage_padded<JRW, JRH>(jregs + f * (Q::JBYTES / 4), sink, J,
+                                           __builtin_amdgcn_readlane(jxa, 32 * f),
+                                           __builtin_amdgcn_readlane(jy0, 32 * f), lane);
                 }
                 wave_lds_sync();
             }
@@ -1251,8 +1317,10 @@ hipError_t launch_dual(const LKBatch& b, int nseq, int max_n, const LKDev& d, hi
         const char* e = std::getenv("SVO_LK_DUAL_MINW");
         return e ? std::atoi(e) : 4;
     }();
-    if (minw == 1)
-        hipLaunchKernelGGL((lk_dual_kernel<WW, WH, 1>), grid, dim3(64), lds_bytes, st, b, d);
+    if (minw == 5)
+        hipLaunchKernelGGL((lk_dual_kernel<WW, WH, 5>), grid, dim3(64), lds_bytes, st, b, d);
+    else if (minw == 3)
+        hipLaunchKernelGGL((lk_dual_kernel<WW, WH, 3>), grid, dim3(64), lds_bytes, st, b, d);
     else
         hipLaunchKernelGGL((lk_dual_kernel<WW, WH, 4>), grid, dim3(64), lds_bytes, st, b, d);
     return hipGetLastError();

@@ -85,6 +85,42 @@ __global__ __launch_bounds__(256) void pyr_down_batched_kernel(const PyrDesc* __
     pyr_down_tile(s.data, s.w, s.h, s.pitch, const_cast<uint8_t*>(d.data), d.w, d.h, d.pitch);
 }
 
+// REFLECT_101 border (kPyrPad pixels each side) of one level, written from the
+// level's interior: the top and bottom bands (full padded width), then the left
+// and right bands of the interior rows. Blocks of one level stride over them.
+__device__ __forceinline__ void pad_level(const ImgLevel& L, int blk, int nblk) {
+    const int w = L.w, h = L.h, pw = w + 2 * kPyrPad;
+    const int n_tb = 2 * kPyrPad * pw, n = n_tb + 2 * kPyrPad * h;
+    uint8_t* __restrict__ d = const_cast<uint8_t*>(L.data);
+    for (int k = blk * 256 + (int)threadIdx.x; k < n; k += nblk * 256) {
+        int x, y;
+        if (k < n_tb) {
+            const int r = k / pw, c = k - r * pw;
+            y = r < kPyrPad ? r - kPyrPad : h + (r - kPyrPad);
+            x = c - kPyrPad;
+        } else {
+            const int k2 = k - n_tb, r = k2 / (2 * kPyrPad), c = k2 - r * (2 * kPyrPad);
+            y = r;
+            x = c < kPyrPad ? c - kPyrPad : w + (c - kPyrPad);
+        }
+        d[(ptrdiff_t)y * L.pitch + x] = d[(ptrdiff_t)refl101(y, h) * L.pitch + refl101(x, w)];
+    }
+}
+
+constexpr int PAD_BLOCKS = 16;  // blocks per (level, sequence)
+
+__global__ __launch_bounds__(256) void pad_batched_kernel(const PyrDesc* __restrict__ descs) {
+    pad_level(descs[blockIdx.z].lv[blockIdx.y], blockIdx.x, gridDim.x);
+}
+__global__ __launch_bounds__(256) void pad_kernel(PyrDesc d) { pad_level(d.lv[blockIdx.y], blockIdx.x, gridDim.x); }
+
+hipError_t launch_pyramid_pad(const PyrDesc* d_descs, int nseq, int w, int h, int nlevels, hipStream_t st) {
+    (void)w;
+    (void)h;
+    hipLaunchKernelGGL(pad_batched_kernel, dim3(PAD_BLOCKS, nlevels, nseq), dim3(256), 0, st, d_descs);
+    return hipGetLastError();
+}
+
 hipError_t launch_pyramid_batched(const PyrDesc* d_descs, int nseq, int w, int h, int nlevels,
                                   hipStream_t st) {
     int lw = w, lh = h;
@@ -94,7 +130,7 @@ hipError_t launch_pyramid_batched(const PyrDesc* d_descs, int nseq, int w, int h
         dim3 grid((lw + PD_TX - 1) / PD_TX, (lh + PD_TY - 1) / PD_TY, nseq);
         hipLaunchKernelGGL(pyr_down_batched_kernel, grid, dim3(256), 0, st, d_descs, l);
     }
-    return hipGetLastError();
+    return launch_pyramid_pad(d_descs, nseq, w, h, nlevels, st);
 }
 
 hipError_t launch_pyramid(const svo_image* img, int first_level, hipStream_t st) {
@@ -105,6 +141,7 @@ hipError_t launch_pyramid(const svo_image* img, int first_level, hipStream_t st)
         hipLaunchKernelGGL(pyr_down_kernel, grid, dim3(256), 0, st, s.data, s.w, s.h, s.pitch,
                            const_cast<uint8_t*>(d.data), d.w, d.h, d.pitch);
     }
+    hipLaunchKernelGGL(pad_kernel, dim3(PAD_BLOCKS, img->nlevels), dim3(256), 0, st, img->desc);
     return hipGetLastError();
 }
 
@@ -210,8 +247,10 @@ hipError_t launch_pyramid_scharr_batched(const PyrDesc* d_descs, const DerivDesc
         lw = nw;
         lh = nh;
     }
-    // the coarsest level's derivative (no pyrDown after it)
-    return launch_scharr_level(d_descs, d_ders, nseq, lw, lh, nlevels - 1, st);
+    // the coarsest level's derivative (no pyrDown after it), then the borders
+    hipError_t e = launch_scharr_level(d_descs, d_ders, nseq, lw, lh, nlevels - 1, st);
+    if (e != hipSuccess) return e;
+    return launch_pyramid_pad(d_descs, nseq, w, h, nlevels, st);
 }
 
 }  // namespace svo

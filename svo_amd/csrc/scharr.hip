@@ -90,9 +90,9 @@ size_t deriv_layout(int w, int h, int nlevels, size_t* off, int* pitch) {
     size_t total = 0;
     int lw = w, lh = h;
     for (int l = 0; l < nlevels; l++) {
-        pitch[l] = (lw + 15) & ~15;
-        off[l] = total;
-        total += (size_t)pitch[l] * lh * 4;
+        pitch[l] = (lw + 2 * kDerPad + 15) & ~15;
+        off[l] = total + ((size_t)kDerPad * pitch[l] + kDerPad) * 4;
+        total += (size_t)pitch[l] * (lh + 2 * kDerPad) * 4;
         total = (total + 255) & ~(size_t)255;
         lw = (lw + 1) / 2;
         lh = (lh + 1) / 2;
