@@ -156,7 +156,8 @@ int svo_image_create(svo_ctx* ctx, int w, int h, int max_levels, svo_image** out
     size_t total = 0;
     int lw = w, lh = h;
     for (int l = 0; l < im->nlevels; l++) {
-        int pitch = (lw + 2 * kPyrPad + 63) & ~63;
+        // + 4: the border writer's last dword of a row may pass column w + kPyrPad - 1
+        int pitch = (lw + 2 * kPyrPad + 4 + 63) & ~63;
         off[l] = total + (size_t)kPyrPad * pitch + kPyrPad;
         total += (size_t)pitch * (lh + 2 * kPyrPad);
         total = (total + 255) & ~(size_t)255;

@@ -148,7 +148,12 @@ hipError_t launch_box_bin(const FastDetBatch& b, int nseq, int w, int h, hipStre
 hipError_t launch_mask_boxes(int w, int h, const float* pts, const int* counts, int n, int pts_stride,
                              int nseq, float half, uint8_t* mask, hipStream_t st);
 
-// Scharr derivative pyramid of one image (packed int16 Ix | Iy << 16 per pixel).
+// Scharr derivative pyramid of one image (packed int16 Ix | Iy << 16 per pixel),
+// stored scaled by 2^kDerShift (|Ix|, |Iy| <= 4080, so 4x still fits int16): a
+// bilinear sum of the scaled values carries the CV_DESCALE(., W_BITS) result in
+// its high 16 bits (W_BITS + kDerShift == 16), which the LK kernels pack by byte
+// permutes instead of shifting every sum.
+constexpr int kDerShift = 2;
 struct DerivDesc {
     uint32_t* data[kMaxLevels];
     int pitch[kMaxLevels];  // elements

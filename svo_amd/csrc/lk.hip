@@ -257,8 +257,9 @@ __global__ __launch_bounds__(256) void lk_kernel(LKBatch B, LKDev p) {
                     const unsigned X1 = __builtin_amdgcn_perm(dv[j + 1][1], dv[j + 1][0], 0x05040100u);
                     const unsigned Y0 = __builtin_amdgcn_perm(dv[j][1], dv[j][0], 0x07060302u);
                     const unsigned Y1 = __builtin_amdgcn_perm(dv[j + 1][1], dv[j + 1][0], 0x07060302u);
-                    const int ix = sdot2(X0, IW0, sdot2(X1, IW1, 1 << (W_BITS - 1))) >> W_BITS;
-                    const int iy = sdot2(Y0, IW0, sdot2(Y1, IW1, 1 << (W_BITS - 1))) >> W_BITS;
+                    constexpr int DS = W_BITS + kDerShift;  // derivatives are stored x 2^kDerShift
+                    const int ix = sdot2(X0, IW0, sdot2(X1, IW1, 1 << (DS - 1))) >> DS;
+                    const int iy = sdot2(Y0, IW0, sdot2(Y1, IW1, 1 << (DS - 1))) >> DS;
                     gix[j] = ix;
                     giy[j] = iy;
                     a11 += ix * ix;
@@ -429,6 +430,10 @@ __device__ __forceinline__ unsigned pair_sel(unsigned sh) {
 
 __device__ __forceinline__ unsigned lo16x2(int lo, int hi) {  // (lo & 0xffff) | (hi << 16) in one v_perm
     return __builtin_amdgcn_perm((unsigned)hi, (unsigned)lo, 0x05040100u);
+}
+// high halves packed: floor(lo / 2^16) | floor(hi / 2^16) << 16, one v_perm
+__device__ __forceinline__ unsigned hi16x2(int lo, int hi) {
+    return __builtin_amdgcn_perm((unsigned)hi, (unsigned)lo, 0x07060302u);
 }
 template <int CTRL, int ROW_MASK, bool BC>
 __device__ __forceinline__ int dpp_add(int v) {
@@ -624,7 +629,7 @@ __global__ __launch_bounds__(256, MINW) void lk_fast_kernel(LKBatch B, LKDev p) 
     // lanes outside the strip map (and rows past the window) run the same code on
     // in-range addresses; their derivatives are zeroed, so they add nothing
     const int r0 = (strip ? sg : 0) * RPG;
-    const int rnd_i = 1 << (W_BITS - 6), rnd_d = 1 << (W_BITS - 1);
+    const int rnd_i = 1 << (W_BITS - 6), rnd_d = 1 << (W_BITS + kDerShift - 1);
 
     constexpr float halfWx = (WW - 1) * 0.5f, halfWy = (WH - 1) * 0.5f;
     const float px = uni_f(prev_xy[2 * pt]), py = uni_f(prev_xy[2 * pt + 1]);
@@ -721,7 +726,7 @@ __global__ __launch_bounds__(256, MINW) void lk_fast_kernel(LKBatch B, LKDev p) 
 
         // ---- I (x32), Ix, Iy at the lane's RPG window pixels, packed by row pairs ----
         // Lanes outside the strip map get zero derivative weights (their Ix, Iy
-        // come out 0: rnd_d >> W_BITS == 0), so no branch per row.
+        // come out 0: rnd_d >> (W_BITS + kDerShift) == 0), so no branch per row.
         unsigned I2[NP], GX2[NP], GY2[NP];
         int a11 = 0, a12 = 0, a22 = 0;
         {
@@ -736,8 +741,8 @@ __global__ __launch_bounds__(256, MINW) void lk_fast_kernel(LKBatch B, LKDev p) 
                 const unsigned X1 = __builtin_amdgcn_perm(dv[j + 1].y, dv[j + 1].x, 0x05040100u);
                 const unsigned Y0 = __builtin_amdgcn_perm(dv[j].y, dv[j].x, 0x07060302u);
                 const unsigned Y1 = __builtin_amdgcn_perm(dv[j + 1].y, dv[j + 1].x, 0x07060302u);
-                const int gxr = sdot2(X0, GW0, sdot2_r(X1, GW1, rnd_d)) >> W_BITS;
-                const int gyr = sdot2(Y0, GW0, sdot2_r(Y1, GW1, rnd_d)) >> W_BITS;
+                const int gxr = sdot2(X0, GW0, sdot2_r(X1, GW1, rnd_d)) >> (W_BITS + kDerShift);
+                const int gyr = sdot2(Y0, GW0, sdot2_r(Y1, GW1, rnd_d)) >> (W_BITS + kDerShift);
                 if (S::FULL) {
                     gx[j] = gxr;
                     gy[j] = gyr;
@@ -973,7 +978,7 @@ __device__ __forceinline__ void strip_setup(const unsigned* P, const u32x2a4* D,
                                             unsigned GW0, unsigned GW1, unsigned* I2, unsigned* GX, unsigned* GY,
                                             int& a11, int& a12, int& a22) {
     constexpr int NP = (NR + 1) / 2;
-    const int rnd_i = 1 << (W_BITS - 6), rnd_d = 1 << (W_BITS - 1);
+    const int rnd_i = 1 << (W_BITS - 6), rnd_d = 1 << (W_BITS + kDerShift - 1);
     int iv[2 * NP], gx[2 * NP], gy[2 * NP];
     iv[2 * NP - 1] = gx[2 * NP - 1] = gy[2 * NP - 1] = 0;
 #pragma unroll
@@ -983,14 +988,15 @@ __device__ __forceinline__ void strip_setup(const unsigned* P, const u32x2a4* D,
         const unsigned X1 = __builtin_amdgcn_perm(D[j + 1].y, D[j + 1].x, 0x05040100u);
         const unsigned Y0 = __builtin_amdgcn_perm(D[j].y, D[j].x, 0x07060302u);
         const unsigned Y1 = __builtin_amdgcn_perm(D[j + 1].y, D[j + 1].x, 0x07060302u);
-        gx[j] = sdot2(X0, GW0, sdot2_r(X1, GW1, rnd_d)) >> W_BITS;
-        gy[j] = sdot2(Y0, GW0, sdot2_r(Y1, GW1, rnd_d)) >> W_BITS;
+        gx[j] = sdot2(X0, GW0, sdot2_r(X1, GW1, rnd_d));  // CV_DESCALE(., W_BITS) in bits 16..31
+        gy[j] = sdot2(Y0, GW0, sdot2_r(Y1, GW1, rnd_d));
     }
+    static_assert(W_BITS + kDerShift == 16, "derivative sums must carry their descaled value in bits 16..31");
 #pragma unroll
     for (int m = 0; m < NP; m++) {
         I2[m] = lo16x2(iv[2 * m], iv[2 * m + 1]);
-        GX[m] = lo16x2(gx[2 * m], gx[2 * m + 1]);
-        GY[m] = lo16x2(gy[2 * m], gy[2 * m + 1]);
+        GX[m] = hi16x2(gx[2 * m], gx[2 * m + 1]);
+        GY[m] = hi16x2(gy[2 * m], gy[2 * m + 1]);
         a11 = sdot2(GX[m], GX[m], a11);
         a12 = sdot2(GX[m], GY[m], a12);
         a22 = sdot2(GY[m], GY[m], a22);
@@ -1015,14 +1021,18 @@ __device__ __forceinline__ bool region_in_pad(const ImgLevel& L, int xa, int y0)
            y0 + JRH <= L.h + kPyrPad;
 }
 
-// One staged dword -> four pixel pairs (this lane's dword and the next lane's).
+// One staged dword -> four pixel pairs (this lane's dword and the next lane's),
+// each pixel scaled by 2^kJShift (<= 32640, int16): the bilinear J sum then
+// carries CV_DESCALE(., W_BITS - 5) in its high 16 bits, packed by one permute.
+constexpr int kJShift = 7;
+static_assert(W_BITS - 5 + kJShift == 16, "J sums must carry their descaled value in bits 16..31");
 __device__ __forceinline__ void stage_write(unsigned* dst, unsigned v, int lane) {
     const unsigned nv = (unsigned)__builtin_amdgcn_ds_bpermute((lane + 1) << 2, (int)v);
     uint4 o;
-    o.x = __builtin_amdgcn_perm(nv, v, 0x0c010c00u);
-    o.y = __builtin_amdgcn_perm(nv, v, 0x0c020c01u);
-    o.z = __builtin_amdgcn_perm(nv, v, 0x0c030c02u);
-    o.w = __builtin_amdgcn_perm(nv, v, 0x0c040c03u);
+    o.x = __builtin_amdgcn_perm(nv, v, 0x0c010c00u) << kJShift;
+    o.y = __builtin_amdgcn_perm(nv, v, 0x0c020c01u) << kJShift;
+    o.z = __builtin_amdgcn_perm(nv, v, 0x0c030c02u) << kJShift;
+    o.w = __builtin_amdgcn_perm(nv, v, 0x0c040c03u) << kJShift;
     *reinterpret_cast<uint4*>(dst) = o;
 }
 
@@ -1085,7 +1095,7 @@ __global__ __launch_bounds__(64, MINW) void lk_dual_kernel(LKBatch B, LKDev p) {
     const bool hasB = l < 31;
     const int cB = upper ? l : (hasB ? 2 * k2 + 1 : 0), rB = upper ? 7 : (hasB ? 14 : 0);
     constexpr float halfWx = (WW - 1) * 0.5f, halfWy = (WH - 1) * 0.5f;
-    const int rnd_i = 1 << (W_BITS - 6);
+    const int rnd_j = 1 << (W_BITS - 6 + kJShift);
 
     const float px = prev_xy[2 * ptc], py = prev_xy[2 * ptc + 1];
     float nx = 0.f, ny = 0.f;
@@ -1263,14 +1273,14 @@ __global__ __launch_bounds__(64, MINW) void lk_dual_kernel(LKBatch B, LKDev p) {
                 int jva[2 * NP], jvb[2 * NP];
                 jva[2 * NP - 1] = jvb[2 * NP - 1] = 0;
 #pragma unroll
-                for (int k = 0; k < NR; k++) {
-                    jva[k] = sdot2(qa[k], W0, sdot2_r(qa[k + 1], W1, rnd_i)) >> (W_BITS - 5);
-                    jvb[k] = sdot2(qb[k], W0, sdot2_r(qb[k + 1], W1, rnd_i)) >> (W_BITS - 5);
+                for (int k = 0; k < NR; k++) {  // J x 2^kJShift: descaled value in bits 16..31
+                    jva[k] = sdot2(qa[k], W0, sdot2_r(qa[k + 1], W1, rnd_j));
+                    jvb[k] = sdot2(qb[k], W0, sdot2_r(qb[k + 1], W1, rnd_j));
                 }
 #pragma unroll
                 for (int m = 0; m < NP; m++) {
-                    const unsigned da = pk_sub16(lo16x2(jva[2 * m], jva[2 * m + 1]), I2A[m]);
-                    const unsigned db = pk_sub16(lo16x2(jvb[2 * m], jvb[2 * m + 1]), I2B[m]);
+                    const unsigned da = pk_sub16(hi16x2(jva[2 * m], jva[2 * m + 1]), I2A[m]);
+                    const unsigned db = pk_sub16(hi16x2(jvb[2 * m], jvb[2 * m + 1]), I2B[m]);
                     b1 = sdot2(da, GXA[m], b1);
                     b2 = sdot2(da, GYA[m], b2);
                     b1 = sdot2(db, GXB[m], b1);

@@ -86,28 +86,37 @@ __global__ __launch_bounds__(256) void pyr_down_batched_kernel(const PyrDesc* __
 }
 
 // REFLECT_101 border (kPyrPad pixels each side) of one level, written from the
-// level's interior: the top and bottom bands (full padded width), then the left
-// and right bands of the interior rows. Blocks of one level stride over them.
+// level's interior one aligned dword (4 pixels) per thread: the top and bottom
+// bands over the full padded width, then the left and right bands of the
+// interior rows (the right band starts at the dword holding column w, so it may
+// rewrite a few interior pixels with their own values). Blocks of one level
+// stride over the dwords.
 __device__ __forceinline__ void pad_level(const ImgLevel& L, int blk, int nblk) {
-    const int w = L.w, h = L.h, pw = w + 2 * kPyrPad;
-    const int n_tb = 2 * kPyrPad * pw, n = n_tb + 2 * kPyrPad * h;
+    constexpr int SIDE = kPyrPad / 4 + 1;  // dwords per row on each side (right side: alignment)
+    const int w = L.w, h = L.h, dw = (w + 2 * kPyrPad + 3) / 4;
+    const int n_tb = 2 * kPyrPad * dw, n = n_tb + 2 * SIDE * h;
     uint8_t* __restrict__ d = const_cast<uint8_t*>(L.data);
     for (int k = blk * 256 + (int)threadIdx.x; k < n; k += nblk * 256) {
-        int x, y;
+        int x0, y;
         if (k < n_tb) {
-            const int r = k / pw, c = k - r * pw;
+            const int r = k / dw, c = k - r * dw;
             y = r < kPyrPad ? r - kPyrPad : h + (r - kPyrPad);
-            x = c - kPyrPad;
+            x0 = 4 * c - kPyrPad;
         } else {
-            const int k2 = k - n_tb, r = k2 / (2 * kPyrPad), c = k2 - r * (2 * kPyrPad);
+            const int k2 = k - n_tb, r = k2 / (2 * SIDE), c = k2 - r * (2 * SIDE);
             y = r;
-            x = c < kPyrPad ? c - kPyrPad : w + (c - kPyrPad);
+            x0 = c < SIDE ? -kPyrPad + 4 * c : (w & ~3) + 4 * (c - SIDE);
+            if (c > 0 && c < SIDE && x0 >= 0) continue;  // left side: SIDE - 1 dwords suffice
         }
-        d[(ptrdiff_t)y * L.pitch + x] = d[(ptrdiff_t)refl101(y, h) * L.pitch + refl101(x, w)];
+        const uint8_t* srow = d + (ptrdiff_t)refl101(y, h) * L.pitch;
+        unsigned v = 0;
+#pragma unroll
+        for (int i = 0; i < 4; i++) v |= (unsigned)srow[refl101(x0 + i, w)] << (8 * i);
+        *reinterpret_cast<unsigned*>(d + (ptrdiff_t)y * L.pitch + x0) = v;
     }
 }
 
-constexpr int PAD_BLOCKS = 16;  // blocks per (level, sequence)
+constexpr int PAD_BLOCKS = 8;  // blocks per (level, sequence)
 
 __global__ __launch_bounds__(256) void pad_batched_kernel(const PyrDesc* __restrict__ descs) {
     pad_level(descs[blockIdx.z].lv[blockIdx.y], blockIdx.x, gridDim.x);
@@ -211,7 +220,7 @@ __global__ __launch_bounds__(256) void pyr_scharr_kernel(const PyrDesc* __restri
                 if (y < sh) {
                     const int ix = (3 * (tr + br) + 10 * mr) - (3 * (tl + bl) + 10 * ml);
                     const int iy = 3 * ((br - tr) + (bl - tl)) + 10 * (bm - tm);
-                    out[(size_t)y * op + x] = ((unsigned)iy << 16) | ((unsigned)ix & 0xFFFFu);
+                    out[(size_t)y * op + x] = ((unsigned)(iy * (1 << kDerShift)) << 16) | ((unsigned)(ix * (1 << kDerShift)) & 0xFFFFu);
                 }
                 tl = ml; tm = mm; tr = mr;
                 ml = bl; mm = bm; mr = br;

@@ -61,7 +61,7 @@ __global__ __launch_bounds__(256) void scharr_kernel(const PyrDesc* __restrict__
         const int bl = T[r + 2][c], bm = T[r + 2][c + 1], br = T[r + 2][c + 2];
         const int ix = (3 * (tr + br) + 10 * mr) - (3 * (tl + bl) + 10 * ml);
         const int iy = 3 * ((br - tr) + (bl - tl)) + 10 * (bm - tm);
-        out[(size_t)y * op + x] = ((unsigned)iy << 16) | ((unsigned)ix & 0xFFFFu);
+        out[(size_t)y * op + x] = ((unsigned)(iy * (1 << kDerShift)) << 16) | ((unsigned)(ix * (1 << kDerShift)) & 0xFFFFu);
     }
 }
 

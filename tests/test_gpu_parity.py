@@ -178,6 +178,28 @@ def test_lk_borders_and_out_of_image(ctx, lk_kernel):
         assert np.array_equal(ge.view(np.uint32), re_.view(np.uint32))
 
 
+@pytest.mark.parametrize("wh", [(321, 241), (322, 187), (323, 99), (324, 130), (45, 37)])
+def test_lk_border_padding_widths(ctx, wh):
+    """Levels are stored with REFLECT_101 borders written dword-wise (DESIGN.md
+    §4): every width mod 4 and tiny levels, points hugging all four edges."""
+    w, h = wh
+    sc, A, B = frames(w, h, seed=w)
+    rng = np.random.default_rng(w)
+    edge = np.concatenate([
+        np.c_[rng.uniform(-22, 12, 60), rng.uniform(0, h, 60)],
+        np.c_[rng.uniform(w - 12, w + 22, 60), rng.uniform(0, h, 60)],
+        np.c_[rng.uniform(0, w, 60), rng.uniform(-22, 12, 60)],
+        np.c_[rng.uniform(0, w, 60), rng.uniform(h - 12, h + 22, 60)],
+    ]).astype(np.float32)
+    ga, gb = ctx.image(A, 4), ctx.image(B, 4)
+    gn, gs, ge = ctx.calc_optical_flow_pyr_lk(ga, gb, edge, **{k: v for k, v in zip(
+        ("win_size", "max_level", "criteria", "flags"), TEMPORAL.values())})
+    rn, rs, re_, _ = O.lk(A, B, edge, *TEMPORAL.values())
+    assert np.array_equal(gs, rs)
+    assert np.array_equal(gn.view(np.uint32), rn.view(np.uint32))
+    assert np.array_equal(ge.view(np.uint32), re_.view(np.uint32))
+
+
 def test_lk_initial_flow_and_criteria(ctx):
     sc, A, B = frames(640, 376, seed=6)
     pts = O.fast(A, 20, True)[:500, :2]
