@@ -375,6 +375,8 @@ int svo_calc_optical_flow_pyr_lk(svo_ctx* ctx, const svo_image* prev, const svo_
     // SVO_LK_QUAD=0: one feature per wave for 21x21 too (tests compare both)
     const char* quad = std::getenv("SVO_LK_QUAD");
     p.quad = quad && quad[0] == '0' ? 0 : 1;
+    const char* multi = std::getenv("SVO_LK_MULTI");
+    if (multi) p.multi = std::atoi(multi);
     // derivative pyramid of prev (calcSharrDeriv per level), then LK
     size_t doff[kMaxLevels];
     int dpitch[kMaxLevels];

@@ -812,6 +812,11 @@ static int fe_front(svo_frontend* fe, int t) {
             return e && e[0] == '0';
         }();
         lp.quad = quad_off ? 0 : 1;
+        static const int multi = [] {
+            const char* e = std::getenv("SVO_LK_MULTI");
+            return e ? std::atoi(e) : 42;
+        }();
+        lp.multi = multi;
     }
     for (int g = 0; g < G; g++) {
         const int a = fe->g0[g], n = fe->gn[g];

@@ -1319,6 +1319,339 @@ __global__ __launch_bounds__(64, MINW) void lk_dual_kernel(LKBatch B, LKDev p) {
     }
 }
 
+// ---------------------------------------------------------------------------
+// FPW features per wave (21x21 windows): each group of LPF = 64 / FPW lanes
+// owns one feature; the window's 63 vertical 7-row strips (21 columns x 3 row
+// groups) are dealt to the group's lanes, lane l taking strips l, l + LPF, ...
+// (strip 63, where it exists, carries zero weights). The per-feature work every
+// lane repeats (bilinear weights, bounds / convergence tests, the 2x2 solve) and
+// the exact group reduction serve FPW features per instruction. Staged next-
+// image regions (margin QJM) for all FPW features share the wave's LDS slice.
+// Same exact integer sums and float solve as every other LK kernel.
+template <int QJM>
+struct MultiShape {
+    static constexpr int JRW = ru4(21 + 2 * QJM + 3), JRH = 21 + 1 + 2 * QJM;
+    static constexpr int JBYTES = JRW * JRH * 4;
+};
+
+// Exact sums over the LPF lanes of each group (every lane receives its group's
+// total), as floats of the exact integers (one rounding): int32 DPP steps while
+// the partial sums provably fit (STEPS32), then 16-bit halves.
+template <int LPF, int STEPS32>
+__device__ __forceinline__ int group_add_step(int v, int step) {
+    switch (step) {
+        case 0: return dpp_row_add<0xb1>(v);   // quad_perm 1,0,3,2
+        case 1: return dpp_row_add<0x4e>(v);   // quad_perm 2,3,0,1
+        case 2: return dpp_row_add<0x124>(v);  // row_ror:4
+        case 3: return dpp_row_add<0x128>(v);  // row_ror:8
+        default: return swz16_add(v);          // lane ^ 16
+    }
+}
+template <int LPF, int STEPS32, int NV>
+__device__ __forceinline__ void group_sum_f(int (&v)[NV], float (&f)[NV]) {
+    constexpr int STEPS = LPF == 16 ? 4 : 5;
+    static_assert(LPF == 16 || LPF == 32, "groups of 16 or 32 lanes");
+#pragma unroll
+    for (int s = 0; s < STEPS32; s++)
+#pragma unroll
+        for (int i = 0; i < NV; i++) v[i] = group_add_step<LPF, STEPS32>(v[i], s);
+    int h[NV], lo[NV];
+#pragma unroll
+    for (int i = 0; i < NV; i++) {
+        h[i] = v[i] >> 16;
+        lo[i] = v[i] & 0xFFFF;
+    }
+#pragma unroll
+    for (int s = STEPS32; s < STEPS; s++)
+#pragma unroll
+        for (int i = 0; i < NV; i++) {
+            h[i] = group_add_step<LPF, STEPS32>(h[i], s);
+            lo[i] = group_add_step<LPF, STEPS32>(lo[i], s);
+        }
+#pragma unroll
+    for (int i = 0; i < NV; i++) f[i] = halves_lane_float(h[i], lo[i]);
+}
+
+template <int FPW, int QJM, int MINW, int KKS = 2>
+__global__ __launch_bounds__(64, MINW) void lk_multi_kernel(LKBatch B, LKDev p) {
+    constexpr int WW = 21, WH = 21;
+    using Q = MultiShape<QJM>;
+    static_assert(WW + QJM + 3 <= kPyrPad && WW + 1 <= kDerPad, "padding too small for the window");
+    constexpr int JRW = Q::JRW, JRH = Q::JRH;
+    constexpr int NR = 7, NP = 4;
+    constexpr int LPF = 64 / FPW;                 // lanes per feature
+    constexpr int K = (63 + LPF - 1) / LPF;       // strips per lane
+    // int32 partial sums: a lane holds <= 7K products |diff * g| <= 8160 * 4080
+    // (A sums: 4080^2); steps while 2^steps * 7K * 8160 * 4080 < 2^31
+    constexpr int STEPS32 = K >= 4 ? 1 : 2;
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    const int lane = threadIdx.x & 63;
+    const int g = lane / LPF, l = lane % LPF;
+    const int seq = blockIdx.y;
+    const int n = B.counts ? B.counts[seq] : B.n;
+    const int pt0 = blockIdx.x * FPW;
+    if (pt0 >= n) return;
+    const int pt = pt0 + g;
+    const bool live = pt < n;
+    const int ptc = live ? pt : n - 1;  // an idle group shadows a real feature, writes nothing
+    const size_t base = (size_t)seq * B.cap;
+    const float* __restrict__ prev_xy = B.prev_xy + 2 * base;
+    float* __restrict__ next_xy = B.next_xy + 2 * base;
+    const cpyr prev = (cpyr)B.prev + seq;
+    const cpyr next = (cpyr)B.next + seq;
+    const DerivDesc& dprev = B.dprev[seq];
+    unsigned* jregs = reinterpret_cast<unsigned*>(lds);
+    unsigned* sink = reinterpret_cast<unsigned*>(lds + FPW * Q::JBYTES);
+    const unsigned* jmine = jregs + g * (Q::JBYTES / 4);
+
+    // the lane's strips: column, first row, LDS offset; strip 63 is a dummy
+    int scol[K], srow[K];
+    bool sreal[K];
+#pragma unroll
+    for (int k = 0; k < K; k++) {
+        const int sidx = l + LPF * k;
+        sreal[k] = sidx < 63;
+        const int sc = sreal[k] ? sidx : 0;
+        scol[k] = sc % 21;
+        srow[k] = (sc / 21) * NR;
+    }
+    constexpr float halfWx = (WW - 1) * 0.5f, halfWy = (WH - 1) * 0.5f;
+    const int rnd_j = 1 << (W_BITS - 6 + kJShift);
+
+    const float px = prev_xy[2 * ptc], py = prev_xy[2 * ptc + 1];
+    float nx = 0.f, ny = 0.f;
+    if (p.flags & SVO_LK_USE_INITIAL_FLOW) {
+        nx = next_xy[2 * ptc];
+        ny = next_xy[2 * ptc + 1];
+    }
+    int st = live ? 1 : 0;
+    float errv = 0.f;
+    int itcount = 0;
+    const int max_level = p.max_level;
+
+    for (int level = max_level; level >= 0; level--) {
+        const ImgLevel I{prev->lv[level].data, prev->lv[level].w, prev->lv[level].h, prev->lv[level].pitch};
+        const ImgLevel J{next->lv[level].data, next->lv[level].w, next->lv[level].h, next->lv[level].pitch};
+        const float lscale = __builtin_amdgcn_ldexpf(1.f, -level);
+        float prevx = px * lscale, prevy = py * lscale;
+        float nextx, nexty;
+        if (level == max_level) {
+            if (p.flags & SVO_LK_USE_INITIAL_FLOW) {
+                nextx = nx * lscale;
+                nexty = ny * lscale;
+            } else {
+                nextx = prevx;
+                nexty = prevy;
+            }
+        } else {
+            nextx = nx * 2.f;
+            nexty = ny * 2.f;
+        }
+        nx = nextx;
+        ny = nexty;
+        prevx -= halfWx;
+        prevy -= halfWy;
+        const int ipx = ufloor(prevx), ipy = ufloor(prevy);
+        const bool inb = !(ipx < -WW || ipx >= I.w || ipy < -WH || ipy >= I.h);
+        if (!inb && level == 0 && live) {
+            st = 0;
+            errv = 0.f;
+        }
+        bool lact = live && inb;
+        const float a = prevx - ipx, b = prevy - ipy;
+        const int iw00 = uround((1.f - a) * (1.f - b) * (1 << W_BITS));
+        const int iw01 = uround(a * (1.f - b) * (1 << W_BITS));
+        const int iw10 = uround((1.f - a) * b * (1 << W_BITS));
+        const int iw11 = (1 << W_BITS) - iw00 - iw01 - iw10;
+        const unsigned IW0 = pack16(iw00, iw01), IW1 = pack16(iw10, iw11);
+
+        int jx0 = ufloor(nextx - halfWx) - QJM, jy0 = ufloor(nexty - halfWy) - QJM;
+        int jxa = jx0 & ~3;
+        unsigned I2[K][NP], GX[K][NP], GY[K][NP];
+        int asum[3] = {0, 0, 0};
+        {
+            // branch-free reads (padded levels); an inactive group (or one whose
+            // region lies beyond the padding: its first bounds test deactivates
+            // it) stages and reads at the level origin, results unused
+            using SL = DualStageLoads<JRW, JRH>;
+            const int lr = lane / SL::LPR, d = lane - lr * SL::LPR;
+            int xs[FPW], ys[FPW];
+#pragma unroll
+            for (int f = 0; f < FPW; f++) {
+                const int xa = __builtin_amdgcn_readlane(jxa, LPF * f), y0 = __builtin_amdgcn_readlane(jy0, LPF * f);
+                const bool ok = __builtin_amdgcn_readlane((int)lact, LPF * f) && region_in_pad<JRW, JRH>(J, xa, y0);
+                xs[f] = ok ? xa : 0;
+                ys[f] = ok ? y0 : 0;
+            }
+            unsigned sv[FPW][SL::NPS];
+#pragma unroll
+            for (int f = 0; f < FPW; f++) {
+                gu8 src = (gu8)J.data + xs[f] + 4 * d;
+#pragma unroll
+                for (int q = 0; q < SL::NPS; q++) {
+                    int r = q * SL::RPP + lr;
+                    r = r < JRH ? r : JRH - 1;
+                    sv[f][q] = *(gu32)(src + (ptrdiff_t)(ys[f] + r) * J.pitch);
+                }
+            }
+            const int dpitch = dprev.pitch[level];
+            gu32 dsrc = (gu32)dprev.data[level];
+            const int sx = inb ? ipx : 0, sy = inb ? ipy : 0;
+            // strips KKS at a time: loads of a group in flight together
+#pragma unroll
+            for (int k0 = 0; k0 < K; k0 += KKS) {
+                constexpr int KK = K >= KKS ? KKS : 1;
+                unsigned P[KK][NR + 1];
+                u32x2a4 D[KK][NR + 1];
+#pragma unroll
+                for (int kk = 0; kk < KK; kk++) {
+                    const int x = sx + scol[k0 + kk], y = sy + srow[k0 + kk];
+                    gu8 ia = (gu8)I.data + (ptrdiff_t)y * I.pitch + x;
+                    gu32 qa = dsrc + (ptrdiff_t)y * dpitch + x;
+#pragma unroll
+                    for (int r = 0; r <= NR; r++) {
+                        P[kk][r] = __builtin_amdgcn_perm(0u, (unsigned)*(gu16u)(ia + (ptrdiff_t)r * I.pitch),
+                                                         0x0c010c00u);
+                        D[kk][r] = *(const __attribute__((address_space(1))) u32x2a4*)(qa + (ptrdiff_t)r * dpitch);
+                    }
+                }
+                if (k0 == 0) {
+                    const bool wr = d < JRW / 4 && lr < SL::RPP;
+#pragma unroll
+                    for (int f = 0; f < FPW; f++) {
+                        unsigned* dpl = wr ? jregs + f * (Q::JBYTES / 4) + 4 * d : sink;
+                        const int dstride = wr ? JRW : 0;
+#pragma unroll
+                        for (int q = 0; q < SL::NPS; q++) {
+                            int r = q * SL::RPP + lr;
+                            r = r < JRH ? r : JRH - 1;
+                            stage_write(dpl + r * dstride, sv[f][q], lane);
+                        }
+                    }
+                }
+#pragma unroll
+                for (int kk = 0; kk < KK; kk++) {
+                    const int k = k0 + kk;
+                    strip_setup<NR>(P[kk], D[kk], IW0, IW1, sreal[k] ? IW0 : 0u, sreal[k] ? IW1 : 0u, I2[k],
+                                    GX[k], GY[k], asum[0], asum[1], asum[2]);
+                }
+            }
+        }
+        wave_lds_sync();
+        float A[3];
+        group_sum_f<LPF, STEPS32>(asum, A);
+        const float A11 = A[0], A12 = A[1], A22 = A[2];
+
+        float D = A11 * A22 - A12 * A12;
+        const float minEig =
+            (A22 + A11 - sqrtf((A11 - A22) * (A11 - A22) + 4.f * A12 * A12)) / (float)(2 * WW * WH);
+        if (lact && p.want_err && (p.flags & SVO_LK_GET_MIN_EIGENVALS)) errv = minEig;
+        if (lact && (minEig < p.min_eig || D < FLT_EPSILON)) {
+            if (level == 0) st = 0;
+            lact = false;
+        }
+        D = 1.f / D;
+
+        nextx -= halfWx;
+        nexty -= halfWy;
+        float pdx = 0.f, pdy = 0.f;
+        for (int j = 0; j < p.max_count; j++) {
+            if (__builtin_amdgcn_ballot_w64(lact) == 0) break;
+            const int inx = ufloor(nextx), iny = ufloor(nexty);
+            if (lact && (inx < -WW || inx >= J.w || iny < -WH || iny >= J.h)) {
+                if (level == 0) st = 0;
+                lact = false;
+            }
+            const bool need = lact && ((unsigned)(inx - jx0) > 2u * QJM || (unsigned)(iny - jy0) > 2u * QJM);
+            if (need) {
+                jx0 = inx - QJM;
+                jy0 = iny - QJM;
+                jxa = jx0 & ~3;
+            }
+            unsigned long long nb = __builtin_amdgcn_ballot_w64(need && l == 0);
+            if (nb) {
+                wave_lds_sync();
+                while (nb) {
+                    const int f = (int)(__builtin_ctzll(nb) / LPF);
+                    nb &= nb - 1;
+                    stage_padded<JRW, JRH>(jregs + f * (Q::JBYTES / 4), sink, J,
+                                           __builtin_amdgcn_readlane(jxa, LPF * f),
+                                           __builtin_amdgcn_readlane(jy0, LPF * f), lane);
+                }
+                wave_lds_sync();
+            }
+            itcount += lact ? 1 : 0;
+            const float aa = nextx - inx, bb = nexty - iny;
+            const int w00 = uround((1.f - aa) * (1.f - bb) * (1 << W_BITS));
+            const int w01 = uround(aa * (1.f - bb) * (1 << W_BITS));
+            const int w10 = uround((1.f - aa) * bb * (1 << W_BITS));
+            const int w11 = (1 << W_BITS) - w00 - w01 - w10;
+            const unsigned W0 = pack16(w00, w01), W1 = pack16(w10, w11);
+            int bsum[2] = {0, 0};
+            {
+                // an inactive group reads inside its own region (results unused)
+                const int ro = lact ? iny - jy0 : 0, co = lact ? inx - jxa : 0;
+                const unsigned* jb = jmine + ro * JRW + co;
+#pragma unroll
+                for (int k = 0; k < K; k++) {
+                    const unsigned* js = jb + srow[k] * JRW + scol[k];
+                    unsigned q[NR + 1];
+#pragma unroll
+                    for (int r = 0; r <= NR; r++) q[r] = js[r * JRW];
+                    int jv[2 * NP];
+                    jv[2 * NP - 1] = 0;
+#pragma unroll
+                    for (int r = 0; r < NR; r++)  // J x 2^kJShift: descaled value in bits 16..31
+                        jv[r] = sdot2(q[r], W0, sdot2_r(q[r + 1], W1, rnd_j));
+#pragma unroll
+                    for (int m = 0; m < NP; m++) {
+                        const unsigned dd = pk_sub16(hi16x2(jv[2 * m], jv[2 * m + 1]), I2[k][m]);
+                        bsum[0] = sdot2(dd, GX[k][m], bsum[0]);
+                        bsum[1] = sdot2(dd, GY[k][m], bsum[1]);
+                    }
+                }
+            }
+            float fb[2];
+            group_sum_f<LPF, STEPS32>(bsum, fb);
+            const float fb1 = fb[0], fb2 = fb[1];
+            const float dx = (A12 * fb2 - A22 * fb1) * D;
+            const float dy = (A12 * fb1 - A11 * fb2) * D;
+            if (lact) {
+                nextx += dx;
+                nexty += dy;
+                nx = nextx + halfWx;
+                ny = nexty + halfWy;
+                if ((double)dx * dx + (double)dy * dy <= p.eps2) {
+                    lact = false;
+                } else if (j > 0 && (double)fabsf(dx + pdx) < 0.01 && (double)fabsf(dy + pdy) < 0.01) {
+                    nx -= dx * 0.5f;
+                    ny -= dy * 0.5f;
+                    lact = false;
+                } else {
+                    pdx = dx;
+                    pdy = dy;
+                }
+            }
+        }
+        wave_lds_sync();
+    }
+    if (l == 0 && live) {
+        next_xy[2 * pt] = nx;
+        next_xy[2 * pt + 1] = ny;
+        B.status[base + pt] = (uint8_t)st;
+        if (B.err) B.err[base + pt] = errv;
+        if (B.iters) B.iters[base + pt] = itcount;
+    }
+}
+
+template <int FPW, int QJM, int MINW = 4, int KKS = 2>
+hipError_t launch_multi(const LKBatch& b, int nseq, int max_n, const LKDev& d, hipStream_t st) {
+    dim3 grid((max_n + FPW - 1) / FPW, nseq);
+    constexpr int lds_bytes = FPW * MultiShape<QJM>::JBYTES + 16;
+    hipLaunchKernelGGL((lk_multi_kernel<FPW, QJM, MINW, KKS>), grid, dim3(64), lds_bytes, st, b, d);
+    return hipGetLastError();
+}
+
 template <int WW, int WH>
 hipError_t launch_dual(const LKBatch& b, int nseq, int max_n, const LKDev& d, hipStream_t st) {
     dim3 grid((max_n + 1) / 2, nseq);
@@ -1387,8 +1720,17 @@ hipError_t launch_lk(const LKBatch& b, int nseq, int max_n, const LKParams& lp, 
     if (!lp.generic) {
         // two features per wave: the SAD error (flags 0 + want_err) stays on lk_fast_kernel
         const bool dual_ok = !(lp.want_err && !(lp.flags & SVO_LK_GET_MIN_EIGENVALS));
-        if (lp.win_w == 21 && lp.win_h == 21 && dual_ok && lp.quad)
-            return launch_dual<21, 21>(b, nseq, max_n, d, st);
+        if (lp.win_w == 21 && lp.win_h == 21 && dual_ok && lp.quad) {
+            // SVO_LK_MULTI: 42 (default) four features per wave, 2-px staging
+            // margin; 43 the same with a 3-px margin; 2 two per wave (generic
+            // map); 0 the dual kernel (its own lane map)
+            switch (lp.multi) {
+                case 0: return launch_dual<21, 21>(b, nseq, max_n, d, st);
+                case 2: return launch_multi<2, 3>(b, nseq, max_n, d, st);
+                case 43: return launch_multi<4, 3, 3>(b, nseq, max_n, d, st);
+                default: return launch_multi<4, 2, 3>(b, nseq, max_n, d, st);
+            }
+        }
         if (lp.win_w == 21 && lp.win_h == 21) return launch_fast<21, 21>(b, nseq, max_n, d, st);
         if (lp.win_w == 11 && lp.win_h == 11) return launch_fast<11, 11>(b, nseq, max_n, d, st);
         if (lp.win_w == 15 && lp.win_h == 15) return launch_fast<15, 15>(b, nseq, max_n, d, st);

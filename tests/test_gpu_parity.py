@@ -123,14 +123,16 @@ TEMPORAL = dict(win=(21, 21), ml=3, crit=(3, 50, 1e-3), flags=S.LK_GET_MIN_EIGEN
 STEREO = dict(win=(11, 11), ml=3, crit=(3, 30, 1e-3), flags=0)                        # R:src/tracking.cpp:101-105
 
 
-@pytest.fixture(params=["fixed-window", "generic", "one-per-wave"])
+@pytest.fixture(params=["fixed-window", "generic", "one-per-wave", "dual", "two-per-wave"])
 def lk_kernel(request, monkeypatch):
-    """Every LK kernel: the compile-time-window ones (21x21 four features per wave
-    by default, 11x11, 15x15, 31x31), the 21x21 one-feature-per-wave kernel
-    (SVO_LK_QUAD=0) and the runtime-window one every other size uses
+    """Every LK kernel: the compile-time-window ones (21x21 four features per
+    wave by default, 11x11, 15x15, 31x31), the 21x21 one-feature-per-wave kernel
+    (SVO_LK_QUAD=0), the 21x21 two-per-wave kernels (SVO_LK_MULTI=0: lk_dual_kernel,
+    2: lk_multi_kernel<2>) and the runtime-window one every other size uses
     (SVO_LK_GENERIC=1)."""
     monkeypatch.setenv("SVO_LK_GENERIC", "1" if request.param == "generic" else "0")
     monkeypatch.setenv("SVO_LK_QUAD", "0" if request.param == "one-per-wave" else "1")
+    monkeypatch.setenv("SVO_LK_MULTI", {"dual": "0", "two-per-wave": "2"}.get(request.param, "42"))
     return request.param
 
 
