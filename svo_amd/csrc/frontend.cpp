@@ -172,7 +172,8 @@ struct svo_frontend {
     void* hmem = nullptr;
     int *h_nB, *h_nA, *h_cnt, *h_added;
     long long* h_itsum;
-    float *h_xyB, *h_obj, *h_samp;
+    float *h_xyB, *h_obj, *h_samp;   // h_xyB / h_obj: this step's parity half of h_*_b
+    float *h_xyB_b[2], *h_obj_b[2];
     double *h_hyps, *h_stats;
     uint32_t *h_bits, *h_best;
     // host-coherent buffers the scoring kernel reads / writes directly (zero-copy:
@@ -195,8 +196,11 @@ struct svo_frontend {
     // the final fits, RANSAC past the prefetched subsets and the n <= 5 solve, so
     // they travel on their own stream once requested
     hipStream_t st_copy = nullptr;
-    hipEvent_t ev_gathered = nullptr, ev_full = nullptr;
+    hipEvent_t ev_gathered = nullptr, ev_full = nullptr;  // ev_full: this step's parity of ev_full_b
+    hipEvent_t ev_full_b[2] = {nullptr, nullptr};
     bool full_queued = false;
+    int fit_parity = 0;  // step parity whose RANSAC results the pending fits refine
+    hipEvent_t ev_counts = nullptr;  // the step's feature counts on the host
     Pool* pool = nullptr;
     // pipeline: slices of the batch [g0[g], g0[g] + gn[g]) on their own streams
     int G = 1;
@@ -330,6 +334,8 @@ int fe_queue_full(svo_frontend* fe) {
     svo_ctx* ctx = fe->ctx;
     const size_t S = fe->S, CAP = fe->CAP;
     SVO_HIP(ctx, hipStreamWaitEvent(fe->st_copy, fe->ev_gathered, 0));
+    // (the copy stream also waited for the RANSAC subsets' D2H: the bulk copy
+    // does not compete with that critical one)
     SVO_HIP(ctx, hipMemcpyAsync(fe->h_xyB, fe->xyB, sizeof(float) * 2 * S * CAP, hipMemcpyDeviceToHost, fe->st_copy));
     SVO_HIP(ctx, hipMemcpyAsync(fe->h_obj, fe->obj, sizeof(float) * 3 * S * CAP, hipMemcpyDeviceToHost, fe->st_copy));
     SVO_HIP(ctx, hipEventRecord(fe->ev_full, fe->st_copy));
@@ -358,7 +364,7 @@ double fe_finish_fits(svo_frontend* fe) {
     if (!fe->fits_pending) return 0.0;
     auto t0 = std::chrono::steady_clock::now();
     (void)hipEventSynchronize(fe->ev_stats);
-    if (fe->full_queued) (void)hipEventSynchronize(fe->ev_full);  // cheirality test reads h_obj
+    (void)hipEventSynchronize(fe->ev_full_b[fe->fit_parity]);  // cheirality test reads h_obj
     fe->pool->run(fe->S, [&](int s) {
         RansacSeq& r = fe->rs[s];
         r.fit(fe->cfg.K, fe->h_stats + 60 * (size_t)s);
@@ -509,6 +515,7 @@ int svo_frontend_create(svo_ctx* ctx, const svo_frontend_config* cfg, svo_fronte
         add(sizeof(int) * S * 4);
         add(sizeof(long long) * S);
         add(sizeof(float) * 5 * (size_t)S * CAP);
+        add(sizeof(float) * 5 * (size_t)S * CAP);  // the second parity of h_xyB / h_obj
         add(sizeof(double) * 12 * (size_t)S * kRansacChunk);
         add(sizeof(int) * (size_t)S * kRansacChunk);
         add(sizeof(uint32_t) * (size_t)S * kRansacChunk * fe->WORDS);
@@ -529,8 +536,12 @@ int svo_frontend_create(svo_ctx* ctx, const svo_frontend_config* cfg, svo_fronte
         fe->h_cnt = carve<int>(p, (size_t)S * kRansacChunk);
         fe->h_added = carve<int>(p, S);
         fe->h_itsum = carve<long long>(p, S);
-        fe->h_xyB = carve<float>(p, 2 * (size_t)S * CAP);
-        fe->h_obj = carve<float>(p, 3 * (size_t)S * CAP);
+        for (int k = 0; k < 2; k++) {
+            fe->h_xyB_b[k] = carve<float>(p, 2 * (size_t)S * CAP);
+            fe->h_obj_b[k] = carve<float>(p, 3 * (size_t)S * CAP);
+        }
+        fe->h_xyB = fe->h_xyB_b[0];
+        fe->h_obj = fe->h_obj_b[0];
         fe->h_hyps = carve<double>(p, 12 * (size_t)S * kRansacChunk);
         fe->h_bits = carve<uint32_t>(p, (size_t)S * kRansacChunk * fe->WORDS);
         fe->h_best = carve<uint32_t>(p, (size_t)S * fe->WORDS);
@@ -618,7 +629,9 @@ int svo_frontend_create(svo_ctx* ctx, const svo_frontend_config* cfg, svo_fronte
         (void)hipEventCreateWithFlags(&fe->ev_gathered, hipEventDisableTiming);
         fe->ev_tail.assign(G, nullptr);
         for (auto& e : fe->ev_tail) (void)hipEventCreateWithFlags(&e, hipEventDisableTiming);
-        (void)hipEventCreateWithFlags(&fe->ev_full, hipEventDisableTiming);
+        for (auto& e : fe->ev_full_b) (void)hipEventCreateWithFlags(&e, hipEventDisableTiming);
+        fe->ev_full = fe->ev_full_b[0];
+        (void)hipEventCreateWithFlags(&fe->ev_counts, hipEventDisableTiming);
         if (hipStreamCreateWithFlags(&fe->st_copy, hipStreamNonBlocking) != hipSuccess) {
             svo_frontend_destroy(fe);
             return set_error(ctx, SVO_ERR_HIP, "svo_frontend_create: stream");
@@ -662,7 +675,9 @@ void svo_frontend_destroy(svo_frontend* fe) {
     if (fe->ev_gathered) (void)hipEventDestroy(fe->ev_gathered);
     for (auto& e : fe->ev_tail)
         if (e) (void)hipEventDestroy(e);
-    if (fe->ev_full) (void)hipEventDestroy(fe->ev_full);
+    for (auto& e : fe->ev_full_b)
+        if (e) (void)hipEventDestroy(e);
+    if (fe->ev_counts) (void)hipEventDestroy(fe->ev_counts);
     delete fe;
 }
 
@@ -759,20 +774,24 @@ int svo_frontend_init(svo_frontend* fe, int t0) {
 // frame t+1's pyramid, compaction / gather / RANSAC subsets and their D2H, FAST.
 // svo_frontend_step enqueues the next step's first half right after its own
 // tail, so the GPU goes on with LK while the caller is between steps.
-static int fe_front(svo_frontend* fe, int t) {
+static int fe_front_lk(svo_frontend* fe, int t) {
     svo_ctx* ctx = fe->ctx;
     hipStream_t st0 = ctx->stream;
     const int S = fe->S, CAP = fe->CAP, G = fe->G;
     const svo_frontend_config& c = fe->cfg;
     const PyrDesc* dprev = fe->d_desc + (size_t)((t - 1) % fe->T) * S;
     const PyrDesc* dcur = fe->d_desc + (size_t)(t % fe->T) * S;
-    hipEvent_t ev_pyr = fe->ev_sync[0], ev_fast = fe->ev_sync[1];
+    hipEvent_t ev_pyr = fe->ev_sync[0];
     int slot;
     // this step's parity buffers (the previous step's stay with its side work)
     fe->xyB = fe->xyB_b[t & 1];
     fe->obj = fe->obj_b[t & 1];
     fe->nB = fe->nB_b[t & 1];
     fe->bits_best = fe->bits_best_b[t & 1];
+    fe->h_xyB = fe->h_xyB_b[t & 1];
+    fe->h_obj = fe->h_obj_b[t & 1];
+    fe->ev_full = fe->ev_full_b[t & 1];
+    fe->full_queued = false;
     // 0. the previous step's SQPnP statistics and the binning of the FAST mask's
     //    box centres (frame t-1's features) normally went out at the end of that
     //    step, ahead of this step's LK (a kernel queued beside LK waits for it:
@@ -832,6 +851,18 @@ static int fe_front(svo_frontend* fe, int t) {
         ph_end(fe, sg, slot);
         SVO_HIP(ctx, hipEventRecord(fe->ev_sync[2 + 2 * g], sg));
     }
+    return SVO_OK;
+}
+
+// The rest of a step's first half: frame t+1's pyramid, compaction / gather /
+// RANSAC subsets and their D2H, the full point copy, FAST.
+static int fe_front_rest(svo_frontend* fe, int t) {
+    svo_ctx* ctx = fe->ctx;
+    hipStream_t st0 = ctx->stream;
+    const int S = fe->S, CAP = fe->CAP, G = fe->G;
+    const PyrDesc* dcur = fe->d_desc + (size_t)(t % fe->T) * S;
+    hipEvent_t ev_fast = fe->ev_sync[1];
+    int slot;
     // 3b'. build frame t+1's pyramid + Scharr ahead, once every LK of this step is
     //      done (the Scharr ping-pong buffer it writes is the one LK reads): it
     //      runs while the host solves RANSAC. Used if the next step is t+1.
@@ -874,6 +905,13 @@ static int fe_front(svo_frontend* fe, int t) {
     // every slice's points are gathered once the last slice's copies are queued
     // (slices run in order on their streams; the full copy waits for the last)
     SVO_HIP(ctx, hipEventRecord(fe->ev_gathered, fe->gst[G - 1]));
+    // the full point set for the final fits / long RANSAC runs, on the copy
+    // stream behind the subsets' D2H (parity buffers: the previous step's fits
+    // still read theirs)
+    {
+        int rq = fe_queue_full(fe);
+        if (rq) return rq;
+    }
 
     // 3b. mask around frame t-1's features (the reference masks with prevFrame's
     //     features, R:src/tracking.cpp:77) + FAST/bucket on frame t, whole batch,
@@ -884,9 +922,13 @@ static int fe_front(svo_frontend* fe, int t) {
     int rc = fe_fast_and_bucket(fe, dcur, true, sf, true);
     if (rc) return rc;
     SVO_HIP(ctx, hipEventRecord(ev_fast, sf));
-
-
     return SVO_OK;
+}
+
+static int fe_front(svo_frontend* fe, int t) {
+    int rc = fe_front_lk(fe, t);
+    if (rc) return rc;
+    return fe_front_rest(fe, t);
 }
 
 int svo_frontend_step(svo_frontend* fe, int t, svo_frontend_stats* stats) {
@@ -918,7 +960,6 @@ int svo_frontend_step(svo_frontend* fe, int t, svo_frontend_stats* stats) {
     // while the GPU tracks this frame
     double ms_fit = fe_finish_fits(fe);
     TP("fits done");
-    fe->full_queued = false;
     hipEvent_t ev_fast = fe->ev_sync[1];
     hipStream_t sf = fe->st_fast;
     int rc = SVO_OK;
@@ -1070,6 +1111,7 @@ int svo_frontend_step(svo_frontend* fe, int t, svo_frontend_stats* stats) {
                                     : 0;
         }
         ms_fit += ms_since(tf);
+        TP("selected");
         SVO_HIP(ctx, hipMemcpyAsync(fe->bits_best + (size_t)a * fe->WORDS, fe->h_best + (size_t)a * fe->WORDS,
                                     sizeof(uint32_t) * n * fe->WORDS, hipMemcpyHostToDevice, sg));
         // the SQPnP statistics only feed the pose fits, which run during the next
@@ -1080,28 +1122,25 @@ int svo_frontend_step(svo_frontend* fe, int t, svo_frontend_stats* stats) {
         CompactBatch cb2{fe->nB + a, nullptr, fe->bits_best + (size_t)a * fe->WORDS, fe->WORDS,
                          fe->xyB + 2 * (size_t)a * CAP, fe->midB + (size_t)a * CAP, nullptr, nullptr,
                          fe->xyA + 2 * (size_t)a * CAP, fe->midA + (size_t)a * CAP, fe->nA + a, CAP};
+        TP("bits queued");
         ph_begin(fe, PH_COMPACT, sg, &slot);
         SVO_HIP(ctx, launch_compact(cb2, n, sg));
         ph_end(fe, sg, slot);
         rc = fe_append(fe, t, a, n, sg);
         if (rc) return rc;
-        SVO_HIP(ctx, hipMemcpyAsync(fe->h_nA + a, fe->nA + a, sizeof(int) * n, hipMemcpyDeviceToHost, sg));
-        SVO_HIP(ctx, hipMemcpyAsync(fe->h_added + a, fe->added + a, sizeof(int) * n, hipMemcpyDeviceToHost, sg));
+        SVO_HIP(ctx, hipEventRecord(fe->ev_tail[g], sg));
+        TP("compact+append queued");
     }
     fe->fits_pending = true;  // statistics land with the stream syncs below
-    rc = fe_queue_full(fe);    // for the fits (cheirality test), off the critical path
-    if (rc) return rc;
-    // the next step's side work, queued now (before its LK): the SQPnP statistics
-    // of these inliers and the binning of these features as next frame's mask boxes
-    for (int g = 0; g < G; g++) {
-        SVO_HIP(ctx, hipEventRecord(fe->ev_tail[g], fe->gst[g]));
-        SVO_HIP(ctx, hipStreamWaitEvent(sf, fe->ev_tail[g], 0));
-    }
+    fe->fit_parity = t & 1;
+    // The critical path goes on with the next step's LK right behind this tail;
+    // only the SQPnP statistics of these inliers go to the GPU ahead of it (a
+    // kernel queued beside LK would wait for it: LK leaves no registers free, and
+    // the pose fits need them at the next step's start).
+    for (int g = 0; g < G; g++) SVO_HIP(ctx, hipStreamWaitEvent(sf, fe->ev_tail[g], 0));
     rc = fe_queue_stats(fe);
     if (rc) return rc;
-    SVO_HIP(ctx, launch_box_bin(fe_fast_batch(fe, dcur, true), S, fe->W, fe->H, sf));
-    fe->boxes_binned = true;
-    TP("tail enqueued");
+    TP("stats queued");
     // this step's counts, before the next step's first half re-fills the mirrors
     int64_t lk_its = 0, tracked = 0;
     for (int s = 0; s < S; s++) {
@@ -1114,15 +1153,31 @@ int svo_frontend_step(svo_frontend* fe, int t, svo_frontend_stats* stats) {
         const char* e = std::getenv("SVO_FE_PREFETCH");
         return !(e && e[0] == '0');
     }();
-    if (prefetch && t + 1 < fe->T) {
-        rc = fe_front(fe, t + 1);
+    const bool ahead = prefetch && t + 1 < fe->T;
+    fe->boxes_binned = true;  // queued just below, behind the next LK
+    if (ahead) {
+        rc = fe_front_lk(fe, t + 1);
+        if (rc) return rc;
+    }
+    TP("next lk queued");
+    // feature counts to the host and the binning of these features as the next
+    // frame's mask boxes, beside the next LK
+    for (int g = 0; g < G; g++) SVO_HIP(ctx, hipStreamWaitEvent(fe->st_copy, fe->ev_tail[g], 0));
+    SVO_HIP(ctx, hipMemcpyAsync(fe->h_nA, fe->nA, sizeof(int) * S, hipMemcpyDeviceToHost, fe->st_copy));
+    SVO_HIP(ctx, hipMemcpyAsync(fe->h_added, fe->added, sizeof(int) * S, hipMemcpyDeviceToHost, fe->st_copy));
+    SVO_HIP(ctx, hipEventRecord(fe->ev_counts, fe->st_copy));
+    SVO_HIP(ctx, launch_box_bin(fe_fast_batch(fe, dcur, true), S, fe->W, fe->H, sf));
+    TP("tail enqueued");
+    if (ahead) {
+        rc = fe_front_rest(fe, t + 1);
         if (rc) return rc;
         fe->front_t = t + 1;
     }
+    TP("next front queued");
     // wait for this step's tail only (the statistics, the next frame's pyramid and
     // the prefetched first half keep running into the next step)
     auto tw = clk::now();
-    for (int g = 0; g < G; g++) SVO_HIP(ctx, hipEventSynchronize(fe->ev_tail[g]));
+    SVO_HIP(ctx, hipEventSynchronize(fe->ev_counts));
     ms_wait += ms_since(tw);
     TP("synced");
     ph_collect(fe);

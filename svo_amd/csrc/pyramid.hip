@@ -89,44 +89,50 @@ __global__ __launch_bounds__(256) void pyr_down_batched_kernel(const PyrDesc* __
 // level's interior one aligned dword (4 pixels) per thread: the top and bottom
 // bands over the full padded width, then the left and right bands of the
 // interior rows (the right band starts at the dword holding column w, so it may
-// rewrite a few interior pixels with their own values). Blocks of one level
-// stride over the dwords.
-__device__ __forceinline__ void pad_level(const ImgLevel& L, int blk, int nblk) {
-    constexpr int SIDE = kPyrPad / 4 + 1;  // dwords per row on each side (right side: alignment)
-    const int w = L.w, h = L.h, dw = (w + 2 * kPyrPad + 3) / 4;
-    const int n_tb = 2 * kPyrPad * dw, n = n_tb + 2 * SIDE * h;
-    uint8_t* __restrict__ d = const_cast<uint8_t*>(L.data);
-    for (int k = blk * 256 + (int)threadIdx.x; k < n; k += nblk * 256) {
-        int x0, y;
-        if (k < n_tb) {
-            const int r = k / dw, c = k - r * dw;
-            y = r < kPyrPad ? r - kPyrPad : h + (r - kPyrPad);
-            x0 = 4 * c - kPyrPad;
-        } else {
-            const int k2 = k - n_tb, r = k2 / (2 * SIDE), c = k2 - r * (2 * SIDE);
-            y = r;
-            x0 = c < SIDE ? -kPyrPad + 4 * c : (w & ~3) + 4 * (c - SIDE);
-            if (c > 0 && c < SIDE && x0 >= 0) continue;  // left side: SIDE - 1 dwords suffice
-        }
-        const uint8_t* srow = d + (ptrdiff_t)refl101(y, h) * L.pitch;
-        unsigned v = 0;
-#pragma unroll
-        for (int i = 0; i < 4; i++) v |= (unsigned)srow[refl101(x0 + i, w)] << (8 * i);
-        *reinterpret_cast<unsigned*>(d + (ptrdiff_t)y * L.pitch + x0) = v;
-    }
+// rewrite a few interior pixels with their own values). One dword per thread
+// (the grid covers level 0's dwords; smaller levels' surplus blocks exit), so
+// the whole border costs one memory round trip.
+__device__ __forceinline__ int refl_pad(int p, int len, bool single) {
+    // levels larger than the padding reflect once (p in [-kPyrPad, len + kPyrPad))
+    if (single) return p < 0 ? -p : (p >= len ? 2 * len - 2 - p : p);
+    return refl101(p, len);
 }
-
-constexpr int PAD_BLOCKS = 8;  // blocks per (level, sequence)
+constexpr int PAD_SIDE = kPyrPad / 4 + 1;  // dwords per row and side (right side: alignment)
+__host__ __device__ constexpr int pad_dwords(int w, int h) {
+    return 2 * kPyrPad * ((w + 2 * kPyrPad + 3) / 4) + 2 * PAD_SIDE * h;
+}
+__device__ __forceinline__ void pad_level(const ImgLevel& L, int k) {
+    const int w = L.w, h = L.h, dw = (w + 2 * kPyrPad + 3) / 4;
+    const int n_tb = 2 * kPyrPad * dw;
+    if (k >= n_tb + 2 * PAD_SIDE * h) return;
+    uint8_t* __restrict__ d = const_cast<uint8_t*>(L.data);
+    int x0, y;
+    if (k < n_tb) {
+        const int r = k / dw, c = k - r * dw;
+        y = r < kPyrPad ? r - kPyrPad : h + (r - kPyrPad);
+        x0 = 4 * c - kPyrPad;
+    } else {
+        const int k2 = k - n_tb, r = k2 / (2 * PAD_SIDE), c = k2 - r * (2 * PAD_SIDE);
+        y = r;
+        x0 = c < PAD_SIDE ? -kPyrPad + 4 * c : (w & ~3) + 4 * (c - PAD_SIDE);
+        if (c < PAD_SIDE && x0 >= 0) return;  // left side: PAD_SIDE - 1 dwords suffice
+    }
+    const bool single = w > kPyrPad && h > kPyrPad;
+    const uint8_t* srow = d + (ptrdiff_t)refl_pad(y, h, single) * L.pitch;
+    unsigned v = 0;
+#pragma unroll
+    for (int i = 0; i < 4; i++) v |= (unsigned)srow[refl_pad(x0 + i, w, single)] << (8 * i);
+    *reinterpret_cast<unsigned*>(d + (ptrdiff_t)y * L.pitch + x0) = v;
+}
 
 __global__ __launch_bounds__(256) void pad_batched_kernel(const PyrDesc* __restrict__ descs) {
-    pad_level(descs[blockIdx.z].lv[blockIdx.y], blockIdx.x, gridDim.x);
+    pad_level(descs[blockIdx.z].lv[blockIdx.y], blockIdx.x * 256 + threadIdx.x);
 }
-__global__ __launch_bounds__(256) void pad_kernel(PyrDesc d) { pad_level(d.lv[blockIdx.y], blockIdx.x, gridDim.x); }
+__global__ __launch_bounds__(256) void pad_kernel(PyrDesc d) { pad_level(d.lv[blockIdx.y], blockIdx.x * 256 + threadIdx.x); }
 
 hipError_t launch_pyramid_pad(const PyrDesc* d_descs, int nseq, int w, int h, int nlevels, hipStream_t st) {
-    (void)w;
-    (void)h;
-    hipLaunchKernelGGL(pad_batched_kernel, dim3(PAD_BLOCKS, nlevels, nseq), dim3(256), 0, st, d_descs);
+    const int blocks = (pad_dwords(w, h) + 255) / 256;  // level 0 has the most
+    hipLaunchKernelGGL(pad_batched_kernel, dim3(blocks, nlevels, nseq), dim3(256), 0, st, d_descs);
     return hipGetLastError();
 }
 
@@ -150,7 +156,8 @@ hipError_t launch_pyramid(const svo_image* img, int first_level, hipStream_t st)
         hipLaunchKernelGGL(pyr_down_kernel, grid, dim3(256), 0, st, s.data, s.w, s.h, s.pitch,
                            const_cast<uint8_t*>(d.data), d.w, d.h, d.pitch);
     }
-    hipLaunchKernelGGL(pad_kernel, dim3(PAD_BLOCKS, img->nlevels), dim3(256), 0, st, img->desc);
+    hipLaunchKernelGGL(pad_kernel, dim3((pad_dwords(img->w, img->h) + 255) / 256, img->nlevels), dim3(256), 0, st,
+                       img->desc);
     return hipGetLastError();
 }
 
@@ -178,7 +185,7 @@ __global__ __launch_bounds__(256) void pyr_scharr_kernel(const PyrDesc* __restri
     const int x0 = blockIdx.x * PD_TX, y0 = blockIdx.y * PD_TY;
     const int sx0 = 2 * x0 - 2, sy0 = 2 * y0 - 2;
     const int xa = sx0 - 2;  // multiple of 4 (x0 is a multiple of 64)
-    __shared__ __attribute__((aligned(16))) uint8_t T[FS_IH][FS_IW];
+    __shared__ __attribute__((aligned(16))) uint8_t T[FS_IH][FS_IW + 8];  // rows 16-byte aligned (b128 reads)
     __shared__ int H[PD_IH][PD_TX + 1];
     const int tid = threadIdx.x;
     const int sw = s.w, sh = s.h;
@@ -197,48 +204,82 @@ __global__ __launch_bounds__(256) void pyr_scharr_kernel(const PyrDesc* __restri
         }
     }
     __syncthreads();
-    // ---- pyrDown: T column 2 + j holds level-l column sx0 + j ----
-    for (int k = tid; k < PD_IH * PD_TX; k += 256) {
-        const int r = k >> 6, c = k & 63;
-        const uint8_t* t = &T[r][2 * c + 2];
-        H[r][c] = t[0] + 4 * t[1] + 6 * t[2] + 4 * t[3] + t[4];
+    // ---- pyrDown rows: T column 2 + j holds level-l column sx0 + j; a task
+    // makes 4 outputs (c = 4q .. 4q + 3) from 4 aligned dwords of its row ----
+    for (int k = tid; k < PD_IH * (PD_TX / 4); k += 256) {
+        const int r = k >> 4, q = k & 15;
+        const uint4 v = *reinterpret_cast<const uint4*>(&T[r][8 * q]);
+        const unsigned w4[4] = {v.x, v.y, v.z, v.w};
+        int bt[16];
+#pragma unroll
+        for (int i = 0; i < 16; i++) bt[i] = (w4[i >> 2] >> (8 * (i & 3))) & 0xFF;
+#pragma unroll
+        for (int m = 0; m < 4; m++)
+            H[r][4 * q + m] = bt[2 * m + 2] + 4 * bt[2 * m + 3] + 6 * bt[2 * m + 4] + 4 * bt[2 * m + 5] + bt[2 * m + 6];
     }
-    // ---- Scharr of level l pixels (2x0 + i, 2y0 + j), i < 128, j < 32: T[2 + j][4 + i] ----
+    // ---- Scharr of level l pixels (2x0 + i, 2y0 + j), i < 128, j < 32: T[2 + j][4 + i];
+    // a task: 4 columns x 4 rows from 3 aligned dwords per staged row, one 16-byte
+    // store per row (columns >= sw are never written: the zero border stays) ----
     {
         uint32_t* __restrict__ out = ders[blockIdx.z].data[level];
         const int op = ders[blockIdx.z].pitch[level];
-        const int i = tid & 127, j0 = (tid >> 7) * 16;
-        const int x = 2 * x0 + i;
+        const int g = tid & 31, q = tid >> 5;
+        const int x = 2 * x0 + 4 * g;
+        int rows[6][6];  // staged rows 1 + 4q .. 6 + 4q, T columns 3 + 4g .. 8 + 4g
+#pragma unroll
+        for (int rr = 0; rr < 6; rr++) {
+            const uint8_t* trow = &T[1 + 4 * q + rr][0];
+            const unsigned a0 = *reinterpret_cast<const unsigned*>(trow + 4 * g);
+            const unsigned a1 = *reinterpret_cast<const unsigned*>(trow + 4 * g + 4);
+            const unsigned a2 = *reinterpret_cast<const unsigned*>(trow + 4 * g + 8);
+            rows[rr][0] = a0 >> 24;
+            rows[rr][1] = a1 & 0xFF;
+            rows[rr][2] = (a1 >> 8) & 0xFF;
+            rows[rr][3] = (a1 >> 16) & 0xFF;
+            rows[rr][4] = a1 >> 24;
+            rows[rr][5] = a2 & 0xFF;
+        }
         if (x < sw) {
-            const int tc = 4 + i;
-            int tl = T[1 + j0][tc - 1], tm = T[1 + j0][tc], tr = T[1 + j0][tc + 1];
-            int ml = T[2 + j0][tc - 1], mm = T[2 + j0][tc], mr = T[2 + j0][tc + 1];
-#pragma unroll 4
-            for (int jj = 0; jj < 16; jj++) {
-                const int y = 2 * y0 + j0 + jj;
-                const int br = T[3 + j0 + jj][tc + 1], bm = T[3 + j0 + jj][tc], bl = T[3 + j0 + jj][tc - 1];
-                if (y < sh) {
+#pragma unroll
+            for (int jj = 0; jj < 4; jj++) {
+                const int y = 2 * y0 + 4 * q + jj;
+                if (y >= sh) break;
+                unsigned o[4];
+#pragma unroll
+                for (int m = 0; m < 4; m++) {
+                    const int tl = rows[jj][m], tm = rows[jj][m + 1], tr = rows[jj][m + 2];
+                    const int ml = rows[jj + 1][m], mr = rows[jj + 1][m + 2];
+                    const int bl = rows[jj + 2][m], bm = rows[jj + 2][m + 1], br = rows[jj + 2][m + 2];
                     const int ix = (3 * (tr + br) + 10 * mr) - (3 * (tl + bl) + 10 * ml);
                     const int iy = 3 * ((br - tr) + (bl - tl)) + 10 * (bm - tm);
-                    out[(size_t)y * op + x] = ((unsigned)(iy * (1 << kDerShift)) << 16) | ((unsigned)(ix * (1 << kDerShift)) & 0xFFFFu);
+                    o[m] = ((unsigned)(iy * (1 << kDerShift)) << 16) | ((unsigned)(ix * (1 << kDerShift)) & 0xFFFFu);
                 }
-                tl = ml; tm = mm; tr = mr;
-                ml = bl; mm = bm; mr = br;
+                uint32_t* dst = out + (size_t)y * op + x;
+                if (x + 3 < sw) {
+                    *reinterpret_cast<uint4*>(dst) = make_uint4(o[0], o[1], o[2], o[3]);
+                } else {
+#pragma unroll
+                    for (int m = 0; m < 4; m++)
+                        if (x + m < sw) dst[m] = o[m];
+                }
             }
         }
     }
     __syncthreads();
+    // ---- pyrDown columns: 4 output rows per thread from 11 sliding H rows ----
     const int c = tid & 63;
     const int x = x0 + c;
     if (x >= d.w) return;
     uint8_t* __restrict__ dst = const_cast<uint8_t*>(d.data);
+    const int r0 = (tid >> 6) * (PD_TY / 4);
+    int hv[2 * (PD_TY / 4) + 3];
+#pragma unroll
+    for (int i = 0; i < 2 * (PD_TY / 4) + 3; i++) hv[i] = H[2 * r0 + i][c];
 #pragma unroll
     for (int i = 0; i < PD_TY / 4; i++) {
-        const int r = (tid >> 6) * (PD_TY / 4) + i;
-        const int y = y0 + r;
+        const int y = y0 + r0 + i;
         if (y < d.h) {
-            const int sum = H[2 * r][c] + 4 * H[2 * r + 1][c] + 6 * H[2 * r + 2][c] + 4 * H[2 * r + 3][c] +
-                            H[2 * r + 4][c];
+            const int sum = hv[2 * i] + 4 * hv[2 * i + 1] + 6 * hv[2 * i + 2] + 4 * hv[2 * i + 3] + hv[2 * i + 4];
             dst[(size_t)y * d.pitch + x] = (uint8_t)((sum + 128) >> 8);
         }
     }

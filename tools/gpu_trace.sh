@@ -1,2 +1,8 @@
+# One steady-state step's GPU timeline (kernel + copy trace) and the host trace.
 cd /tmp && export TMPDIR=/tmp; cd $GRAFT_REPO_ROOT
-timeout -k 10 300 rocprofv3 --kernel-trace --memory-copy-trace -d gpurun_out/tr_g1 -o run --output-format csv -- python bench.py --steps 4 --warmup 1 --seq 64 --no-cpu-baseline --no-single > gpurun_out/tr_g1.log 2>&1 || exit 1
+mkdir -p gpurun_out
+T=/tmp/svo_trace
+SVO_FE_TRACE=1 timeout -k 10 300 rocprofv3 --kernel-trace --memory-copy-trace -d $T -o run --output-format csv -- python bench.py --steps ${1:-12} --warmup 3 --seq 64 --no-cpu-baseline --no-single > $T.log 2>&1 || { tail -5 $T.log; exit 1; }
+python tools/timeline.py $T > gpurun_out/timeline.txt
+grep "fe t=" $T.log | tail -12 > gpurun_out/hosttrace.txt
+tail -1 $T.log | cut -c1-200 >> gpurun_out/hosttrace.txt

@@ -15,7 +15,7 @@ for r in csv.DictReader(open(f"{d}/run_kernel_trace.csv")):
 for r in csv.DictReader(open(f"{d}/run_memory_copy_trace.csv")):
     rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), "C:" + r["Direction"][:24], r.get("Queue_Id", "")))
 rows.sort()
-lk = [x for x in rows if "lk_fast" in x[2] or x[2] == "K:lk_kernel"]
+lk = [x for x in rows if x[2].startswith("K:lk_")]
 t0, tp = lk[-1][0], lk[-2][0]
 print(f"step period {(t0 - tp) / 1e3:.1f} us")
 for a, b, n, q in rows:
