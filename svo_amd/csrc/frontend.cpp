@@ -175,7 +175,9 @@ struct svo_frontend {
     float *h_xyB, *h_obj, *h_samp;   // h_xyB / h_obj: this step's parity half of h_*_b
     float *h_xyB_b[2], *h_obj_b[2];
     double *h_hyps, *h_stats;
-    uint32_t *h_bits, *h_best;
+    uint32_t *h_bits, *h_best;  // h_best: this step's parity of h_best_b (host-coherent)
+    uint32_t* h_best_b[2];
+    void* zout = nullptr;  // host-coherent: counts, sums, RANSAC subsets, inlier bits
     // host-coherent buffers the scoring kernel reads / writes directly (zero-copy:
     // no H2D of the hypotheses, no D2H of bits / counts, no count memset)
     void* zmem = nullptr;
@@ -189,6 +191,8 @@ struct svo_frontend {
     std::vector<double> pose;  // [s][6]
     bool fits_pending = false;
     bool stats_pending = false;
+    int stats_parity = 0;  // step parity whose inliers the pending statistics cover
+    hipStream_t st_stats = nullptr;  // high priority: the statistics overtake LK's blocks
     bool boxes_binned = false;  // box_bin already queued for the next step's FAST
     int pyr_ready = -1;  // frame index whose pyramid + Scharr were built ahead
     hipEvent_t ev_stats = nullptr;  // SQPnP statistics of the last step on the host
@@ -299,10 +303,8 @@ int fe_fast_and_bucket(svo_frontend* fe, const PyrDesc* descs_cur, bool use_mask
     return SVO_OK;
 }
 
-// keyframe top-up of sequences [g0, g0 + n)
-int fe_append(svo_frontend* fe, int t, int g0, int n, hipStream_t st) {
-    svo_ctx* ctx = fe->ctx;
-    int slot;
+// keyframe top-up arguments for sequences from g0 on
+AppendBatch fe_append_batch(svo_frontend* fe, int t, int g0) {
     AppendBatch ab;
     ab.n = fe->nA + g0;
     ab.xy = fe->xyA + 2 * (size_t)g0 * fe->CAP;
@@ -321,8 +323,15 @@ int fe_append(svo_frontend* fe, int t, int g0, int n, hipStream_t st) {
     ab.depth_seed = fe->seed_d + g0;
     ab.added = fe->added + g0;
     std::memcpy(ab.K, fe->cfg.K, sizeof(ab.K));
+    return ab;
+}
+
+// keyframe top-up of sequences [g0, g0 + n)
+int fe_append(svo_frontend* fe, int t, int g0, int n, hipStream_t st) {
+    svo_ctx* ctx = fe->ctx;
+    int slot;
     ph_begin(fe, PH_APPEND, st, &slot);
-    SVO_HIP(ctx, launch_append(ab, n, st));
+    SVO_HIP(ctx, launch_append(fe_append_batch(fe, t, g0), n, st));
     ph_end(fe, st, slot);
     return SVO_OK;
 }
@@ -345,14 +354,18 @@ int fe_queue_full(svo_frontend* fe) {
 
 // Queue the SQPnP sufficient statistics of the last step's RANSAC inliers (the
 // bits are on the device since that step) on the FAST stream, then their D2H.
+// (on their own stream, written straight to host-coherent memory; the inputs
+// -- inlier bits on the host, points from the post-LK kernel the host already
+// waited for -- need no device-side wait, so they are queued right behind the
+// tail kernel and run beside it, ahead of the next LK)
 int fe_queue_stats(svo_frontend* fe) {
     if (!fe->stats_pending) return SVO_OK;
     svo_ctx* ctx = fe->ctx;
-    hipStream_t sf = fe->st_fast;
-    SVO_HIP(ctx, launch_suffstats(fe->obj, fe->xyB, fe->nB, fe->CAP, fe->bits_best, fe->WORDS, fe->S, fe->cfg.K,
-                                  fe->stats, sf));
-    SVO_HIP(ctx, hipMemcpyAsync(fe->h_stats, fe->stats, sizeof(double) * 60 * fe->S, hipMemcpyDeviceToHost, sf));
-    SVO_HIP(ctx, hipEventRecord(fe->ev_stats, sf));
+    const int p = fe->stats_parity;
+    hipStream_t ss = fe->st_stats;
+    SVO_HIP(ctx, launch_suffstats(fe->obj_b[p], fe->xyB_b[p], fe->nB_b[p], fe->CAP, fe->h_best_b[p], fe->WORDS, fe->S,
+                                  fe->cfg.K, fe->h_stats, ss));
+    SVO_HIP(ctx, hipEventRecord(fe->ev_stats, ss));
     fe->stats_pending = false;
     return SVO_OK;
 }
@@ -531,11 +544,7 @@ int svo_frontend_create(svo_ctx* ctx, const svo_frontend_config* cfg, svo_fronte
     }
     {
         char* p = (char*)fe->hmem;
-        fe->h_nB = carve<int>(p, S);
-        fe->h_nA = carve<int>(p, S);
         fe->h_cnt = carve<int>(p, (size_t)S * kRansacChunk);
-        fe->h_added = carve<int>(p, S);
-        fe->h_itsum = carve<long long>(p, S);
         for (int k = 0; k < 2; k++) {
             fe->h_xyB_b[k] = carve<float>(p, 2 * (size_t)S * CAP);
             fe->h_obj_b[k] = carve<float>(p, 3 * (size_t)S * CAP);
@@ -544,10 +553,9 @@ int svo_frontend_create(svo_ctx* ctx, const svo_frontend_config* cfg, svo_fronte
         fe->h_obj = fe->h_obj_b[0];
         fe->h_hyps = carve<double>(p, 12 * (size_t)S * kRansacChunk);
         fe->h_bits = carve<uint32_t>(p, (size_t)S * kRansacChunk * fe->WORDS);
-        fe->h_best = carve<uint32_t>(p, (size_t)S * fe->WORDS);
-        fe->h_stats = carve<double>(p, 60 * (size_t)S);
-        fe->h_samp = carve<float>(p, (size_t)kSampleFloats * kRansacPrefetch * S);
-        std::memset(fe->h_nA, 0, sizeof(int) * S);
+
+
+
     }
     // zero-copy scoring buffers (coherent: the kernel's writes are visible to the
     // host once the stream is synchronised)
@@ -568,6 +576,36 @@ int svo_frontend_create(svo_ctx* ctx, const svo_frontend_config* cfg, svo_fronte
             fe->z_bits = carve<uint32_t>(p, (size_t)S * kRansacChunk * fe->WORDS);
             fe->z_wcnt = carve<int>(p, (size_t)S * kRansacChunk * fe->WS);
         }
+    }
+    // host-coherent outputs the kernels write directly (no D2H copies on the
+    // critical path): post-LK counts / iteration sums / RANSAC subsets, the tail's
+    // counts; and the inlier bits the tail and the statistics read (parity pair)
+    {
+        size_t zb = 0;
+        auto add = [&](size_t b) { zb = ((zb + 255) & ~(size_t)255) + b; };
+        add(sizeof(int) * S * 3);
+        add(sizeof(long long) * S);
+        add(sizeof(float) * kSampleFloats * kRansacPrefetch * (size_t)S);
+        add(sizeof(uint32_t) * (size_t)S * fe->WORDS);
+        add(sizeof(uint32_t) * (size_t)S * fe->WORDS);
+        add(sizeof(double) * 60 * (size_t)S);
+        add(1024);
+        if (hipHostMalloc(&fe->zout, zb, hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess) {
+            fe->zout = nullptr;
+            svo_frontend_destroy(fe);
+            return set_error(ctx, SVO_ERR_HIP, "svo_frontend_create: host-coherent alloc");
+        }
+        std::memset(fe->zout, 0, zb);
+        char* p = (char*)fe->zout;
+        fe->h_nB = carve<int>(p, S);
+        fe->h_nA = carve<int>(p, S);
+        fe->h_added = carve<int>(p, S);
+        fe->h_itsum = carve<long long>(p, S);
+        fe->h_samp = carve<float>(p, (size_t)kSampleFloats * kRansacPrefetch * S);
+        fe->h_best_b[0] = carve<uint32_t>(p, (size_t)S * fe->WORDS);
+        fe->h_best_b[1] = carve<uint32_t>(p, (size_t)S * fe->WORDS);
+        fe->h_best = fe->h_best_b[0];
+        fe->h_stats = carve<double>(p, 60 * (size_t)S);
     }
     // derivative pyramids of the last two frames of every sequence (ping-pong)
     {
@@ -619,6 +657,10 @@ int svo_frontend_create(svo_ctx* ctx, const svo_frontend_config* cfg, svo_fronte
                 svo_frontend_destroy(fe);
                 return set_error(ctx, SVO_ERR_HIP, "svo_frontend_create: stream");
             }
+        if (hipStreamCreateWithPriority(&fe->st_stats, hipStreamNonBlocking, greatest) != hipSuccess) {
+            svo_frontend_destroy(fe);
+            return set_error(ctx, SVO_ERR_HIP, "svo_frontend_create: stream");
+        }
         if (hipStreamCreateWithPriority(&fe->st_fast, hipStreamNonBlocking, least) != hipSuccess) {
             svo_frontend_destroy(fe);
             return set_error(ctx, SVO_ERR_HIP, "svo_frontend_create: stream");
@@ -654,6 +696,7 @@ void svo_frontend_destroy(svo_frontend* fe) {
     if (fe->dermem) (void)hipFree(fe->dermem);
     if (fe->hmem) (void)hipHostFree(fe->hmem);
     if (fe->zmem) (void)hipHostFree(fe->zmem);
+    if (fe->zout) (void)hipHostFree(fe->zout);
     for (auto& e : fe->ev)
         if (e) (void)hipEventDestroy(e);
     for (auto& g : fe->gst)
@@ -664,6 +707,10 @@ void svo_frontend_destroy(svo_frontend* fe) {
     if (fe->st_fast) {
         (void)hipStreamSynchronize(fe->st_fast);
         (void)hipStreamDestroy(fe->st_fast);
+    }
+    if (fe->st_stats) {
+        (void)hipStreamSynchronize(fe->st_stats);
+        (void)hipStreamDestroy(fe->st_stats);
     }
     for (auto& e : fe->ev_sync)
         if (e) (void)hipEventDestroy(e);
@@ -688,6 +735,7 @@ static int fe_drain(svo_frontend* fe) {
     if (fe->front_t < 0) return SVO_OK;
     for (auto& g : fe->gst) SVO_HIP(ctx, hipStreamSynchronize(g));
     if (fe->st_fast) SVO_HIP(ctx, hipStreamSynchronize(fe->st_fast));
+    if (fe->st_stats) SVO_HIP(ctx, hipStreamSynchronize(fe->st_stats));
     if (fe->st_copy) SVO_HIP(ctx, hipStreamSynchronize(fe->st_copy));
     SVO_HIP(ctx, hipStreamSynchronize(ctx->stream));
     fe->front_t = -1;
@@ -787,7 +835,8 @@ static int fe_front_lk(svo_frontend* fe, int t) {
     fe->xyB = fe->xyB_b[t & 1];
     fe->obj = fe->obj_b[t & 1];
     fe->nB = fe->nB_b[t & 1];
-    fe->bits_best = fe->bits_best_b[t & 1];
+    fe->h_best = fe->h_best_b[t & 1];
+    fe->bits_best = fe->h_best;  // the statistics kernel reads the host-coherent bits
     fe->h_xyB = fe->h_xyB_b[t & 1];
     fe->h_obj = fe->h_obj_b[t & 1];
     fe->ev_full = fe->ev_full_b[t & 1];
@@ -880,26 +929,19 @@ static int fe_front_rest(svo_frontend* fe, int t) {
     for (int g = 0; g < G; g++) {
         const int a = fe->g0[g], n = fe->gn[g];
         hipStream_t sg = fe->gst[g];
-        const int mp = CAP;  // grid bound (the kernels read the device counts)
-        CompactBatch cb{fe->nA + a, fe->status + (size_t)a * CAP, nullptr, 0, fe->next_xy + 2 * (size_t)a * CAP,
-                        fe->midA + (size_t)a * CAP, fe->iters + (size_t)a * CAP, fe->itsum + a,
-                        fe->xyB + 2 * (size_t)a * CAP, fe->midB + (size_t)a * CAP, fe->nB + a, CAP};
-        ph_begin(fe, PH_COMPACT, sg, &slot);
-        SVO_HIP(ctx, launch_compact(cb, n, sg));
-        ph_end(fe, sg, slot);
-        ph_begin(fe, PH_GATHER, sg, &slot);
-        SVO_HIP(ctx, launch_gather(fe->nB + a, fe->midB + (size_t)a * CAP, fe->map + 3 * (size_t)a * fe->MAPCAP, CAP,
-                                   fe->MAPCAP, fe->obj + 3 * (size_t)a * CAP, n, mp, sg));
-        ph_end(fe, sg, slot);
-        // the RANSAC subsets of the first hypotheses, gathered here: the host needs
-        // ~100 B per hypothesis instead of the whole point set
+        // keep status == 1 (R:src/tracking.cpp:169-175), gather the map points, draw
+        // and gather the first RANSAC subsets (the host needs ~100 B per hypothesis
+        // instead of the whole point set): one kernel, outputs the host reads written
+        // straight to host-coherent memory
         const size_t sfl = (size_t)kSampleFloats * kRansacPrefetch;
-        SVO_HIP(ctx, launch_ransac_samples(fe->nB + a, fe->obj + 3 * (size_t)a * CAP, fe->xyB + 2 * (size_t)a * CAP,
-                                           CAP, kRansacPrefetch, n, fe->samp + sfl * a, sg));
-        SVO_HIP(ctx, hipMemcpyAsync(fe->h_nB + a, fe->nB + a, sizeof(int) * n, hipMemcpyDeviceToHost, sg));
-        SVO_HIP(ctx, hipMemcpyAsync(fe->h_itsum + a, fe->itsum + a, sizeof(long long) * n, hipMemcpyDeviceToHost, sg));
-        SVO_HIP(ctx, hipMemcpyAsync(fe->h_samp + sfl * a, fe->samp + sfl * a, sizeof(float) * sfl * n,
-                                    hipMemcpyDeviceToHost, sg));
+        PostLkBatch pb{fe->nA + a, fe->status + (size_t)a * CAP, fe->next_xy + 2 * (size_t)a * CAP,
+                       fe->midA + (size_t)a * CAP, fe->iters + (size_t)a * CAP, fe->xyB + 2 * (size_t)a * CAP,
+                       fe->midB + (size_t)a * CAP, fe->nB + a, fe->map + 3 * (size_t)a * fe->MAPCAP, fe->MAPCAP,
+                       fe->obj + 3 * (size_t)a * CAP, CAP, kRansacPrefetch, fe->h_nB + a, fe->h_itsum + a,
+                       fe->h_samp + sfl * a};
+        ph_begin(fe, PH_COMPACT, sg, &slot);
+        SVO_HIP(ctx, launch_post_lk(pb, n, sg));
+        ph_end(fe, sg, slot);
         SVO_HIP(ctx, hipEventRecord(fe->ev_sync[3 + 2 * g], sg));
     }
     // every slice's points are gathered once the last slice's copies are queued
@@ -1112,22 +1154,19 @@ int svo_frontend_step(svo_frontend* fe, int t, svo_frontend_stats* stats) {
         }
         ms_fit += ms_since(tf);
         TP("selected");
-        SVO_HIP(ctx, hipMemcpyAsync(fe->bits_best + (size_t)a * fe->WORDS, fe->h_best + (size_t)a * fe->WORDS,
-                                    sizeof(uint32_t) * n * fe->WORDS, hipMemcpyHostToDevice, sg));
         // the SQPnP statistics only feed the pose fits, which run during the next
         // step's LK: they are queued then (fe_queue_stats), off the critical path
         fe->stats_pending = true;
+        fe->stats_parity = t & 1;
         // the mask (reads xyA) and FAST (writes kps) must be done before xyA is rewritten / kps read
         SVO_HIP(ctx, hipStreamWaitEvent(sg, ev_fast, 0));
-        CompactBatch cb2{fe->nB + a, nullptr, fe->bits_best + (size_t)a * fe->WORDS, fe->WORDS,
-                         fe->xyB + 2 * (size_t)a * CAP, fe->midB + (size_t)a * CAP, nullptr, nullptr,
-                         fe->xyA + 2 * (size_t)a * CAP, fe->midA + (size_t)a * CAP, fe->nA + a, CAP};
-        TP("bits queued");
-        ph_begin(fe, PH_COMPACT, sg, &slot);
-        SVO_HIP(ctx, launch_compact(cb2, n, sg));
+        // drop the outliers (R:src/tracking.cpp:218-229; the kernel reads the inlier
+        // bits from host-coherent memory) and top up to n_features, one kernel
+        TailBatch tb{fe->nB + a, fe->h_best + (size_t)a * fe->WORDS, fe->WORDS, fe->xyB + 2 * (size_t)a * CAP,
+                     fe->midB + (size_t)a * CAP, fe->h_nA + a, fe->h_added + a};
+        ph_begin(fe, PH_APPEND, sg, &slot);
+        SVO_HIP(ctx, launch_tail(tb, fe_append_batch(fe, t, a), n, sg));
         ph_end(fe, sg, slot);
-        rc = fe_append(fe, t, a, n, sg);
-        if (rc) return rc;
         SVO_HIP(ctx, hipEventRecord(fe->ev_tail[g], sg));
         TP("compact+append queued");
     }
@@ -1138,9 +1177,6 @@ int svo_frontend_step(svo_frontend* fe, int t, svo_frontend_stats* stats) {
     // kernel queued beside LK would wait for it: LK leaves no registers free, and
     // the pose fits need them at the next step's start).
     for (int g = 0; g < G; g++) SVO_HIP(ctx, hipStreamWaitEvent(sf, fe->ev_tail[g], 0));
-    rc = fe_queue_stats(fe);
-    if (rc) return rc;
-    TP("stats queued");
     // this step's counts, before the next step's first half re-fills the mirrors
     int64_t lk_its = 0, tracked = 0;
     for (int s = 0; s < S; s++) {
@@ -1155,17 +1191,14 @@ int svo_frontend_step(svo_frontend* fe, int t, svo_frontend_stats* stats) {
     }();
     const bool ahead = prefetch && t + 1 < fe->T;
     fe->boxes_binned = true;  // queued just below, behind the next LK
+    rc = fe_queue_stats(fe);
+    if (rc) return rc;
     if (ahead) {
         rc = fe_front_lk(fe, t + 1);
         if (rc) return rc;
     }
     TP("next lk queued");
-    // feature counts to the host and the binning of these features as the next
-    // frame's mask boxes, beside the next LK
-    for (int g = 0; g < G; g++) SVO_HIP(ctx, hipStreamWaitEvent(fe->st_copy, fe->ev_tail[g], 0));
-    SVO_HIP(ctx, hipMemcpyAsync(fe->h_nA, fe->nA, sizeof(int) * S, hipMemcpyDeviceToHost, fe->st_copy));
-    SVO_HIP(ctx, hipMemcpyAsync(fe->h_added, fe->added, sizeof(int) * S, hipMemcpyDeviceToHost, fe->st_copy));
-    SVO_HIP(ctx, hipEventRecord(fe->ev_counts, fe->st_copy));
+    // the binning of these features as the next frame's mask boxes, beside the next LK
     SVO_HIP(ctx, launch_box_bin(fe_fast_batch(fe, dcur, true), S, fe->W, fe->H, sf));
     TP("tail enqueued");
     if (ahead) {
@@ -1177,7 +1210,7 @@ int svo_frontend_step(svo_frontend* fe, int t, svo_frontend_stats* stats) {
     // wait for this step's tail only (the statistics, the next frame's pyramid and
     // the prefetched first half keep running into the next step)
     auto tw = clk::now();
-    SVO_HIP(ctx, hipEventSynchronize(fe->ev_counts));
+    for (int g = 0; g < G; g++) SVO_HIP(ctx, hipEventSynchronize(fe->ev_tail[g]));
     ms_wait += ms_since(tw);
     TP("synced");
     ph_collect(fe);
@@ -1208,6 +1241,7 @@ int svo_frontend_synchronize(svo_frontend* fe) {
     if (rq) return rq;
     for (auto& g : fe->gst) SVO_HIP(ctx, hipStreamSynchronize(g));
     if (fe->st_fast) SVO_HIP(ctx, hipStreamSynchronize(fe->st_fast));
+    if (fe->st_stats) SVO_HIP(ctx, hipStreamSynchronize(fe->st_stats));
     SVO_HIP(ctx, hipStreamSynchronize(ctx->stream));
     fe_finish_fits(fe);
     return SVO_OK;

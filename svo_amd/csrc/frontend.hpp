@@ -29,6 +29,45 @@ hipError_t launch_gather(const int* n, const int* mid, const double* map, int ca
 hipError_t launch_ransac_samples(const int* counts, const float* obj, const float* img, int cap, int nh, int nseq,
                                  float* samp, hipStream_t st);
 
+// Everything between temporal LK and the host's RANSAC, one 1024-thread block
+// per sequence: stable compaction of the tracked features (status == 1) into
+// xy_out / mid_out / n_out, the LK iteration sum, the map-point gather into obj
+// (float, as solvePnPRansac converts), and the 5-point subsets of the first nh
+// RANSAC hypotheses (cv::RNG(-1) draws over the new count) gathered as
+// obj[5][3] + img[5][2] floats. h_n / h_iters / h_samp are host-coherent
+// (zero-copy): the host reads them once the kernel is done.
+struct PostLkBatch {
+    const int* n_in;
+    const uint8_t* status;
+    const float* xy_in;
+    const int* mid_in;
+    const int* iters;
+    float* xy_out;
+    int* mid_out;
+    int* n_out;
+    const double* map;
+    int map_cap;
+    float* obj;
+    int cap, nh;
+    int* h_n;
+    long long* h_iters;
+    float* h_samp;  // [s][nh][25]
+};
+hipError_t launch_post_lk(const PostLkBatch& b, int nseq, hipStream_t st);
+
+// The step's tail, one block per sequence: stable compaction by the RANSAC
+// inlier bits (read from host-coherent memory), then the keyframe top-up
+// (append_kernel's body). h_n / h_added: host-coherent copies of the counts.
+struct TailBatch {
+    const int* n_in;
+    const uint32_t* bits;  // [s][words_cap], host-coherent
+    int words_cap;
+    const float* xy_in;
+    const int* mid_in;
+    int* h_n;
+    int* h_added;
+};
+
 struct AppendBatch {
     int* n;             // features per sequence (in/out)
     float* xy;          // [s][cap] xy
@@ -46,5 +85,7 @@ struct AppendBatch {
     double K[9];
 };
 hipError_t launch_append(const AppendBatch& b, int nseq, hipStream_t st);
+// compaction (TailBatch: into ab.xy / ab.mid / ab.n) + top-up (AppendBatch)
+hipError_t launch_tail(const TailBatch& tb, const AppendBatch& ab, int nseq, hipStream_t st);
 
 }  // namespace svo
