@@ -44,7 +44,8 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 
 
 def lib_path() -> str:
-    return os.path.join(_HERE, "lib", "libsvo_gpu.so")
+    # SVO_GPU_LIB: another build of the same library (A/B measurements)
+    return os.environ.get("SVO_GPU_LIB") or os.path.join(_HERE, "lib", "libsvo_gpu.so")
 
 
 class SvoError(RuntimeError):

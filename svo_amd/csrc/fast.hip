@@ -18,6 +18,8 @@
 // keep count; (3) per-row stable write at the row's exclusive offset.
 #include "common.hpp"
 
+#include <cstdlib>
+
 namespace svo {
 
 namespace {
@@ -383,6 +385,212 @@ __global__ __launch_bounds__(256) void fast_detect_kernel(FastDetBatch B, int th
     }
 }
 
+// ---- fused detection, wave-private form: each wave owns every 4th row of the
+// tile's score region (34 x 66: the 64 x 32 tile and a 1-pixel halo, whose
+// scores NMS needs) and runs, with no block barrier, (A0) the compass pre-test
+// of its rows -> a wave-private queue (ballot ranks, no atomics), (A1) the full
+// segment test of the queue, compacted in place to the corners, (B) their
+// cornerScore with packed 16-bit min/max (the a-chain in the low halves, the
+// negated b-chain in the high ones). One barrier, then NMS / box mask / output
+// exactly as fast_detect_kernel (same output arrays). ----
+typedef short fs16x2 __attribute__((ext_vector_type(2)));
+constexpr int FW_Q = 9 * FD_SW + 8;  // queue entries per wave (<= 9 rows x 66 positions)
+
+__device__ __forceinline__ fs16x2 as_s2(unsigned v) { return __builtin_bit_cast(fs16x2, v); }
+__device__ __forceinline__ unsigned as_u(fs16x2 v) { return __builtin_bit_cast(unsigned, v); }
+
+// cornerScore<16> (fast_score.cpp) with both chains in one packed pass: low half
+// a0 = max_k max(min(a_k, d[k]), min(a_k, d[k+9])) from threshold, high half the
+// same on e = -d from -inf (= -B of the b-chain); b0 = min(-a0, B), score = -b0 - 1
+__device__ __forceinline__ int corner_score16_pk(int v, const int* ring, int threshold) {
+    fs16x2 D[25];
+    const fs16x2 sgn = {(short)-1, (short)1};
+    const fs16x2 base = {(short)v, (short)-v};
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+        const fs16x2 r2 = {(short)ring[k], (short)ring[k]};
+        D[k] = r2 * sgn + base;  // (v - r, r - v)
+    }
+#pragma unroll
+    for (int k = 16; k < 25; k++) D[k] = D[k - 16];
+    fs16x2 acc = {(short)threshold, (short)-32768};
+#pragma unroll
+    for (int k = 0; k < 16; k += 2) {
+        fs16x2 a = __builtin_elementwise_min(D[k + 1], D[k + 2]);
+#pragma unroll
+        for (int j = 3; j <= 8; j++) a = __builtin_elementwise_min(a, D[k + j]);
+        acc = __builtin_elementwise_max(acc, __builtin_elementwise_min(a, D[k]));
+        acc = __builtin_elementwise_max(acc, __builtin_elementwise_min(a, D[k + 9]));
+    }
+    const int a0 = acc.x, nb = acc.y;  // nb = -B
+    return (max(a0, nb) - 1) & 0xFF;   // -min(-a0, B) - 1, (uchar) as FAST_t
+}
+
+__global__ __launch_bounds__(256) void fast_detect_w_kernel(FastDetBatch B, int threshold, int nonmax) {
+    const ImgLevel L = B.descs[blockIdx.z].lv[0];
+    const int w = L.w, h = L.h;
+    const int x0 = blockIdx.x * FD_TX, y0 = blockIdx.y * FD_TY;
+    const size_t seq = blockIdx.z;
+    __shared__ __attribute__((aligned(16))) uint8_t T[FD_IH][FD_IW];
+    __shared__ uint16_t SC[FD_SH][FD_SW + 2];  // bit 8: corner, low byte: score
+    __shared__ uint16_t CQ[4][FW_Q];
+    __shared__ unsigned long long TM[FD_TY];
+    __shared__ unsigned long long RB[FD_TY];
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const bool inside = x0 >= 4 && y0 >= 4 && x0 - 4 + FD_IW <= w && y0 - 4 + FD_IH <= h;
+    if (inside) {
+        for (int k = tid; k < FD_IH * (FD_IW / 4); k += 256) {
+            const int r = k / (FD_IW / 4), c4 = k - r * (FD_IW / 4);
+            const uint8_t* src = L.data + (size_t)(y0 - 4 + r) * L.pitch + (x0 - 4 + 4 * c4);
+            *reinterpret_cast<uint32_t*>(&T[r][4 * c4]) = *reinterpret_cast<const uint32_t*>(src);
+        }
+    } else {
+        for (int k = tid; k < FD_IH * FD_IW; k += 256) {
+            const int r = k / FD_IW, c = k - r * FD_IW;
+            const int y = y0 - 4 + r, x = x0 - 4 + c;
+            T[r][c] = ((unsigned)y < (unsigned)h && (unsigned)x < (unsigned)w) ? L.data[(size_t)y * L.pitch + x] : 0;
+        }
+    }
+    const bool boxes = B.box_pts != nullptr;
+    if (boxes && tid < FD_TY) TM[tid] = ~0ull;
+    __syncthreads();
+    const int hi_t = threshold, lo_t = -threshold;
+    // ---- A0: compass pre-test of this wave's rows sr = wv, wv + 4, ... (lane -> column
+    // sc = lane + 1), then the two halo columns of those rows; queue (sr << 7 | sc) ----
+    uint16_t* q = CQ[wv];
+    int nq = 0;
+    auto pretest = [&](int sr, int sc, bool ok) {
+        const int y = y0 - 1 + sr, x = x0 - 1 + sc;
+        bool cand = false;
+        if (ok && x >= 3 && x < w - 3 && y >= 3 && y < h - 3) {
+            const int ty = sr + 3, tx = sc + 3;
+            const int v = T[ty][tx], hi = v + hi_t, lo = v + lo_t;
+            const int p0 = T[ty + 3][tx], p8 = T[ty - 3][tx], p4 = T[ty][tx + 3], p12 = T[ty][tx - 3];
+            const bool bright = (p0 > hi || p8 > hi) && (p4 > hi || p12 > hi);
+            const bool dark = (p0 < lo || p8 < lo) && (p4 < lo || p12 < lo);
+            cand = bright || dark;
+        }
+        const unsigned long long bal = __ballot(cand);
+        if (cand) q[nq + __popcll(bal & ((1ull << lane) - 1ull))] = (uint16_t)((sr << 7) | sc);
+        nq += __popcll(bal);
+    };
+    for (int sr = wv; sr < FD_SH; sr += 4) {
+        SC[sr][lane + 1] = 0;
+        if (lane < 2) SC[sr][lane * 65] = 0;
+        pretest(sr, lane + 1, true);
+    }
+    {
+        // halo columns 0 and 65 of the wave's rows (<= 9 rows -> 18 positions)
+        const int nr = (FD_SH - wv + 3) / 4;
+        const int sr = wv + 4 * (lane >> 1), sc = (lane & 1) * 65;
+        pretest(sr, sc, lane < 2 * nr);
+    }
+    // ---- A1: full segment test of the queue, compacted in place to the corners ----
+    int nc = 0;
+    for (int base = 0; base < nq; base += 64) {
+        const int i = base + lane;
+        bool corner = false;
+        int k = 0;
+        if (i < nq) {
+            k = q[i];
+            const int sr = k >> 7, sc = k & 127;
+            const int ty = sr + 3, tx = sc + 3;
+            const int v = T[ty][tx];
+            // packed compare: low half r - (v + t + 1) (sign: not brighter), high half
+            // r - (v - t) (sign: darker); sign bits gathered to bit q and 16 + q
+            const fs16x2 th = {(short)(v + threshold + 1), (short)(v - threshold)};
+            unsigned acc = 0;
+#pragma unroll
+            for (int qq = 0; qq < 16; qq++) {
+                const int rv = T[ty + c_ring[qq][1]][tx + c_ring[qq][0]];
+                const fs16x2 r2 = {(short)rv, (short)rv};
+                const unsigned sg = as_u(r2 - th);
+                acc |= (sg >> (15 - qq)) & (0x00010001u << qq);
+            }
+            corner = run9(~acc & 0xFFFFu) || run9(acc >> 16);
+        }
+        const unsigned long long bal = __ballot(corner);
+        if (corner) {
+            const int sr = k >> 7, sc = k & 127;
+            SC[sr][sc] = 0x100;
+            q[nc + __popcll(bal & ((1ull << lane) - 1ull))] = (uint16_t)k;  // index <= i: already read
+        }
+        nc += __popcll(bal);
+    }
+    // ---- B: cornerScore of the corners (NMS only) ----
+    if (nonmax) {
+        for (int i = lane; i < nc; i += 64) {
+            const int k = q[i];
+            const int sr = k >> 7, sc = k & 127;
+            const int ty = sr + 3, tx = sc + 3;
+            const int v = T[ty][tx];
+            int ring[16];
+#pragma unroll
+            for (int qq = 0; qq < 16; qq++) ring[qq] = T[ty + c_ring[qq][1]][tx + c_ring[qq][0]];
+            SC[sr][sc] = (uint16_t)(0x100 | corner_score16_pk(v, ring, threshold));
+        }
+    }
+    // tile mask from the previous frame's feature boxes (as fast_detect_kernel)
+    if (boxes) {
+        const int nb = (h + 15) / 16, ncl = (w + 63) / 64;
+        const int* __restrict__ cells = B.box_band + seq * (size_t)(nb * ncl + 1);
+        const int b0 = max(0, (int)floorf((y0 - B.box_half - 1.f) / 16.f));
+        const int b1 = min(nb - 1, (int)floorf((y0 + FD_TY + B.box_half + 1.f) / 16.f));
+        const int cb0 = max(0, (int)floorf((x0 - B.box_half - 1.f) / 64.f));
+        const int cb1 = min(ncl - 1, (int)floorf((x0 + FD_TX + B.box_half + 1.f) / 64.f));
+        const float* __restrict__ pts = B.box_binned + 2 * seq * (size_t)B.box_stride;
+        for (int bq = b0; bq <= b1; bq++)
+            for (int i = cells[bq * ncl + cb0] + tid, i1 = cells[bq * ncl + cb1 + 1]; i < i1; i += 256) {
+                const float px = pts[2 * i], py = pts[2 * i + 1];
+                const int xa = (int)__builtin_rintf(px - B.box_half), ya = (int)__builtin_rintf(py - B.box_half);
+                const int xb = (int)__builtin_rintf(px + B.box_half), yb = (int)__builtin_rintf(py + B.box_half);
+                int xl = min(xa, xb), xr = max(xa, xb), yt = min(ya, yb), yd = max(ya, yb);
+                xl = max(xl, max(0, x0));
+                xr = min(xr, min(w - 1, x0 + FD_TX - 1));
+                yt = max(yt, max(0, y0));
+                yd = min(yd, min(h - 1, y0 + FD_TY - 1));
+                if (xl > xr || yt > yd) continue;
+                const int c0 = xl - x0, c1 = xr - x0;  // 0..63
+                const unsigned long long span =
+                    (c1 - c0 == 63) ? ~0ull : (((1ull << (c1 - c0 + 1)) - 1ull) << c0);
+                for (int y = yt; y <= yd; y++) atomicAnd(&TM[y - y0], ~span);
+            }
+    }
+    __syncthreads();
+    const int x = x0 + lane;
+    const uint8_t* __restrict__ mask = B.mask ? B.mask + seq * B.npx : nullptr;
+#pragma unroll
+    for (int i = 0; i < FD_TY / 4; i++) {
+        const int r = wv * (FD_TY / 4) + i;
+        const int y = y0 + r;
+        const int c = lane + 1, rr = r + 1;
+        const unsigned v = SC[rr][c];
+        bool keep = (v & 0x100) != 0 && x < w && y < h;
+        if (nonmax) {
+            auto sb = [&](int y2, int x2) { return (int)reinterpret_cast<const uint8_t*>(&SC[y2][x2])[0]; };
+            int m = max(max(sb(rr, c - 1), sb(rr, c + 1)), sb(rr - 1, c - 1));
+            m = max(max(m, sb(rr - 1, c)), sb(rr - 1, c + 1));
+            m = max(max(m, sb(rr + 1, c - 1)), sb(rr + 1, c));
+            m = max(m, sb(rr + 1, c + 1));
+            keep = keep && (int)(v & 0xFF) > m;
+        }
+        if (mask) {
+            const int yy = y < h ? y : h - 1, xx = x < w ? x : w - 1;
+            keep = keep && mask[(size_t)yy * w + xx] != 0;
+        }
+        if (boxes) keep = keep && ((TM[r] >> lane) & 1ull);
+        const unsigned long long bal = __ballot(keep);
+        if (lane == 0) RB[r] = bal;
+    }
+    __syncthreads();
+    if (tid < FD_TY && y0 + tid < h) {
+        const unsigned long long bal = RB[tid];
+        const size_t row = seq * h + y0 + tid;
+        B.bits[row * B.nseg + blockIdx.x] = bal;
+        if (bal) atomicAdd(&B.rowcnt[row], __popcll(bal));
+    }
+}
+
 // Box centres of one sequence binned by cell (16-row band x 64-column tile):
 // counting sort, one block per sequence; order within a cell is irrelevant
 // (the mask is an AND of boxes).
@@ -556,7 +764,14 @@ hipError_t launch_fast_detect(const FastDetBatch& b, int nseq, int w, int h, int
         if (e != hipSuccess) return e;
     }
     dim3 grid((w + FD_TX - 1) / FD_TX, (h + FD_TY - 1) / FD_TY, nseq);
-    hipLaunchKernelGGL(fast_detect_kernel, grid, dim3(256), 0, st, b, threshold, nonmax);
+    static const int ver = [] {
+        const char* e = std::getenv("SVO_FAST_V");
+        return e ? std::atoi(e) : 2;
+    }();
+    if (ver == 1)
+        hipLaunchKernelGGL(fast_detect_kernel, grid, dim3(256), 0, st, b, threshold, nonmax);
+    else
+        hipLaunchKernelGGL(fast_detect_w_kernel, grid, dim3(256), 0, st, b, threshold, nonmax);
     hipLaunchKernelGGL(fast_scan_kernel, dim3(nseq), dim3(1024), 0, st, b, h);
     hipLaunchKernelGGL(fast_emit_kernel, dim3(h, nseq), dim3(64), 0, st, b, threshold, nonmax);
     return hipGetLastError();

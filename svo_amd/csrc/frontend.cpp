@@ -192,7 +192,6 @@ struct svo_frontend {
     bool fits_pending = false;
     bool stats_pending = false;
     int stats_parity = 0;  // step parity whose inliers the pending statistics cover
-    hipStream_t st_stats = nullptr;  // high priority: the statistics overtake LK's blocks
     bool boxes_binned = false;  // box_bin already queued for the next step's FAST
     int pyr_ready = -1;  // frame index whose pyramid + Scharr were built ahead
     hipEvent_t ev_stats = nullptr;  // SQPnP statistics of the last step on the host
@@ -354,7 +353,10 @@ int fe_queue_full(svo_frontend* fe) {
 
 // Queue the SQPnP sufficient statistics of the last step's RANSAC inliers (the
 // bits are on the device since that step) on the FAST stream, then their D2H.
-// (on their own stream, written straight to host-coherent memory; the inputs
+// (on the copy stream -- the box has 4 hardware queues (GPU_MAX_HW_QUEUES), so
+// the step keeps to 4 streams: ctx->stream (pyramids), the slice stream (LK,
+// post-LK, scoring, tail), the FAST stream and the copy stream; written straight
+// to host-coherent memory; the inputs
 // -- inlier bits on the host, points from the post-LK kernel the host already
 // waited for -- need no device-side wait, so they are queued right behind the
 // tail kernel and run beside it, ahead of the next LK)
@@ -362,7 +364,7 @@ int fe_queue_stats(svo_frontend* fe) {
     if (!fe->stats_pending) return SVO_OK;
     svo_ctx* ctx = fe->ctx;
     const int p = fe->stats_parity;
-    hipStream_t ss = fe->st_stats;
+    hipStream_t ss = fe->st_copy;
     SVO_HIP(ctx, launch_suffstats(fe->obj_b[p], fe->xyB_b[p], fe->nB_b[p], fe->CAP, fe->h_best_b[p], fe->WORDS, fe->S,
                                   fe->cfg.K, fe->h_stats, ss));
     SVO_HIP(ctx, hipEventRecord(fe->ev_stats, ss));
@@ -657,10 +659,6 @@ int svo_frontend_create(svo_ctx* ctx, const svo_frontend_config* cfg, svo_fronte
                 svo_frontend_destroy(fe);
                 return set_error(ctx, SVO_ERR_HIP, "svo_frontend_create: stream");
             }
-        if (hipStreamCreateWithPriority(&fe->st_stats, hipStreamNonBlocking, greatest) != hipSuccess) {
-            svo_frontend_destroy(fe);
-            return set_error(ctx, SVO_ERR_HIP, "svo_frontend_create: stream");
-        }
         if (hipStreamCreateWithPriority(&fe->st_fast, hipStreamNonBlocking, least) != hipSuccess) {
             svo_frontend_destroy(fe);
             return set_error(ctx, SVO_ERR_HIP, "svo_frontend_create: stream");
@@ -708,10 +706,6 @@ void svo_frontend_destroy(svo_frontend* fe) {
         (void)hipStreamSynchronize(fe->st_fast);
         (void)hipStreamDestroy(fe->st_fast);
     }
-    if (fe->st_stats) {
-        (void)hipStreamSynchronize(fe->st_stats);
-        (void)hipStreamDestroy(fe->st_stats);
-    }
     for (auto& e : fe->ev_sync)
         if (e) (void)hipEventDestroy(e);
     if (fe->ev_stats) (void)hipEventDestroy(fe->ev_stats);
@@ -735,7 +729,6 @@ static int fe_drain(svo_frontend* fe) {
     if (fe->front_t < 0) return SVO_OK;
     for (auto& g : fe->gst) SVO_HIP(ctx, hipStreamSynchronize(g));
     if (fe->st_fast) SVO_HIP(ctx, hipStreamSynchronize(fe->st_fast));
-    if (fe->st_stats) SVO_HIP(ctx, hipStreamSynchronize(fe->st_stats));
     if (fe->st_copy) SVO_HIP(ctx, hipStreamSynchronize(fe->st_copy));
     SVO_HIP(ctx, hipStreamSynchronize(ctx->stream));
     fe->front_t = -1;
@@ -854,13 +847,14 @@ static int fe_front_lk(svo_frontend* fe, int t) {
     }
     // 1. pyramid of frame t and its Scharr derivative pyramid (used when frame
     //    t is the prev image of the next step; OpenCV recomputes it per call)
+    //    (built ahead by the previous step's fe_front_rest, which recorded ev_pyr)
     if (fe->pyr_ready != t) {
         ph_begin(fe, PH_PYR, st0, &slot);
         SVO_HIP(ctx, launch_pyramid_scharr_batched(dcur, fe->d_der + (size_t)(t & 1) * S, S, fe->W, fe->H, fe->nlev,
                                                    st0));
         ph_end(fe, st0, slot);
+        SVO_HIP(ctx, hipEventRecord(ev_pyr, st0));
     }
-    SVO_HIP(ctx, hipEventRecord(ev_pyr, st0));
 
     // 3. per slice: temporal LK (trackFrames), keep status == 1, gather map
     //    points, D2H. Slice g's LK starts after slice g-1's so that slice 0's
@@ -914,7 +908,9 @@ static int fe_front_rest(svo_frontend* fe, int t) {
     int slot;
     // 3b'. build frame t+1's pyramid + Scharr ahead, once every LK of this step is
     //      done (the Scharr ping-pong buffer it writes is the one LK reads): it
-    //      runs while the host solves RANSAC. Used if the next step is t+1.
+    //      runs beside FAST while the host solves RANSAC (measured: serialising it
+    //      behind the post-LK kernel on the slice stream is slower). Used if the
+    //      next step is t+1; ev_pyr records its end.
     fe->pyr_ready = -1;
     {
         const int tn = t + 1;
@@ -924,6 +920,7 @@ static int fe_front_rest(svo_frontend* fe, int t) {
         SVO_HIP(ctx, launch_pyramid_scharr_batched(dnext, fe->d_der + (size_t)(tn & 1) * S, S, fe->W, fe->H,
                                                    fe->nlev, st0));
         ph_end(fe, st0, slot);
+        SVO_HIP(ctx, hipEventRecord(fe->ev_sync[0], st0));
         fe->pyr_ready = tn;
     }
     for (int g = 0; g < G; g++) {
@@ -947,6 +944,7 @@ static int fe_front_rest(svo_frontend* fe, int t) {
     // every slice's points are gathered once the last slice's copies are queued
     // (slices run in order on their streams; the full copy waits for the last)
     SVO_HIP(ctx, hipEventRecord(fe->ev_gathered, fe->gst[G - 1]));
+
     // the full point set for the final fits / long RANSAC runs, on the copy
     // stream behind the subsets' D2H (parity buffers: the previous step's fits
     // still read theirs)
@@ -1021,6 +1019,7 @@ int svo_frontend_step(svo_frontend* fe, int t, svo_frontend_stats* stats) {
     for (int g = 0; g < G; g++) {
         const int a = fe->g0[g], n = fe->gn[g];
         hipStream_t sg = fe->gst[g];
+        hipStream_t sq = sg;  // the slice stream is idle while the host solves RANSAC
         TP("ransac begin");
         auto tw = clk::now();
         SVO_HIP(ctx, hipEventSynchronize(fe->ev_sync[3 + 2 * g]));
@@ -1094,22 +1093,22 @@ int svo_frontend_step(svo_frontend* fe, int t, svo_frontend_stats* stats) {
             } else {
                 SVO_HIP(ctx, hipMemcpyAsync(fe->hyps + 12 * (size_t)a * kRansacChunk,
                                             fe->h_hyps + 12 * (size_t)a * kRansacChunk,
-                                            sizeof(double) * 12 * n * kRansacChunk, hipMemcpyHostToDevice, sg));
+                                            sizeof(double) * 12 * n * kRansacChunk, hipMemcpyHostToDevice, sq));
             }
-            ph_begin(fe, PH_PNP, sg, &slot);
-            SVO_HIP(ctx, launch_pnp_residuals(pb, n, max_b, c.K[0], c.K[4], c.K[2], c.K[5], thr, sg));
-            ph_end(fe, sg, slot);
+            ph_begin(fe, PH_PNP, sq, &slot);
+            SVO_HIP(ctx, launch_pnp_residuals(pb, n, max_b, c.K[0], c.K[4], c.K[2], c.K[5], thr, sq));
+            ph_end(fe, sq, slot);
             if (!zc) {
                 SVO_HIP(ctx, hipMemcpyAsync(fe->h_cnt + (size_t)a * kRansacChunk, fe->cnt + (size_t)a * kRansacChunk,
-                                            sizeof(int) * n * kRansacChunk, hipMemcpyDeviceToHost, sg));
+                                            sizeof(int) * n * kRansacChunk, hipMemcpyDeviceToHost, sq));
                 const size_t rowb = sizeof(uint32_t) * (size_t)kRansacChunk * fe->WORDS;
                 SVO_HIP(ctx, hipMemcpy2DAsync(fe->h_bits + (size_t)a * kRansacChunk * fe->WORDS, rowb,
                                               fe->bits_all + (size_t)a * kRansacChunk * fe->WORDS, rowb,
                                               sizeof(uint32_t) * (size_t)mmax * fe->WORDS, n, hipMemcpyDeviceToHost,
-                                              sg));
+                                              sq));
             }
             TP("scoring enqueued");
-            SVO_HIP(ctx, hipStreamSynchronize(sg));
+            SVO_HIP(ctx, hipStreamSynchronize(sq));
             ms_wait += ms_since(tw);
             TP("scores on host");
             // consume is a few compares per hypothesis: cheaper here than a pool dispatch
@@ -1241,7 +1240,6 @@ int svo_frontend_synchronize(svo_frontend* fe) {
     if (rq) return rq;
     for (auto& g : fe->gst) SVO_HIP(ctx, hipStreamSynchronize(g));
     if (fe->st_fast) SVO_HIP(ctx, hipStreamSynchronize(fe->st_fast));
-    if (fe->st_stats) SVO_HIP(ctx, hipStreamSynchronize(fe->st_stats));
     SVO_HIP(ctx, hipStreamSynchronize(ctx->stream));
     fe_finish_fits(fe);
     return SVO_OK;
