@@ -408,6 +408,17 @@ constexpr int ru4(int v) { return (v + 3) & ~3; }
 typedef uint32_t u32x2a4 __attribute__((ext_vector_type(2), aligned(4)));
 typedef uint16_t u16a1 __attribute__((aligned(1)));
 typedef const __attribute__((address_space(1))) u16a1* gu16u;  // unaligned 2-byte global loads
+
+// Global loads at a wave-uniform base plus an unsigned 32-bit byte offset: the
+// saddr + voffset form (no 64-bit address arithmetic per lane). Padded levels:
+// the base is the padded origin, so every offset inside the padding is >= 0.
+template <typename T>
+__device__ __forceinline__ T ldg_off(gu8 base, unsigned off) {
+    return *(const __attribute__((address_space(1))) T*)(base + off);
+}
+__device__ __forceinline__ gu8 pad_origin(const uint8_t* data, int pitch, int pad_px, int elem) {
+    return (gu8)data - (size_t)pad_px * ((size_t)pitch + 1) * elem;
+}
 typedef const __attribute__((address_space(4))) PyrDesc* cpyr;  // scalar (s_load) descriptor reads
 
 template <int WW, int WH>
@@ -1042,7 +1053,8 @@ __device__ __forceinline__ void stage_padded(unsigned* dst, unsigned* sink, cons
                                              int lane) {
     constexpr int LPR = W / 4 + 1, RPP = 64 / LPR, NP = (H + RPP - 1) / RPP;
     const int lr = lane / LPR, d = lane - lr * LPR;
-    gu8 src = (gu8)L.data + xa + 4 * d;
+    const gu8 base = pad_origin(L.data, L.pitch, kPyrPad, 1);
+    const unsigned o0 = (unsigned)(xa + kPyrPad + 4 * d) + (unsigned)(y0 + kPyrPad) * (unsigned)L.pitch;
     const bool wr = d < W / 4 && lr < RPP;
     unsigned* dpl = wr ? dst + 4 * d : sink;
     const int dstride = wr ? W : 0;
@@ -1051,7 +1063,7 @@ __device__ __forceinline__ void stage_padded(unsigned* dst, unsigned* sink, cons
     for (int q = 0; q < NP; q++) {
         int r = q * RPP + lr;
         r = r < H ? r : H - 1;
-        v[q] = *(gu32)(src + (ptrdiff_t)(y0 + r) * L.pitch);
+        v[q] = ldg_off<unsigned>(base, o0 + (unsigned)r * (unsigned)L.pitch);
     }
 #pragma unroll
     for (int q = 0; q < NP; q++) {
@@ -1484,18 +1496,20 @@ __global__ __launch_bounds__(64, MINW) void lk_multi_kernel(LKBatch B, LKDev p) 
                 ys[f] = ok ? y0 : 0;
             }
             unsigned sv[FPW][SL::NPS];
+            const gu8 jbase = pad_origin(J.data, J.pitch, kPyrPad, 1);
 #pragma unroll
             for (int f = 0; f < FPW; f++) {
-                gu8 src = (gu8)J.data + xs[f] + 4 * d;
+                const unsigned o0 = (unsigned)(xs[f] + kPyrPad + 4 * d) + (unsigned)(ys[f] + kPyrPad) * (unsigned)J.pitch;
 #pragma unroll
                 for (int q = 0; q < SL::NPS; q++) {
                     int r = q * SL::RPP + lr;
                     r = r < JRH ? r : JRH - 1;
-                    sv[f][q] = *(gu32)(src + (ptrdiff_t)(ys[f] + r) * J.pitch);
+                    sv[f][q] = ldg_off<unsigned>(jbase, o0 + (unsigned)r * (unsigned)J.pitch);
                 }
             }
             const int dpitch = dprev.pitch[level];
-            gu32 dsrc = (gu32)dprev.data[level];
+            const gu8 ibase = pad_origin(I.data, I.pitch, kPyrPad, 1);
+            const gu8 dbase = pad_origin((const uint8_t*)dprev.data[level], dpitch, kDerPad, 4);
             const int sx = inb ? ipx : 0, sy = inb ? ipy : 0;
             // strips KKS at a time: loads of a group in flight together
 #pragma unroll
@@ -1506,13 +1520,13 @@ __global__ __launch_bounds__(64, MINW) void lk_multi_kernel(LKBatch B, LKDev p) 
 #pragma unroll
                 for (int kk = 0; kk < KK; kk++) {
                     const int x = sx + scol[k0 + kk], y = sy + srow[k0 + kk];
-                    gu8 ia = (gu8)I.data + (ptrdiff_t)y * I.pitch + x;
-                    gu32 qa = dsrc + (ptrdiff_t)y * dpitch + x;
+                    const unsigned oi = (unsigned)(x + kPyrPad) + (unsigned)(y + kPyrPad) * (unsigned)I.pitch;
+                    const unsigned od = 4u * ((unsigned)(x + kDerPad) + (unsigned)(y + kDerPad) * (unsigned)dpitch);
 #pragma unroll
                     for (int r = 0; r <= NR; r++) {
-                        P[kk][r] = __builtin_amdgcn_perm(0u, (unsigned)*(gu16u)(ia + (ptrdiff_t)r * I.pitch),
+                        P[kk][r] = __builtin_amdgcn_perm(0u, (unsigned)ldg_off<u16a1>(ibase, oi + (unsigned)r * I.pitch),
                                                          0x0c010c00u);
-                        D[kk][r] = *(const __attribute__((address_space(1))) u32x2a4*)(qa + (ptrdiff_t)r * dpitch);
+                        D[kk][r] = ldg_off<u32x2a4>(dbase, od + 4u * (unsigned)r * (unsigned)dpitch);
                     }
                 }
                 if (k0 == 0) {
