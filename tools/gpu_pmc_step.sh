@@ -2,13 +2,13 @@
 cd /tmp && export TMPDIR=/tmp; cd $GRAFT_REPO_ROOT
 O=gpurun_out
 B="python bench.py --steps 8 --warmup 2 --no-cpu-baseline --no-single"
-timeout -k 10 200 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VMEM -d $O/ps1 -o run --output-format csv -- $B > $O/ps.log 2>&1 &&
-timeout -k 10 200 rocprofv3 --pmc SQ_ACTIVE_INST_VALU SQ_BUSY_CYCLES SQ_INSTS_BRANCH SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_SCA SQ_INSTS_SMEM -d $O/ps2 -o run --output-format csv -- $B >> $O/ps.log 2>&1 || { tail -20 $O/ps.log; exit 1; }
+timeout -k 10 200 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VMEM -d /tmp/ps1 -o run --output-format csv -- $B > $O/ps.log 2>&1 &&
+timeout -k 10 200 rocprofv3 --pmc SQ_ACTIVE_INST_VALU SQ_BUSY_CYCLES SQ_INSTS_BRANCH SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_SCA SQ_INSTS_SMEM -d /tmp/ps2 -o run --output-format csv -- $B >> $O/ps.log 2>&1 || { tail -20 $O/ps.log; exit 1; }
 python - <<'P'
 import csv, glob, collections, re
 agg = collections.defaultdict(lambda: collections.defaultdict(float))
 disp = collections.defaultdict(set)
-for f in glob.glob('gpurun_out/ps[12]/**/run_counter_collection.csv', recursive=True):
+for f in glob.glob('/tmp/ps[12]/**/run_counter_collection.csv', recursive=True):
     for r in csv.DictReader(open(f)):
         m = re.search(r'([a-z_0-9]+_kernel)', r['Kernel_Name'])
         if not m: continue

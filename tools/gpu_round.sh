@@ -19,3 +19,5 @@ cp profiles/pmc_summary.json $O/pmc_summary.json
 timeout -k 10 600 python bench.py > $O/bench.log 2>&1 || { tail -20 $O/bench.log; exit 1; }
 tail -1 $O/bench.log
 for c in 1080p 4k; do timeout -k 10 400 python bench.py --config $c --seq 16 --steps 10 --warmup 2 --no-cpu-baseline --no-single > $O/bench_$c.log 2>&1 || { tail -5 $O/bench_$c.log; exit 1; }; tail -1 $O/bench_$c.log | cut -c1-400; done
+timeout -k 10 600 bash tools/gpu_pmc_step.sh > $O/pmc_instructions.txt 2>&1 || { tail -5 $O/pmc_instructions.txt; exit 1; }
+tail -20 $O/pmc_instructions.txt
