@@ -188,6 +188,7 @@ struct svo_frontend {
     bool zero_copy = true;
     std::vector<RansacSeq> rs;
     std::vector<int> pred_iters;  // [s] RANSAC hypotheses the last frame's outlier ratio implies
+    int chunk0 = 2;                // floor of the first hypothesis chunk
     std::vector<double> pose;  // [s][6]
     bool fits_pending = false;
     bool stats_pending = false;
@@ -633,6 +634,10 @@ int svo_frontend_create(svo_ctx* ctx, const svo_frontend_config* cfg, svo_fronte
     }
     fe->rs.resize(S);
     fe->pred_iters.assign(S, 0);
+    {
+        const char* e = std::getenv("SVO_FE_CHUNK0");
+        fe->chunk0 = e ? std::max(1, std::atoi(e)) : 2;
+    }
     fe->pose.assign((size_t)S * 6, 0.0);
     int nt = c.host_threads > 0 ? c.host_threads : (int)std::thread::hardware_concurrency();
     nt = std::max(1, std::min({nt, S, 16}));
@@ -1034,7 +1039,10 @@ int svo_frontend_step(svo_frontend* fe, int t, svo_frontend_stats* stats) {
             r.nsamp = kRansacPrefetch;
             // first chunk sized by the hypotheses the previous frame's outlier ratio
             // implies (a prediction only: a short chunk costs one more scoring round)
-            r.first_chunk = std::max(2, fe->pred_iters[s]);
+            // (floor 2, SVO_FE_CHUNK0: a floor of 1 saves an EPnP per sequence when
+            // one hypothesis is predicted, but the extra scoring rounds of the misses
+            // measured slower on the benchmark)
+            r.first_chunk = std::max(fe->chunk0, fe->pred_iters[s]);
             need_full |= r.direct && !r.done;  // n <= 5: EPnP on all points
             max_b = std::max(max_b, fe->h_nB[s]);
         }

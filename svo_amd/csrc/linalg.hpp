@@ -72,7 +72,7 @@ SVO_HD void sym_eig(double* A, int n, double* w, double* V) {
 // Jacobi for the 12x12 EPnP system. Same convention as sym_eig: A (n x n,
 // n <= 12, row-major) is read only; eigenvalues descending in w; eigenvector
 // i in row i of Vt.
-SVO_HD void sym_eig_ql(const double* A, int n, double* w, double* Vt) {
+SVO_HD void sym_eig_ql_n(const double* A, int n, double* w, double* Vt) {
     double V[144], d[12], e[12];
     for (int i = 0; i < n * n; i++) V[i] = A[i];
     // tred2: V <- orthogonal Q, d/e <- diagonal / off-diagonal of Q^T A Q
@@ -211,6 +211,159 @@ SVO_HD void sym_eig_ql(const double* A, int n, double* w, double* Vt) {
         w[i] = d[order[i]];
         for (int k = 0; k < n; k++) Vt[i * n + k] = V[k * n + order[i]];
     }
+}
+
+// sym_eig_ql for a compile-time n with V stored transposed, so that the column
+// updates of tred2 / tql2 (the rotation loop above all) are contiguous and
+// unrolled: the same arithmetic per element in the same order, bit-identical.
+template <int N>
+SVO_HD void sym_eig_ql_t(const double* A, double* w, double* Vt) {
+    constexpr int n = N;
+    double W[N * N], d[N], e[N];  // W = V^T: the column updates of tred2 / tql2 run contiguous
+    for (int r = 0; r < n; r++)
+        for (int c = 0; c < n; c++) W[c * n + r] = A[r * n + c];
+    // tred2: V <- orthogonal Q, d/e <- diagonal / off-diagonal of Q^T A Q
+    for (int j = 0; j < n; j++) d[j] = W[j * n + n - 1];
+    for (int i = n - 1; i > 0; i--) {
+        double scale = 0, h = 0;
+        for (int k = 0; k < i; k++) scale += fabs(d[k]);
+        if (scale == 0) {
+            e[i] = d[i - 1];
+            for (int j = 0; j < i; j++) {
+                d[j] = W[j * n + i - 1];
+                W[j * n + i] = 0;
+                W[i * n + j] = 0;
+            }
+        } else {
+            for (int k = 0; k < i; k++) {
+                d[k] /= scale;
+                h += d[k] * d[k];
+            }
+            double f = d[i - 1];
+            double g = sqrt(h);
+            if (f > 0) g = -g;
+            e[i] = scale * g;
+            h = h - f * g;
+            d[i - 1] = f - g;
+            for (int j = 0; j < i; j++) e[j] = 0;
+            for (int j = 0; j < i; j++) {
+                f = d[j];
+                W[i * n + j] = f;
+                g = e[j] + W[j * n + j] * f;
+                for (int k = j + 1; k <= i - 1; k++) {
+                    g += W[j * n + k] * d[k];
+                    e[k] += W[j * n + k] * f;
+                }
+                e[j] = g;
+            }
+            f = 0;
+            for (int j = 0; j < i; j++) {
+                e[j] /= h;
+                f += e[j] * d[j];
+            }
+            const double hh = f / (h + h);
+            for (int j = 0; j < i; j++) e[j] -= hh * d[j];
+            for (int j = 0; j < i; j++) {
+                f = d[j];
+                g = e[j];
+                for (int k = j; k <= i - 1; k++) W[j * n + k] -= (f * e[k] + g * d[k]);
+                d[j] = W[j * n + i - 1];
+                W[j * n + i] = 0;
+            }
+        }
+        d[i] = h;
+    }
+    for (int i = 0; i < n - 1; i++) {
+        W[i * n + n - 1] = W[i * n + i];
+        W[i * n + i] = 1;
+        const double h = d[i + 1];
+        if (h != 0) {
+            for (int k = 0; k <= i; k++) d[k] = W[(i + 1) * n + k] / h;
+            for (int j = 0; j <= i; j++) {
+                double g = 0;
+                for (int k = 0; k <= i; k++) g += W[(i + 1) * n + k] * W[j * n + k];
+                for (int k = 0; k <= i; k++) W[j * n + k] -= g * d[k];
+            }
+        }
+        for (int k = 0; k <= i; k++) W[(i + 1) * n + k] = 0;
+    }
+    for (int j = 0; j < n; j++) {
+        d[j] = W[j * n + n - 1];
+        W[j * n + n - 1] = 0;
+    }
+    W[(n - 1) * n + n - 1] = 1;
+    e[0] = 0;
+    // tql2: diagonalise the tridiagonal form, accumulating into V
+    for (int i = 1; i < n; i++) e[i - 1] = e[i];
+    e[n - 1] = 0;
+    double f = 0, tst1 = 0;
+    const double eps = 2.220446049250313e-16;
+    for (int l = 0; l < n; l++) {
+        tst1 = fmax(tst1, fabs(d[l]) + fabs(e[l]));
+        int m = l;
+        while (m < n - 1 && fabs(e[m]) > eps * tst1) m++;
+        if (m > l) {
+            for (int iter = 0; iter < 60; iter++) {
+                double g = d[l];
+                double p = (d[l + 1] - g) / (2 * e[l]);
+                double r = sqrt(p * p + 1);
+                if (p < 0) r = -r;
+                d[l] = e[l] / (p + r);
+                d[l + 1] = e[l] * (p + r);
+                const double dl1 = d[l + 1];
+                double h = g - d[l];
+                for (int i = l + 2; i < n; i++) d[i] -= h;
+                f += h;
+                p = d[m];
+                double c = 1, c2 = 1, c3 = 1, s = 0, s2 = 0;
+                const double el1 = e[l + 1];
+                for (int i = m - 1; i >= l; i--) {
+                    c3 = c2;
+                    c2 = c;
+                    s2 = s;
+                    g = c * e[i];
+                    h = c * p;
+                    r = sqrt(p * p + e[i] * e[i]);
+                    e[i + 1] = s * r;
+                    s = e[i] / r;
+                    c = p / r;
+                    p = c * d[i] - s * g;
+                    d[i + 1] = h + s * (c * g + s * d[i]);
+                    for (int k = 0; k < n; k++) {
+                        h = W[(i + 1) * n + k];
+                        W[(i + 1) * n + k] = s * W[i * n + k] + c * h;
+                        W[i * n + k] = c * W[i * n + k] - s * h;
+                    }
+                }
+                p = -s * s2 * c3 * el1 * e[l] / dl1;
+                e[l] = s * p;
+                d[l] = c * p;
+                if (!(fabs(e[l]) > eps * tst1)) break;
+            }
+        }
+        d[l] = d[l] + f;
+        e[l] = 0;
+    }
+    int order[N];
+    for (int i = 0; i < n; i++) order[i] = i;
+    for (int i = 1; i < n; i++) {  // insertion sort, descending
+        int v = order[i], j = i - 1;
+        while (j >= 0 && d[order[j]] < d[v]) {
+            order[j + 1] = order[j];
+            j--;
+        }
+        order[j + 1] = v;
+    }
+    for (int i = 0; i < n; i++) {
+        w[i] = d[order[i]];
+        for (int k = 0; k < n; k++) Vt[i * n + k] = W[order[i] * n + k];
+    }
+}
+
+
+SVO_HD void sym_eig_ql(const double* A, int n, double* w, double* Vt) {
+    if (n == 12) return sym_eig_ql_t<12>(A, w, Vt);  // the EPnP system
+    sym_eig_ql_n(A, n, w, Vt);
 }
 
 // One-sided Jacobi SVD of a (m x n, m <= 12, n <= 12): a = U diag(s) V^T,
