@@ -147,8 +147,8 @@ struct svo_frontend {
     std::vector<int> seed_host;      // [s]
     std::vector<PyrDesc> desc_host;  // [t*S + s]
     PyrDesc* d_desc = nullptr;       // [t][s]
-    void* dermem = nullptr;          // Scharr pyramids, ping-pong [2][s]
-    DerivDesc* d_der = nullptr;      // [2][s]
+    void* dermem = nullptr;          // Scharr pyramids of frames t-1, t, t+1: [3][s], frame f in f % 3
+    DerivDesc* d_der = nullptr;      // [3][s]
     // device state (one allocation)
     void* dmem = nullptr;
     float *xyA, *next_xy, *xyB, *obj, *kps, *cand, *box_binned;
@@ -189,6 +189,7 @@ struct svo_frontend {
     std::vector<RansacSeq> rs;
     std::vector<int> pred_iters;  // [s] RANSAC hypotheses the last frame's outlier ratio implies
     int chunk0 = 2;                // floor of the first hypothesis chunk
+    bool pyr_early = true;         // frame t+1's pyramid beside LK(t) (SVO_FE_PYR_EARLY)
     std::vector<double> pose;  // [s][6]
     bool fits_pending = false;
     bool stats_pending = false;
@@ -610,24 +611,25 @@ int svo_frontend_create(svo_ctx* ctx, const svo_frontend_config* cfg, svo_fronte
         fe->h_best = fe->h_best_b[0];
         fe->h_stats = carve<double>(p, 60 * (size_t)S);
     }
-    // derivative pyramids of the last two frames of every sequence (ping-pong)
+    // derivative pyramids of three frames of every sequence (t - 1: LK's prev,
+    // t, and t + 1, built beside LK(t))
     {
         size_t doff[kMaxLevels];
         int dpitch[kMaxLevels];
         const size_t dbytes = (deriv_layout(c.width, c.height, fe->nlev, doff, dpitch) + 255) & ~(size_t)255;
-        if (hipMalloc(&fe->dermem, dbytes * 2 * S + 256 + sizeof(DerivDesc) * 2 * S) != hipSuccess) {
+        if (hipMalloc(&fe->dermem, dbytes * 3 * S + 256 + sizeof(DerivDesc) * 3 * S) != hipSuccess) {
             svo_frontend_destroy(fe);
             return set_error(ctx, SVO_ERR_HIP, "svo_frontend_create: deriv alloc");
         }
-        std::vector<DerivDesc> hd(2 * (size_t)S);
-        char* base = (char*)fe->dermem + ((sizeof(DerivDesc) * 2 * S + 255) & ~(size_t)255);
-        for (int k = 0; k < 2 * S; k++)
+        std::vector<DerivDesc> hd(3 * (size_t)S);
+        char* base = (char*)fe->dermem + ((sizeof(DerivDesc) * 3 * S + 255) & ~(size_t)255);
+        for (int k = 0; k < 3 * S; k++)
             for (int l = 0; l < kMaxLevels; l++) {
                 hd[k].data[l] = l < fe->nlev ? (uint32_t*)(base + dbytes * k + doff[l]) : nullptr;
                 hd[k].pitch[l] = l < fe->nlev ? dpitch[l] : 0;
             }
         fe->d_der = (DerivDesc*)fe->dermem;
-        SVO_HIP(ctx, hipMemsetAsync(base, 0, dbytes * 2 * S, ctx->stream));  // zero borders, never rewritten
+        SVO_HIP(ctx, hipMemsetAsync(base, 0, dbytes * 3 * S, ctx->stream));  // zero borders, never rewritten
         SVO_HIP(ctx, hipMemcpyAsync(fe->d_der, hd.data(), sizeof(DerivDesc) * hd.size(), hipMemcpyHostToDevice,
                                     ctx->stream));
         SVO_HIP(ctx, hipStreamSynchronize(ctx->stream));
@@ -637,6 +639,8 @@ int svo_frontend_create(svo_ctx* ctx, const svo_frontend_config* cfg, svo_fronte
     {
         const char* e = std::getenv("SVO_FE_CHUNK0");
         fe->chunk0 = e ? std::max(1, std::atoi(e)) : 2;
+        const char* pe = std::getenv("SVO_FE_PYR_EARLY");
+        fe->pyr_early = !(pe && pe[0] == '0');
     }
     fe->pose.assign((size_t)S * 6, 0.0);
     int nt = c.host_threads > 0 ? c.host_threads : (int)std::thread::hardware_concurrency();
@@ -800,7 +804,7 @@ int svo_frontend_init(svo_frontend* fe, int t0) {
     svo_ctx* ctx = fe->ctx;
     const int S = fe->S;
     const PyrDesc* dcur = fe->d_desc + (size_t)(t0 % fe->T) * S;
-    SVO_HIP(ctx, launch_pyramid_scharr_batched(dcur, fe->d_der + (size_t)(t0 & 1) * S, S, fe->W, fe->H, fe->nlev,
+    SVO_HIP(ctx, launch_pyramid_scharr_batched(dcur, fe->d_der + (size_t)(t0 % 3) * S, S, fe->W, fe->H, fe->nlev,
                                                ctx->stream));
     SVO_HIP(ctx, hipMemsetAsync(fe->nA, 0, sizeof(int) * S, ctx->stream));
     SVO_HIP(ctx, hipMemsetAsync(fe->map_n, 0, sizeof(int) * S, ctx->stream));
@@ -855,7 +859,7 @@ static int fe_front_lk(svo_frontend* fe, int t) {
     //    (built ahead by the previous step's fe_front_rest, which recorded ev_pyr)
     if (fe->pyr_ready != t) {
         ph_begin(fe, PH_PYR, st0, &slot);
-        SVO_HIP(ctx, launch_pyramid_scharr_batched(dcur, fe->d_der + (size_t)(t & 1) * S, S, fe->W, fe->H, fe->nlev,
+        SVO_HIP(ctx, launch_pyramid_scharr_batched(dcur, fe->d_der + (size_t)(t % 3) * S, S, fe->W, fe->H, fe->nlev,
                                                    st0));
         ph_end(fe, st0, slot);
         SVO_HIP(ctx, hipEventRecord(ev_pyr, st0));
@@ -891,13 +895,27 @@ static int fe_front_lk(svo_frontend* fe, int t) {
         const int mp = CAP;  // grid bound: the host counts of the previous tail may not be back yet
         SVO_HIP(ctx, hipStreamWaitEvent(sg, ev_pyr, 0));
         if (g > 0) SVO_HIP(ctx, hipStreamWaitEvent(sg, fe->ev_sync[2 + 2 * (g - 1)], 0));
-        LKBatch lb{dprev + a, dcur + a, fe->d_der + (size_t)((t - 1) & 1) * S + a, fe->xyA + 2 * (size_t)a * CAP,
+        LKBatch lb{dprev + a, dcur + a, fe->d_der + (size_t)((t - 1) % 3) * S + a, fe->xyA + 2 * (size_t)a * CAP,
                    fe->next_xy + 2 * (size_t)a * CAP, fe->status + (size_t)a * CAP, nullptr,
                    fe->iters + (size_t)a * CAP, fe->nA + a, 0, CAP};
         ph_begin(fe, PH_LK, sg, &slot);
         SVO_HIP(ctx, launch_lk(lb, n, mp, lp, sg));
         ph_end(fe, sg, slot);
         SVO_HIP(ctx, hipEventRecord(fe->ev_sync[2 + 2 * g], sg));
+    }
+    // 3'. frame t+1's pyramid + Scharr + borders, queued beside this LK: the
+    //     derivative pyramids are triple-buffered (frame f in f % 3), so nothing
+    //     this step reads is overwritten, and the memory-bound pyramid shares the
+    //     GPU with the VALU-bound LK instead of the post-LK window
+    if (fe->pyr_early) {
+        const int tn = t + 1;
+        const PyrDesc* dnext = fe->d_desc + (size_t)(tn % fe->T) * S;
+        ph_begin(fe, PH_PYR, st0, &slot);
+        SVO_HIP(ctx, launch_pyramid_scharr_batched(dnext, fe->d_der + (size_t)(tn % 3) * S, S, fe->W, fe->H,
+                                                   fe->nlev, st0));
+        ph_end(fe, st0, slot);
+        SVO_HIP(ctx, hipEventRecord(ev_pyr, st0));
+        fe->pyr_ready = tn;
     }
     return SVO_OK;
 }
@@ -911,18 +929,16 @@ static int fe_front_rest(svo_frontend* fe, int t) {
     const PyrDesc* dcur = fe->d_desc + (size_t)(t % fe->T) * S;
     hipEvent_t ev_fast = fe->ev_sync[1];
     int slot;
-    // 3b'. build frame t+1's pyramid + Scharr ahead, once every LK of this step is
-    //      done (the Scharr ping-pong buffer it writes is the one LK reads): it
-    //      runs beside FAST while the host solves RANSAC (measured: serialising it
-    //      behind the post-LK kernel on the slice stream is slower). Used if the
-    //      next step is t+1; ev_pyr records its end.
-    fe->pyr_ready = -1;
-    {
+    // 3b'. (SVO_FE_PYR_EARLY=0 only) build frame t+1's pyramid + Scharr ahead once
+    //      every LK of this step is done: it then runs beside FAST while the host
+    //      solves RANSAC. Used if the next step is t+1; ev_pyr records its end.
+    if (!fe->pyr_early) {
+        fe->pyr_ready = -1;
         const int tn = t + 1;
         const PyrDesc* dnext = fe->d_desc + (size_t)(tn % fe->T) * S;
         SVO_HIP(ctx, hipStreamWaitEvent(st0, fe->ev_sync[2 + 2 * (G - 1)], 0));
         ph_begin(fe, PH_PYR, st0, &slot);
-        SVO_HIP(ctx, launch_pyramid_scharr_batched(dnext, fe->d_der + (size_t)(tn & 1) * S, S, fe->W, fe->H,
+        SVO_HIP(ctx, launch_pyramid_scharr_batched(dnext, fe->d_der + (size_t)(tn % 3) * S, S, fe->W, fe->H,
                                                    fe->nlev, st0));
         ph_end(fe, st0, slot);
         SVO_HIP(ctx, hipEventRecord(fe->ev_sync[0], st0));
