@@ -39,6 +39,19 @@ constexpr float FLT_SCALE = 1.f / (1 << 20);
 
 __device__ __forceinline__ int descale(int x, int n) { return (x + (1 << (n - 1))) >> n; }
 
+// OpenCV's `delta.ddot(delta) <= criteria.epsilon^2` (double products of float
+// deltas) decided in float where the float sum is far enough from eps2, in double
+// only inside the 2^-20 band around it
+__device__ __forceinline__ bool converged(float dx, float dy, float lo, float hi, double eps2) {
+    const float sf = dx * dx + dy * dy;
+    if (sf < lo) return true;
+    if (sf > hi) return false;
+    return (double)dx * dx + (double)dy * dy <= eps2;
+}
+// `std::abs(a + b) < 0.01` with a float sum promoted to double: the largest float
+// below 0.01 is the bound
+__device__ __forceinline__ bool below_001(float v) { return fabsf(v) <= 0x1.47ae14p-7f; }
+
 __device__ __forceinline__ int refl101(int p, int len) {
     if ((unsigned)p < (unsigned)len) return p;
     if (len == 1) return 0;
@@ -85,6 +98,7 @@ struct LKDev {
     int ip_bytes, lds_wave;        // per-wave LDS carve
     int max_level, max_count;
     double eps2;
+    float eps2_lo, eps2_hi;  // float brackets of eps2 (see converged())
     int flags, want_err;
     float min_eig;
 };
@@ -1308,9 +1322,9 @@ __global__ __launch_bounds__(64, MINW) void lk_dual_kernel(LKBatch B, LKDev p) {
                 nexty += dy;
                 nx = nextx + halfWx;
                 ny = nexty + halfWy;
-                if ((double)dx * dx + (double)dy * dy <= p.eps2) {
+                if (converged(dx, dy, p.eps2_lo, p.eps2_hi, p.eps2)) {
                     lact = false;
-                } else if (j > 0 && (double)fabsf(dx + pdx) < 0.01 && (double)fabsf(dy + pdy) < 0.01) {
+                } else if (j > 0 && below_001(dx + pdx) && below_001(dy + pdy)) {
                     nx -= dx * 0.5f;
                     ny -= dy * 0.5f;
                     lact = false;
@@ -1635,9 +1649,9 @@ __global__ __launch_bounds__(64, MINW) void lk_multi_kernel(LKBatch B, LKDev p) 
                 nexty += dy;
                 nx = nextx + halfWx;
                 ny = nexty + halfWy;
-                if ((double)dx * dx + (double)dy * dy <= p.eps2) {
+                if (converged(dx, dy, p.eps2_lo, p.eps2_hi, p.eps2)) {
                     lact = false;
-                } else if (j > 0 && (double)fabsf(dx + pdx) < 0.01 && (double)fabsf(dy + pdy) < 0.01) {
+                } else if (j > 0 && below_001(dx + pdx) && below_001(dy + pdy)) {
                     nx -= dx * 0.5f;
                     ny -= dy * 0.5f;
                     lact = false;
@@ -1728,6 +1742,12 @@ hipError_t launch_lk(const LKBatch& b, int nseq, int max_n, const LKParams& lp, 
     d.max_level = lp.max_level;
     d.max_count = lp.max_count;
     d.eps2 = lp.eps2;
+    // |float(dx*dx + dy*dy) / exact - 1| <= 3 * 2^-24: outside eps2 * (1 -+ 2^-20) the
+    // float sum decides the double comparison exactly
+    d.eps2_lo = (float)(lp.eps2 * (1.0 - 0x1p-20));
+    d.eps2_hi = (float)(lp.eps2 * (1.0 + 0x1p-20));
+    if ((double)d.eps2_lo > lp.eps2 * (1.0 - 0x1p-20)) d.eps2_lo = nextafterf(d.eps2_lo, 0.f);
+    if ((double)d.eps2_hi < lp.eps2 * (1.0 + 0x1p-20)) d.eps2_hi = nextafterf(d.eps2_hi, INFINITY);
     d.flags = lp.flags;
     d.want_err = lp.want_err;
     d.min_eig = lp.min_eig;
