@@ -134,13 +134,24 @@ class EPnP {
             r[9] = dot3(dv[3][i], dv[3][i]);
         }
     }
+    // The 6 x {4, 3, 5} least-squares systems are solved by Householder QR
+    // (qr_solve, as the Gauss-Newton steps): OpenCV solves them by SVD
+    // (cvSolve(CV_SVD)); for these full-rank systems both give the unique
+    // least-squares solution up to rounding, which the 5 Gauss-Newton steps then
+    // refine -- at a fraction of the SVD's cost.
+    SVO_HD static void lstsq_qr(const double* A, int nc, const double* rho, double* x) {
+        double Aq[30], bq[6];
+        for (int i = 0; i < 6 * nc; i++) Aq[i] = A[i];
+        for (int i = 0; i < 6; i++) bq[i] = rho[i];
+        qr_solve(Aq, 6, nc, bq, x);
+    }
     SVO_HD static void betas_approx(int which, const double* L, const double* rho, double* b) {
         static const int cols1[4] = {0, 1, 3, 6};
         double A[30], x[5];
         if (which == 1) {
             for (int i = 0; i < 6; i++)
                 for (int k = 0; k < 4; k++) A[4 * i + k] = L[10 * i + cols1[k]];
-            la::lstsq(A, 6, 4, rho, x);
+            lstsq_qr(A, 4, rho, x);
             const double sg = x[0] < 0 ? -1.0 : 1.0;
             b[0] = sqrt(sg * x[0]);
             b[1] = sg * x[1] / b[0];
@@ -151,7 +162,7 @@ class EPnP {
         const int nc = which == 2 ? 3 : 5;
         for (int i = 0; i < 6; i++)
             for (int k = 0; k < nc; k++) A[nc * i + k] = L[10 * i + k];
-        la::lstsq(A, 6, nc, rho, x);
+        lstsq_qr(A, nc, rho, x);
         if (x[0] < 0) {
             b[0] = sqrt(-x[0]);
             b[1] = (x[2] < 0) ? sqrt(-x[2]) : 0.0;
