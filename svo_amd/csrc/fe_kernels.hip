@@ -167,7 +167,12 @@ __global__ __launch_bounds__(256) void ransac_sample_kernel(const int* __restric
     }
 }
 
-// Stable compaction of one sequence by a keep predicate, by a 1024-thread
+// Block size of the per-sequence post-LK / tail kernels: 4 waves, so that a block
+// finds room on a CU while another slice's LK still occupies the GPU (a
+// 1024-thread block waits for a whole CU to drain).
+constexpr int kFeBlock = 256;
+
+// Stable compaction of one sequence by a keep predicate, by a kFeBlock-thread
 // block: keep(i) for i < n, kept entries of xy / mid moved to their rank.
 template <typename Keep>
 __device__ __forceinline__ int block_compact(int n, Keep keep, const float* __restrict__ xy_in,
@@ -176,7 +181,7 @@ __device__ __forceinline__ int block_compact(int n, Keep keep, const float* __re
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     if (tid == 0) *base_s = 0;
     __syncthreads();
-    for (int c0 = 0; c0 < n; c0 += 1024) {
+    for (int c0 = 0; c0 < n; c0 += kFeBlock) {
         const int i = c0 + tid;
         const bool k = i < n && keep(i);
         const unsigned long long bal = __ballot(k);
@@ -200,7 +205,7 @@ __device__ __forceinline__ int block_compact(int n, Keep keep, const float* __re
         }
         if (tid == 0) {
             int tot = 0;
-            for (int q = 0; q < 16; q++) tot += wsum[q];
+            for (int q = 0; q < kFeBlock / 64; q++) tot += wsum[q];
             *base_s += tot;
         }
         __syncthreads();
@@ -216,10 +221,10 @@ __device__ __forceinline__ unsigned fast_mod(unsigned x, unsigned n, unsigned m)
     return r;
 }
 
-__global__ __launch_bounds__(1024) void post_lk_kernel(PostLkBatch B) {
+__global__ __launch_bounds__(kFeBlock) void post_lk_kernel(PostLkBatch B) {
     const int s = blockIdx.x;
     const size_t o = (size_t)s * B.cap;
-    __shared__ int wsum[16];
+    __shared__ int wsum[kFeBlock / 64];
     __shared__ int base_s;
     __shared__ unsigned long long it_s;
     __shared__ int idx[5 * 64];
@@ -228,7 +233,7 @@ __global__ __launch_bounds__(1024) void post_lk_kernel(PostLkBatch B) {
     const int n_in = B.n_in[s];
     const uint8_t* __restrict__ st = B.status + o;
     long long it = 0;
-    for (int i = tid; i < n_in; i += 1024) it += B.iters[o + i];
+    for (int i = tid; i < n_in; i += kFeBlock) it += B.iters[o + i];
     const int n = block_compact(n_in, [&](int i) { return st[i] != 0; }, B.xy_in + 2 * o, B.mid_in + o,
                                 B.xy_out + 2 * o, B.mid_out + o, wsum, &base_s);
     for (int off = 32; off > 0; off >>= 1) it += __shfl_xor(it, off);
@@ -254,7 +259,7 @@ __global__ __launch_bounds__(1024) void post_lk_kernel(PostLkBatch B) {
     }
     const int* __restrict__ mid = B.mid_out + o;
     const double* __restrict__ map = B.map + 3 * (size_t)s * B.map_cap;
-    for (int i = tid; i < n; i += 1024) {
+    for (int i = tid; i < n; i += kFeBlock) {
         const double* X = map + 3 * (size_t)mid[i];
         B.obj[3 * (o + i)] = (float)X[0];
         B.obj[3 * (o + i) + 1] = (float)X[1];
@@ -269,7 +274,7 @@ __global__ __launch_bounds__(1024) void post_lk_kernel(PostLkBatch B) {
     if (draws) {
         const float* __restrict__ xy = B.xy_out + 2 * o;
         float* __restrict__ dst = B.h_samp + (size_t)25 * B.nh * s;
-        for (int k = tid; k < 5 * B.nh; k += 1024) {
+        for (int k = tid; k < 5 * B.nh; k += kFeBlock) {
             const int j = k / 5, i = k - 5 * j, p = idx[k];
             const double* X = map + 3 * (size_t)mid[p];
             float* h = dst + 25 * j;
@@ -327,9 +332,9 @@ __device__ __forceinline__ void append_body(const AppendBatch& B, int s) {
     }
 }
 
-__global__ __launch_bounds__(1024) void tail_kernel(TailBatch T, AppendBatch A) {
+__global__ __launch_bounds__(kFeBlock) void tail_kernel(TailBatch T, AppendBatch A) {
     const int s = blockIdx.x;
-    __shared__ int wsum[16];
+    __shared__ int wsum[kFeBlock / 64];
     __shared__ int base_s;
     const size_t o = (size_t)s * A.cap;
     const uint32_t* __restrict__ bits = T.bits + (size_t)s * T.words_cap;
@@ -347,12 +352,12 @@ __global__ __launch_bounds__(1024) void tail_kernel(TailBatch T, AppendBatch A) 
 }  // namespace
 
 hipError_t launch_post_lk(const PostLkBatch& b, int nseq, hipStream_t st) {
-    hipLaunchKernelGGL(post_lk_kernel, dim3(nseq), dim3(1024), 0, st, b);
+    hipLaunchKernelGGL(post_lk_kernel, dim3(nseq), dim3(kFeBlock), 0, st, b);
     return hipGetLastError();
 }
 
 hipError_t launch_tail(const TailBatch& tb, const AppendBatch& ab, int nseq, hipStream_t st) {
-    hipLaunchKernelGGL(tail_kernel, dim3(nseq), dim3(1024), 0, st, tb, ab);
+    hipLaunchKernelGGL(tail_kernel, dim3(nseq), dim3(kFeBlock), 0, st, tb, ab);
     return hipGetLastError();
 }
 

@@ -190,6 +190,7 @@ struct svo_frontend {
     std::vector<int> pred_iters;  // [s] RANSAC hypotheses the last frame's outlier ratio implies
     int chunk0 = 2;                // floor of the first hypothesis chunk
     bool pyr_early = true;         // frame t+1's pyramid beside LK(t) (SVO_FE_PYR_EARLY)
+    bool fast_early = true;        // FAST(t) queued behind LK(t), not after it (SVO_FE_FAST_EARLY)
     std::vector<double> pose;  // [s][6]
     bool fits_pending = false;
     bool stats_pending = false;
@@ -201,6 +202,7 @@ struct svo_frontend {
     // the final fits, RANSAC past the prefetched subsets and the n <= 5 solve, so
     // they travel on their own stream once requested
     hipStream_t st_copy = nullptr;
+    bool st_copy_owned = true;
     hipEvent_t ev_gathered = nullptr, ev_full = nullptr;  // ev_full: this step's parity of ev_full_b
     hipEvent_t ev_full_b[2] = {nullptr, nullptr};
     bool full_queued = false;
@@ -641,6 +643,8 @@ int svo_frontend_create(svo_ctx* ctx, const svo_frontend_config* cfg, svo_fronte
         fe->chunk0 = e ? std::max(1, std::atoi(e)) : 2;
         const char* pe = std::getenv("SVO_FE_PYR_EARLY");
         fe->pyr_early = !(pe && pe[0] == '0');
+        const char* fe_ = std::getenv("SVO_FE_FAST_EARLY");
+        fe->fast_early = !(fe_ && fe_[0] == '0');
     }
     fe->pose.assign((size_t)S * 6, 0.0);
     int nt = c.host_threads > 0 ? c.host_threads : (int)std::thread::hardware_concurrency();
@@ -662,12 +666,17 @@ int svo_frontend_create(svo_ctx* ctx, const svo_frontend_config* cfg, svo_fronte
         }
         int least = 0, greatest = 0;
         (void)hipDeviceGetStreamPriorityRange(&least, &greatest);
+        // slice 0 at the highest priority, later slices one level lower: their LKs
+        // run concurrently (no serialisation between slices), slice 0's blocks are
+        // dispatched first and finish first, so its RANSAC overlaps the later LKs
         fe->gst.assign(G, nullptr);
-        for (auto& g : fe->gst)
-            if (hipStreamCreateWithPriority(&g, hipStreamNonBlocking, greatest) != hipSuccess) {
+        for (int g = 0; g < G; g++) {
+            const int pr = g == 0 ? greatest : std::min(std::max(greatest + 1, greatest), least);
+            if (hipStreamCreateWithPriority(&fe->gst[g], hipStreamNonBlocking, pr) != hipSuccess) {
                 svo_frontend_destroy(fe);
                 return set_error(ctx, SVO_ERR_HIP, "svo_frontend_create: stream");
             }
+        }
         if (hipStreamCreateWithPriority(&fe->st_fast, hipStreamNonBlocking, least) != hipSuccess) {
             svo_frontend_destroy(fe);
             return set_error(ctx, SVO_ERR_HIP, "svo_frontend_create: stream");
@@ -681,7 +690,12 @@ int svo_frontend_create(svo_ctx* ctx, const svo_frontend_config* cfg, svo_fronte
         for (auto& e : fe->ev_full_b) (void)hipEventCreateWithFlags(&e, hipEventDisableTiming);
         fe->ev_full = fe->ev_full_b[0];
         (void)hipEventCreateWithFlags(&fe->ev_counts, hipEventDisableTiming);
-        if (hipStreamCreateWithFlags(&fe->st_copy, hipStreamNonBlocking) != hipSuccess) {
+        // 4 hardware queues: with several slices the copy stream's work shares the
+        // pyramid stream
+        if (G > 1) {
+            fe->st_copy = ctx->stream;
+            fe->st_copy_owned = false;
+        } else if (hipStreamCreateWithFlags(&fe->st_copy, hipStreamNonBlocking) != hipSuccess) {
             svo_frontend_destroy(fe);
             return set_error(ctx, SVO_ERR_HIP, "svo_frontend_create: stream");
         }
@@ -718,7 +732,7 @@ void svo_frontend_destroy(svo_frontend* fe) {
     for (auto& e : fe->ev_sync)
         if (e) (void)hipEventDestroy(e);
     if (fe->ev_stats) (void)hipEventDestroy(fe->ev_stats);
-    if (fe->st_copy) {
+    if (fe->st_copy && fe->st_copy_owned) {
         (void)hipStreamSynchronize(fe->st_copy);
         (void)hipStreamDestroy(fe->st_copy);
     }
@@ -894,7 +908,7 @@ static int fe_front_lk(svo_frontend* fe, int t) {
         hipStream_t sg = fe->gst[g];
         const int mp = CAP;  // grid bound: the host counts of the previous tail may not be back yet
         SVO_HIP(ctx, hipStreamWaitEvent(sg, ev_pyr, 0));
-        if (g > 0) SVO_HIP(ctx, hipStreamWaitEvent(sg, fe->ev_sync[2 + 2 * (g - 1)], 0));
+
         LKBatch lb{dprev + a, dcur + a, fe->d_der + (size_t)((t - 1) % 3) * S + a, fe->xyA + 2 * (size_t)a * CAP,
                    fe->next_xy + 2 * (size_t)a * CAP, fe->status + (size_t)a * CAP, nullptr,
                    fe->iters + (size_t)a * CAP, fe->nA + a, 0, CAP};
@@ -902,6 +916,17 @@ static int fe_front_lk(svo_frontend* fe, int t) {
         SVO_HIP(ctx, launch_lk(lb, n, mp, lp, sg));
         ph_end(fe, sg, slot);
         SVO_HIP(ctx, hipEventRecord(fe->ev_sync[2 + 2 * g], sg));
+    }
+    // 3b. mask around frame t-1's features (the reference masks with prevFrame's
+    //     features, R:src/tracking.cpp:77) + FAST/bucket on frame t, whole batch:
+    //     independent of this step's LK and pose, so it is queued right behind the
+    //     LK on the low-priority FAST stream, where it fills the CUs the LK's last
+    //     waves leave idle and the post-LK window; the tail waits for it
+    if (fe->fast_early) {
+        hipStream_t sf = fe->st_fast;
+        int rc = fe_fast_and_bucket(fe, dcur, true, sf, true);
+        if (rc) return rc;
+        SVO_HIP(ctx, hipEventRecord(fe->ev_sync[1], sf));
     }
     // 3'. frame t+1's pyramid + Scharr + borders, queued beside this LK: the
     //     derivative pyramids are triple-buffered (frame f in f % 3), so nothing
@@ -965,6 +990,7 @@ static int fe_front_rest(svo_frontend* fe, int t) {
     // every slice's points are gathered once the last slice's copies are queued
     // (slices run in order on their streams; the full copy waits for the last)
     SVO_HIP(ctx, hipEventRecord(fe->ev_gathered, fe->gst[G - 1]));
+    for (int g = 0; g + 1 < G; g++) SVO_HIP(ctx, hipStreamWaitEvent(fe->st_copy, fe->ev_sync[3 + 2 * g], 0));
 
     // the full point set for the final fits / long RANSAC runs, on the copy
     // stream behind the subsets' D2H (parity buffers: the previous step's fits
@@ -974,15 +1000,15 @@ static int fe_front_rest(svo_frontend* fe, int t) {
         if (rq) return rq;
     }
 
-    // 3b. mask around frame t-1's features (the reference masks with prevFrame's
-    //     features, R:src/tracking.cpp:77) + FAST/bucket on frame t, whole batch,
-    //     on its own stream after the last LK: independent of the pose, it fills
-    //     the GPU while the host solves RANSAC (and does not slow LK down)
-    hipStream_t sf = fe->st_fast;
-    SVO_HIP(ctx, hipStreamWaitEvent(sf, fe->ev_sync[2 + 2 * (G - 1)], 0));
-    int rc = fe_fast_and_bucket(fe, dcur, true, sf, true);
-    if (rc) return rc;
-    SVO_HIP(ctx, hipEventRecord(ev_fast, sf));
+    // 3b. (SVO_FE_FAST_EARLY=0 only) mask around frame t-1's features + FAST/bucket
+    //     on frame t after every LK of the step
+    if (!fe->fast_early) {
+        hipStream_t sf = fe->st_fast;
+        for (int g = 0; g < G; g++) SVO_HIP(ctx, hipStreamWaitEvent(sf, fe->ev_sync[2 + 2 * g], 0));
+        int rc = fe_fast_and_bucket(fe, dcur, true, sf, true);
+        if (rc) return rc;
+        SVO_HIP(ctx, hipEventRecord(ev_fast, sf));
+    }
     return SVO_OK;
 }
 
@@ -1213,7 +1239,10 @@ int svo_frontend_step(svo_frontend* fe, int t, svo_frontend_stats* stats) {
         return !(e && e[0] == '0');
     }();
     const bool ahead = prefetch && t + 1 < fe->T;
-    fe->boxes_binned = true;  // queued just below, behind the next LK
+    // the binning of these features as the next frame's mask boxes, on the FAST
+    // stream ahead of the next step's FAST (queued with its LK)
+    SVO_HIP(ctx, launch_box_bin(fe_fast_batch(fe, dcur, true), S, fe->W, fe->H, sf));
+    fe->boxes_binned = true;
     rc = fe_queue_stats(fe);
     if (rc) return rc;
     if (ahead) {
@@ -1221,8 +1250,6 @@ int svo_frontend_step(svo_frontend* fe, int t, svo_frontend_stats* stats) {
         if (rc) return rc;
     }
     TP("next lk queued");
-    // the binning of these features as the next frame's mask boxes, beside the next LK
-    SVO_HIP(ctx, launch_box_bin(fe_fast_batch(fe, dcur, true), S, fe->W, fe->H, sf));
     TP("tail enqueued");
     if (ahead) {
         rc = fe_front_rest(fe, t + 1);

@@ -16,7 +16,12 @@ for r in csv.DictReader(open(f"{d}/run_memory_copy_trace.csv")):
     rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), "C:" + r["Direction"][:24], r.get("Queue_Id", "")))
 rows.sort()
 lk = [x for x in rows if x[2].startswith("K:lk_")]
-t0, tp = lk[-1][0], lk[-2][0]
+# slices of one step launch their LKs together: step starts = LK starts > 100 us apart
+starts = [lk[0][0]]
+for x in lk[1:]:
+    if x[0] - starts[-1] > 100_000:
+        starts.append(x[0])
+t0, tp = starts[-1], starts[-2]
 print(f"step period {(t0 - tp) / 1e3:.1f} us")
 for a, b, n, q in rows:
     if tp <= a < t0:
