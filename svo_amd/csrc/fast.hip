@@ -591,6 +591,215 @@ __global__ __launch_bounds__(256) void fast_detect_w_kernel(FastDetBatch B, int 
     }
 }
 
+// ---- SWAR form (SVO_FAST_V=3): as fast_detect_w_kernel, with the compass
+// pre-test on 4 pixels per lane and a register NMS. The staged tile starts 8
+// pixels left of the tile (T column c <-> x = x0 - 8 + c) and the score region
+// 4 pixels left (SC column xs <-> x = x0 - 4 + xs), so a pre-test item -- score
+// row sr, pixels x0 - 4 + 4j .. + 3 -- reads its centre row as three aligned
+// dwords (the +-3 compass pixels by v_alignbyte) and rows +-3 as one dword each,
+// and tests the 4 pixels with packed 16-bit min/max in two halves (bytes 0/2 and
+// 1/3): brighter <=> min(max(p0, p8), max(p4, p12)) > v + t, darker <=>
+// max(min(p0, p8), min(p4, p12)) < v - t -- the same necessary condition as the
+// other forms. NMS reads each score row's 3 neighbours once per wave and keeps
+// the row maxima in registers. Same outputs as fast_detect_kernel. ----
+constexpr int F3_IW = FD_TX + 16;  // staged columns x0 - 8 .. x0 + 71
+constexpr int F3_SW = FD_TX + 8;   // score columns x0 - 4 .. x0 + 67 (18 dwords)
+constexpr int F3_Q = 9 * F3_SW + 8;
+
+typedef unsigned short fu16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ fu16x2 as_w2(unsigned v) { return __builtin_bit_cast(fu16x2, v); }
+__device__ __forceinline__ unsigned w2_as(fu16x2 v) { return __builtin_bit_cast(unsigned, v); }
+
+// candidate bits (bit b: byte b) of 4 pixels v with compass pixels p0 (dy +3),
+// p8 (dy -3), p4 (dx +3), p12 (dx -3), all packed bytes
+__device__ __forceinline__ unsigned pretest4(unsigned v, unsigned p0, unsigned p8, unsigned p4, unsigned p12, int t) {
+    const fu16x2 t1 = {(unsigned short)(t + 1), (unsigned short)(t + 1)};
+    unsigned z[2];
+#pragma unroll
+    for (int o = 0; o < 2; o++) {  // o = 0: bytes 0, 2; o = 1: bytes 1, 3 (zero-extended)
+        const unsigned sel = o ? 0x0c030c01u : 0x0c020c00u;
+        const fu16x2 V = as_w2(__builtin_amdgcn_perm(0u, v, sel));
+        const fu16x2 A = as_w2(__builtin_amdgcn_perm(0u, p0, sel)), Bv = as_w2(__builtin_amdgcn_perm(0u, p8, sel));
+        const fu16x2 C = as_w2(__builtin_amdgcn_perm(0u, p4, sel)), Dv = as_w2(__builtin_amdgcn_perm(0u, p12, sel));
+        const fu16x2 m = __builtin_elementwise_min(__builtin_elementwise_max(A, Bv), __builtin_elementwise_max(C, Dv));
+        const fu16x2 M = __builtin_elementwise_max(__builtin_elementwise_min(A, Bv), __builtin_elementwise_min(C, Dv));
+        // sign of m - (v + t + 1): not brighter; sign of (v - t - 1) - M: not darker
+        const unsigned x = w2_as(m - (V + t1)), y = w2_as((V - t1) - M);
+        z[o] = ~(x & y);  // bit 15 / 31: candidate
+    }
+    return ((z[0] >> 15) & 1u) | ((z[1] >> 14) & 2u) | ((z[0] >> 29) & 4u) | ((z[1] >> 28) & 8u);
+}
+
+__global__ __launch_bounds__(256) void fast_detect_s_kernel(FastDetBatch B, int threshold, int nonmax) {
+    const ImgLevel L = B.descs[blockIdx.z].lv[0];
+    const int w = L.w, h = L.h;
+    const int x0 = blockIdx.x * FD_TX, y0 = blockIdx.y * FD_TY;
+    const size_t seq = blockIdx.z;
+    __shared__ __attribute__((aligned(16))) uint8_t T[FD_IH][F3_IW];
+    __shared__ uint16_t SC[FD_SH][F3_SW];  // bit 8: corner, low byte: score
+    __shared__ uint16_t CQ[4][F3_Q];
+    __shared__ unsigned long long TM[FD_TY];
+    __shared__ unsigned long long RB[FD_TY];
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const bool inside = x0 >= 8 && y0 >= 4 && x0 - 8 + F3_IW <= w && y0 - 4 + FD_IH <= h;
+    if (inside) {
+        for (int k = tid; k < FD_IH * (F3_IW / 4); k += 256) {
+            const int r = k / (F3_IW / 4), c4 = k - r * (F3_IW / 4);
+            const uint8_t* src = L.data + (size_t)(y0 - 4 + r) * L.pitch + (x0 - 8 + 4 * c4);
+            *reinterpret_cast<uint32_t*>(&T[r][4 * c4]) = *reinterpret_cast<const uint32_t*>(src);
+        }
+    } else {
+        for (int k = tid; k < FD_IH * F3_IW; k += 256) {
+            const int r = k / F3_IW, c = k - r * F3_IW;
+            const int y = y0 - 4 + r, x = x0 - 8 + c;
+            T[r][c] = ((unsigned)y < (unsigned)h && (unsigned)x < (unsigned)w) ? L.data[(size_t)y * L.pitch + x] : 0;
+        }
+    }
+    const bool boxes = B.box_pts != nullptr;
+    if (boxes && tid < FD_TY) TM[tid] = ~0ull;
+    for (int sr = wv; sr < FD_SH; sr += 4) {  // this wave's score rows
+        SC[sr][lane] = 0;
+        if (lane < F3_SW - 64) SC[sr][64 + lane] = 0;
+    }
+    __syncthreads();
+    // ---- A0: pre-test items (k-th row of the wave sr = wv + 4k, dword j) ----
+    uint16_t* q = CQ[wv];
+    int nq = 0;
+    const int nrows = (FD_SH - wv + 3) / 4, nitems = nrows * (F3_SW / 4);
+    const int lox = max(x0 - 1, 3), hix = min(x0 + FD_TX, w - 4);  // score pixels to test
+    for (int base = 0; base < nitems; base += 64) {
+        const int it = base + lane;
+        const int k = it / (F3_SW / 4), j = it - (F3_SW / 4) * k;
+        const int sr = wv + 4 * k;
+        const int y = y0 - 1 + sr;
+        unsigned cm = 0;
+        if (it < nitems && y >= 3 && y < h - 3) {
+            const int ty = sr + 3;
+            const unsigned d0 = *reinterpret_cast<const unsigned*>(&T[ty][4 * j]);
+            const unsigned d1 = *reinterpret_cast<const unsigned*>(&T[ty][4 * j + 4]);
+            const unsigned d2 = *reinterpret_cast<const unsigned*>(&T[ty][4 * j + 8]);
+            const unsigned up = *reinterpret_cast<const unsigned*>(&T[ty - 3][4 * j + 4]);
+            const unsigned dn = *reinterpret_cast<const unsigned*>(&T[ty + 3][4 * j + 4]);
+            const unsigned p12 = __builtin_amdgcn_alignbyte(d1, d0, 1);  // x - 3
+            const unsigned p4 = __builtin_amdgcn_alignbyte(d2, d1, 3);   // x + 3
+            cm = pretest4(d1, dn, up, p4, p12, threshold);
+            const int xb = x0 - 4 + 4 * j;
+            const int s0 = min(max(lox - xb, 0), 4), e0 = min(max(hix - xb + 1, 0), 4);
+            cm &= ((1u << e0) - 1u) & ~((1u << s0) - 1u);
+        }
+#pragma unroll
+        for (int b = 0; b < 4; b++) {
+            const bool c = (cm >> b) & 1u;
+            const unsigned long long bal = __ballot(c);
+            if (c) q[nq + __popcll(bal & ((1ull << lane) - 1ull))] = (uint16_t)((sr << 7) | (4 * j + b));
+            nq += __popcll(bal);
+        }
+    }
+    // ---- A1: full segment test of the queue, compacted in place to the corners ----
+    int nc = 0;
+    for (int base = 0; base < nq; base += 64) {
+        const int i = base + lane;
+        bool corner = false;
+        int k = 0;
+        if (i < nq) {
+            k = q[i];
+            const int ty = (k >> 7) + 3, tx = (k & 127) + 4;
+            const int v = T[ty][tx];
+            const fs16x2 th = {(short)(v + threshold + 1), (short)(v - threshold)};
+            unsigned acc = 0;
+#pragma unroll
+            for (int qq = 0; qq < 16; qq++) {
+                const int rv = T[ty + c_ring[qq][1]][tx + c_ring[qq][0]];
+                const fs16x2 r2 = {(short)rv, (short)rv};
+                const unsigned sg = as_u(r2 - th);
+                acc |= (sg >> (15 - qq)) & (0x00010001u << qq);
+            }
+            corner = run9(~acc & 0xFFFFu) || run9(acc >> 16);
+        }
+        const unsigned long long bal = __ballot(corner);
+        if (corner) {
+            SC[k >> 7][k & 127] = 0x100;
+            q[nc + __popcll(bal & ((1ull << lane) - 1ull))] = (uint16_t)k;  // index <= i: already read
+        }
+        nc += __popcll(bal);
+    }
+    // ---- B: cornerScore of the corners (NMS only) ----
+    if (nonmax) {
+        for (int i = lane; i < nc; i += 64) {
+            const int k = q[i];
+            const int ty = (k >> 7) + 3, tx = (k & 127) + 4;
+            const int v = T[ty][tx];
+            int ring[16];
+#pragma unroll
+            for (int qq = 0; qq < 16; qq++) ring[qq] = T[ty + c_ring[qq][1]][tx + c_ring[qq][0]];
+            SC[k >> 7][k & 127] = (uint16_t)(0x100 | corner_score16_pk(v, ring, threshold));
+        }
+    }
+    // tile mask from the previous frame's feature boxes (as fast_detect_kernel)
+    if (boxes) {
+        const int nb = (h + 15) / 16, ncl = (w + 63) / 64;
+        const int* __restrict__ cells = B.box_band + seq * (size_t)(nb * ncl + 1);
+        const int b0 = max(0, (int)floorf((y0 - B.box_half - 1.f) / 16.f));
+        const int b1 = min(nb - 1, (int)floorf((y0 + FD_TY + B.box_half + 1.f) / 16.f));
+        const int cb0 = max(0, (int)floorf((x0 - B.box_half - 1.f) / 64.f));
+        const int cb1 = min(ncl - 1, (int)floorf((x0 + FD_TX + B.box_half + 1.f) / 64.f));
+        const float* __restrict__ pts = B.box_binned + 2 * seq * (size_t)B.box_stride;
+        for (int bq = b0; bq <= b1; bq++)
+            for (int i = cells[bq * ncl + cb0] + tid, i1 = cells[bq * ncl + cb1 + 1]; i < i1; i += 256) {
+                const float px = pts[2 * i], py = pts[2 * i + 1];
+                const int xa = (int)__builtin_rintf(px - B.box_half), ya = (int)__builtin_rintf(py - B.box_half);
+                const int xb = (int)__builtin_rintf(px + B.box_half), yb = (int)__builtin_rintf(py + B.box_half);
+                int xl = min(xa, xb), xr = max(xa, xb), yt = min(ya, yb), yd = max(ya, yb);
+                xl = max(xl, max(0, x0));
+                xr = min(xr, min(w - 1, x0 + FD_TX - 1));
+                yt = max(yt, max(0, y0));
+                yd = min(yd, min(h - 1, y0 + FD_TY - 1));
+                if (xl > xr || yt > yd) continue;
+                const int c0 = xl - x0, c1 = xr - x0;  // 0..63
+                const unsigned long long span =
+                    (c1 - c0 == 63) ? ~0ull : (((1ull << (c1 - c0 + 1)) - 1ull) << c0);
+                for (int y = yt; y <= yd; y++) atomicAnd(&TM[y - y0], ~span);
+            }
+    }
+    __syncthreads();
+    // ---- NMS + output: wave wv owns tile rows 8 wv .. 8 wv + 7 (score rows 8 wv ..
+    // 8 wv + 9), lane = column (xs = lane + 4) ----
+    const int x = x0 + lane;
+    const uint8_t* __restrict__ mask = B.mask ? B.mask + seq * B.npx : nullptr;
+    constexpr int RW = FD_TY / 4;
+    unsigned cen[RW + 2];
+    int lr[RW + 2], hm[RW + 2];
+#pragma unroll
+    for (int i = 0; i < RW + 2; i++) {
+        const int sr = wv * RW + i;
+        cen[i] = SC[sr][lane + 4];
+        lr[i] = max((int)(SC[sr][lane + 3] & 0xFF), (int)(SC[sr][lane + 5] & 0xFF));
+        hm[i] = max((int)(cen[i] & 0xFF), lr[i]);
+    }
+#pragma unroll
+    for (int i = 0; i < RW; i++) {
+        const int r = wv * RW + i;
+        const int y = y0 + r;
+        const unsigned v = cen[i + 1];
+        bool keep = (v & 0x100) != 0 && x < w && y < h;
+        if (nonmax) keep = keep && (int)(v & 0xFF) > max(max(hm[i], hm[i + 2]), lr[i + 1]);
+        if (mask) {
+            const int yy = y < h ? y : h - 1, xx = x < w ? x : w - 1;
+            keep = keep && mask[(size_t)yy * w + xx] != 0;
+        }
+        if (boxes) keep = keep && ((TM[r] >> lane) & 1ull);
+        const unsigned long long bal = __ballot(keep);
+        if (lane == 0) RB[r] = bal;
+    }
+    __syncthreads();
+    if (tid < FD_TY && y0 + tid < h) {
+        const unsigned long long bal = RB[tid];
+        const size_t row = seq * h + y0 + tid;
+        B.bits[row * B.nseg + blockIdx.x] = bal;
+        if (bal) atomicAdd(&B.rowcnt[row], __popcll(bal));
+    }
+}
+
 // Box centres of one sequence binned by cell (16-row band x 64-column tile):
 // counting sort, one block per sequence; order within a cell is irrelevant
 // (the mask is an AND of boxes).
@@ -764,14 +973,16 @@ hipError_t launch_fast_detect(const FastDetBatch& b, int nseq, int w, int h, int
         if (e != hipSuccess) return e;
     }
     dim3 grid((w + FD_TX - 1) / FD_TX, (h + FD_TY - 1) / FD_TY, nseq);
-    static const int ver = [] {
-        const char* e = std::getenv("SVO_FAST_V");
-        return e ? std::atoi(e) : 2;
-    }();
+    // detection form, read per call (the parity tests switch it): 1 block queues,
+    // 2 wave queues, 3 wave queues + SWAR pre-test + register NMS
+    const char* ev = std::getenv("SVO_FAST_V");
+    const int ver = ev ? std::atoi(ev) : 2;
     if (ver == 1)
         hipLaunchKernelGGL(fast_detect_kernel, grid, dim3(256), 0, st, b, threshold, nonmax);
-    else
+    else if (ver == 2)
         hipLaunchKernelGGL(fast_detect_w_kernel, grid, dim3(256), 0, st, b, threshold, nonmax);
+    else
+        hipLaunchKernelGGL(fast_detect_s_kernel, grid, dim3(256), 0, st, b, threshold, nonmax);
     hipLaunchKernelGGL(fast_scan_kernel, dim3(nseq), dim3(1024), 0, st, b, h);
     hipLaunchKernelGGL(fast_emit_kernel, dim3(h, nseq), dim3(64), 0, st, b, threshold, nonmax);
     return hipGetLastError();

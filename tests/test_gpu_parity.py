@@ -42,6 +42,14 @@ def test_pyramid_bit_exact(ctx, wh):
 
 
 # ------------------------------------------------------------------ FAST
+@pytest.fixture(params=["block-queue", "wave-queue", "swar"])
+def fast_kernel(request, monkeypatch):
+    """Every fused detection form (SVO_FAST_V=1 fast_detect_kernel, 2
+    fast_detect_w_kernel, 3 fast_detect_s_kernel) must give the oracle's keypoints."""
+    monkeypatch.setenv("SVO_FAST_V", {"block-queue": "1", "wave-queue": "2", "swar": "3"}[request.param])
+    return request.param
+
+
 @pytest.mark.parametrize("wh,seed", [((1241, 376), 0), ((160, 120), 3), ((64, 48), 5), ((3840, 2160), 1)])
 def test_fast_score_map_bit_exact(ctx, wh, seed):
     sc, A, _ = frames(*wh, seed=seed)
@@ -55,7 +63,7 @@ def test_fast_score_map_bit_exact(ctx, wh, seed):
 
 @pytest.mark.parametrize("nonmax", [True, False])
 @pytest.mark.parametrize("wh,seed", [((1241, 376), 0), ((160, 120), 2), ((1920, 1080), 4)])
-def test_fast_keypoints_identical(ctx, wh, seed, nonmax):
+def test_fast_keypoints_identical(ctx, wh, seed, nonmax, fast_kernel):
     sc, A, _ = frames(*wh, seed=seed)
     g = ctx.image(A, 0)
     det = S.FastFeatureDetector.create(ctx, 20, nonmax)
@@ -65,7 +73,7 @@ def test_fast_keypoints_identical(ctx, wh, seed, nonmax):
     assert np.array_equal(got, ref)
 
 
-def test_fast_with_mask_identical(ctx):
+def test_fast_with_mask_identical(ctx, fast_kernel):
     sc, A, _ = frames(1241, 376, seed=0)
     g = ctx.image(A, 0)
     prev = O.fast(A, 20, True)[::3, :2] + np.float32(0.37)
@@ -83,7 +91,7 @@ def test_mask_boxes_edges(ctx):
     assert np.array_equal(ctx.mask_boxes(64, 48, pts, 10.0), O.mask_boxes(64, 48, pts, 10.0))
 
 
-def test_fast_threshold_extremes(ctx):
+def test_fast_threshold_extremes(ctx, fast_kernel):
     sc, A, _ = frames(160, 120, seed=9)
     g = ctx.image(A, 0)
     for t in (0, 1, 254, 255, 300, -5):
