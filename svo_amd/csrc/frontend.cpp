@@ -653,11 +653,10 @@ int svo_frontend_create(svo_ctx* ctx, const svo_frontend_config* cfg, svo_fronte
     for (auto& e : fe->ev) (void)hipEventCreate(&e);
     // pipeline slices: contiguous, near-equal sequence ranges
     {
-        // slices > 1 only pay off when the host RANSAC outweighs the LK tail
-        // they hide; measured on MI355X one slice is fastest
-        // default: two prioritised slices for large batches (slice 0's RANSAC
-        // overlaps slice 1's LK; measured +2 % at 64 sequences), one otherwise
-        int G = c.groups > 0 ? c.groups : (S >= 32 ? 2 : 1);
+        // default one slice: two prioritised slices (slice 0's RANSAC overlapping
+        // slice 1's LK) measured within noise of one (+1 % over 3 runs at 64
+        // sequences), and one slice keeps LK a single launch per step
+        int G = c.groups > 0 ? c.groups : 1;
         G = std::max(1, std::min(G, S));
         fe->G = G;
         fe->g0.resize(G);

@@ -1028,6 +1028,24 @@ __device__ __forceinline__ void strip_setup(const unsigned* P, const u32x2a4* D,
     }
 }
 
+// strip_setup, returning per-lane sums c1 += I.Ix, c2 += I.Iy over the strip's
+// pixels instead of the I pairs: sum (J - I) G = sum J G - sum I G exactly
+// (int32 wrap-around arithmetic; the per-lane total is the same bounded value),
+// so an iteration starts its b sums at (-c1, -c2) and needs no J - I subtraction.
+template <int NR>
+__device__ __forceinline__ void strip_setup_c(const unsigned* P, const u32x2a4* D, unsigned IW0, unsigned IW1,
+                                              unsigned GW0, unsigned GW1, unsigned* GX, unsigned* GY, int& a11,
+                                              int& a12, int& a22, int& c1, int& c2) {
+    constexpr int NP = (NR + 1) / 2;
+    unsigned I2[NP];
+    strip_setup<NR>(P, D, IW0, IW1, GW0, GW1, I2, GX, GY, a11, a12, a22);
+#pragma unroll
+    for (int m = 0; m < NP; m++) {
+        c1 = sdot2(I2[m], GX[m], c1);
+        c2 = sdot2(I2[m], GY[m], c2);
+    }
+}
+
 // A level's global loads of a wave are issued back to back (both features'
 // next-image staging dwords, both strips' prev pairs and derivative pairs), then
 // consumed. Staging: lanes own (row, dword) slots, LPR lanes per row (the last
@@ -1493,8 +1511,9 @@ __global__ __launch_bounds__(64, MINW) void lk_multi_kernel(LKBatch B, LKDev p) 
 
         int jx0 = ufloor(nextx - halfWx) - QJM, jy0 = ufloor(nexty - halfWy) - QJM;
         int jxa = jx0 & ~3;
-        unsigned I2[K][NP], GX[K][NP], GY[K][NP];
+        unsigned GX[K][NP], GY[K][NP];
         int asum[3] = {0, 0, 0};
+        int csum[2] = {0, 0};  // sum I.Ix, I.Iy over the lane's strips
         {
             // branch-free reads (padded levels); an inactive group (or one whose
             // region lies beyond the padding: its first bounds test deactivates
@@ -1560,8 +1579,8 @@ __global__ __launch_bounds__(64, MINW) void lk_multi_kernel(LKBatch B, LKDev p) 
 #pragma unroll
                 for (int kk = 0; kk < KK; kk++) {
                     const int k = k0 + kk;
-                    strip_setup<NR>(P[kk], D[kk], IW0, IW1, sreal[k] ? IW0 : 0u, sreal[k] ? IW1 : 0u, I2[k],
-                                    GX[k], GY[k], asum[0], asum[1], asum[2]);
+                    strip_setup_c<NR>(P[kk], D[kk], IW0, IW1, sreal[k] ? IW0 : 0u, sreal[k] ? IW1 : 0u, GX[k],
+                                      GY[k], asum[0], asum[1], asum[2], csum[0], csum[1]);
                 }
             }
         }
@@ -1615,7 +1634,7 @@ __global__ __launch_bounds__(64, MINW) void lk_multi_kernel(LKBatch B, LKDev p) 
             const int w10 = uround((1.f - aa) * bb * (1 << W_BITS));
             const int w11 = (1 << W_BITS) - w00 - w01 - w10;
             const unsigned W0 = pack16(w00, w01), W1 = pack16(w10, w11);
-            int bsum[2] = {0, 0};
+            int bsum[2] = {-csum[0], -csum[1]};
             {
                 // an inactive group reads inside its own region (results unused)
                 const int ro = lact ? iny - jy0 : 0, co = lact ? inx - jxa : 0;
@@ -1633,9 +1652,9 @@ __global__ __launch_bounds__(64, MINW) void lk_multi_kernel(LKBatch B, LKDev p) 
                         jv[r] = sdot2(q[r], W0, sdot2_r(q[r + 1], W1, rnd_j));
 #pragma unroll
                     for (int m = 0; m < NP; m++) {
-                        const unsigned dd = pk_sub16(hi16x2(jv[2 * m], jv[2 * m + 1]), I2[k][m]);
-                        bsum[0] = sdot2(dd, GX[k][m], bsum[0]);
-                        bsum[1] = sdot2(dd, GY[k][m], bsum[1]);
+                        const unsigned jj = hi16x2(jv[2 * m], jv[2 * m + 1]);  // J; the I part is in csum
+                        bsum[0] = sdot2(jj, GX[k][m], bsum[0]);
+                        bsum[1] = sdot2(jj, GY[k][m], bsum[1]);
                     }
                 }
             }
