@@ -591,6 +591,172 @@ __global__ __launch_bounds__(256) void fast_detect_w_kernel(FastDetBatch B, int 
     }
 }
 
+// ---- queue-NMS form (SVO_FAST_V=4): as fast_detect_w_kernel up to the scores;
+// NMS then visits only the wave's corners instead of every pixel of its rows
+// (the dense pass was ~30 % of the kernel's VALU), and the box mask is applied to
+// the finished row words. Same outputs. ----
+__global__ __launch_bounds__(256) void fast_detect_q_kernel(FastDetBatch B, int threshold, int nonmax) {
+    const ImgLevel L = B.descs[blockIdx.z].lv[0];
+    const int w = L.w, h = L.h;
+    const int x0 = blockIdx.x * FD_TX, y0 = blockIdx.y * FD_TY;
+    const size_t seq = blockIdx.z;
+    __shared__ __attribute__((aligned(16))) uint8_t T[FD_IH][FD_IW];
+    __shared__ uint16_t SC[FD_SH][FD_SW + 2];  // bit 8: corner, low byte: score
+    __shared__ uint16_t CQ[4][FW_Q];
+    __shared__ unsigned long long TM[FD_TY];
+    __shared__ unsigned long long RB[FD_TY];
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const bool inside = x0 >= 4 && y0 >= 4 && x0 - 4 + FD_IW <= w && y0 - 4 + FD_IH <= h;
+    if (inside) {
+        for (int k = tid; k < FD_IH * (FD_IW / 4); k += 256) {
+            const int r = k / (FD_IW / 4), c4 = k - r * (FD_IW / 4);
+            const uint8_t* src = L.data + (size_t)(y0 - 4 + r) * L.pitch + (x0 - 4 + 4 * c4);
+            *reinterpret_cast<uint32_t*>(&T[r][4 * c4]) = *reinterpret_cast<const uint32_t*>(src);
+        }
+    } else {
+        for (int k = tid; k < FD_IH * FD_IW; k += 256) {
+            const int r = k / FD_IW, c = k - r * FD_IW;
+            const int y = y0 - 4 + r, x = x0 - 4 + c;
+            T[r][c] = ((unsigned)y < (unsigned)h && (unsigned)x < (unsigned)w) ? L.data[(size_t)y * L.pitch + x] : 0;
+        }
+    }
+    const bool boxes = B.box_pts != nullptr;
+    if (boxes && tid < FD_TY) TM[tid] = ~0ull;
+    if (tid < FD_TY) RB[tid] = 0ull;
+    __syncthreads();
+    const int hi_t = threshold, lo_t = -threshold;
+    // ---- A0: compass pre-test of this wave's rows sr = wv, wv + 4, ... (lane -> column
+    // sc = lane + 1), then the two halo columns of those rows; queue (sr << 7 | sc) ----
+    uint16_t* q = CQ[wv];
+    int nq = 0;
+    auto pretest = [&](int sr, int sc, bool ok) {
+        const int y = y0 - 1 + sr, x = x0 - 1 + sc;
+        bool cand = false;
+        if (ok && x >= 3 && x < w - 3 && y >= 3 && y < h - 3) {
+            const int ty = sr + 3, tx = sc + 3;
+            const int v = T[ty][tx], hi = v + hi_t, lo = v + lo_t;
+            const int p0 = T[ty + 3][tx], p8 = T[ty - 3][tx], p4 = T[ty][tx + 3], p12 = T[ty][tx - 3];
+            const bool bright = (p0 > hi || p8 > hi) && (p4 > hi || p12 > hi);
+            const bool dark = (p0 < lo || p8 < lo) && (p4 < lo || p12 < lo);
+            cand = bright || dark;
+        }
+        const unsigned long long bal = __ballot(cand);
+        if (cand) q[nq + __popcll(bal & ((1ull << lane) - 1ull))] = (uint16_t)((sr << 7) | sc);
+        nq += __popcll(bal);
+    };
+    for (int sr = wv; sr < FD_SH; sr += 4) {
+        SC[sr][lane + 1] = 0;
+        if (lane < 2) SC[sr][lane * 65] = 0;
+        pretest(sr, lane + 1, true);
+    }
+    {
+        // halo columns 0 and 65 of the wave's rows (<= 9 rows -> 18 positions)
+        const int nr = (FD_SH - wv + 3) / 4;
+        const int sr = wv + 4 * (lane >> 1), sc = (lane & 1) * 65;
+        pretest(sr, sc, lane < 2 * nr);
+    }
+    // ---- A1: full segment test of the queue, compacted in place to the corners ----
+    int nc = 0;
+    for (int base = 0; base < nq; base += 64) {
+        const int i = base + lane;
+        bool corner = false;
+        int k = 0;
+        if (i < nq) {
+            k = q[i];
+            const int sr = k >> 7, sc = k & 127;
+            const int ty = sr + 3, tx = sc + 3;
+            const int v = T[ty][tx];
+            // packed compare: low half r - (v + t + 1) (sign: not brighter), high half
+            // r - (v - t) (sign: darker); sign bits gathered to bit q and 16 + q
+            const fs16x2 th = {(short)(v + threshold + 1), (short)(v - threshold)};
+            unsigned acc = 0;
+#pragma unroll
+            for (int qq = 0; qq < 16; qq++) {
+                const int rv = T[ty + c_ring[qq][1]][tx + c_ring[qq][0]];
+                const fs16x2 r2 = {(short)rv, (short)rv};
+                const unsigned sg = as_u(r2 - th);
+                acc |= (sg >> (15 - qq)) & (0x00010001u << qq);
+            }
+            corner = run9(~acc & 0xFFFFu) || run9(acc >> 16);
+        }
+        const unsigned long long bal = __ballot(corner);
+        if (corner) {
+            const int sr = k >> 7, sc = k & 127;
+            SC[sr][sc] = 0x100;
+            q[nc + __popcll(bal & ((1ull << lane) - 1ull))] = (uint16_t)k;  // index <= i: already read
+        }
+        nc += __popcll(bal);
+    }
+    // ---- B: cornerScore of the corners (NMS only) ----
+    if (nonmax) {
+        for (int i = lane; i < nc; i += 64) {
+            const int k = q[i];
+            const int sr = k >> 7, sc = k & 127;
+            const int ty = sr + 3, tx = sc + 3;
+            const int v = T[ty][tx];
+            int ring[16];
+#pragma unroll
+            for (int qq = 0; qq < 16; qq++) ring[qq] = T[ty + c_ring[qq][1]][tx + c_ring[qq][0]];
+            SC[sr][sc] = (uint16_t)(0x100 | corner_score16_pk(v, ring, threshold));
+        }
+    }
+    // tile mask from the previous frame's feature boxes (as fast_detect_kernel)
+    if (boxes) {
+        const int nb = (h + 15) / 16, ncl = (w + 63) / 64;
+        const int* __restrict__ cells = B.box_band + seq * (size_t)(nb * ncl + 1);
+        const int b0 = max(0, (int)floorf((y0 - B.box_half - 1.f) / 16.f));
+        const int b1 = min(nb - 1, (int)floorf((y0 + FD_TY + B.box_half + 1.f) / 16.f));
+        const int cb0 = max(0, (int)floorf((x0 - B.box_half - 1.f) / 64.f));
+        const int cb1 = min(ncl - 1, (int)floorf((x0 + FD_TX + B.box_half + 1.f) / 64.f));
+        const float* __restrict__ pts = B.box_binned + 2 * seq * (size_t)B.box_stride;
+        for (int bq = b0; bq <= b1; bq++)
+            for (int i = cells[bq * ncl + cb0] + tid, i1 = cells[bq * ncl + cb1 + 1]; i < i1; i += 256) {
+                const float px = pts[2 * i], py = pts[2 * i + 1];
+                const int xa = (int)__builtin_rintf(px - B.box_half), ya = (int)__builtin_rintf(py - B.box_half);
+                const int xb = (int)__builtin_rintf(px + B.box_half), yb = (int)__builtin_rintf(py + B.box_half);
+                int xl = min(xa, xb), xr = max(xa, xb), yt = min(ya, yb), yd = max(ya, yb);
+                xl = max(xl, max(0, x0));
+                xr = min(xr, min(w - 1, x0 + FD_TX - 1));
+                yt = max(yt, max(0, y0));
+                yd = min(yd, min(h - 1, y0 + FD_TY - 1));
+                if (xl > xr || yt > yd) continue;
+                const int c0 = xl - x0, c1 = xr - x0;  // 0..63
+                const unsigned long long span =
+                    (c1 - c0 == 63) ? ~0ull : (((1ull << (c1 - c0 + 1)) - 1ull) << c0);
+                for (int y = yt; y <= yd; y++) atomicAnd(&TM[y - y0], ~span);
+            }
+    }
+    __syncthreads();
+    // NMS over this wave's corners only (a few % of the pixels): strict maximum over
+    // the 8 neighbours' score bytes (non-corners score 0), the host mask per corner,
+    // keep bits OR-ed into the row words
+    const uint8_t* __restrict__ mask = B.mask ? B.mask + seq * B.npx : nullptr;
+    for (int i = lane; i < nc; i += 64) {
+        const int k = q[i];
+        const int sr = k >> 7, sc = k & 127;
+        if (sr < 1 || sr > FD_TY || sc < 1 || sc > FD_TX) continue;  // halo: scores only
+        const int x = x0 + sc - 1, y = y0 + sr - 1;
+        bool keep = x < w && y < h;
+        if (nonmax) {
+            auto sb = [&](int y2, int x2) { return (int)reinterpret_cast<const uint8_t*>(&SC[y2][x2])[0]; };
+            int m = max(max(sb(sr, sc - 1), sb(sr, sc + 1)), sb(sr - 1, sc - 1));
+            m = max(max(m, sb(sr - 1, sc)), sb(sr - 1, sc + 1));
+            m = max(max(m, sb(sr + 1, sc - 1)), sb(sr + 1, sc));
+            m = max(m, sb(sr + 1, sc + 1));
+            keep = keep && sb(sr, sc) > m;
+        }
+        if (mask && keep) keep = mask[(size_t)y * w + x] != 0;
+        if (keep) atomicOr(&RB[sr - 1], 1ull << (sc - 1));
+    }
+    __syncthreads();
+    if (tid < FD_TY && y0 + tid < h) {
+        const unsigned long long bal = RB[tid] & (boxes ? TM[tid] : ~0ull);
+        const size_t row = seq * h + y0 + tid;
+        B.bits[row * B.nseg + blockIdx.x] = bal;
+        if (bal) atomicAdd(&B.rowcnt[row], __popcll(bal));
+    }
+}
+
 // ---- SWAR form (SVO_FAST_V=3): as fast_detect_w_kernel, with the compass
 // pre-test on 4 pixels per lane and a register NMS. The staged tile starts 8
 // pixels left of the tile (T column c <-> x = x0 - 8 + c) and the score region
@@ -974,15 +1140,18 @@ hipError_t launch_fast_detect(const FastDetBatch& b, int nseq, int w, int h, int
     }
     dim3 grid((w + FD_TX - 1) / FD_TX, (h + FD_TY - 1) / FD_TY, nseq);
     // detection form, read per call (the parity tests switch it): 1 block queues,
-    // 2 wave queues, 3 wave queues + SWAR pre-test + register NMS
+    // 2 wave queues, 3 wave queues + SWAR pre-test + register NMS, 4 wave queues +
+    // NMS over the corner queue
     const char* ev = std::getenv("SVO_FAST_V");
-    const int ver = ev ? std::atoi(ev) : 2;
+    const int ver = ev ? std::atoi(ev) : 4;
     if (ver == 1)
         hipLaunchKernelGGL(fast_detect_kernel, grid, dim3(256), 0, st, b, threshold, nonmax);
     else if (ver == 2)
         hipLaunchKernelGGL(fast_detect_w_kernel, grid, dim3(256), 0, st, b, threshold, nonmax);
-    else
+    else if (ver == 3)
         hipLaunchKernelGGL(fast_detect_s_kernel, grid, dim3(256), 0, st, b, threshold, nonmax);
+    else
+        hipLaunchKernelGGL(fast_detect_q_kernel, grid, dim3(256), 0, st, b, threshold, nonmax);
     hipLaunchKernelGGL(fast_scan_kernel, dim3(nseq), dim3(1024), 0, st, b, h);
     hipLaunchKernelGGL(fast_emit_kernel, dim3(h, nseq), dim3(64), 0, st, b, threshold, nonmax);
     return hipGetLastError();

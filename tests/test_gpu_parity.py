@@ -42,11 +42,12 @@ def test_pyramid_bit_exact(ctx, wh):
 
 
 # ------------------------------------------------------------------ FAST
-@pytest.fixture(params=["block-queue", "wave-queue", "swar"])
+@pytest.fixture(params=["block-queue", "wave-queue", "swar", "queue-nms"])
 def fast_kernel(request, monkeypatch):
     """Every fused detection form (SVO_FAST_V=1 fast_detect_kernel, 2
-    fast_detect_w_kernel, 3 fast_detect_s_kernel) must give the oracle's keypoints."""
-    monkeypatch.setenv("SVO_FAST_V", {"block-queue": "1", "wave-queue": "2", "swar": "3"}[request.param])
+    fast_detect_w_kernel, 3 fast_detect_s_kernel, 4 fast_detect_q_kernel) must give
+    the oracle's keypoints."""
+    monkeypatch.setenv("SVO_FAST_V", {"block-queue": "1", "wave-queue": "2", "swar": "3", "queue-nms": "4"}[request.param])
     return request.param
 
 
