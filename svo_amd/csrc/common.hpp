@@ -197,7 +197,17 @@ struct LKBatch {
     int* iters;   // nullable
     const int* counts;  // nullable
     int n, cap;
+    // nullable (lk_multi_kernel only): streamed hand-off -- each block writes its
+    // next_xy / iters (iters | status << 30) write-through (sc1), drains its stores
+    // and then stores stamp to done[seq * done_stride + blockIdx.x] (sc1), so a
+    // consumer can take a sequence as soon as all its blocks' flags show the stamp.
+    // Flags, not a counter: one agent-scope atomic add per block cost LK +27 %.
+    int* done = nullptr;
+    int done_stride = 0;
+    int stamp = 0;
 };
+// LK block flags one per 128-B line (kFlagSpread ints apart)
+constexpr int kFlagSpread = 32;
 hipError_t launch_lk(const LKBatch& b, int nseq, int max_n, const LKParams& p, hipStream_t st);
 bool lk_supported(int win_w, int win_h);
 

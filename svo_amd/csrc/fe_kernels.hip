@@ -174,7 +174,7 @@ constexpr int kFeBlock = 256;
 
 // Stable compaction of one sequence by a keep predicate, by a kFeBlock-thread
 // block: keep(i) for i < n, kept entries of xy / mid moved to their rank.
-template <typename Keep>
+template <bool SC1 = false, typename Keep>
 __device__ __forceinline__ int block_compact(int n, Keep keep, const float* __restrict__ xy_in,
                                              const int* __restrict__ mid_in, float* __restrict__ xy_out,
                                              int* __restrict__ mid_out, int* wsum, int* base_s) {
@@ -192,8 +192,15 @@ __device__ __forceinline__ int block_compact(int n, Keep keep, const float* __re
         float x = 0.f, y = 0.f;
         int m = 0;
         if (k) {
-            x = xy_in[2 * i];
-            y = xy_in[2 * i + 1];
+            if (SC1) {  // written write-through by a still-running producer (streamed LK)
+                const unsigned long long v = __hip_atomic_load(
+                    reinterpret_cast<const unsigned long long*>(xy_in + 2 * i), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                x = __uint_as_float((unsigned)v);
+                y = __uint_as_float((unsigned)(v >> 32));
+            } else {
+                x = xy_in[2 * i];
+                y = xy_in[2 * i + 1];
+            }
             m = mid_in[i];
         }
         __syncthreads();  // every read of this chunk before any write (in place allowed)
@@ -233,9 +240,46 @@ __global__ __launch_bounds__(kFeBlock) void post_lk_kernel(PostLkBatch B) {
     const int n_in = B.n_in[s];
     const uint8_t* __restrict__ st = B.status + o;
     long long it = 0;
-    for (int i = tid; i < n_in; i += kFeBlock) it += B.iters[o + i];
-    const int n = block_compact(n_in, [&](int i) { return st[i] != 0; }, B.xy_in + 2 * o, B.mid_in + o,
-                                B.xy_out + 2 * o, B.mid_out + o, wsum, &base_s);
+    int n;
+    if (B.done) {
+        // streamed: wait for this sequence's LK blocks (bounded: a lost producer
+        // ends the wait after ~1 s and raises h_fail instead of hanging the GPU)
+        if (tid < 64) {  // wave 0 polls every block flag of the sequence (sc1 loads)
+            const int need = (n_in + B.fpw - 1) / B.fpw;
+            const int* __restrict__ fl = B.done + (size_t)s * B.done_stride * kFlagSpread;
+            int spins = 0;
+            bool fail = false;
+            // cheap probe first: the sequence's last block (dispatched last) -- one
+            // address, one request per poll; a full sweep of every flag only then
+            while (need > 0 && !fail &&
+                   __hip_atomic_load(fl + (size_t)(need - 1) * kFlagSpread, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) !=
+                       B.lk_stamp) {
+                __builtin_amdgcn_s_sleep(32);
+                fail = ++spins > (1 << 20);
+            }
+            for (;;) {
+                bool ok = true;
+                for (int i = tid; i < need; i += 64)
+                    ok &= __hip_atomic_load(fl + (size_t)i * kFlagSpread, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+                          B.lk_stamp;
+                if (__all(ok) || fail) break;
+                __builtin_amdgcn_s_sleep(4);
+                fail = ++spins > (1 << 20);
+            }
+            if (fail && tid == 0) __hip_atomic_store(B.h_fail, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+        __syncthreads();
+        const int* __restrict__ itw = B.iters + o;
+        for (int i = tid; i < n_in; i += kFeBlock)
+            it += __hip_atomic_load(itw + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & ((1 << 30) - 1);
+        n = block_compact<true>(
+            n_in, [&](int i) { return (__hip_atomic_load(itw + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >> 30) != 0; },
+            B.xy_in + 2 * o, B.mid_in + o, B.xy_out + 2 * o, B.mid_out + o, wsum, &base_s);
+    } else {
+        for (int i = tid; i < n_in; i += kFeBlock) it += B.iters[o + i];
+        n = block_compact(n_in, [&](int i) { return st[i] != 0; }, B.xy_in + 2 * o, B.mid_in + o, B.xy_out + 2 * o,
+                          B.mid_out + o, wsum, &base_s);
+    }
     for (int off = 32; off > 0; off >>= 1) it += __shfl_xor(it, off);
     if (lane == 0) atomicAdd(&it_s, (unsigned long long)it);
     // wave 0 lane 0 replays the RANSAC draws (they depend only on n) while the
@@ -283,6 +327,16 @@ __global__ __launch_bounds__(kFeBlock) void post_lk_kernel(PostLkBatch B) {
             h[3 * i + 2] = (float)X[2];
             h[15 + 2 * i] = xy[2 * p];
             h[15 + 2 * i + 1] = xy[2 * p + 1];
+        }
+    }
+    if (B.h_ready) {
+        // publish to the host: every wave's stores drained, then one system release
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (tid == 0) {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __hip_atomic_store(B.h_ready + s, B.stamp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         }
     }
 }

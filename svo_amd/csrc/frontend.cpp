@@ -208,6 +208,17 @@ struct svo_frontend {
     bool full_queued = false;
     int fit_parity = 0;  // step parity whose RANSAC results the pending fits refine
     hipEvent_t ev_counts = nullptr;  // the step's feature counts on the host
+    // streamed post-LK (SVO_FE_STREAM=1, one slice, lk_multi_kernel): post_lk is
+    // queued before LK on the copy stream and takes each sequence as soon as its LK
+    // blocks are counted in d_done; the host starts a sequence's RANSAC hypotheses
+    // once h_ready[s] shows the step's stamp, while LK still runs for later ones
+    bool stream_post = false, sp_active = false;
+    int stream_mode = 0;  // 2: the same hand-off, post_lk queued after LK (diagnostic)
+    int* d_done = nullptr;  // [s][done_stride] LK block flags (device)
+    int done_stride = 0, lk_stamp = 0;
+    int* h_ready = nullptr;  // [s] host-coherent stamps
+    int* h_fail = nullptr;   // host-coherent: a streamed wait timed out
+    hipEvent_t ev_prelk = nullptr;
     Pool* pool = nullptr;
     // pipeline: slices of the batch [g0[g], g0[g] + gn[g]) on their own streams
     int G = 1;
@@ -595,6 +606,7 @@ int svo_frontend_create(svo_ctx* ctx, const svo_frontend_config* cfg, svo_fronte
         add(sizeof(uint32_t) * (size_t)S * fe->WORDS);
         add(sizeof(uint32_t) * (size_t)S * fe->WORDS);
         add(sizeof(double) * 60 * (size_t)S);
+        add(sizeof(int) * ((size_t)S + 1));
         add(1024);
         if (hipHostMalloc(&fe->zout, zb, hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess) {
             fe->zout = nullptr;
@@ -612,6 +624,10 @@ int svo_frontend_create(svo_ctx* ctx, const svo_frontend_config* cfg, svo_fronte
         fe->h_best_b[1] = carve<uint32_t>(p, (size_t)S * fe->WORDS);
         fe->h_best = fe->h_best_b[0];
         fe->h_stats = carve<double>(p, 60 * (size_t)S);
+        fe->h_ready = carve<int>(p, (size_t)S + 1);
+        fe->h_fail = fe->h_ready + S;
+        for (int s = 0; s < S; s++) fe->h_ready[s] = -1;
+        *fe->h_fail = 0;
     }
     // derivative pyramids of three frames of every sequence (t - 1: LK's prev,
     // t, and t + 1, built beside LK(t))
@@ -645,6 +661,18 @@ int svo_frontend_create(svo_ctx* ctx, const svo_frontend_config* cfg, svo_fronte
         fe->pyr_early = !(pe && pe[0] == '0');
         const char* fe_ = std::getenv("SVO_FE_FAST_EARLY");
         fe->fast_early = !(fe_ && fe_[0] == '0');
+        const char* sp = std::getenv("SVO_FE_STREAM");
+        fe->stream_post = sp && (sp[0] == '1' || sp[0] == '2');
+        fe->stream_mode = sp ? std::atoi(sp) : 0;
+    }
+    // (on the context stream: a first use of the null stream would take a fifth
+    // hardware queue and serialise the step's streams)
+    fe->done_stride = ((fe->CAP + 3) / 4 + 63) & ~63;
+    if (hipMalloc(&fe->d_done, sizeof(int) * kFlagSpread * (size_t)fe->done_stride * S) != hipSuccess ||
+        hipMemsetAsync(fe->d_done, 0, sizeof(int) * kFlagSpread * (size_t)fe->done_stride * S, ctx->stream) !=
+            hipSuccess) {
+        svo_frontend_destroy(fe);
+        return set_error(ctx, SVO_ERR_HIP, "svo_frontend_create: counter alloc");
     }
     fe->pose.assign((size_t)S * 6, 0.0);
     int nt = c.host_threads > 0 ? c.host_threads : (int)std::thread::hardware_concurrency();
@@ -695,6 +723,7 @@ int svo_frontend_create(svo_ctx* ctx, const svo_frontend_config* cfg, svo_fronte
         for (auto& e : fe->ev_full_b) (void)hipEventCreateWithFlags(&e, hipEventDisableTiming);
         fe->ev_full = fe->ev_full_b[0];
         (void)hipEventCreateWithFlags(&fe->ev_counts, hipEventDisableTiming);
+        (void)hipEventCreateWithFlags(&fe->ev_prelk, hipEventDisableTiming);
         // 4 hardware queues: with several slices the copy stream's work shares the
         // pyramid stream
         if (G > 1) {
@@ -747,6 +776,8 @@ void svo_frontend_destroy(svo_frontend* fe) {
     for (auto& e : fe->ev_full_b)
         if (e) (void)hipEventDestroy(e);
     if (fe->ev_counts) (void)hipEventDestroy(fe->ev_counts);
+    if (fe->ev_prelk) (void)hipEventDestroy(fe->ev_prelk);
+    if (fe->d_done) (void)hipFree(fe->d_done);
     delete fe;
 }
 
@@ -843,6 +874,17 @@ int svo_frontend_init(svo_frontend* fe, int t0) {
 // frame t+1's pyramid, compaction / gather / RANSAC subsets and their D2H, FAST.
 // svo_frontend_step enqueues the next step's first half right after its own
 // tail, so the GPU goes on with LK while the caller is between steps.
+// post_lk's arguments for the sequences [a, a + n) of this step's parity buffers
+static PostLkBatch fe_post_lk_batch(svo_frontend* fe, int a) {
+    const int CAP = fe->CAP;
+    const size_t sfl = (size_t)kSampleFloats * kRansacPrefetch;
+    return PostLkBatch{fe->nA + a, fe->status + (size_t)a * CAP, fe->next_xy + 2 * (size_t)a * CAP,
+                       fe->midA + (size_t)a * CAP, fe->iters + (size_t)a * CAP, fe->xyB + 2 * (size_t)a * CAP,
+                       fe->midB + (size_t)a * CAP, fe->nB + a, fe->map + 3 * (size_t)a * fe->MAPCAP, fe->MAPCAP,
+                       fe->obj + 3 * (size_t)a * CAP, CAP, kRansacPrefetch, fe->h_nB + a, fe->h_itsum + a,
+                       fe->h_samp + sfl * a};
+}
+
 static int fe_front_lk(svo_frontend* fe, int t) {
     svo_ctx* ctx = fe->ctx;
     hipStream_t st0 = ctx->stream;
@@ -908,6 +950,8 @@ static int fe_front_lk(svo_frontend* fe, int t) {
         }();
         lp.multi = multi;
     }
+    // streamed post-LK: one slice and the four-per-wave kernel (the one that counts)
+    fe->sp_active = fe->stream_post && G == 1 && lp.quad && lp.multi != 0 && !fe->frames.empty();
     for (int g = 0; g < G; g++) {
         const int a = fe->g0[g], n = fe->gn[g];
         hipStream_t sg = fe->gst[g];
@@ -917,6 +961,36 @@ static int fe_front_lk(svo_frontend* fe, int t) {
         LKBatch lb{dprev + a, dcur + a, fe->d_der + (size_t)((t - 1) % 3) * S + a, fe->xyA + 2 * (size_t)a * CAP,
                    fe->next_xy + 2 * (size_t)a * CAP, fe->status + (size_t)a * CAP, nullptr,
                    fe->iters + (size_t)a * CAP, fe->nA + a, 0, CAP};
+        if (fe->sp_active) {
+            // post_lk goes first, on the copy stream, behind everything LK(t) waits
+            // for (the previous tail): it waits on the device for each sequence's LK
+            PostLkBatch pb = fe_post_lk_batch(fe, a);
+            fe->lk_stamp++;
+            pb.done = fe->d_done + (size_t)a * fe->done_stride * kFlagSpread;
+            pb.done_stride = fe->done_stride;
+            pb.lk_stamp = fe->lk_stamp;
+            pb.fpw = 4;
+            pb.h_ready = fe->h_ready + a;
+            pb.stamp = t;
+            pb.h_fail = fe->h_fail;
+            lb.done = fe->d_done + (size_t)a * fe->done_stride * kFlagSpread;
+            lb.done_stride = fe->done_stride;
+            lb.stamp = fe->lk_stamp;
+            if (fe->stream_mode == 2) {
+                ph_begin(fe, PH_LK, sg, &slot);
+                SVO_HIP(ctx, launch_lk(lb, n, mp, lp, sg));
+                ph_end(fe, sg, slot);
+                SVO_HIP(ctx, hipEventRecord(fe->ev_sync[2 + 2 * g], sg));
+                SVO_HIP(ctx, hipStreamWaitEvent(fe->st_copy, fe->ev_sync[2 + 2 * g], 0));
+                SVO_HIP(ctx, launch_post_lk(pb, n, fe->st_copy));
+                SVO_HIP(ctx, hipEventRecord(fe->ev_sync[3 + 2 * g], fe->st_copy));
+                continue;
+            }
+            SVO_HIP(ctx, hipEventRecord(fe->ev_prelk, sg));
+            SVO_HIP(ctx, hipStreamWaitEvent(fe->st_copy, fe->ev_prelk, 0));
+            SVO_HIP(ctx, launch_post_lk(pb, n, fe->st_copy));
+            SVO_HIP(ctx, hipEventRecord(fe->ev_sync[3 + 2 * g], fe->st_copy));
+        }
         ph_begin(fe, PH_LK, sg, &slot);
         SVO_HIP(ctx, launch_lk(lb, n, mp, lp, sg));
         ph_end(fe, sg, slot);
@@ -974,7 +1048,12 @@ static int fe_front_rest(svo_frontend* fe, int t) {
         SVO_HIP(ctx, hipEventRecord(fe->ev_sync[0], st0));
         fe->pyr_ready = tn;
     }
-    for (int g = 0; g < G; g++) {
+    for (int g = 0; g < G && fe->sp_active; g++) {
+        // streamed: post_lk is already queued; the scoring and the tail (slice
+        // stream) read its outputs
+        SVO_HIP(ctx, hipStreamWaitEvent(fe->gst[g], fe->ev_sync[3 + 2 * g], 0));
+    }
+    for (int g = 0; g < G && !fe->sp_active; g++) {
         const int a = fe->g0[g], n = fe->gn[g];
         hipStream_t sg = fe->gst[g];
         // keep status == 1 (R:src/tracking.cpp:169-175), gather the map points, draw
@@ -994,7 +1073,7 @@ static int fe_front_rest(svo_frontend* fe, int t) {
     }
     // every slice's points are gathered once the last slice's copies are queued
     // (slices run in order on their streams; the full copy waits for the last)
-    SVO_HIP(ctx, hipEventRecord(fe->ev_gathered, fe->gst[G - 1]));
+    SVO_HIP(ctx, hipEventRecord(fe->ev_gathered, fe->sp_active ? fe->st_copy : fe->gst[G - 1]));
     for (int g = 0; g + 1 < G; g++) SVO_HIP(ctx, hipStreamWaitEvent(fe->st_copy, fe->ev_sync[3 + 2 * g], 0));
 
     // the full point set for the final fits / long RANSAC runs, on the copy
@@ -1074,13 +1153,40 @@ int svo_frontend_step(svo_frontend* fe, int t, svo_frontend_stats* stats) {
         hipStream_t sq = sg;  // the slice stream is idle while the host solves RANSAC
         TP("ransac begin");
         auto tw = clk::now();
-        SVO_HIP(ctx, hipEventSynchronize(fe->ev_sync[3 + 2 * g]));
+        const bool pregen = fe->sp_active;
+        if (pregen) {
+            // streamed: each sequence's first hypothesis chunk as soon as its post-LK
+            // results land (h_ready), while LK still runs for later sequences
+            const int* rdy = fe->h_ready;
+            const int* fail = fe->h_fail;
+            fe->pool->run(n, [&](int i) {
+                const int s = a + i;
+                while (__atomic_load_n(rdy + s, __ATOMIC_ACQUIRE) != t && !__atomic_load_n(fail, __ATOMIC_ACQUIRE))
+                    __builtin_ia32_pause();
+                RansacSeq& r = fe->rs[s];
+                r.begin(fe->h_obj + 3 * (size_t)s * CAP, fe->h_xyB + 2 * (size_t)s * CAP, fe->h_nB[s],
+                        c.pnp_iterations);
+                r.samp = fe->h_samp + (size_t)kSampleFloats * kRansacPrefetch * s;
+                r.nsamp = kRansacPrefetch;
+                r.first_chunk = std::max(fe->chunk0, fe->pred_iters[s]);
+                ms[s] = (!r.direct && !r.done && r.next_end() <= r.nsamp) ? r.gen_chunk(c.K) : 0;
+            });
+            if (*fe->h_fail) return set_error(ctx, SVO_ERR_HIP, "svo_frontend_step: streamed post-LK wait timed out");
+            SVO_HIP(ctx, hipEventSynchronize(fe->ev_sync[3 + 2 * g]));  // post_lk's device outputs (done by now)
+        } else {
+            SVO_HIP(ctx, hipEventSynchronize(fe->ev_sync[3 + 2 * g]));
+        }
         TP("lk results on host");
         ms_wait += ms_since(tw);
         int max_b = 0;
         bool need_full = false;
         for (int s = a; s < a + n; s++) {
             RansacSeq& r = fe->rs[s];
+            if (pregen) {
+                need_full |= r.direct && !r.done;
+                max_b = std::max(max_b, fe->h_nB[s]);
+                continue;
+            }
             r.begin(fe->h_obj + 3 * (size_t)s * CAP, fe->h_xyB + 2 * (size_t)s * CAP, fe->h_nB[s], c.pnp_iterations);
             r.samp = fe->h_samp + (size_t)kSampleFloats * kRansacPrefetch * s;
             r.nsamp = kRansacPrefetch;
@@ -1106,22 +1212,26 @@ int svo_frontend_step(svo_frontend* fe, int t, svo_frontend_stats* stats) {
             int rf = ensure_full();
             if (rf) return rf;
         }
+        bool first = pregen;  // the first round's chunks are already generated
         for (;;) {
-            // sequences still sampling (no pool dispatch once all are done)
-            bool any = false;
-            for (int s = a; s < a + n; s++) {
-                any |= !fe->rs[s].done && !fe->rs[s].direct;
-                need_full |= fe->rs[s].next_end() > fe->rs[s].nsamp;
+            if (!first) {
+                // sequences still sampling (no pool dispatch once all are done)
+                bool any = false;
+                for (int s = a; s < a + n; s++) {
+                    any |= !fe->rs[s].done && !fe->rs[s].direct;
+                    need_full |= fe->rs[s].next_end() > fe->rs[s].nsamp;
+                }
+                if (!any) break;
+                if (need_full) {  // past the prefetched subsets (> 26 hypotheses): rare
+                    int rf = ensure_full();
+                    if (rf) return rf;
+                }
+                auto th = clk::now();
+                fe->pool->run(n, [&](int i) { ms[a + i] = fe->rs[a + i].gen_chunk(c.K); });
+                ms_hyp += ms_since(th);
             }
-            if (!any) break;
-            if (need_full) {  // past the prefetched subsets (> 26 hypotheses): rare
-                int rf = ensure_full();
-                if (rf) return rf;
-            }
-            auto th = clk::now();
-            fe->pool->run(n, [&](int i) { ms[a + i] = fe->rs[a + i].gen_chunk(c.K); });
+            first = false;
             TP("hyps generated");
-            ms_hyp += ms_since(th);
             int mmax = 0;
             for (int s = a; s < a + n; s++) mmax = std::max(mmax, ms[s]);
             if (mmax == 0) break;
@@ -1319,7 +1429,9 @@ int svo_frontend_features(svo_frontend* fe, int seq, float* xy, int cap, int* n)
     SVO_HIP(ctx, hipStreamSynchronize(ctx->stream));
     const int k = std::min(cnt, cap);
     if (k > 0 && xy)
-        SVO_HIP(ctx, hipMemcpy(xy, fe->xyA + 2 * (size_t)seq * fe->CAP, sizeof(float) * 2 * k, hipMemcpyDeviceToHost));
+        SVO_HIP(ctx, hipMemcpyAsync(xy, fe->xyA + 2 * (size_t)seq * fe->CAP, sizeof(float) * 2 * k,
+                                    hipMemcpyDeviceToHost, ctx->stream));
+        SVO_HIP(ctx, hipStreamSynchronize(ctx->stream));
     if (n) *n = cnt;
     return SVO_OK;
 }

@@ -52,6 +52,17 @@ struct PostLkBatch {
     int* h_n;
     long long* h_iters;
     float* h_samp;  // [s][nh][25]
+    // streamed mode (done != null): the block of sequence s first waits until LK
+    // has counted ceil(n_in / fpw) blocks of s in done[s] (then resets it), reads
+    // next_xy / iters (iters | status << 30) with sc1 loads, and at its end
+    // publishes h_ready[s] = stamp (system scope) after its host-coherent writes;
+    // h_fail[0] = 1 if the wait timed out
+    int* done = nullptr;  // LK's block flags of this launch (LKBatch::done)
+    int done_stride = 0, lk_stamp = 0;
+    int fpw = 4;
+    int* h_ready = nullptr;
+    int stamp = 0;
+    int* h_fail = nullptr;
 };
 hipError_t launch_post_lk(const PostLkBatch& b, int nseq, hipStream_t st);
 
