@@ -134,6 +134,9 @@ struct FastDetBatch {
     float* box_binned = nullptr;
     int* box_band = nullptr;
     bool box_prebinned = false;  // launch_box_bin already ran (e.g. ahead, off the critical path)
+    // nullable [s][npx]: fast_detect_q_kernel writes the score of every kept corner
+    // there, so the emit pass reads one byte instead of re-scoring from the image
+    uint8_t* score_map = nullptr;
 };
 // ints of band-offset scratch per sequence for an image of height h
 // Box centres are binned by cell: 16-row band x 64-column tile (the FAST tile
@@ -197,17 +200,15 @@ struct LKBatch {
     int* iters;   // nullable
     const int* counts;  // nullable
     int n, cap;
-    // nullable (lk_multi_kernel only): streamed hand-off -- each block writes its
-    // next_xy / iters (iters | status << 30) write-through (sc1), drains its stores
-    // and then stores stamp to done[seq * done_stride + blockIdx.x] (sc1), so a
-    // consumer can take a sequence as soon as all its blocks' flags show the stamp.
-    // Flags, not a counter: one agent-scope atomic add per block cost LK +27 %.
-    int* done = nullptr;
-    int done_stride = 0;
-    int stamp = 0;
+    // nullable (lk_multi_kernel only): streamed hand-off -- each feature's result
+    // also goes to rec[4 * (s * cap + i)] as ONE 16-byte write-through (sc1) store
+    // of two tagged 8-byte granules {x, stamp << 24 | status << 23 | iters},
+    // {y, stamp}, so a consumer polling with sc1 loads takes a sequence once every
+    // record shows the step's stamp -- no fence, flag or counter per block (a flag
+    // store behind a vmcnt drain cost the kernel ~20 %, an atomic add ~27 %)
+    unsigned* rec = nullptr;
+    int stamp = 0;  // 1 .. 255
 };
-// LK block flags one per 128-B line (kFlagSpread ints apart)
-constexpr int kFlagSpread = 32;
 hipError_t launch_lk(const LKBatch& b, int nseq, int max_n, const LKParams& p, hipStream_t st);
 bool lk_supported(int win_w, int win_h);
 

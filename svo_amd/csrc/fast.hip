@@ -746,7 +746,11 @@ __global__ __launch_bounds__(256) void fast_detect_q_kernel(FastDetBatch B, int 
             keep = keep && sb(sr, sc) > m;
         }
         if (mask && keep) keep = mask[(size_t)y * w + x] != 0;
-        if (keep) atomicOr(&RB[sr - 1], 1ull << (sc - 1));
+        if (keep) {
+            atomicOr(&RB[sr - 1], 1ull << (sc - 1));
+            // (a box may still drop it: then the byte is never read)
+            if (B.score_map) B.score_map[seq * B.npx + (size_t)y * w + x] = (uint8_t)(SC[sr][sc] & 0xFF);
+        }
     }
     __syncthreads();
     if (tid < FD_TY && y0 + tid < h) {
@@ -1022,33 +1026,33 @@ __global__ __launch_bounds__(256) void box_bin_kernel(FastDetBatch B, int w, int
     }
 }
 
-// exclusive scan of the per-row counts of one sequence (one block per sequence)
-__global__ __launch_bounds__(1024) void fast_scan_kernel(FastDetBatch B, int h) {
+// exclusive scan of the per-row counts of one sequence (one 256-thread block per
+// sequence -- it finds room beside LK, a 1024-thread block waits for a whole CU):
+// each thread sums a run of consecutive rows, one block scan of the run sums
+constexpr int kScanBlock = 256;
+__global__ __launch_bounds__(kScanBlock) void fast_scan_kernel(FastDetBatch B, int h) {
     const size_t seq = blockIdx.x;
     const int* __restrict__ cnt = B.rowcnt + seq * h;
     int* __restrict__ off = B.rowoff + seq * h;
-    __shared__ int part[1024];
-    __shared__ int carry;
+    __shared__ int part[kScanBlock];
     const int tid = threadIdx.x;
-    if (tid == 0) carry = 0;
+    const int run = (h + kScanBlock - 1) / kScanBlock, y0 = tid * run, y1 = min(h, y0 + run);
+    int sum = 0;
+    for (int y = y0; y < y1; y++) sum += cnt[y];
+    part[tid] = sum;
     __syncthreads();
-    for (int y0 = 0; y0 < h; y0 += 1024) {
-        const int y = y0 + tid;
-        const int v = y < h ? cnt[y] : 0;
-        part[tid] = v;
+    for (int o = 1; o < kScanBlock; o <<= 1) {
+        const int t = tid >= o ? part[tid - o] : 0;
         __syncthreads();
-        for (int o = 1; o < 1024; o <<= 1) {
-            const int t = tid >= o ? part[tid - o] : 0;
-            __syncthreads();
-            part[tid] += t;
-            __syncthreads();
-        }
-        if (y < h) off[y] = carry + part[tid] - v;
-        __syncthreads();
-        if (tid == 0) carry += part[1023];
+        part[tid] += t;
         __syncthreads();
     }
-    if (tid == 0) B.n_out[seq] = carry;
+    int acc = part[tid] - sum;
+    for (int y = y0; y < y1; y++) {
+        off[y] = acc;
+        acc += cnt[y];
+    }
+    if (tid == kScanBlock - 1) B.n_out[seq] = part[kScanBlock - 1];
 }
 
 // raster-order write of one row's keypoints (one wave per row); the FAST
@@ -1071,7 +1075,9 @@ __global__ __launch_bounds__(64) void fast_emit_kernel(FastDetBatch B, int thres
             if (idx < B.cap) {
                 const int x = sgi * 64 + lane;
                 float resp = 0.f;
-                if (nonmax) {
+                if (nonmax && B.score_map) {
+                    resp = (float)B.score_map[seq * B.npx + (size_t)y * L.w + x];
+                } else if (nonmax) {
                     const uint8_t* p = L.data + (size_t)y * L.pitch + x;
                     int ring[16];
 #pragma unroll
@@ -1130,8 +1136,9 @@ hipError_t launch_fast_collect(const FastBatch& b, int nseq, int w, int h, int n
     return hipGetLastError();
 }
 
-hipError_t launch_fast_detect(const FastDetBatch& b, int nseq, int w, int h, int threshold, int nonmax,
+hipError_t launch_fast_detect(const FastDetBatch& b0, int nseq, int w, int h, int threshold, int nonmax,
                               hipStream_t st) {
+    FastDetBatch b = b0;
     hipError_t e = hipMemsetAsync(b.rowcnt, 0, sizeof(int) * (size_t)h * nseq, st);
     if (e != hipSuccess) return e;
     if (b.box_pts && !b.box_prebinned) {
@@ -1144,6 +1151,7 @@ hipError_t launch_fast_detect(const FastDetBatch& b, int nseq, int w, int h, int
     // NMS over the corner queue
     const char* ev = std::getenv("SVO_FAST_V");
     const int ver = ev ? std::atoi(ev) : 4;
+    if (ver != 4) b.score_map = nullptr;  // only fast_detect_q_kernel fills it
     if (ver == 1)
         hipLaunchKernelGGL(fast_detect_kernel, grid, dim3(256), 0, st, b, threshold, nonmax);
     else if (ver == 2)
@@ -1152,7 +1160,7 @@ hipError_t launch_fast_detect(const FastDetBatch& b, int nseq, int w, int h, int
         hipLaunchKernelGGL(fast_detect_s_kernel, grid, dim3(256), 0, st, b, threshold, nonmax);
     else
         hipLaunchKernelGGL(fast_detect_q_kernel, grid, dim3(256), 0, st, b, threshold, nonmax);
-    hipLaunchKernelGGL(fast_scan_kernel, dim3(nseq), dim3(1024), 0, st, b, h);
+    hipLaunchKernelGGL(fast_scan_kernel, dim3(nseq), dim3(kScanBlock), 0, st, b, h);
     hipLaunchKernelGGL(fast_emit_kernel, dim3(h, nseq), dim3(64), 0, st, b, threshold, nonmax);
     return hipGetLastError();
 }

@@ -192,11 +192,10 @@ __device__ __forceinline__ int block_compact(int n, Keep keep, const float* __re
         float x = 0.f, y = 0.f;
         int m = 0;
         if (k) {
-            if (SC1) {  // written write-through by a still-running producer (streamed LK)
-                const unsigned long long v = __hip_atomic_load(
-                    reinterpret_cast<const unsigned long long*>(xy_in + 2 * i), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                x = __uint_as_float((unsigned)v);
-                y = __uint_as_float((unsigned)(v >> 32));
+            if (SC1) {  // xy_in = streamed LK records {x, tag}, {y, tag} (sc1 loads)
+                const unsigned long long* r = reinterpret_cast<const unsigned long long*>(xy_in + 4 * i);
+                x = __uint_as_float((unsigned)__hip_atomic_load(r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+                y = __uint_as_float((unsigned)__hip_atomic_load(r + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
             } else {
                 x = xy_in[2 * i];
                 y = xy_in[2 * i + 1];
@@ -241,27 +240,29 @@ __global__ __launch_bounds__(kFeBlock) void post_lk_kernel(PostLkBatch B) {
     const uint8_t* __restrict__ st = B.status + o;
     long long it = 0;
     int n;
-    if (B.done) {
-        // streamed: wait for this sequence's LK blocks (bounded: a lost producer
+    if (B.rec) {
+        // streamed: wait for this sequence's LK records (bounded: a lost producer
         // ends the wait after ~1 s and raises h_fail instead of hanging the GPU)
-        if (tid < 64) {  // wave 0 polls every block flag of the sequence (sc1 loads)
-            const int need = (n_in + B.fpw - 1) / B.fpw;
-            const int* __restrict__ fl = B.done + (size_t)s * B.done_stride * kFlagSpread;
+        const unsigned* __restrict__ rc = B.rec + 4 * o;
+        const unsigned stamp = (unsigned)B.lk_stamp;
+        auto ld8 = [&](int i, int h) {
+            return __hip_atomic_load(reinterpret_cast<const unsigned long long*>(rc + 4 * i + 2 * h), __ATOMIC_RELAXED,
+                                     __HIP_MEMORY_SCOPE_AGENT);
+        };
+        auto tagged = [&](int i) {
+            return (unsigned)(ld8(i, 0) >> 56) == stamp && (unsigned)(ld8(i, 1) >> 32) == stamp;
+        };
+        if (tid < 64) {
             int spins = 0;
             bool fail = false;
-            // cheap probe first: the sequence's last block (dispatched last) -- one
-            // address, one request per poll; a full sweep of every flag only then
-            while (need > 0 && !fail &&
-                   __hip_atomic_load(fl + (size_t)(need - 1) * kFlagSpread, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) !=
-                       B.lk_stamp) {
+            // cheap probe first: the last feature (its block is dispatched last)
+            while (n_in > 0 && !fail && (unsigned)(ld8(n_in - 1, 1) >> 32) != stamp) {
                 __builtin_amdgcn_s_sleep(32);
                 fail = ++spins > (1 << 20);
             }
             for (;;) {
                 bool ok = true;
-                for (int i = tid; i < need; i += 64)
-                    ok &= __hip_atomic_load(fl + (size_t)i * kFlagSpread, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
-                          B.lk_stamp;
+                for (int i = tid; i < n_in; i += 64) ok &= tagged(i);
                 if (__all(ok) || fail) break;
                 __builtin_amdgcn_s_sleep(4);
                 fail = ++spins > (1 << 20);
@@ -269,12 +270,10 @@ __global__ __launch_bounds__(kFeBlock) void post_lk_kernel(PostLkBatch B) {
             if (fail && tid == 0) __hip_atomic_store(B.h_fail, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         }
         __syncthreads();
-        const int* __restrict__ itw = B.iters + o;
-        for (int i = tid; i < n_in; i += kFeBlock)
-            it += __hip_atomic_load(itw + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & ((1 << 30) - 1);
+        for (int i = tid; i < n_in; i += kFeBlock) it += (long long)((unsigned)(ld8(i, 0) >> 32) & ((1u << 23) - 1u));
         n = block_compact<true>(
-            n_in, [&](int i) { return (__hip_atomic_load(itw + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >> 30) != 0; },
-            B.xy_in + 2 * o, B.mid_in + o, B.xy_out + 2 * o, B.mid_out + o, wsum, &base_s);
+            n_in, [&](int i) { return ((ld8(i, 0) >> 55) & 1ull) != 0; }, reinterpret_cast<const float*>(rc),
+            B.mid_in + o, B.xy_out + 2 * o, B.mid_out + o, wsum, &base_s);
     } else {
         for (int i = tid; i < n_in; i += kFeBlock) it += B.iters[o + i];
         n = block_compact(n_in, [&](int i) { return st[i] != 0; }, B.xy_in + 2 * o, B.mid_in + o, B.xy_out + 2 * o,

@@ -210,12 +210,13 @@ struct svo_frontend {
     hipEvent_t ev_counts = nullptr;  // the step's feature counts on the host
     // streamed post-LK (SVO_FE_STREAM=1, one slice, lk_multi_kernel): post_lk is
     // queued before LK on the copy stream and takes each sequence as soon as its LK
-    // blocks are counted in d_done; the host starts a sequence's RANSAC hypotheses
+    // records carry the step's stamp (d_rec); the host starts a sequence's RANSAC hypotheses
     // once h_ready[s] shows the step's stamp, while LK still runs for later ones
     bool stream_post = false, sp_active = false;
     int stream_mode = 0;  // 2: the same hand-off, post_lk queued after LK (diagnostic)
-    int* d_done = nullptr;  // [s][done_stride] LK block flags (device)
-    int done_stride = 0, lk_stamp = 0;
+    unsigned* d_rec = nullptr;  // [s][CAP][4] streamed LK records (device)
+    uint8_t* score_map = nullptr;  // [s][npx] FAST scores of the kept corners
+    int lk_stamp = 0;
     int* h_ready = nullptr;  // [s] host-coherent stamps
     int* h_fail = nullptr;   // host-coherent: a streamed wait timed out
     hipEvent_t ev_prelk = nullptr;
@@ -287,6 +288,7 @@ T* carve(char*& p, size_t count) {
 FastDetBatch fe_fast_batch(svo_frontend* fe, const PyrDesc* descs_cur, bool use_mask) {
     FastDetBatch fb{descs_cur, nullptr, fe->fbits, fe->rowcnt, fe->rowoff,
                     (svo_keypoint*)fe->kps, fe->kn, fe->npx, (fe->W + 63) / 64, fe->KCAP};
+    fb.score_map = fe->score_map;
     if (use_mask) {  // boxes around the previous frame's features, rasterised per FAST tile
         fb.box_pts = fe->xyA;
         fb.box_counts = fe->nA;
@@ -667,10 +669,9 @@ int svo_frontend_create(svo_ctx* ctx, const svo_frontend_config* cfg, svo_fronte
     }
     // (on the context stream: a first use of the null stream would take a fifth
     // hardware queue and serialise the step's streams)
-    fe->done_stride = ((fe->CAP + 3) / 4 + 63) & ~63;
-    if (hipMalloc(&fe->d_done, sizeof(int) * kFlagSpread * (size_t)fe->done_stride * S) != hipSuccess ||
-        hipMemsetAsync(fe->d_done, 0, sizeof(int) * kFlagSpread * (size_t)fe->done_stride * S, ctx->stream) !=
-            hipSuccess) {
+    if (hipMalloc(&fe->score_map, fe->npx * S) != hipSuccess ||
+        hipMalloc(&fe->d_rec, 16 * (size_t)fe->CAP * S) != hipSuccess ||
+        hipMemsetAsync(fe->d_rec, 0, 16 * (size_t)fe->CAP * S, ctx->stream) != hipSuccess) {
         svo_frontend_destroy(fe);
         return set_error(ctx, SVO_ERR_HIP, "svo_frontend_create: counter alloc");
     }
@@ -777,7 +778,8 @@ void svo_frontend_destroy(svo_frontend* fe) {
         if (e) (void)hipEventDestroy(e);
     if (fe->ev_counts) (void)hipEventDestroy(fe->ev_counts);
     if (fe->ev_prelk) (void)hipEventDestroy(fe->ev_prelk);
-    if (fe->d_done) (void)hipFree(fe->d_done);
+    if (fe->d_rec) (void)hipFree(fe->d_rec);
+    if (fe->score_map) (void)hipFree(fe->score_map);
     delete fe;
 }
 
@@ -965,16 +967,13 @@ static int fe_front_lk(svo_frontend* fe, int t) {
             // post_lk goes first, on the copy stream, behind everything LK(t) waits
             // for (the previous tail): it waits on the device for each sequence's LK
             PostLkBatch pb = fe_post_lk_batch(fe, a);
-            fe->lk_stamp++;
-            pb.done = fe->d_done + (size_t)a * fe->done_stride * kFlagSpread;
-            pb.done_stride = fe->done_stride;
+            fe->lk_stamp = fe->lk_stamp % 255 + 1;
+            pb.rec = fe->d_rec + 4 * (size_t)a * CAP;
             pb.lk_stamp = fe->lk_stamp;
-            pb.fpw = 4;
             pb.h_ready = fe->h_ready + a;
             pb.stamp = t;
             pb.h_fail = fe->h_fail;
-            lb.done = fe->d_done + (size_t)a * fe->done_stride * kFlagSpread;
-            lb.done_stride = fe->done_stride;
+            lb.rec = fe->d_rec + 4 * (size_t)a * CAP;
             lb.stamp = fe->lk_stamp;
             if (fe->stream_mode == 2) {
                 ph_begin(fe, PH_LK, sg, &slot);
@@ -1159,10 +1158,19 @@ int svo_frontend_step(svo_frontend* fe, int t, svo_frontend_stats* stats) {
             // results land (h_ready), while LK still runs for later sequences
             const int* rdy = fe->h_ready;
             const int* fail = fe->h_fail;
+            std::atomic<bool> late{false};
+            const auto t_wait = clk::now();
             fe->pool->run(n, [&](int i) {
                 const int s = a + i;
-                while (__atomic_load_n(rdy + s, __ATOMIC_ACQUIRE) != t && !__atomic_load_n(fail, __ATOMIC_ACQUIRE))
+                // bounded: the device side gives up after ~1 s (h_fail); the host after 2 s
+                for (unsigned k = 0; __atomic_load_n(rdy + s, __ATOMIC_ACQUIRE) != t; k++) {
+                    if (__atomic_load_n(fail, __ATOMIC_ACQUIRE) || late.load(std::memory_order_relaxed)) return;
+                    if ((k & 1023u) == 1023u && ms_since(t_wait) > 2000.0) {
+                        late.store(true);
+                        return;
+                    }
                     __builtin_ia32_pause();
+                }
                 RansacSeq& r = fe->rs[s];
                 r.begin(fe->h_obj + 3 * (size_t)s * CAP, fe->h_xyB + 2 * (size_t)s * CAP, fe->h_nB[s],
                         c.pnp_iterations);
@@ -1171,7 +1179,8 @@ int svo_frontend_step(svo_frontend* fe, int t, svo_frontend_stats* stats) {
                 r.first_chunk = std::max(fe->chunk0, fe->pred_iters[s]);
                 ms[s] = (!r.direct && !r.done && r.next_end() <= r.nsamp) ? r.gen_chunk(c.K) : 0;
             });
-            if (*fe->h_fail) return set_error(ctx, SVO_ERR_HIP, "svo_frontend_step: streamed post-LK wait timed out");
+            if (*fe->h_fail || late.load())
+                return set_error(ctx, SVO_ERR_HIP, "svo_frontend_step: streamed post-LK wait timed out");
             SVO_HIP(ctx, hipEventSynchronize(fe->ev_sync[3 + 2 * g]));  // post_lk's device outputs (done by now)
         } else {
             SVO_HIP(ctx, hipEventSynchronize(fe->ev_sync[3 + 2 * g]));

@@ -52,14 +52,12 @@ struct PostLkBatch {
     int* h_n;
     long long* h_iters;
     float* h_samp;  // [s][nh][25]
-    // streamed mode (done != null): the block of sequence s first waits until LK
-    // has counted ceil(n_in / fpw) blocks of s in done[s] (then resets it), reads
-    // next_xy / iters (iters | status << 30) with sc1 loads, and at its end
-    // publishes h_ready[s] = stamp (system scope) after its host-coherent writes;
-    // h_fail[0] = 1 if the wait timed out
-    int* done = nullptr;  // LK's block flags of this launch (LKBatch::done)
-    int done_stride = 0, lk_stamp = 0;
-    int fpw = 4;
+    // streamed mode (rec != null): the block of sequence s first waits until all
+    // n_in LK records (LKBatch::rec) of s show lk_stamp, reads them with sc1
+    // loads, and at its end publishes h_ready[s] = stamp (system scope) after its
+    // host-coherent writes; h_fail[0] = 1 if the wait timed out
+    const unsigned* rec = nullptr;
+    int lk_stamp = 0;
     int* h_ready = nullptr;
     int stamp = 0;
     int* h_fail = nullptr;

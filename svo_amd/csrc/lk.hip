@@ -1416,7 +1416,7 @@ __device__ __forceinline__ void group_sum_f(int (&v)[NV], float (&f)[NV]) {
     for (int i = 0; i < NV; i++) f[i] = halves_lane_float(h[i], lo[i]);
 }
 
-// STREAM: the streamed hand-off epilogue (LKBatch::done); a separate instance, so
+// STREAM: the streamed hand-off epilogue (LKBatch::rec); a separate instance, so
 // the default kernel's code is untouched by it
 template <int FPW, int QJM, int MINW, int KKS = 2, bool STREAM = false>
 __global__ __launch_bounds__(64, MINW) void lk_multi_kernel(LKBatch B, LKDev p) {
@@ -1685,24 +1685,16 @@ __global__ __launch_bounds__(64, MINW) void lk_multi_kernel(LKBatch B, LKDev p) 
         wave_lds_sync();
     }
     if constexpr (STREAM) {
-        // streamed hand-off (MI355X_MICROARCH.md, inter-workgroup visibility, row
-        // 1): write-through stores, the wave's vmcnt drained, then one sc1 flag
-        // store per block; the consumer polls with sc1 loads and reads sc1.
-        // Measured: this epilogue alone costs the kernel ~20 % (an agent-scope
-        // atomic add instead ~27 %), so SVO_FE_STREAM stays off by default.
+        // streamed hand-off: one 16-B sc1 store of two tagged granules per feature
         if (l == 0 && live) {
-            const unsigned long long xy2 = (unsigned long long)__float_as_uint(nx) |
-                                           ((unsigned long long)__float_as_uint(ny) << 32);
-            __hip_atomic_store(reinterpret_cast<unsigned long long*>(next_xy + 2 * pt), xy2, __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(B.iters + base + pt, itcount | (st << 30), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            typedef unsigned u32x4v __attribute__((ext_vector_type(4)));
+            const u32x4v v = {__float_as_uint(nx), ((unsigned)B.stamp << 24) | ((unsigned)st << 23) | (unsigned)itcount,
+                              __float_as_uint(ny), (unsigned)B.stamp};
+            unsigned* dst = B.rec + 4 * (base + pt);
+            asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(dst), "v"(v) : "memory");
             B.status[base + pt] = (uint8_t)st;
             if (B.err) B.err[base + pt] = errv;
         }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        if (lane == 0)
-            __hip_atomic_store(B.done + ((size_t)seq * B.done_stride + blockIdx.x) * kFlagSpread, B.stamp,
-                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         return;
     }
     if (l == 0 && live) {
@@ -1718,7 +1710,7 @@ template <int FPW, int QJM, int MINW = 4, int KKS = 2>
 hipError_t launch_multi(const LKBatch& b, int nseq, int max_n, const LKDev& d, hipStream_t st) {
     dim3 grid((max_n + FPW - 1) / FPW, nseq);
     constexpr int lds_bytes = FPW * MultiShape<QJM>::JBYTES + 16;
-    if (b.done)
+    if (b.rec)
         hipLaunchKernelGGL((lk_multi_kernel<FPW, QJM, MINW, KKS, true>), grid, dim3(64), lds_bytes, st, b, d);
     else
         hipLaunchKernelGGL((lk_multi_kernel<FPW, QJM, MINW, KKS>), grid, dim3(64), lds_bytes, st, b, d);
