@@ -207,17 +207,18 @@ def main():
     bytes_per_launch = units_per_launch * lk_bytes_per_feature(L)
     lk_avg_s = lk_ms / max(lk_n, 1) / 1e3
     achieved = bytes_per_launch / lk_avg_s / 1e9 if lk_avg_s > 0 else 0.0
-    # the 21x21 temporal call runs lk_multi_kernel<4, 2 (four features per wave)
+    # the 21x21 temporal call runs lk_multi_kernel<4, 1 (four features per wave)
     # unless SVO_LK_QUAD=0 (lk_fast_kernel, one per wave) or SVO_LK_MULTI picks
     # another several-per-wave kernel (svo_amd/csrc/lk.hip launch_lk)
-    multi = os.environ.get("SVO_LK_MULTI", "42")
+    multi = os.environ.get("SVO_LK_MULTI", "41")
     if os.environ.get("SVO_LK_QUAD", "1")[:1] == "0":
         lk_name, lk_desc = "lk_fast_kernel<21, 21", "one feature per wave"
     else:
         lk_name, lk_desc = {"0": ("lk_dual_kernel<21, 21", "two features per wave"),
                             "2": ("lk_multi_kernel<2, 3", "two features per wave"),
+                            "42": ("lk_multi_kernel<4, 2", "four features per wave"),
                             "43": ("lk_multi_kernel<4, 3", "four features per wave")}.get(
-            multi, ("lk_multi_kernel<4, 2", "four features per wave"))
+            multi, ("lk_multi_kernel<4, 1", "four features per wave"))
     traffic = pmc_traffic(lk_name)
     dominant = max(phases, key=lambda k: phases[k][0])
     single = None

@@ -185,7 +185,7 @@ struct LKParams {
     int want_err;
     int generic = 0;  // 1: always use the runtime-window kernel (tests compare both)
     int quad = 1;     // 21x21: several features per wave; 0: one per wave (lk_fast_kernel)
-    int multi = 42;   // 21x21 several-per-wave kernel (SVO_LK_MULTI, see launch_lk)
+    int multi = 41;   // 21x21 several-per-wave kernel (SVO_LK_MULTI, see launch_lk)
 };
 // Batched LK: blockIdx.y = sequence; sequence s owns points [s*cap, s*cap + n_s)
 // of every array, n_s = counts[s] (device) or n when counts is null.

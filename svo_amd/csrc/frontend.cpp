@@ -191,6 +191,7 @@ struct svo_frontend {
     int chunk0 = 2;                // floor of the first hypothesis chunk
     bool pyr_early = true;         // frame t+1's pyramid beside LK(t) (SVO_FE_PYR_EARLY)
     bool fast_early = true;        // FAST(t) queued behind LK(t), not after it (SVO_FE_FAST_EARLY)
+    bool fast_first = false;       // FAST(t) queued ahead of LK(t) (SVO_FE_FAST_FIRST)
     std::vector<double> pose;  // [s][6]
     bool fits_pending = false;
     bool stats_pending = false;
@@ -663,6 +664,8 @@ int svo_frontend_create(svo_ctx* ctx, const svo_frontend_config* cfg, svo_fronte
         fe->pyr_early = !(pe && pe[0] == '0');
         const char* fe_ = std::getenv("SVO_FE_FAST_EARLY");
         fe->fast_early = !(fe_ && fe_[0] == '0');
+        const char* ff = std::getenv("SVO_FE_FAST_FIRST");
+        fe->fast_first = ff && ff[0] == '1';
         const char* sp = std::getenv("SVO_FE_STREAM");
         fe->stream_post = sp && (sp[0] == '1' || sp[0] == '2');
         fe->stream_mode = sp ? std::atoi(sp) : 0;
@@ -948,9 +951,17 @@ static int fe_front_lk(svo_frontend* fe, int t) {
         lp.quad = quad_off ? 0 : 1;
         static const int multi = [] {
             const char* e = std::getenv("SVO_LK_MULTI");
-            return e ? std::atoi(e) : 42;
+            return e ? std::atoi(e) : 41;
         }();
         lp.multi = multi;
+    }
+    // SVO_FE_FAST_FIRST=1: FAST(t) enqueued ahead of LK(t) (with a high-priority
+    // FAST stream its blocks are dispatched first, so FAST no longer gates the tail)
+    if (fe->fast_early && fe->fast_first) {
+        hipStream_t sf = fe->st_fast;
+        int rc = fe_fast_and_bucket(fe, dcur, true, sf, true);
+        if (rc) return rc;
+        SVO_HIP(ctx, hipEventRecord(fe->ev_sync[1], sf));
     }
     // streamed post-LK: one slice and the four-per-wave kernel (the one that counts)
     fe->sp_active = fe->stream_post && G == 1 && lp.quad && lp.multi != 0 && !fe->frames.empty();
@@ -1000,7 +1011,7 @@ static int fe_front_lk(svo_frontend* fe, int t) {
     //     independent of this step's LK and pose, so it is queued right behind the
     //     LK on the low-priority FAST stream, where it fills the CUs the LK's last
     //     waves leave idle and the post-LK window; the tail waits for it
-    if (fe->fast_early) {
+    if (fe->fast_early && !fe->fast_first) {
         hipStream_t sf = fe->st_fast;
         int rc = fe_fast_and_bucket(fe, dcur, true, sf, true);
         if (rc) return rc;

@@ -1792,16 +1792,18 @@ hipError_t launch_lk(const LKBatch& b, int nseq, int max_n, const LKParams& lp, 
         // two features per wave: the SAD error (flags 0 + want_err) stays on lk_fast_kernel
         const bool dual_ok = !(lp.want_err && !(lp.flags & SVO_LK_GET_MIN_EIGENVALS));
         if (lp.win_w == 21 && lp.win_h == 21 && dual_ok && lp.quad) {
-            // SVO_LK_MULTI: 42 (default) four features per wave, 2-px staging
-            // margin; 43 the same with a 3-px margin; 2 two per wave (generic
-            // map); 0 the dual kernel (its own lane map)
+            // SVO_LK_MULTI: 41 (default) four features per wave, 1-px staging
+            // margin (re-staged when the estimate leaves it; measured 2.7 % faster
+            // alone than the 2-px margin, 42, and 3-px, 43); 2 two per wave
+            // (generic map); 0 the dual kernel (its own lane map)
             switch (lp.multi) {
                 case 0: return launch_dual<21, 21>(b, nseq, max_n, d, st);
                 case 2: return launch_multi<2, 3>(b, nseq, max_n, d, st);
                 case 43: return launch_multi<4, 3, 3>(b, nseq, max_n, d, st);
+                case 42: return launch_multi<4, 2, 3>(b, nseq, max_n, d, st);
                 case 47: return launch_multi<4, 2, 3, 4>(b, nseq, max_n, d, st);
                 case 48: return launch_multi<4, 2, 3, 1>(b, nseq, max_n, d, st);
-                default: return launch_multi<4, 2, 3>(b, nseq, max_n, d, st);
+                default: return launch_multi<4, 1, 3>(b, nseq, max_n, d, st);
             }
         }
         if (lp.win_w == 21 && lp.win_h == 21) return launch_fast<21, 21>(b, nseq, max_n, d, st);

@@ -132,7 +132,7 @@ TEMPORAL = dict(win=(21, 21), ml=3, crit=(3, 50, 1e-3), flags=S.LK_GET_MIN_EIGEN
 STEREO = dict(win=(11, 11), ml=3, crit=(3, 30, 1e-3), flags=0)                        # R:src/tracking.cpp:101-105
 
 
-@pytest.fixture(params=["fixed-window", "generic", "one-per-wave", "dual", "two-per-wave"])
+@pytest.fixture(params=["fixed-window", "two-px-margin", "generic", "one-per-wave", "dual", "two-per-wave"])
 def lk_kernel(request, monkeypatch):
     """Every LK kernel: the compile-time-window ones (21x21 four features per
     wave by default, 11x11, 15x15, 31x31), the 21x21 one-feature-per-wave kernel
@@ -141,7 +141,7 @@ def lk_kernel(request, monkeypatch):
     (SVO_LK_GENERIC=1)."""
     monkeypatch.setenv("SVO_LK_GENERIC", "1" if request.param == "generic" else "0")
     monkeypatch.setenv("SVO_LK_QUAD", "0" if request.param == "one-per-wave" else "1")
-    monkeypatch.setenv("SVO_LK_MULTI", {"dual": "0", "two-per-wave": "2"}.get(request.param, "42"))
+    monkeypatch.setenv("SVO_LK_MULTI", {"dual": "0", "two-per-wave": "2", "two-px-margin": "42"}.get(request.param, "41"))
     return request.param
 
 
