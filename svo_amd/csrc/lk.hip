@@ -1801,6 +1801,7 @@ hipError_t launch_lk(const LKBatch& b, int nseq, int max_n, const LKParams& lp, 
                 case 2: return launch_multi<2, 3>(b, nseq, max_n, d, st);
                 case 43: return launch_multi<4, 3, 3>(b, nseq, max_n, d, st);
                 case 42: return launch_multi<4, 2, 3>(b, nseq, max_n, d, st);
+                case 40: return launch_multi<4, 0, 3>(b, nseq, max_n, d, st);
                 case 47: return launch_multi<4, 2, 3, 4>(b, nseq, max_n, d, st);
                 case 48: return launch_multi<4, 2, 3, 1>(b, nseq, max_n, d, st);
                 default: return launch_multi<4, 1, 3>(b, nseq, max_n, d, st);
