@@ -267,9 +267,13 @@ __global__ __launch_bounds__(kFeBlock) void post_lk_kernel(PostLkBatch B) {
                 __builtin_amdgcn_s_sleep(4);
                 fail = ++spins > (1 << 20);
             }
-            if (fail && tid == 0) __hip_atomic_store(B.h_fail, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            if (fail && tid == 0) {
+                __hip_atomic_store(B.h_fail, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                it_s = ~0ull;  // tells the block to stop (it_s is re-zeroed below otherwise unused so far)
+            }
         }
         __syncthreads();
+        if (it_s == ~0ull) return;  // LK never ran beside us (kernels serialised): the host re-runs us after LK
         for (int i = tid; i < n_in; i += kFeBlock) it += (long long)((unsigned)(ld8(i, 0) >> 32) & ((1u << 23) - 1u));
         n = block_compact<true>(
             n_in, [&](int i) { return ((ld8(i, 0) >> 55) & 1ull) != 0; }, reinterpret_cast<const float*>(rc),

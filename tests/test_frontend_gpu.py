@@ -13,6 +13,15 @@ from svo_amd.scene import Scene
 pytestmark = pytest.mark.gpu
 
 
+@pytest.fixture(autouse=True, params=["streamed", "after-lk"])
+def post_lk_mode(request, monkeypatch):
+    """Both post-LK schedules (read when a Frontend is created): the default
+    streamed hand-off (post_lk waits on the device for each sequence's LK
+    records) and SVO_FE_STREAM=0 (post_lk queued after LK)."""
+    monkeypatch.setenv("SVO_FE_STREAM", "1" if request.param == "streamed" else "0")
+    return request.param
+
+
 def make_frontend(ctx, scenes, T, n_features, **kw):
     sc0 = scenes[0]
     cfg = S.FrontendConfig(sc0.w, sc0.h, sc0.K, n_seq=len(scenes), n_frames=T, n_features=n_features, **kw)
