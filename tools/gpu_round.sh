@@ -5,7 +5,7 @@ TAG=${1:-r01}
 export TMPDIR=/tmp
 O=gpurun_out
 mkdir -p $O
-B="python bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-single"
+B="python bench.py --steps 50 --warmup 10 --no-cpu-baseline --no-single"
 timeout -k 10 900 python -m pytest tests -m gpu -q --timeout 300 -p no:cacheprovider > $O/gpu_tests.log 2>&1 || { echo "tests failed"; tail -30 $O/gpu_tests.log; exit 1; }
 tail -2 $O/gpu_tests.log
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { cat $O/smoke.log; exit 1; }
