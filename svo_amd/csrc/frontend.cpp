@@ -670,7 +670,10 @@ int svo_frontend_create(svo_ctx* ctx, const svo_frontend_config* cfg, svo_fronte
         // default on (one slice); off where kernels are serialised (it needs post_lk
         // and LK side by side; a timed-out hand-off also turns it off, see step)
         const char* ser = std::getenv("AMD_SERIALIZE_KERNEL");
-        fe->stream_post = !(sp && sp[0] == '0') && !(ser && std::atoi(ser) != 0);
+        // and for large per-sequence feature sets (one post_lk block per sequence then
+        // trails LK: 1080p / 8000 and 4K / 16000 features measured 5-7 % slower)
+        fe->stream_post = !(sp && sp[0] == '0') && !(ser && std::atoi(ser) != 0) &&
+                          (fe->CAP <= 4096 || (sp && sp[0] == '1'));
         fe->stream_mode = sp ? std::atoi(sp) : 1;
     }
     // (on the context stream: a first use of the null stream would take a fifth
