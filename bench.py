@@ -166,7 +166,15 @@ def main():
     W, H, N, ML, label = CONFIGS[args.config]
     Sq, K, Wm = args.seq, args.steps, args.warmup
     T = Wm + K + 1
-    ctx = S.Context(local)
+    device = local
+    if world > 1:
+        # One rank per GPU; ranks beyond the visible devices (a multi-rank rehearsal on a
+        # one-GPU box) share them round-robin. device_count() does not initialise HIP.
+        import torch
+        n_dev = torch.cuda.device_count()
+        if n_dev > 0:
+            device = local % n_dev
+    ctx = S.Context(device)
     seeds = sequence_seeds(rank, Sq)
     scenes = [Scene(W, H, seed=sd) for sd in seeds]
     cfg = S.FrontendConfig(W, H, scenes[0].K, n_seq=Sq, n_frames=T, n_features=N, max_level=ML,
