@@ -2,14 +2,17 @@
 """Benchmark: the reference's per-frame tracking step on MI355X.
 
 Metric (BASELINE.json): frames/sec @1241x376, 2000 feats; LK iters/sec; achieved
-HBM GB/s. A "step" = one frame of every sequence in the batch through
-pyramid(frame t) -> temporal LK (21x21, maxLevel 3, 50 it, MIN_EIGENVALS) ->
-status compaction -> solvePnPRansac (100 it, 8 px, 0.999: host EPnP + GPU
-scoring) -> outlier removal -> mask + FAST(20, NMS) -> top-up to 2000 features
-(R:src/tracking.cpp:240-269, keyframe-every-frame upper bound). Frames are
-synthetic KITTI-sized renders (svo_amd/scene.py), uploaded to HBM before the
-timed region. Multi-GPU: one process per GPU, each advancing its own batch of
-independent sequences (weak scaling, no collective on the data path).
+HBM GB/s. A "step" = one stereo frame of every sequence in the batch through
+pyramids (left + Scharr, right) -> temporal LK (21x21, maxLevel 3, 50 it,
+MIN_EIGENVALS) -> status compaction -> solvePnPRansac (100 it, 8 px, 0.999: host
+EPnP + GPU scoring, host SQPnP-objective fit) -> outlier removal -> keyframe:
+mask + FAST(20, NMS), the first (2000 - n) corners stereo-matched (11x11 LK,
+maxLevel 3, 30 it), |yR - yL| < 40, DLT triangulation, z > 0, world frame by the
+estimated pose (R:src/tracking.cpp:240-269; every frame a keyframe that tops the
+set up to 2000 features). Frames are synthetic KITTI-sized stereo renders
+(svo_amd/scene.py), uploaded to HBM before the timed region. Multi-GPU: one
+process per GPU, each advancing its own batch of independent sequences (weak
+scaling, no collective on the data path).
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--seq S] [--config kitti|1080p|4k]
 """
@@ -35,20 +38,34 @@ CONFIGS = {
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (guides/MI355X_MICROARCH.md)
 
 
+def level_sizes(W: int, H: int, max_level: int):
+    sizes = [(W, H)]
+    for _ in range(max_level):
+        w, h = sizes[-1]
+        sizes.append(((w + 1) // 2, (h + 1) // 2))
+    return sizes
+
+
 def lk_bytes_per_feature(levels: int, win: int = 21) -> int:
     """B_lk per feature = L((win+3)^2 + (win+1)^2) + 21."""
     return levels * ((win + 3) ** 2 + (win + 1) ** 2) + 21
 
 
+def pyr_bytes_per_frame(W: int, H: int, max_level: int) -> int:
+    """B_pyr = sum_{l<L} w_l h_l (reads) + sum_{l>=1} w_l h_l (writes)."""
+    sizes = level_sizes(W, H, max_level)
+    return sum(w * h for w, h in sizes[:-1]) + sum(w * h for w, h in sizes[1:])
+
+
+def deriv_bytes_per_frame(W: int, H: int, max_level: int) -> int:
+    """The Scharr derivative pyramid the same launch writes (int16 Ix, Iy per pixel
+    of every level; not in SURVEY's B_pyr, stated separately)."""
+    return sum(4 * w * h for w, h in level_sizes(W, H, max_level))
+
+
 def frame_bytes(W: int, H: int, n: int, max_level: int, win: int = 21) -> int:
     """B = B_pyr + B_fast + B_lk per frame."""
-    sizes = [(W, H)]
-    for _ in range(max_level):
-        w, h = sizes[-1]
-        sizes.append(((w + 1) // 2, (h + 1) // 2))
-    L = max_level + 1
-    b_pyr = sum(w * h for w, h in sizes[:-1]) + sum(w * h for w, h in sizes[1:])
-    return b_pyr + W * H + n * lk_bytes_per_feature(L, win)
+    return pyr_bytes_per_frame(W, H, max_level) + W * H + n * lk_bytes_per_feature(max_level + 1, win)
 
 
 def dist_setup():
@@ -90,17 +107,18 @@ def allreduce_sum(dist, v: float) -> float:
     return float(t.item())
 
 
-def pmc_traffic(kernel_prefix: str):  # substring of the demangled kernel name
-    """Per-launch HBM bytes of a kernel from a committed rocprofv3 PMC summary
-    (profiles/pmc_summary.json, written by tools/pmc_summary.py), or None."""
+def pmc_traffic(cfg_name: str, kernel_prefix: str):  # substring of the demangled kernel name
+    """Per-launch HBM bytes of a kernel from the rocprofv3 PMC summary measured on
+    THIS config's workload (profiles/pmc_summary.json configs[cfg_name], written by
+    tools/pmc_summary.py --config), or None when that config was not measured."""
     path = os.path.join(ROOT, "profiles", "pmc_summary.json")
     try:
         with open(path) as f:
             d = json.load(f)
-        for k, v in d.get("kernels", {}).items():
+        for k, v in d.get("configs", {}).get(cfg_name, {}).get("kernels", {}).items():
             if kernel_prefix in k:
                 return v.get("hbm_bytes_per_launch")
-    except Exception:
+    except (OSError, ValueError):
         return None
     return None
 
@@ -121,12 +139,12 @@ def cpu_baseline(cfg_name: str, seconds: float):
     def run(threads, secs):
         O.set_threads(threads)
         sc = Scene(W, H, seed=101)
-        loop = OracleLoop(sc, N, depth_seed=101).init(0)
+        loop = OracleLoop(sc, N).init(0)
         dt, n = 0.0, 0
         while dt < secs and n < 5000:
-            frame = sc.frame(n + 1)  # rendered outside the timed region
+            left, right = sc.frame(n + 1), sc.right(n + 1)  # rendered outside the timed region
             t0 = time.perf_counter()
-            loop.step(n + 1, frame)
+            loop.step(n + 1, left, right)
             dt += time.perf_counter() - t0
             n += 1
         return n, dt
@@ -135,8 +153,8 @@ def cpu_baseline(cfg_name: str, seconds: float):
     n1, dt1 = run(1, seconds)
     O.set_threads(cores)
     return {"value": round(n / dt, 3), "unit": "frames/s", "cores": cores, "kind": "port",
-            "sample": f"{n} frames of one {W}x{H} sequence, {N} feats, {dt:.1f} s; oracle/ C restatement "
-                      f"of the OpenCV path (LK OpenMP over {cores} threads, FAST/PnP single-thread)",
+            "sample": f"{n} stereo frames of one {W}x{H} sequence, {N} feats, {dt:.1f} s; oracle/ C restatement "
+                      f"of the OpenCV path (LK OpenMP over {cores} threads, FAST/PnP/triangulation single-thread)",
             "single_thread": {"value": round(n1 / dt1, 3), "cores": 1,
                               "sample": f"{n1} frames, {dt1:.1f} s, everything on one thread"}}
 
@@ -177,28 +195,36 @@ def main():
     ctx = S.Context(device)
     seeds = sequence_seeds(rank, Sq)
     scenes = [Scene(W, H, seed=sd) for sd in seeds]
+    # the synthetic camera ping-pongs with period 2 * scene.period (32 frames), so
+    # P rendered stereo pairs per sequence are reused cyclically (frame t = pair
+    # t mod P; rendering is host work outside the timing, all T frames resident)
+    P = min(T, 2 * scenes[0].period)
     cfg = S.FrontendConfig(W, H, scenes[0].K, n_seq=Sq, n_frames=T, n_features=N, max_level=ML,
                            host_threads=args.threads, timing=args.timing, groups=args.groups)
     fe = S.Frontend(ctx, cfg)
+    pairs0 = None
     for s, sc in enumerate(scenes):
+        pairs = [(sc.frame(t), sc.right(t)) for t in range(P)]
         for t in range(T):
-            fe.set_frame(s, t, sc.frame(t), sc.R(t), depth_seed=sc.seed)
+            fe.set_frame(s, t, *pairs[t % P])
+        if s == 0:
+            pairs0 = pairs
+        if s % 16 == 15:
+            print(f"[bench] rank {rank}: {s + 1}/{Sq} sequences rendered and uploaded", file=sys.stderr, flush=True)
     fe.init(0)
+    feats_after = {}  # features after step t = the inputs of LK(t + 1)
     for t in range(1, Wm + 1):
-        fe.step(t)
+        feats_after[t] = fe.step(t).as_dict()["features"]
     fe.reset_times()
     tot = {"lk_iterations": 0, "tracked": 0, "inliers": 0, "added": 0, "hypotheses": 0,
            "host_ms_hyp": 0.0, "host_ms_fit": 0.0, "host_ms_wait": 0.0}
-    lk_units = 0
-    feats_prev = None
     barrier(dist)
     t0 = time.perf_counter()
     for t in range(Wm + 1, Wm + K + 1):
         st = fe.step(t).as_dict()
         for k in tot:
             tot[k] += st[k]
-        lk_units += st["tracked"] if feats_prev is None else feats_prev
-        feats_prev = st["features"]
+        feats_after[t] = st["features"]
     fe.synchronize()  # the last step's pose fits / prefetched pyramid belong to the timed work
     barrier(dist)
     dt = time.perf_counter() - t0
@@ -210,9 +236,15 @@ def main():
 
     if rank != 0:
         return
-    # roofline of the dominant kernel (by device time): LK
+    # roofline of the dominant kernel (by device time): LK. The event pairs folded
+    # after reset_times bracket the LK launches of the last lk_n timed steps
+    # (step Wm+1's LK went out during the warm-up); LK(t) tracks the features left
+    # after step t-1, so those launches processed feats_after[t-1] features each.
     lk_ms, lk_n = phases["lk"]
     L = ML + 1
+    last = Wm + K
+    lk_units = sum(feats_after[t - 1] for t in range(last - lk_n + 1, last + 1)) if lk_n > 0 else 0
+    assert lk_n <= K, "more LK launches timed than steps"
     units_per_launch = lk_units / max(lk_n, 1)
     bytes_per_launch = units_per_launch * lk_bytes_per_feature(L)
     lk_avg_s = lk_ms / max(lk_n, 1) / 1e3
@@ -229,13 +261,24 @@ def main():
                             "42": ("lk_multi_kernel<4, 2", "four features per wave"),
                             "43": ("lk_multi_kernel<4, 3", "four features per wave")}.get(
             multi, ("lk_multi_kernel<4, 1", "four features per wave"))
-    traffic = pmc_traffic(lk_name)
+    traffic = pmc_traffic(args.config, lk_name)
     dominant = max(phases, key=lambda k: phases[k][0])
+    # pyramid + Scharr of one new left frame per sequence per step (the launch
+    # chain pyr_scharr_kernel x levels + the coarsest Scharr + borders)
+    # (in the step it runs beside LK, which stretches it: its roofline is taken
+    # from the same chain timed alone, 20 rebuilds of the last frame, after the
+    # timed region; the in-step average is reported beside it)
+    pyr_ms, pyr_n = phases.get("pyramid", (0.0, 0))
+    pyr_instep_s = pyr_ms / max(pyr_n, 1) / 1e3
+    pyr_avg_s = fe.time_pyramid(Wm + K, 20) / 1e3
+    pyr_bytes = Sq * pyr_bytes_per_frame(W, H, ML)
+    der_bytes = Sq * deriv_bytes_per_frame(W, H, ML)
+    pyr_traffic = pmc_traffic(args.config, "pyr_scharr_kernel")
     single = None
     if not args.no_single:
         fe1 = S.Frontend(ctx, S.FrontendConfig(W, H, scenes[0].K, n_seq=1, n_frames=T, n_features=N, max_level=ML))
         for t in range(T):
-            fe1.set_frame(0, t, scenes[0].frame(t), scenes[0].R(t), depth_seed=scenes[0].seed)
+            fe1.set_frame(0, t, *pairs0[t % P])
         fe1.init(0)
         for t in range(1, Wm + 1):
             fe1.step(t)
@@ -279,6 +322,23 @@ def main():
             "units_per_launch": round(units_per_launch, 1),
             "bytes_per_unit": lk_bytes_per_feature(L),
             "avg_launch_us": round(lk_avg_s * 1e6, 3),
+            "launches_timed": lk_n,
+        },
+        "roofline_pyramid": {
+            "kernel": "pyr_scharr_kernel chain (pyrDown + Scharr of every level, borders), "
+                      f"one new left frame of {Sq} sequences per launch",
+            "bound": "hbm",
+            "achieved": round(pyr_bytes / pyr_avg_s / 1e9, 2) if pyr_avg_s > 0 else 0.0,
+            "peak": HBM_PEAK_GBPS,
+            "unit": "GB/s",
+            "frac": round(pyr_bytes / pyr_avg_s / 1e9 / HBM_PEAK_GBPS, 4) if pyr_avg_s > 0 else 0.0,
+            "traffic": pyr_traffic,
+            "algorithmic_bytes_per_launch": pyr_bytes,
+            "derivative_bytes_per_launch": der_bytes,
+            "achieved_incl_derivatives": round((pyr_bytes + der_bytes) / pyr_avg_s / 1e9, 2) if pyr_avg_s > 0 else 0.0,
+            "avg_launch_us": round(pyr_avg_s * 1e6, 3),
+            "timing": "alone, 20 launches (HIP events on the launch stream)",
+            "in_step_avg_launch_us": round(pyr_instep_s * 1e6, 3),
         },
     }
     if not args.no_cpu_baseline:

@@ -206,12 +206,15 @@ int svo_refine_poses(svo_ctx* ctx, const double* obj_xyz, const float* img_xy, c
 
 /* ------------------------------------------------------------ batched front end
  * The reference's per-frame loop (Tracking::startStereo, R:src/tracking.cpp:232-276:
- * trackFrames -> calculatePose -> keyframe extractFeatures) for n_seq independent
- * camera sequences advanced in lockstep: every kernel launch covers the whole
- * batch, all state (pyramids, features, map points) stays in HBM, and only the
- * RANSAC minimal solver (EPnP) runs on the host between GPU scoring launches.
- * Map points of new features come from the synthetic scene's depth (stand-in for
- * triangulateNewMapPoints, which needs a stereo pair: DESIGN.md). */
+ * trackFrames -> calculatePose -> keyframe extractFeatures + findLeftFeaturesInRight
+ * + triangulateNewMapPoints) for n_seq independent stereo sequences advanced in
+ * lockstep: every kernel launch covers the whole batch, all state (left / right
+ * pyramids, features, map points) stays in HBM, and only the RANSAC minimal solver
+ * (EPnP) and the final SQPnP-objective fit run on the host between GPU launches.
+ * Every frame is a keyframe whose new features top the set up to n_features: the
+ * first (n_features - n) masked FAST corners are matched in the right image (stereo
+ * LK), filtered (status, |yR - yL| < y_threshold), triangulated with P_left /
+ * P_right (z > 0) and moved to the world frame by the frame's estimated pose. */
 typedef struct svo_frontend svo_frontend;
 
 typedef struct svo_frontend_config {
@@ -239,6 +242,14 @@ typedef struct svo_frontend_config {
     int groups;             /* pipeline groups: the batch is split into this many
                                slices whose LK / RANSAC overlap (host RANSAC of one
                                slice while the GPU tracks the next); 0 = auto */
+    /* stereo keyframe path (R:src/tracking.cpp:94-152) */
+    float P_left[12];       /* mProjectionMatrixLeft (KITTI calib P2, R:src/main.cpp:25-28), row-major 3x4 */
+    float P_right[12];      /* mProjectionMatrixRight (P3, :29-32) */
+    float y_threshold;      /* R:configs/config.yaml:16 -> 40 */
+    int stereo_win;         /* R:src/tracking.cpp:104 -> 11 */
+    int stereo_max_level;   /* -> 3 */
+    int stereo_max_count;   /* :97 -> 30 */
+    double stereo_epsilon;  /* -> 1e-3 */
 } svo_frontend_config;
 
 typedef struct svo_frontend_stats {
@@ -255,13 +266,13 @@ typedef struct svo_frontend_stats {
 
 int svo_frontend_create(svo_ctx* ctx, const svo_frontend_config* cfg, svo_frontend** out);
 void svo_frontend_destroy(svo_frontend* fe);
-/* Frame t of sequence seq: level 0 upload (H2D, untimed) + world->camera
- * rotation of the synthetic scene and its depth seed (for new map points). */
-int svo_frontend_set_frame(svo_frontend* fe, int seq, int t, const uint8_t* gray, int stride,
-                           const double R[9], int depth_seed);
-/* Same from a BGR 8UC3 frame (svo_image_upload_bgr's conversion). */
-int svo_frontend_set_frame_bgr(svo_frontend* fe, int seq, int t, const uint8_t* bgr, int stride,
-                               const double R[9], int depth_seed);
+/* Stereo pair t of sequence seq (left / right grey, same stride): level-0 uploads
+ * (H2D, untimed; R:include/async_image_loader.h:57-69 delivers the pair). */
+int svo_frontend_set_frame(svo_frontend* fe, int seq, int t, const uint8_t* left, const uint8_t* right,
+                           int stride);
+/* Same from BGR 8UC3 frames (svo_image_upload_bgr's conversion). */
+int svo_frontend_set_frame_bgr(svo_frontend* fe, int seq, int t, const uint8_t* left_bgr,
+                               const uint8_t* right_bgr, int stride);
 /* Build every resident frame's pyramid now (else each step builds its own). */
 int svo_frontend_prebuild_pyramids(svo_frontend* fe);
 /* First keyframe: FAST (+bucket) on frame t0 of every sequence, map points. */
@@ -274,11 +285,18 @@ int svo_frontend_step(svo_frontend* fe, int t, svo_frontend_stats* stats);
 int svo_frontend_synchronize(svo_frontend* fe);
 int svo_frontend_pose(svo_frontend* fe, int seq, double rvec[3], double tvec[3]);
 int svo_frontend_features(svo_frontend* fe, int seq, float* xy, int cap, int* n);
+/* World positions (MapPoint::mWorldPos) of the current features' map points, in
+ * feature order (synchronises the front end first). */
+int svo_frontend_map_points(svo_frontend* fe, int seq, double* xyz, int cap, int* n);
 /* Accumulated per-phase device time (ms) and launch counts since create/reset:
- * phases: 0 pyramid, 1 lk, 2 compact, 3 gather, 4 pnp_score, 5 mask, 6 fast,
- * 7 bucket, 8 append. Returns the number of phases. */
+ * phases: 0 pyramid (left + Scharr), 1 lk, 2 post_lk, 3 stereo_lk, 4 pnp_score,
+ * 5 tail, 6 fast, 7 bucket, 8 append, 9 pyramid_right. Returns the number of phases. */
 int svo_frontend_phase_times(svo_frontend* fe, double* ms, int64_t* launches, int cap);
 void svo_frontend_reset_times(svo_frontend* fe);
+/* The pyramid + Scharr launch chain of frame t (every sequence) timed alone on the
+ * context stream: reps rebuilds (identical contents) after one warm-up, HIP
+ * events around them; ms per chain. Synchronises the front end first. */
+int svo_frontend_time_pyramid(svo_frontend* fe, int t, int reps, double* ms_per_launch);
 
 /* ------------------------------------------------------------ synthetic input
  * Deterministic synthetic KITTI-like frames: a textured canvas
@@ -295,7 +313,7 @@ int svo_synth_frame(const uint8_t* canvas, int cw, int ch, int margin_x, int mar
 
 /* Right view of a rectified stereo pair of the same synthetic scene: the
  * canvas surface sits at depth rho(u, v) = 12 + 5 sin(u/97 + seed) +
- * 4 cos(v/61 - seed/2) (world z; the field the frontend's map points use) and
+ * 4 cos(v/61 - seed/2) (world z) and
  * the right camera is the left one shifted by the baseline (fx * b = bf). */
 int svo_synth_frame_right(const uint8_t* canvas, int cw, int ch, int margin_x, int margin_y,
                           const double R[9], const double K[9], double bf, int depth_seed,

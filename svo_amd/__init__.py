@@ -95,8 +95,10 @@ _SIGS = [
                                    _f64p, _f64p, _i32p]),
     ("svo_frontend_create", C.c_int, [_vp, _vp, C.POINTER(_vp)]),
     ("svo_frontend_destroy", None, [_vp]),
-    ("svo_frontend_set_frame", C.c_int, [_vp, C.c_int, C.c_int, _u8p, C.c_int, _f64p, C.c_int]),
-    ("svo_frontend_set_frame_bgr", C.c_int, [_vp, C.c_int, C.c_int, _u8p, C.c_int, _f64p, C.c_int]),
+    ("svo_frontend_set_frame", C.c_int, [_vp, C.c_int, C.c_int, _u8p, _u8p, C.c_int]),
+    ("svo_frontend_set_frame_bgr", C.c_int, [_vp, C.c_int, C.c_int, _u8p, _u8p, C.c_int]),
+    ("svo_frontend_map_points", C.c_int, [_vp, C.c_int, _f64p, C.c_int, _i32p]),
+    ("svo_frontend_time_pyramid", C.c_int, [_vp, C.c_int, C.c_int, _f64p]),
     ("svo_frontend_prebuild_pyramids", C.c_int, [_vp]),
     ("svo_frontend_init", C.c_int, [_vp, C.c_int]),
     ("svo_frontend_step", C.c_int, [_vp, C.c_int, _vp]),
@@ -431,19 +433,31 @@ class FrontendConfig(C.Structure):
         ("bucket_size", C.c_int), ("per_bucket", C.c_int), ("pnp_iterations", C.c_int),
         ("pnp_reproj", C.c_float), ("pnp_confidence", C.c_double), ("K", C.c_double * 9),
         ("host_threads", C.c_int), ("timing", C.c_int), ("groups", C.c_int),
+        ("P_left", C.c_float * 12), ("P_right", C.c_float * 12), ("y_threshold", C.c_float),
+        ("stereo_win", C.c_int), ("stereo_max_level", C.c_int), ("stereo_max_count", C.c_int),
+        ("stereo_epsilon", C.c_double),
     ]
 
-    def __init__(self, width, height, K, n_seq=1, n_frames=2, n_features=2000, **kw):
+    def __init__(self, width, height, K, n_seq=1, n_frames=2, n_features=2000, P_left=None, P_right=None, **kw):
+        """P_left / P_right: the stereo rig's 3x4 projection matrices (KITTI calib P2 /
+        P3, R:src/main.cpp:25-32); default K[I|0] and K[I|(-bf, 0, 0)] with the
+        synthetic scene's fx * baseline (svo_amd.scene.STEREO_BF)."""
         super().__init__()
         d = dict(max_level=3, win=21, lk_max_count=50, lk_epsilon=1e-3, min_eig=1e-4,
                  lk_flags=LK_GET_MIN_EIGENVALS, fast_threshold=20, fast_nonmax=1, mask_half=10.0,
                  bucket_size=0, per_bucket=0, pnp_iterations=100, pnp_reproj=8.0, pnp_confidence=0.999,
-                 host_threads=0, timing=0, groups=0)
+                 host_threads=0, timing=0, groups=0, y_threshold=40.0, stereo_win=11, stereo_max_level=3,
+                 stereo_max_count=30, stereo_epsilon=1e-3)
         d.update(kw)
         self.width, self.height, self.n_seq, self.n_frames, self.n_features = width, height, n_seq, n_frames, n_features
         for k, v in d.items():
             setattr(self, k, v)
         self.K[:] = [float(x) for x in np.asarray(K, np.float64).ravel()]
+        if P_left is None or P_right is None:
+            from .scene import stereo_projections
+            P_left, P_right = stereo_projections(K)
+        self.P_left[:] = [float(x) for x in np.asarray(P_left, np.float32).ravel()]
+        self.P_right[:] = [float(x) for x in np.asarray(P_right, np.float32).ravel()]
 
 
 class FrontendStats(C.Structure):
@@ -456,7 +470,7 @@ class FrontendStats(C.Structure):
                 for k, _ in self._fields_}
 
 
-PHASES = ["pyramid", "lk", "compact", "gather", "pnp_score", "mask", "fast", "bucket", "append"]
+PHASES = ["pyramid", "lk", "post_lk", "stereo_lk", "pnp_score", "tail", "fast", "bucket", "append", "pyramid_right"]
 
 
 class Frontend:
@@ -469,19 +483,18 @@ class Frontend:
         ctx._check(lib().svo_frontend_create(ctx.handle, C.byref(cfg), C.byref(h)))
         self.handle = h
 
-    def set_frame(self, seq, t, gray, R=None, depth_seed=0):
-        """Frame t of sequence seq: (h, w) grey, or (h, w, 3) BGR converted on the device."""
-        gray = _c(gray, np.uint8)
-        Rp = None
-        if R is not None:
-            R = _c(R, np.float64).reshape(9)
-            Rp = _p(R, _f64p)
-        if gray.ndim == 3:
-            self.ctx._check(lib().svo_frontend_set_frame_bgr(self.handle, seq, t, _p(gray, _u8p), 3 * gray.shape[1],
-                                                             Rp, int(depth_seed)))
+    def set_frame(self, seq, t, left, right):
+        """Stereo pair t of sequence seq: (h, w) grey, or (h, w, 3) BGR converted on the device."""
+        left = _c(left, np.uint8)
+        right = _c(right, np.uint8)
+        if left.shape != right.shape:
+            raise SvoError("set_frame: left / right shapes differ")
+        if left.ndim == 3:
+            self.ctx._check(lib().svo_frontend_set_frame_bgr(self.handle, seq, t, _p(left, _u8p), _p(right, _u8p),
+                                                             3 * left.shape[1]))
             return
-        self.ctx._check(lib().svo_frontend_set_frame(self.handle, seq, t, _p(gray, _u8p), gray.shape[1], Rp,
-                                                     int(depth_seed)))
+        self.ctx._check(lib().svo_frontend_set_frame(self.handle, seq, t, _p(left, _u8p), _p(right, _u8p),
+                                                     left.shape[1]))
 
     def prebuild_pyramids(self):
         self.ctx._check(lib().svo_frontend_prebuild_pyramids(self.handle))
@@ -509,6 +522,19 @@ class Frontend:
         n = C.c_int()
         self.ctx._check(lib().svo_frontend_features(self.handle, seq, _p(xy, _f32p), cap, C.byref(n)))
         return xy[: min(n.value, cap)].copy()
+
+    def map_points(self, seq, cap=1 << 16):
+        """World positions of the current features' map points (float64, (n, 3))."""
+        xyz = np.empty((cap, 3), np.float64)
+        n = C.c_int()
+        self.ctx._check(lib().svo_frontend_map_points(self.handle, seq, _p(xyz, _f64p), cap, C.byref(n)))
+        return xyz[: min(n.value, cap)].copy()
+
+    def time_pyramid(self, t, reps=20):
+        """ms per pyramid + Scharr launch chain of frame t, timed alone."""
+        ms = np.zeros(1)
+        self.ctx._check(lib().svo_frontend_time_pyramid(self.handle, int(t), int(reps), _p(ms, _f64p)))
+        return float(ms[0])
 
     def phase_times(self):
         ms = np.zeros(16)

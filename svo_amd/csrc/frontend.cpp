@@ -1,19 +1,23 @@
 // Batched, device-resident tracking front end: the per-frame loop of
 // Tracking::startStereo (R:src/tracking.cpp:232-276) for n_seq independent
-// sequences advanced in lockstep.
+// stereo sequences advanced in lockstep.
 //
 //   step(t), for every sequence s at once:
-//     pyramid(frame t)                                   [pyramid.hip]
+//     pyramid + Scharr of left frame t+1, pyramid of right t   [pyramid.hip]   (beside LK)
 //     temporal LK  frame t-1 -> t (21x21, L3, 50 it)     [lk.hip]        trackFrames :154-179
-//     mask of boxes around frame t-1's features          [fast.hip]      extractFeatures :76-79
-//     FAST(t=20, NMS) on frame t with that mask          [fast.hip]      :82
-//     bucket selection (optional)                        [bucket.hip]    bucket.cpp (dead code)
-//     keep status==1 (stable compaction), gather map pts [frontend.hip]  :169-175, :182-187
+//     mask of boxes around frame t-1's features + FAST   [fast.hip]      extractFeatures :74-92
+//     (host) final SQPnP fits of step t-1 -> poses       [pose.cpp]      calculatePose :191-214
+//     keyframe points of t-1 to the world frame, keep status == 1,
+//       gather map points, first RANSAC subsets          [fe_kernels]    :169-175, :182-187, :141
 //     RANSAC: host EPnP chunks <-> GPU scoring launches  [pose.cpp, pnp.hip] calculatePose :191-196
-//     drop outliers (stable compaction)                  [frontend.hip]  :218-229
-//     keyframe top-up to n_features with new map points  [frontend.hip]  :247-255
+//     drop outliers + the first (n_features - n) corners [fe_kernels]    :218-229
+//     stereo LK of those corners into right frame t      [lk.hip]        findLeftFeaturesInRight :94-118
+//     |yR - yL| < 40, DLT triangulation, z > 0, append   [fe_kernels]    triangulateNewMapPoints :120-152
 //
-// FAST and the bucket run on the GPU while the host builds RANSAC hypotheses.
+// FAST runs on the GPU beside LK; the host builds RANSAC hypotheses while the GPU
+// scores; the final pose fits run on the host while the GPU tracks the next frame,
+// so a keyframe's new map points stay in its camera frame until the next step
+// moves them to the world frame with that pose (PendingMap, frontend.hpp).
 #include <algorithm>
 #include <cstdio>
 #include <cstdlib>
@@ -27,6 +31,7 @@
 #include <vector>
 
 #include "frontend.hpp"
+#include "linalg.hpp"
 #include "pose.hpp"
 
 namespace svo {
@@ -127,8 +132,8 @@ class Pool {
     double spin_us_ = 3000.0;
 };
 
-constexpr int kPhases = 9;
-enum Phase { PH_PYR, PH_LK, PH_COMPACT, PH_GATHER, PH_PNP, PH_MASK, PH_FAST, PH_BUCKET, PH_APPEND };
+constexpr int kPhases = 10;
+enum Phase { PH_PYR, PH_LK, PH_POST, PH_STEREO, PH_PNP, PH_TAIL, PH_FAST, PH_BUCKET, PH_APPEND, PH_PYR_R };
 
 }  // namespace
 
@@ -140,32 +145,33 @@ struct svo_frontend {
     svo_ctx* ctx = nullptr;
     svo_frontend_config cfg{};
     int S = 0, T = 0, CAP = 0, MAPCAP = 0, WORDS = 0, KCAP = 0, BCAP = 0;
-    int W = 0, H = 0, nlev = 0, ml = 0;
+    int W = 0, H = 0, nlev = 0, ml = 0, ml_st = 0;
     size_t npx = 0, bscr = 0;
-    std::vector<svo_image*> frames;  // [s*T + t]
-    std::vector<double> rot_host;    // [s*T + t][9]
-    std::vector<int> seed_host;      // [s]
-    std::vector<PyrDesc> desc_host;  // [t*S + s]
-    PyrDesc* d_desc = nullptr;       // [t][s]
+    std::vector<svo_image*> frames;    // left  [s*T + t]
+    std::vector<svo_image*> frames_r;  // right [s*T + t]
+    std::vector<PyrDesc> desc_host;    // [t*S + s]
+    std::vector<PyrDesc> desc_r_host;  // [t*S + s]
+    PyrDesc* d_desc = nullptr;         // [t][s]
+    PyrDesc* d_desc_r = nullptr;       // [t][s]
     void* dermem = nullptr;          // Scharr pyramids of frames t-1, t, t+1: [3][s], frame f in f % 3
     DerivDesc* d_der = nullptr;      // [3][s]
     // device state (one allocation)
     void* dmem = nullptr;
     float *xyA, *next_xy, *xyB, *obj, *kps, *cand, *box_binned;
+    float *st_xy, *st_next;  // keyframe candidates (left) and their stereo LK matches (right)
+    uint8_t* st_status;
     int* box_band;
-    int *midA, *midB, *nA, *nB, *iters, *kn, *bn, *map_n, *rowcnt, *rowoff, *scr, *cnt, *added, *seed_d;
+    int *midA, *midB, *nA, *nB, *iters, *kn, *bn, *map_n, *rowcnt, *rowoff, *scr, *cnt, *added, *st_n;
+    int *pend0, *pend_n;  // PendingMap ranges
     unsigned long long* fbits;
-    long long* itsum;
-    uint8_t *status, *mask;
-    uint32_t *bits_all, *bits_best;
-    double *map, *hyps, *rot_d, *stats;
-    float* samp;  // [s][kRansacPrefetch][kSampleFloats] RANSAC subsets gathered on the device
+    uint8_t* status;
+    uint32_t* bits_all;
+    double *map, *hyps;
     // the tracked-point arrays of a step (xyB, obj, nB) and its inlier bits are
     // double-buffered by step parity: the side work of step t (SQPnP statistics,
     // full copy to the host) reads them while step t+1 already runs
     float *xyB_b[2], *obj_b[2];
     int* nB_b[2];
-    uint32_t* bits_best_b[2];
     int front_t = -1;  // step whose first half (LK .. FAST) is already enqueued
     std::vector<hipEvent_t> ev_tail;  // [g] end of a step's tail on slice g
     // host mirrors (pinned)
@@ -175,9 +181,10 @@ struct svo_frontend {
     float *h_xyB, *h_obj, *h_samp;   // h_xyB / h_obj: this step's parity half of h_*_b
     float *h_xyB_b[2], *h_obj_b[2];
     double *h_hyps, *h_stats;
+    double* h_pose = nullptr;  // [s][12] camera -> world of the last fitted frame (host-coherent)
     uint32_t *h_bits, *h_best;  // h_best: this step's parity of h_best_b (host-coherent)
     uint32_t* h_best_b[2];
-    void* zout = nullptr;  // host-coherent: counts, sums, RANSAC subsets, inlier bits
+    void* zout = nullptr;  // host-coherent: counts, sums, RANSAC subsets, inlier bits, poses
     // host-coherent buffers the scoring kernel reads / writes directly (zero-copy:
     // no H2D of the hypotheses, no D2H of bits / counts, no count memset)
     void* zmem = nullptr;
@@ -206,28 +213,17 @@ struct svo_frontend {
     bool st_copy_owned = true;
     hipEvent_t ev_gathered = nullptr, ev_full = nullptr;  // ev_full: this step's parity of ev_full_b
     hipEvent_t ev_full_b[2] = {nullptr, nullptr};
+    hipEvent_t ev_pyr_r = nullptr;  // right pyramid of the step's frame built
     bool full_queued = false;
     int fit_parity = 0;  // step parity whose RANSAC results the pending fits refine
-    hipEvent_t ev_counts = nullptr;  // the step's feature counts on the host
-    // streamed post-LK (default; SVO_FE_STREAM=0 off; one slice, lk_multi_kernel): post_lk is
-    // queued before LK on the copy stream and takes each sequence as soon as its LK
-    // records carry the step's stamp (d_rec); the host starts a sequence's RANSAC hypotheses
-    // once h_ready[s] shows the step's stamp, while LK still runs for later ones
-    bool stream_post = false, sp_active = false;
-    int stream_mode = 0;  // 2: the same hand-off, post_lk queued after LK (diagnostic)
-    unsigned* d_rec = nullptr;  // [s][CAP][4] streamed LK records (device)
     uint8_t* score_map = nullptr;  // [s][npx] FAST scores of the kept corners
-    int lk_stamp = 0;
-    int* h_ready = nullptr;  // [s] host-coherent stamps
-    int* h_fail = nullptr;   // host-coherent: a streamed wait timed out
-    hipEvent_t ev_prelk = nullptr;
     Pool* pool = nullptr;
     // pipeline: slices of the batch [g0[g], g0[g] + gn[g]) on their own streams
     int G = 1;
     std::vector<int> g0, gn;
     std::vector<hipStream_t> gst;     // per slice (high priority)
     hipStream_t st_fast = nullptr;    // mask + FAST + bucket (low priority)
-    // [0] pyramid done, [1] FAST done, [2 + 2g] LK done, [3 + 2g] D2H done, [2 + 2G + g] stats D2H done
+    // [0] pyramid done, [1] FAST done, [2 + 2g] LK done, [3 + 2g] post-LK done
     std::vector<hipEvent_t> ev_sync;
     // timing
     hipEvent_t ev[256];
@@ -264,7 +260,8 @@ void ph_begin(svo_frontend* fe, int ph, hipStream_t st, int* slot) {
     *slot = -1;
     if (!fe->cfg.timing) return;
     // timing 2: only the big phases (each event pair costs a few us of host time)
-    if (fe->cfg.timing == 2 && ph != PH_LK && ph != PH_PYR && ph != PH_FAST) return;
+    if (fe->cfg.timing == 2 && ph != PH_LK && ph != PH_PYR && ph != PH_FAST && ph != PH_STEREO && ph != PH_PYR_R)
+        return;
     const int sl = fe->ev_used;
     for (auto& p : fe->pending)  // ring wrapped onto a pair still in flight
         if (p.second == sl) ph_fold(fe, true);
@@ -320,37 +317,108 @@ int fe_fast_and_bucket(svo_frontend* fe, const PyrDesc* descs_cur, bool use_mask
     return SVO_OK;
 }
 
-// keyframe top-up arguments for sequences from g0 on
-AppendBatch fe_append_batch(svo_frontend* fe, int t, int g0) {
-    AppendBatch ab;
-    ab.n = fe->nA + g0;
-    ab.xy = fe->xyA + 2 * (size_t)g0 * fe->CAP;
-    ab.mid = fe->midA + (size_t)g0 * fe->CAP;
-    ab.cap = fe->CAP;
-    ab.n_target = fe->cfg.n_features;
-    const bool bucketed = fe->cfg.bucket_size > 0;
-    ab.cand = bucketed ? fe->cand + 2 * (size_t)g0 * fe->BCAP : fe->kps + 3 * (size_t)g0 * fe->KCAP;
-    ab.cand_elem = bucketed ? 2 : 3;
-    ab.cand_cap = bucketed ? fe->BCAP : fe->KCAP;
-    ab.cand_n = (bucketed ? fe->bn : fe->kn) + g0;
-    ab.map = fe->map + 3 * (size_t)g0 * fe->MAPCAP;
-    ab.map_n = fe->map_n + g0;
-    ab.map_cap = fe->MAPCAP;
-    ab.rot = fe->rot_d + 9 * ((size_t)(t % fe->T) * fe->S + g0);
-    ab.depth_seed = fe->seed_d + g0;
-    ab.added = fe->added + g0;
-    std::memcpy(ab.K, fe->cfg.K, sizeof(ab.K));
-    return ab;
-}
-
-// keyframe top-up of sequences [g0, g0 + n)
-int fe_append(svo_frontend* fe, int t, int g0, int n, hipStream_t st) {
+// The keyframe of sequences [g0, g0 + n) on stream st (R:src/tracking.cpp:247-255,
+// every frame a keyframe topping the set up to n_features): outlier compaction
+// (inlier bits `bits`, or every point when n_in is all zero) + the first
+// candidates (tail_kernel), their stereo LK into the right frame t
+// (findLeftFeaturesInRight), then filter + triangulation + append (append_kernel).
+// xy_in / mid_in / n_in: the step's tracked points (compacted into xyA / midA / nA).
+// max_take: a host bound on every sequence's candidate count (the stereo LK grid).
+int fe_keyframe(svo_frontend* fe, int t, int g0, int n, const int* n_in, const uint32_t* bits, const float* xy_in,
+                const int* mid_in, int max_take, hipStream_t st) {
     svo_ctx* ctx = fe->ctx;
+    const svo_frontend_config& c = fe->cfg;
+    const size_t CAP = fe->CAP, a = g0;
     int slot;
+    const bool bucketed = c.bucket_size > 0;
+    TailBatch tb;
+    tb.n_in = n_in;
+    tb.bits = bits;
+    tb.words_cap = fe->WORDS;
+    tb.xy_in = xy_in;
+    tb.mid_in = mid_in;
+    tb.xy_out = fe->xyA + 2 * a * CAP;
+    tb.mid_out = fe->midA + a * CAP;
+    tb.n_out = fe->nA + a;
+    tb.cap = fe->CAP;
+    tb.n_target = c.n_features;
+    tb.cand = bucketed ? fe->cand + 2 * a * fe->BCAP : fe->kps + 3 * a * fe->KCAP;
+    tb.cand_elem = bucketed ? 2 : 3;
+    tb.cand_cap = bucketed ? fe->BCAP : fe->KCAP;
+    tb.cand_n = (bucketed ? fe->bn : fe->kn) + a;
+    tb.map_n = fe->map_n + a;
+    tb.map_cap = fe->MAPCAP;
+    tb.st_xy = fe->st_xy + 2 * a * CAP;
+    tb.st_n = fe->st_n + a;
+    ph_begin(fe, PH_TAIL, st, &slot);
+    SVO_HIP(ctx, launch_tail(tb, n, st));
+    ph_end(fe, st, slot);
+    // findLeftFeaturesInRight: calcOpticalFlowPyrLK(left, right, pts, 11x11, 3,
+    // {COUNT+EPS, 30, 0.001}), flags 0 (R:src/tracking.cpp:97-105); the left
+    // frame's derivative pyramid is the one the next step's temporal LK reads
+    SVO_HIP(ctx, hipStreamWaitEvent(st, fe->ev_pyr_r, 0));
+    const PyrDesc* dl = fe->d_desc + (size_t)(t % fe->T) * fe->S + a;
+    const PyrDesc* dr = fe->d_desc_r + (size_t)(t % fe->T) * fe->S + a;
+    LKBatch lb{dl, dr, fe->d_der + (size_t)(t % 3) * fe->S + a, fe->st_xy + 2 * a * CAP, fe->st_next + 2 * a * CAP,
+               fe->st_status + a * CAP, nullptr, nullptr, fe->st_n + a, 0, fe->CAP};
+    LKParams lp;
+    lp.win_w = lp.win_h = c.stereo_win;
+    lp.max_level = fe->ml_st;
+    lp.max_count = std::min(std::max(c.stereo_max_count, 0), 100);
+    const double eps = std::min(std::max(c.stereo_epsilon, 0.0), 10.0);
+    lp.eps2 = eps * eps;
+    lp.flags = 0;
+    lp.min_eig = (float)c.min_eig;
+    lp.want_err = 0;
+    ph_begin(fe, PH_STEREO, st, &slot);
+    SVO_HIP(ctx, launch_lk(lb, n, std::min(std::max(max_take, 0), fe->CAP), lp, st));
+    ph_end(fe, st, slot);
+    AppendBatch ab;
+    ab.n = fe->nA + a;
+    ab.xy = fe->xyA + 2 * a * CAP;
+    ab.mid = fe->midA + a * CAP;
+    ab.cap = fe->CAP;
+    ab.st_xy = fe->st_xy + 2 * a * CAP;
+    ab.st_next = fe->st_next + 2 * a * CAP;
+    ab.st_status = fe->st_status + a * CAP;
+    ab.st_n = fe->st_n + a;
+    ab.y_threshold = c.y_threshold;
+    std::memcpy(ab.P, c.P_left, sizeof(float) * 12);
+    std::memcpy(ab.P + 12, c.P_right, sizeof(float) * 12);
+    ab.map = fe->map + 3 * a * fe->MAPCAP;
+    ab.map_n = fe->map_n + a;
+    ab.map_cap = fe->MAPCAP;
+    ab.pend0 = fe->pend0 + a;
+    ab.pend_n = fe->pend_n + a;
+    ab.added = fe->added + a;
+    ab.h_n = fe->h_nA + a;
+    ab.h_added = fe->h_added + a;
     ph_begin(fe, PH_APPEND, st, &slot);
-    SVO_HIP(ctx, launch_append(fe_append_batch(fe, t, g0), n, st));
+    SVO_HIP(ctx, launch_append(ab, n, st));
     ph_end(fe, st, slot);
     return SVO_OK;
+}
+
+PendingMap fe_pending(svo_frontend* fe, int a) {
+    return PendingMap{fe->map + 3 * (size_t)a * fe->MAPCAP, fe->MAPCAP, fe->pend0 + a, fe->pend_n + a,
+                      fe->h_pose + 12 * (size_t)a};
+}
+
+// Frame::pose() of a fitted frame (R:src/tracking.cpp:198-214): the inverse of
+// the solvePnPRansac model [R(rvec) | tvec] (svo::SE3d::inverse), identity
+// when RANSAC found no model (rvec = tvec = 0, as the host mirror)
+void fe_set_pose(svo_frontend* fe, int s, bool ok, const double rvec[3], const double tvec[3]) {
+    double* T = fe->h_pose + 12 * (size_t)s;
+    double R[9];
+    const double zero[3] = {0, 0, 0};
+    if (!ok) {
+        rvec = zero;
+        tvec = zero;
+    }
+    la::rodrigues(rvec, R);
+    for (int i = 0; i < 3; i++)
+        for (int j = 0; j < 3; j++) T[3 * i + j] = R[3 * j + i];
+    for (int i = 0; i < 3; i++) T[9 + i] = -(T[3 * i] * tvec[0] + T[3 * i + 1] * tvec[1] + T[3 * i + 2] * tvec[2]);
 }
 
 // Full D2H of the step's tracked points and map points (after ev_gathered), on
@@ -401,10 +469,14 @@ double fe_finish_fits(svo_frontend* fe) {
     fe->pool->run(fe->S, [&](int s) {
         RansacSeq& r = fe->rs[s];
         r.fit(fe->cfg.K, fe->h_stats + 60 * (size_t)s);
+        double* P = &fe->pose[6 * (size_t)s];
         if (r.ok) {
-            std::memcpy(&fe->pose[6 * (size_t)s], r.rvec, sizeof(r.rvec));
-            std::memcpy(&fe->pose[6 * (size_t)s + 3], r.tvec, sizeof(r.tvec));
+            std::memcpy(P, r.rvec, sizeof(r.rvec));
+            std::memcpy(P + 3, r.tvec, sizeof(r.tvec));
+        } else {
+            std::fill(P, P + 6, 0.0);
         }
+        fe_set_pose(fe, s, r.ok, P, P + 3);
     });
     fe->fits_pending = false;
     return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
@@ -418,7 +490,9 @@ int svo_frontend_create(svo_ctx* ctx, const svo_frontend_config* cfg, svo_fronte
     if (!ctx || !cfg || !out) return SVO_ERR_ARG;
     const svo_frontend_config& c = *cfg;
     if (c.width <= 0 || c.height <= 0 || c.n_seq <= 0 || c.n_frames < 2 || c.n_features <= 0 || c.max_level < 0 ||
-        !lk_supported(c.win, c.win) || c.pnp_iterations <= 0 || !(c.pnp_confidence > 0 && c.pnp_confidence < 1) ||
+        !lk_supported(c.win, c.win) || c.stereo_win <= 2 || c.stereo_max_level < 0 ||
+        !lk_supported(c.stereo_win, c.stereo_win) || c.pnp_iterations <= 0 ||
+        !(c.pnp_confidence > 0 && c.pnp_confidence < 1) ||
         (c.bucket_size > 0 && (c.per_bucket <= 0 || c.width / c.bucket_size <= 0)))
         return set_error(ctx, SVO_ERR_ARG, "svo_frontend_create: bad config");
     svo_frontend* fe = new svo_frontend();
@@ -436,70 +510,51 @@ int svo_frontend_create(svo_ctx* ctx, const svo_frontend_config* cfg, svo_fronte
     fe->MAPCAP = fe->CAP * (c.n_frames + 2);
     fe->npx = (size_t)c.width * c.height;
     fe->ml = lk_levels_for_window(c.width, c.height, c.win, c.win, c.max_level);
-    fe->nlev = fe->ml + 1;
+    fe->ml_st = lk_levels_for_window(c.width, c.height, c.stereo_win, c.stereo_win, c.stereo_max_level);
+    fe->nlev = std::max(fe->ml, fe->ml_st) + 1;
     fe->bscr = c.bucket_size > 0 ? bucket_scratch_ints(c.width, c.height, c.bucket_size, c.per_bucket, fe->KCAP) : 1;
     const int S = fe->S, CAP = fe->CAP;
-    // frames
+    // frames: left and right pyramids of every resident stereo pair
     fe->frames.assign((size_t)S * fe->T, nullptr);
-    for (auto& f : fe->frames) {
-        int rc = svo_image_create(ctx, c.width, c.height, fe->ml, &f);
-        if (rc) {
-            svo_frontend_destroy(fe);
-            return rc;
+    fe->frames_r.assign((size_t)S * fe->T, nullptr);
+    for (auto* v : {&fe->frames, &fe->frames_r})
+        for (auto& f : *v) {
+            int rc = svo_image_create(ctx, c.width, c.height, fe->nlev - 1, &f);
+            if (rc) {
+                svo_frontend_destroy(fe);
+                return rc;
+            }
         }
-    }
     fe->desc_host.resize((size_t)fe->T * S);
+    fe->desc_r_host.resize((size_t)fe->T * S);
     for (int t = 0; t < fe->T; t++)
-        for (int s = 0; s < S; s++) fe->desc_host[(size_t)t * S + s] = fe->frames[(size_t)s * fe->T + t]->desc;
-    fe->rot_host.assign((size_t)fe->T * S * 9, 0.0);
-    for (size_t i = 0; i < fe->rot_host.size(); i += 9) fe->rot_host[i] = fe->rot_host[i + 4] = fe->rot_host[i + 8] = 1;
-    fe->seed_host.assign(S, 0);
-    // device state
+        for (int s = 0; s < S; s++) {
+            fe->desc_host[(size_t)t * S + s] = fe->frames[(size_t)s * fe->T + t]->desc;
+            fe->desc_r_host[(size_t)t * S + s] = fe->frames_r[(size_t)s * fe->T + t]->desc;
+        }
+    // device state: one allocation, laid out by the carve sequence below (run once
+    // on a null base to size it)
     size_t bytes = 0;
-    {
-        char* p = nullptr;
-        auto add = [&](size_t b) { p = (char*)(((uintptr_t)p + 255) & ~(uintptr_t)255) + b; };
-        add(sizeof(PyrDesc) * fe->T * S);
-        add(sizeof(float) * 2 * S * CAP * 3);  // xyA next_xy xyB
-        add(sizeof(float) * 3 * S * CAP);      // obj
-        add(sizeof(float) * 3 * (size_t)S * fe->KCAP);
-        add(sizeof(float) * 2 * (size_t)S * fe->BCAP);
-        add(sizeof(int) * S * CAP * 3);  // midA midB iters
-        add(sizeof(int) * S * 16);       // counts
-        add(sizeof(int) * (size_t)S * c.height);
-        add(sizeof(int) * fe->bscr * S);
-        add(sizeof(int) * S * kRansacChunk);
-        add(sizeof(long long) * S);
-        add(S * (size_t)CAP);          // status
-        add(fe->npx * S);              // mask
-        add(sizeof(unsigned long long) * (size_t)S * c.height * ((c.width + 63) / 64));  // FAST keep bits
-        add(sizeof(int) * (size_t)S * c.height);  // rowoff
-        add(sizeof(uint32_t) * (size_t)S * kRansacChunk * fe->WORDS);
-        add(sizeof(uint32_t) * (size_t)S * fe->WORDS);
-        add(sizeof(double) * 3 * (size_t)S * fe->MAPCAP);
-        add(sizeof(double) * 12 * (size_t)S * kRansacChunk);
-        add(sizeof(double) * 9 * (size_t)S * fe->T);
-        add(sizeof(double) * 60 * (size_t)S);
-        add(sizeof(float) * 2 * (size_t)S * CAP);               // box centres binned by band
-        add(sizeof(float) * kSampleFloats * kRansacPrefetch * (size_t)S);
-        add(sizeof(int) * (size_t)S * fast_box_cells(c.width, c.height));
-        add(sizeof(float) * 2 * (size_t)S * CAP);               // second xyB
-        add(sizeof(float) * 3 * (size_t)S * CAP);               // second obj
-        add(sizeof(int) * S);                                   // second nB
-        add(sizeof(uint32_t) * (size_t)S * fe->WORDS);          // second bits_best
-        add(4096);
-        bytes = (size_t)p;
-    }
-    if (hipMalloc(&fe->dmem, bytes) != hipSuccess) {
-        svo_frontend_destroy(fe);
-        return set_error(ctx, SVO_ERR_HIP, "svo_frontend_create: hipMalloc(%zu)", bytes);
-    }
-    {
-        char* p = (char*)fe->dmem;
+    char* const dbase0 = nullptr;
+    for (int pass = 0; pass < 2; pass++) {
+        if (pass == 1) {
+            if (hipMalloc(&fe->dmem, bytes) != hipSuccess) {
+                svo_frontend_destroy(fe);
+                return set_error(ctx, SVO_ERR_HIP, "svo_frontend_create: hipMalloc(%zu)", bytes);
+            }
+        }
+        char* p = pass == 0 ? dbase0 : (char*)fe->dmem;
         fe->d_desc = carve<PyrDesc>(p, (size_t)fe->T * S);
+        fe->d_desc_r = carve<PyrDesc>(p, (size_t)fe->T * S);
         fe->xyA = carve<float>(p, 2 * (size_t)S * CAP);
         fe->next_xy = carve<float>(p, 2 * (size_t)S * CAP);
         fe->xyB = carve<float>(p, 2 * (size_t)S * CAP);
+        fe->st_xy = carve<float>(p, 2 * (size_t)S * CAP);
+        fe->st_next = carve<float>(p, 2 * (size_t)S * CAP);
+        fe->st_status = carve<uint8_t>(p, (size_t)S * CAP);
+        fe->st_n = carve<int>(p, S);
+        fe->pend0 = carve<int>(p, S);
+        fe->pend_n = carve<int>(p, S);
         fe->obj = carve<float>(p, 3 * (size_t)S * CAP);
         fe->kps = carve<float>(p, 3 * (size_t)S * fe->KCAP);
         fe->cand = carve<float>(p, 2 * (size_t)S * fe->BCAP);
@@ -512,32 +567,24 @@ int svo_frontend_create(svo_ctx* ctx, const svo_frontend_config* cfg, svo_fronte
         fe->bn = carve<int>(p, S);
         fe->map_n = carve<int>(p, S);
         fe->added = carve<int>(p, S);
-        fe->seed_d = carve<int>(p, S);
         fe->rowcnt = carve<int>(p, (size_t)S * c.height);
         fe->scr = carve<int>(p, fe->bscr * S);
         fe->cnt = carve<int>(p, (size_t)S * kRansacChunk);
-        fe->itsum = carve<long long>(p, S);
         fe->status = carve<uint8_t>(p, (size_t)S * CAP);
-        fe->mask = carve<uint8_t>(p, fe->npx * S);
         fe->fbits = carve<unsigned long long>(p, (size_t)S * c.height * ((c.width + 63) / 64));
         fe->rowoff = carve<int>(p, (size_t)S * c.height);
         fe->bits_all = carve<uint32_t>(p, (size_t)S * kRansacChunk * fe->WORDS);
-        fe->bits_best = carve<uint32_t>(p, (size_t)S * fe->WORDS);
         fe->map = carve<double>(p, 3 * (size_t)S * fe->MAPCAP);
         fe->hyps = carve<double>(p, 12 * (size_t)S * kRansacChunk);
-        fe->rot_d = carve<double>(p, 9 * (size_t)S * fe->T);
-        fe->stats = carve<double>(p, 60 * (size_t)S);
         fe->box_binned = carve<float>(p, 2 * (size_t)S * CAP);
         fe->box_band = carve<int>(p, (size_t)S * fast_box_cells(c.width, c.height));
-        fe->samp = carve<float>(p, (size_t)kSampleFloats * kRansacPrefetch * S);
         fe->xyB_b[0] = fe->xyB;
         fe->obj_b[0] = fe->obj;
         fe->nB_b[0] = fe->nB;
-        fe->bits_best_b[0] = fe->bits_best;
         fe->xyB_b[1] = carve<float>(p, 2 * (size_t)S * CAP);
         fe->obj_b[1] = carve<float>(p, 3 * (size_t)S * CAP);
         fe->nB_b[1] = carve<int>(p, S);
-        fe->bits_best_b[1] = carve<uint32_t>(p, (size_t)S * fe->WORDS);
+        bytes = (size_t)(p - (pass == 0 ? dbase0 : (char*)fe->dmem)) + 256;
     }
     (void)hipMemsetAsync(fe->dmem, 0, bytes, ctx->stream);
     // host mirrors
@@ -609,7 +656,7 @@ int svo_frontend_create(svo_ctx* ctx, const svo_frontend_config* cfg, svo_fronte
         add(sizeof(uint32_t) * (size_t)S * fe->WORDS);
         add(sizeof(uint32_t) * (size_t)S * fe->WORDS);
         add(sizeof(double) * 60 * (size_t)S);
-        add(sizeof(int) * ((size_t)S + 1));
+        add(sizeof(double) * 12 * (size_t)S);
         add(1024);
         if (hipHostMalloc(&fe->zout, zb, hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess) {
             fe->zout = nullptr;
@@ -627,10 +674,8 @@ int svo_frontend_create(svo_ctx* ctx, const svo_frontend_config* cfg, svo_fronte
         fe->h_best_b[1] = carve<uint32_t>(p, (size_t)S * fe->WORDS);
         fe->h_best = fe->h_best_b[0];
         fe->h_stats = carve<double>(p, 60 * (size_t)S);
-        fe->h_ready = carve<int>(p, (size_t)S + 1);
-        fe->h_fail = fe->h_ready + S;
-        for (int s = 0; s < S; s++) fe->h_ready[s] = -1;
-        *fe->h_fail = 0;
+        fe->h_pose = carve<double>(p, 12 * (size_t)S);
+        for (int s = 0; s < S; s++) fe_set_pose(fe, s, false, nullptr, nullptr);
     }
     // derivative pyramids of three frames of every sequence (t - 1: LK's prev,
     // t, and t + 1, built beside LK(t))
@@ -666,23 +711,12 @@ int svo_frontend_create(svo_ctx* ctx, const svo_frontend_config* cfg, svo_fronte
         fe->fast_early = !(fe_ && fe_[0] == '0');
         const char* ff = std::getenv("SVO_FE_FAST_FIRST");
         fe->fast_first = ff && ff[0] == '1';
-        const char* sp = std::getenv("SVO_FE_STREAM");
-        // default on (one slice); off where kernels are serialised (it needs post_lk
-        // and LK side by side; a timed-out hand-off also turns it off, see step)
-        const char* ser = std::getenv("AMD_SERIALIZE_KERNEL");
-        // and for large per-sequence feature sets (one post_lk block per sequence then
-        // trails LK: 1080p / 8000 and 4K / 16000 features measured 5-7 % slower)
-        fe->stream_post = !(sp && sp[0] == '0') && !(ser && std::atoi(ser) != 0) &&
-                          (fe->CAP <= 4096 || (sp && sp[0] == '1'));
-        fe->stream_mode = sp ? std::atoi(sp) : 1;
     }
     // (on the context stream: a first use of the null stream would take a fifth
     // hardware queue and serialise the step's streams)
-    if (hipMalloc(&fe->score_map, fe->npx * S) != hipSuccess ||
-        hipMalloc(&fe->d_rec, 16 * (size_t)fe->CAP * S) != hipSuccess ||
-        hipMemsetAsync(fe->d_rec, 0, 16 * (size_t)fe->CAP * S, ctx->stream) != hipSuccess) {
+    if (hipMalloc(&fe->score_map, fe->npx * S) != hipSuccess) {
         svo_frontend_destroy(fe);
-        return set_error(ctx, SVO_ERR_HIP, "svo_frontend_create: counter alloc");
+        return set_error(ctx, SVO_ERR_HIP, "svo_frontend_create: score map alloc");
     }
     fe->pose.assign((size_t)S * 6, 0.0);
     int nt = c.host_threads > 0 ? c.host_threads : (int)std::thread::hardware_concurrency();
@@ -716,19 +750,17 @@ int svo_frontend_create(svo_ctx* ctx, const svo_frontend_config* cfg, svo_fronte
                 return set_error(ctx, SVO_ERR_HIP, "svo_frontend_create: stream");
             }
         }
-        // FAST stream priority (SVO_FE_FAST_PRIO: 0 lowest, 1 normal, 2 highest). With
-        // the streamed post-LK the RANSAC chain overlaps LK and FAST(t) gates the
-        // tail, so FAST runs at normal priority (measured +4 % over 60-step runs);
-        // without it, at the lowest
+        // FAST stream priority (SVO_FE_FAST_PRIO: 0 lowest (default: FAST fills the
+        // CUs LK leaves idle and the post-LK window), 1 normal, 2 highest)
         const int normal_pr = std::min(std::max(greatest + 1, greatest), least);
-        int fast_pr = fe->stream_post ? normal_pr : least;
+        int fast_pr = least;
         if (const char* e = std::getenv("SVO_FE_FAST_PRIO"))
             fast_pr = e[0] == '2' ? greatest : e[0] == '1' ? normal_pr : least;
         if (hipStreamCreateWithPriority(&fe->st_fast, hipStreamNonBlocking, fast_pr) != hipSuccess) {
             svo_frontend_destroy(fe);
             return set_error(ctx, SVO_ERR_HIP, "svo_frontend_create: stream");
         }
-        fe->ev_sync.assign(2 + 3 * G, nullptr);
+        fe->ev_sync.assign(2 + 2 * G, nullptr);
         for (auto& e : fe->ev_sync) (void)hipEventCreateWithFlags(&e, hipEventDisableTiming);
         (void)hipEventCreateWithFlags(&fe->ev_stats, hipEventDisableTiming);
         (void)hipEventCreateWithFlags(&fe->ev_gathered, hipEventDisableTiming);
@@ -736,8 +768,7 @@ int svo_frontend_create(svo_ctx* ctx, const svo_frontend_config* cfg, svo_fronte
         for (auto& e : fe->ev_tail) (void)hipEventCreateWithFlags(&e, hipEventDisableTiming);
         for (auto& e : fe->ev_full_b) (void)hipEventCreateWithFlags(&e, hipEventDisableTiming);
         fe->ev_full = fe->ev_full_b[0];
-        (void)hipEventCreateWithFlags(&fe->ev_counts, hipEventDisableTiming);
-        (void)hipEventCreateWithFlags(&fe->ev_prelk, hipEventDisableTiming);
+        (void)hipEventCreateWithFlags(&fe->ev_pyr_r, hipEventDisableTiming);
         // 4 hardware queues: with several slices the copy stream's work shares the
         // pyramid stream
         if (G > 1) {
@@ -750,6 +781,8 @@ int svo_frontend_create(svo_ctx* ctx, const svo_frontend_config* cfg, svo_fronte
     }
     SVO_HIP(ctx, hipMemcpyAsync(fe->d_desc, fe->desc_host.data(), sizeof(PyrDesc) * fe->desc_host.size(),
                                 hipMemcpyHostToDevice, ctx->stream));
+    SVO_HIP(ctx, hipMemcpyAsync(fe->d_desc_r, fe->desc_r_host.data(), sizeof(PyrDesc) * fe->desc_r_host.size(),
+                                hipMemcpyHostToDevice, ctx->stream));
     SVO_HIP(ctx, hipStreamSynchronize(ctx->stream));
     *out = fe;
     return SVO_OK;
@@ -759,8 +792,9 @@ void svo_frontend_destroy(svo_frontend* fe) {
     if (!fe) return;
     if (fe->ctx) (void)hipStreamSynchronize(fe->ctx->stream);
     delete fe->pool;
-    for (auto* f : fe->frames)
-        if (f) svo_image_destroy(fe->ctx, f);
+    for (auto* v : {&fe->frames, &fe->frames_r})
+        for (auto* f : *v)
+            if (f) svo_image_destroy(fe->ctx, f);
     if (fe->dmem) (void)hipFree(fe->dmem);
     if (fe->dermem) (void)hipFree(fe->dermem);
     if (fe->hmem) (void)hipHostFree(fe->hmem);
@@ -789,9 +823,7 @@ void svo_frontend_destroy(svo_frontend* fe) {
         if (e) (void)hipEventDestroy(e);
     for (auto& e : fe->ev_full_b)
         if (e) (void)hipEventDestroy(e);
-    if (fe->ev_counts) (void)hipEventDestroy(fe->ev_counts);
-    if (fe->ev_prelk) (void)hipEventDestroy(fe->ev_prelk);
-    if (fe->d_rec) (void)hipFree(fe->d_rec);
+    if (fe->ev_pyr_r) (void)hipEventDestroy(fe->ev_pyr_r);
     if (fe->score_map) (void)hipFree(fe->score_map);
     delete fe;
 }
@@ -810,54 +842,54 @@ static int fe_drain(svo_frontend* fe) {
     return SVO_OK;
 }
 
-static int fe_set_frame(svo_frontend* fe, int seq, int t, const uint8_t* px, int stride, bool bgr,
-                        const double R[9], int depth_seed) {
-    if (!fe || seq < 0 || seq >= fe->S || t < 0 || t >= fe->T || !px || stride < (bgr ? 3 : 1) * fe->W)
+static int fe_set_frame(svo_frontend* fe, int seq, int t, const uint8_t* left, const uint8_t* right, int stride,
+                        bool bgr) {
+    if (!fe || seq < 0 || seq >= fe->S || t < 0 || t >= fe->T || !left || !right || stride < (bgr ? 3 : 1) * fe->W)
         return SVO_ERR_ARG;
     svo_ctx* ctx = fe->ctx;
     int rd = fe_drain(fe);
     if (rd) return rd;
-    svo_image* im = fe->frames[(size_t)seq * fe->T + t];
     if (fe->pyr_ready >= 0 && fe->pyr_ready % fe->T == t) fe->pyr_ready = -1;  // built from the old image
-    uint8_t* l0 = const_cast<uint8_t*>(im->desc.lv[0].data);
-    if (bgr) {
-        int rc = ingest_bgr(ctx, px, stride, fe->W, fe->H, l0, im->desc.lv[0].pitch);
-        if (rc) return rc;
-    } else {
-        SVO_HIP(ctx, hipMemcpy2DAsync(l0, im->desc.lv[0].pitch, px, stride, fe->W, fe->H, hipMemcpyHostToDevice,
-                                      ctx->stream));
+    for (int side = 0; side < 2; side++) {
+        svo_image* im = (side ? fe->frames_r : fe->frames)[(size_t)seq * fe->T + t];
+        const uint8_t* px = side ? right : left;
+        uint8_t* l0 = const_cast<uint8_t*>(im->desc.lv[0].data);
+        if (bgr) {
+            int rc = ingest_bgr(ctx, px, stride, fe->W, fe->H, l0, im->desc.lv[0].pitch);
+            if (rc) return rc;
+        } else {
+            SVO_HIP(ctx, hipMemcpy2DAsync(l0, im->desc.lv[0].pitch, px, stride, fe->W, fe->H, hipMemcpyHostToDevice,
+                                          ctx->stream));
+        }
     }
-    if (R) {
-        std::memcpy(&fe->rot_host[9 * ((size_t)t * fe->S + seq)], R, sizeof(double) * 9);
-        SVO_HIP(ctx, hipMemcpyAsync(fe->rot_d + 9 * ((size_t)t * fe->S + seq), R, sizeof(double) * 9,
-                                    hipMemcpyHostToDevice, ctx->stream));
-    }
-    fe->seed_host[seq] = depth_seed;
-    SVO_HIP(ctx, hipMemcpyAsync(fe->seed_d + seq, &fe->seed_host[seq], sizeof(int), hipMemcpyHostToDevice,
-                                ctx->stream));
     SVO_HIP(ctx, hipStreamSynchronize(ctx->stream));
     return SVO_OK;
 }
 
-int svo_frontend_set_frame(svo_frontend* fe, int seq, int t, const uint8_t* gray, int stride, const double R[9],
-                           int depth_seed) {
-    return fe_set_frame(fe, seq, t, gray, stride, false, R, depth_seed);
+int svo_frontend_set_frame(svo_frontend* fe, int seq, int t, const uint8_t* left, const uint8_t* right, int stride) {
+    return fe_set_frame(fe, seq, t, left, right, stride, false);
 }
 
-int svo_frontend_set_frame_bgr(svo_frontend* fe, int seq, int t, const uint8_t* bgr, int stride,
-                               const double R[9], int depth_seed) {
-    return fe_set_frame(fe, seq, t, bgr, stride, true, R, depth_seed);
+int svo_frontend_set_frame_bgr(svo_frontend* fe, int seq, int t, const uint8_t* left_bgr, const uint8_t* right_bgr,
+                               int stride) {
+    return fe_set_frame(fe, seq, t, left_bgr, right_bgr, stride, true);
 }
 
 int svo_frontend_prebuild_pyramids(svo_frontend* fe) {
     if (!fe) return SVO_ERR_ARG;
-    for (int t = 0; t < fe->T; t++)
+    for (int t = 0; t < fe->T; t++) {
         SVO_HIP(fe->ctx, launch_pyramid_batched(fe->d_desc + (size_t)t * fe->S, fe->S, fe->W, fe->H, fe->nlev,
                                                 fe->ctx->stream));
+        SVO_HIP(fe->ctx, launch_pyramid_batched(fe->d_desc_r + (size_t)t * fe->S, fe->S, fe->W, fe->H, fe->nlev,
+                                                fe->ctx->stream));
+    }
     SVO_HIP(fe->ctx, hipStreamSynchronize(fe->ctx->stream));
     return SVO_OK;
 }
 
+// Tracking::startStereo's first frame (R:src/tracking.cpp:233-235): extractFeatures
+// (FAST without a mask: prevFrame == frame has no features yet), stereo match,
+// triangulation with the identity pose (Frame's default), capped at n_features.
 int svo_frontend_init(svo_frontend* fe, int t0) {
     if (!fe || t0 < 0) return SVO_ERR_ARG;
     int rd = fe_drain(fe);
@@ -871,35 +903,62 @@ int svo_frontend_init(svo_frontend* fe, int t0) {
     const PyrDesc* dcur = fe->d_desc + (size_t)(t0 % fe->T) * S;
     SVO_HIP(ctx, launch_pyramid_scharr_batched(dcur, fe->d_der + (size_t)(t0 % 3) * S, S, fe->W, fe->H, fe->nlev,
                                                ctx->stream));
+    SVO_HIP(ctx, launch_pyramid_batched(fe->d_desc_r + (size_t)(t0 % fe->T) * S, S, fe->W, fe->H, fe->nlev,
+                                        ctx->stream));
+    SVO_HIP(ctx, hipEventRecord(fe->ev_pyr_r, ctx->stream));
     SVO_HIP(ctx, hipMemsetAsync(fe->nA, 0, sizeof(int) * S, ctx->stream));
     SVO_HIP(ctx, hipMemsetAsync(fe->map_n, 0, sizeof(int) * S, ctx->stream));
+    SVO_HIP(ctx, hipMemsetAsync(fe->pend_n, 0, sizeof(int) * S, ctx->stream));
     int rc = fe_fast_and_bucket(fe, dcur, false, ctx->stream);
     if (rc) return rc;
-    rc = fe_append(fe, t0, 0, S, ctx->stream);
+    // n_in = nA (zero): nothing to compact, the candidates fill the set
+    rc = fe_keyframe(fe, t0, 0, S, fe->nA, nullptr, fe->xyA, fe->midA, fe->cfg.n_features, ctx->stream);
     if (rc) return rc;
-    SVO_HIP(ctx, hipMemcpyAsync(fe->h_nA, fe->nA, sizeof(int) * S, hipMemcpyDeviceToHost, ctx->stream));
+    for (int s = 0; s < S; s++) fe_set_pose(fe, s, false, nullptr, nullptr);
+    SVO_HIP(ctx, launch_finalize_map(fe_pending(fe, 0), S, ctx->stream));
     SVO_HIP(ctx, hipStreamSynchronize(ctx->stream));
     ph_collect(fe);
     std::fill(fe->pose.begin(), fe->pose.end(), 0.0);
     return SVO_OK;
 }
 
-// First half of a step (enqueue only, no host waits): the previous step's side
-// work if still pending, the pyramid of frame t if not built ahead, temporal LK,
-// frame t+1's pyramid, compaction / gather / RANSAC subsets and their D2H, FAST.
-// svo_frontend_step enqueues the next step's first half right after its own
-// tail, so the GPU goes on with LK while the caller is between steps.
 // post_lk's arguments for the sequences [a, a + n) of this step's parity buffers
 static PostLkBatch fe_post_lk_batch(svo_frontend* fe, int a) {
     const int CAP = fe->CAP;
     const size_t sfl = (size_t)kSampleFloats * kRansacPrefetch;
     return PostLkBatch{fe->nA + a, fe->status + (size_t)a * CAP, fe->next_xy + 2 * (size_t)a * CAP,
                        fe->midA + (size_t)a * CAP, fe->iters + (size_t)a * CAP, fe->xyB + 2 * (size_t)a * CAP,
-                       fe->midB + (size_t)a * CAP, fe->nB + a, fe->map + 3 * (size_t)a * fe->MAPCAP, fe->MAPCAP,
-                       fe->obj + 3 * (size_t)a * CAP, CAP, kRansacPrefetch, fe->h_nB + a, fe->h_itsum + a,
-                       fe->h_samp + sfl * a};
+                       fe->midB + (size_t)a * CAP, fe->nB + a, fe_pending(fe, a), fe->obj + 3 * (size_t)a * CAP,
+                       CAP, kRansacPrefetch, fe->h_nB + a, fe->h_itsum + a, fe->h_samp + sfl * a};
 }
 
+// Post-LK of step t on every slice, queued once the previous step's poses are
+// set (fe_finish_fits): its keyframe points go to the world frame first.
+static int fe_post(svo_frontend* fe, int t) {
+    svo_ctx* ctx = fe->ctx;
+    const int G = fe->G;
+    int slot;
+    for (int g = 0; g < G; g++) {
+        hipStream_t sg = fe->gst[g];
+        ph_begin(fe, PH_POST, sg, &slot);
+        SVO_HIP(ctx, launch_post_lk(fe_post_lk_batch(fe, fe->g0[g]), fe->gn[g], sg));
+        ph_end(fe, sg, slot);
+        SVO_HIP(ctx, hipEventRecord(fe->ev_sync[3 + 2 * g], sg));
+    }
+    // every slice's points are gathered once the last slice's post-LK is done
+    SVO_HIP(ctx, hipEventRecord(fe->ev_gathered, fe->gst[G - 1]));
+    for (int g = 0; g + 1 < G; g++) SVO_HIP(ctx, hipStreamWaitEvent(fe->st_copy, fe->ev_sync[3 + 2 * g], 0));
+    // the full point set for the final fits / long RANSAC runs, on the copy stream
+    // (parity buffers: the previous step's fits still read theirs)
+    (void)t;
+    return fe_queue_full(fe);
+}
+
+// First half of a step (enqueue only, no host waits): the previous step's side
+// work if still pending, the pyramid of frame t if not built ahead, temporal LK,
+// FAST, the right pyramid of frame t and frame t+1's left pyramid.
+// svo_frontend_step enqueues the next step's first half right after its own
+// tail, so the GPU goes on with LK while the caller is between steps.
 static int fe_front_lk(svo_frontend* fe, int t) {
     svo_ctx* ctx = fe->ctx;
     hipStream_t st0 = ctx->stream;
@@ -914,7 +973,6 @@ static int fe_front_lk(svo_frontend* fe, int t) {
     fe->obj = fe->obj_b[t & 1];
     fe->nB = fe->nB_b[t & 1];
     fe->h_best = fe->h_best_b[t & 1];
-    fe->bits_best = fe->h_best;  // the statistics kernel reads the host-coherent bits
     fe->h_xyB = fe->h_xyB_b[t & 1];
     fe->h_obj = fe->h_obj_b[t & 1];
     fe->ev_full = fe->ev_full_b[t & 1];
@@ -973,44 +1031,14 @@ static int fe_front_lk(svo_frontend* fe, int t) {
         if (rc) return rc;
         SVO_HIP(ctx, hipEventRecord(fe->ev_sync[1], sf));
     }
-    // streamed post-LK: one slice and the four-per-wave kernel (the one that counts)
-    fe->sp_active = fe->stream_post && G == 1 && lp.quad && lp.multi != 0 && !fe->frames.empty();
     for (int g = 0; g < G; g++) {
         const int a = fe->g0[g], n = fe->gn[g];
         hipStream_t sg = fe->gst[g];
         const int mp = CAP;  // grid bound: the host counts of the previous tail may not be back yet
         SVO_HIP(ctx, hipStreamWaitEvent(sg, ev_pyr, 0));
-
         LKBatch lb{dprev + a, dcur + a, fe->d_der + (size_t)((t - 1) % 3) * S + a, fe->xyA + 2 * (size_t)a * CAP,
                    fe->next_xy + 2 * (size_t)a * CAP, fe->status + (size_t)a * CAP, nullptr,
                    fe->iters + (size_t)a * CAP, fe->nA + a, 0, CAP};
-        if (fe->sp_active) {
-            // post_lk goes first, on the copy stream, behind everything LK(t) waits
-            // for (the previous tail): it waits on the device for each sequence's LK
-            PostLkBatch pb = fe_post_lk_batch(fe, a);
-            fe->lk_stamp = fe->lk_stamp % 255 + 1;
-            pb.rec = fe->d_rec + 4 * (size_t)a * CAP;
-            pb.lk_stamp = fe->lk_stamp;
-            pb.h_ready = fe->h_ready + a;
-            pb.stamp = t;
-            pb.h_fail = fe->h_fail;
-            lb.rec = fe->d_rec + 4 * (size_t)a * CAP;
-            lb.stamp = fe->lk_stamp;
-            if (fe->stream_mode == 2) {
-                ph_begin(fe, PH_LK, sg, &slot);
-                SVO_HIP(ctx, launch_lk(lb, n, mp, lp, sg));
-                ph_end(fe, sg, slot);
-                SVO_HIP(ctx, hipEventRecord(fe->ev_sync[2 + 2 * g], sg));
-                SVO_HIP(ctx, hipStreamWaitEvent(fe->st_copy, fe->ev_sync[2 + 2 * g], 0));
-                SVO_HIP(ctx, launch_post_lk(pb, n, fe->st_copy));
-                SVO_HIP(ctx, hipEventRecord(fe->ev_sync[3 + 2 * g], fe->st_copy));
-                continue;
-            }
-            SVO_HIP(ctx, hipEventRecord(fe->ev_prelk, sg));
-            SVO_HIP(ctx, hipStreamWaitEvent(fe->st_copy, fe->ev_prelk, 0));
-            SVO_HIP(ctx, launch_post_lk(pb, n, fe->st_copy));
-            SVO_HIP(ctx, hipEventRecord(fe->ev_sync[3 + 2 * g], fe->st_copy));
-        }
         ph_begin(fe, PH_LK, sg, &slot);
         SVO_HIP(ctx, launch_lk(lb, n, mp, lp, sg));
         ph_end(fe, sg, slot);
@@ -1031,6 +1059,12 @@ static int fe_front_lk(svo_frontend* fe, int t) {
     //     derivative pyramids are triple-buffered (frame f in f % 3), so nothing
     //     this step reads is overwritten, and the memory-bound pyramid shares the
     //     GPU with the VALU-bound LK instead of the post-LK window
+    // 3''. the right frame t's pyramid (no derivatives: it is the stereo LK's next
+    //      image), beside LK; the keyframe's stereo LK waits for ev_pyr_r
+    ph_begin(fe, PH_PYR_R, st0, &slot);
+    SVO_HIP(ctx, launch_pyramid_batched(fe->d_desc_r + (size_t)(t % fe->T) * S, S, fe->W, fe->H, fe->nlev, st0));
+    ph_end(fe, st0, slot);
+    SVO_HIP(ctx, hipEventRecord(fe->ev_pyr_r, st0));
     if (fe->pyr_early) {
         const int tn = t + 1;
         const PyrDesc* dnext = fe->d_desc + (size_t)(tn % fe->T) * S;
@@ -1044,18 +1078,15 @@ static int fe_front_lk(svo_frontend* fe, int t) {
     return SVO_OK;
 }
 
-// The rest of a step's first half: frame t+1's pyramid, compaction / gather /
-// RANSAC subsets and their D2H, the full point copy, FAST.
+// The rest of a step's first half: frame t+1's pyramid (SVO_FE_PYR_EARLY=0) and
+// FAST (SVO_FE_FAST_EARLY=0) after every LK of the step.
 static int fe_front_rest(svo_frontend* fe, int t) {
     svo_ctx* ctx = fe->ctx;
     hipStream_t st0 = ctx->stream;
-    const int S = fe->S, CAP = fe->CAP, G = fe->G;
+    const int S = fe->S, G = fe->G;
     const PyrDesc* dcur = fe->d_desc + (size_t)(t % fe->T) * S;
     hipEvent_t ev_fast = fe->ev_sync[1];
     int slot;
-    // 3b'. (SVO_FE_PYR_EARLY=0 only) build frame t+1's pyramid + Scharr ahead once
-    //      every LK of this step is done: it then runs beside FAST while the host
-    //      solves RANSAC. Used if the next step is t+1; ev_pyr records its end.
     if (!fe->pyr_early) {
         fe->pyr_ready = -1;
         const int tn = t + 1;
@@ -1068,44 +1099,6 @@ static int fe_front_rest(svo_frontend* fe, int t) {
         SVO_HIP(ctx, hipEventRecord(fe->ev_sync[0], st0));
         fe->pyr_ready = tn;
     }
-    for (int g = 0; g < G && fe->sp_active; g++) {
-        // streamed: post_lk is already queued; the scoring and the tail (slice
-        // stream) read its outputs
-        SVO_HIP(ctx, hipStreamWaitEvent(fe->gst[g], fe->ev_sync[3 + 2 * g], 0));
-    }
-    for (int g = 0; g < G && !fe->sp_active; g++) {
-        const int a = fe->g0[g], n = fe->gn[g];
-        hipStream_t sg = fe->gst[g];
-        // keep status == 1 (R:src/tracking.cpp:169-175), gather the map points, draw
-        // and gather the first RANSAC subsets (the host needs ~100 B per hypothesis
-        // instead of the whole point set): one kernel, outputs the host reads written
-        // straight to host-coherent memory
-        const size_t sfl = (size_t)kSampleFloats * kRansacPrefetch;
-        PostLkBatch pb{fe->nA + a, fe->status + (size_t)a * CAP, fe->next_xy + 2 * (size_t)a * CAP,
-                       fe->midA + (size_t)a * CAP, fe->iters + (size_t)a * CAP, fe->xyB + 2 * (size_t)a * CAP,
-                       fe->midB + (size_t)a * CAP, fe->nB + a, fe->map + 3 * (size_t)a * fe->MAPCAP, fe->MAPCAP,
-                       fe->obj + 3 * (size_t)a * CAP, CAP, kRansacPrefetch, fe->h_nB + a, fe->h_itsum + a,
-                       fe->h_samp + sfl * a};
-        ph_begin(fe, PH_COMPACT, sg, &slot);
-        SVO_HIP(ctx, launch_post_lk(pb, n, sg));
-        ph_end(fe, sg, slot);
-        SVO_HIP(ctx, hipEventRecord(fe->ev_sync[3 + 2 * g], sg));
-    }
-    // every slice's points are gathered once the last slice's copies are queued
-    // (slices run in order on their streams; the full copy waits for the last)
-    SVO_HIP(ctx, hipEventRecord(fe->ev_gathered, fe->sp_active ? fe->st_copy : fe->gst[G - 1]));
-    for (int g = 0; g + 1 < G; g++) SVO_HIP(ctx, hipStreamWaitEvent(fe->st_copy, fe->ev_sync[3 + 2 * g], 0));
-
-    // the full point set for the final fits / long RANSAC runs, on the copy
-    // stream behind the subsets' D2H (parity buffers: the previous step's fits
-    // still read theirs)
-    {
-        int rq = fe_queue_full(fe);
-        if (rq) return rq;
-    }
-
-    // 3b. (SVO_FE_FAST_EARLY=0 only) mask around frame t-1's features + FAST/bucket
-    //     on frame t after every LK of the step
     if (!fe->fast_early) {
         hipStream_t sf = fe->st_fast;
         for (int g = 0; g < G; g++) SVO_HIP(ctx, hipStreamWaitEvent(sf, fe->ev_sync[2 + 2 * g], 0));
@@ -1147,10 +1140,16 @@ int svo_frontend_step(svo_frontend* fe, int t, svo_frontend_stats* stats) {
     }
     fe->front_t = -1;
     TP("front enqueued");
-    // the previous step's final pose fits, deferred to here: the host does them
-    // while the GPU tracks this frame
+    // the previous step's final pose fits: the host does them while the GPU tracks
+    // this frame; they set the poses that move the previous keyframe's new map
+    // points to the world frame, so this step's post-LK is queued right after
     double ms_fit = fe_finish_fits(fe);
     TP("fits done");
+    {
+        int rp = fe_post(fe, t);
+        if (rp) return rp;
+    }
+    TP("post-lk queued");
     hipEvent_t ev_fast = fe->ev_sync[1];
     hipStream_t sf = fe->st_fast;
     int rc = SVO_OK;
@@ -1166,75 +1165,20 @@ int svo_frontend_step(svo_frontend* fe, int t, svo_frontend_stats* stats) {
     std::vector<int> ms(S, 0);
 
     // 4. per slice, in order: calculatePose (RANSAC per sequence, hypotheses
-    //    scored on the GPU), drop outliers (R:src/tracking.cpp:218-229), top up
+    //    scored on the GPU), drop outliers (R:src/tracking.cpp:218-229), keyframe
     for (int g = 0; g < G; g++) {
         const int a = fe->g0[g], n = fe->gn[g];
         hipStream_t sg = fe->gst[g];
         hipStream_t sq = sg;  // the slice stream is idle while the host solves RANSAC
         TP("ransac begin");
         auto tw = clk::now();
-        bool pre_ok = fe->sp_active;  // the streamed pre-pass produced this round's chunks
-        if (pre_ok) {
-            // streamed: each sequence's first hypothesis chunk as soon as its post-LK
-            // results land (h_ready), while LK still runs for later sequences
-            const int* rdy = fe->h_ready;
-            const int* fail = fe->h_fail;
-            std::atomic<bool> late{false};
-            const auto t_wait = clk::now();
-            fe->pool->run(n, [&](int i) {
-                const int s = a + i;
-                // bounded: the device side gives up after ~1 s (h_fail); the host after 2 s
-                for (unsigned k = 0; __atomic_load_n(rdy + s, __ATOMIC_ACQUIRE) != t; k++) {
-                    if (__atomic_load_n(fail, __ATOMIC_ACQUIRE) || late.load(std::memory_order_relaxed)) return;
-                    if ((k & 1023u) == 1023u && ms_since(t_wait) > 2000.0) {
-                        late.store(true);
-                        return;
-                    }
-                    __builtin_ia32_pause();
-                }
-                RansacSeq& r = fe->rs[s];
-                r.begin(fe->h_obj + 3 * (size_t)s * CAP, fe->h_xyB + 2 * (size_t)s * CAP, fe->h_nB[s],
-                        c.pnp_iterations);
-                r.samp = fe->h_samp + (size_t)kSampleFloats * kRansacPrefetch * s;
-                r.nsamp = kRansacPrefetch;
-                r.first_chunk = std::max(fe->chunk0, fe->pred_iters[s]);
-                ms[s] = (!r.direct && !r.done && r.next_end() <= r.nsamp) ? r.gen_chunk(c.K) : 0;
-            });
-            if (*fe->h_fail || late.load()) {
-                // the hand-off needs post_lk and LK to run side by side; where kernels
-                // are serialised (a profiler's counter pass, AMD_SERIALIZE_KERNEL) the
-                // device wait times out: this step's post-LK re-runs behind LK (the
-                // records are complete then) and the mode stays off from here on
-                SVO_HIP(ctx, hipEventSynchronize(fe->ev_sync[3 + 2 * g]));
-                if (!*fe->h_fail) return set_error(ctx, SVO_ERR_HIP, "svo_frontend_step: streamed post-LK lost");
-                fe->stream_post = false;
-                *fe->h_fail = 0;
-                PostLkBatch pb = fe_post_lk_batch(fe, a);
-                pb.rec = fe->d_rec + 4 * (size_t)a * CAP;
-                pb.lk_stamp = fe->lk_stamp;
-                SVO_HIP(ctx, launch_post_lk(pb, n, fe->gst[g]));
-                SVO_HIP(ctx, hipEventRecord(fe->ev_sync[3 + 2 * g], fe->gst[g]));
-                SVO_HIP(ctx, hipEventRecord(fe->ev_gathered, fe->gst[g]));
-                fe->full_queued = false;
-                SVO_HIP(ctx, hipEventSynchronize(fe->ev_sync[3 + 2 * g]));
-                pre_ok = false;
-            } else {
-                SVO_HIP(ctx, hipEventSynchronize(fe->ev_sync[3 + 2 * g]));  // post_lk's device outputs (done by now)
-            }
-        } else {
-            SVO_HIP(ctx, hipEventSynchronize(fe->ev_sync[3 + 2 * g]));
-        }
+        SVO_HIP(ctx, hipEventSynchronize(fe->ev_sync[3 + 2 * g]));
         TP("lk results on host");
         ms_wait += ms_since(tw);
         int max_b = 0;
         bool need_full = false;
         for (int s = a; s < a + n; s++) {
             RansacSeq& r = fe->rs[s];
-            if (pre_ok) {
-                need_full |= r.direct && !r.done;
-                max_b = std::max(max_b, fe->h_nB[s]);
-                continue;
-            }
             r.begin(fe->h_obj + 3 * (size_t)s * CAP, fe->h_xyB + 2 * (size_t)s * CAP, fe->h_nB[s], c.pnp_iterations);
             r.samp = fe->h_samp + (size_t)kSampleFloats * kRansacPrefetch * s;
             r.nsamp = kRansacPrefetch;
@@ -1260,25 +1204,21 @@ int svo_frontend_step(svo_frontend* fe, int t, svo_frontend_stats* stats) {
             int rf = ensure_full();
             if (rf) return rf;
         }
-        bool first = pre_ok;  // the first round's chunks are already generated
         for (;;) {
-            if (!first) {
-                // sequences still sampling (no pool dispatch once all are done)
-                bool any = false;
-                for (int s = a; s < a + n; s++) {
-                    any |= !fe->rs[s].done && !fe->rs[s].direct;
-                    need_full |= fe->rs[s].next_end() > fe->rs[s].nsamp;
-                }
-                if (!any) break;
-                if (need_full) {  // past the prefetched subsets (> 26 hypotheses): rare
-                    int rf = ensure_full();
-                    if (rf) return rf;
-                }
-                auto th = clk::now();
-                fe->pool->run(n, [&](int i) { ms[a + i] = fe->rs[a + i].gen_chunk(c.K); });
-                ms_hyp += ms_since(th);
+            // sequences still sampling (no pool dispatch once all are done)
+            bool any = false;
+            for (int s = a; s < a + n; s++) {
+                any |= !fe->rs[s].done && !fe->rs[s].direct;
+                need_full |= fe->rs[s].next_end() > fe->rs[s].nsamp;
             }
-            first = false;
+            if (!any) break;
+            if (need_full) {  // past the prefetched subsets (> 26 hypotheses): rare
+                int rf = ensure_full();
+                if (rf) return rf;
+            }
+            auto th = clk::now();
+            fe->pool->run(n, [&](int i) { ms[a + i] = fe->rs[a + i].gen_chunk(c.K); });
+            ms_hyp += ms_since(th);
             TP("hyps generated");
             int mmax = 0;
             for (int s = a; s < a + n; s++) mmax = std::max(mmax, ms[s]);
@@ -1333,9 +1273,9 @@ int svo_frontend_step(svo_frontend* fe, int t, svo_frontend_stats* stats) {
                     const int nw = (fe->h_nB[s] + 63) / 64;
                     for (int j = 0; j < ms[s]; j++) {
                         const int* wc = fe->z_wcnt + ((size_t)s * kRansacChunk + j) * fe->WS;
-                        int t = 0;
-                        for (int w = 0; w < nw; w++) t += wc[w];
-                        cnts[j] = t;
+                        int tt = 0;
+                        for (int w = 0; w < nw; w++) tt += wc[w];
+                        cnts[j] = tt;
                     }
                 }
                 fe->rs[s].consume(cnts, bits, fe->WORDS, c.pnp_confidence);
@@ -1345,9 +1285,12 @@ int svo_frontend_step(svo_frontend* fe, int t, svo_frontend_stats* stats) {
         // SQPnP-objective fit only refines the pose, from statistics summed on the GPU
         TP("consumed");
         auto tf = clk::now();
+        int max_take = 0;  // the keyframe's candidates per sequence are at most n_features - kept
         for (int s = a; s < a + n; s++) {
             RansacSeq& r = fe->rs[s];
             r.select(c.K, false);
+            const int kept = r.ok ? r.maxGood : (r.n < 4 ? r.n : 0);
+            max_take = std::max(max_take, c.n_features - kept);
             uint32_t* b = fe->h_best + (size_t)s * fe->WORDS;
             std::memset(b, 0, sizeof(uint32_t) * fe->WORDS);
             if (r.ok) {
@@ -1372,15 +1315,13 @@ int svo_frontend_step(svo_frontend* fe, int t, svo_frontend_stats* stats) {
         fe->stats_parity = t & 1;
         // the mask (reads xyA) and FAST (writes kps) must be done before xyA is rewritten / kps read
         SVO_HIP(ctx, hipStreamWaitEvent(sg, ev_fast, 0));
-        // drop the outliers (R:src/tracking.cpp:218-229; the kernel reads the inlier
-        // bits from host-coherent memory) and top up to n_features, one kernel
-        TailBatch tb{fe->nB + a, fe->h_best + (size_t)a * fe->WORDS, fe->WORDS, fe->xyB + 2 * (size_t)a * CAP,
-                     fe->midB + (size_t)a * CAP, fe->h_nA + a, fe->h_added + a};
-        ph_begin(fe, PH_APPEND, sg, &slot);
-        SVO_HIP(ctx, launch_tail(tb, fe_append_batch(fe, t, a), n, sg));
-        ph_end(fe, sg, slot);
+        // drop the outliers (the kernel reads the inlier bits from host-coherent
+        // memory), then the keyframe: candidates, stereo LK, triangulation, append
+        rc = fe_keyframe(fe, t, a, n, fe->nB + a, fe->h_best + (size_t)a * fe->WORDS, fe->xyB + 2 * (size_t)a * CAP,
+                         fe->midB + (size_t)a * CAP, max_take, sg);
+        if (rc) return rc;
         SVO_HIP(ctx, hipEventRecord(fe->ev_tail[g], sg));
-        TP("compact+append queued");
+        TP("tail queued");
     }
     fe->fits_pending = true;  // statistics land with the stream syncs below
     fe->fit_parity = t & 1;
@@ -1409,13 +1350,7 @@ int svo_frontend_step(svo_frontend* fe, int t, svo_frontend_stats* stats) {
     rc = fe_queue_stats(fe);
     if (rc) return rc;
     if (ahead) {
-        rc = fe_front_lk(fe, t + 1);
-        if (rc) return rc;
-    }
-    TP("next lk queued");
-    TP("tail enqueued");
-    if (ahead) {
-        rc = fe_front_rest(fe, t + 1);
+        rc = fe_front(fe, t + 1);
         if (rc) return rc;
         fe->front_t = t + 1;
     }
@@ -1456,6 +1391,10 @@ int svo_frontend_synchronize(svo_frontend* fe) {
     if (fe->st_fast) SVO_HIP(ctx, hipStreamSynchronize(fe->st_fast));
     SVO_HIP(ctx, hipStreamSynchronize(ctx->stream));
     fe_finish_fits(fe);
+    // the last keyframe's map points to the world frame (the next post-LK finds
+    // nothing pending then)
+    SVO_HIP(ctx, launch_finalize_map(fe_pending(fe, 0), fe->S, ctx->stream));
+    SVO_HIP(ctx, hipStreamSynchronize(ctx->stream));
     return SVO_OK;
 }
 
@@ -1476,11 +1415,65 @@ int svo_frontend_features(svo_frontend* fe, int seq, float* xy, int cap, int* n)
     SVO_HIP(ctx, hipMemcpyAsync(&cnt, fe->nA + seq, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
     SVO_HIP(ctx, hipStreamSynchronize(ctx->stream));
     const int k = std::min(cnt, cap);
-    if (k > 0 && xy)
+    if (k > 0 && xy) {
         SVO_HIP(ctx, hipMemcpyAsync(xy, fe->xyA + 2 * (size_t)seq * fe->CAP, sizeof(float) * 2 * k,
                                     hipMemcpyDeviceToHost, ctx->stream));
         SVO_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    }
     if (n) *n = cnt;
+    return SVO_OK;
+}
+
+int svo_frontend_map_points(svo_frontend* fe, int seq, double* xyz, int cap, int* n) {
+    if (!fe || seq < 0 || seq >= fe->S || cap < 0 || (cap > 0 && !xyz)) return SVO_ERR_ARG;
+    int rc = svo_frontend_synchronize(fe);
+    if (rc) return rc;
+    svo_ctx* ctx = fe->ctx;
+    int cnt = 0, mn = 0;
+    SVO_HIP(ctx, hipMemcpyAsync(&cnt, fe->nA + seq, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
+    SVO_HIP(ctx, hipMemcpyAsync(&mn, fe->map_n + seq, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
+    SVO_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    std::vector<int> mid((size_t)cnt);
+    std::vector<double> map(3 * (size_t)mn);
+    if (cnt > 0)
+        SVO_HIP(ctx, hipMemcpyAsync(mid.data(), fe->midA + (size_t)seq * fe->CAP, sizeof(int) * cnt,
+                                    hipMemcpyDeviceToHost, ctx->stream));
+    if (mn > 0)
+        SVO_HIP(ctx, hipMemcpyAsync(map.data(), fe->map + 3 * (size_t)seq * fe->MAPCAP, sizeof(double) * 3 * mn,
+                                    hipMemcpyDeviceToHost, ctx->stream));
+    SVO_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    for (int i = 0; i < std::min(cnt, cap); i++) {
+        if (mid[i] < 0 || mid[i] >= mn) return set_error(ctx, SVO_ERR_HIP, "svo_frontend_map_points: bad map id");
+        std::memcpy(xyz + 3 * (size_t)i, &map[3 * (size_t)mid[i]], sizeof(double) * 3);
+    }
+    if (n) *n = cnt;
+    return SVO_OK;
+}
+
+int svo_frontend_time_pyramid(svo_frontend* fe, int t, int reps, double* ms_per_launch) {
+    if (!fe || t < 0 || reps <= 0 || !ms_per_launch) return SVO_ERR_ARG;
+    int rc = svo_frontend_synchronize(fe);
+    if (rc) return rc;
+    svo_ctx* ctx = fe->ctx;
+    const int S = fe->S;
+    const PyrDesc* d = fe->d_desc + (size_t)(t % fe->T) * S;
+    const DerivDesc* dd = fe->d_der + (size_t)(t % 3) * S;
+    hipEvent_t e0, e1;
+    SVO_HIP(ctx, hipEventCreate(&e0));
+    SVO_HIP(ctx, hipEventCreate(&e1));
+    // one untimed rebuild first (caches warm, identical contents)
+    SVO_HIP(ctx, launch_pyramid_scharr_batched(d, dd, S, fe->W, fe->H, fe->nlev, ctx->stream));
+    SVO_HIP(ctx, hipEventRecord(e0, ctx->stream));
+    for (int i = 0; i < reps; i++)
+        SVO_HIP(ctx, launch_pyramid_scharr_batched(d, dd, S, fe->W, fe->H, fe->nlev, ctx->stream));
+    SVO_HIP(ctx, hipEventRecord(e1, ctx->stream));
+    SVO_HIP(ctx, hipEventSynchronize(e1));
+    float ms = 0.f;
+    SVO_HIP(ctx, hipEventElapsedTime(&ms, e0, e1));
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    *ms_per_launch = ms / reps;
+    fe->pyr_ready = -1;
     return SVO_OK;
 }
 

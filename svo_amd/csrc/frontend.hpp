@@ -5,37 +5,29 @@
 
 namespace svo {
 
-struct CompactBatch {
-    const int* n_in;
-    const uint8_t* status;  // either status (u8 per point) ...
-    const uint32_t* bits;   // ... or a bitmask (words_cap words per sequence)
-    int words_cap;
-    const float* xy_in;
-    const int* mid_in;
-    const int* iters;        // nullable: per-point LK iterations to sum
-    long long* iters_sum;    // nullable: per-sequence sum
-    float* xy_out;
-    int* mid_out;
-    int* n_out;
-    int cap;
+// Keyframe map points of the previous step are stored in the left camera frame
+// of their keyframe until that frame's pose is known (the host's final SQPnP fit
+// runs while the GPU tracks the next frame): map[pend0[s] .. pend0[s] + pend_n[s])
+// of sequence s are moved to the world frame by pose[s] = {R (row-major 3x3),
+// t} (camera -> world, Frame::pose(), R:src/tracking.cpp:141) before anything
+// reads them; pend_n[s] is zeroed then, so the step is idempotent.
+struct PendingMap {
+    double* map;         // [s][map_cap] xyz
+    int map_cap;
+    const int* pend0;    // [s]
+    int* pend_n;         // [s]
+    const double* pose;  // [s][12], host-coherent
 };
-hipError_t launch_compact(const CompactBatch& b, int nseq, hipStream_t st);
-hipError_t launch_gather(const int* n, const int* mid, const double* map, int cap, int map_cap, float* obj,
-                         int nseq, int max_n, hipStream_t st);
 
-// The 5-point subsets of the first nh (<= 64) RANSAC hypotheses of every
-// sequence (cv::RNG(-1) draws over counts[s] points), gathered as obj[5][3] +
-// img[5][2] floats per hypothesis into samp[s][nh][25].
-hipError_t launch_ransac_samples(const int* counts, const float* obj, const float* img, int cap, int nh, int nseq,
-                                 float* samp, hipStream_t st);
-
-// Everything between temporal LK and the host's RANSAC, one 1024-thread block
-// per sequence: stable compaction of the tracked features (status == 1) into
-// xy_out / mid_out / n_out, the LK iteration sum, the map-point gather into obj
-// (float, as solvePnPRansac converts), and the 5-point subsets of the first nh
-// RANSAC hypotheses (cv::RNG(-1) draws over the new count) gathered as
-// obj[5][3] + img[5][2] floats. h_n / h_iters / h_samp are host-coherent
-// (zero-copy): the host reads them once the kernel is done.
+// Everything between temporal LK and the host's RANSAC, one block per
+// sequence: the pending keyframe map points to the world frame (PendingMap),
+// stable compaction of the tracked features (status == 1,
+// R:src/tracking.cpp:169-175) into xy_out / mid_out / n_out, the LK iteration
+// sum, the map-point gather into obj (float, as solvePnPRansac converts
+// Point3d, :182-187), and the 5-point subsets of the first nh RANSAC hypotheses
+// (cv::RNG(-1) draws over the new count) gathered as obj[5][3] + img[5][2]
+// floats. h_n / h_iters / h_samp are host-coherent (zero-copy): the host reads
+// them once the kernel is done.
 struct PostLkBatch {
     const int* n_in;
     const uint8_t* status;
@@ -45,56 +37,69 @@ struct PostLkBatch {
     float* xy_out;
     int* mid_out;
     int* n_out;
-    const double* map;
-    int map_cap;
+    PendingMap pm;
     float* obj;
     int cap, nh;
     int* h_n;
     long long* h_iters;
     float* h_samp;  // [s][nh][25]
-    // streamed mode (rec != null): the block of sequence s first waits until all
-    // n_in LK records (LKBatch::rec) of s show lk_stamp, reads them with sc1
-    // loads, and at its end publishes h_ready[s] = stamp (system scope) after its
-    // host-coherent writes; h_fail[0] = 1 if the wait timed out
-    const unsigned* rec = nullptr;
-    int lk_stamp = 0;
-    int* h_ready = nullptr;
-    int stamp = 0;
-    int* h_fail = nullptr;
 };
 hipError_t launch_post_lk(const PostLkBatch& b, int nseq, hipStream_t st);
+// PendingMap alone (before the map is read by anything but post_lk)
+hipError_t launch_finalize_map(const PendingMap& pm, int nseq, hipStream_t st);
 
-// The step's tail, one block per sequence: stable compaction by the RANSAC
-// inlier bits (read from host-coherent memory), then the keyframe top-up
-// (append_kernel's body). h_n / h_added: host-coherent copies of the counts.
+// The step's tail, part 1, one block per sequence: stable compaction by the
+// RANSAC inlier bits (read from host-coherent memory; R:src/tracking.cpp:218-229)
+// into xy_out / mid_out / n_out, then the keyframe's new-feature candidates: the
+// first take = min(n_target - n, candidates, capacity) masked FAST corners
+// (extractFeatures, :74-92), copied to st_xy (the stereo LK's input) with their
+// count in st_n.
 struct TailBatch {
     const int* n_in;
     const uint32_t* bits;  // [s][words_cap], host-coherent
     int words_cap;
     const float* xy_in;
     const int* mid_in;
-    int* h_n;
-    int* h_added;
-};
-
-struct AppendBatch {
-    int* n;             // features per sequence (in/out)
-    float* xy;          // [s][cap] xy
-    int* mid;           // [s][cap]
+    float* xy_out;
+    int* mid_out;
+    int* n_out;
     int cap, n_target;
     const float* cand;  // candidates, cand_elem floats each, cand_cap per sequence
     int cand_elem, cand_cap;
     const int* cand_n;
-    double* map;        // [s][map_cap] xyz
+    const int* map_n;
+    int map_cap;
+    float* st_xy;  // [s][cap]
+    int* st_n;     // [s]
+};
+hipError_t launch_tail(const TailBatch& tb, int nseq, hipStream_t st);
+
+// The step's tail, part 2 (after the stereo LK of st_xy into the right image),
+// one block per sequence: findLeftFeaturesInRight's filter (status and
+// |yR - yL| < y_threshold, R:src/tracking.cpp:109-114), triangulateNewMapPoints'
+// DLT with P_left / P_right and z > 0 (:120-152), and the survivors appended in
+// order as new features with new map points (left camera frame, pending the
+// frame's pose: PendingMap). h_n / h_added: host-coherent copies of the counts.
+struct AppendBatch {
+    int* n;       // features per sequence (in/out)
+    float* xy;    // [s][cap]
+    int* mid;     // [s][cap]
+    int cap;
+    const float* st_xy;      // [s][cap] left points
+    const float* st_next;    // [s][cap] right points (stereo LK)
+    const uint8_t* st_status;
+    const int* st_n;
+    float y_threshold;
+    float P[24];  // P_left, P_right
+    double* map;  // [s][map_cap]
     int* map_n;
     int map_cap;
-    const double* rot;  // [s] 3x3 world->camera of this frame
-    const int* depth_seed;
-    int* added;         // nullable
-    double K[9];
+    int* pend0;
+    int* pend_n;
+    int* added;   // nullable
+    int* h_n;     // nullable, host-coherent
+    int* h_added; // nullable, host-coherent
 };
 hipError_t launch_append(const AppendBatch& b, int nseq, hipStream_t st);
-// compaction (TailBatch: into ab.xy / ab.mid / ab.n) + top-up (AppendBatch)
-hipError_t launch_tail(const TailBatch& tb, const AppendBatch& ab, int nseq, hipStream_t st);
 
 }  // namespace svo

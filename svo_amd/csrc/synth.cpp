@@ -4,8 +4,10 @@
 // at ANY depth along a canvas ray reprojects exactly (no stereo needed to make
 // consistent 3D points). The reference reads KITTI PNGs instead
 // (R:include/async_image_loader.h:57-69); KITTI is not available here.
+#include <algorithm>
 #include <cmath>
 #include <cstring>
+#include <thread>
 #include <vector>
 
 #include "svo_gpu.h"
@@ -21,6 +23,20 @@ inline uint64_t splitmix(uint64_t& s) {
 inline uint64_t hash3(uint64_t seed, uint64_t a, uint64_t b) {
     uint64_t s = seed ^ (a * 0x9E3779B97F4A7C15ULL) ^ (b * 0xC2B2AE3D27D4EB4FULL);
     return splitmix(s);
+}
+
+// rows [0, h) in contiguous bands on up to 16 host threads (deterministic: each
+// pixel depends on its own coordinates only)
+template <class F>
+void for_rows(int h, F f) {
+    const int nt = std::max(1, std::min({16, (int)std::thread::hardware_concurrency(), h / 16}));
+    if (nt == 1) {
+        f(0, h);
+        return;
+    }
+    std::vector<std::thread> th;
+    for (int i = 0; i < nt; i++) th.emplace_back(f, (int)((int64_t)h * i / nt), (int)((int64_t)h * (i + 1) / nt));
+    for (auto& t : th) t.join();
 }
 
 }  // namespace
@@ -57,7 +73,8 @@ extern "C" int svo_synth_frame(const uint8_t* canvas, int cw, int ch, int margin
                                uint8_t* frame, int w, int h) {
     if (!canvas || !R || !K || !frame || w <= 0 || h <= 0) return SVO_ERR_ARG;
     const double fx = K[0], fy = K[4], cx = K[2], cy = K[5];
-    for (int y = 0; y < h; y++)
+    for_rows(h, [&](int y0, int y1) {
+    for (int y = y0; y < y1; y++)
         for (int x = 0; x < w; x++) {
             // camera ray, rotated to the world (canvas) frame: R^T K^-1 p
             const double dx = (x - cx) / fx, dy = (y - cy) / fy;
@@ -77,6 +94,7 @@ extern "C" int svo_synth_frame(const uint8_t* canvas, int cw, int ch, int margin
             int iv8 = (int)std::floor(val + 0.5);
             frame[(size_t)y * w + x] = (uint8_t)(iv8 < 0 ? 0 : iv8 > 255 ? 255 : iv8);
         }
+    });
     return SVO_OK;
 }
 
@@ -85,16 +103,19 @@ extern "C" int svo_synth_frame(const uint8_t* canvas, int cw, int ch, int margin
 // field the map points use), so the right view of right pixel (xr, y) is the
 // left view of the pixel xl solving xl = xr + bf / z(xl, y), with z the
 // camera-frame depth of the surface point seen at left pixel (xl, y).
-// Fixed-point iteration (a contraction: |d(bf/z)/dx| << 1 for this field).
+// Fixed-point iteration (a contraction: |d(bf/z)/dx| << 1 for this field),
+// stopped once the step is below 1e-7 px.
 extern "C" int svo_synth_frame_right(const uint8_t* canvas, int cw, int ch, int margin_x, int margin_y,
                                      const double R[9], const double K[9], double bf, int depth_seed,
                                      uint64_t noise_seed, int noise, uint8_t* frame, int w, int h) {
     if (!canvas || !R || !K || !frame || w <= 0 || h <= 0) return SVO_ERR_ARG;
     const double fx = K[0], fy = K[4], cx = K[2], cy = K[5];
     const double seed = (double)depth_seed;
-    for (int y = 0; y < h; y++)
+    for_rows(h, [&](int y0, int y1) {
+    for (int y = y0; y < y1; y++) {
+        double xprev = 0.0;  // the previous pixel's solution: a warm start for this one
         for (int x = 0; x < w; x++) {
-            double xl = x, u = -1, v = -1;
+            double xl = x == 0 ? 0.0 : xprev + 1.0, u = -1, v = -1;
             for (int it = 0; it < 12; it++) {
                 const double dx = (xl - cx) / fx, dy = (y - cy) / fy;
                 const double wx = R[0] * dx + R[3] * dy + R[6];
@@ -105,8 +126,12 @@ extern "C" int svo_synth_frame_right(const uint8_t* canvas, int cw, int ch, int 
                 const double rho = 12.0 + 5.0 * std::sin(cu / 97.0 + seed) + 4.0 * std::cos(cv / 61.0 - 0.5 * seed);
                 u = cu + margin_x;
                 v = cv + margin_y;
-                xl = x + bf * wz / rho;  // camera-frame depth of the surface point = rho / wz
+                const double xn = x + bf * wz / rho;  // camera-frame depth of the surface point = rho / wz
+                const bool done = std::fabs(xn - xl) < 1e-7;
+                xl = xn;
+                if (done) break;
             }
+            xprev = xl;
             u = u < 0 ? 0 : u > cw - 1.001 ? cw - 1.001 : u;
             v = v < 0 ? 0 : v > ch - 1.001 ? ch - 1.001 : v;
             const int iu = (int)u, iv = (int)v;
@@ -118,5 +143,7 @@ extern "C" int svo_synth_frame_right(const uint8_t* canvas, int cw, int ch, int 
             int iv8 = (int)std::floor(val + 0.5);
             frame[(size_t)y * w + x] = (uint8_t)(iv8 < 0 ? 0 : iv8 > 255 ? 255 : iv8);
         }
+    }
+    });
     return SVO_OK;
 }

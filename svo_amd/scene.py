@@ -7,8 +7,9 @@ Per frame the camera turns so that the image moves by about (+1.37, -0.82) px
 and rolls 0.25 deg (ping-pong over `period` frames so the view stays on the
 canvas): frame-to-frame motion is the homography K R K^-1, the same order of
 motion as the survey's similarity warp, and a 3D point placed at ANY depth on
-a canvas ray reprojects exactly -- which gives consistent PnP inputs without
-stereo triangulation.
+a canvas ray reprojects exactly. The canvas surface sits on a smooth depth
+field, and a rectified right view (`right`) renders it with the disparity
+fx * b / depth, so stereo LK + triangulation recover the depth.
 """
 from __future__ import annotations
 
@@ -34,6 +35,16 @@ def intrinsics(w: int, h: int) -> np.ndarray:
     K = np.array([[KITTI_FX * sx, 0, KITTI_CX * sx], [0, KITTI_FY * sx, KITTI_CY * sy], [0, 0, 1]],
                  np.float32)
     return K.astype(np.float64)
+
+
+def stereo_projections(K, bf: float = STEREO_BF):
+    """KITTI-style calib rows of the rectified rig (R:src/main.cpp:25-32) as float32
+    3x4: left P = K[I|0], right P = K[I|0] with P[0, 3] = -fx * b."""
+    P0 = np.zeros((3, 4), np.float32)
+    P0[:, :3] = np.asarray(K, np.float64)
+    P1 = P0.copy()
+    P1[0, 3] = -bf
+    return P0, P1
 
 
 def rot(axis: str, a: float) -> np.ndarray:
@@ -84,11 +95,7 @@ class Scene:
 
     def projections(self, bf: float = STEREO_BF):
         """KITTI-style calib rows P0 (left) and P1 (right) as float32 3x4 (R:src/main.cpp:25-32)."""
-        P0 = np.zeros((3, 4), np.float32)
-        P0[:, :3] = self.K
-        P1 = P0.copy()
-        P1[0, 3] = -bf
-        return P0, P1
+        return stereo_projections(self.K, bf)
 
     def depth(self, cu: np.ndarray, cv: np.ndarray) -> np.ndarray:
         """Smooth positive depth field over canvas coordinates (metres)."""

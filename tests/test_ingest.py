@@ -65,13 +65,12 @@ def test_gpu_frontend_bgr_frames_equal_grey_frames():
         cfg = S.FrontendConfig(W, H, sc.K, n_seq=1, n_frames=3, n_features=300, max_level=3)
         fe = S.Frontend(ctx, cfg)
         for t in range(3):
-            g = sc.frame(t)
+            g, gr = sc.frame(t), sc.right(t)
             if colour:
-                # a BGR frame whose conversion is exactly g: equal channels
-                frame = np.repeat(g[..., None], 3, axis=2)
+                # BGR frames whose conversion is exactly g: equal channels
+                fe.set_frame(0, t, np.repeat(g[..., None], 3, axis=2), np.repeat(gr[..., None], 3, axis=2))
             else:
-                frame = g
-            fe.set_frame(0, t, frame, sc.R(t), depth_seed=sc.seed)
+                fe.set_frame(0, t, g, gr)
         fe.init(0)
         fe.step(1)
         fe.step(2)

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Fold rocprofv3 PMC passes into profiles/pmc_summary.json.
 
-    python tools/pmc_summary.py FETCH_CSV WRITE_CSV [OUT_JSON] [--label TEXT]
+    python tools/pmc_summary.py FETCH_CSV WRITE_CSV [OUT_JSON] [--label TEXT] [--config NAME]
 
 FETCH_CSV / WRITE_CSV are the `*_counter_collection.csv` files of two separate
 `rocprofv3 --pmc FETCH_SIZE` / `--pmc WRITE_SIZE` passes over the same command
@@ -9,6 +9,8 @@ FETCH_CSV / WRITE_CSV are the `*_counter_collection.csv` files of two separate
 and WRITE_SIZE per dispatch (KiB), and HBM bytes per launch
     = 2 * FETCH_SIZE * 1024 + WRITE_SIZE * 1024
 (gfx950 FETCH_SIZE counts half the bytes of a read: MI355X_MICROARCH.md §HBM).
+The summary is stored under configs[NAME] (bench.py --config; default "kitti"),
+so each bench config reads only the counters measured on its own workload.
 """
 import csv
 import json
@@ -34,10 +36,13 @@ def read(path, counter):
 
 def main():
     args = [a for a in sys.argv[1:] if not a.startswith("--")]
-    label = ""
+    label, cfg = "", "kitti"
     if "--label" in sys.argv:
         label = sys.argv[sys.argv.index("--label") + 1]
         args.remove(label)
+    if "--config" in sys.argv:
+        cfg = sys.argv[sys.argv.index("--config") + 1]
+        args.remove(cfg)
     fetch_csv, write_csv = args[0], args[1]
     out = args[2] if len(args) > 2 else "profiles/pmc_summary.json"
     fe, wr = read(fetch_csv, "FETCH_SIZE"), read(write_csv, "WRITE_SIZE")
@@ -48,8 +53,14 @@ def main():
         kernels[k] = {"dispatches": max(len(fe.get(k, [])), len(wr.get(k, []))),
                       "fetch_size_kib": round(f, 1), "write_size_kib": round(w, 1),
                       "hbm_bytes_per_launch": int(2 * f * 1024 + w * 1024)}
-    doc = {"source": label, "correction": "hbm = 2*FETCH_SIZE*1024 + WRITE_SIZE*1024 (gfx950 FETCH_SIZE halves reads)",
-           "kernels": kernels}
+    try:
+        with open(out) as fi:
+            doc = json.load(fi)
+    except (OSError, ValueError):
+        doc = {}
+    doc = {"correction": "hbm = 2*FETCH_SIZE*1024 + WRITE_SIZE*1024 (gfx950 FETCH_SIZE halves reads)",
+           "configs": doc.get("configs", {})}
+    doc["configs"][cfg] = {"source": label, "kernels": kernels}
     with open(out, "w") as fo:
         json.dump(doc, fo, indent=1)
     for k, v in kernels.items():
