@@ -1,5 +1,6 @@
-// EPnP minimal solver shared by the host RANSAC (pose.cpp) and the GPU RANSAC
-// kernel (ransac.hip): __host__ __device__, fixed sizes, no allocation.
+// EPnP minimal solver of the host RANSAC (pose.cpp): __host__ __device__, fixed
+// sizes, no allocation, so the same code also runs on the device
+// (tools/epnp_probe.hip measures it there).
 #pragma once
 
 #include "linalg.hpp"

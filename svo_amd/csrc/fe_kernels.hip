@@ -19,6 +19,10 @@ constexpr int kFeBlock = 256;
 // double Jacobi SVD): 1024 threads per sequence keep its critical-path latency
 // at about one SVD for the usual few hundred candidates.
 constexpr int kAppendBlock = 1024;
+// post_lk: its chain of dependent passes (compaction chunks, map-point gathers)
+// is latency-bound; 512 threads halve the chunks of a 2000-feature sequence
+// against 256 and still fit beside FAST's 256-thread blocks
+constexpr int kPostBlock = 512;
 
 // Stable compaction of one sequence by a keep predicate, by a BS-thread block:
 // keep(i) for i < n, kept entries of xy / mid moved to their rank (in place
@@ -90,10 +94,10 @@ __device__ __forceinline__ void finalize_body(const PendingMap& P, int s) {
 
 __global__ __launch_bounds__(kFeBlock) void finalize_map_kernel(PendingMap P) { finalize_body(P, blockIdx.x); }
 
-__global__ __launch_bounds__(kFeBlock) void post_lk_kernel(PostLkBatch B) {
+__global__ __launch_bounds__(kPostBlock) void post_lk_kernel(PostLkBatch B) {
     const int s = blockIdx.x;
     const size_t o = (size_t)s * B.cap;
-    __shared__ int wsum[kFeBlock / 64];
+    __shared__ int wsum[kPostBlock / 64];
     __shared__ int base_s;
     __shared__ unsigned long long it_s;
     __shared__ int idx[5 * 64];
@@ -103,8 +107,8 @@ __global__ __launch_bounds__(kFeBlock) void post_lk_kernel(PostLkBatch B) {
     const int n_in = B.n_in[s];
     const uint8_t* __restrict__ st = B.status + o;
     long long it = 0;
-    for (int i = tid; i < n_in; i += kFeBlock) it += B.iters[o + i];
-    const int n = block_compact<kFeBlock>(n_in, [&](int i) { return st[i] != 0; }, B.xy_in + 2 * o, B.mid_in + o,
+    for (int i = tid; i < n_in; i += kPostBlock) it += B.iters[o + i];
+    const int n = block_compact<kPostBlock>(n_in, [&](int i) { return st[i] != 0; }, B.xy_in + 2 * o, B.mid_in + o,
                                           B.xy_out + 2 * o, B.mid_out + o, wsum, &base_s);
     for (int off = 32; off > 0; off >>= 1) it += __shfl_xor(it, off);
     if (lane == 0) atomicAdd(&it_s, (unsigned long long)it);
@@ -129,7 +133,7 @@ __global__ __launch_bounds__(kFeBlock) void post_lk_kernel(PostLkBatch B) {
     }
     const int* __restrict__ mid = B.mid_out + o;
     const double* __restrict__ map = B.pm.map + 3 * (size_t)s * B.pm.map_cap;
-    for (int i = tid; i < n; i += kFeBlock) {
+    for (int i = tid; i < n; i += kPostBlock) {
         const double* X = map + 3 * (size_t)mid[i];
         B.obj[3 * (o + i)] = (float)X[0];
         B.obj[3 * (o + i) + 1] = (float)X[1];
@@ -144,7 +148,7 @@ __global__ __launch_bounds__(kFeBlock) void post_lk_kernel(PostLkBatch B) {
     if (draws) {
         const float* __restrict__ xy = B.xy_out + 2 * o;
         float* __restrict__ dst = B.h_samp + (size_t)25 * B.nh * s;
-        for (int k = tid; k < 5 * B.nh; k += kFeBlock) {
+        for (int k = tid; k < 5 * B.nh; k += kPostBlock) {
             const int j = k / 5, i = k - 5 * j, p = idx[k];
             const double* X = map + 3 * (size_t)mid[p];
             float* h = dst + 25 * j;
@@ -157,40 +161,55 @@ __global__ __launch_bounds__(kFeBlock) void post_lk_kernel(PostLkBatch B) {
     }
 }
 
-__global__ __launch_bounds__(kFeBlock) void tail_kernel(TailBatch T) {
-    const int s = blockIdx.x;
-    __shared__ int wsum[kFeBlock / 64];
-    __shared__ int base_s;
+// Outlier compaction by the inlier bits + the keyframe's take (tail_kernel's
+// body, BS threads); copy_cand: also copy the candidates to st_xy (the stereo
+// LK's input; a speculative prep already wrote them otherwise).
+template <int BS>
+__device__ __forceinline__ void tail_body(const TailBatch& T, int s, bool copy_cand, int* wsum, int* base_s,
+                                          int* n_kept, int* take_out) {
     const size_t o = (size_t)s * T.cap;
     const uint32_t* __restrict__ bits = T.bits + (size_t)s * T.words_cap;
-    const int n = block_compact<kFeBlock>(
+    const int n = block_compact<BS>(
         T.n_in[s], [&](int i) { return ((bits[i >> 5] >> (i & 31)) & 1u) != 0; }, T.xy_in + 2 * o, T.mid_in + o,
-        T.xy_out + 2 * o, T.mid_out + o, wsum, &base_s);
+        T.xy_out + 2 * o, T.mid_out + o, wsum, base_s);
     // new-feature candidates of the keyframe: the first `take` masked corners
     int take = min(max(T.n_target - n, 0), min(T.cand_n[s], T.cand_cap));
     take = min(take, T.cap - n);
     take = max(min(take, T.map_cap - T.map_n[s]), 0);
-    const float* c = T.cand + (size_t)T.cand_elem * ((size_t)s * T.cand_cap);
-    for (int j = threadIdx.x; j < take; j += kFeBlock) {
-        T.st_xy[2 * (o + j)] = c[(size_t)T.cand_elem * j];
-        T.st_xy[2 * (o + j) + 1] = c[(size_t)T.cand_elem * j + 1];
+    if (copy_cand) {
+        const float* c = T.cand + (size_t)T.cand_elem * ((size_t)s * T.cand_cap);
+        for (int j = threadIdx.x; j < take; j += BS) {
+            T.st_xy[2 * (o + j)] = c[(size_t)T.cand_elem * j];
+            T.st_xy[2 * (o + j) + 1] = c[(size_t)T.cand_elem * j + 1];
+        }
     }
     if (threadIdx.x == 0) {
         T.n_out[s] = n;
         T.st_n[s] = take;
     }
+    *n_kept = n;
+    *take_out = take;
 }
 
-__global__ __launch_bounds__(kAppendBlock) void append_kernel(AppendBatch A) {
-    const int s = blockIdx.x;
-    __shared__ int wsum[kAppendBlock / 64];
+__global__ __launch_bounds__(kFeBlock) void tail_kernel(TailBatch T) {
+    __shared__ int wsum[kFeBlock / 64];
     __shared__ int base_s;
+    int n, take;
+    tail_body<kFeBlock>(T, blockIdx.x, true, wsum, &base_s, &n, &take);
+}
+
+// findLeftFeaturesInRight's filter + triangulateNewMapPoints + append for the
+// stereo matches of st_xy[0, take) of sequence s, n0 features already kept.
+template <int BS>
+__device__ __forceinline__ void append_body(const AppendBatch& A, int s, int n0, int take, int* wsum, int* base_sp) {
+    int& base_s = *base_sp;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const size_t o = (size_t)s * A.cap;
-    const int n0 = A.n[s], take = A.st_n[s], m0 = A.map_n[s];
+    const int m0 = A.map_n[s];
+    __syncthreads();  // base_s / wsum reuse after the caller's own block work
     if (tid == 0) base_s = 0;
     __syncthreads();
-    for (int c0 = 0; c0 < take; c0 += kAppendBlock) {
+    for (int c0 = 0; c0 < take; c0 += BS) {
         const int j = c0 + tid;
         bool keep = false;
         float xl = 0.f, yl = 0.f, x3[3] = {0.f, 0.f, 0.f};
@@ -228,7 +247,7 @@ __global__ __launch_bounds__(kAppendBlock) void append_kernel(AppendBatch A) {
         __syncthreads();
         if (tid == 0) {
             int tot = 0;
-            for (int q = 0; q < kAppendBlock / 64; q++) tot += wsum[q];
+            for (int q = 0; q < BS / 64; q++) tot += wsum[q];
             base_s += tot;
         }
         __syncthreads();
@@ -245,11 +264,40 @@ __global__ __launch_bounds__(kAppendBlock) void append_kernel(AppendBatch A) {
     }
 }
 
+__global__ __launch_bounds__(kAppendBlock) void append_kernel(AppendBatch A) {
+    __shared__ int wsum[kAppendBlock / 64];
+    __shared__ int base_s;
+    const int s = blockIdx.x;
+    append_body<kAppendBlock>(A, s, A.n[s], A.st_n[s], wsum, &base_s);
+}
+
+__global__ __launch_bounds__(kAppendBlock) void keyframe_fused_kernel(TailBatch T, AppendBatch A) {
+    __shared__ int wsum[kAppendBlock / 64];
+    __shared__ int base_s;
+    const int s = blockIdx.x;
+    int n, take;
+    tail_body<kAppendBlock>(T, s, false, wsum, &base_s, &n, &take);
+    append_body<kAppendBlock>(A, s, n, take, wsum, &base_s);
+}
+
+__global__ __launch_bounds__(kFeBlock) void stereo_prep_kernel(StereoPrepBatch B) {
+    const int s = blockIdx.x;
+    int spec = min(max(B.n_target - B.n_tracked[s] + B.margin, 0), min(B.cand_n[s], B.cand_cap));
+    spec = max(min(min(spec, B.cap), B.map_cap - B.map_n[s]), 0);
+    const float* c = B.cand + (size_t)B.cand_elem * ((size_t)s * B.cand_cap);
+    float* dst = B.st_xy + 2 * (size_t)s * B.cap;
+    for (int j = threadIdx.x; j < spec; j += kFeBlock) {
+        dst[2 * j] = c[(size_t)B.cand_elem * j];
+        dst[2 * j + 1] = c[(size_t)B.cand_elem * j + 1];
+    }
+    if (threadIdx.x == 0) B.spec_n[s] = spec;
+}
+
 }  // namespace
 
 hipError_t launch_post_lk(const PostLkBatch& b, int nseq, hipStream_t st) {
     if (b.nh > 64) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(post_lk_kernel, dim3(nseq), dim3(kFeBlock), 0, st, b);
+    hipLaunchKernelGGL(post_lk_kernel, dim3(nseq), dim3(kPostBlock), 0, st, b);
     return hipGetLastError();
 }
 
@@ -265,6 +313,16 @@ hipError_t launch_tail(const TailBatch& tb, int nseq, hipStream_t st) {
 
 hipError_t launch_append(const AppendBatch& b, int nseq, hipStream_t st) {
     hipLaunchKernelGGL(append_kernel, dim3(nseq), dim3(kAppendBlock), 0, st, b);
+    return hipGetLastError();
+}
+
+hipError_t launch_keyframe_fused(const TailBatch& tb, const AppendBatch& ab, int nseq, hipStream_t st) {
+    hipLaunchKernelGGL(keyframe_fused_kernel, dim3(nseq), dim3(kAppendBlock), 0, st, tb, ab);
+    return hipGetLastError();
+}
+
+hipError_t launch_stereo_prep(const StereoPrepBatch& b, int nseq, hipStream_t st) {
+    hipLaunchKernelGGL(stereo_prep_kernel, dim3(nseq), dim3(kFeBlock), 0, st, b);
     return hipGetLastError();
 }
 

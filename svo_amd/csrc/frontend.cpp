@@ -163,6 +163,8 @@ struct svo_frontend {
     int* box_band;
     int *midA, *midB, *nA, *nB, *iters, *kn, *bn, *map_n, *rowcnt, *rowoff, *scr, *cnt, *added, *st_n;
     int *pend0, *pend_n;  // PendingMap ranges
+    int* spec_n;          // speculative stereo candidates per sequence (StereoPrepBatch)
+    int spec_margin = 32;  // RANSAC drops covered by the speculative stereo LK (SVO_FE_SPEC_MARGIN, < 0: off)
     unsigned long long* fbits;
     uint8_t* status;
     uint32_t* bits_all;
@@ -263,8 +265,9 @@ void ph_begin(svo_frontend* fe, int ph, hipStream_t st, int* slot) {
     if (fe->cfg.timing == 2 && ph != PH_LK && ph != PH_PYR && ph != PH_FAST && ph != PH_STEREO && ph != PH_PYR_R)
         return;
     const int sl = fe->ev_used;
-    for (auto& p : fe->pending)  // ring wrapped onto a pair still in flight
-        if (p.second == sl) ph_fold(fe, true);
+    bool wrapped = false;  // ring wrapped onto a pair still in flight
+    for (const auto& p : fe->pending) wrapped |= p.second == sl;
+    if (wrapped) ph_fold(fe, true);
     fe->ev_used = (fe->ev_used + 2) % kEvRing;
     *slot = sl;
     (void)hipEventRecord(fe->ev[sl], st);
@@ -317,6 +320,36 @@ int fe_fast_and_bucket(svo_frontend* fe, const PyrDesc* descs_cur, bool use_mask
     return SVO_OK;
 }
 
+// findLeftFeaturesInRight: calcOpticalFlowPyrLK(left, right, pts, 11x11, 3,
+// {COUNT+EPS, 30, 0.001}), flags 0 (R:src/tracking.cpp:97-105) of st_xy[0,
+// counts[s]) of sequences [a, a + n) of frame t; max_n bounds every count (the
+// grid). The left frame's derivative pyramid is the one the next step's
+// temporal LK reads.
+int fe_stereo_lk(svo_frontend* fe, int t, int a, int n, const int* counts, int max_n, hipStream_t st) {
+    svo_ctx* ctx = fe->ctx;
+    const svo_frontend_config& c = fe->cfg;
+    const size_t CAP = fe->CAP;
+    int slot;
+    SVO_HIP(ctx, hipStreamWaitEvent(st, fe->ev_pyr_r, 0));
+    const PyrDesc* dl = fe->d_desc + (size_t)(t % fe->T) * fe->S + a;
+    const PyrDesc* dr = fe->d_desc_r + (size_t)(t % fe->T) * fe->S + a;
+    LKBatch lb{dl, dr, fe->d_der + (size_t)(t % 3) * fe->S + a, fe->st_xy + 2 * a * CAP, fe->st_next + 2 * a * CAP,
+               fe->st_status + a * CAP, nullptr, nullptr, counts, 0, fe->CAP};
+    LKParams lp;
+    lp.win_w = lp.win_h = c.stereo_win;
+    lp.max_level = fe->ml_st;
+    lp.max_count = std::min(std::max(c.stereo_max_count, 0), 100);
+    const double eps = std::min(std::max(c.stereo_epsilon, 0.0), 10.0);
+    lp.eps2 = eps * eps;
+    lp.flags = 0;
+    lp.min_eig = (float)c.min_eig;
+    lp.want_err = 0;
+    ph_begin(fe, PH_STEREO, st, &slot);
+    SVO_HIP(ctx, launch_lk(lb, n, std::min(std::max(max_n, 0), fe->CAP), lp, st));
+    ph_end(fe, st, slot);
+    return SVO_OK;
+}
+
 // The keyframe of sequences [g0, g0 + n) on stream st (R:src/tracking.cpp:247-255,
 // every frame a keyframe topping the set up to n_features): outlier compaction
 // (inlier bits `bits`, or every point when n_in is all zero) + the first
@@ -324,8 +357,11 @@ int fe_fast_and_bucket(svo_frontend* fe, const PyrDesc* descs_cur, bool use_mask
 // (findLeftFeaturesInRight), then filter + triangulation + append (append_kernel).
 // xy_in / mid_in / n_in: the step's tracked points (compacted into xyA / midA / nA).
 // max_take: a host bound on every sequence's candidate count (the stereo LK grid).
+// spec: the speculative stereo LK (fe_queue_spec) already matched every
+// sequence's take candidates: compaction, filter, triangulation and append run
+// as one kernel.
 int fe_keyframe(svo_frontend* fe, int t, int g0, int n, const int* n_in, const uint32_t* bits, const float* xy_in,
-                const int* mid_in, int max_take, hipStream_t st) {
+                const int* mid_in, int max_take, hipStream_t st, bool spec = false) {
     svo_ctx* ctx = fe->ctx;
     const svo_frontend_config& c = fe->cfg;
     const size_t CAP = fe->CAP, a = g0;
@@ -350,29 +386,6 @@ int fe_keyframe(svo_frontend* fe, int t, int g0, int n, const int* n_in, const u
     tb.map_cap = fe->MAPCAP;
     tb.st_xy = fe->st_xy + 2 * a * CAP;
     tb.st_n = fe->st_n + a;
-    ph_begin(fe, PH_TAIL, st, &slot);
-    SVO_HIP(ctx, launch_tail(tb, n, st));
-    ph_end(fe, st, slot);
-    // findLeftFeaturesInRight: calcOpticalFlowPyrLK(left, right, pts, 11x11, 3,
-    // {COUNT+EPS, 30, 0.001}), flags 0 (R:src/tracking.cpp:97-105); the left
-    // frame's derivative pyramid is the one the next step's temporal LK reads
-    SVO_HIP(ctx, hipStreamWaitEvent(st, fe->ev_pyr_r, 0));
-    const PyrDesc* dl = fe->d_desc + (size_t)(t % fe->T) * fe->S + a;
-    const PyrDesc* dr = fe->d_desc_r + (size_t)(t % fe->T) * fe->S + a;
-    LKBatch lb{dl, dr, fe->d_der + (size_t)(t % 3) * fe->S + a, fe->st_xy + 2 * a * CAP, fe->st_next + 2 * a * CAP,
-               fe->st_status + a * CAP, nullptr, nullptr, fe->st_n + a, 0, fe->CAP};
-    LKParams lp;
-    lp.win_w = lp.win_h = c.stereo_win;
-    lp.max_level = fe->ml_st;
-    lp.max_count = std::min(std::max(c.stereo_max_count, 0), 100);
-    const double eps = std::min(std::max(c.stereo_epsilon, 0.0), 10.0);
-    lp.eps2 = eps * eps;
-    lp.flags = 0;
-    lp.min_eig = (float)c.min_eig;
-    lp.want_err = 0;
-    ph_begin(fe, PH_STEREO, st, &slot);
-    SVO_HIP(ctx, launch_lk(lb, n, std::min(std::max(max_take, 0), fe->CAP), lp, st));
-    ph_end(fe, st, slot);
     AppendBatch ab;
     ab.n = fe->nA + a;
     ab.xy = fe->xyA + 2 * a * CAP;
@@ -393,9 +406,52 @@ int fe_keyframe(svo_frontend* fe, int t, int g0, int n, const int* n_in, const u
     ab.added = fe->added + a;
     ab.h_n = fe->h_nA + a;
     ab.h_added = fe->h_added + a;
+    if (spec) {
+        ph_begin(fe, PH_TAIL, st, &slot);
+        SVO_HIP(ctx, launch_keyframe_fused(tb, ab, n, st));
+        ph_end(fe, st, slot);
+        return SVO_OK;
+    }
+    ph_begin(fe, PH_TAIL, st, &slot);
+    SVO_HIP(ctx, launch_tail(tb, n, st));
+    ph_end(fe, st, slot);
+    int rc = fe_stereo_lk(fe, t, (int)a, n, fe->st_n + a, max_take, st);
+    if (rc) return rc;
     ph_begin(fe, PH_APPEND, st, &slot);
     SVO_HIP(ctx, launch_append(ab, n, st));
     ph_end(fe, st, slot);
+    return SVO_OK;
+}
+
+// The speculative stereo LK of step t (StereoPrepBatch) for the sequences [a, a
+// + n) of one slice, on the FAST stream (behind FAST: the candidates), queued
+// once the host has seen the slice's post-LK counts (max_spec bounds every
+// sequence's spec: the grid): it runs beside the host's RANSAC. ev_sync[1] is
+// re-recorded behind it, so the keyframe's wait for FAST covers it too.
+int fe_queue_spec(svo_frontend* fe, int t, int a, int n, int max_spec) {
+    svo_ctx* ctx = fe->ctx;
+    const svo_frontend_config& c = fe->cfg;
+    const size_t CAP = fe->CAP;
+    hipStream_t sf = fe->st_fast;
+    const bool bucketed = c.bucket_size > 0;
+    StereoPrepBatch pb;
+    pb.n_tracked = fe->nB + a;
+    pb.cand = bucketed ? fe->cand + 2 * a * fe->BCAP : fe->kps + 3 * a * fe->KCAP;
+    pb.cand_elem = bucketed ? 2 : 3;
+    pb.cand_cap = bucketed ? fe->BCAP : fe->KCAP;
+    pb.cand_n = (bucketed ? fe->bn : fe->kn) + a;
+    pb.map_n = fe->map_n + a;
+    pb.map_cap = fe->MAPCAP;
+    pb.cap = fe->CAP;
+    pb.n_target = c.n_features;
+    pb.margin = fe->spec_margin;
+    pb.st_xy = fe->st_xy + 2 * a * CAP;
+    pb.spec_n = fe->spec_n + a;
+    // the slice's post-LK is complete (the host waited for it), FAST is ahead on sf
+    SVO_HIP(ctx, launch_stereo_prep(pb, n, sf));
+    int rc = fe_stereo_lk(fe, t, a, n, fe->spec_n + a, max_spec, sf);
+    if (rc) return rc;
+    SVO_HIP(ctx, hipEventRecord(fe->ev_sync[1], sf));
     return SVO_OK;
 }
 
@@ -555,6 +611,7 @@ int svo_frontend_create(svo_ctx* ctx, const svo_frontend_config* cfg, svo_fronte
         fe->st_n = carve<int>(p, S);
         fe->pend0 = carve<int>(p, S);
         fe->pend_n = carve<int>(p, S);
+        fe->spec_n = carve<int>(p, S);
         fe->obj = carve<float>(p, 3 * (size_t)S * CAP);
         fe->kps = carve<float>(p, 3 * (size_t)S * fe->KCAP);
         fe->cand = carve<float>(p, 2 * (size_t)S * fe->BCAP);
@@ -711,6 +768,8 @@ int svo_frontend_create(svo_ctx* ctx, const svo_frontend_config* cfg, svo_fronte
         fe->fast_early = !(fe_ && fe_[0] == '0');
         const char* ff = std::getenv("SVO_FE_FAST_FIRST");
         fe->fast_first = ff && ff[0] == '1';
+        const char* sm = std::getenv("SVO_FE_SPEC_MARGIN");
+        fe->spec_margin = sm ? std::atoi(sm) : 32;
     }
     // (on the context stream: a first use of the null stream would take a fifth
     // hardware queue and serialise the step's streams)
@@ -1122,6 +1181,11 @@ int svo_frontend_step(svo_frontend* fe, int t, svo_frontend_stats* stats) {
         const char* e = std::getenv("SVO_FE_TRACE");
         return e && e[0] == '1';
     }();
+    // per-round RANSAC inputs / scores on stderr (SVO_FE_DEBUG=1)
+    static const bool debug_on = [] {
+        const char* e = std::getenv("SVO_FE_DEBUG");
+        return e && e[0] == '1';
+    }();
     const auto trace_t0 = std::chrono::steady_clock::now();
     std::vector<std::pair<const char*, double>> trace;
     auto TP = [&](const char* label) {
@@ -1175,6 +1239,16 @@ int svo_frontend_step(svo_frontend* fe, int t, svo_frontend_stats* stats) {
         SVO_HIP(ctx, hipEventSynchronize(fe->ev_sync[3 + 2 * g]));
         TP("lk results on host");
         ms_wait += ms_since(tw);
+        // the keyframe's stereo matches, speculatively, beside this RANSAC (FAST
+        // is already queued ahead of it on the FAST stream)
+        const bool spec = fe->spec_margin >= 0;
+        if (spec) {
+            int max_spec = 0;
+            for (int s = a; s < a + n; s++) max_spec = std::max(max_spec, c.n_features - fe->h_nB[s] + fe->spec_margin);
+            int rq = fe_queue_spec(fe, t, a, n, std::min(max_spec, CAP));
+            if (rq) return rq;
+            TP("spec stereo queued");
+        }
         int max_b = 0;
         bool need_full = false;
         for (int s = a; s < a + n; s++) {
@@ -1278,6 +1352,18 @@ int svo_frontend_step(svo_frontend* fe, int t, svo_frontend_stats* stats) {
                         cnts[j] = tt;
                     }
                 }
+                if (debug_on) {
+                    const RansacSeq& r = fe->rs[s];
+                    unsigned hs = 0;
+                    for (int k = 0; k < kSampleFloats * ms[s]; k++) {
+                        unsigned u;
+                        std::memcpy(&u, r.samp + (size_t)kSampleFloats * (r.nh - ms[s]) + k, 4);
+                        hs = hs * 31u + u;
+                    }
+                    std::fprintf(stderr, "[fe dbg t=%d s=%d] n=%d nh=%d m=%d samp=%08x cnt=", t, s, r.n, r.nh, ms[s], hs);
+                    for (int j = 0; j < ms[s]; j++) std::fprintf(stderr, "%d(%d,%.17g) ", cnts[j], (int)r.valid[j], r.hyp[12 * j]);
+                    std::fprintf(stderr, "\n");
+                }
                 fe->rs[s].consume(cnts, bits, fe->WORDS, c.pnp_confidence);
             }
         }
@@ -1286,11 +1372,13 @@ int svo_frontend_step(svo_frontend* fe, int t, svo_frontend_stats* stats) {
         TP("consumed");
         auto tf = clk::now();
         int max_take = 0;  // the keyframe's candidates per sequence are at most n_features - kept
+        bool spec_ok = spec;  // every sequence dropped at most spec_margin points
         for (int s = a; s < a + n; s++) {
             RansacSeq& r = fe->rs[s];
             r.select(c.K, false);
             const int kept = r.ok ? r.maxGood : (r.n < 4 ? r.n : 0);
             max_take = std::max(max_take, c.n_features - kept);
+            spec_ok &= fe->h_nB[s] - kept <= fe->spec_margin;
             uint32_t* b = fe->h_best + (size_t)s * fe->WORDS;
             std::memset(b, 0, sizeof(uint32_t) * fe->WORDS);
             if (r.ok) {
@@ -1318,7 +1406,7 @@ int svo_frontend_step(svo_frontend* fe, int t, svo_frontend_stats* stats) {
         // drop the outliers (the kernel reads the inlier bits from host-coherent
         // memory), then the keyframe: candidates, stereo LK, triangulation, append
         rc = fe_keyframe(fe, t, a, n, fe->nB + a, fe->h_best + (size_t)a * fe->WORDS, fe->xyB + 2 * (size_t)a * CAP,
-                         fe->midB + (size_t)a * CAP, max_take, sg);
+                         fe->midB + (size_t)a * CAP, max_take, sg, spec_ok);
         if (rc) return rc;
         SVO_HIP(ctx, hipEventRecord(fe->ev_tail[g], sg));
         TP("tail queued");

@@ -102,4 +102,29 @@ struct AppendBatch {
 };
 hipError_t launch_append(const AppendBatch& b, int nseq, hipStream_t st);
 
+// Speculative stereo input, one block per sequence, queued as soon as the step's
+// tracked count n_tracked (post-LK) and the FAST candidates are known, i.e. before
+// the RANSAC: the keyframe takes the first take = min(n_target - kept, ...)
+// candidates, kept <= n_tracked inliers, so the first
+//   spec = min(n_target - n_tracked + margin, cand_n, cand_cap, cap, map_cap - map_n)
+// candidates cover take whenever RANSAC drops at most `margin` points. They are
+// copied to st_xy with their count in spec_n, and their stereo LK runs beside
+// the host's RANSAC (a feature's LK depends on nothing but its own point).
+struct StereoPrepBatch {
+    const int* n_tracked;
+    const float* cand;
+    int cand_elem, cand_cap;
+    const int* cand_n;
+    const int* map_n;
+    int map_cap, cap, n_target, margin;
+    float* st_xy;
+    int* spec_n;
+};
+hipError_t launch_stereo_prep(const StereoPrepBatch& b, int nseq, hipStream_t st);
+
+// tail_kernel + append_kernel in one launch, for a step whose speculative stereo
+// LK covered every sequence's take (st_next / st_status already hold the matches
+// of st_xy[0, take)); same results as the two kernels with the LK between them.
+hipError_t launch_keyframe_fused(const TailBatch& tb, const AppendBatch& ab, int nseq, hipStream_t st);
+
 }  // namespace svo

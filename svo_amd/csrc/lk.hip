@@ -11,11 +11,12 @@
 // MI355X design:
 //  * A feature's levels are independent of every other feature, so the whole
 //    coarse-to-fine pass is one launch: no grid sync between levels.
-//  * Per level the wave stages the (win+3)^2 u8 patch of the previous image in
-//    LDS (REFLECT_101 outside the image, as OpenCV's padded pyramid), computes
-//    the Scharr derivative at the (win+1)^2 bilinear grid points in LDS (zero
-//    outside the image, as OpenCV's zero-padded derivative level) -- no
-//    derivative image is ever materialised in HBM.
+//  * The Scharr derivatives of the previous image come from its derivative
+//    pyramid (scharr.hip / pyr_scharr_kernel: packed Ix | Iy << 16 per pixel,
+//    stored x4, zero-padded borders as OpenCV's derivative levels), built once
+//    per frame and reused by every LK call on it (OpenCV recomputes it per
+//    call); the prev / next u8 pyramid levels are stored with 32-px REFLECT_101
+//    borders (kPyrPad), so window reads near the image edge are branch-free.
 //  * Lane <-> pixel map: lane = g*win_w + c owns column c, rows [g*RPG,
 //    (g+1)*RPG): vertically adjacent window pixels share J rows, so one GN
 //    iteration reads RPG+1 rows x 2 bytes per lane instead of 4 per pixel.

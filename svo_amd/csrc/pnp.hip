@@ -54,8 +54,11 @@ __global__ __launch_bounds__(256) void pnp_residual_kernel(PnpBatch B, double fx
         if (lane == 1 && w0 + 1 < words) bits[w0 + 1] = (uint32_t)(bal >> 32);
     }
     if (B.cnt && lane == 0 && bal) atomicAdd(&B.cnt[(size_t)seq * ms + h], __popcll(bal));
-    if (B.wave_cnt && lane == 0)
-        B.wave_cnt[((size_t)seq * ms + h) * B.wave_stride + (blockIdx.x * 256 + threadIdx.x) / 64] = __popcll(bal);
+    // only the waves that hold points (the reader sums ceil(n / 64) of them): a
+    // wave past n would land in the next hypothesis' row whenever the row stride
+    // (ceil(cap / 64) waves) is not a multiple of the block's 4 waves
+    const int wave = (blockIdx.x * 256 + threadIdx.x) / 64;
+    if (B.wave_cnt && lane == 0 && wave * 64 < n) B.wave_cnt[((size_t)seq * ms + h) * B.wave_stride + wave] = __popcll(bal);
 }
 
 }  // namespace

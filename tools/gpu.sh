@@ -1,0 +1,184 @@
+# One driver for every GPU-box session (run from the repo root on the box):
+#
+#   bash tools/gpu.sh MODE [ARGS...] [-- MODE [ARGS...] ...]
+#
+#   tests [PYTEST_ARGS]     pytest -m gpu (default: the whole suite)
+#   smoke                   __graft_entry__.smoke()
+#   bench [BENCH_ARGS]      one bench.py line (default: the driver's defaults)
+#   fe                      frontend + new-parity tests, short bench
+#   trace [STEPS]           one steady step's GPU timeline + host trace
+#   prof TAG [BENCH_ARGS]   rocprofv3 --kernel-trace --stats of a bench run
+#   pmc TAG CONFIG [SEQ]    FETCH_SIZE / WRITE_SIZE passes of a bench run of CONFIG,
+#                           folded into profiles/pmc_summary.json (configs[CONFIG])
+#   mix TAG [BENCH_ARGS]    SQ instruction mix per wave of every step kernel
+#   lksplit                 LK VALU / time with the iteration cap at 1, 2, 50
+#   ab VAR "V1 V2" [RUNS]   bench A/B of an environment switch
+#   round TAG               tests, smoke, prof, pmc (3 configs), mix, bench lines
+#
+# Every GPU step has its own time limit; the first failure ends the session.
+set -o pipefail
+cd /tmp && export TMPDIR=/tmp
+cd "${GRAFT_REPO_ROOT:-/root/repo}"
+O=gpurun_out
+mkdir -p $O
+BQ="python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-single"
+
+fail() { echo "FAILED: $1"; [ -n "$2" ] && tail -30 "$2"; exit 1; }
+
+run_tests() {
+    local args="${*:-tests}"
+    timeout -k 10 900 python -u -m pytest $args -m gpu -x -v --timeout 300 --timeout-method thread \
+        -p no:cacheprovider > $O/gpu_tests.log 2>&1 || fail tests $O/gpu_tests.log
+    tail -1 $O/gpu_tests.log
+}
+
+run_smoke() {
+    timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || fail smoke $O/smoke.log
+    cat $O/smoke.log
+}
+
+run_bench() {
+    local tag=$1; shift
+    timeout -k 10 600 python bench.py "$@" > $O/bench_$tag.log 2>&1 || fail bench $O/bench_$tag.log
+    tail -1 $O/bench_$tag.log | cut -c1-1500
+}
+
+run_fe() {
+    timeout -k 10 600 python -u -m pytest tests/test_frontend_gpu.py tests/test_ingest.py -x -v --timeout 300 \
+        --timeout-method thread -p no:cacheprovider -m gpu > $O/fe_tests.log 2>&1 || fail fe-tests $O/fe_tests.log
+    tail -1 $O/fe_tests.log
+    run_bench quick --steps 20 --warmup 5 --no-cpu-baseline
+}
+
+run_trace() {
+    local T=/tmp/svo_trace
+    SVO_FE_TRACE=1 timeout -k 10 300 rocprofv3 --kernel-trace --memory-copy-trace -d $T -o run --output-format csv -- \
+        python bench.py --steps ${1:-12} --warmup 3 --seq 64 --no-cpu-baseline --no-single > $T.log 2>&1 || fail trace $T.log
+    python tools/timeline.py $T > $O/timeline.txt
+    grep "fe t=" $T.log | tail -16 > $O/hosttrace.txt
+    cat $O/timeline.txt $O/hosttrace.txt
+}
+
+run_prof() {
+    local tag=$1; shift
+    local args="${*:---steps 50 --warmup 10 --no-cpu-baseline --no-single}"
+    rm -rf $O/prof_$tag
+    timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/prof_$tag -o run --output-format csv -- \
+        python bench.py $args > $O/prof_$tag.log 2>&1 || fail prof $O/prof_$tag.log
+    tail -1 $O/prof_$tag.log | cut -c1-600
+    python - $O/prof_$tag <<'P'
+import csv, glob, sys
+f = glob.glob(sys.argv[1] + '/**/run_kernel_stats.csv', recursive=True)[0]
+for r in list(csv.DictReader(open(f)))[:16]:
+    print(f"{r['Name'][:70]:70s} calls={r['Calls']:>6s} avg_us={float(r['AverageNs'])/1e3:9.2f} pct={float(r['Percentage']):6.2f}")
+P
+}
+
+run_pmc() {
+    local tag=$1 cfg=$2 seq=${3:-64}
+    local B="python bench.py --config $cfg --seq $seq --steps 10 --warmup 3 --no-cpu-baseline --no-single"
+    rm -rf $O/pmc_fetch_$cfg $O/pmc_write_$cfg
+    timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE -d $O/pmc_fetch_$cfg -o run --output-format csv -- $B \
+        > $O/pmc_fetch_$cfg.log 2>&1 || fail pmc-fetch $O/pmc_fetch_$cfg.log
+    timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE -d $O/pmc_write_$cfg -o run --output-format csv -- $B \
+        > $O/pmc_write_$cfg.log 2>&1 || fail pmc-write $O/pmc_write_$cfg.log
+    python tools/pmc_summary.py $(find $O/pmc_fetch_$cfg -name "*counter_collection.csv" | head -1) \
+        $(find $O/pmc_write_$cfg -name "*counter_collection.csv" | head -1) profiles/pmc_summary.json \
+        --config $cfg --label "$tag: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes over '$B'" || fail pmc-summary
+    cp profiles/pmc_summary.json $O/pmc_summary.json
+    rm -rf $O/pmc_fetch_$cfg $O/pmc_write_$cfg
+}
+
+run_mix() {
+    local tag=$1; shift
+    local B="python bench.py ${*:---steps 8 --warmup 2 --no-cpu-baseline --no-single}"
+    timeout -s KILL 200 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_WAIT_INST_ANY \
+        SQ_ACTIVE_INST_ANY SQ_INSTS_VMEM -d /tmp/ps1 -o run --output-format csv -- $B > $O/mix.log 2>&1 || fail mix1 $O/mix.log
+    timeout -s KILL 200 rocprofv3 --pmc SQ_ACTIVE_INST_VALU SQ_BUSY_CYCLES SQ_INSTS_BRANCH SQ_WAIT_INST_LDS \
+        SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_SCA SQ_INSTS_SMEM -d /tmp/ps2 -o run --output-format csv \
+        -- $B >> $O/mix.log 2>&1 || fail mix2 $O/mix.log
+    python - > $O/mix_$tag.txt <<'P'
+import csv, glob, collections, re
+agg = collections.defaultdict(lambda: collections.defaultdict(float))
+disp = collections.defaultdict(set)
+for f in glob.glob('/tmp/ps[12]/**/run_counter_collection.csv', recursive=True):
+    for r in csv.DictReader(open(f)):
+        m = re.search(r'([a-z_0-9]+_kernel)', r['Kernel_Name'])
+        if not m: continue
+        k = m.group(1)
+        agg[k][r['Counter_Name']] += float(r['Counter_Value'])
+        disp[k].add((f, r['Dispatch_Id']))
+for k, d in agg.items():
+    n = len(disp[k]) / 2
+    w = d.get('SQ_WAVES', 1)
+    print(f"{k:28s} disp {n:5.0f} waves/disp {w/n:9.0f} | per wave: " + ' '.join(f"{c.replace('SQ_','')}={v/w:.0f}" for c, v in sorted(d.items()) if c != 'SQ_WAVES'))
+P
+    cat $O/mix_$tag.txt
+    rm -rf /tmp/ps1 /tmp/ps2
+}
+
+run_lksplit() {
+    for c in 1 2 50; do local T=/tmp/lks_$c
+        timeout -s KILL 90 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAVES SQ_BUSY_CYCLES SQ_INSTS_VMEM \
+            -d $T -o run --output-format csv -- python tools/microbench.py lk --points 128000 --reps 2 --count $c \
+            > $T.log 2>&1 || fail lksplit-pmc $T.log
+        timeout -k 10 90 rocprofv3 --kernel-trace --stats -d ${T}k -o run --output-format csv -- \
+            python tools/microbench.py lk --points 128000 --reps 3 --count $c >> $T.log 2>&1 || fail lksplit-time $T.log
+        python - $T $c <<'P'
+import csv, glob, sys, collections
+agg = collections.defaultdict(float)
+for f in glob.glob(sys.argv[1] + '/**/run_counter_collection.csv', recursive=True):
+    for r in csv.DictReader(open(f)):
+        if 'lk_multi' in r['Kernel_Name']: agg[r['Counter_Name']] += float(r['Counter_Value'])
+dur = []
+for f in glob.glob(sys.argv[1] + 'k/**/run_kernel_trace.csv', recursive=True):
+    for r in csv.DictReader(open(f)):
+        if 'lk_multi' in r['Kernel_Name']: dur.append((int(r['End_Timestamp']) - int(r['Start_Timestamp'])) / 1e3)
+print('count', sys.argv[2], 'us', [round(d, 1) for d in dur], ' '.join(f"{k}={v/2/128000*4:.0f}/wave" for k, v in sorted(agg.items())))
+P
+    done
+}
+
+run_ab() {
+    local var=$1 vals=$2 runs=${3:-2}
+    for r in $(seq $runs); do for v in $vals; do
+        env $var=$v timeout -k 10 200 $BQ > $O/ab.log 2>&1 || fail ab $O/ab.log
+        python -c "
+import json; d=json.loads(open('$O/ab.log').read().strip().splitlines()[-1]); p=d['phase_ms_per_step']
+print('$var=$v', d['value'], d['ms_per_step'], 'lk', p['lk'], 'fast', p['fast'], 'pyr', p['pyramid'])"
+    done; done
+}
+
+run_round() {
+    local tag=$1
+    run_tests
+    run_smoke
+    run_prof "$tag"
+    for c in kitti 1080p 4k; do
+        if [ $c = kitti ]; then run_pmc "$tag" $c 64; else run_pmc "$tag" $c 16; fi
+    done
+    run_mix "$tag"
+    run_bench "$tag" --steps 50 --warmup 10
+    for c in 1080p 4k; do run_bench "${tag}_$c" --config $c --seq 16 --steps 20 --warmup 5 --no-cpu-baseline; done
+}
+
+while [ $# -gt 0 ]; do
+    mode=$1; shift
+    args=()
+    while [ $# -gt 0 ] && [ "$1" != "--" ]; do args+=("$1"); shift; done
+    [ "$1" = "--" ] && shift
+    case $mode in
+        tests) run_tests "${args[@]}" ;;
+        smoke) run_smoke ;;
+        bench) run_bench main "${args[@]}" ;;
+        fe) run_fe ;;
+        trace) run_trace "${args[@]}" ;;
+        prof) run_prof "${args[@]}" ;;
+        pmc) run_pmc "${args[@]}" ;;
+        mix) run_mix "${args[@]}" ;;
+        lksplit) run_lksplit ;;
+        ab) run_ab "${args[@]}" ;;
+        round) run_round "${args[@]}" ;;
+        *) fail "unknown mode $mode" ;;
+    esac
+done

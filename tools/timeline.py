@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Print one frontend step's GPU timeline from a rocprofv3 --kernel-trace
---memory-copy-trace CSV pair (tools/gpu_trace.sh)."""
+--memory-copy-trace CSV pair (bash tools/gpu.sh trace)."""
 import csv
 import re
 import sys
@@ -15,7 +15,7 @@ for r in csv.DictReader(open(f"{d}/run_kernel_trace.csv")):
 for r in csv.DictReader(open(f"{d}/run_memory_copy_trace.csv")):
     rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), "C:" + r["Direction"][:24], r.get("Queue_Id", "")))
 rows.sort()
-lk = [x for x in rows if x[2].startswith("K:lk_")]
+lk = [x for x in rows if x[2].startswith("K:lk_multi")] or [x for x in rows if x[2].startswith("K:lk_")]
 # slices of one step launch their LKs together: step starts = LK starts > 100 us apart
 starts = [lk[0][0]]
 for x in lk[1:]:
