@@ -212,6 +212,7 @@ def main():
         if s % 16 == 15:
             print(f"[bench] rank {rank}: {s + 1}/{Sq} sequences rendered and uploaded", file=sys.stderr, flush=True)
     fe.init(0)
+    host_cpus = fe.host_cpus()  # this rank's pinned share of the node (svo_host_cpu_plan)
     feats_after = {}  # features after step t = the inputs of LK(t + 1)
     for t in range(1, Wm + 1):
         feats_after[t] = fe.step(t).as_dict()["features"]
@@ -303,7 +304,7 @@ def main():
         "data": "synthetic (rendered KITTI-size frames, seeded; no dataset on the box)",
         "config": {"workload": label, "sequences_per_gpu": Sq, "global_batch": Sq * world,
                    "features": N, "win": 21, "max_level": ML, "parallelism": f"{world} x independent sequences",
-                   "groups": args.groups},
+                   "groups": args.groups, "host_cpus_rank0": len(host_cpus)},
         "lk_iters_per_s": round(lk_iters_total / dt_max, 1),
         "achieved_GBps_algorithmic": round(frames * frame_bytes(W, H, N, ML) / dt_max / 1e9, 2),
         "single_stream_fps": round(single, 2) if single else None,

@@ -298,6 +298,19 @@ void svo_frontend_reset_times(svo_frontend* fe);
  * events around them; ms per chain. Synchronises the front end first. */
 int svo_frontend_time_pyramid(svo_frontend* fe, int t, int reps, double* ms_per_launch);
 
+/* Host cores for a front end's RANSAC / pose-fit pool when several ranks (one
+ * process per GPU) share a node: this process's allowed CPUs ordered by NUMA
+ * node are split among the local ranks, each rank taking its share of the node
+ * its GPU sits on (gpu_node[r] = NUMA node of local rank r's GPU, or null to
+ * split the whole ordered list by rank). Writes at most cap CPU ids to cpus and
+ * their count to n; the sets of distinct local ranks are disjoint whenever the
+ * node has at least one CPU per rank. svo_frontend_create pins its pool with
+ * this plan (LOCAL_RANK / LOCAL_WORLD_SIZE from the environment, as
+ * torch.distributed.run sets them) and sizes it to the set (at most 16). */
+int svo_host_cpu_plan(int local_rank, int local_world, const int* gpu_node, int* cpus, int cap, int* n);
+/* The CPUs a front end's pool threads are pinned to (empty: not pinned). */
+int svo_frontend_host_cpus(svo_frontend* fe, int* cpus, int cap, int* n);
+
 /* ------------------------------------------------------------ synthetic input
  * Deterministic synthetic KITTI-like frames: a textured canvas
  * of random rectangles, box-blurred, seen through a rotating pinhole camera

@@ -107,6 +107,8 @@ _SIGS = [
     ("svo_frontend_features", C.c_int, [_vp, C.c_int, _f32p, C.c_int, _i32p]),
     ("svo_frontend_phase_times", C.c_int, [_vp, _f64p, C.POINTER(C.c_int64), C.c_int]),
     ("svo_frontend_reset_times", None, [_vp]),
+    ("svo_host_cpu_plan", C.c_int, [C.c_int, C.c_int, _i32p, _i32p, C.c_int, _i32p]),
+    ("svo_frontend_host_cpus", C.c_int, [_vp, _i32p, C.c_int, _i32p]),
     ("svo_synth_canvas", C.c_int, [C.c_uint64, C.c_int, C.c_int, C.c_int, _u8p]),
     ("svo_synth_frame", C.c_int, [_u8p, C.c_int, C.c_int, C.c_int, C.c_int, _f64p, _f64p,
                                   C.c_uint64, C.c_int, _u8p, C.c_int, C.c_int]),
@@ -115,6 +117,18 @@ _SIGS = [
 ]
 
 SYMBOLS = [s[0] for s in _SIGS]
+
+
+def host_cpu_plan(local_rank, local_world, gpu_node=None, cap=4096):
+    """svo_host_cpu_plan: this rank's share of the node's CPUs (host code, no GPU)."""
+    cpus = np.zeros(cap, np.int32)
+    n = C.c_int(0)
+    gn = None if gpu_node is None else np.ascontiguousarray(gpu_node, np.int32)
+    rc = lib().svo_host_cpu_plan(int(local_rank), int(local_world), None if gn is None else _p(gn, _i32p),
+                                 _p(cpus, _i32p), cap, C.byref(n))
+    if rc != 0:
+        raise SvoError(f"svo_host_cpu_plan: error {rc}")
+    return cpus[:min(n.value, cap)].tolist()
 
 
 def lib():
@@ -544,6 +558,13 @@ class Frontend:
 
     def reset_times(self):
         lib().svo_frontend_reset_times(self.handle)
+
+    def host_cpus(self):
+        """CPUs the host pool is pinned to (svo_host_cpu_plan's share of this rank)."""
+        cpus = np.zeros(4096, np.int32)
+        n = C.c_int(0)
+        self.ctx._check(lib().svo_frontend_host_cpus(self.handle, _p(cpus, _i32p), 4096, C.byref(n)))
+        return cpus[:n.value].tolist()
 
     def close(self):
         if getattr(self, "handle", None):

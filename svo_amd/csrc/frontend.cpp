@@ -18,8 +18,16 @@
 // scores; the final pose fits run on the host while the GPU tracks the next frame,
 // so a keyframe's new map points stay in its camera frame until the next step
 // moves them to the world frame with that pose (PendingMap, frontend.hpp).
+#include <pthread.h>
+#include <sched.h>
+
+#include <cctype>
+
 #include <algorithm>
 #include <cstdio>
+#include <fstream>
+#include <sstream>
+#include <string>
 #include <cstdlib>
 #include <chrono>
 #include <atomic>
@@ -46,12 +54,25 @@ namespace {
 // (a worker that wakes late with nothing left to take is not waited for).
 // Tasks are claimed by CAS on (generation << 32 | index), so a worker still
 // holding an old generation can never take (or skip) a task of a newer job.
+// Workers are pinned to `cpus` (the rank's share of the node, svo_host_cpu_plan)
+// when it is non-empty. The spin is bounded below one step (SVO_POOL_SPIN_US,
+// default 400 us): between the step's two pool jobs the workers stay hot, across
+// an idle caller they sleep, so a rank does not burn its cores between steps.
 class Pool {
    public:
-    explicit Pool(int n) {
+    explicit Pool(int n, const std::vector<int>& cpus = {}) {
         const char* e = std::getenv("SVO_POOL_SPIN_US");
-        spin_us_ = e ? std::atof(e) : 3000.0;
-        for (int i = 0; i < n; i++) th_.emplace_back([this] { loop(); });
+        spin_us_ = e ? std::atof(e) : 400.0;
+        for (int i = 0; i < n; i++) {
+            th_.emplace_back([this] { loop(); });
+            if (!cpus.empty()) {
+                cpu_set_t set;
+                CPU_ZERO(&set);
+                for (int c : cpus)
+                    if (c >= 0 && c < CPU_SETSIZE) CPU_SET(c, &set);
+                (void)pthread_setaffinity_np(th_.back().native_handle(), sizeof(set), &set);
+            }
+        }
     }
     ~Pool() {
         {
@@ -129,8 +150,88 @@ class Pool {
     std::atomic<uint64_t> next_{0}, gen_{0};
     std::atomic<int> done_{0}, sleeping_{0};
     std::atomic<bool> stop_{false};
-    double spin_us_ = 3000.0;
+    double spin_us_ = 400.0;
 };
+
+// ---- host core plan (svo_host_cpu_plan) ----
+std::vector<int> parse_cpulist(const std::string& txt) {  // "0-3,8,10-11"
+    std::vector<int> out;
+    std::stringstream ss(txt);
+    std::string tok;
+    while (std::getline(ss, tok, ',')) {
+        if (tok.empty() || tok[0] == '\n') continue;
+        const size_t dash = tok.find('-');
+        const int a = std::atoi(tok.c_str());
+        const int b = dash == std::string::npos ? a : std::atoi(tok.c_str() + dash + 1);
+        for (int c = a; c <= b; c++) out.push_back(c);
+    }
+    return out;
+}
+
+// NUMA node of every CPU id (-1: unknown), from /sys/devices/system/node
+std::vector<int> cpu_nodes(int max_cpu) {
+    std::vector<int> node((size_t)max_cpu + 1, -1);
+    for (int m = 0; m < 64; m++) {
+        std::ifstream f("/sys/devices/system/node/node" + std::to_string(m) + "/cpulist");
+        if (!f) continue;
+        std::string txt;
+        std::getline(f, txt);
+        for (int c : parse_cpulist(txt))
+            if (c >= 0 && c <= max_cpu) node[c] = m;
+    }
+    return node;
+}
+
+std::vector<int> host_cpu_plan(int rank, int world, const int* gpu_node) {
+    cpu_set_t set;
+    CPU_ZERO(&set);
+    std::vector<int> allowed;
+    if (sched_getaffinity(0, sizeof(set), &set) == 0)
+        for (int c = 0; c < CPU_SETSIZE; c++)
+            if (CPU_ISSET(c, &set)) allowed.push_back(c);
+    if (allowed.empty() || world <= 0 || rank < 0 || rank >= world) return {};
+    const std::vector<int> node = cpu_nodes(allowed.back());
+    std::stable_sort(allowed.begin(), allowed.end(), [&](int a, int b) { return node[a] < node[b]; });
+    auto split = [](const std::vector<int>& cpus, int idx, int k) {
+        std::vector<int> out;
+        const int m = (int)cpus.size();
+        if (m == 0 || k <= 0) return out;
+        if (m < k) {  // fewer CPUs than ranks: shared, one each
+            out.push_back(cpus[idx % m]);
+            return out;
+        }
+        const int lo = (int)((int64_t)m * idx / k), hi = (int)((int64_t)m * (idx + 1) / k);
+        out.assign(cpus.begin() + lo, cpus.begin() + hi);
+        return out;
+    };
+    if (gpu_node && gpu_node[rank] >= 0) {
+        // the ranks whose GPUs sit on this rank's node share that node's CPUs
+        const int my = gpu_node[rank];
+        int idx = 0, k = 0;
+        for (int r = 0; r < world; r++)
+            if (gpu_node[r] == my) {
+                if (r < rank) idx++;
+                k++;
+            }
+        std::vector<int> local;
+        for (int c : allowed)
+            if (node[c] == my) local.push_back(c);
+        if ((int)local.size() >= k) return split(local, idx, k);
+    }
+    return split(allowed, rank, world);
+}
+
+// NUMA node of HIP device d (-1: unknown), from its PCI address in sysfs
+int device_numa_node(int d) {
+    char bus[64] = {0};
+    if (hipDeviceGetPCIBusId(bus, sizeof(bus), d) != hipSuccess) return -1;
+    std::string id(bus);
+    for (auto& ch : id) ch = (char)std::tolower((unsigned char)ch);
+    std::ifstream f("/sys/bus/pci/devices/" + id + "/numa_node");
+    int v = -1;
+    if (f) f >> v;
+    return v;
+}
 
 constexpr int kPhases = 10;
 enum Phase { PH_PYR, PH_LK, PH_POST, PH_STEREO, PH_PNP, PH_TAIL, PH_FAST, PH_BUCKET, PH_APPEND, PH_PYR_R };
@@ -220,6 +321,7 @@ struct svo_frontend {
     int fit_parity = 0;  // step parity whose RANSAC results the pending fits refine
     uint8_t* score_map = nullptr;  // [s][npx] FAST scores of the kept corners
     Pool* pool = nullptr;
+    std::vector<int> host_cpus;  // the pool's pinned CPU set (svo_host_cpu_plan)
     // pipeline: slices of the batch [g0[g], g0[g] + gn[g]) on their own streams
     int G = 1;
     std::vector<int> g0, gn;
@@ -424,11 +526,13 @@ int fe_keyframe(svo_frontend* fe, int t, int g0, int n, const int* n_in, const u
 }
 
 // The speculative stereo LK of step t (StereoPrepBatch) for the sequences [a, a
-// + n) of one slice, on the FAST stream (behind FAST: the candidates), queued
-// once the host has seen the slice's post-LK counts (max_spec bounds every
-// sequence's spec: the grid): it runs beside the host's RANSAC. ev_sync[1] is
-// re-recorded behind it, so the keyframe's wait for FAST covers it too.
-int fe_queue_spec(svo_frontend* fe, int t, int a, int n, int max_spec) {
+// + n) of one slice, on the FAST stream (behind FAST: the candidates) after the
+// slice's post-LK (ev_post: the tracked counts), queued with the post-LK so that
+// no host round trip precedes it: it runs beside the host's RANSAC. max_spec
+// bounds every sequence's spec (the grid; blocks past a sequence's count exit at
+// once). ev_sync[1] is re-recorded behind it, so the keyframe's wait for FAST
+// covers it too.
+int fe_queue_spec(svo_frontend* fe, int t, int a, int n, int max_spec, hipEvent_t ev_post) {
     svo_ctx* ctx = fe->ctx;
     const svo_frontend_config& c = fe->cfg;
     const size_t CAP = fe->CAP;
@@ -447,7 +551,7 @@ int fe_queue_spec(svo_frontend* fe, int t, int a, int n, int max_spec) {
     pb.margin = fe->spec_margin;
     pb.st_xy = fe->st_xy + 2 * a * CAP;
     pb.spec_n = fe->spec_n + a;
-    // the slice's post-LK is complete (the host waited for it), FAST is ahead on sf
+    SVO_HIP(ctx, hipStreamWaitEvent(sf, ev_post, 0));
     SVO_HIP(ctx, launch_stereo_prep(pb, n, sf));
     int rc = fe_stereo_lk(fe, t, a, n, fe->spec_n + a, max_spec, sf);
     if (rc) return rc;
@@ -778,9 +882,27 @@ int svo_frontend_create(svo_ctx* ctx, const svo_frontend_config* cfg, svo_fronte
         return set_error(ctx, SVO_ERR_HIP, "svo_frontend_create: score map alloc");
     }
     fe->pose.assign((size_t)S * 6, 0.0);
-    int nt = c.host_threads > 0 ? c.host_threads : (int)std::thread::hardware_concurrency();
+    // host pool: this rank's share of the node's cores (NUMA-local to its GPU),
+    // at most 16 threads (the box's CPU share per GPU) and one per sequence
+    {
+        const char* lr = std::getenv("LOCAL_RANK");
+        const char* lw = std::getenv("LOCAL_WORLD_SIZE");
+        const int rank = lr ? std::atoi(lr) : 0, world = lw ? std::max(1, std::atoi(lw)) : 1;
+        int ndev = 0;
+        (void)hipGetDeviceCount(&ndev);
+        std::vector<int> gnode(world, -1);
+        for (int r = 0; r < world && ndev > 0; r++) gnode[r] = device_numa_node(r % ndev);
+        fe->host_cpus = host_cpu_plan(std::min(rank, world - 1), world, gnode.data());
+        if (world == 1 && c.host_threads <= 0 && (int)fe->host_cpus.size() > 16) {
+            // one rank: keep to 16 cores of the GPU's node (its CPU share on the box)
+            fe->host_cpus.resize(16);
+        }
+    }
+    int nt = c.host_threads > 0 ? c.host_threads
+                                : (fe->host_cpus.empty() ? (int)std::thread::hardware_concurrency()
+                                                         : (int)fe->host_cpus.size());
     nt = std::max(1, std::min({nt, S, 16}));
-    fe->pool = new Pool(nt - 1);
+    fe->pool = new Pool(nt - 1, fe->host_cpus);
     for (auto& e : fe->ev) (void)hipEventCreate(&e);
     // pipeline slices: contiguous, near-equal sequence ranges
     {
@@ -1003,13 +1125,18 @@ static int fe_post(svo_frontend* fe, int t) {
         SVO_HIP(ctx, launch_post_lk(fe_post_lk_batch(fe, fe->g0[g]), fe->gn[g], sg));
         ph_end(fe, sg, slot);
         SVO_HIP(ctx, hipEventRecord(fe->ev_sync[3 + 2 * g], sg));
+        // the keyframe's stereo matches, speculatively, beside this slice's RANSAC
+        if (fe->spec_margin >= 0) {
+            int rq = fe_queue_spec(fe, t, fe->g0[g], fe->gn[g],
+                                   std::min(fe->cfg.n_features + fe->spec_margin, fe->CAP), fe->ev_sync[3 + 2 * g]);
+            if (rq) return rq;
+        }
     }
     // every slice's points are gathered once the last slice's post-LK is done
     SVO_HIP(ctx, hipEventRecord(fe->ev_gathered, fe->gst[G - 1]));
     for (int g = 0; g + 1 < G; g++) SVO_HIP(ctx, hipStreamWaitEvent(fe->st_copy, fe->ev_sync[3 + 2 * g], 0));
     // the full point set for the final fits / long RANSAC runs, on the copy stream
     // (parity buffers: the previous step's fits still read theirs)
-    (void)t;
     return fe_queue_full(fe);
 }
 
@@ -1239,16 +1366,7 @@ int svo_frontend_step(svo_frontend* fe, int t, svo_frontend_stats* stats) {
         SVO_HIP(ctx, hipEventSynchronize(fe->ev_sync[3 + 2 * g]));
         TP("lk results on host");
         ms_wait += ms_since(tw);
-        // the keyframe's stereo matches, speculatively, beside this RANSAC (FAST
-        // is already queued ahead of it on the FAST stream)
-        const bool spec = fe->spec_margin >= 0;
-        if (spec) {
-            int max_spec = 0;
-            for (int s = a; s < a + n; s++) max_spec = std::max(max_spec, c.n_features - fe->h_nB[s] + fe->spec_margin);
-            int rq = fe_queue_spec(fe, t, a, n, std::min(max_spec, CAP));
-            if (rq) return rq;
-            TP("spec stereo queued");
-        }
+        const bool spec = fe->spec_margin >= 0;  // the stereo LK went out with the post-LK (fe_post)
         int max_b = 0;
         bool need_full = false;
         for (int s = a; s < a + n; s++) {
@@ -1562,6 +1680,22 @@ int svo_frontend_time_pyramid(svo_frontend* fe, int t, int reps, double* ms_per_
     (void)hipEventDestroy(e1);
     *ms_per_launch = ms / reps;
     fe->pyr_ready = -1;
+    return SVO_OK;
+}
+
+int svo_host_cpu_plan(int local_rank, int local_world, const int* gpu_node, int* cpus, int cap, int* n) {
+    if (local_world <= 0 || local_rank < 0 || local_rank >= local_world || cap < 0 || (cap > 0 && !cpus))
+        return SVO_ERR_ARG;
+    const std::vector<int> v = host_cpu_plan(local_rank, local_world, gpu_node);
+    for (int i = 0; i < (int)v.size() && i < cap; i++) cpus[i] = v[i];
+    if (n) *n = (int)v.size();
+    return SVO_OK;
+}
+
+int svo_frontend_host_cpus(svo_frontend* fe, int* cpus, int cap, int* n) {
+    if (!fe || cap < 0 || (cap > 0 && !cpus)) return SVO_ERR_ARG;
+    for (int i = 0; i < (int)fe->host_cpus.size() && i < cap; i++) cpus[i] = fe->host_cpus[i];
+    if (n) *n = (int)fe->host_cpus.size();
     return SVO_OK;
 }
 

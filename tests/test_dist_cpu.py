@@ -46,3 +46,36 @@ def test_bench_dist_plumbing_gloo(world):
         assert s == 4.0 * world            # total sequences
         flat = [x for seeds in allseeds for x in seeds]
         assert len(flat) == len(set(flat)) == 4 * world   # disjoint shards
+
+
+def _plan_worker(rank, world, port, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(world), RANK=str(rank),
+                      LOCAL_RANK=str(rank), LOCAL_WORLD_SIZE=str(world))
+    import svo_amd as S
+    w, r, local, dist = bench.dist_setup()
+    mine = S.host_cpu_plan(local, w)                   # no GPU: split the node by rank
+    numa = S.host_cpu_plan(local, w, [0] * w)          # both GPUs on NUMA node 0
+    allp = [None] * world
+    dist.all_gather_object(allp, (mine, numa))
+    out[rank] = allp
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2])
+def test_host_cpu_plan_disjoint_per_rank_gloo(world):
+    """Each rank's RANSAC pool gets its own cores (svo_host_cpu_plan): with one
+    process per GPU on a node the ranks' sets are disjoint, non-empty, inside
+    the allowed CPUs, and NUMA-node-local when the GPUs' node is given."""
+    allowed = sorted(os.sched_getaffinity(0))
+    if len(allowed) < world:
+        pytest.skip("fewer CPUs than ranks")
+    port = _free_port()
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_plan_worker, args=(world, port, out), nprocs=world, join=True)
+    plans = out[0]
+    for k in range(2):
+        sets = [set(p[k]) for p in plans]
+        assert all(sets) and all(s <= set(allowed) for s in sets)
+        assert not set.intersection(*sets)
+    assert set().union(*(set(p[0]) for p in plans)) == set(allowed)   # the whole node is used
