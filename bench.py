@@ -212,7 +212,10 @@ def main():
         if s % 16 == 15:
             print(f"[bench] rank {rank}: {s + 1}/{Sq} sequences rendered and uploaded", file=sys.stderr, flush=True)
     fe.init(0)
-    host_cpus = fe.host_cpus()  # this rank's pinned share of the node (svo_host_cpu_plan)
+    try:
+        host_cpus = fe.host_cpus()  # this rank's pinned share of the node (svo_host_cpu_plan)
+    except (AttributeError, S.SvoError):  # an older library under SVO_GPU_LIB A/B
+        host_cpus = []
     feats_after = {}  # features after step t = the inputs of LK(t + 1)
     for t in range(1, Wm + 1):
         feats_after[t] = fe.step(t).as_dict()["features"]
@@ -241,11 +244,14 @@ def main():
     # after reset_times bracket the LK launches of the last lk_n timed steps
     # (step Wm+1's LK went out during the warm-up); LK(t) tracks the features left
     # after step t-1, so those launches processed feats_after[t-1] features each.
+    # (with G pipeline slices a step's LK is G launches, one per slice of the batch)
     lk_ms, lk_n = phases["lk"]
     L = ML + 1
     last = Wm + K
-    lk_units = sum(feats_after[t - 1] for t in range(last - lk_n + 1, last + 1)) if lk_n > 0 else 0
-    assert lk_n <= K, "more LK launches timed than steps"
+    G = max(1, min(args.groups, Sq)) if args.groups > 0 else 1
+    lk_steps = lk_n // G
+    lk_units = sum(feats_after[t - 1] for t in range(last - lk_steps + 1, last + 1)) if lk_steps > 0 else 0
+    assert lk_steps <= K and lk_n % G == 0, "LK launches timed do not match the steps"
     units_per_launch = lk_units / max(lk_n, 1)
     bytes_per_launch = units_per_launch * lk_bytes_per_feature(L)
     lk_avg_s = lk_ms / max(lk_n, 1) / 1e3

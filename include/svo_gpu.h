@@ -89,6 +89,11 @@ int svo_image_upload_bgr(svo_ctx* ctx, svo_image* img, const uint8_t* bgr, int s
 int svo_image_build_pyramid(svo_ctx* ctx, svo_image* img);
 int svo_image_level_size(const svo_image* img, int level, int* w, int* h);
 int svo_image_download_level(svo_ctx* ctx, const svo_image* img, int level, uint8_t* dst, int stride);
+/* The Scharr derivatives of pyramid level `level` (built pyramid required) as the
+ * LK kernels read them: calcSharrDeriv (inside calcOpticalFlowPyrLK,
+ * R:src/tracking.cpp:101, :160) scaled by 4, int16 ix / iy of that level's w x h
+ * with `stride` elements per row; either output may be null. */
+int svo_image_scharr_level(svo_ctx* ctx, const svo_image* img, int level, int16_t* ix, int16_t* iy, int stride);
 
 /* ------------------------------------------------------------ FAST
  * cv::FastFeatureDetector(threshold, nonmaxSuppression, TYPE_9_16)::detect(
@@ -293,6 +298,12 @@ int svo_frontend_map_points(svo_frontend* fe, int seq, double* xyz, int cap, int
  * 5 tail, 6 fast, 7 bucket, 8 append, 9 pyramid_right. Returns the number of phases. */
 int svo_frontend_phase_times(svo_frontend* fe, double* ms, int64_t* launches, int cap);
 void svo_frontend_reset_times(svo_frontend* fe);
+/* The Scharr derivatives (svo_image_scharr_level's layout) of frame t of sequence
+ * seq as the front end's fused pyrDown + Scharr pass built them; frame t must be
+ * one of the last three frames whose pyramid was built (the derivative pyramids
+ * are triple-buffered): after svo_frontend_init(t0) frame t0, after
+ * svo_frontend_step(t) frames t and t + 1. Synchronises the front end first. */
+int svo_frontend_scharr_level(svo_frontend* fe, int seq, int t, int level, int16_t* ix, int16_t* iy, int stride);
 /* The pyramid + Scharr launch chain of frame t (every sequence) timed alone on the
  * context stream: reps rebuilds (identical contents) after one warm-up, HIP
  * events around them; ms per chain. Synchronises the front end first. */

@@ -74,6 +74,7 @@ _SIGS = [
     ("svo_image_build_pyramid", C.c_int, [_vp, _vp]),
     ("svo_image_level_size", C.c_int, [_vp, C.c_int, _i32p, _i32p]),
     ("svo_image_download_level", C.c_int, [_vp, _vp, C.c_int, _u8p, C.c_int]),
+    ("svo_image_scharr_level", C.c_int, [_vp, _vp, C.c_int, C.POINTER(C.c_int16), C.POINTER(C.c_int16), C.c_int]),
     ("svo_fast_detect", C.c_int, [_vp, _vp, C.c_int, C.c_int, _u8p, _f32p, C.c_int, _i32p]),
     ("svo_orb_detect", C.c_int, [_vp, _vp, _vp, _u8p, _f32p, _i32p, C.c_int, _i32p]),
     ("svo_fast_score_map", C.c_int, [_vp, _vp, C.c_int, _u8p, _u8p]),
@@ -99,6 +100,8 @@ _SIGS = [
     ("svo_frontend_set_frame_bgr", C.c_int, [_vp, C.c_int, C.c_int, _u8p, _u8p, C.c_int]),
     ("svo_frontend_map_points", C.c_int, [_vp, C.c_int, _f64p, C.c_int, _i32p]),
     ("svo_frontend_time_pyramid", C.c_int, [_vp, C.c_int, C.c_int, _f64p]),
+    ("svo_frontend_scharr_level", C.c_int, [_vp, C.c_int, C.c_int, C.c_int, C.POINTER(C.c_int16),
+                                            C.POINTER(C.c_int16), C.c_int]),
     ("svo_frontend_prebuild_pyramids", C.c_int, [_vp]),
     ("svo_frontend_init", C.c_int, [_vp, C.c_int]),
     ("svo_frontend_step", C.c_int, [_vp, C.c_int, _vp]),
@@ -139,7 +142,10 @@ def lib():
         if not os.path.exists(path):
             raise SvoError(f"HIP extension not built: {path} missing (run __graft_entry__.build())")
         L = C.CDLL(path)
+        ab = bool(os.environ.get("SVO_GPU_LIB"))
         for name, res, args in _SIGS:
+            if ab and not hasattr(L, name):  # an older build under A/B: its missing entry points stay unbound
+                continue
             f = getattr(L, name)
             f.restype = res
             f.argtypes = args
@@ -169,6 +175,20 @@ class Image:
         out = np.empty((h.value, w.value), np.uint8)
         self.ctx._check(L.svo_image_download_level(self.ctx.handle, self.handle, l, _p(out, _u8p), w.value))
         return out
+
+    def scharr(self, l: int):
+        """(ix, iy) of level l as the LK kernels read them: Scharr derivatives x 4
+        (int16) -- svo_image_scharr_level."""
+        L = lib()
+        w, h = C.c_int(), C.c_int()
+        if L.svo_image_level_size(self.handle, l, C.byref(w), C.byref(h)) != 0:
+            raise SvoError(f"no level {l}")
+        ix = np.empty((h.value, w.value), np.int16)
+        iy = np.empty_like(ix)
+        self.ctx._check(L.svo_image_scharr_level(self.ctx.handle, self.handle, l,
+                                                 ix.ctypes.data_as(C.POINTER(C.c_int16)),
+                                                 iy.ctypes.data_as(C.POINTER(C.c_int16)), w.value))
+        return ix, iy
 
     def upload(self, gray: np.ndarray):
         gray = _c(gray, np.uint8)
@@ -558,6 +578,16 @@ class Frontend:
 
     def reset_times(self):
         lib().svo_frontend_reset_times(self.handle)
+
+    def scharr(self, seq, t, level, w, h):
+        """(ix, iy) of frame t's level (w x h) as the fused pyrDown + Scharr pass built
+        them (svo_frontend_scharr_level)."""
+        ix = np.empty((h, w), np.int16)
+        iy = np.empty_like(ix)
+        self.ctx._check(lib().svo_frontend_scharr_level(self.handle, int(seq), int(t), int(level),
+                                                        ix.ctypes.data_as(C.POINTER(C.c_int16)),
+                                                        iy.ctypes.data_as(C.POINTER(C.c_int16)), w))
+        return ix, iy
 
     def host_cpus(self):
         """CPUs the host pool is pinned to (svo_host_cpu_plan's share of this rank)."""

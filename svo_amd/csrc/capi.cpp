@@ -94,6 +94,22 @@ static PyrDesc* stage_desc(svo_ctx* ctx, const svo_image* img, void* dst) {
 
 using namespace svo;
 
+namespace svo {
+int download_deriv_level(svo_ctx* ctx, const DerivDesc& dd, int level, int w, int h, int16_t* ix, int16_t* iy,
+                         int stride) {
+    std::vector<uint32_t> v((size_t)w * h);
+    SVO_HIP(ctx, hipMemcpy2D(v.data(), (size_t)w * 4, dd.data[level], (size_t)dd.pitch[level] * 4, (size_t)w * 4, h,
+                             hipMemcpyDeviceToHost));
+    for (int y = 0; y < h; y++)
+        for (int x = 0; x < w; x++) {
+            const uint32_t p = v[(size_t)y * w + x];
+            if (ix) ix[(size_t)y * stride + x] = (int16_t)(p & 0xFFFFu);
+            if (iy) iy[(size_t)y * stride + x] = (int16_t)(p >> 16);
+        }
+    return SVO_OK;
+}
+}  // namespace svo
+
 extern "C" {
 
 const char* svo_version(void) { return "svo_gpu gfx950 hip " SVO_HIP_VERSION_STR; }
@@ -226,6 +242,42 @@ int svo_image_download_level(svo_ctx* ctx, const svo_image* img, int level, uint
                                   ctx->stream));
     SVO_HIP(ctx, hipStreamSynchronize(ctx->stream));
     return SVO_OK;
+}
+
+
+int svo_image_scharr_level(svo_ctx* ctx, const svo_image* img, int level, int16_t* ix, int16_t* iy, int stride) {
+    if (!ctx || !img || level < 0 || level >= img->nlevels)
+        return set_error(ctx, SVO_ERR_ARG, "svo_image_scharr_level: bad arguments");
+    const ImgLevel& L = img->desc.lv[level];
+    if (stride < L.w) return set_error(ctx, SVO_ERR_ARG, "svo_image_scharr_level: stride");
+    const int nl = level + 1;
+    size_t doff[kMaxLevels];
+    int dpitch[kMaxLevels];
+    const size_t dbytes = deriv_layout(img->w, img->h, nl, doff, dpitch);
+    char* d = (char*)scratch(ctx, 8, dbytes + 1024);
+    if (!d) return set_error(ctx, SVO_ERR_HIP, "scratch alloc");
+    struct Staged {
+        PyrDesc pd;
+        DerivDesc dd;
+    };
+    Staged* hs = (Staged*)pinned(ctx, sizeof(Staged));
+    if (!hs) return set_error(ctx, SVO_ERR_HIP, "pinned alloc");
+    SVO_HIP(ctx, hipStreamSynchronize(ctx->stream));  // pinned staging is reused
+    char* dbase = d + 512;
+    hs->pd = img->desc;
+    for (int l = 0; l < kMaxLevels; l++) {
+        hs->dd.data[l] = l < nl ? (uint32_t*)(dbase + doff[l]) : nullptr;
+        hs->dd.pitch[l] = l < nl ? dpitch[l] : 0;
+    }
+    PyrDesc* ddesc = (PyrDesc*)d;
+    DerivDesc* dder = (DerivDesc*)(d + 256);
+    static_assert(sizeof(PyrDesc) <= 256 && sizeof(DerivDesc) <= 256, "staging slots");
+    SVO_HIP(ctx, hipMemcpyAsync(ddesc, &hs->pd, sizeof(PyrDesc), hipMemcpyHostToDevice, ctx->stream));
+    SVO_HIP(ctx, hipMemcpyAsync(dder, &hs->dd, sizeof(DerivDesc), hipMemcpyHostToDevice, ctx->stream));
+    SVO_HIP(ctx, hipMemsetAsync(dbase, 0, dbytes, ctx->stream));
+    SVO_HIP(ctx, launch_scharr(ddesc, dder, 1, img->w, img->h, nl, ctx->stream));
+    SVO_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    return download_deriv_level(ctx, hs->dd, level, L.w, L.h, ix, iy, stride);
 }
 
 // ------------------------------------------------------------------ FAST

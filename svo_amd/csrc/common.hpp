@@ -164,6 +164,10 @@ struct DerivDesc {
 // off[l] = element-0 offset (bytes) of level l's interior from the buffer start;
 // the buffer must be zeroed once (the borders are never written).
 size_t deriv_layout(int w, int h, int nlevels, size_t* off, int* pitch);
+// level `level` (w x h) of a derivative pyramid to the host, split into ix / iy
+// (int16, x 2^kDerShift as stored); either output may be null (capi.cpp)
+int download_deriv_level(svo_ctx* ctx, const DerivDesc& dd, int level, int w, int h, int16_t* ix, int16_t* iy,
+                         int stride);
 // REFLECT_101 border of levels [0, nlevels) of nseq pyramids (after they are built)
 hipError_t launch_pyramid_pad(const PyrDesc* d_descs, int nseq, int w, int h, int nlevels, hipStream_t st);
 // one level's derivative (level dims lw x lh)

@@ -221,6 +221,11 @@ std::vector<int> host_cpu_plan(int rank, int world, const int* gpu_node) {
     return split(allowed, rank, world);
 }
 
+int world_size_env() {
+    const char* lw = std::getenv("LOCAL_WORLD_SIZE");
+    return lw ? std::max(1, std::atoi(lw)) : 1;
+}
+
 // NUMA node of HIP device d (-1: unknown), from its PCI address in sysfs
 int device_numa_node(int d) {
     char bus[64] = {0};
@@ -265,6 +270,8 @@ struct svo_frontend {
     int *midA, *midB, *nA, *nB, *iters, *kn, *bn, *map_n, *rowcnt, *rowoff, *scr, *cnt, *added, *st_n;
     int *pend0, *pend_n;  // PendingMap ranges
     int* spec_n;          // speculative stereo candidates per sequence (StereoPrepBatch)
+    std::vector<int> lk_queued;  // [g] step whose temporal LK is already queued on slice g
+    bool pipe = true;            // next step's LK of a slice queued right behind its keyframe (SVO_FE_PIPE)
     int spec_margin = 32;  // RANSAC drops covered by the speculative stereo LK (SVO_FE_SPEC_MARGIN, < 0: off)
     unsigned long long* fbits;
     uint8_t* status;
@@ -872,6 +879,8 @@ int svo_frontend_create(svo_ctx* ctx, const svo_frontend_config* cfg, svo_fronte
         fe->fast_early = !(fe_ && fe_[0] == '0');
         const char* ff = std::getenv("SVO_FE_FAST_FIRST");
         fe->fast_first = ff && ff[0] == '1';
+        const char* pp = std::getenv("SVO_FE_PIPE");
+        fe->pipe = !(pp && pp[0] == '0');
         const char* sm = std::getenv("SVO_FE_SPEC_MARGIN");
         fe->spec_margin = sm ? std::atoi(sm) : 32;
     }
@@ -892,14 +901,15 @@ int svo_frontend_create(svo_ctx* ctx, const svo_frontend_config* cfg, svo_fronte
         (void)hipGetDeviceCount(&ndev);
         std::vector<int> gnode(world, -1);
         for (int r = 0; r < world && ndev > 0; r++) gnode[r] = device_numa_node(r % ndev);
-        fe->host_cpus = host_cpu_plan(std::min(rank, world - 1), world, gnode.data());
-        if (world == 1 && c.host_threads <= 0 && (int)fe->host_cpus.size() > 16) {
-            // one rank: keep to 16 cores of the GPU's node (its CPU share on the box)
-            fe->host_cpus.resize(16);
-        }
+        // SVO_POOL_PIN: 1 pin always, 0 never; default: pin when several ranks share
+        // the node (one process alone keeps the OS placement: pinning it to fixed
+        // cores measured up to 4x slower host work on a shared box)
+        const char* pe = std::getenv("SVO_POOL_PIN");
+        const bool pin = pe ? pe[0] == '1' : world > 1;
+        if (pin) fe->host_cpus = host_cpu_plan(std::min(rank, world - 1), world, gnode.data());
     }
     int nt = c.host_threads > 0 ? c.host_threads
-                                : (fe->host_cpus.empty() ? (int)std::thread::hardware_concurrency()
+                                : (fe->host_cpus.empty() ? (int)std::thread::hardware_concurrency() / world_size_env()
                                                          : (int)fe->host_cpus.size());
     nt = std::max(1, std::min({nt, S, 16}));
     fe->pool = new Pool(nt - 1, fe->host_cpus);
@@ -924,8 +934,11 @@ int svo_frontend_create(svo_ctx* ctx, const svo_frontend_config* cfg, svo_fronte
         // run concurrently (no serialisation between slices), slice 0's blocks are
         // dispatched first and finish first, so its RANSAC overlaps the later LKs
         fe->gst.assign(G, nullptr);
+        // SVO_FE_SLICE_PRIO=0: every slice at the same (highest) priority
+        const char* spe = std::getenv("SVO_FE_SLICE_PRIO");
+        const bool slice_prio = !(spe && spe[0] == '0');
         for (int g = 0; g < G; g++) {
-            const int pr = g == 0 ? greatest : std::min(std::max(greatest + 1, greatest), least);
+            const int pr = (g == 0 || !slice_prio) ? greatest : std::min(std::max(greatest + 1, greatest), least);
             if (hipStreamCreateWithPriority(&fe->gst[g], hipStreamNonBlocking, pr) != hipSuccess) {
                 svo_frontend_destroy(fe);
                 return set_error(ctx, SVO_ERR_HIP, "svo_frontend_create: stream");
@@ -946,6 +959,7 @@ int svo_frontend_create(svo_ctx* ctx, const svo_frontend_config* cfg, svo_fronte
         (void)hipEventCreateWithFlags(&fe->ev_stats, hipEventDisableTiming);
         (void)hipEventCreateWithFlags(&fe->ev_gathered, hipEventDisableTiming);
         fe->ev_tail.assign(G, nullptr);
+        fe->lk_queued.assign(G, -1);
         for (auto& e : fe->ev_tail) (void)hipEventCreateWithFlags(&e, hipEventDisableTiming);
         for (auto& e : fe->ev_full_b) (void)hipEventCreateWithFlags(&e, hipEventDisableTiming);
         fe->ev_full = fe->ev_full_b[0];
@@ -1020,6 +1034,7 @@ static int fe_drain(svo_frontend* fe) {
     SVO_HIP(ctx, hipStreamSynchronize(ctx->stream));
     fe->front_t = -1;
     fe->pyr_ready = -1;
+    std::fill(fe->lk_queued.begin(), fe->lk_queued.end(), -1);
     return SVO_OK;
 }
 
@@ -1140,6 +1155,51 @@ static int fe_post(svo_frontend* fe, int t) {
     return fe_queue_full(fe);
 }
 
+// Temporal LK of step t (frame t-1 -> t, trackFrames R:src/tracking.cpp:154-179)
+// for slice g on its stream, behind the pyramid of frame t (ev_sync[0]).
+static int fe_lk_slice(svo_frontend* fe, int t, int g) {
+    svo_ctx* ctx = fe->ctx;
+    const int S = fe->S, CAP = fe->CAP;
+    const svo_frontend_config& c = fe->cfg;
+    const PyrDesc* dprev = fe->d_desc + (size_t)((t - 1) % fe->T) * S;
+    const PyrDesc* dcur = fe->d_desc + (size_t)(t % fe->T) * S;
+    LKParams lp;
+    lp.win_w = lp.win_h = c.win;
+    lp.max_level = fe->ml;
+    lp.max_count = std::min(std::max(c.lk_max_count, 0), 100);
+    const double eps = std::min(std::max(c.lk_epsilon, 0.0), 10.0);
+    lp.eps2 = eps * eps;
+    lp.flags = c.lk_flags & ~SVO_LK_USE_INITIAL_FLOW;
+    lp.min_eig = (float)c.min_eig;
+    lp.want_err = 0;
+    {
+        static const bool quad_off = [] {
+            const char* e = std::getenv("SVO_LK_QUAD");
+            return e && e[0] == '0';
+        }();
+        lp.quad = quad_off ? 0 : 1;
+        static const int multi = [] {
+            const char* e = std::getenv("SVO_LK_MULTI");
+            return e ? std::atoi(e) : 41;
+        }();
+        lp.multi = multi;
+    }
+    const int a = fe->g0[g], n = fe->gn[g];
+    hipStream_t sg = fe->gst[g];
+    const int mp = CAP;  // grid bound: the host counts of the previous tail may not be back yet
+    SVO_HIP(ctx, hipStreamWaitEvent(sg, fe->ev_sync[0], 0));
+    LKBatch lb{dprev + a, dcur + a, fe->d_der + (size_t)((t - 1) % 3) * S + a, fe->xyA + 2 * (size_t)a * CAP,
+               fe->next_xy + 2 * (size_t)a * CAP, fe->status + (size_t)a * CAP, nullptr,
+               fe->iters + (size_t)a * CAP, fe->nA + a, 0, CAP};
+    int slot;
+    ph_begin(fe, PH_LK, sg, &slot);
+    SVO_HIP(ctx, launch_lk(lb, n, mp, lp, sg));
+    ph_end(fe, sg, slot);
+    SVO_HIP(ctx, hipEventRecord(fe->ev_sync[2 + 2 * g], sg));
+    fe->lk_queued[g] = t;
+    return SVO_OK;
+}
+
 // First half of a step (enqueue only, no host waits): the previous step's side
 // work if still pending, the pyramid of frame t if not built ahead, temporal LK,
 // FAST, the right pyramid of frame t and frame t+1's left pyramid.
@@ -1148,9 +1208,7 @@ static int fe_post(svo_frontend* fe, int t) {
 static int fe_front_lk(svo_frontend* fe, int t) {
     svo_ctx* ctx = fe->ctx;
     hipStream_t st0 = ctx->stream;
-    const int S = fe->S, CAP = fe->CAP, G = fe->G;
-    const svo_frontend_config& c = fe->cfg;
-    const PyrDesc* dprev = fe->d_desc + (size_t)((t - 1) % fe->T) * S;
+    const int S = fe->S, G = fe->G;
     const PyrDesc* dcur = fe->d_desc + (size_t)(t % fe->T) * S;
     hipEvent_t ev_pyr = fe->ev_sync[0];
     int slot;
@@ -1185,50 +1243,12 @@ static int fe_front_lk(svo_frontend* fe, int t) {
         SVO_HIP(ctx, hipEventRecord(ev_pyr, st0));
     }
 
-    // 3. per slice: temporal LK (trackFrames), keep status == 1, gather map
-    //    points, D2H. Slice g's LK starts after slice g-1's so that slice 0's
-    //    results reach the host first and its RANSAC overlaps slice 1's LK.
-    LKParams lp;
-    lp.win_w = lp.win_h = c.win;
-    lp.max_level = fe->ml;
-    lp.max_count = std::min(std::max(c.lk_max_count, 0), 100);
-    const double eps = std::min(std::max(c.lk_epsilon, 0.0), 10.0);
-    lp.eps2 = eps * eps;
-    lp.flags = c.lk_flags & ~SVO_LK_USE_INITIAL_FLOW;
-    lp.min_eig = (float)c.min_eig;
-    lp.want_err = 0;
-    {
-        static const bool quad_off = [] {
-            const char* e = std::getenv("SVO_LK_QUAD");
-            return e && e[0] == '0';
-        }();
-        lp.quad = quad_off ? 0 : 1;
-        static const int multi = [] {
-            const char* e = std::getenv("SVO_LK_MULTI");
-            return e ? std::atoi(e) : 41;
-        }();
-        lp.multi = multi;
-    }
-    // SVO_FE_FAST_FIRST=1: FAST(t) enqueued ahead of LK(t) (with a high-priority
-    // FAST stream its blocks are dispatched first, so FAST no longer gates the tail)
-    if (fe->fast_early && fe->fast_first) {
-        hipStream_t sf = fe->st_fast;
-        int rc = fe_fast_and_bucket(fe, dcur, true, sf, true);
-        if (rc) return rc;
-        SVO_HIP(ctx, hipEventRecord(fe->ev_sync[1], sf));
-    }
+    // 3. per slice: temporal LK (trackFrames) -- unless the pipelined schedule
+    //    already queued it behind the slice's previous keyframe (fe_lk_slice)
     for (int g = 0; g < G; g++) {
-        const int a = fe->g0[g], n = fe->gn[g];
-        hipStream_t sg = fe->gst[g];
-        const int mp = CAP;  // grid bound: the host counts of the previous tail may not be back yet
-        SVO_HIP(ctx, hipStreamWaitEvent(sg, ev_pyr, 0));
-        LKBatch lb{dprev + a, dcur + a, fe->d_der + (size_t)((t - 1) % 3) * S + a, fe->xyA + 2 * (size_t)a * CAP,
-                   fe->next_xy + 2 * (size_t)a * CAP, fe->status + (size_t)a * CAP, nullptr,
-                   fe->iters + (size_t)a * CAP, fe->nA + a, 0, CAP};
-        ph_begin(fe, PH_LK, sg, &slot);
-        SVO_HIP(ctx, launch_lk(lb, n, mp, lp, sg));
-        ph_end(fe, sg, slot);
-        SVO_HIP(ctx, hipEventRecord(fe->ev_sync[2 + 2 * g], sg));
+        if (fe->lk_queued[g] == t) continue;
+        int rl = fe_lk_slice(fe, t, g);
+        if (rl) return rl;
     }
     // 3b. mask around frame t-1's features (the reference masks with prevFrame's
     //     features, R:src/tracking.cpp:77) + FAST/bucket on frame t, whole batch:
@@ -1528,6 +1548,13 @@ int svo_frontend_step(svo_frontend* fe, int t, svo_frontend_stats* stats) {
         if (rc) return rc;
         SVO_HIP(ctx, hipEventRecord(fe->ev_tail[g], sg));
         TP("tail queued");
+        // pipelined schedule: this slice's next LK goes out right behind its
+        // keyframe (frame t+1's pyramid was queued with this step's front), so
+        // the GPU tracks it while the host runs the next slices' RANSAC
+        if (fe->pipe && G > 1 && t + 1 < fe->T && fe->pyr_ready == t + 1) {
+            int rl = fe_lk_slice(fe, t + 1, g);
+            if (rl) return rl;
+        }
     }
     fe->fits_pending = true;  // statistics land with the stream syncs below
     fe->fit_parity = t & 1;
@@ -1654,6 +1681,18 @@ int svo_frontend_map_points(svo_frontend* fe, int seq, double* xyz, int cap, int
     }
     if (n) *n = cnt;
     return SVO_OK;
+}
+
+int svo_frontend_scharr_level(svo_frontend* fe, int seq, int t, int level, int16_t* ix, int16_t* iy, int stride) {
+    if (!fe || seq < 0 || seq >= fe->S || t < 0 || level < 0 || level >= fe->nlev) return SVO_ERR_ARG;
+    int rc = svo_frontend_synchronize(fe);
+    if (rc) return rc;
+    svo_ctx* ctx = fe->ctx;
+    const ImgLevel& L = fe->desc_host[(size_t)(t % fe->T) * fe->S + seq].lv[level];
+    if (stride < L.w) return set_error(ctx, SVO_ERR_ARG, "svo_frontend_scharr_level: stride");
+    DerivDesc dd;
+    SVO_HIP(ctx, hipMemcpy(&dd, fe->d_der + (size_t)(t % 3) * fe->S + seq, sizeof(dd), hipMemcpyDeviceToHost));
+    return download_deriv_level(ctx, dd, level, L.w, L.h, ix, iy, stride);
 }
 
 int svo_frontend_time_pyramid(svo_frontend* fe, int t, int reps, double* ms_per_launch) {

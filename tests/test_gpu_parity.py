@@ -41,6 +41,49 @@ def test_pyramid_bit_exact(ctx, wh):
         lvl = O.pyr_down(lvl)
 
 
+# ------------------------------------------------------------------ Scharr derivative pyramid
+@pytest.mark.parametrize("wh", [(1241, 376), (161, 121), (97, 33), (7, 5), (2, 3)])
+def test_scharr_levels_bit_exact(ctx, wh):
+    """svo_image_scharr_level: every level's Scharr derivatives (stored x4, as LK
+    reads them) against the oracle's calcSharrDeriv restatement on that level."""
+    w, h = wh
+    rng = np.random.default_rng(w + 7 * h)
+    img = rng.integers(0, 256, (h, w), dtype=np.uint8)
+    g = ctx.image(img, max_levels=3)
+    lvl = img
+    for l in range(4):
+        ix, iy = g.scharr(l)
+        ref = O.scharr(lvl).astype(np.int32)
+        assert np.array_equal(ix.astype(np.int32), 4 * ref[..., 0]), f"ix level {l}"
+        assert np.array_equal(iy.astype(np.int32), 4 * ref[..., 1]), f"iy level {l}"
+        lvl = O.pyr_down(lvl)
+
+
+@pytest.mark.parametrize("wh", [(1241, 376), (640, 376), (401, 203)])
+def test_frontend_scharr_pyramid_bit_exact(ctx, wh):
+    """The front end's fused pyrDown + Scharr pass (pyr_scharr_kernel; scharr_kernel
+    for the coarsest level) against the oracle on every level of its frames."""
+    w, h = wh
+    scenes = [Scene(w, h, seed=s) for s in (3, 4)]
+    cfg = S.FrontendConfig(w, h, scenes[0].K, n_seq=2, n_frames=3, n_features=300)
+    fe = S.Frontend(ctx, cfg)
+    for s, sc in enumerate(scenes):
+        for t in range(3):
+            fe.set_frame(s, t, sc.frame(t), sc.right(t))
+    fe.init(0)
+    fe.step(1)   # builds frame 2's derivatives ahead (frames 1 and 2 resident)
+    for s, sc in enumerate(scenes):
+        for t in (1, 2):
+            lvl = sc.frame(t)
+            for l in range(4):
+                ix, iy = fe.scharr(s, t, l, lvl.shape[1], lvl.shape[0])
+                ref = O.scharr(lvl).astype(np.int32)
+                assert np.array_equal(ix.astype(np.int32), 4 * ref[..., 0]), f"seq {s} t {t} ix level {l}"
+                assert np.array_equal(iy.astype(np.int32), 4 * ref[..., 1]), f"seq {s} t {t} iy level {l}"
+                lvl = O.pyr_down(lvl)
+    fe.close()
+
+
 # ------------------------------------------------------------------ FAST
 @pytest.fixture(params=["block-queue", "wave-queue", "swar", "queue-nms"])
 def fast_kernel(request, monkeypatch):

@@ -12,6 +12,8 @@
 #                           folded into profiles/pmc_summary.json (configs[CONFIG])
 #   mix TAG [BENCH_ARGS]    SQ instruction mix per wave of every step kernel
 #   lksplit                 LK VALU / time with the iteration cap at 1, 2, 50
+#   lkab "V1 V2 .."         standalone LK kernel time per SVO_LK_MULTI variant
+#   lkmem [LIB ..]          LK memory-pipeline + issue counters (TA, TCP, SQ), per library build
 #   ab VAR "V1 V2" [RUNS]   bench A/B of an environment switch
 #   round TAG               tests, smoke, prof, pmc (3 configs), mix, bench lines
 #
@@ -139,6 +141,50 @@ P
     done
 }
 
+run_lkab() {
+    for v in ${1:-41}; do
+        local T=/tmp/lkab_$v
+        SVO_LK_MULTI=$v timeout -k 10 120 rocprofv3 --kernel-trace --stats -d $T -o run --output-format csv -- \
+            python tools/microbench.py lk --points 128000 --reps 5 > $T.log 2>&1 || fail lkab $T.log
+        echo "== SVO_LK_MULTI=$v"
+        python3 - $T <<'P'
+import csv, glob, sys
+f = glob.glob(sys.argv[1] + '/**/*kernel_stats.csv', recursive=True)[0]
+for r in csv.DictReader(open(f)):
+    if 'lk_multi' in r['Name'] or 'lk_fast' in r['Name'] or 'lk_dual' in r['Name']:
+        print(r['Name'][40:110], r['Calls'], round(float(r['AverageNs']) / 1e3, 1), round(float(r['MinNs']) / 1e3, 1))
+P
+    done
+}
+
+run_lkmem() {
+    local MB="python tools/microbench.py lk --points 128000 --reps 2"
+    for lib in ${@:-libsvo_gpu.so}; do
+        local i=0
+        for set in "TA_TA_BUSY_sum TA_DATA_STALLED_BY_TC_CYCLES_sum GRBM_GUI_ACTIVE GRBM_COUNT" \
+                   "TCP_PENDING_STALL_CYCLES_sum TCP_READ_TAGCONFLICT_STALL_CYCLES_sum TCP_TOTAL_ACCESSES_sum TCP_TCC_READ_REQ_sum" \
+                   "SQ_WAVES SQ_INSTS_VMEM_RD SQ_INSTS_VALU SQ_INSTS_LDS SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES"; do
+            i=$((i + 1))
+            local T=/tmp/lkm_${lib}_$i
+            SVO_GPU_LIB=$PWD/svo_amd/lib/$lib timeout -s KILL 90 rocprofv3 --pmc $set -d $T -o run --output-format csv -- $MB \
+                > $T.log 2>&1 || fail "lkmem pass $i" $T.log
+        done
+        echo "== $lib"
+        python3 - $lib <<'P'
+import csv, glob, sys, collections
+lib = sys.argv[1]
+agg = collections.defaultdict(float); n = collections.defaultdict(int)
+for f in glob.glob(f'/tmp/lkm_{lib}_*/**/*counter_collection.csv', recursive=True):
+    for r in csv.DictReader(open(f)):
+        if 'lk_multi' in r['Kernel_Name']:
+            agg[r['Counter_Name']] += float(r['Counter_Value']); n[r['Counter_Name']] += 1
+w = agg.get('SQ_WAVES', 1)
+for k in sorted(agg):
+    print(f"  {k:40s} per dispatch {agg[k] / n[k]:14.0f}   per wave {agg[k] / w:10.1f}")
+P
+    done
+}
+
 run_ab() {
     local var=$1 vals=$2 runs=${3:-2}
     for r in $(seq $runs); do for v in $vals; do
@@ -177,6 +223,8 @@ while [ $# -gt 0 ]; do
         pmc) run_pmc "${args[@]}" ;;
         mix) run_mix "${args[@]}" ;;
         lksplit) run_lksplit ;;
+        lkab) run_lkab "${args[@]}" ;;
+        lkmem) run_lkmem "${args[@]}" ;;
         ab) run_ab "${args[@]}" ;;
         round) run_round "${args[@]}" ;;
         *) fail "unknown mode $mode" ;;
