@@ -115,11 +115,11 @@ def pmc_traffic(cfg_name: str, kernel_prefix: str):  # substring of the demangle
     try:
         with open(path) as f:
             d = json.load(f)
-        for k, v in d.get("configs", {}).get(cfg_name, {}).get("kernels", {}).items():
-            if kernel_prefix in k:
-                return v.get("hbm_bytes_per_launch")
     except (OSError, ValueError):
         return None
+    for k, v in d.get("configs", {}).get(cfg_name, {}).get("kernels", {}).items():
+        if kernel_prefix in k and not (kernel_prefix == "scharr_kernel" and "pyr_scharr" in k):
+            return v.get("hbm_bytes_per_launch")
     return None
 
 
@@ -280,7 +280,11 @@ def main():
     pyr_avg_s = fe.time_pyramid(Wm + K, 20) / 1e3
     pyr_bytes = Sq * pyr_bytes_per_frame(W, H, ML)
     der_bytes = Sq * deriv_bytes_per_frame(W, H, ML)
-    pyr_traffic = pmc_traffic(args.config, "pyr_scharr_kernel")
+    # the chain's HBM bytes: (nlev - 1) pyr_scharr launches (their average over the
+    # levels x the count = the sum) + the coarsest level's scharr + the borders
+    t_ps, t_sc, t_pad = (pmc_traffic(args.config, k) for k in ("pyr_scharr_kernel", "scharr_kernel",
+                                                                "pad_batched_kernel"))
+    pyr_traffic = ML * t_ps + t_sc + t_pad if None not in (t_ps, t_sc, t_pad) else None
     single = None
     if not args.no_single:
         fe1 = S.Frontend(ctx, S.FrontendConfig(W, H, scenes[0].K, n_seq=1, n_frames=T, n_features=N, max_level=ML))

@@ -239,6 +239,10 @@ struct PnpBatch {
 };
 hipError_t launch_pnp_residuals(const PnpBatch& b, int nseq, int max_n, double fx, double fy, double cx,
                                 double cy, float thresh2, hipStream_t st);
+// The same scoring, one block per (hypothesis, sequence): bits as above and ONE
+// inlier count per hypothesis in b.cnt (required; no memset needed)
+hipError_t launch_pnp_score(const PnpBatch& b, int nseq, double fx, double fy, double cx, double cy, float thresh2,
+                            hipStream_t st);
 
 // Batched bucket selection: blockIdx.x = sequence. Input points are in_elem
 // floats apart (2 = xy pairs, 3 = svo_keypoint), in_cap per sequence.
