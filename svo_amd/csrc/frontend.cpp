@@ -300,8 +300,7 @@ struct svo_frontend {
     void* zmem = nullptr;
     double* z_hyps = nullptr;     // [s][kRansacChunk][12]
     uint32_t* z_bits = nullptr;   // [s][kRansacChunk][WORDS]
-    int* z_wcnt = nullptr;        // [s][kRansacChunk][WS] inliers per wave of 64 points
-    int WS = 0;
+    int* z_cnt = nullptr;         // [s][kRansacChunk] inliers per hypothesis
     bool zero_copy = true;
     std::vector<RansacSeq> rs;
     std::vector<int> pred_iters;  // [s] RANSAC hypotheses the last frame's outlier ratio implies
@@ -797,10 +796,9 @@ int svo_frontend_create(svo_ctx* ctx, const svo_frontend_config* cfg, svo_fronte
     {
         const char* e = std::getenv("SVO_FE_ZEROCOPY");
         fe->zero_copy = !(e && e[0] == '0');
-        fe->WS = (CAP + 63) / 64;
         const size_t zb = ((sizeof(double) * 12 * (size_t)S * kRansacChunk + 255) & ~(size_t)255) +
                           ((sizeof(uint32_t) * (size_t)S * kRansacChunk * fe->WORDS + 255) & ~(size_t)255) +
-                          sizeof(int) * (size_t)S * kRansacChunk * fe->WS;
+                          sizeof(int) * (size_t)S * kRansacChunk + 256;
         if (fe->zero_copy && hipHostMalloc(&fe->zmem, zb, hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess) {
             fe->zmem = nullptr;
             fe->zero_copy = false;
@@ -809,7 +807,7 @@ int svo_frontend_create(svo_ctx* ctx, const svo_frontend_config* cfg, svo_fronte
             char* p = (char*)fe->zmem;
             fe->z_hyps = carve<double>(p, 12 * (size_t)S * kRansacChunk);
             fe->z_bits = carve<uint32_t>(p, (size_t)S * kRansacChunk * fe->WORDS);
-            fe->z_wcnt = carve<int>(p, (size_t)S * kRansacChunk * fe->WS);
+            fe->z_cnt = carve<int>(p, (size_t)S * kRansacChunk);
         }
     }
     // host-coherent outputs the kernels write directly (no D2H copies on the
@@ -1449,19 +1447,20 @@ int svo_frontend_step(svo_frontend* fe, int t, svo_frontend_stats* stats) {
                         fe->hyps + 12 * (size_t)a * kRansacChunk, mmax, nullptr,
                         fe->bits_all + (size_t)a * kRansacChunk * fe->WORDS, fe->WORDS, fe->cnt + (size_t)a * kRansacChunk};
             pb.mstride = kRansacChunk;
-            if (zc) {  // the kernel reads the hypotheses and writes bits / per-wave counts in host memory
+            if (zc) {  // the kernel reads the hypotheses and writes bits / counts in host memory
                 pb.hyp = fe->z_hyps + 12 * (size_t)a * kRansacChunk;
                 pb.bits = fe->z_bits + (size_t)a * kRansacChunk * fe->WORDS;
-                pb.cnt = nullptr;
-                pb.wave_cnt = fe->z_wcnt + (size_t)a * kRansacChunk * fe->WS;
-                pb.wave_stride = fe->WS;
+                pb.cnt = fe->z_cnt + (size_t)a * kRansacChunk;
             } else {
                 SVO_HIP(ctx, hipMemcpyAsync(fe->hyps + 12 * (size_t)a * kRansacChunk,
                                             fe->h_hyps + 12 * (size_t)a * kRansacChunk,
                                             sizeof(double) * 12 * n * kRansacChunk, hipMemcpyHostToDevice, sq));
             }
             ph_begin(fe, PH_PNP, sq, &slot);
-            SVO_HIP(ctx, launch_pnp_residuals(pb, n, max_b, c.K[0], c.K[4], c.K[2], c.K[5], thr, sq));
+            if (zc)
+                SVO_HIP(ctx, launch_pnp_score(pb, n, c.K[0], c.K[4], c.K[2], c.K[5], thr, sq));
+            else
+                SVO_HIP(ctx, launch_pnp_residuals(pb, n, max_b, c.K[0], c.K[4], c.K[2], c.K[5], thr, sq));
             ph_end(fe, sq, slot);
             if (!zc) {
                 SVO_HIP(ctx, hipMemcpyAsync(fe->h_cnt + (size_t)a * kRansacChunk, fe->cnt + (size_t)a * kRansacChunk,
@@ -1479,17 +1478,8 @@ int svo_frontend_step(svo_frontend* fe, int t, svo_frontend_stats* stats) {
             // consume is a few compares per hypothesis: cheaper here than a pool dispatch
             for (int s = a; s < a + n; s++) {
                 if (ms[s] <= 0) continue;
-                int* cnts = fe->h_cnt + (size_t)s * kRansacChunk;
+                int* cnts = (zc ? fe->z_cnt : fe->h_cnt) + (size_t)s * kRansacChunk;
                 const uint32_t* bits = (zc ? fe->z_bits : fe->h_bits) + (size_t)s * kRansacChunk * fe->WORDS;
-                if (zc) {  // inlier counts = sum of the waves that hold points
-                    const int nw = (fe->h_nB[s] + 63) / 64;
-                    for (int j = 0; j < ms[s]; j++) {
-                        const int* wc = fe->z_wcnt + ((size_t)s * kRansacChunk + j) * fe->WS;
-                        int tt = 0;
-                        for (int w = 0; w < nw; w++) tt += wc[w];
-                        cnts[j] = tt;
-                    }
-                }
                 if (debug_on) {
                     const RansacSeq& r = fe->rs[s];
                     unsigned hs = 0;

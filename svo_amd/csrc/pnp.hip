@@ -16,6 +16,26 @@ namespace svo {
 
 namespace {
 
+// projectPoints + normL2Sqr<float> of point i under hypothesis R (the double
+// expression order of calibration.cpp, -ffp-contract=off): the squared residual
+__device__ __forceinline__ float pnp_residual2(const double* R, const float* __restrict__ obj,
+                                               const float* __restrict__ img, int i, double fx, double fy, double cx,
+                                               double cy) {
+    const double X = obj[3 * i], Y = obj[3 * i + 1], Z = obj[3 * i + 2];
+    double x = R[0] * X + R[1] * Y + R[2] * Z + R[9];
+    double y = R[3] * X + R[4] * Y + R[5] * Z + R[10];
+    double z = R[6] * X + R[7] * Y + R[8] * Z + R[11];
+    z = z ? 1. / z : 1;
+    x *= z;
+    y *= z;
+    const float u = (float)(x * fx + cx), v = (float)(y * fy + cy);
+    const float dx = img[2 * i] - u, dy = img[2 * i + 1] - v;
+    float s = 0.f;
+    s += dx * dx;
+    s += dy * dy;
+    return s;
+}
+
 __global__ __launch_bounds__(256) void pnp_residual_kernel(PnpBatch B, double fx, double fy, double cx,
                                                            double cy, float thresh2) {
     const int seq = blockIdx.z;
@@ -29,18 +49,7 @@ __global__ __launch_bounds__(256) void pnp_residual_kernel(PnpBatch B, double fx
     const double* R = B.hyp + 12 * ((size_t)seq * ms + h);  // uniform -> scalar loads
     bool inl = false;
     if (i < n) {
-        const double X = obj[3 * i], Y = obj[3 * i + 1], Z = obj[3 * i + 2];
-        double x = R[0] * X + R[1] * Y + R[2] * Z + R[9];
-        double y = R[3] * X + R[4] * Y + R[5] * Z + R[10];
-        double z = R[6] * X + R[7] * Y + R[8] * Z + R[11];
-        z = z ? 1. / z : 1;
-        x *= z;
-        y *= z;
-        const float u = (float)(x * fx + cx), v = (float)(y * fy + cy);
-        const float dx = img[2 * i] - u, dy = img[2 * i + 1] - v;
-        float s = 0.f;
-        s += dx * dx;
-        s += dy * dy;
+        const float s = pnp_residual2(R, obj, img, i, fx, fy, cx, cy);
         if (B.err) B.err[((size_t)seq * ms + h) * B.cap + i] = s;
         inl = s <= thresh2;
     }
@@ -61,7 +70,53 @@ __global__ __launch_bounds__(256) void pnp_residual_kernel(PnpBatch B, double fx
     if (B.wave_cnt && lane == 0 && wave * 64 < n) B.wave_cnt[((size_t)seq * ms + h) * B.wave_stride + wave] = __popcll(bal);
 }
 
+// One block per (hypothesis, sequence) over all of the sequence's points: the same
+// inlier test, bits written word by word as pnp_residual_kernel does, and the
+// inlier count reduced inside the block and written ONCE per hypothesis (B.cnt,
+// which may live in host-coherent memory: the host reads m counts per sequence
+// instead of summing per-wave counts out of uncached memory)
+constexpr int kScoreBlock = 1024;
+__global__ __launch_bounds__(kScoreBlock) void pnp_score_kernel(PnpBatch B, double fx, double fy, double cx, double cy,
+                                                                float thresh2) {
+    const int seq = blockIdx.y, h = blockIdx.x;
+    const int n = B.counts ? B.counts[seq] : B.n;
+    const float* __restrict__ obj = B.obj + 3 * (size_t)seq * B.cap;
+    const float* __restrict__ img = B.img + 2 * (size_t)seq * B.cap;
+    const int ms = B.mstride ? B.mstride : B.m;
+    const double* R = B.hyp + 12 * ((size_t)seq * ms + h);
+    uint32_t* bits = B.bits ? B.bits + ((size_t)seq * ms + h) * B.words_cap : nullptr;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int words = (n + 31) >> 5;
+    int cnt = 0;
+    for (int base = 0; base < n; base += kScoreBlock) {
+        const int i = base + threadIdx.x;
+        const bool inl = i < n && pnp_residual2(R, obj, img, i, fx, fy, cx, cy) <= thresh2;
+        const unsigned long long bal = __ballot(inl);
+        const int w0 = (base + (threadIdx.x & ~63)) >> 5;
+        if (bits) {
+            if (lane == 0 && w0 < words) bits[w0] = (uint32_t)bal;
+            if (lane == 1 && w0 + 1 < words) bits[w0 + 1] = (uint32_t)(bal >> 32);
+        }
+        cnt += __popcll(bal);
+    }
+    __shared__ int part[kScoreBlock / 64];
+    if (lane == 0) part[wv] = cnt;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int tot = 0;
+        for (int q = 0; q < kScoreBlock / 64; q++) tot += part[q];
+        B.cnt[(size_t)seq * ms + h] = tot;
+    }
+}
+
 }  // namespace
+
+hipError_t launch_pnp_score(const PnpBatch& b, int nseq, double fx, double fy, double cx, double cy, float thresh2,
+                            hipStream_t st) {
+    if (b.m <= 0 || nseq <= 0 || !b.cnt) return b.cnt ? hipSuccess : hipErrorInvalidValue;
+    hipLaunchKernelGGL(pnp_score_kernel, dim3(b.m, nseq), dim3(kScoreBlock), 0, st, b, fx, fy, cx, cy, thresh2);
+    return hipGetLastError();
+}
 
 hipError_t launch_pnp_residuals(const PnpBatch& b, int nseq, int max_n, double fx, double fy, double cx,
                                 double cy, float thresh2, hipStream_t st) {
