@@ -217,8 +217,10 @@ def main():
     except (AttributeError, S.SvoError):  # an older library under SVO_GPU_LIB A/B
         host_cpus = []
     feats_after = {}  # features after step t = the inputs of LK(t + 1)
+    tracked_at = {}  # tracked points of step t = the inputs of LK(t + 1) when it runs ahead
     for t in range(1, Wm + 1):
-        feats_after[t] = fe.step(t).as_dict()["features"]
+        st = fe.step(t).as_dict()
+        feats_after[t], tracked_at[t] = st["features"], st["tracked"]
     fe.reset_times()
     tot = {"lk_iterations": 0, "tracked": 0, "inliers": 0, "added": 0, "hypotheses": 0,
            "host_ms_hyp": 0.0, "host_ms_fit": 0.0, "host_ms_wait": 0.0}
@@ -228,7 +230,7 @@ def main():
         st = fe.step(t).as_dict()
         for k in tot:
             tot[k] += st[k]
-        feats_after[t] = st["features"]
+        feats_after[t], tracked_at[t] = st["features"], st["tracked"]
     fe.synchronize()  # the last step's pose fits / prefetched pyramid belong to the timed work
     barrier(dist)
     dt = time.perf_counter() - t0
@@ -250,7 +252,12 @@ def main():
     last = Wm + K
     G = max(1, min(args.groups, Sq)) if args.groups > 0 else 1
     lk_steps = lk_n // G
-    lk_units = sum(feats_after[t - 1] for t in range(last - lk_steps + 1, last + 1)) if lk_steps > 0 else 0
+    # LK ahead (one slice, SVO_FE_AHEAD=1): LK(t) is queued at step t-1, over its
+    # tracked points (the appended features go in a separate small launch, phase
+    # "lk_new"), so the timed launches are those of steps Wm+2 .. last
+    ahead = G == 1 and os.environ.get("SVO_FE_AHEAD", "0")[:1] == "1"
+    src = tracked_at if ahead else feats_after
+    lk_units = sum(src[t - 1] for t in range(last - lk_steps + 1, last + 1)) if lk_steps > 0 else 0
     assert lk_steps <= K and lk_n % G == 0, "LK launches timed do not match the steps"
     units_per_launch = lk_units / max(lk_n, 1)
     bytes_per_launch = units_per_launch * lk_bytes_per_feature(L)

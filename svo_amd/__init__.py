@@ -504,7 +504,8 @@ class FrontendStats(C.Structure):
                 for k, _ in self._fields_}
 
 
-PHASES = ["pyramid", "lk", "post_lk", "stereo_lk", "pnp_score", "tail", "fast", "bucket", "append", "pyramid_right"]
+PHASES = ["pyramid", "lk", "post_lk", "stereo_lk", "pnp_score", "tail", "fast", "bucket", "append", "pyramid_right",
+          "lk_new"]
 
 
 class Frontend:

@@ -25,12 +25,12 @@ constexpr int kAppendBlock = 1024;
 constexpr int kPostBlock = 512;
 
 // Stable compaction of one sequence by a keep predicate, by a BS-thread block:
-// keep(i) for i < n, kept entries of xy / mid moved to their rank (in place
-// allowed). Returns the kept count.
-template <int BS, typename Keep>
-__device__ __forceinline__ int block_compact(int n, Keep keep, const float* __restrict__ xy_in,
-                                             const int* __restrict__ mid_in, float* __restrict__ xy_out,
-                                             int* __restrict__ mid_out, int* wsum, int* base_s) {
+// keep(i) for i < n, kept entries load(i, x, y, mid) moved to their rank in
+// xy_out / mid_out (in place allowed: every read of a chunk precedes its writes,
+// and an entry never moves up). Returns the kept count.
+template <int BS, typename Keep, typename Load>
+__device__ __forceinline__ int block_compact_fn(int n, Keep keep, Load load, float* xy_out, int* mid_out, int* wsum,
+                                                int* base_s) {
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     if (tid == 0) *base_s = 0;
     __syncthreads();
@@ -44,11 +44,7 @@ __device__ __forceinline__ int block_compact(int n, Keep keep, const float* __re
         for (int q = 0; q < wv; q++) off += wsum[q];
         float x = 0.f, y = 0.f;
         int m = 0;
-        if (k) {
-            x = xy_in[2 * i];
-            y = xy_in[2 * i + 1];
-            m = mid_in[i];
-        }
+        if (k) load(i, x, y, m);
         __syncthreads();  // every read of this chunk before any write (in place allowed)
         if (k) {
             const int d = off + __popcll(bal & ((1ull << lane) - 1ull));
@@ -64,6 +60,19 @@ __device__ __forceinline__ int block_compact(int n, Keep keep, const float* __re
         __syncthreads();
     }
     return *base_s;
+}
+
+template <int BS, typename Keep>
+__device__ __forceinline__ int block_compact(int n, Keep keep, const float* xy_in, const int* mid_in, float* xy_out,
+                                             int* mid_out, int* wsum, int* base_s) {
+    return block_compact_fn<BS>(
+        n, keep,
+        [&](int i, float& x, float& y, int& m) {
+            x = xy_in[2 * i];
+            y = xy_in[2 * i + 1];
+            m = mid_in[i];
+        },
+        xy_out, mid_out, wsum, base_s);
 }
 
 // x mod n for 32-bit x, n >= 1, with a precomputed m = floor((2^32 - 1) / n)
@@ -107,9 +116,39 @@ __global__ __launch_bounds__(kPostBlock) void post_lk_kernel(PostLkBatch B) {
     const int n_in = B.n_in[s];
     const uint8_t* __restrict__ st = B.status + o;
     long long it = 0;
-    for (int i = tid; i < n_in; i += kPostBlock) it += B.iters[o + i];
-    const int n = block_compact<kPostBlock>(n_in, [&](int i) { return st[i] != 0; }, B.xy_in + 2 * o, B.mid_in + o,
-                                          B.xy_out + 2 * o, B.mid_out + o, wsum, &base_s);
+    int n;
+    if (!B.keep_bits) {
+        for (int i = tid; i < n_in; i += kPostBlock) it += B.iters[o + i];
+        n = block_compact<kPostBlock>(n_in, [&](int i) { return st[i] != 0; }, B.xy_in + 2 * o, B.mid_in + o,
+                                      B.xy_out + 2 * o, B.mid_out + o, wsum, &base_s);
+    } else {
+        // LK ran ahead over the last step's tracked points (before its RANSAC) and
+        // over its appended features: the features LK(t) would have tracked are
+        // the inliers (keep_bits) in order, then the appended ones (map ids pend0 +
+        // j), so compacting (inlier && status) ++ status2 gives the same set
+        const uint32_t* __restrict__ kb = B.keep_bits + (size_t)s * B.words_cap;
+        const int n2 = B.n2[s], m2 = B.pm.pend0[s];
+        const uint8_t* __restrict__ st2 = B.status2 + o;
+        auto inl = [&](int i) { return ((kb[i >> 5] >> (i & 31)) & 1u) != 0; };
+        for (int i = tid; i < n_in; i += kPostBlock)
+            if (inl(i)) it += B.iters[o + i];
+        for (int j = tid; j < n2; j += kPostBlock) it += B.iters2[o + j];
+        n = block_compact_fn<kPostBlock>(
+            n_in + n2, [&](int i) { return i < n_in ? inl(i) && st[i] != 0 : st2[i - n_in] != 0; },
+            [&](int i, float& x, float& y, int& m) {
+                if (i < n_in) {
+                    x = B.xy_in[2 * (o + i)];
+                    y = B.xy_in[2 * (o + i) + 1];
+                    m = B.mid_in[o + i];
+                } else {
+                    const int j = i - n_in;
+                    x = B.xy2[2 * (o + j)];
+                    y = B.xy2[2 * (o + j) + 1];
+                    m = m2 + j;
+                }
+            },
+            B.xy_out + 2 * o, B.mid_out + o, wsum, &base_s);
+    }
     for (int off = 32; off > 0; off >>= 1) it += __shfl_xor(it, off);
     if (lane == 0) atomicAdd(&it_s, (unsigned long long)it);
     // lane 0 replays the RANSAC draws (they depend only on n) while the block
@@ -236,6 +275,10 @@ __device__ __forceinline__ void append_body(const AppendBatch& A, int s, int n0,
             const size_t f = o + n0 + d;
             A.xy[2 * f] = xl;
             A.xy[2 * f + 1] = yl;
+            if (A.ap_xy) {  // the new features alone, the next LK-ahead's second input
+                A.ap_xy[2 * (o + d)] = xl;
+                A.ap_xy[2 * (o + d) + 1] = yl;
+            }
             A.mid[f] = m0 + d;
             // left camera frame (double of the float point, as Eigen::Vector3d{p_w.x,
             // p_w.y, p_w.z}); the pose is applied once known (PendingMap)
@@ -264,20 +307,22 @@ __device__ __forceinline__ void append_body(const AppendBatch& A, int s, int n0,
     }
 }
 
-__global__ __launch_bounds__(kAppendBlock) void append_kernel(AppendBatch A) {
-    __shared__ int wsum[kAppendBlock / 64];
+template <int BS>
+__global__ __launch_bounds__(BS) void append_kernel(AppendBatch A) {
+    __shared__ int wsum[BS / 64];
     __shared__ int base_s;
     const int s = blockIdx.x;
-    append_body<kAppendBlock>(A, s, A.n[s], A.st_n[s], wsum, &base_s);
+    append_body<BS>(A, s, A.n[s], A.st_n[s], wsum, &base_s);
 }
 
-__global__ __launch_bounds__(kAppendBlock) void keyframe_fused_kernel(TailBatch T, AppendBatch A) {
-    __shared__ int wsum[kAppendBlock / 64];
+template <int BS>
+__global__ __launch_bounds__(BS) void keyframe_fused_kernel(TailBatch T, AppendBatch A) {
+    __shared__ int wsum[BS / 64];
     __shared__ int base_s;
     const int s = blockIdx.x;
     int n, take;
-    tail_body<kAppendBlock>(T, s, false, wsum, &base_s, &n, &take);
-    append_body<kAppendBlock>(A, s, n, take, wsum, &base_s);
+    tail_body<BS>(T, s, false, wsum, &base_s, &n, &take);
+    append_body<BS>(A, s, n, take, wsum, &base_s);
 }
 
 __global__ __launch_bounds__(kFeBlock) void stereo_prep_kernel(StereoPrepBatch B) {
@@ -311,13 +356,19 @@ hipError_t launch_tail(const TailBatch& tb, int nseq, hipStream_t st) {
     return hipGetLastError();
 }
 
-hipError_t launch_append(const AppendBatch& b, int nseq, hipStream_t st) {
-    hipLaunchKernelGGL(append_kernel, dim3(nseq), dim3(kAppendBlock), 0, st, b);
+hipError_t launch_append(const AppendBatch& b, int nseq, hipStream_t st, bool small) {
+    if (small)
+        hipLaunchKernelGGL(append_kernel<kFeBlock>, dim3(nseq), dim3(kFeBlock), 0, st, b);
+    else
+        hipLaunchKernelGGL(append_kernel<kAppendBlock>, dim3(nseq), dim3(kAppendBlock), 0, st, b);
     return hipGetLastError();
 }
 
-hipError_t launch_keyframe_fused(const TailBatch& tb, const AppendBatch& ab, int nseq, hipStream_t st) {
-    hipLaunchKernelGGL(keyframe_fused_kernel, dim3(nseq), dim3(kAppendBlock), 0, st, tb, ab);
+hipError_t launch_keyframe_fused(const TailBatch& tb, const AppendBatch& ab, int nseq, hipStream_t st, bool small) {
+    if (small)
+        hipLaunchKernelGGL(keyframe_fused_kernel<kFeBlock>, dim3(nseq), dim3(kFeBlock), 0, st, tb, ab);
+    else
+        hipLaunchKernelGGL(keyframe_fused_kernel<kAppendBlock>, dim3(nseq), dim3(kAppendBlock), 0, st, tb, ab);
     return hipGetLastError();
 }
 

@@ -238,8 +238,8 @@ int device_numa_node(int d) {
     return v;
 }
 
-constexpr int kPhases = 10;
-enum Phase { PH_PYR, PH_LK, PH_POST, PH_STEREO, PH_PNP, PH_TAIL, PH_FAST, PH_BUCKET, PH_APPEND, PH_PYR_R };
+constexpr int kPhases = 11;
+enum Phase { PH_PYR, PH_LK, PH_POST, PH_STEREO, PH_PNP, PH_TAIL, PH_FAST, PH_BUCKET, PH_APPEND, PH_PYR_R, PH_LK_NEW };
 
 }  // namespace
 
@@ -273,6 +273,17 @@ struct svo_frontend {
     std::vector<int> lk_queued;  // [g] step whose temporal LK is already queued on slice g
     bool pipe = true;            // next step's LK of a slice queued right behind its keyframe (SVO_FE_PIPE)
     int spec_margin = 32;  // RANSAC drops covered by the speculative stereo LK (SVO_FE_SPEC_MARGIN, < 0: off)
+    // LK ahead (SVO_FE_AHEAD, one slice): LK(t+1) runs over step t's tracked
+    // points right behind its post-LK, beside the host's RANSAC, and a small LK
+    // over the keyframe's appended features follows the keyframe; the next post-LK
+    // keeps the inliers' and the appended features' tracks (PostLkBatch)
+    bool ahead = false;
+    int ahead_t = -1;            // step whose temporal LK ran ahead
+    float *ap_xy = nullptr, *ap_next = nullptr;  // appended features [s][CAP] and their tracks
+    uint8_t* ap_status = nullptr;
+    int* ap_iters = nullptr;
+    hipStream_t st_kf = nullptr;  // RANSAC scoring + keyframe + appended LK (highest priority)
+    hipEvent_t ev_aplk = nullptr;  // appended features' LK done
     unsigned long long* fbits;
     uint8_t* status;
     uint32_t* bits_all;
@@ -469,7 +480,7 @@ int fe_stereo_lk(svo_frontend* fe, int t, int a, int n, const int* counts, int m
 // sequence's take candidates: compaction, filter, triangulation and append run
 // as one kernel.
 int fe_keyframe(svo_frontend* fe, int t, int g0, int n, const int* n_in, const uint32_t* bits, const float* xy_in,
-                const int* mid_in, int max_take, hipStream_t st, bool spec = false) {
+                const int* mid_in, int max_take, hipStream_t st, bool spec = false, bool ap = false) {
     svo_ctx* ctx = fe->ctx;
     const svo_frontend_config& c = fe->cfg;
     const size_t CAP = fe->CAP, a = g0;
@@ -514,9 +525,10 @@ int fe_keyframe(svo_frontend* fe, int t, int g0, int n, const int* n_in, const u
     ab.added = fe->added + a;
     ab.h_n = fe->h_nA + a;
     ab.h_added = fe->h_added + a;
+    ab.ap_xy = ap ? fe->ap_xy + 2 * a * CAP : nullptr;  // LK ahead: the new features alone too
     if (spec) {
         ph_begin(fe, PH_TAIL, st, &slot);
-        SVO_HIP(ctx, launch_keyframe_fused(tb, ab, n, st));
+        SVO_HIP(ctx, launch_keyframe_fused(tb, ab, n, st, ap));
         ph_end(fe, st, slot);
         return SVO_OK;
     }
@@ -526,7 +538,7 @@ int fe_keyframe(svo_frontend* fe, int t, int g0, int n, const int* n_in, const u
     int rc = fe_stereo_lk(fe, t, (int)a, n, fe->st_n + a, max_take, st);
     if (rc) return rc;
     ph_begin(fe, PH_APPEND, st, &slot);
-    SVO_HIP(ctx, launch_append(ab, n, st));
+    SVO_HIP(ctx, launch_append(ab, n, st, ap));
     ph_end(fe, st, slot);
     return SVO_OK;
 }
@@ -616,7 +628,9 @@ int fe_queue_stats(svo_frontend* fe) {
     if (!fe->stats_pending) return SVO_OK;
     svo_ctx* ctx = fe->ctx;
     const int p = fe->stats_parity;
-    hipStream_t ss = fe->st_copy;
+    // (LK ahead: on the keyframe stream -- the next post-LK waits for the fits
+    // these feed, and the running LK would starve a lower-priority stream)
+    hipStream_t ss = fe->st_kf ? fe->st_kf : fe->st_copy;
     SVO_HIP(ctx, launch_suffstats(fe->obj_b[p], fe->xyB_b[p], fe->nB_b[p], fe->CAP, fe->h_best_b[p], fe->WORDS, fe->S,
                                   fe->cfg.K, fe->h_stats, ss));
     SVO_HIP(ctx, hipEventRecord(fe->ev_stats, ss));
@@ -745,6 +759,10 @@ int svo_frontend_create(svo_ctx* ctx, const svo_frontend_config* cfg, svo_fronte
         fe->hyps = carve<double>(p, 12 * (size_t)S * kRansacChunk);
         fe->box_binned = carve<float>(p, 2 * (size_t)S * CAP);
         fe->box_band = carve<int>(p, (size_t)S * fast_box_cells(c.width, c.height));
+        fe->ap_xy = carve<float>(p, 2 * (size_t)S * CAP);
+        fe->ap_next = carve<float>(p, 2 * (size_t)S * CAP);
+        fe->ap_status = carve<uint8_t>(p, (size_t)S * CAP);
+        fe->ap_iters = carve<int>(p, (size_t)S * CAP);
         fe->xyB_b[0] = fe->xyB;
         fe->obj_b[0] = fe->obj;
         fe->nB_b[0] = fe->nB;
@@ -935,8 +953,31 @@ int svo_frontend_create(svo_ctx* ctx, const svo_frontend_config* cfg, svo_fronte
         // SVO_FE_SLICE_PRIO=0: every slice at the same (highest) priority
         const char* spe = std::getenv("SVO_FE_SLICE_PRIO");
         const bool slice_prio = !(spe && spe[0] == '0');
+        const int normal_pr = std::min(std::max(greatest + 1, greatest), least);
+        // LK ahead (SVO_FE_AHEAD=1, one slice; off by default: measured 61.7k-71.3k
+        // frames/s against 72.1k-73.5k on the KITTI bench -- the step is already
+        // close to GPU-throughput bound (the kernels' solo times add up to more than
+        // the step), and the RANSAC / keyframe / statistics kernels queued beside a
+        // running LK wait for CUs whatever the stream priorities, which puts the
+        // statistics -> fits -> next post-LK chain behind LK instead of beside it).
+        // Its LK stream runs at SVO_FE_LK_PRIO (0 lowest (default), 1 normal, 2
+        // highest) under the keyframe stream (highest).
+        {
+            const char* e = std::getenv("SVO_FE_AHEAD");
+            fe->ahead = G == 1 && e && e[0] == '1';
+        }
+        int lk_pr = greatest;
+        if (fe->ahead) {
+            const char* e = std::getenv("SVO_FE_LK_PRIO");
+            lk_pr = (e && e[0] == '2') ? greatest : (e && e[0] == '1') ? normal_pr : least;
+            if (hipStreamCreateWithPriority(&fe->st_kf, hipStreamNonBlocking, greatest) != hipSuccess) {
+                svo_frontend_destroy(fe);
+                return set_error(ctx, SVO_ERR_HIP, "svo_frontend_create: stream");
+            }
+            (void)hipEventCreateWithFlags(&fe->ev_aplk, hipEventDisableTiming);
+        }
         for (int g = 0; g < G; g++) {
-            const int pr = (g == 0 || !slice_prio) ? greatest : std::min(std::max(greatest + 1, greatest), least);
+            const int pr = fe->ahead ? lk_pr : (g == 0 || !slice_prio) ? greatest : normal_pr;
             if (hipStreamCreateWithPriority(&fe->gst[g], hipStreamNonBlocking, pr) != hipSuccess) {
                 svo_frontend_destroy(fe);
                 return set_error(ctx, SVO_ERR_HIP, "svo_frontend_create: stream");
@@ -944,8 +985,9 @@ int svo_frontend_create(svo_ctx* ctx, const svo_frontend_config* cfg, svo_fronte
         }
         // FAST stream priority (SVO_FE_FAST_PRIO: 0 lowest (default: FAST fills the
         // CUs LK leaves idle and the post-LK window), 1 normal, 2 highest)
-        const int normal_pr = std::min(std::max(greatest + 1, greatest), least);
-        int fast_pr = least;
+        // (LK ahead: highest by default -- the speculative stereo LK on it is on
+        // the keyframe's critical path, LK is not)
+        int fast_pr = fe->ahead ? greatest : least;
         if (const char* e = std::getenv("SVO_FE_FAST_PRIO"))
             fast_pr = e[0] == '2' ? greatest : e[0] == '1' ? normal_pr : least;
         if (hipStreamCreateWithPriority(&fe->st_fast, hipStreamNonBlocking, fast_pr) != hipSuccess) {
@@ -962,9 +1004,9 @@ int svo_frontend_create(svo_ctx* ctx, const svo_frontend_config* cfg, svo_fronte
         for (auto& e : fe->ev_full_b) (void)hipEventCreateWithFlags(&e, hipEventDisableTiming);
         fe->ev_full = fe->ev_full_b[0];
         (void)hipEventCreateWithFlags(&fe->ev_pyr_r, hipEventDisableTiming);
-        // 4 hardware queues: with several slices the copy stream's work shares the
-        // pyramid stream
-        if (G > 1) {
+        // 4 hardware queues: with several slices (or the keyframe stream of LK
+        // ahead) the copy stream's work shares the pyramid stream
+        if (G > 1 || fe->ahead) {
             fe->st_copy = ctx->stream;
             fe->st_copy_owned = false;
         } else if (hipStreamCreateWithFlags(&fe->st_copy, hipStreamNonBlocking) != hipSuccess) {
@@ -1017,6 +1059,11 @@ void svo_frontend_destroy(svo_frontend* fe) {
     for (auto& e : fe->ev_full_b)
         if (e) (void)hipEventDestroy(e);
     if (fe->ev_pyr_r) (void)hipEventDestroy(fe->ev_pyr_r);
+    if (fe->st_kf) {
+        (void)hipStreamSynchronize(fe->st_kf);
+        (void)hipStreamDestroy(fe->st_kf);
+    }
+    if (fe->ev_aplk) (void)hipEventDestroy(fe->ev_aplk);
     if (fe->score_map) (void)hipFree(fe->score_map);
     delete fe;
 }
@@ -1025,13 +1072,15 @@ void svo_frontend_destroy(svo_frontend* fe) {
 // stream finish and forget it; the frame pyramids built ahead go too.
 static int fe_drain(svo_frontend* fe) {
     svo_ctx* ctx = fe->ctx;
-    if (fe->front_t < 0) return SVO_OK;
+    if (fe->front_t < 0 && fe->ahead_t < 0) return SVO_OK;
     for (auto& g : fe->gst) SVO_HIP(ctx, hipStreamSynchronize(g));
+    if (fe->st_kf) SVO_HIP(ctx, hipStreamSynchronize(fe->st_kf));
     if (fe->st_fast) SVO_HIP(ctx, hipStreamSynchronize(fe->st_fast));
     if (fe->st_copy) SVO_HIP(ctx, hipStreamSynchronize(fe->st_copy));
     SVO_HIP(ctx, hipStreamSynchronize(ctx->stream));
     fe->front_t = -1;
     fe->pyr_ready = -1;
+    fe->ahead_t = -1;  // the next step tracks the kept + appended list (xyA) again
     std::fill(fe->lk_queued.begin(), fe->lk_queued.end(), -1);
     return SVO_OK;
 }
@@ -1116,51 +1165,9 @@ int svo_frontend_init(svo_frontend* fe, int t0) {
     return SVO_OK;
 }
 
-// post_lk's arguments for the sequences [a, a + n) of this step's parity buffers
-static PostLkBatch fe_post_lk_batch(svo_frontend* fe, int a) {
-    const int CAP = fe->CAP;
-    const size_t sfl = (size_t)kSampleFloats * kRansacPrefetch;
-    return PostLkBatch{fe->nA + a, fe->status + (size_t)a * CAP, fe->next_xy + 2 * (size_t)a * CAP,
-                       fe->midA + (size_t)a * CAP, fe->iters + (size_t)a * CAP, fe->xyB + 2 * (size_t)a * CAP,
-                       fe->midB + (size_t)a * CAP, fe->nB + a, fe_pending(fe, a), fe->obj + 3 * (size_t)a * CAP,
-                       CAP, kRansacPrefetch, fe->h_nB + a, fe->h_itsum + a, fe->h_samp + sfl * a};
-}
-
-// Post-LK of step t on every slice, queued once the previous step's poses are
-// set (fe_finish_fits): its keyframe points go to the world frame first.
-static int fe_post(svo_frontend* fe, int t) {
-    svo_ctx* ctx = fe->ctx;
-    const int G = fe->G;
-    int slot;
-    for (int g = 0; g < G; g++) {
-        hipStream_t sg = fe->gst[g];
-        ph_begin(fe, PH_POST, sg, &slot);
-        SVO_HIP(ctx, launch_post_lk(fe_post_lk_batch(fe, fe->g0[g]), fe->gn[g], sg));
-        ph_end(fe, sg, slot);
-        SVO_HIP(ctx, hipEventRecord(fe->ev_sync[3 + 2 * g], sg));
-        // the keyframe's stereo matches, speculatively, beside this slice's RANSAC
-        if (fe->spec_margin >= 0) {
-            int rq = fe_queue_spec(fe, t, fe->g0[g], fe->gn[g],
-                                   std::min(fe->cfg.n_features + fe->spec_margin, fe->CAP), fe->ev_sync[3 + 2 * g]);
-            if (rq) return rq;
-        }
-    }
-    // every slice's points are gathered once the last slice's post-LK is done
-    SVO_HIP(ctx, hipEventRecord(fe->ev_gathered, fe->gst[G - 1]));
-    for (int g = 0; g + 1 < G; g++) SVO_HIP(ctx, hipStreamWaitEvent(fe->st_copy, fe->ev_sync[3 + 2 * g], 0));
-    // the full point set for the final fits / long RANSAC runs, on the copy stream
-    // (parity buffers: the previous step's fits still read theirs)
-    return fe_queue_full(fe);
-}
-
-// Temporal LK of step t (frame t-1 -> t, trackFrames R:src/tracking.cpp:154-179)
-// for slice g on its stream, behind the pyramid of frame t (ev_sync[0]).
-static int fe_lk_slice(svo_frontend* fe, int t, int g) {
-    svo_ctx* ctx = fe->ctx;
-    const int S = fe->S, CAP = fe->CAP;
+// trackFrames' calcOpticalFlowPyrLK parameters (R:src/tracking.cpp:154-179)
+static LKParams fe_temporal_params(const svo_frontend* fe) {
     const svo_frontend_config& c = fe->cfg;
-    const PyrDesc* dprev = fe->d_desc + (size_t)((t - 1) % fe->T) * S;
-    const PyrDesc* dcur = fe->d_desc + (size_t)(t % fe->T) * S;
     LKParams lp;
     lp.win_w = lp.win_h = c.win;
     lp.max_level = fe->ml;
@@ -1182,13 +1189,125 @@ static int fe_lk_slice(svo_frontend* fe, int t, int g) {
         }();
         lp.multi = multi;
     }
+    return lp;
+}
+
+static int fe_lk_slice(svo_frontend* fe, int t, int g, const float* xy_in, const int* n_in);
+
+// LK ahead: LK(t+1) of the features step t's keyframe appended (ap_xy, added[s]
+// of them, at most max_n), on the keyframe stream right behind it; ev_aplk
+// marks it done for post_lk(t+1)
+static int fe_lk_new(svo_frontend* fe, int t1, int max_n) {
+    svo_ctx* ctx = fe->ctx;
+    const int S = fe->S;
+    hipStream_t sk = fe->st_kf;
+    const PyrDesc* dprev = fe->d_desc + (size_t)((t1 - 1) % fe->T) * S;
+    const PyrDesc* dcur = fe->d_desc + (size_t)(t1 % fe->T) * S;
+    const LKParams lp = fe_temporal_params(fe);
+    LKBatch lb{dprev, dcur, fe->d_der + (size_t)((t1 - 1) % 3) * S, fe->ap_xy, fe->ap_next, fe->ap_status, nullptr,
+               fe->ap_iters, fe->added, 0, fe->CAP};
+    SVO_HIP(ctx, hipStreamWaitEvent(sk, fe->ev_sync[0], 0));  // frame t1's pyramid
+    int slot;
+    ph_begin(fe, PH_LK_NEW, sk, &slot);
+    SVO_HIP(ctx, launch_lk(lb, S, std::min(std::max(max_n, 0), fe->CAP), lp, sk));
+    ph_end(fe, sk, slot);
+    SVO_HIP(ctx, hipEventRecord(fe->ev_aplk, sk));
+    return SVO_OK;
+}
+
+// post_lk's arguments for the sequences [a, a + n) of this step's parity buffers
+static PostLkBatch fe_post_lk_batch(svo_frontend* fe, int a) {
+    const int CAP = fe->CAP;
+    const size_t sfl = (size_t)kSampleFloats * kRansacPrefetch;
+    return PostLkBatch{fe->nA + a, fe->status + (size_t)a * CAP, fe->next_xy + 2 * (size_t)a * CAP,
+                       fe->midA + (size_t)a * CAP, fe->iters + (size_t)a * CAP, fe->xyB + 2 * (size_t)a * CAP,
+                       fe->midB + (size_t)a * CAP, fe->nB + a, fe_pending(fe, a), fe->obj + 3 * (size_t)a * CAP,
+                       CAP, kRansacPrefetch, fe->h_nB + a, fe->h_itsum + a, fe->h_samp + sfl * a};
+}
+
+// post_lk of step t whose LK ran ahead (fe_lk_ahead at step t-1): the first
+// input is step t-1's tracked list (its parity of xyB / nB, tracks in next_xy,
+// ids in midB, compacted in place) filtered by its inlier bits, the second the
+// keyframe's appended features (ap_*)
+static PostLkBatch fe_post_lk_ahead_batch(svo_frontend* fe, int t) {
+    const int p = (t - 1) & 1;
+    PostLkBatch b = fe_post_lk_batch(fe, 0);
+    b.n_in = fe->nB_b[p];
+    b.mid_in = fe->midB;
+    b.keep_bits = fe->h_best_b[p];
+    b.words_cap = fe->WORDS;
+    b.n2 = fe->added;
+    b.xy2 = fe->ap_next;
+    b.status2 = fe->ap_status;
+    b.iters2 = fe->ap_iters;
+    return b;
+}
+
+// Post-LK of step t on every slice, queued once the previous step's poses are
+// set (fe_finish_fits): its keyframe points go to the world frame first.
+static int fe_post(svo_frontend* fe, int t) {
+    static const bool trace_on = [] {
+        const char* e = std::getenv("SVO_FE_TRACE");
+        return e && e[0] == '1';
+    }();
+    const auto t0 = std::chrono::steady_clock::now();
+    auto TP = [&](const char* label) {
+        if (trace_on)
+            std::fprintf(stderr, "[fe post t=%d] %8.1f us  %s\n", t,
+                         std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count(), label);
+    };
+    svo_ctx* ctx = fe->ctx;
+    const int G = fe->G;
+    int slot;
+    const bool ahead = fe->ahead_t == t;  // (one slice)
+    for (int g = 0; g < G; g++) {
+        hipStream_t sg = fe->gst[g];
+        if (ahead) SVO_HIP(ctx, hipStreamWaitEvent(sg, fe->ev_aplk, 0));
+        ph_begin(fe, PH_POST, sg, &slot);
+        SVO_HIP(ctx, launch_post_lk(ahead ? fe_post_lk_ahead_batch(fe, t) : fe_post_lk_batch(fe, fe->g0[g]), fe->gn[g],
+                                    sg));
+        ph_end(fe, sg, slot);
+        SVO_HIP(ctx, hipEventRecord(fe->ev_sync[3 + 2 * g], sg));
+        TP("post_lk launched");
+        // the keyframe's stereo matches, speculatively, beside this slice's RANSAC
+        if (fe->spec_margin >= 0) {
+            int rq = fe_queue_spec(fe, t, fe->g0[g], fe->gn[g],
+                                   std::min(fe->cfg.n_features + fe->spec_margin, fe->CAP), fe->ev_sync[3 + 2 * g]);
+            if (rq) return rq;
+        }
+        TP("spec stereo launched");
+    }
+    // every slice's points are gathered once the last slice's post-LK is done
+    SVO_HIP(ctx, hipEventRecord(fe->ev_gathered, fe->gst[G - 1]));
+    // LK ahead: LK(t+1) over these tracked points, right behind the post-LK (frame
+    // t+1's pyramid went out with this step's front half)
+    if (fe->ahead && t + 1 < fe->T && fe->pyr_ready == t + 1) {
+        int rl = fe_lk_slice(fe, t + 1, 0, fe->xyB, fe->nB);
+        if (rl) return rl;
+        fe->ahead_t = t + 1;
+        TP("lk ahead launched");
+    }
+    for (int g = 0; g + 1 < G; g++) SVO_HIP(ctx, hipStreamWaitEvent(fe->st_copy, fe->ev_sync[3 + 2 * g], 0));
+    // the full point set for the final fits / long RANSAC runs, on the copy stream
+    // (parity buffers: the previous step's fits still read theirs)
+    return fe_queue_full(fe);
+}
+
+// Temporal LK of step t (frame t-1 -> t, trackFrames R:src/tracking.cpp:154-179)
+// for slice g on its stream, behind the pyramid of frame t (ev_sync[0]).
+static int fe_lk_slice(svo_frontend* fe, int t, int g, const float* xy_in, const int* n_in) {
+    svo_ctx* ctx = fe->ctx;
+    const int S = fe->S, CAP = fe->CAP;
+    const PyrDesc* dprev = fe->d_desc + (size_t)((t - 1) % fe->T) * S;
+    const PyrDesc* dcur = fe->d_desc + (size_t)(t % fe->T) * S;
+    const LKParams lp = fe_temporal_params(fe);
     const int a = fe->g0[g], n = fe->gn[g];
     hipStream_t sg = fe->gst[g];
     const int mp = CAP;  // grid bound: the host counts of the previous tail may not be back yet
     SVO_HIP(ctx, hipStreamWaitEvent(sg, fe->ev_sync[0], 0));
-    LKBatch lb{dprev + a, dcur + a, fe->d_der + (size_t)((t - 1) % 3) * S + a, fe->xyA + 2 * (size_t)a * CAP,
+    LKBatch lb{dprev + a, dcur + a, fe->d_der + (size_t)((t - 1) % 3) * S + a, xy_in + 2 * (size_t)a * CAP,
                fe->next_xy + 2 * (size_t)a * CAP, fe->status + (size_t)a * CAP, nullptr,
-               fe->iters + (size_t)a * CAP, fe->nA + a, 0, CAP};
+               fe->iters + (size_t)a * CAP, n_in + a, 0, CAP};
     int slot;
     ph_begin(fe, PH_LK, sg, &slot);
     SVO_HIP(ctx, launch_lk(lb, n, mp, lp, sg));
@@ -1245,7 +1364,7 @@ static int fe_front_lk(svo_frontend* fe, int t) {
     //    already queued it behind the slice's previous keyframe (fe_lk_slice)
     for (int g = 0; g < G; g++) {
         if (fe->lk_queued[g] == t) continue;
-        int rl = fe_lk_slice(fe, t, g);
+        int rl = fe_lk_slice(fe, t, g, fe->xyA, fe->nA);
         if (rl) return rl;
     }
     // 3b. mask around frame t-1's features (the reference masks with prevFrame's
@@ -1377,8 +1496,11 @@ int svo_frontend_step(svo_frontend* fe, int t, svo_frontend_stats* stats) {
     //    scored on the GPU), drop outliers (R:src/tracking.cpp:218-229), keyframe
     for (int g = 0; g < G; g++) {
         const int a = fe->g0[g], n = fe->gn[g];
-        hipStream_t sg = fe->gst[g];
-        hipStream_t sq = sg;  // the slice stream is idle while the host solves RANSAC
+        // the slice stream is idle while the host solves RANSAC -- unless LK(t+1)
+        // runs ahead on it: then scoring and keyframe go on the keyframe stream
+        const bool ahead_next = fe->ahead_t == t + 1;
+        hipStream_t sg = ahead_next ? fe->st_kf : fe->gst[g];
+        hipStream_t sq = sg;
         TP("ransac begin");
         auto tw = clk::now();
         SVO_HIP(ctx, hipEventSynchronize(fe->ev_sync[3 + 2 * g]));
@@ -1534,15 +1656,20 @@ int svo_frontend_step(svo_frontend* fe, int t, svo_frontend_stats* stats) {
         // drop the outliers (the kernel reads the inlier bits from host-coherent
         // memory), then the keyframe: candidates, stereo LK, triangulation, append
         rc = fe_keyframe(fe, t, a, n, fe->nB + a, fe->h_best + (size_t)a * fe->WORDS, fe->xyB + 2 * (size_t)a * CAP,
-                         fe->midB + (size_t)a * CAP, max_take, sg, spec_ok);
+                         fe->midB + (size_t)a * CAP, max_take, sg, spec_ok, ahead_next);
         if (rc) return rc;
         SVO_HIP(ctx, hipEventRecord(fe->ev_tail[g], sg));
+        // LK ahead: the appended features' LK(t+1), which post_lk(t+1) waits for
+        if (ahead_next) {
+            int rl = fe_lk_new(fe, t + 1, max_take);
+            if (rl) return rl;
+        }
         TP("tail queued");
         // pipelined schedule: this slice's next LK goes out right behind its
         // keyframe (frame t+1's pyramid was queued with this step's front), so
         // the GPU tracks it while the host runs the next slices' RANSAC
         if (fe->pipe && G > 1 && t + 1 < fe->T && fe->pyr_ready == t + 1) {
-            int rl = fe_lk_slice(fe, t + 1, g);
+            int rl = fe_lk_slice(fe, t + 1, g, fe->xyA, fe->nA);
             if (rl) return rl;
         }
     }
@@ -1611,6 +1738,7 @@ int svo_frontend_synchronize(svo_frontend* fe) {
     int rq = fe_queue_stats(fe);
     if (rq) return rq;
     for (auto& g : fe->gst) SVO_HIP(ctx, hipStreamSynchronize(g));
+    if (fe->st_kf) SVO_HIP(ctx, hipStreamSynchronize(fe->st_kf));
     if (fe->st_fast) SVO_HIP(ctx, hipStreamSynchronize(fe->st_fast));
     SVO_HIP(ctx, hipStreamSynchronize(ctx->stream));
     fe_finish_fits(fe);

@@ -43,6 +43,18 @@ struct PostLkBatch {
     int* h_n;
     long long* h_iters;
     float* h_samp;  // [s][nh][25]
+    // LK ahead (nullable keep_bits: the plain form above). The temporal LK ran over
+    // the previous step's tracked points before its RANSAC (n_in / status / xy_in
+    // / mid_in / iters: that list) and, separately, over its n2[s] appended
+    // features (status2 / xy2 / iters2; map ids pend0[s] + j): the tracked set is
+    // (keep_bits && status) ++ status2, in that order, as LK over the kept +
+    // appended list would give
+    const uint32_t* keep_bits = nullptr;  // [s][words_cap], host-coherent
+    int words_cap = 0;
+    const int* n2 = nullptr;
+    const float* xy2 = nullptr;
+    const uint8_t* status2 = nullptr;
+    const int* iters2 = nullptr;
 };
 hipError_t launch_post_lk(const PostLkBatch& b, int nseq, hipStream_t st);
 // PendingMap alone (before the map is read by anything but post_lk)
@@ -99,8 +111,9 @@ struct AppendBatch {
     int* added;   // nullable
     int* h_n;     // nullable, host-coherent
     int* h_added; // nullable, host-coherent
+    float* ap_xy = nullptr;  // nullable: the appended features alone, [s][cap] (LK ahead's second input)
 };
-hipError_t launch_append(const AppendBatch& b, int nseq, hipStream_t st);
+hipError_t launch_append(const AppendBatch& b, int nseq, hipStream_t st, bool small = false);
 
 // Speculative stereo input, one block per sequence, queued as soon as the step's
 // tracked count n_tracked (post-LK) and the FAST candidates are known, i.e. before
@@ -125,6 +138,9 @@ hipError_t launch_stereo_prep(const StereoPrepBatch& b, int nseq, hipStream_t st
 // tail_kernel + append_kernel in one launch, for a step whose speculative stereo
 // LK covered every sequence's take (st_next / st_status already hold the matches
 // of st_xy[0, take)); same results as the two kernels with the LK between them.
-hipError_t launch_keyframe_fused(const TailBatch& tb, const AppendBatch& ab, int nseq, hipStream_t st);
+// small: 256-thread blocks (they find room beside a running LK; the default
+// 1024 keeps one SVD of latency for a few hundred candidates on an idle GPU)
+hipError_t launch_keyframe_fused(const TailBatch& tb, const AppendBatch& ab, int nseq, hipStream_t st,
+                                 bool small = false);
 
 }  // namespace svo

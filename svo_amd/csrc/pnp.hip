@@ -74,8 +74,10 @@ __global__ __launch_bounds__(256) void pnp_residual_kernel(PnpBatch B, double fx
 // inlier test, bits written word by word as pnp_residual_kernel does, and the
 // inlier count reduced inside the block and written ONCE per hypothesis (B.cnt,
 // which may live in host-coherent memory: the host reads m counts per sequence
-// instead of summing per-wave counts out of uncached memory)
-constexpr int kScoreBlock = 1024;
+// instead of summing per-wave counts out of uncached memory). 256 threads: the
+// blocks must find room on CUs a running LK occupies (a 1024-thread block
+// waits for a whole CU to drain: measured 290 us against ~25 us)
+constexpr int kScoreBlock = 256;
 __global__ __launch_bounds__(kScoreBlock) void pnp_score_kernel(PnpBatch B, double fx, double fy, double cx, double cy,
                                                                 float thresh2) {
     const int seq = blockIdx.y, h = blockIdx.x;

@@ -36,13 +36,18 @@ def _compare_step(fe, ref, st, rs, t, seq=0, check_map=True):
         np.testing.assert_allclose(fe.map_points(seq), ref.X, rtol=2e-5, atol=1e-6)
 
 
+@pytest.mark.parametrize("ahead", ["1", "0"])
 @pytest.mark.parametrize("spec", ["-1", "0", "32"])
 @pytest.mark.parametrize("bucket", [(0, 0), (50, 4)])
-def test_frontend_matches_oracle_loop(bucket, spec, monkeypatch):
+def test_frontend_matches_oracle_loop(bucket, spec, ahead, monkeypatch):
     """spec: SVO_FE_SPEC_MARGIN -- the keyframe's stereo LK run speculatively beside
     the RANSAC (32: the default; 0: the fused keyframe only when RANSAC dropped
-    nothing, else the serial tail + stereo LK + append; -1: always serial)."""
+    nothing, else the serial tail + stereo LK + append; -1: always serial).
+    ahead: SVO_FE_AHEAD -- LK(t+1) over step t's tracked points before its RANSAC,
+    plus a small LK of the appended features, merged by the next post-LK (1), or
+    LK over the kept + appended list after the keyframe (0, the default)."""
     monkeypatch.setenv("SVO_FE_SPEC_MARGIN", spec)
+    monkeypatch.setenv("SVO_FE_AHEAD", ahead)
     ctx = S.Context(0)
     W, H, N, T = 640, 376, 800, 8
     sc = Scene(W, H, seed=3)

@@ -57,7 +57,7 @@ run_trace() {
     SVO_FE_TRACE=1 timeout -k 10 300 rocprofv3 --kernel-trace --memory-copy-trace -d $T -o run --output-format csv -- \
         python bench.py --steps ${1:-12} --warmup 3 --seq 64 --no-cpu-baseline --no-single > $T.log 2>&1 || fail trace $T.log
     python tools/timeline.py $T > $O/timeline.txt
-    grep "fe t=" $T.log | tail -16 > $O/hosttrace.txt
+    grep "fe t=\|fe post t=" $T.log | tail -24 > $O/hosttrace.txt
     cat $O/timeline.txt $O/hosttrace.txt
 }
 
