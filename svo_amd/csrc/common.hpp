@@ -204,14 +204,6 @@ struct LKBatch {
     int* iters;   // nullable
     const int* counts;  // nullable
     int n, cap;
-    // nullable (lk_multi_kernel only): streamed hand-off -- each feature's result
-    // also goes to rec[4 * (s * cap + i)] as ONE 16-byte write-through (sc1) store
-    // of two tagged 8-byte granules {x, stamp << 24 | status << 23 | iters},
-    // {y, stamp}, so a consumer polling with sc1 loads takes a sequence once every
-    // record shows the step's stamp -- no fence, flag or counter per block (a flag
-    // store behind a vmcnt drain cost the kernel ~20 %, an atomic add ~27 %)
-    unsigned* rec = nullptr;
-    int stamp = 0;  // 1 .. 255
 };
 hipError_t launch_lk(const LKBatch& b, int nseq, int max_n, const LKParams& p, hipStream_t st);
 bool lk_supported(int win_w, int win_h);

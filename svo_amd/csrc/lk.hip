@@ -1417,9 +1417,7 @@ __device__ __forceinline__ void group_sum_f(int (&v)[NV], float (&f)[NV]) {
     for (int i = 0; i < NV; i++) f[i] = halves_lane_float(h[i], lo[i]);
 }
 
-// STREAM: the streamed hand-off epilogue (LKBatch::rec); a separate instance, so
-// the default kernel's code is untouched by it
-template <int FPW, int QJM, int MINW, int KKS = 2, bool STREAM = false>
+template <int FPW, int QJM, int MINW, int KKS = 2>
 __global__ __launch_bounds__(64, MINW) void lk_multi_kernel(LKBatch B, LKDev p) {
     constexpr int WW = 21, WH = 21;
     using Q = MultiShape<QJM>;
@@ -1685,19 +1683,6 @@ __global__ __launch_bounds__(64, MINW) void lk_multi_kernel(LKBatch B, LKDev p) 
         }
         wave_lds_sync();
     }
-    if constexpr (STREAM) {
-        // streamed hand-off: one 16-B sc1 store of two tagged granules per feature
-        if (l == 0 && live) {
-            typedef unsigned u32x4v __attribute__((ext_vector_type(4)));
-            const u32x4v v = {__float_as_uint(nx), ((unsigned)B.stamp << 24) | ((unsigned)st << 23) | (unsigned)itcount,
-                              __float_as_uint(ny), (unsigned)B.stamp};
-            unsigned* dst = B.rec + 4 * (base + pt);
-            asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(dst), "v"(v) : "memory");
-            B.status[base + pt] = (uint8_t)st;
-            if (B.err) B.err[base + pt] = errv;
-        }
-        return;
-    }
     if (l == 0 && live) {
         next_xy[2 * pt] = nx;
         next_xy[2 * pt + 1] = ny;
@@ -1711,10 +1696,7 @@ template <int FPW, int QJM, int MINW = 4, int KKS = 2>
 hipError_t launch_multi(const LKBatch& b, int nseq, int max_n, const LKDev& d, hipStream_t st) {
     dim3 grid((max_n + FPW - 1) / FPW, nseq);
     constexpr int lds_bytes = FPW * MultiShape<QJM>::JBYTES + 16;
-    if (b.rec)
-        hipLaunchKernelGGL((lk_multi_kernel<FPW, QJM, MINW, KKS, true>), grid, dim3(64), lds_bytes, st, b, d);
-    else
-        hipLaunchKernelGGL((lk_multi_kernel<FPW, QJM, MINW, KKS>), grid, dim3(64), lds_bytes, st, b, d);
+    hipLaunchKernelGGL((lk_multi_kernel<FPW, QJM, MINW, KKS>), grid, dim3(64), lds_bytes, st, b, d);
     return hipGetLastError();
 }
 
