@@ -177,6 +177,15 @@ int svo_solve_pnp_ransac(svo_ctx* ctx, const double* obj_xyz, const float* img_x
                          double confidence, double rvec[3], double tvec[3], int* inliers,
                          int* n_inliers);
 
+/* RANSAC's minimal solver alone: SOLVEPNP_EPNP on 5 points, the model estimator
+ * solvePnPRansac runs per hypothesis (R:src/tracking.cpp:191-196), for m subsets
+ * given as 25 floats each (obj xyz x5, then img xy x5, as the front end gathers
+ * them). device = 1: one 64-lane wave per subset on the GPU (epnp_wave.hpp);
+ * device = 0: the host solver the RANSAC uses. Outputs are bit-identical.
+ * Rt: m x 12 doubles (R row-major, t); ok: m ints (0: non-finite model). */
+int svo_epnp_subsets(svo_ctx* ctx, const float* subsets, int m, const double K[9], int device, double* Rt,
+                     int* ok);
+
 /* ------------------------------------------------------------ triangulation
  * cv::triangulatePoints(P1, P2, pts1, pts2, points4D) then
  * cv::convertPointsFromHomogeneous (R:src/tracking.cpp:125-131). P1, P2: 3x4

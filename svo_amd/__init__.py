@@ -89,6 +89,7 @@ _SIGS = [
                                     _f32p, _u8p, _i32p]),
     ("svo_solve_pnp_ransac", C.c_int, [_vp, _f64p, _f32p, C.c_int, _f64p, C.c_int, C.c_float,
                                        C.c_double, _f64p, _f64p, _i32p, _i32p]),
+    ("svo_epnp_subsets", C.c_int, [_vp, _f32p, C.c_int, _f64p, C.c_int, _f64p, _i32p]),
     ("svo_triangulate_points", C.c_int, [_vp, _f32p, _f32p, _f32p, _f32p, C.c_int, _f32p, _f32p]),
     ("svo_reprojection_jacobians", C.c_int, [_vp, _f64p, _f32p, _i32p, C.c_int, C.c_int, _f64p, _f64p,
                                              C.c_double, _f64p, _f64p, _f64p]),
@@ -384,6 +385,18 @@ class Context:
                                             _p(err, _f32p) if err is not None else None,
                                             _p(mask, _u8p), _p(counts, _i32p)))
         return err, mask, counts
+
+    def epnp_subsets(self, subsets, K, device: bool = True):
+        """RANSAC's EPnP on (m, 25) float subsets (obj xyz x5, img xy x5) -> (Rt (m, 12), ok (m,)):
+        one wave per subset on the GPU (device) or the host solver; bit-identical."""
+        subsets = _c(subsets, np.float32).reshape(-1, 25)
+        K = _c(K, np.float64).reshape(9)
+        m = len(subsets)
+        Rt = np.zeros((m, 12), np.float64)
+        ok = np.zeros(m, np.int32)
+        self._check(lib().svo_epnp_subsets(self.handle, _p(subsets, _f32p), m, _p(K, _f64p), int(device),
+                                           _p(Rt, _f64p), _p(ok, _i32p)))
+        return Rt, ok
 
     def triangulate_points(self, P1, P2, pts1, pts2):
         """cv::triangulatePoints + convertPointsFromHomogeneous -> (xyzw (n,4), xyz (n,3)) float32."""

@@ -7,6 +7,7 @@
 #include <vector>
 
 #include "common.hpp"
+#include "epnp.hpp"
 
 namespace svo {
 
@@ -516,6 +517,37 @@ int svo_pnp_residuals(svo_ctx* ctx, const float* obj_xyz, const float* img_xy, i
     if (mask)
         for (int h = 0; h < m; h++)
             for (int i = 0; i < n; i++) mask[(size_t)h * n + i] = (bits[(size_t)h * words + (i >> 5)] >> (i & 31)) & 1;
+    return SVO_OK;
+}
+
+int svo_epnp_subsets(svo_ctx* ctx, const float* subsets, int m, const double K[9], int device, double* Rt,
+                     int* ok) {
+    if (!ctx || m < 0 || (m > 0 && (!subsets || !Rt || !ok)) || !K)
+        return set_error(ctx, SVO_ERR_ARG, "svo_epnp_subsets: bad arguments");
+    if (m == 0) return SVO_OK;
+    if (!device) {
+        for (int j = 0; j < m; j++) {
+            const float* sp = subsets + 25 * (size_t)j;
+            double R[9], t[3];
+            ok[j] = epnp_pixels(sp, sp + 15, nullptr, 5, K, R, t) ? 1 : 0;
+            std::memcpy(Rt + 12 * (size_t)j, R, sizeof(R));
+            std::memcpy(Rt + 12 * (size_t)j + 9, t, sizeof(t));
+        }
+        return SVO_OK;
+    }
+    const size_t bytes = sizeof(double) * (9 + 12 * (size_t)m) + sizeof(float) * 25 * (size_t)m + sizeof(int) * m + 1024;
+    char* d = (char*)scratch(ctx, 9, bytes);
+    if (!d) return set_error(ctx, SVO_ERR_HIP, "scratch alloc");
+    double* dK = (double*)d;
+    double* dRt = dK + 9;
+    float* dsub = (float*)(dRt + 12 * (size_t)m);
+    int* dok = (int*)(dsub + 25 * (size_t)m);
+    SVO_HIP(ctx, hipMemcpyAsync(dK, K, sizeof(double) * 9, hipMemcpyHostToDevice, ctx->stream));
+    SVO_HIP(ctx, hipMemcpyAsync(dsub, subsets, sizeof(float) * 25 * (size_t)m, hipMemcpyHostToDevice, ctx->stream));
+    SVO_HIP(ctx, launch_epnp_wave(dsub, m, dK, dRt, dok, ctx->stream));
+    SVO_HIP(ctx, hipMemcpyAsync(Rt, dRt, sizeof(double) * 12 * (size_t)m, hipMemcpyDeviceToHost, ctx->stream));
+    SVO_HIP(ctx, hipMemcpyAsync(ok, dok, sizeof(int) * (size_t)m, hipMemcpyDeviceToHost, ctx->stream));
+    SVO_HIP(ctx, hipStreamSynchronize(ctx->stream));
     return SVO_OK;
 }
 

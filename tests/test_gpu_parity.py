@@ -393,6 +393,27 @@ def test_pnp_ransac_near_threshold(ctx):
     assert flips == 0
 
 
+def test_epnp_wave_matches_host(ctx):
+    """RANSAC's EPnP minimal solver run one 64-lane wave per subset on the GPU
+    (epnp_wave.hpp) vs the host solver the front end uses: bit-identical R / t on
+    5-point subsets of the RANSAC test problems (clean, with outliers, and the
+    near-threshold set)."""
+    rng = np.random.default_rng(5)
+    subs = []
+    for seed in range(3):
+        sc, X, uv, _ = _pnp_problem(seed=seed)
+        for _ in range(200):
+            idx = rng.choice(len(X), 5, replace=False)
+            subs.append(np.r_[X[idx].astype(np.float32).ravel(), uv[idx].astype(np.float32).ravel()])
+    subs = np.array(subs, np.float32)
+    K = Scene(1241, 376, seed=0).K
+    Rd, okd = ctx.epnp_subsets(subs, K, device=True)
+    Rh, okh = ctx.epnp_subsets(subs, K, device=False)
+    assert okh.sum() == len(subs)
+    assert np.array_equal(okd, okh)
+    assert np.array_equal(Rd.view(np.uint64), Rh.view(np.uint64))
+
+
 def test_pnp_ransac_too_few_points(ctx):
     with pytest.raises(S.SvoError):
         ctx.solve_pnp_ransac(np.zeros((3, 3)), np.zeros((3, 2), np.float32), np.eye(3))
