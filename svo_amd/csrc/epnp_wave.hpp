@@ -19,6 +19,11 @@
 
 #include "linalg.hpp"
 
+// phase time stamps for tools/epnp_wave_probe.hip (no-op in the library)
+#ifndef WEP_STAMP
+#define WEP_STAMP(k)
+#endif
+
 namespace svo {
 namespace wep {
 
@@ -357,6 +362,7 @@ __device__ inline void eig12(Work& S, int lane) {
     double* d = S.d;
     double* e = S.e;
     // tred2
+    WEP_STAMP(1);
     if (lane < n) d[lane] = W[lane * n + n - 1];
     wsync();
     for (int i = n - 1; i > 0; i--) {
@@ -425,6 +431,7 @@ __device__ inline void eig12(Work& S, int lane) {
         if (lane == 0) d[i] = h;
         wsync();
     }
+    WEP_STAMP(2);
     for (int i = 0; i < n - 1; i++) {
         if (lane == 0) {
             W[i * n + n - 1] = W[i * n + i];
@@ -458,6 +465,7 @@ __device__ inline void eig12(Work& S, int lane) {
     }
     wsync();
     // tql2
+    WEP_STAMP(3);
     {
         const double v = lane >= 1 && lane < n ? e[lane] : 0.0;
         wsync();
@@ -540,6 +548,7 @@ __device__ inline void eig12(Work& S, int lane) {
         }
         wsync();
     }
+    WEP_STAMP(4);
     // insertion sort, descending (uniform; the index array in LDS)
     if (lane == 0) {
         int* order = S.ord;
@@ -650,6 +659,7 @@ __device__ inline bool solve5(Work& S, int lane, const float* obj, const float* 
     }
     wsync();
     eig12(S, lane);
+    WEP_STAMP(5);
     // make_L: lane e < 60 forms L[e] (row i = e / 10: control-point pair, col c)
     if (lane < 60) {
         const int i = lane / 10, c = lane - 10 * i;
@@ -693,6 +703,7 @@ __device__ inline bool solve5(Work& S, int lane, const float* obj, const float* 
             rho[i] = (a[0] - b[0]) * (a[0] - b[0]) + (a[1] - b[1]) * (a[1] - b[1]) + (a[2] - b[2]) * (a[2] - b[2]);
         }
     }
+    WEP_STAMP(6);
     // betas 1..3 + Gauss-Newton + R, t; best by mean reprojection error
     double Rs[3][9], ts[3][3], err[3];
 #pragma unroll
@@ -775,6 +786,7 @@ __device__ inline bool solve5(Work& S, int lane, const float* obj, const float* 
         }
         err[k] = sum / np;
     }
+    WEP_STAMP(7);
     int N = 0;
     if (err[1] < err[0]) N = 1;
     if (err[2] < (N == 0 ? err[0] : err[1])) N = 2;

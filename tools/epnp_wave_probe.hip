@@ -13,6 +13,13 @@
 #include <vector>
 
 #include "epnp.hpp"
+// phase stamps of hypothesis 0 (s_memtime, lane 0): 1 tred2, 2 back-transform,
+// 3 tql2, 4 sort, 5 make_L, 6 betas + Gauss-Newton + R,t (7 end)
+__device__ unsigned long long g_stamps[8];
+#define WEP_STAMP(k)                                                                 \
+    do {                                                                             \
+        if (blockIdx.x == 0 && threadIdx.x == 0) g_stamps[k] = __builtin_amdgcn_s_memtime(); \
+    } while (0)
 #include "epnp_wave.hpp"
 
 using namespace svo;
@@ -25,6 +32,7 @@ __global__ void __launch_bounds__(64) epnp_wave_kernel(const float* samp, int m,
     for (int i = 0; i < 9; i++) K[i] = Kd[i];
     const float* sp = samp + 25 * (size_t)j;
     double R[9], t[3];
+    WEP_STAMP(0);
     const bool v = wep::solve5(S, lane, sp, sp + 15, K, R, t);
     if (lane == 0) {
         ok[j] = v ? 1 : 0;
@@ -93,6 +101,15 @@ int main(int argc, char** argv) {
             best = std::fmin(best, ms);
         }
         printf("wave EPnP: %5d hypotheses, %8.1f us per launch (best of 5)\n", m, 1e3 * best);
+    }
+    {
+        unsigned long long st[8];
+        (void)hipMemcpyFromSymbol(st, HIP_SYMBOL(g_stamps), sizeof(st));
+        const char* nm[7] = {"prelude + M^T M", "tred2", "back-transform", "tql2", "sort", "make_L",
+                             "betas + Gauss-Newton + R,t"};
+        printf("phases of one hypothesis (s_memtime, shader clock cycles):");
+        for (int k = 0; k < 7; k++) printf(" %s %llu;", nm[k], st[k + 1] - st[k]);
+        printf("\n");
     }
     std::vector<double> gout(12 * (size_t)mbig);
     std::vector<int> gok(mbig);
