@@ -23,7 +23,7 @@ cd /tmp && export TMPDIR=/tmp
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 O=gpurun_out
 mkdir -p $O
-BQ="python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-single"
+BQ="python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-single --no-bucketed"
 
 fail() { echo "FAILED: $1"; [ -n "$2" ] && tail -30 "$2"; exit 1; }
 
@@ -55,7 +55,7 @@ run_fe() {
 run_trace() {
     local T=/tmp/svo_trace
     SVO_FE_TRACE=1 timeout -k 10 300 rocprofv3 --kernel-trace --memory-copy-trace -d $T -o run --output-format csv -- \
-        python bench.py --steps ${1:-12} --warmup 3 --seq 64 --no-cpu-baseline --no-single > $T.log 2>&1 || fail trace $T.log
+        python bench.py --steps ${1:-12} --warmup 3 --seq 64 --no-cpu-baseline --no-single --no-bucketed > $T.log 2>&1 || fail trace $T.log
     python tools/timeline.py $T > $O/timeline.txt
     grep "fe t=\|fe post t=" $T.log | tail -24 > $O/hosttrace.txt
     cat $O/timeline.txt $O/hosttrace.txt
@@ -63,7 +63,7 @@ run_trace() {
 
 run_prof() {
     local tag=$1; shift
-    local args="${*:---steps 50 --warmup 10 --no-cpu-baseline --no-single}"
+    local args="${*:---steps 50 --warmup 10 --no-cpu-baseline --no-single --no-bucketed}"
     rm -rf $O/prof_$tag
     timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/prof_$tag -o run --output-format csv -- \
         python bench.py $args > $O/prof_$tag.log 2>&1 || fail prof $O/prof_$tag.log
@@ -78,7 +78,7 @@ P
 
 run_pmc() {
     local tag=$1 cfg=$2 seq=${3:-64}
-    local B="python bench.py --config $cfg --seq $seq --steps 10 --warmup 3 --no-cpu-baseline --no-single"
+    local B="python bench.py --config $cfg --seq $seq --steps 10 --warmup 3 --no-cpu-baseline --no-single --no-bucketed"
     rm -rf $O/pmc_fetch_$cfg $O/pmc_write_$cfg
     timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE -d $O/pmc_fetch_$cfg -o run --output-format csv -- $B \
         > $O/pmc_fetch_$cfg.log 2>&1 || fail pmc-fetch $O/pmc_fetch_$cfg.log
@@ -93,7 +93,7 @@ run_pmc() {
 
 run_mix() {
     local tag=$1; shift
-    local B="python bench.py ${*:---steps 8 --warmup 2 --no-cpu-baseline --no-single}"
+    local B="python bench.py ${*:---steps 8 --warmup 2 --no-cpu-baseline --no-single --no-bucketed}"
     timeout -s KILL 200 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_WAIT_INST_ANY \
         SQ_ACTIVE_INST_ANY SQ_INSTS_VMEM -d /tmp/ps1 -o run --output-format csv -- $B > $O/mix.log 2>&1 || fail mix1 $O/mix.log
     timeout -s KILL 200 rocprofv3 --pmc SQ_ACTIVE_INST_VALU SQ_BUSY_CYCLES SQ_INSTS_BRANCH SQ_WAIT_INST_LDS \
