@@ -1787,6 +1787,8 @@ hipError_t launch_lk(const LKBatch& b, int nseq, int max_n, const LKParams& lp, 
                 case 40: return launch_multi<4, 0, 3>(b, nseq, max_n, d, st);
                 case 47: return launch_multi<4, 2, 3, 4>(b, nseq, max_n, d, st);
                 case 48: return launch_multi<4, 2, 3, 1>(b, nseq, max_n, d, st);
+                case 44: return launch_multi<4, 1, 4>(b, nseq, max_n, d, st);  // <= 128 VGPRs
+                case 45: return launch_multi<4, 1, 3, 1>(b, nseq, max_n, d, st);
                 default: return launch_multi<4, 1, 3>(b, nseq, max_n, d, st);
             }
         }
