@@ -273,6 +273,11 @@ struct svo_frontend {
     std::vector<int> lk_queued;  // [g] step whose temporal LK is already queued on slice g
     bool pipe = true;            // next step's LK of a slice queued right behind its keyframe (SVO_FE_PIPE)
     int spec_margin = 32;  // RANSAC drops covered by the speculative stereo LK (SVO_FE_SPEC_MARGIN, < 0: off)
+    // speculative stereo LK queued right behind FAST(t), beside LK(t), sized from
+    // the features before LK (SVO_FE_SPEC_EARLY, default on): the margin then
+    // covers LK and RANSAC losses together
+    bool spec_early = true;
+    int spec_t = -1;  // step whose speculative stereo LK went out with its front half
     // LK ahead (SVO_FE_AHEAD, one slice): LK(t+1) runs over step t's tracked
     // points right behind its post-LK, beside the host's RANSAC, and a small LK
     // over the keyframe's appended features follows the keyframe; the next post-LK
@@ -550,14 +555,14 @@ int fe_keyframe(svo_frontend* fe, int t, int g0, int n, const int* n_in, const u
 // bounds every sequence's spec (the grid; blocks past a sequence's count exit at
 // once). ev_sync[1] is re-recorded behind it, so the keyframe's wait for FAST
 // covers it too.
-int fe_queue_spec(svo_frontend* fe, int t, int a, int n, int max_spec, hipEvent_t ev_post) {
+int fe_queue_spec(svo_frontend* fe, int t, int a, int n, int max_spec, hipEvent_t ev_post, const int* n_before) {
     svo_ctx* ctx = fe->ctx;
     const svo_frontend_config& c = fe->cfg;
     const size_t CAP = fe->CAP;
     hipStream_t sf = fe->st_fast;
     const bool bucketed = c.bucket_size > 0;
     StereoPrepBatch pb;
-    pb.n_tracked = fe->nB + a;
+    pb.n_tracked = n_before + a;
     pb.cand = bucketed ? fe->cand + 2 * a * fe->BCAP : fe->kps + 3 * a * fe->KCAP;
     pb.cand_elem = bucketed ? 2 : 3;
     pb.cand_cap = bucketed ? fe->BCAP : fe->KCAP;
@@ -569,7 +574,7 @@ int fe_queue_spec(svo_frontend* fe, int t, int a, int n, int max_spec, hipEvent_
     pb.margin = fe->spec_margin;
     pb.st_xy = fe->st_xy + 2 * a * CAP;
     pb.spec_n = fe->spec_n + a;
-    SVO_HIP(ctx, hipStreamWaitEvent(sf, ev_post, 0));
+    if (ev_post) SVO_HIP(ctx, hipStreamWaitEvent(sf, ev_post, 0));
     SVO_HIP(ctx, launch_stereo_prep(pb, n, sf));
     int rc = fe_stereo_lk(fe, t, a, n, fe->spec_n + a, max_spec, sf);
     if (rc) return rc;
@@ -899,6 +904,8 @@ int svo_frontend_create(svo_ctx* ctx, const svo_frontend_config* cfg, svo_fronte
         fe->pipe = !(pp && pp[0] == '0');
         const char* sm = std::getenv("SVO_FE_SPEC_MARGIN");
         fe->spec_margin = sm ? std::atoi(sm) : 32;
+        const char* se = std::getenv("SVO_FE_SPEC_EARLY");
+        fe->spec_early = !(se && se[0] == '0');
     }
     // (on the context stream: a first use of the null stream would take a fifth
     // hardware queue and serialise the step's streams)
@@ -1081,6 +1088,7 @@ static int fe_drain(svo_frontend* fe) {
     fe->front_t = -1;
     fe->pyr_ready = -1;
     fe->ahead_t = -1;  // the next step tracks the kept + appended list (xyA) again
+    fe->spec_t = -1;
     std::fill(fe->lk_queued.begin(), fe->lk_queued.end(), -1);
     return SVO_OK;
 }
@@ -1270,9 +1278,10 @@ static int fe_post(svo_frontend* fe, int t) {
         SVO_HIP(ctx, hipEventRecord(fe->ev_sync[3 + 2 * g], sg));
         TP("post_lk launched");
         // the keyframe's stereo matches, speculatively, beside this slice's RANSAC
-        if (fe->spec_margin >= 0) {
+        if (fe->spec_margin >= 0 && fe->spec_t != t) {
             int rq = fe_queue_spec(fe, t, fe->g0[g], fe->gn[g],
-                                   std::min(fe->cfg.n_features + fe->spec_margin, fe->CAP), fe->ev_sync[3 + 2 * g]);
+                                   std::min(fe->cfg.n_features + fe->spec_margin, fe->CAP), fe->ev_sync[3 + 2 * g],
+                                   fe->nB);
             if (rq) return rq;
         }
         TP("spec stereo launched");
@@ -1388,6 +1397,17 @@ static int fe_front_lk(svo_frontend* fe, int t) {
     SVO_HIP(ctx, launch_pyramid_batched(fe->d_desc_r + (size_t)(t % fe->T) * S, S, fe->W, fe->H, fe->nlev, st0));
     ph_end(fe, st0, slot);
     SVO_HIP(ctx, hipEventRecord(fe->ev_pyr_r, st0));
+    // 3c. the keyframe's stereo matches, speculatively, right behind FAST (and frame
+    //     t's left / right pyramids: fe_stereo_lk waits for ev_pyr_r, queued behind
+    //     both): the keyframe takes the first n_features - kept candidates and kept
+    //     <= n_before (the features LK(t) tracks), so the first n_features -
+    //     n_before + margin cover the take whenever LK and RANSAC together lose at
+    //     most `margin` points; fe_queue_spec re-records ev_sync[1]
+    if (fe->fast_early && !fe->fast_first && fe->spec_margin >= 0 && fe->spec_early) {
+        int rc = fe_queue_spec(fe, t, 0, S, std::min(fe->cfg.n_features + fe->spec_margin, fe->CAP), nullptr, fe->nA);
+        if (rc) return rc;
+        fe->spec_t = t;
+    }
     if (fe->pyr_early) {
         const int tn = t + 1;
         const PyrDesc* dnext = fe->d_desc + (size_t)(tn % fe->T) * S;
@@ -1628,7 +1648,7 @@ int svo_frontend_step(svo_frontend* fe, int t, svo_frontend_stats* stats) {
             r.select(c.K, false);
             const int kept = r.ok ? r.maxGood : (r.n < 4 ? r.n : 0);
             max_take = std::max(max_take, c.n_features - kept);
-            spec_ok &= fe->h_nB[s] - kept <= fe->spec_margin;
+            spec_ok &= (fe->spec_t == t ? fe->h_nA[s] : fe->h_nB[s]) - kept <= fe->spec_margin;
             uint32_t* b = fe->h_best + (size_t)s * fe->WORDS;
             std::memset(b, 0, sizeof(uint32_t) * fe->WORDS);
             if (r.ok) {
