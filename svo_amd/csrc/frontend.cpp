@@ -274,10 +274,13 @@ struct svo_frontend {
     bool pipe = true;            // next step's LK of a slice queued right behind its keyframe (SVO_FE_PIPE)
     int spec_margin = 32;  // RANSAC drops covered by the speculative stereo LK (SVO_FE_SPEC_MARGIN, < 0: off)
     // speculative stereo LK queued right behind FAST(t), beside LK(t), sized from
-    // the features before LK (SVO_FE_SPEC_EARLY, default on): the margin then
+    // the features before LK (SVO_FE_SPEC_EARLY=1; off by default: measured 0.2-1.5 %
+    // slower than queueing it behind post-LK at all three configs): the margin then
     // covers LK and RANSAC losses together
-    bool spec_early = true;
+    bool spec_early = false;
     int spec_t = -1;  // step whose speculative stereo LK went out with its front half
+    int spec_margin_t = 32;  // the margin that speculation used (spec_margin + the last LK losses)
+    int lk_loss_max = 0;     // max over sequences of the last step's LK losses (n_before - n_tracked)
     // LK ahead (SVO_FE_AHEAD, one slice): LK(t+1) runs over step t's tracked
     // points right behind its post-LK, beside the host's RANSAC, and a small LK
     // over the keyframe's appended features follows the keyframe; the next post-LK
@@ -555,7 +558,8 @@ int fe_keyframe(svo_frontend* fe, int t, int g0, int n, const int* n_in, const u
 // bounds every sequence's spec (the grid; blocks past a sequence's count exit at
 // once). ev_sync[1] is re-recorded behind it, so the keyframe's wait for FAST
 // covers it too.
-int fe_queue_spec(svo_frontend* fe, int t, int a, int n, int max_spec, hipEvent_t ev_post, const int* n_before) {
+int fe_queue_spec(svo_frontend* fe, int t, int a, int n, int max_spec, hipEvent_t ev_post, const int* n_before,
+                  int margin) {
     svo_ctx* ctx = fe->ctx;
     const svo_frontend_config& c = fe->cfg;
     const size_t CAP = fe->CAP;
@@ -571,7 +575,7 @@ int fe_queue_spec(svo_frontend* fe, int t, int a, int n, int max_spec, hipEvent_
     pb.map_cap = fe->MAPCAP;
     pb.cap = fe->CAP;
     pb.n_target = c.n_features;
-    pb.margin = fe->spec_margin;
+    pb.margin = margin;
     pb.st_xy = fe->st_xy + 2 * a * CAP;
     pb.spec_n = fe->spec_n + a;
     if (ev_post) SVO_HIP(ctx, hipStreamWaitEvent(sf, ev_post, 0));
@@ -905,7 +909,7 @@ int svo_frontend_create(svo_ctx* ctx, const svo_frontend_config* cfg, svo_fronte
         const char* sm = std::getenv("SVO_FE_SPEC_MARGIN");
         fe->spec_margin = sm ? std::atoi(sm) : 32;
         const char* se = std::getenv("SVO_FE_SPEC_EARLY");
-        fe->spec_early = !(se && se[0] == '0');
+        fe->spec_early = se && se[0] == '1';
     }
     // (on the context stream: a first use of the null stream would take a fifth
     // hardware queue and serialise the step's streams)
@@ -1281,7 +1285,7 @@ static int fe_post(svo_frontend* fe, int t) {
         if (fe->spec_margin >= 0 && fe->spec_t != t) {
             int rq = fe_queue_spec(fe, t, fe->g0[g], fe->gn[g],
                                    std::min(fe->cfg.n_features + fe->spec_margin, fe->CAP), fe->ev_sync[3 + 2 * g],
-                                   fe->nB);
+                                   fe->nB, fe->spec_margin);
             if (rq) return rq;
         }
         TP("spec stereo launched");
@@ -1403,10 +1407,13 @@ static int fe_front_lk(svo_frontend* fe, int t) {
     //     <= n_before (the features LK(t) tracks), so the first n_features -
     //     n_before + margin cover the take whenever LK and RANSAC together lose at
     //     most `margin` points; fe_queue_spec re-records ev_sync[1]
+    //     (the margin grows by the last step's largest LK loss, which it now covers)
     if (fe->fast_early && !fe->fast_first && fe->spec_margin >= 0 && fe->spec_early) {
-        int rc = fe_queue_spec(fe, t, 0, S, std::min(fe->cfg.n_features + fe->spec_margin, fe->CAP), nullptr, fe->nA);
+        const int margin = std::min(fe->spec_margin + fe->lk_loss_max, fe->CAP);
+        int rc = fe_queue_spec(fe, t, 0, S, std::min(fe->cfg.n_features + margin, fe->CAP), nullptr, fe->nA, margin);
         if (rc) return rc;
         fe->spec_t = t;
+        fe->spec_margin_t = margin;
     }
     if (fe->pyr_early) {
         const int tn = t + 1;
@@ -1512,6 +1519,7 @@ int svo_frontend_step(svo_frontend* fe, int t, svo_frontend_stats* stats) {
     int64_t nhyp = 0, inl = 0;
     std::vector<int> ms(S, 0);
 
+    int lk_loss = 0;  // largest LK loss of this step (n_before - n_tracked), for the next speculation
     // 4. per slice, in order: calculatePose (RANSAC per sequence, hypotheses
     //    scored on the GPU), drop outliers (R:src/tracking.cpp:218-229), keyframe
     for (int g = 0; g < G; g++) {
@@ -1648,7 +1656,8 @@ int svo_frontend_step(svo_frontend* fe, int t, svo_frontend_stats* stats) {
             r.select(c.K, false);
             const int kept = r.ok ? r.maxGood : (r.n < 4 ? r.n : 0);
             max_take = std::max(max_take, c.n_features - kept);
-            spec_ok &= (fe->spec_t == t ? fe->h_nA[s] : fe->h_nB[s]) - kept <= fe->spec_margin;
+            spec_ok &= fe->spec_t == t ? fe->h_nA[s] - kept <= fe->spec_margin_t : fe->h_nB[s] - kept <= fe->spec_margin;
+            lk_loss = std::max(lk_loss, fe->h_nA[s] - fe->h_nB[s]);
             uint32_t* b = fe->h_best + (size_t)s * fe->WORDS;
             std::memset(b, 0, sizeof(uint32_t) * fe->WORDS);
             if (r.ok) {
@@ -1693,6 +1702,7 @@ int svo_frontend_step(svo_frontend* fe, int t, svo_frontend_stats* stats) {
             if (rl) return rl;
         }
     }
+    fe->lk_loss_max = lk_loss;
     fe->fits_pending = true;  // statistics land with the stream syncs below
     fe->fit_parity = t & 1;
     // The critical path goes on with the next step's LK right behind this tail;

@@ -64,6 +64,25 @@ def test_frontend_matches_oracle_loop(bucket, spec, ahead, monkeypatch):
         np.testing.assert_allclose(O.rodrigues(rv), sc.R(t), atol=3e-3)
 
 
+@pytest.mark.parametrize("early", ["0", "1"])
+def test_frontend_speculative_stereo_schedules(early, monkeypatch):
+    """SVO_FE_SPEC_EARLY: the speculative stereo LK queued with the front half,
+    behind FAST (1; sized from the features before LK) or behind the post-LK (0,
+    the default; sized from the tracked count) -- both against the oracle loop, at
+    a small margin (4; the front-half schedule adds the last step's largest LK loss)."""
+    monkeypatch.setenv("SVO_FE_SPEC_EARLY", early)
+    monkeypatch.setenv("SVO_FE_SPEC_MARGIN", "4")
+    ctx = S.Context(0)
+    W, H, N, T = 640, 376, 800, 8
+    fe = make_frontend(ctx, [Scene(W, H, seed=5)], T, N)
+    fe.init(0)
+    ref = OracleLoop(Scene(W, H, seed=5), N).init(0)
+    for t in range(1, T):
+        st = fe.step(t).as_dict()
+        rs = ref.step(t)
+        _compare_step(fe, ref, st, rs, t)
+
+
 def test_frontend_200_frames_kitti_matches_oracle_loop():
     """BASELINE.json configs[0]: 200 frames of a 1241x376 sequence with 2000
     features, every step against the oracle loop (R:src/tracking.cpp:232-276)."""

@@ -15,6 +15,7 @@
 #   lkab "V1 V2 .."         standalone LK kernel time per SVO_LK_MULTI variant
 #   lkmem [LIB ..]          LK memory-pipeline + issue counters (TA, TCP, SQ), per library build
 #   ab VAR "V1 V2" [RUNS]   bench A/B of an environment switch
+#   abcfg VAR "V1 V2"       the same A/B at the 1080p, 4K and KITTI configs
 #   round TAG               tests, smoke, prof, pmc (3 configs), mix, bench lines
 #
 # Every GPU step has its own time limit; the first failure ends the session.
@@ -195,6 +196,21 @@ print('$var=$v', d['value'], d['ms_per_step'], 'lk', p['lk'], 'fast', p['fast'],
     done; done
 }
 
+run_abcfg() {
+    local var=$1 vals=$2
+    for cfg in 1080p 4k kitti; do
+        local seq=16
+        [ $cfg = kitti ] && seq=64
+        for v in $vals; do
+            env $var=$v timeout -k 10 200 python bench.py --config $cfg --seq $seq --steps 20 --warmup 5 --no-cpu-baseline \
+                --no-single --no-bucketed > $O/abc.log 2>&1 || fail abcfg $O/abc.log
+            python -c "
+import json; d=json.loads(open('$O/abc.log').read().strip().splitlines()[-1]); p=d['phase_ms_per_step']
+print('$cfg $var=$v', d['value'], d['ms_per_step'], 'lk', p['lk'], 'stereo', p['stereo_lk'])"
+        done
+    done
+}
+
 run_round() {
     local tag=$1
     run_tests
@@ -226,6 +242,7 @@ while [ $# -gt 0 ]; do
         lkab) run_lkab "${args[@]}" ;;
         lkmem) run_lkmem "${args[@]}" ;;
         ab) run_ab "${args[@]}" ;;
+        abcfg) run_abcfg "${args[@]}" ;;
         round) run_round "${args[@]}" ;;
         *) fail "unknown mode $mode" ;;
     esac
