@@ -299,7 +299,7 @@ def main():
                                                                 "pad_batched_kernel"))
     pyr_traffic = ML * t_ps + t_sc + t_pad if None not in (t_ps, t_sc, t_pad) else None
     single = None
-    if not args.no_single:
+    if not args.no_single and world == 1:
         fe1 = S.Frontend(ctx, S.FrontendConfig(W, H, scenes[0].K, n_seq=1, n_frames=T, n_features=N, max_level=ML))
         for t in range(T):
             fe1.set_frame(0, t, *pairs0[t % P])
@@ -390,7 +390,7 @@ def main():
             "in_step_avg_launch_us": round(pyr_instep_s * 1e6, 3),
         },
     }
-    if not args.no_cpu_baseline:
+    if not args.no_cpu_baseline and world == 1:  # rank 0 at N = 1 only
         out["cpu_baseline"] = cpu_baseline(args.config, args.cpu_seconds)
     print(json.dumps(out), flush=True)
 
