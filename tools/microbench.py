@@ -4,6 +4,7 @@
     python tools/microbench.py lk --points 128000 --reps 5
     python tools/microbench.py pyr --reps 20
     python tools/microbench.py fast --reps 20
+    python tools/microbench.py fepyr --reps 20 --seq 64   (the front end's batched pyramid chain)
 """
 import argparse
 import os
@@ -19,7 +20,8 @@ from svo_amd.scene import Scene  # noqa: E402
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("what", choices=["lk", "pyr", "fast", "stereo"])
+    ap.add_argument("what", choices=["lk", "pyr", "fast", "stereo", "fepyr"])
+    ap.add_argument("--seq", type=int, default=64)
     ap.add_argument("--points", type=int, default=128000)
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--w", type=int, default=1241)
@@ -49,6 +51,14 @@ def main():
         for r in range(args.reps):
             ga.upload(A)
         print("pyr done")
+    elif args.what == "fepyr":
+        cfg = S.FrontendConfig(args.w, args.h, sc.K, n_seq=args.seq, n_frames=2, n_features=2000, max_level=3)
+        fe = S.Frontend(ctx, cfg)
+        for s_ in range(args.seq):
+            for t in range(2):
+                fe.set_frame(s_, t, A if t == 0 else B, B)
+        ms = fe.time_pyramid(1, args.reps)
+        print(f"fepyr {args.seq} x {args.w}x{args.h}: {ms * 1e3:.1f} us per chain")
     elif args.what == "fast":
         for r in range(args.reps):
             kp = ctx.fast_detect(ga, 20, True)
