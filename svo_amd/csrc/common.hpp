@@ -223,11 +223,6 @@ struct PnpBatch {
     int words_cap;
     int* cnt;        // nullable
     int mstride = 0; // hypothesis-row stride of hyp/err/bits/cnt per sequence (0: m)
-    // alternatively to cnt: per-wave inlier counts, [seq][row][wave] with
-    // wave_stride entries per row (no memset / atomics; the reader sums the
-    // waves that start below n). All outputs may live in host-coherent memory.
-    int* wave_cnt = nullptr;
-    int wave_stride = 0;
 };
 hipError_t launch_pnp_residuals(const PnpBatch& b, int nseq, int max_n, double fx, double fy, double cx,
                                 double cy, float thresh2, hipStream_t st);

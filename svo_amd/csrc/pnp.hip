@@ -63,18 +63,13 @@ __global__ __launch_bounds__(256) void pnp_residual_kernel(PnpBatch B, double fx
         if (lane == 1 && w0 + 1 < words) bits[w0 + 1] = (uint32_t)(bal >> 32);
     }
     if (B.cnt && lane == 0 && bal) atomicAdd(&B.cnt[(size_t)seq * ms + h], __popcll(bal));
-    // only the waves that hold points (the reader sums ceil(n / 64) of them): a
-    // wave past n would land in the next hypothesis' row whenever the row stride
-    // (ceil(cap / 64) waves) is not a multiple of the block's 4 waves
-    const int wave = (blockIdx.x * 256 + threadIdx.x) / 64;
-    if (B.wave_cnt && lane == 0 && wave * 64 < n) B.wave_cnt[((size_t)seq * ms + h) * B.wave_stride + wave] = __popcll(bal);
 }
 
 // One block per (hypothesis, sequence) over all of the sequence's points: the same
 // inlier test, bits written word by word as pnp_residual_kernel does, and the
 // inlier count reduced inside the block and written ONCE per hypothesis (B.cnt,
 // which may live in host-coherent memory: the host reads m counts per sequence
-// instead of summing per-wave counts out of uncached memory). 256 threads: the
+// instead of summing per-wave counts out of uncached memory, as round 1 did). 256 threads: the
 // blocks must find room on CUs a running LK occupies (a 1024-thread block
 // waits for a whole CU to drain: measured 290 us against ~25 us)
 constexpr int kScoreBlock = 256;
