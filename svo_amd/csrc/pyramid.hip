@@ -8,6 +8,8 @@
 // Unlike the reference, which rebuilds both pyramids on every LK call, a frame's
 // pyramid is built once, kept in HBM and shared by the temporal and stereo LK
 // calls. HBM roofline: reads w*h, writes w*h/4 bytes per level.
+#include <cstdlib>
+
 #include "common.hpp"
 
 namespace svo {
@@ -177,6 +179,8 @@ namespace {
 constexpr int FS_IW = 2 * PD_TX + 8;  // 136 staged columns: sx0 - 2 .. sx0 + 133 (dword aligned)
 constexpr int FS_IH = PD_IH;          // 36 rows
 
+// NT: the derivative and level stores as non-temporal (streaming) stores
+template <bool NT>
 __global__ __launch_bounds__(256) void pyr_scharr_kernel(const PyrDesc* __restrict__ descs,
                                                          const DerivDesc* __restrict__ ders, int level) {
     const PyrDesc& P = descs[blockIdx.z];
@@ -256,7 +260,13 @@ __global__ __launch_bounds__(256) void pyr_scharr_kernel(const PyrDesc* __restri
                 }
                 uint32_t* dst = out + (size_t)y * op + x;
                 if (x + 3 < sw) {
-                    *reinterpret_cast<uint4*>(dst) = make_uint4(o[0], o[1], o[2], o[3]);
+                    if constexpr (NT) {
+                        typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+                        const u32x4 v = {o[0], o[1], o[2], o[3]};
+                        __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(dst));
+                    } else {
+                        *reinterpret_cast<uint4*>(dst) = make_uint4(o[0], o[1], o[2], o[3]);
+                    }
                 } else {
 #pragma unroll
                     for (int m = 0; m < 4; m++)
@@ -293,7 +303,16 @@ hipError_t launch_pyramid_scharr_batched(const PyrDesc* d_descs, const DerivDesc
     for (int l = 0; l + 1 < nlevels; l++) {
         const int nw = (lw + 1) / 2, nh = (lh + 1) / 2;
         dim3 grid((nw + PD_TX - 1) / PD_TX, (nh + PD_TY - 1) / PD_TY, nseq);
-        hipLaunchKernelGGL(pyr_scharr_kernel, grid, dim3(256), 0, st, d_descs, d_ders, l);
+        // non-temporal derivative stores (SVO_PYR_NT=0: plain): the chain alone
+        // 97.6 -> 89.5 us per 64 frames, the step unchanged (LK reads them a step later)
+        static const bool nt = [] {
+            const char* e = std::getenv("SVO_PYR_NT");
+            return !(e && e[0] == '0');
+        }();
+        if (nt)
+            hipLaunchKernelGGL(pyr_scharr_kernel<true>, grid, dim3(256), 0, st, d_descs, d_ders, l);
+        else
+            hipLaunchKernelGGL(pyr_scharr_kernel<false>, grid, dim3(256), 0, st, d_descs, d_ders, l);
         lw = nw;
         lh = nh;
     }
