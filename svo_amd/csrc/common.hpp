@@ -204,6 +204,10 @@ struct LKBatch {
     int* iters;   // nullable
     const int* counts;  // nullable
     int n, cap;
+    // > 0 (one-feature-per-wave kernel only): grid for this many features per
+    // sequence; waves loop over any beyond it (a device-side count the host only
+    // bounds loosely, e.g. the speculative stereo candidates)
+    int grid_hint = 0;
 };
 hipError_t launch_lk(const LKBatch& b, int nseq, int max_n, const LKParams& p, hipStream_t st);
 bool lk_supported(int win_w, int win_h);

@@ -281,6 +281,7 @@ struct svo_frontend {
     int spec_t = -1;  // step whose speculative stereo LK went out with its front half
     int spec_margin_t = 32;  // the margin that speculation used (spec_margin + the last LK losses)
     int lk_loss_max = 0;     // max over sequences of the last step's LK losses (n_before - n_tracked)
+    int min_tracked = 0;     // min over sequences of the last step's tracked count (stereo LK grid hint)
     // LK ahead (SVO_FE_AHEAD, one slice): LK(t+1) runs over step t's tracked
     // points right behind its post-LK, beside the host's RANSAC, and a small LK
     // over the keyframe's appended features follows the keyframe; the next post-LK
@@ -452,7 +453,8 @@ int fe_fast_and_bucket(svo_frontend* fe, const PyrDesc* descs_cur, bool use_mask
 // counts[s]) of sequences [a, a + n) of frame t; max_n bounds every count (the
 // grid). The left frame's derivative pyramid is the one the next step's
 // temporal LK reads.
-int fe_stereo_lk(svo_frontend* fe, int t, int a, int n, const int* counts, int max_n, hipStream_t st) {
+int fe_stereo_lk(svo_frontend* fe, int t, int a, int n, const int* counts, int max_n, hipStream_t st,
+                 int grid_hint = 0) {
     svo_ctx* ctx = fe->ctx;
     const svo_frontend_config& c = fe->cfg;
     const size_t CAP = fe->CAP;
@@ -462,6 +464,7 @@ int fe_stereo_lk(svo_frontend* fe, int t, int a, int n, const int* counts, int m
     const PyrDesc* dr = fe->d_desc_r + (size_t)(t % fe->T) * fe->S + a;
     LKBatch lb{dl, dr, fe->d_der + (size_t)(t % 3) * fe->S + a, fe->st_xy + 2 * a * CAP, fe->st_next + 2 * a * CAP,
                fe->st_status + a * CAP, nullptr, nullptr, counts, 0, fe->CAP};
+    lb.grid_hint = grid_hint;
     LKParams lp;
     lp.win_w = lp.win_h = c.stereo_win;
     lp.max_level = fe->ml_st;
@@ -580,7 +583,10 @@ int fe_queue_spec(svo_frontend* fe, int t, int a, int n, int max_spec, hipEvent_
     pb.spec_n = fe->spec_n + a;
     if (ev_post) SVO_HIP(ctx, hipStreamWaitEvent(sf, ev_post, 0));
     SVO_HIP(ctx, launch_stereo_prep(pb, n, sf));
-    int rc = fe_stereo_lk(fe, t, a, n, fe->spec_n + a, max_spec, sf);
+    // grid for the speculation the last step's smallest tracked count implies
+    // (+ slack); the kernel's waves loop over any candidates beyond it
+    const int hint = std::min(fe->CAP, fe->cfg.n_features - fe->min_tracked + margin + 32);
+    int rc = fe_stereo_lk(fe, t, a, n, fe->spec_n + a, max_spec, sf, hint);
     if (rc) return rc;
     SVO_HIP(ctx, hipEventRecord(fe->ev_sync[1], sf));
     return SVO_OK;
@@ -1703,6 +1709,11 @@ int svo_frontend_step(svo_frontend* fe, int t, svo_frontend_stats* stats) {
         }
     }
     fe->lk_loss_max = lk_loss;
+    {
+        int mt = fe->CAP;
+        for (int s = 0; s < S; s++) mt = std::min(mt, fe->h_nB[s]);
+        fe->min_tracked = mt;
+    }
     fe->fits_pending = true;  // statistics land with the stream syncs below
     fe->fit_parity = t & 1;
     // The critical path goes on with the next step's LK right behind this tail;

@@ -636,8 +636,8 @@ __global__ __launch_bounds__(256, MINW) void lk_fast_kernel(LKBatch B, LKDev p) 
     const int wid = threadIdx.x >> 6;
     const int seq = blockIdx.y;
     const int n = B.counts ? B.counts[seq] : B.n;
-    const int pt = blockIdx.x * 4 + wid;
-    if (pt >= n) return;
+    // a wave per feature; a grid smaller than the count (LKBatch::grid_hint) loops
+    for (int pt = blockIdx.x * 4 + wid; pt < n; pt += gridDim.x * 4) {
     const size_t base = (size_t)seq * B.cap;
     const float* __restrict__ prev_xy = B.prev_xy + 2 * base;
     float* __restrict__ next_xy = B.next_xy + 2 * base;
@@ -911,6 +911,7 @@ __global__ __launch_bounds__(256, MINW) void lk_fast_kernel(LKBatch B, LKDev p) 
         if (B.err) B.err[base + pt] = errv;
         if (B.iters) B.iters[base + pt] = itcount;
     }
+    }  // features of this wave
 }
 
 // ---------------------------------------------------------------------------
@@ -1719,7 +1720,8 @@ hipError_t launch_dual(const LKBatch& b, int nseq, int max_n, const LKDev& d, hi
 
 template <int WW, int WH>
 hipError_t launch_fast(const LKBatch& b, int nseq, int max_n, const LKDev& d, hipStream_t st) {
-    dim3 grid((max_n + 3) / 4, nseq);
+    const int gn = b.grid_hint > 0 && b.grid_hint < max_n ? b.grid_hint : max_n;
+    dim3 grid((gn + 3) / 4, nseq);
     constexpr int lds_bytes = 4 * Shape<WW, WH>::WAVE_BYTES;
     // occupancy is limited by LDS (7 blocks/CU) and ~70 VGPRs alike; capping the
     // VGPRs lower spills (measured: launch bounds 6/7/8 waves all slower)
