@@ -137,13 +137,26 @@ struct FastDetBatch {
     // nullable [s][npx]: fast_detect_q_kernel writes the score of every kept corner
     // there, so the emit pass reads one byte instead of re-scoring from the image
     uint8_t* score_map = nullptr;
+    // speculative stereo input, filled by the scan / emit passes (StereoPrepBatch's
+    // rule, frontend.hpp): spec_n[s] = min(max(spec_target - spec_tracked[s] +
+    // spec_margin, 0), corners, cap), clamped to spec_cap and spec_map_cap -
+    // spec_map_n[s]; emit copies the first spec_n[s] corners to spec_xy + 2 * s *
+    // spec_cap. Null spec_n: off.
+    const int* spec_tracked = nullptr;
+    const int* spec_map_n = nullptr;
+    int spec_target = 0, spec_margin = 0, spec_cap = 0, spec_map_cap = 0;
+    float* spec_xy = nullptr;
+    int* spec_n = nullptr;
 };
+// stage: 0 detect + scan + emit, 1 detect only (the row counts are cleared first),
+// 2 scan + emit of a detection already queued
+constexpr int kFastAll = 0, kFastDetect = 1, kFastCollect = 2;
 // ints of band-offset scratch per sequence for an image of height h
 // Box centres are binned by cell: 16-row band x 64-column tile (the FAST tile
 // grid), cell-major per band; [s][cells + 1] offsets.
 inline int fast_box_cells(int w, int h) { return ((h + 15) / 16) * ((w + 63) / 64) + 1; }
 hipError_t launch_fast_detect(const FastDetBatch& b, int nseq, int w, int h, int threshold, int nonmax,
-                              hipStream_t st);
+                              hipStream_t st, int stage = kFastAll);
 // The band binning of the box centres alone (needs only box_pts / box_counts).
 hipError_t launch_box_bin(const FastDetBatch& b, int nseq, int w, int h, hipStream_t st);
 // Masks for nseq sequences (w*h each): 255 + filled boxes around counts[s] (or n)

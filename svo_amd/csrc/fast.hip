@@ -1052,7 +1052,15 @@ __global__ __launch_bounds__(kScanBlock) void fast_scan_kernel(FastDetBatch B, i
         off[y] = acc;
         acc += cnt[y];
     }
-    if (tid == kScanBlock - 1) B.n_out[seq] = part[kScanBlock - 1];
+    if (tid == kScanBlock - 1) {
+        const int total = part[kScanBlock - 1];
+        B.n_out[seq] = total;
+        if (B.spec_n) {
+            int spec = min(max(B.spec_target - B.spec_tracked[seq] + B.spec_margin, 0), min(total, B.cap));
+            spec = max(min(min(spec, B.spec_cap), B.spec_map_cap - B.spec_map_n[seq]), 0);
+            B.spec_n[seq] = spec;
+        }
+    }
 }
 
 // raster-order write of one row's keypoints (one wave per row); the FAST
@@ -1089,6 +1097,11 @@ __global__ __launch_bounds__(64) void fast_emit_kernel(FastDetBatch B, int thres
                 kp.y = (float)y;
                 kp.response = resp;
                 out[idx] = kp;
+                if (B.spec_n && idx < B.spec_n[seq]) {  // the speculative stereo LK's input
+                    float* sx = B.spec_xy + 2 * (seq * (size_t)B.spec_cap + idx);
+                    sx[0] = (float)x;
+                    sx[1] = (float)y;
+                }
             }
         }
         off += __popcll(m);
@@ -1137,8 +1150,13 @@ hipError_t launch_fast_collect(const FastBatch& b, int nseq, int w, int h, int n
 }
 
 hipError_t launch_fast_detect(const FastDetBatch& b0, int nseq, int w, int h, int threshold, int nonmax,
-                              hipStream_t st) {
+                              hipStream_t st, int stage) {
     FastDetBatch b = b0;
+    if (stage == kFastCollect) {
+        hipLaunchKernelGGL(fast_scan_kernel, dim3(nseq), dim3(kScanBlock), 0, st, b, h);
+        hipLaunchKernelGGL(fast_emit_kernel, dim3(h, nseq), dim3(64), 0, st, b, threshold, nonmax);
+        return hipGetLastError();
+    }
     hipError_t e = hipMemsetAsync(b.rowcnt, 0, sizeof(int) * (size_t)h * nseq, st);
     if (e != hipSuccess) return e;
     if (b.box_pts && !b.box_prebinned) {
@@ -1160,6 +1178,7 @@ hipError_t launch_fast_detect(const FastDetBatch& b0, int nseq, int w, int h, in
         hipLaunchKernelGGL(fast_detect_s_kernel, grid, dim3(256), 0, st, b, threshold, nonmax);
     else
         hipLaunchKernelGGL(fast_detect_q_kernel, grid, dim3(256), 0, st, b, threshold, nonmax);
+    if (stage == kFastDetect) return hipGetLastError();
     hipLaunchKernelGGL(fast_scan_kernel, dim3(nseq), dim3(kScanBlock), 0, st, b, h);
     hipLaunchKernelGGL(fast_emit_kernel, dim3(h, nseq), dim3(64), 0, st, b, threshold, nonmax);
     return hipGetLastError();

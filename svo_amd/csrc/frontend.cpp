@@ -280,6 +280,12 @@ struct svo_frontend {
     bool spec_early = false;
     int spec_t = -1;  // step whose speculative stereo LK went out with its front half
     int spec_margin_t = 32;  // the margin that speculation used (spec_margin + the last LK losses)
+    // FAST's row scan + emit queued behind the post-LK, filling the speculative
+    // stereo input as they write the corners (one slice, no bucketing, post-LK
+    // speculation): no separate prep kernel and stream wait on the keyframe's path
+    // (SVO_FE_FAST_SPLIT=1; off by default: measured within noise to 1.6 % slower
+    // at the three configs)
+    bool fast_split = false;
     int lk_loss_max = 0;     // max over sequences of the last step's LK losses (n_before - n_tracked)
     int min_tracked = 0;     // min over sequences of the last step's tracked count (stereo LK grid hint)
     // LK ahead (SVO_FE_AHEAD, one slice): LK(t+1) runs over step t's tracked
@@ -430,14 +436,15 @@ FastDetBatch fe_fast_batch(svo_frontend* fe, const PyrDesc* descs_cur, bool use_
 }
 
 int fe_fast_and_bucket(svo_frontend* fe, const PyrDesc* descs_cur, bool use_mask, hipStream_t st,
-                       bool prebinned = false) {
+                       bool prebinned = false, int stage = kFastAll) {
     svo_ctx* ctx = fe->ctx;
     int slot;
     FastDetBatch fb = fe_fast_batch(fe, descs_cur, use_mask);
     fb.box_prebinned = prebinned;
     ph_begin(fe, PH_FAST, st, &slot);
-    SVO_HIP(ctx, launch_fast_detect(fb, fe->S, fe->W, fe->H, fe->cfg.fast_threshold, fe->cfg.fast_nonmax, st));
+    SVO_HIP(ctx, launch_fast_detect(fb, fe->S, fe->W, fe->H, fe->cfg.fast_threshold, fe->cfg.fast_nonmax, st, stage));
     ph_end(fe, st, slot);
+    if (stage == kFastDetect) return SVO_OK;
     if (fe->cfg.bucket_size > 0) {
         ph_begin(fe, PH_BUCKET, st, &slot);
         BucketBatch bb{fe->kps, 3, fe->KCAP, fe->kn, 0, nullptr, fe->cand, nullptr, fe->BCAP, fe->bn, fe->scr,
@@ -916,6 +923,8 @@ int svo_frontend_create(svo_ctx* ctx, const svo_frontend_config* cfg, svo_fronte
         fe->spec_margin = sm ? std::atoi(sm) : 32;
         const char* se = std::getenv("SVO_FE_SPEC_EARLY");
         fe->spec_early = se && se[0] == '1';
+        const char* fs = std::getenv("SVO_FE_FAST_SPLIT");
+        fe->fast_split = fs && fs[0] == '1';
     }
     // (on the context stream: a first use of the null stream would take a fifth
     // hardware queue and serialise the step's streams)
@@ -955,6 +964,8 @@ int svo_frontend_create(svo_ctx* ctx, const svo_frontend_config* cfg, svo_fronte
         int G = c.groups > 0 ? c.groups : 1;
         G = std::max(1, std::min(G, S));
         fe->G = G;
+        fe->fast_split = fe->fast_split && G == 1 && c.bucket_size <= 0 && fe->spec_margin >= 0 && !fe->spec_early &&
+                         fe->fast_early && !fe->fast_first;
         fe->g0.resize(G);
         fe->gn.resize(G);
         for (int g = 0; g < G; g++) {
@@ -1288,7 +1299,28 @@ static int fe_post(svo_frontend* fe, int t) {
         SVO_HIP(ctx, hipEventRecord(fe->ev_sync[3 + 2 * g], sg));
         TP("post_lk launched");
         // the keyframe's stereo matches, speculatively, beside this slice's RANSAC
-        if (fe->spec_margin >= 0 && fe->spec_t != t) {
+        if (fe->fast_split) {
+            // FAST's scan + emit of frame t behind the post-LK, writing the first
+            // spec corners to the stereo input, then their stereo LK
+            hipStream_t sf = fe->st_fast;
+            SVO_HIP(ctx, hipStreamWaitEvent(sf, fe->ev_sync[3 + 2 * g], 0));
+            FastDetBatch fb = fe_fast_batch(fe, fe->d_desc + (size_t)(t % fe->T) * fe->S, true);
+            fb.spec_tracked = fe->nB;
+            fb.spec_map_n = fe->map_n;
+            fb.spec_target = fe->cfg.n_features;
+            fb.spec_margin = fe->spec_margin;
+            fb.spec_cap = fe->CAP;
+            fb.spec_map_cap = fe->MAPCAP;
+            fb.spec_xy = fe->st_xy;
+            fb.spec_n = fe->spec_n;
+            SVO_HIP(ctx, launch_fast_detect(fb, fe->S, fe->W, fe->H, fe->cfg.fast_threshold, fe->cfg.fast_nonmax, sf,
+                                            kFastCollect));
+            const int max_spec = std::min(fe->cfg.n_features + fe->spec_margin, fe->CAP);
+            const int hint = std::min(fe->CAP, fe->cfg.n_features - fe->min_tracked + fe->spec_margin + 32);
+            int rq = fe_stereo_lk(fe, t, 0, fe->S, fe->spec_n, max_spec, sf, hint);
+            if (rq) return rq;
+            SVO_HIP(ctx, hipEventRecord(fe->ev_sync[1], sf));
+        } else if (fe->spec_margin >= 0 && fe->spec_t != t) {
             int rq = fe_queue_spec(fe, t, fe->g0[g], fe->gn[g],
                                    std::min(fe->cfg.n_features + fe->spec_margin, fe->CAP), fe->ev_sync[3 + 2 * g],
                                    fe->nB, fe->spec_margin);
@@ -1393,7 +1425,7 @@ static int fe_front_lk(svo_frontend* fe, int t) {
     //     waves leave idle and the post-LK window; the tail waits for it
     if (fe->fast_early && !fe->fast_first) {
         hipStream_t sf = fe->st_fast;
-        int rc = fe_fast_and_bucket(fe, dcur, true, sf, true);
+        int rc = fe_fast_and_bucket(fe, dcur, true, sf, true, fe->fast_split ? kFastDetect : kFastAll);
         if (rc) return rc;
         SVO_HIP(ctx, hipEventRecord(fe->ev_sync[1], sf));
     }

@@ -64,13 +64,15 @@ def test_frontend_matches_oracle_loop(bucket, spec, ahead, monkeypatch):
         np.testing.assert_allclose(O.rodrigues(rv), sc.R(t), atol=3e-3)
 
 
+@pytest.mark.parametrize("split", ["0", "1"])
 @pytest.mark.parametrize("early", ["0", "1"])
-def test_frontend_speculative_stereo_schedules(early, monkeypatch):
+def test_frontend_speculative_stereo_schedules(early, split, monkeypatch):
     """SVO_FE_SPEC_EARLY: the speculative stereo LK queued with the front half,
     behind FAST (1; sized from the features before LK) or behind the post-LK (0,
     the default; sized from the tracked count) -- both against the oracle loop, at
     a small margin (4; the front-half schedule adds the last step's largest LK loss)."""
     monkeypatch.setenv("SVO_FE_SPEC_EARLY", early)
+    monkeypatch.setenv("SVO_FE_FAST_SPLIT", split)  # FAST's scan + emit behind post-LK fill the stereo input
     monkeypatch.setenv("SVO_FE_SPEC_MARGIN", "4")
     ctx = S.Context(0)
     W, H, N, T = 640, 376, 800, 8
