@@ -595,34 +595,39 @@ __global__ __launch_bounds__(256) void fast_detect_w_kernel(FastDetBatch B, int 
 // NMS then visits only the wave's corners instead of every pixel of its rows
 // (the dense pass was ~30 % of the kernel's VALU), and the box mask is applied to
 // the finished row words. Same outputs. ----
+template <int TY>
 __global__ __launch_bounds__(256) void fast_detect_q_kernel(FastDetBatch B, int threshold, int nonmax) {
+    constexpr int QSH = TY + 2, QIH = TY + 8;           // score rows (halo 1), staged rows (halo 4)
+    constexpr int QQ = ((QSH + 3) / 4) * FD_SW + 8;      // queue entries per wave
+    static_assert(2 * ((QSH + 3) / 4) <= 64, "halo pre-test: one lane per (row, side)");
+    static_assert(QSH < 512, "queue entries pack (row << 7 | column) into 16 bits");
     const ImgLevel L = B.descs[blockIdx.z].lv[0];
     const int w = L.w, h = L.h;
-    const int x0 = blockIdx.x * FD_TX, y0 = blockIdx.y * FD_TY;
+    const int x0 = blockIdx.x * FD_TX, y0 = blockIdx.y * TY;
     const size_t seq = blockIdx.z;
-    __shared__ __attribute__((aligned(16))) uint8_t T[FD_IH][FD_IW];
-    __shared__ uint16_t SC[FD_SH][FD_SW + 2];  // bit 8: corner, low byte: score
-    __shared__ uint16_t CQ[4][FW_Q];
-    __shared__ unsigned long long TM[FD_TY];
-    __shared__ unsigned long long RB[FD_TY];
+    __shared__ __attribute__((aligned(16))) uint8_t T[QIH][FD_IW];
+    __shared__ uint16_t SC[QSH][FD_SW + 2];  // bit 8: corner, low byte: score
+    __shared__ uint16_t CQ[4][QQ];
+    __shared__ unsigned long long TM[TY];
+    __shared__ unsigned long long RB[TY];
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-    const bool inside = x0 >= 4 && y0 >= 4 && x0 - 4 + FD_IW <= w && y0 - 4 + FD_IH <= h;
+    const bool inside = x0 >= 4 && y0 >= 4 && x0 - 4 + FD_IW <= w && y0 - 4 + QIH <= h;
     if (inside) {
-        for (int k = tid; k < FD_IH * (FD_IW / 4); k += 256) {
+        for (int k = tid; k < QIH * (FD_IW / 4); k += 256) {
             const int r = k / (FD_IW / 4), c4 = k - r * (FD_IW / 4);
             const uint8_t* src = L.data + (size_t)(y0 - 4 + r) * L.pitch + (x0 - 4 + 4 * c4);
             *reinterpret_cast<uint32_t*>(&T[r][4 * c4]) = *reinterpret_cast<const uint32_t*>(src);
         }
     } else {
-        for (int k = tid; k < FD_IH * FD_IW; k += 256) {
+        for (int k = tid; k < QIH * FD_IW; k += 256) {
             const int r = k / FD_IW, c = k - r * FD_IW;
             const int y = y0 - 4 + r, x = x0 - 4 + c;
             T[r][c] = ((unsigned)y < (unsigned)h && (unsigned)x < (unsigned)w) ? L.data[(size_t)y * L.pitch + x] : 0;
         }
     }
     const bool boxes = B.box_pts != nullptr;
-    if (boxes && tid < FD_TY) TM[tid] = ~0ull;
-    if (tid < FD_TY) RB[tid] = 0ull;
+    if (boxes && tid < TY) TM[tid] = ~0ull;
+    if (tid < TY) RB[tid] = 0ull;
     __syncthreads();
     const int hi_t = threshold, lo_t = -threshold;
     // ---- A0: compass pre-test of this wave's rows sr = wv, wv + 4, ... (lane -> column
@@ -644,14 +649,14 @@ __global__ __launch_bounds__(256) void fast_detect_q_kernel(FastDetBatch B, int 
         if (cand) q[nq + __popcll(bal & ((1ull << lane) - 1ull))] = (uint16_t)((sr << 7) | sc);
         nq += __popcll(bal);
     };
-    for (int sr = wv; sr < FD_SH; sr += 4) {
+    for (int sr = wv; sr < QSH; sr += 4) {
         SC[sr][lane + 1] = 0;
         if (lane < 2) SC[sr][lane * 65] = 0;
         pretest(sr, lane + 1, true);
     }
     {
         // halo columns 0 and 65 of the wave's rows (<= 9 rows -> 18 positions)
-        const int nr = (FD_SH - wv + 3) / 4;
+        const int nr = (QSH - wv + 3) / 4;
         const int sr = wv + 4 * (lane >> 1), sc = (lane & 1) * 65;
         pretest(sr, sc, lane < 2 * nr);
     }
@@ -705,7 +710,7 @@ __global__ __launch_bounds__(256) void fast_detect_q_kernel(FastDetBatch B, int 
         const int nb = (h + 15) / 16, ncl = (w + 63) / 64;
         const int* __restrict__ cells = B.box_band + seq * (size_t)(nb * ncl + 1);
         const int b0 = max(0, (int)floorf((y0 - B.box_half - 1.f) / 16.f));
-        const int b1 = min(nb - 1, (int)floorf((y0 + FD_TY + B.box_half + 1.f) / 16.f));
+        const int b1 = min(nb - 1, (int)floorf((y0 + TY + B.box_half + 1.f) / 16.f));
         const int cb0 = max(0, (int)floorf((x0 - B.box_half - 1.f) / 64.f));
         const int cb1 = min(ncl - 1, (int)floorf((x0 + FD_TX + B.box_half + 1.f) / 64.f));
         const float* __restrict__ pts = B.box_binned + 2 * seq * (size_t)B.box_stride;
@@ -718,7 +723,7 @@ __global__ __launch_bounds__(256) void fast_detect_q_kernel(FastDetBatch B, int 
                 xl = max(xl, max(0, x0));
                 xr = min(xr, min(w - 1, x0 + FD_TX - 1));
                 yt = max(yt, max(0, y0));
-                yd = min(yd, min(h - 1, y0 + FD_TY - 1));
+                yd = min(yd, min(h - 1, y0 + TY - 1));
                 if (xl > xr || yt > yd) continue;
                 const int c0 = xl - x0, c1 = xr - x0;  // 0..63
                 const unsigned long long span =
@@ -734,7 +739,7 @@ __global__ __launch_bounds__(256) void fast_detect_q_kernel(FastDetBatch B, int 
     for (int i = lane; i < nc; i += 64) {
         const int k = q[i];
         const int sr = k >> 7, sc = k & 127;
-        if (sr < 1 || sr > FD_TY || sc < 1 || sc > FD_TX) continue;  // halo: scores only
+        if (sr < 1 || sr > TY || sc < 1 || sc > FD_TX) continue;  // halo: scores only
         const int x = x0 + sc - 1, y = y0 + sr - 1;
         bool keep = x < w && y < h;
         if (nonmax) {
@@ -753,7 +758,7 @@ __global__ __launch_bounds__(256) void fast_detect_q_kernel(FastDetBatch B, int 
         }
     }
     __syncthreads();
-    if (tid < FD_TY && y0 + tid < h) {
+    if (tid < TY && y0 + tid < h) {
         const unsigned long long bal = RB[tid] & (boxes ? TM[tid] : ~0ull);
         const size_t row = seq * h + y0 + tid;
         B.bits[row * B.nseg + blockIdx.x] = bal;
@@ -1176,8 +1181,16 @@ hipError_t launch_fast_detect(const FastDetBatch& b0, int nseq, int w, int h, in
         hipLaunchKernelGGL(fast_detect_w_kernel, grid, dim3(256), 0, st, b, threshold, nonmax);
     else if (ver == 3)
         hipLaunchKernelGGL(fast_detect_s_kernel, grid, dim3(256), 0, st, b, threshold, nonmax);
-    else
-        hipLaunchKernelGGL(fast_detect_q_kernel, grid, dim3(256), 0, st, b, threshold, nonmax);
+    else {
+        // tile height of the queue form (SVO_FAST_QTY: 32 default, 64 -- 81.0 vs 83.6 us
+        // alone per 64-frame launch, but stretched longer beside LK: step within noise)
+        const char* ty = std::getenv("SVO_FAST_QTY");
+        if (ty && std::atoi(ty) == 64)
+            hipLaunchKernelGGL(fast_detect_q_kernel<64>, dim3(grid.x, (h + 63) / 64, nseq), dim3(256), 0, st, b,
+                               threshold, nonmax);
+        else
+            hipLaunchKernelGGL(fast_detect_q_kernel<32>, grid, dim3(256), 0, st, b, threshold, nonmax);
+    }
     if (stage == kFastDetect) return hipGetLastError();
     hipLaunchKernelGGL(fast_scan_kernel, dim3(nseq), dim3(kScanBlock), 0, st, b, h);
     hipLaunchKernelGGL(fast_emit_kernel, dim3(h, nseq), dim3(64), 0, st, b, threshold, nonmax);

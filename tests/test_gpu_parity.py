@@ -85,12 +85,16 @@ def test_frontend_scharr_pyramid_bit_exact(ctx, wh):
 
 
 # ------------------------------------------------------------------ FAST
-@pytest.fixture(params=["block-queue", "wave-queue", "swar", "queue-nms"])
+@pytest.fixture(params=["block-queue", "wave-queue", "swar", "queue-nms", "queue-nms-64"])
 def fast_kernel(request, monkeypatch):
     """Every fused detection form (SVO_FAST_V=1 fast_detect_kernel, 2
-    fast_detect_w_kernel, 3 fast_detect_s_kernel, 4 fast_detect_q_kernel) must give
-    the oracle's keypoints."""
-    monkeypatch.setenv("SVO_FAST_V", {"block-queue": "1", "wave-queue": "2", "swar": "3", "queue-nms": "4"}[request.param])
+    fast_detect_w_kernel, 3 fast_detect_s_kernel, 4 fast_detect_q_kernel with its
+    32-row tile, and the same with the 64-row tile, SVO_FAST_QTY=64) must give the
+    oracle's keypoints."""
+    monkeypatch.setenv("SVO_FAST_V", {"block-queue": "1", "wave-queue": "2", "swar": "3", "queue-nms": "4",
+                                      "queue-nms-64": "4"}[request.param])
+    if request.param == "queue-nms-64":
+        monkeypatch.setenv("SVO_FAST_QTY", "64")
     return request.param
 
 
