@@ -1411,6 +1411,15 @@ static int fe_front_lk(svo_frontend* fe, int t) {
         SVO_HIP(ctx, hipEventRecord(ev_pyr, st0));
     }
 
+    // 2'. SVO_FE_FAST_FIRST=1: FAST(t) (mask around frame t-1's features + detection,
+    //     step 3b below) submitted ahead of the LK instead of behind it: same FAST
+    //     stream, so it stays ordered behind the box binning of frame t-1's features
+    if (fe->fast_early && fe->fast_first) {
+        hipStream_t sf = fe->st_fast;
+        int rc = fe_fast_and_bucket(fe, dcur, true, sf, true, kFastAll);
+        if (rc) return rc;
+        SVO_HIP(ctx, hipEventRecord(fe->ev_sync[1], sf));
+    }
     // 3. per slice: temporal LK (trackFrames) -- unless the pipelined schedule
     //    already queued it behind the slice's previous keyframe (fe_lk_slice)
     for (int g = 0; g < G; g++) {

@@ -85,6 +85,22 @@ def test_frontend_speculative_stereo_schedules(early, split, monkeypatch):
         _compare_step(fe, ref, st, rs, t)
 
 
+@pytest.mark.parametrize("first", ["0", "1"])
+def test_frontend_fast_first_schedule(first, monkeypatch):
+    """SVO_FE_FAST_FIRST: FAST(t) submitted ahead of LK(t) on the FAST stream (1) or
+    right behind it (0, the default) -- both against the oracle loop."""
+    monkeypatch.setenv("SVO_FE_FAST_FIRST", first)
+    ctx = S.Context(0)
+    W, H, N, T = 640, 376, 800, 8
+    fe = make_frontend(ctx, [Scene(W, H, seed=7)], T, N)
+    fe.init(0)
+    ref = OracleLoop(Scene(W, H, seed=7), N).init(0)
+    for t in range(1, T):
+        st = fe.step(t).as_dict()
+        rs = ref.step(t)
+        _compare_step(fe, ref, st, rs, t)
+
+
 def test_frontend_200_frames_kitti_matches_oracle_loop():
     """BASELINE.json configs[0]: 200 frames of a 1241x376 sequence with 2000
     features, every step against the oracle loop (R:src/tracking.cpp:232-276)."""
