@@ -150,7 +150,9 @@ struct FastDetBatch {
 };
 // stage: 0 detect + scan + emit, 1 detect only (the row counts are cleared first),
 // 2 scan + emit of a detection already queued
-constexpr int kFastAll = 0, kFastDetect = 1, kFastCollect = 2;
+// kFastBoxes: the detection already ran without the box mask (kFastDetect with no
+// box_pts): AND the rasterised boxes into its row words, recount, scan + emit
+constexpr int kFastAll = 0, kFastDetect = 1, kFastCollect = 2, kFastBoxes = 3;
 // ints of band-offset scratch per sequence for an image of height h
 // Box centres are binned by cell: 16-row band x 64-column tile (the FAST tile
 // grid), cell-major per band; [s][cells + 1] offsets.

@@ -766,6 +766,51 @@ __global__ __launch_bounds__(256) void fast_detect_q_kernel(FastDetBatch B, int 
     }
 }
 
+// ---- box filter of an unmasked detection (kFastBoxes): the previous frame's
+// feature boxes rasterised per 64x32 tile exactly as fast_detect_q_kernel<32> does
+// (cv::rectangle semantics from the band-binned centres), ANDed into the row words
+// the detection wrote, row counts recounted. The boxes are applied after NMS in
+// every form, so detecting first and masking later gives the same keypoints. ----
+__global__ __launch_bounds__(256) void fast_box_filter_kernel(FastDetBatch B, int w, int h) {
+    constexpr int TY = 32;
+    const int x0 = blockIdx.x * FD_TX, y0 = blockIdx.y * TY;
+    const size_t seq = blockIdx.z;
+    __shared__ unsigned long long TM[TY];
+    const int tid = threadIdx.x;
+    if (tid < TY) TM[tid] = ~0ull;
+    __syncthreads();
+    const int nb = (h + 15) / 16, ncl = (w + 63) / 64;
+    const int* __restrict__ cells = B.box_band + seq * (size_t)(nb * ncl + 1);
+    const int b0 = max(0, (int)floorf((y0 - B.box_half - 1.f) / 16.f));
+    const int b1 = min(nb - 1, (int)floorf((y0 + TY + B.box_half + 1.f) / 16.f));
+    const int cb0 = max(0, (int)floorf((x0 - B.box_half - 1.f) / 64.f));
+    const int cb1 = min(ncl - 1, (int)floorf((x0 + FD_TX + B.box_half + 1.f) / 64.f));
+    const float* __restrict__ pts = B.box_binned + 2 * seq * (size_t)B.box_stride;
+    for (int bq = b0; bq <= b1; bq++)
+        for (int i = cells[bq * ncl + cb0] + tid, i1 = cells[bq * ncl + cb1 + 1]; i < i1; i += 256) {
+            const float px = pts[2 * i], py = pts[2 * i + 1];
+            const int xa = (int)__builtin_rintf(px - B.box_half), ya = (int)__builtin_rintf(py - B.box_half);
+            const int xb = (int)__builtin_rintf(px + B.box_half), yb = (int)__builtin_rintf(py + B.box_half);
+            int xl = min(xa, xb), xr = max(xa, xb), yt = min(ya, yb), yd = max(ya, yb);
+            xl = max(xl, max(0, x0));
+            xr = min(xr, min(w - 1, x0 + FD_TX - 1));
+            yt = max(yt, max(0, y0));
+            yd = min(yd, min(h - 1, y0 + TY - 1));
+            if (xl > xr || yt > yd) continue;
+            const int c0 = xl - x0, c1 = xr - x0;  // 0..63
+            const unsigned long long span = (c1 - c0 == 63) ? ~0ull : (((1ull << (c1 - c0 + 1)) - 1ull) << c0);
+            for (int y = yt; y <= yd; y++) atomicAnd(&TM[y - y0], ~span);
+        }
+    __syncthreads();
+    if (tid < TY && y0 + tid < h) {
+        const size_t row = seq * h + y0 + tid;
+        unsigned long long* word = B.bits + row * B.nseg + blockIdx.x;
+        const unsigned long long bal = *word & TM[tid];
+        *word = bal;
+        if (bal) atomicAdd(&B.rowcnt[row], __popcll(bal));
+    }
+}
+
 // ---- SWAR form (SVO_FAST_V=3): as fast_detect_w_kernel, with the compass
 // pre-test on 4 pixels per lane and a register NMS. The staged tile starts 8
 // pixels left of the tile (T column c <-> x = x0 - 8 + c) and the score region
@@ -1158,6 +1203,22 @@ hipError_t launch_fast_detect(const FastDetBatch& b0, int nseq, int w, int h, in
                               hipStream_t st, int stage) {
     FastDetBatch b = b0;
     if (stage == kFastCollect) {
+        hipLaunchKernelGGL(fast_scan_kernel, dim3(nseq), dim3(kScanBlock), 0, st, b, h);
+        hipLaunchKernelGGL(fast_emit_kernel, dim3(h, nseq), dim3(64), 0, st, b, threshold, nonmax);
+        return hipGetLastError();
+    }
+    if (stage == kFastBoxes) {
+        if (b.mask) return hipErrorInvalidValue;  // a host mask goes with the detection
+        if (b.box_pts) {
+            hipError_t e = hipMemsetAsync(b.rowcnt, 0, sizeof(int) * (size_t)h * nseq, st);
+            if (e != hipSuccess) return e;
+            if (!b.box_prebinned) {
+                e = launch_box_bin(b, nseq, w, h, st);
+                if (e != hipSuccess) return e;
+            }
+            hipLaunchKernelGGL(fast_box_filter_kernel, dim3((w + FD_TX - 1) / FD_TX, (h + 31) / 32, nseq), dim3(256),
+                               0, st, b, w, h);
+        }
         hipLaunchKernelGGL(fast_scan_kernel, dim3(nseq), dim3(kScanBlock), 0, st, b, h);
         hipLaunchKernelGGL(fast_emit_kernel, dim3(h, nseq), dim3(64), 0, st, b, threshold, nonmax);
         return hipGetLastError();

@@ -334,6 +334,13 @@ struct svo_frontend {
     bool pyr_early = true;         // frame t+1's pyramid beside LK(t) (SVO_FE_PYR_EARLY)
     bool fast_early = true;        // FAST(t) queued behind LK(t), not after it (SVO_FE_FAST_EARLY)
     bool fast_first = false;       // FAST(t) queued ahead of LK(t) (SVO_FE_FAST_FIRST)
+    int fast_pre = 0;              // FAST detection of frame t+1 queued in step t (SVO_FE_FAST_PRE):
+                                   // 1 on the pyramid stream behind this step's FAST, 2 on the
+                                   // FAST stream behind this step's speculative stereo LK
+    int pre_t = -1;                // frame whose unmasked detection sits in fbits / rowcnt / score_map
+    int front_fast_t = -1;         // frame whose FAST chain recorded ev_fdone
+    hipEvent_t ev_pre = nullptr;   // that detection done (pyramid stream)
+    hipEvent_t ev_fdone = nullptr; // this step's FAST chain done (FAST stream)
     std::vector<double> pose;  // [s][6]
     bool fits_pending = false;
     bool stats_pending = false;
@@ -452,6 +459,22 @@ int fe_fast_and_bucket(svo_frontend* fe, const PyrDesc* descs_cur, bool use_mask
         SVO_HIP(ctx, launch_bucket(bb, fe->S, fe->W, fe->H, fe->cfg.bucket_size, fe->cfg.per_bucket, st));
         ph_end(fe, st, slot);
     }
+    return SVO_OK;
+}
+
+// SVO_FE_FAST_PRE: frame tn's FAST detection + NMS without the box mask (the mask
+// drops corners after NMS, so it can wait for frame tn-1's features) queued on `st`
+// once the current step's FAST chain has consumed the row words; step tn keeps only
+// the box filter, the recount, scan and emit behind its LK (kFastBoxes)
+static int fe_queue_pre(svo_frontend* fe, int tn, hipStream_t st) {
+    svo_ctx* ctx = fe->ctx;
+    const PyrDesc* dnext = fe->d_desc + (size_t)(tn % fe->T) * fe->S;
+    SVO_HIP(ctx, hipStreamWaitEvent(st, fe->ev_fdone, 0));
+    FastDetBatch fb = fe_fast_batch(fe, dnext, false);
+    SVO_HIP(ctx, launch_fast_detect(fb, fe->S, fe->W, fe->H, fe->cfg.fast_threshold, fe->cfg.fast_nonmax, st,
+                                    kFastDetect));
+    SVO_HIP(ctx, hipEventRecord(fe->ev_pre, st));
+    fe->pre_t = tn;
     return SVO_OK;
 }
 
@@ -917,6 +940,8 @@ int svo_frontend_create(svo_ctx* ctx, const svo_frontend_config* cfg, svo_fronte
         fe->fast_early = !(fe_ && fe_[0] == '0');
         const char* ff = std::getenv("SVO_FE_FAST_FIRST");
         fe->fast_first = ff && ff[0] == '1';
+        const char* fp = std::getenv("SVO_FE_FAST_PRE");
+        fe->fast_pre = fp && fp[0] ? std::max(0, std::min(2, std::atoi(fp))) : 0;
         const char* pp = std::getenv("SVO_FE_PIPE");
         fe->pipe = !(pp && pp[0] == '0');
         const char* sm = std::getenv("SVO_FE_SPEC_MARGIN");
@@ -966,6 +991,7 @@ int svo_frontend_create(svo_ctx* ctx, const svo_frontend_config* cfg, svo_fronte
         fe->G = G;
         fe->fast_split = fe->fast_split && G == 1 && c.bucket_size <= 0 && fe->spec_margin >= 0 && !fe->spec_early &&
                          fe->fast_early && !fe->fast_first;
+        if (!(G == 1 && fe->fast_early && !fe->fast_first && !fe->fast_split)) fe->fast_pre = 0;
         fe->g0.resize(G);
         fe->gn.resize(G);
         for (int g = 0; g < G; g++) {
@@ -1032,6 +1058,8 @@ int svo_frontend_create(svo_ctx* ctx, const svo_frontend_config* cfg, svo_fronte
         for (auto& e : fe->ev_full_b) (void)hipEventCreateWithFlags(&e, hipEventDisableTiming);
         fe->ev_full = fe->ev_full_b[0];
         (void)hipEventCreateWithFlags(&fe->ev_pyr_r, hipEventDisableTiming);
+        (void)hipEventCreateWithFlags(&fe->ev_pre, hipEventDisableTiming);
+        (void)hipEventCreateWithFlags(&fe->ev_fdone, hipEventDisableTiming);
         // 4 hardware queues: with several slices (or the keyframe stream of LK
         // ahead) the copy stream's work shares the pyramid stream
         if (G > 1 || fe->ahead) {
@@ -1077,6 +1105,8 @@ void svo_frontend_destroy(svo_frontend* fe) {
     for (auto& e : fe->ev_sync)
         if (e) (void)hipEventDestroy(e);
     if (fe->ev_stats) (void)hipEventDestroy(fe->ev_stats);
+    if (fe->ev_pre) (void)hipEventDestroy(fe->ev_pre);
+    if (fe->ev_fdone) (void)hipEventDestroy(fe->ev_fdone);
     if (fe->st_copy && fe->st_copy_owned) {
         (void)hipStreamSynchronize(fe->st_copy);
         (void)hipStreamDestroy(fe->st_copy);
@@ -1122,6 +1152,7 @@ static int fe_set_frame(svo_frontend* fe, int seq, int t, const uint8_t* left, c
     int rd = fe_drain(fe);
     if (rd) return rd;
     if (fe->pyr_ready >= 0 && fe->pyr_ready % fe->T == t) fe->pyr_ready = -1;  // built from the old image
+    if (fe->pre_t >= 0 && fe->pre_t % fe->T == t) fe->pre_t = -1;  // detected on the old image
     for (int side = 0; side < 2; side++) {
         svo_image* im = (side ? fe->frames_r : fe->frames)[(size_t)seq * fe->T + t];
         const uint8_t* px = side ? right : left;
@@ -1167,6 +1198,7 @@ int svo_frontend_init(svo_frontend* fe, int t0) {
     int rd = fe_drain(fe);
     if (rd) return rd;
     fe->pyr_ready = -1;
+    fe->pre_t = -1;
     fe->fits_pending = false;
     fe->stats_pending = false;
     fe->boxes_binned = false;
@@ -1328,6 +1360,10 @@ static int fe_post(svo_frontend* fe, int t) {
         }
         TP("spec stereo launched");
     }
+    if (fe->fast_pre == 2 && fe->front_fast_t == t) {
+        int rc = fe_queue_pre(fe, t + 1, fe->st_fast);
+        if (rc) return rc;
+    }
     // every slice's points are gathered once the last slice's post-LK is done
     SVO_HIP(ctx, hipEventRecord(fe->ev_gathered, fe->gst[G - 1]));
     // LK ahead: LK(t+1) over these tracked points, right behind the post-LK (frame
@@ -1434,9 +1470,21 @@ static int fe_front_lk(svo_frontend* fe, int t) {
     //     waves leave idle and the post-LK window; the tail waits for it
     if (fe->fast_early && !fe->fast_first) {
         hipStream_t sf = fe->st_fast;
-        int rc = fe_fast_and_bucket(fe, dcur, true, sf, true, fe->fast_split ? kFastDetect : kFastAll);
+        int stage = fe->fast_split ? kFastDetect : kFastAll;
+        if (fe->fast_pre && fe->pre_t == t) {
+            // SVO_FE_FAST_PRE: frame t was detected (unmasked) during step t-1; only the
+            // box mask of frame t-1's features, the recount, scan and emit remain
+            SVO_HIP(ctx, hipStreamWaitEvent(sf, fe->ev_pre, 0));
+            stage = kFastBoxes;
+        }
+        fe->pre_t = -1;
+        int rc = fe_fast_and_bucket(fe, dcur, true, sf, true, stage);
         if (rc) return rc;
         SVO_HIP(ctx, hipEventRecord(fe->ev_sync[1], sf));
+        if (fe->fast_pre) {
+            SVO_HIP(ctx, hipEventRecord(fe->ev_fdone, sf));
+            fe->front_fast_t = t;
+        }
     }
     // 3'. frame t+1's pyramid + Scharr + borders, queued beside this LK: the
     //     derivative pyramids are triple-buffered (frame f in f % 3), so nothing
@@ -1471,6 +1519,15 @@ static int fe_front_lk(svo_frontend* fe, int t) {
         ph_end(fe, st0, slot);
         SVO_HIP(ctx, hipEventRecord(ev_pyr, st0));
         fe->pyr_ready = tn;
+    }
+    // SVO_FE_FAST_PRE: frame t+1's FAST detection + NMS without the box mask (the
+    // mask drops corners after NMS, so it can wait for frame t's features), on the
+    // pyramid stream once this step's emit has consumed the row words: it fills
+    // the CUs the latency-bound post-LK / stereo chain leaves, and step t+1 keeps
+    // only the box filter, scan and emit behind its LK
+    if (fe->fast_pre == 1) {
+        int rc = fe_queue_pre(fe, t + 1, st0);
+        if (rc) return rc;
     }
     return SVO_OK;
 }

@@ -85,16 +85,25 @@ def test_frontend_speculative_stereo_schedules(early, split, monkeypatch):
         _compare_step(fe, ref, st, rs, t)
 
 
-@pytest.mark.parametrize("first", ["0", "1"])
-def test_frontend_fast_first_schedule(first, monkeypatch):
-    """SVO_FE_FAST_FIRST: FAST(t) submitted ahead of LK(t) on the FAST stream (1) or
-    right behind it (0, the default) -- both against the oracle loop."""
-    monkeypatch.setenv("SVO_FE_FAST_FIRST", first)
+@pytest.mark.parametrize("bucket", [(0, 0), (50, 4)])
+@pytest.mark.parametrize("sched", ["behind", "first", "pre", "pre2", "default"])
+def test_frontend_fast_schedules(sched, bucket, monkeypatch):
+    """Where FAST(t) runs, each against the oracle loop: right behind LK(t) (the
+    default), submitted ahead of it (SVO_FE_FAST_FIRST=1), or detected without the box
+    mask during step t-1 with only the box filter + scan + emit behind LK(t)
+    (SVO_FE_FAST_PRE=1 on the pyramid stream, 2 on the FAST stream behind the
+    speculative stereo LK; the mask drops corners after NMS); and the default."""
+    if sched == "default":
+        monkeypatch.delenv("SVO_FE_FAST_FIRST", raising=False)
+        monkeypatch.delenv("SVO_FE_FAST_PRE", raising=False)
+    else:
+        monkeypatch.setenv("SVO_FE_FAST_FIRST", "1" if sched == "first" else "0")
+        monkeypatch.setenv("SVO_FE_FAST_PRE", {"pre": "1", "pre2": "2"}.get(sched, "0"))
     ctx = S.Context(0)
     W, H, N, T = 640, 376, 800, 8
-    fe = make_frontend(ctx, [Scene(W, H, seed=7)], T, N)
+    fe = make_frontend(ctx, [Scene(W, H, seed=7)], T, N, bucket_size=bucket[0], per_bucket=bucket[1])
     fe.init(0)
-    ref = OracleLoop(Scene(W, H, seed=7), N).init(0)
+    ref = OracleLoop(Scene(W, H, seed=7), N, bucket=bucket).init(0)
     for t in range(1, T):
         st = fe.step(t).as_dict()
         rs = ref.step(t)
