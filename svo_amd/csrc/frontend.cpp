@@ -941,7 +941,7 @@ int svo_frontend_create(svo_ctx* ctx, const svo_frontend_config* cfg, svo_fronte
         const char* ff = std::getenv("SVO_FE_FAST_FIRST");
         fe->fast_first = ff && ff[0] == '1';
         const char* fp = std::getenv("SVO_FE_FAST_PRE");
-        fe->fast_pre = fp && fp[0] ? std::max(0, std::min(2, std::atoi(fp))) : 0;
+        fe->fast_pre = fp && fp[0] ? std::max(0, std::min(2, std::atoi(fp))) : 1;
         const char* pp = std::getenv("SVO_FE_PIPE");
         fe->pipe = !(pp && pp[0] == '0');
         const char* sm = std::getenv("SVO_FE_SPEC_MARGIN");
