@@ -79,6 +79,46 @@ def dist_setup():
     return world, rank, local, dist
 
 
+def _free_port() -> int:
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(n: int, argv) -> int:
+    """`bench.py --gpus N` started without a launcher (no WORLD_SIZE in the env):
+    start N child processes of this script, one per GPU, with the env
+    torch.distributed.run would give them (RANK / LOCAL_RANK / WORLD_SIZE /
+    LOCAL_WORLD_SIZE / MASTER_*; rendezvous on 127.0.0.1), and exit with the
+    worst child status. This process never touches the GPU (no HIP call before
+    the children start, no exec), so the children own the devices."""
+    import subprocess
+    port = os.environ.get("MASTER_PORT") or str(_free_port())
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv), env=env))
+    # a rank that fails leaves the others waiting in a barrier: end them too
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            c = p.poll()
+            if c is None:
+                continue
+            live.remove(p)
+            if c != 0 and rc == 0:
+                rc = c if c > 0 else 1
+                for q in live:
+                    q.terminate()
+        time.sleep(0.05)
+    return rc
+
+
 def sequence_seeds(rank: int, per_gpu: int):
     """Seeds of the independent sequences this rank owns (disjoint across ranks)."""
     return [rank * per_gpu + s + 1 for s in range(per_gpu)]
@@ -134,7 +174,12 @@ def cpu_baseline(cfg_name: str, seconds: float):
     from oracle_loop import OracleLoop  # noqa: E402
     from svo_amd.scene import Scene
     W, H, N, _, _ = CONFIGS[cfg_name]
-    cores = int(os.environ.get("OMP_NUM_THREADS", "0")) or (os.cpu_count() or 1)
+    # every CPU this process may run on (the rank's share of the node), not
+    # OMP_NUM_THREADS: SURVEY §8(d) asks for LK over all host cores
+    try:
+        cores = len(os.sched_getaffinity(0))
+    except AttributeError:
+        cores = os.cpu_count() or 1
 
     def run(threads, secs):
         O.set_threads(threads)
@@ -153,6 +198,7 @@ def cpu_baseline(cfg_name: str, seconds: float):
     n1, dt1 = run(1, seconds)
     O.set_threads(cores)
     return {"value": round(n / dt, 3), "unit": "frames/s", "cores": cores, "kind": "port",
+            "nproc": os.cpu_count(), "omp_num_threads_env": os.environ.get("OMP_NUM_THREADS"),
             "sample": f"{n} stereo frames of one {W}x{H} sequence, {N} feats, {dt:.1f} s; oracle/ C restatement "
                       f"of the OpenCV path (LK OpenMP over {cores} threads, FAST/PnP/triangulation single-thread)",
             "single_thread": {"value": round(n1 / dt1, 3), "cores": 1,
@@ -169,7 +215,6 @@ def main():
     ap.add_argument("--seq", type=int, default=64, help="independent sequences per GPU (batched launches)")
     ap.add_argument("--config", default="kitti", choices=sorted(CONFIGS))
     ap.add_argument("--threads", type=int, default=0, help="host RANSAC threads (0 = auto)")
-    ap.add_argument("--groups", type=int, default=0, help="pipeline slices of the batch (0 = auto)")
     ap.add_argument("--timing", type=int, default=2, choices=(0, 1, 2),
                     help="phase events: 1 all phases, 2 only LK/pyramid/FAST (lighter host tail)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
@@ -177,9 +222,26 @@ def main():
     ap.add_argument("--no-single", action="store_true")
     ap.add_argument("--no-bucketed", action="store_true",
                     help="skip the second measurement with bucketed selection in the loop")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="set up the ranks, print each rank's shard and exit (no GPU call)")
     args = ap.parse_args()
 
+    if args.gpus < 1:
+        ap.error("--gpus must be >= 1")
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
     world, rank, local, dist = dist_setup()
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but the launcher started {world} ranks")
+    if args.dry_run:
+        seeds = sequence_seeds(rank, args.seq)
+        barrier(dist)
+        tot = allreduce_sum(dist, float(len(seeds)))
+        print(json.dumps({"rank": rank, "local_rank": local, "world": world, "seeds": seeds,
+                          "total_sequences": int(tot)}), flush=True)
+        if dist is not None:
+            dist.destroy_process_group()
+        return
     import svo_amd as S
     from svo_amd.scene import Scene
 
@@ -202,7 +264,7 @@ def main():
     # t mod P; rendering is host work outside the timing, all T frames resident)
     P = min(T, 2 * scenes[0].period)
     cfg = S.FrontendConfig(W, H, scenes[0].K, n_seq=Sq, n_frames=T, n_features=N, max_level=ML,
-                           host_threads=args.threads, timing=args.timing, groups=args.groups)
+                           host_threads=args.threads, timing=args.timing)
     fe = S.Frontend(ctx, cfg)
     pairs0 = None
     keep_pairs = not args.no_bucketed and world == 1
@@ -223,20 +285,24 @@ def main():
     except (AttributeError, S.SvoError):  # an older library under SVO_GPU_LIB A/B
         host_cpus = []
     feats_after = {}  # features after step t = the inputs of LK(t + 1)
-    tracked_at = {}  # tracked points of step t = the inputs of LK(t + 1) when it runs ahead
     for t in range(1, Wm + 1):
         st = fe.step(t).as_dict()
-        feats_after[t], tracked_at[t] = st["features"], st["tracked"]
+        feats_after[t] = st["features"]
     fe.reset_times()
     tot = {"lk_iterations": 0, "tracked": 0, "inliers": 0, "added": 0, "hypotheses": 0,
            "host_ms_hyp": 0.0, "host_ms_fit": 0.0, "host_ms_wait": 0.0}
+    step_s = []  # host wall time of each timed step (a slow run shows whether one step or all were slow)
     barrier(dist)
     t0 = time.perf_counter()
+    tp = t0
     for t in range(Wm + 1, Wm + K + 1):
         st = fe.step(t).as_dict()
+        now = time.perf_counter()
+        step_s.append(now - tp)
+        tp = now
         for k in tot:
             tot[k] += st[k]
-        feats_after[t], tracked_at[t] = st["features"], st["tracked"]
+        feats_after[t] = st["features"]
     fe.synchronize()  # the last step's pose fits / prefetched pyramid belong to the timed work
     barrier(dist)
     dt = time.perf_counter() - t0
@@ -252,35 +318,21 @@ def main():
     # after reset_times bracket the LK launches of the last lk_n timed steps
     # (step Wm+1's LK went out during the warm-up); LK(t) tracks the features left
     # after step t-1, so those launches processed feats_after[t-1] features each.
-    # (with G pipeline slices a step's LK is G launches, one per slice of the batch)
     lk_ms, lk_n = phases["lk"]
     L = ML + 1
     last = Wm + K
-    G = max(1, min(args.groups, Sq)) if args.groups > 0 else 1
-    lk_steps = lk_n // G
-    # LK ahead (one slice, SVO_FE_AHEAD=1): LK(t) is queued at step t-1, over its
-    # tracked points (the appended features go in a separate small launch, phase
-    # "lk_new"), so the timed launches are those of steps Wm+2 .. last
-    ahead = G == 1 and os.environ.get("SVO_FE_AHEAD", "0")[:1] == "1"
-    src = tracked_at if ahead else feats_after
-    lk_units = sum(src[t - 1] for t in range(last - lk_steps + 1, last + 1)) if lk_steps > 0 else 0
-    assert lk_steps <= K and lk_n % G == 0, "LK launches timed do not match the steps"
+    lk_units = sum(feats_after[t - 1] for t in range(last - lk_n + 1, last + 1)) if lk_n > 0 else 0
+    assert lk_n <= K, "LK launches timed do not match the steps"
     units_per_launch = lk_units / max(lk_n, 1)
     bytes_per_launch = units_per_launch * lk_bytes_per_feature(L)
     lk_avg_s = lk_ms / max(lk_n, 1) / 1e3
     achieved = bytes_per_launch / lk_avg_s / 1e9 if lk_avg_s > 0 else 0.0
     # the 21x21 temporal call runs lk_multi_kernel<4, 1 (four features per wave)
-    # unless SVO_LK_QUAD=0 (lk_fast_kernel, one per wave) or SVO_LK_MULTI picks
-    # another several-per-wave kernel (svo_amd/csrc/lk.hip launch_lk)
-    multi = os.environ.get("SVO_LK_MULTI", "41")
+    # unless SVO_LK_QUAD=0 (lk_fast_kernel, one per wave; svo_amd/csrc/lk.hip launch_lk)
     if os.environ.get("SVO_LK_QUAD", "1")[:1] == "0":
         lk_name, lk_desc = "lk_fast_kernel<21, 21", "one feature per wave"
     else:
-        lk_name, lk_desc = {"0": ("lk_dual_kernel<21, 21", "two features per wave"),
-                            "2": ("lk_multi_kernel<2, 3", "two features per wave"),
-                            "42": ("lk_multi_kernel<4, 2", "four features per wave"),
-                            "43": ("lk_multi_kernel<4, 3", "four features per wave")}.get(
-            multi, ("lk_multi_kernel<4, 1", "four features per wave"))
+        lk_name, lk_desc = "lk_multi_kernel<4, 1", "four features per wave"
     traffic = pmc_traffic(args.config, lk_name)
     dominant = max(phases, key=lambda k: phases[k][0])
     # pyramid + Scharr of one new left frame per sequence per step (the launch
@@ -351,13 +403,15 @@ def main():
         "data": "synthetic (rendered KITTI-size frames, seeded; no dataset on the box)",
         "config": {"workload": label, "sequences_per_gpu": Sq, "global_batch": Sq * world,
                    "features": N, "win": 21, "max_level": ML, "parallelism": f"{world} x independent sequences",
-                   "groups": args.groups, "host_cpus_rank0": len(host_cpus)},
+                   "host_cpus_rank0": len(host_cpus)},
         "lk_iters_per_s": round(lk_iters_total / dt_max, 1),
         "achieved_GBps_algorithmic": round(frames * frame_bytes(W, H, N, ML) / dt_max / 1e9, 2),
         "single_stream_fps": round(single, 2) if single else None,
         "bucketed": bucketed,
         "phase_ms_per_step": {k: round(v[0] / K, 4) for k, v in phases.items()},
         "stats_per_step": {k: round(v / K, 3) for k, v in tot.items()},
+        "step_ms": {"median": round(float(np.median(step_s)) * 1e3, 4), "p90": round(float(np.percentile(step_s, 90)) * 1e3, 4),
+                    "max": round(max(step_s) * 1e3, 4), "min": round(min(step_s) * 1e3, 4)},
         "roofline": {
             "kernel": f"{lk_name}> (temporal LK 21x21, all levels, {lk_desc})",
             "dominant_phase": dominant,

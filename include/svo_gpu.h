@@ -225,10 +225,17 @@ int svo_refine_poses(svo_ctx* ctx, const double* obj_xyz, const float* img_xy, c
  * lockstep: every kernel launch covers the whole batch, all state (left / right
  * pyramids, features, map points) stays in HBM, and only the RANSAC minimal solver
  * (EPnP) and the final SQPnP-objective fit run on the host between GPU launches.
- * Every frame is a keyframe whose new features top the set up to n_features: the
- * first (n_features - n) masked FAST corners are matched in the right image (stereo
- * LK), filtered (status, |yR - yL| < y_threshold), triangulated with P_left /
- * P_right (z > 0) and moved to the world frame by the frame's estimated pose. */
+ * A keyframe's new features are the first (n_features - n) masked FAST corners,
+ * matched in the right image (stereo LK), filtered (status, |yR - yL| <
+ * y_threshold), triangulated with P_left / P_right (z > 0) and moved to the world
+ * frame by the frame's estimated pose. Which frames are keyframes: keyframe_rule
+ * SVO_KF_EVERY (every frame, topping the set up to n_features: the benchmark's
+ * upper bound) or SVO_KF_REFERENCE (Tracking::nextFrame, R:src/tracking.cpp:68-69:
+ * frame 0, and a frame whose predecessor was no keyframe and kept fewer than
+ * features_to_track features; it takes every masked corner, n_features being
+ * the feature capacity). */
+#define SVO_KF_EVERY 0
+#define SVO_KF_REFERENCE 1
 typedef struct svo_frontend svo_frontend;
 
 typedef struct svo_frontend_config {
@@ -253,9 +260,8 @@ typedef struct svo_frontend_config {
     double K[9];            /* camera matrix (float-rounded, as the Matx33f K) */
     int host_threads;       /* RANSAC host threads; 0 = auto */
     int timing;             /* 1 = per-phase HIP events; 2 = only LK, pyramid, FAST */
-    int groups;             /* pipeline groups: the batch is split into this many
-                               slices whose LK / RANSAC overlap (host RANSAC of one
-                               slice while the GPU tracks the next); 0 = auto */
+    int keyframe_rule;      /* SVO_KF_EVERY (default) or SVO_KF_REFERENCE */
+    int features_to_track;  /* SVO_KF_REFERENCE threshold, R:configs/config.yaml:15 -> 70 */
     /* stereo keyframe path (R:src/tracking.cpp:94-152) */
     float P_left[12];       /* mProjectionMatrixLeft (KITTI calib P2, R:src/main.cpp:25-28), row-major 3x4 */
     float P_right[12];      /* mProjectionMatrixRight (P3, :29-32) */
@@ -276,6 +282,7 @@ typedef struct svo_frontend_stats {
     double host_ms_hyp;     /* host wall time generating hypotheses (EPnP) */
     double host_ms_fit;     /* host wall time in the final fits */
     double host_ms_wait;    /* host wall time blocked on the GPU */
+    int64_t keyframes;      /* sequences whose frame was a keyframe this step */
 } svo_frontend_stats;
 
 int svo_frontend_create(svo_ctx* ctx, const svo_frontend_config* cfg, svo_frontend** out);
@@ -304,7 +311,8 @@ int svo_frontend_features(svo_frontend* fe, int seq, float* xy, int cap, int* n)
 int svo_frontend_map_points(svo_frontend* fe, int seq, double* xyz, int cap, int* n);
 /* Accumulated per-phase device time (ms) and launch counts since create/reset:
  * phases: 0 pyramid (left + Scharr), 1 lk, 2 post_lk, 3 stereo_lk, 4 pnp_score,
- * 5 tail, 6 fast, 7 bucket, 8 append, 9 pyramid_right. Returns the number of phases. */
+ * 5 tail (keyframe), 6 fast, 7 bucket, 8 append, 9 pyramid_right. Returns the number
+ * of phases. */
 int svo_frontend_phase_times(svo_frontend* fe, double* ms, int64_t* launches, int cap);
 void svo_frontend_reset_times(svo_frontend* fe);
 /* The Scharr derivatives (svo_image_scharr_level's layout) of frame t of sequence

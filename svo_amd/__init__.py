@@ -468,10 +468,16 @@ class Context:
         return rc == 1, rvec, tvec, inl[: ninl.value].copy()
 
 
+KF_EVERY, KF_REFERENCE = 0, 1  # SVO_KF_EVERY / SVO_KF_REFERENCE
+
+
 class FrontendConfig(C.Structure):
     """svo_frontend_config (include/svo_gpu.h); defaults = the reference's
     temporal-tracking call (R:src/tracking.cpp:157-165), FAST params
-    (R:configs/config.yaml:29-32) and solvePnPRansac args (:191-196)."""
+    (R:configs/config.yaml:29-32), solvePnPRansac args (:191-196) and
+    features_to_track (R:configs/config.yaml:15). keyframe_rule: KF_EVERY (every
+    frame a keyframe topping the set up to n_features; the benchmark) or
+    KF_REFERENCE (Tracking::nextFrame's rule, R:src/tracking.cpp:68-69)."""
     _fields_ = [
         ("width", C.c_int), ("height", C.c_int), ("n_seq", C.c_int), ("n_frames", C.c_int),
         ("n_features", C.c_int), ("max_level", C.c_int), ("win", C.c_int), ("lk_max_count", C.c_int),
@@ -479,7 +485,7 @@ class FrontendConfig(C.Structure):
         ("fast_threshold", C.c_int), ("fast_nonmax", C.c_int), ("mask_half", C.c_float),
         ("bucket_size", C.c_int), ("per_bucket", C.c_int), ("pnp_iterations", C.c_int),
         ("pnp_reproj", C.c_float), ("pnp_confidence", C.c_double), ("K", C.c_double * 9),
-        ("host_threads", C.c_int), ("timing", C.c_int), ("groups", C.c_int),
+        ("host_threads", C.c_int), ("timing", C.c_int), ("keyframe_rule", C.c_int), ("features_to_track", C.c_int),
         ("P_left", C.c_float * 12), ("P_right", C.c_float * 12), ("y_threshold", C.c_float),
         ("stereo_win", C.c_int), ("stereo_max_level", C.c_int), ("stereo_max_count", C.c_int),
         ("stereo_epsilon", C.c_double),
@@ -493,7 +499,8 @@ class FrontendConfig(C.Structure):
         d = dict(max_level=3, win=21, lk_max_count=50, lk_epsilon=1e-3, min_eig=1e-4,
                  lk_flags=LK_GET_MIN_EIGENVALS, fast_threshold=20, fast_nonmax=1, mask_half=10.0,
                  bucket_size=0, per_bucket=0, pnp_iterations=100, pnp_reproj=8.0, pnp_confidence=0.999,
-                 host_threads=0, timing=0, groups=0, y_threshold=40.0, stereo_win=11, stereo_max_level=3,
+                 host_threads=0, timing=0, keyframe_rule=KF_EVERY, features_to_track=70, y_threshold=40.0,
+                 stereo_win=11, stereo_max_level=3,
                  stereo_max_count=30, stereo_epsilon=1e-3)
         d.update(kw)
         self.width, self.height, self.n_seq, self.n_frames, self.n_features = width, height, n_seq, n_frames, n_features
@@ -510,15 +517,15 @@ class FrontendConfig(C.Structure):
 class FrontendStats(C.Structure):
     _fields_ = [("lk_iterations", C.c_int64), ("tracked", C.c_int64), ("inliers", C.c_int64),
                 ("added", C.c_int64), ("features", C.c_int64), ("hypotheses", C.c_int64),
-                ("host_ms_hyp", C.c_double), ("host_ms_fit", C.c_double), ("host_ms_wait", C.c_double)]
+                ("host_ms_hyp", C.c_double), ("host_ms_fit", C.c_double), ("host_ms_wait", C.c_double),
+                ("keyframes", C.c_int64)]
 
     def as_dict(self):
         return {k: (float(getattr(self, k)) if k.startswith("host_") else int(getattr(self, k)))
                 for k, _ in self._fields_}
 
 
-PHASES = ["pyramid", "lk", "post_lk", "stereo_lk", "pnp_score", "tail", "fast", "bucket", "append", "pyramid_right",
-          "lk_new"]
+PHASES = ["pyramid", "lk", "post_lk", "stereo_lk", "pnp_score", "tail", "fast", "bucket", "append", "pyramid_right"]
 
 
 class Frontend:

@@ -422,14 +422,7 @@ int svo_calc_optical_flow_pyr_lk(svo_ctx* ctx, const svo_image* prev, const svo_
     p.flags = flags;
     p.min_eig = (float)min_eig_threshold;
     p.want_err = err ? 1 : 0;
-    // test hook: SVO_LK_GENERIC=1 routes every window through the runtime-size kernel
-    const char* gen = std::getenv("SVO_LK_GENERIC");
-    p.generic = gen && gen[0] == '1' ? 1 : 0;
-    // SVO_LK_QUAD=0: one feature per wave for 21x21 too (tests compare both)
-    const char* quad = std::getenv("SVO_LK_QUAD");
-    p.quad = quad && quad[0] == '0' ? 0 : 1;
-    const char* multi = std::getenv("SVO_LK_MULTI");
-    if (multi) p.multi = std::atoi(multi);
+    lk_apply_env(p);
     // derivative pyramid of prev (calcSharrDeriv per level), then LK
     size_t doff[kMaxLevels];
     int dpitch[kMaxLevels];

@@ -137,22 +137,12 @@ struct FastDetBatch {
     // nullable [s][npx]: fast_detect_q_kernel writes the score of every kept corner
     // there, so the emit pass reads one byte instead of re-scoring from the image
     uint8_t* score_map = nullptr;
-    // speculative stereo input, filled by the scan / emit passes (StereoPrepBatch's
-    // rule, frontend.hpp): spec_n[s] = min(max(spec_target - spec_tracked[s] +
-    // spec_margin, 0), corners, cap), clamped to spec_cap and spec_map_cap -
-    // spec_map_n[s]; emit copies the first spec_n[s] corners to spec_xy + 2 * s *
-    // spec_cap. Null spec_n: off.
-    const int* spec_tracked = nullptr;
-    const int* spec_map_n = nullptr;
-    int spec_target = 0, spec_margin = 0, spec_cap = 0, spec_map_cap = 0;
-    float* spec_xy = nullptr;
-    int* spec_n = nullptr;
 };
-// stage: 0 detect + scan + emit, 1 detect only (the row counts are cleared first),
-// 2 scan + emit of a detection already queued
-// kFastBoxes: the detection already ran without the box mask (kFastDetect with no
-// box_pts): AND the rasterised boxes into its row words, recount, scan + emit
-constexpr int kFastAll = 0, kFastDetect = 1, kFastCollect = 2, kFastBoxes = 3;
+// stage: kFastAll detect + scan + emit, kFastDetect detect only (the row counts
+// are cleared first); kFastBoxes: the detection already ran without the box mask
+// (kFastDetect with no box_pts): AND the rasterised boxes into its row words,
+// recount, scan + emit
+constexpr int kFastAll = 0, kFastDetect = 1, kFastBoxes = 3;
 // ints of band-offset scratch per sequence for an image of height h
 // Box centres are binned by cell: 16-row band x 64-column tile (the FAST tile
 // grid), cell-major per band; [s][cells + 1] offsets.
@@ -203,9 +193,11 @@ struct LKParams {
     float min_eig;
     int want_err;
     int generic = 0;  // 1: always use the runtime-window kernel (tests compare both)
-    int quad = 1;     // 21x21: several features per wave; 0: one per wave (lk_fast_kernel)
-    int multi = 41;   // 21x21 several-per-wave kernel (SVO_LK_MULTI, see launch_lk)
+    int quad = 1;     // 21x21: four features per wave; 0: one per wave (lk_fast_kernel)
 };
+// A/B and test hooks of the kernel choice, read per call: SVO_LK_GENERIC=1 (the
+// runtime-window kernel for every window), SVO_LK_QUAD=0 (21x21 one per wave)
+void lk_apply_env(LKParams& p);
 // Batched LK: blockIdx.y = sequence; sequence s owns points [s*cap, s*cap + n_s)
 // of every array, n_s = counts[s] (device) or n when counts is null.
 struct LKBatch {

@@ -197,204 +197,20 @@ __global__ __launch_bounds__(256) void fast_write_kernel(FastBatch B, int w, int
     }
 }
 
-// ---- fused detection: FAST-9 + score + NMS + mask for a 64x16 tile (scores
-// of a 1-pixel halo recomputed), one 64-bit keep mask per (row, 64-px segment)
-// and per-row counts (integer atomics) ----
+// ---- fused detection (fast_detect_q_kernel): FAST-9 + score + NMS + box mask for
+// a 64 x TY tile of a frame, one 64-bit keep word per (row, 64-px segment) and
+// per-row counts. Each wave owns every 4th row of the tile's score region (the
+// tile and a 1-pixel halo, whose scores NMS needs) and runs, with no block
+// barrier, (A0) the compass pre-test of its rows -> a wave-private queue (ballot
+// ranks, no atomics), (A1) the full segment test of the queue, compacted in
+// place to the corners, (B) their cornerScore with packed 16-bit min/max (the
+// a-chain in the low halves, the negated b-chain in the high ones). One barrier,
+// then NMS over the wave's corners only, the box mask ANDed into the finished
+// row words. ----
 constexpr int FD_TX = 64, FD_TY = 32;
-constexpr int FD_SW = FD_TX + 2, FD_SH = FD_TY + 2;  // score region (halo 1)
-constexpr int FD_IW = FD_TX + 8, FD_IH = FD_TY + 8;  // image region (halo 4)
-
-__global__ __launch_bounds__(256) void fast_detect_kernel(FastDetBatch B, int threshold, int nonmax) {
-    const ImgLevel L = B.descs[blockIdx.z].lv[0];
-    const int w = L.w, h = L.h;
-    const int x0 = blockIdx.x * FD_TX, y0 = blockIdx.y * FD_TY;
-    const size_t seq = blockIdx.z;
-    __shared__ uint8_t T[FD_IH][FD_IW];
-    __shared__ uint16_t SC[FD_SH][FD_SW + 2];  // bit 8: corner, low byte: score
-    const int tid = threadIdx.x;
-    const bool inside = x0 >= 4 && y0 >= 4 && x0 - 4 + FD_IW <= w && y0 - 4 + FD_IH <= h;
-    if (inside) {
-        for (int k = tid; k < FD_IH * (FD_IW / 4); k += 256) {
-            const int r = k / (FD_IW / 4), c4 = k - r * (FD_IW / 4);
-            const uint8_t* src = L.data + (size_t)(y0 - 4 + r) * L.pitch + (x0 - 4 + 4 * c4);
-            // x0 - 4 is a multiple of 4 and pitch is a multiple of 64: aligned dword
-            *reinterpret_cast<uint32_t*>(&T[r][4 * c4]) = *reinterpret_cast<const uint32_t*>(src);
-        }
-    } else {
-        for (int k = tid; k < FD_IH * FD_IW; k += 256) {
-            const int r = k / FD_IW, c = k - r * FD_IW;
-            const int y = y0 - 4 + r, x = x0 - 4 + c;
-            T[r][c] = ((unsigned)y < (unsigned)h && (unsigned)x < (unsigned)w) ? L.data[(size_t)y * L.pitch + x] : 0;
-        }
-    }
-    __syncthreads();
-    // phase A0: OpenCV FAST_t's first pre-test as a necessary condition: a 9-arc
-    // of the 16-ring holds one pixel of each antipodal pair, so a corner has
-    // (b0 | b8) & (b4 | b12) for "brighter" or the same for "darker" on the
-    // compass pixels. Only survivors (a small fraction: flat areas and straight
-    // edges fail) are queued for the full 16-pixel test, which then runs with
-    // full waves (phase A1); corners are queued again for the score (phase B).
-    constexpr int NSC = FD_SH * FD_SW;
-    __shared__ uint16_t CQ[NSC], CQ1[NSC];
-    __shared__ int ncq, ncq1;
-    if (tid == 0) ncq = ncq1 = 0;
-    __syncthreads();
-    for (int base = 0; base < NSC; base += 256) {
-        const int k = base + tid;
-        const int r = k / FD_SW, c = k - r * FD_SW;
-        const int y = y0 - 1 + r, x = x0 - 1 + c;
-        bool cand = false;
-        if (k < NSC && x >= 3 && x < w - 3 && y >= 3 && y < h - 3) {
-            const int ty = r + 3, tx = c + 3;
-            const int v = T[ty][tx], hi = v + threshold, lo = v - threshold;
-            const int p0 = T[ty + 3][tx], p8 = T[ty - 3][tx], p4 = T[ty][tx + 3], p12 = T[ty][tx - 3];
-            const bool bright = (p0 > hi || p8 > hi) && (p4 > hi || p12 > hi);
-            const bool dark = (p0 < lo || p8 < lo) && (p4 < lo || p12 < lo);
-            cand = bright || dark;
-        }
-        if (k < NSC) SC[r][c] = 0;
-        const unsigned long long bal = __ballot(cand);
-        if (bal) {
-            int qb = 0;
-            if ((tid & 63) == 0) qb = atomicAdd(&ncq1, __popcll(bal));
-            qb = __builtin_amdgcn_readfirstlane(qb);
-            if (cand) CQ1[qb + __popcll(bal & ((1ull << (tid & 63)) - 1ull))] = (uint16_t)k;
-        }
-    }
-    __syncthreads();
-    // phase A1: full segment test of the candidates
-    const int nq1 = ncq1;
-    for (int base = 0; base < nq1; base += 256) {
-        const int i = base + tid;
-        bool corner = false;
-        int k = 0;
-        if (i < nq1) {
-            k = CQ1[i];
-            const int r = k / FD_SW, c = k - r * FD_SW;
-            const int ty = r + 3, tx = c + 3;
-            const int v = T[ty][tx];
-            unsigned bright = 0, dark = 0;
-#pragma unroll
-            for (int q = 0; q < 16; q++) {
-                const int rv = T[ty + c_ring[q][1]][tx + c_ring[q][0]];
-                bright |= (unsigned)(rv > v + threshold) << q;
-                dark |= (unsigned)(rv < v - threshold) << q;
-            }
-            corner = run9(bright) || run9(dark);
-            if (corner) {
-                const int r2 = k / FD_SW, c2 = k - r2 * FD_SW;
-                SC[r2][c2] = 0x100;
-            }
-        }
-        if (nonmax) {
-            const unsigned long long bal = __ballot(corner);
-            if (bal) {
-                int qb = 0;
-                if ((tid & 63) == 0) qb = atomicAdd(&ncq, __popcll(bal));
-                qb = __builtin_amdgcn_readfirstlane(qb);
-                if (corner) CQ[qb + __popcll(bal & ((1ull << (tid & 63)) - 1ull))] = (uint16_t)k;
-            }
-        }
-    }
-    __syncthreads();
-    // phase B: cornerScore of the queued corners, dense
-    if (nonmax) {
-        const int nq = ncq;
-        for (int i = tid; i < nq; i += 256) {
-            const int k = CQ[i];
-            const int r = k / FD_SW, c = k - r * FD_SW;
-            const int ty = r + 3, tx = c + 3;
-            const int v = T[ty][tx];
-            int ring[16];
-#pragma unroll
-            for (int q = 0; q < 16; q++) ring[q] = T[ty + c_ring[q][1]][tx + c_ring[q][0]];
-            SC[r][c] = (uint16_t)(0x100 | corner_score16(v, ring, threshold));
-        }
-    }
-    // tile mask from the previous frame's feature boxes (R:src/tracking.cpp:76-79,
-    // cv::rectangle FILLED with cvRound corners, clipped): one bit per pixel of
-    // the 64x16 tile, cleared by every box that overlaps it -- no W x H mask in HBM
-    __shared__ unsigned long long TM[FD_TY];
-    const bool boxes = B.box_pts != nullptr;
-    if (boxes) {
-        if (tid < FD_TY) TM[tid] = ~0ull;
-        __syncthreads();
-        // only the cells (16-row band x 64-column tile) whose box centres can reach this tile
-        const int nb = (h + 15) / 16, nc = (w + 63) / 64;
-        const int* __restrict__ cells = B.box_band + seq * (size_t)(nb * nc + 1);
-        const int b0 = max(0, (int)floorf((y0 - B.box_half - 1.f) / 16.f));
-        const int b1 = min(nb - 1, (int)floorf((y0 + FD_TY + B.box_half + 1.f) / 16.f));
-        const int cb0 = max(0, (int)floorf((x0 - B.box_half - 1.f) / 64.f));
-        const int cb1 = min(nc - 1, (int)floorf((x0 + FD_TX + B.box_half + 1.f) / 64.f));
-        const float* __restrict__ pts = B.box_binned + 2 * seq * (size_t)B.box_stride;
-        for (int bq = b0; bq <= b1; bq++)
-        for (int i = cells[bq * nc + cb0] + tid, i1 = cells[bq * nc + cb1 + 1]; i < i1; i += 256) {
-            const float px = pts[2 * i], py = pts[2 * i + 1];
-            const int xa = (int)__builtin_rintf(px - B.box_half), ya = (int)__builtin_rintf(py - B.box_half);
-            const int xb = (int)__builtin_rintf(px + B.box_half), yb = (int)__builtin_rintf(py + B.box_half);
-            int xl = min(xa, xb), xr = max(xa, xb), yt = min(ya, yb), yd = max(ya, yb);
-            xl = max(xl, max(0, x0));
-            xr = min(xr, min(w - 1, x0 + FD_TX - 1));
-            yt = max(yt, max(0, y0));
-            yd = min(yd, min(h - 1, y0 + FD_TY - 1));
-            if (xl > xr || yt > yd) continue;
-            const int c0 = xl - x0, c1 = xr - x0;  // 0..63
-            const unsigned long long span =
-                (c1 - c0 == 63) ? ~0ull : (((1ull << (c1 - c0 + 1)) - 1ull) << c0);
-            for (int y = yt; y <= yd; y++) atomicAnd(&TM[y - y0], ~span);
-        }
-    }
-    __syncthreads();
-    const int lane = tid & 63, wv = tid >> 6;
-    const int x = x0 + lane;
-    const uint8_t* __restrict__ mask = B.mask ? B.mask + seq * B.npx : nullptr;
-    // per row: the keep bits of the tile's 64 columns; one wave then writes all
-    // rows' bit words and count atomics with single vector instructions
-    __shared__ unsigned long long RB[FD_TY];
-#pragma unroll
-    for (int i = 0; i < FD_TY / 4; i++) {
-        const int r = wv * (FD_TY / 4) + i;
-        const int y = y0 + r;
-        const int c = lane + 1, rr = r + 1;
-        const unsigned v = SC[rr][c];
-        bool keep = (v & 0x100) != 0 && x < w && y < h;
-        if (nonmax) {
-            // strict maximum over the 8 neighbours' score bytes (non-corners score 0),
-            // branch-free: byte reads of the low halves + max3
-            auto sb = [&](int y2, int x2) { return (int)reinterpret_cast<const uint8_t*>(&SC[y2][x2])[0]; };
-            int m = max(max(sb(rr, c - 1), sb(rr, c + 1)), sb(rr - 1, c - 1));
-            m = max(max(m, sb(rr - 1, c)), sb(rr - 1, c + 1));
-            m = max(max(m, sb(rr + 1, c - 1)), sb(rr + 1, c));
-            m = max(m, sb(rr + 1, c + 1));
-            keep = keep && (int)(v & 0xFF) > m;
-        }
-        if (mask) {  // host mask (svo_fast_detect): runByPixelsMask
-            const int yy = y < h ? y : h - 1, xx = x < w ? x : w - 1;
-            keep = keep && mask[(size_t)yy * w + xx] != 0;
-        }
-        if (boxes) keep = keep && ((TM[r] >> lane) & 1ull);
-        const unsigned long long bal = __ballot(keep);
-        if (lane == 0) RB[r] = bal;
-    }
-    __syncthreads();
-    if (tid < FD_TY && y0 + tid < h) {
-        const unsigned long long bal = RB[tid];
-        const size_t row = seq * h + y0 + tid;
-        B.bits[row * B.nseg + blockIdx.x] = bal;
-        if (bal) atomicAdd(&B.rowcnt[row], __popcll(bal));
-    }
-}
-
-// ---- fused detection, wave-private form: each wave owns every 4th row of the
-// tile's score region (34 x 66: the 64 x 32 tile and a 1-pixel halo, whose
-// scores NMS needs) and runs, with no block barrier, (A0) the compass pre-test
-// of its rows -> a wave-private queue (ballot ranks, no atomics), (A1) the full
-// segment test of the queue, compacted in place to the corners, (B) their
-// cornerScore with packed 16-bit min/max (the a-chain in the low halves, the
-// negated b-chain in the high ones). One barrier, then NMS / box mask / output
-// exactly as fast_detect_kernel (same output arrays). ----
+constexpr int FD_SW = FD_TX + 2;  // score region columns (halo 1)
+constexpr int FD_IW = FD_TX + 8;  // staged image columns (halo 4)
 typedef short fs16x2 __attribute__((ext_vector_type(2)));
-constexpr int FW_Q = 9 * FD_SW + 8;  // queue entries per wave (<= 9 rows x 66 positions)
 
 __device__ __forceinline__ fs16x2 as_s2(unsigned v) { return __builtin_bit_cast(fs16x2, v); }
 __device__ __forceinline__ unsigned as_u(fs16x2 v) { return __builtin_bit_cast(unsigned, v); }
@@ -426,175 +242,6 @@ __device__ __forceinline__ int corner_score16_pk(int v, const int* ring, int thr
     return (max(a0, nb) - 1) & 0xFF;   // -min(-a0, B) - 1, (uchar) as FAST_t
 }
 
-__global__ __launch_bounds__(256) void fast_detect_w_kernel(FastDetBatch B, int threshold, int nonmax) {
-    const ImgLevel L = B.descs[blockIdx.z].lv[0];
-    const int w = L.w, h = L.h;
-    const int x0 = blockIdx.x * FD_TX, y0 = blockIdx.y * FD_TY;
-    const size_t seq = blockIdx.z;
-    __shared__ __attribute__((aligned(16))) uint8_t T[FD_IH][FD_IW];
-    __shared__ uint16_t SC[FD_SH][FD_SW + 2];  // bit 8: corner, low byte: score
-    __shared__ uint16_t CQ[4][FW_Q];
-    __shared__ unsigned long long TM[FD_TY];
-    __shared__ unsigned long long RB[FD_TY];
-    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-    const bool inside = x0 >= 4 && y0 >= 4 && x0 - 4 + FD_IW <= w && y0 - 4 + FD_IH <= h;
-    if (inside) {
-        for (int k = tid; k < FD_IH * (FD_IW / 4); k += 256) {
-            const int r = k / (FD_IW / 4), c4 = k - r * (FD_IW / 4);
-            const uint8_t* src = L.data + (size_t)(y0 - 4 + r) * L.pitch + (x0 - 4 + 4 * c4);
-            *reinterpret_cast<uint32_t*>(&T[r][4 * c4]) = *reinterpret_cast<const uint32_t*>(src);
-        }
-    } else {
-        for (int k = tid; k < FD_IH * FD_IW; k += 256) {
-            const int r = k / FD_IW, c = k - r * FD_IW;
-            const int y = y0 - 4 + r, x = x0 - 4 + c;
-            T[r][c] = ((unsigned)y < (unsigned)h && (unsigned)x < (unsigned)w) ? L.data[(size_t)y * L.pitch + x] : 0;
-        }
-    }
-    const bool boxes = B.box_pts != nullptr;
-    if (boxes && tid < FD_TY) TM[tid] = ~0ull;
-    __syncthreads();
-    const int hi_t = threshold, lo_t = -threshold;
-    // ---- A0: compass pre-test of this wave's rows sr = wv, wv + 4, ... (lane -> column
-    // sc = lane + 1), then the two halo columns of those rows; queue (sr << 7 | sc) ----
-    uint16_t* q = CQ[wv];
-    int nq = 0;
-    auto pretest = [&](int sr, int sc, bool ok) {
-        const int y = y0 - 1 + sr, x = x0 - 1 + sc;
-        bool cand = false;
-        if (ok && x >= 3 && x < w - 3 && y >= 3 && y < h - 3) {
-            const int ty = sr + 3, tx = sc + 3;
-            const int v = T[ty][tx], hi = v + hi_t, lo = v + lo_t;
-            const int p0 = T[ty + 3][tx], p8 = T[ty - 3][tx], p4 = T[ty][tx + 3], p12 = T[ty][tx - 3];
-            const bool bright = (p0 > hi || p8 > hi) && (p4 > hi || p12 > hi);
-            const bool dark = (p0 < lo || p8 < lo) && (p4 < lo || p12 < lo);
-            cand = bright || dark;
-        }
-        const unsigned long long bal = __ballot(cand);
-        if (cand) q[nq + __popcll(bal & ((1ull << lane) - 1ull))] = (uint16_t)((sr << 7) | sc);
-        nq += __popcll(bal);
-    };
-    for (int sr = wv; sr < FD_SH; sr += 4) {
-        SC[sr][lane + 1] = 0;
-        if (lane < 2) SC[sr][lane * 65] = 0;
-        pretest(sr, lane + 1, true);
-    }
-    {
-        // halo columns 0 and 65 of the wave's rows (<= 9 rows -> 18 positions)
-        const int nr = (FD_SH - wv + 3) / 4;
-        const int sr = wv + 4 * (lane >> 1), sc = (lane & 1) * 65;
-        pretest(sr, sc, lane < 2 * nr);
-    }
-    // ---- A1: full segment test of the queue, compacted in place to the corners ----
-    int nc = 0;
-    for (int base = 0; base < nq; base += 64) {
-        const int i = base + lane;
-        bool corner = false;
-        int k = 0;
-        if (i < nq) {
-            k = q[i];
-            const int sr = k >> 7, sc = k & 127;
-            const int ty = sr + 3, tx = sc + 3;
-            const int v = T[ty][tx];
-            // packed compare: low half r - (v + t + 1) (sign: not brighter), high half
-            // r - (v - t) (sign: darker); sign bits gathered to bit q and 16 + q
-            const fs16x2 th = {(short)(v + threshold + 1), (short)(v - threshold)};
-            unsigned acc = 0;
-#pragma unroll
-            for (int qq = 0; qq < 16; qq++) {
-                const int rv = T[ty + c_ring[qq][1]][tx + c_ring[qq][0]];
-                const fs16x2 r2 = {(short)rv, (short)rv};
-                const unsigned sg = as_u(r2 - th);
-                acc |= (sg >> (15 - qq)) & (0x00010001u << qq);
-            }
-            corner = run9(~acc & 0xFFFFu) || run9(acc >> 16);
-        }
-        const unsigned long long bal = __ballot(corner);
-        if (corner) {
-            const int sr = k >> 7, sc = k & 127;
-            SC[sr][sc] = 0x100;
-            q[nc + __popcll(bal & ((1ull << lane) - 1ull))] = (uint16_t)k;  // index <= i: already read
-        }
-        nc += __popcll(bal);
-    }
-    // ---- B: cornerScore of the corners (NMS only) ----
-    if (nonmax) {
-        for (int i = lane; i < nc; i += 64) {
-            const int k = q[i];
-            const int sr = k >> 7, sc = k & 127;
-            const int ty = sr + 3, tx = sc + 3;
-            const int v = T[ty][tx];
-            int ring[16];
-#pragma unroll
-            for (int qq = 0; qq < 16; qq++) ring[qq] = T[ty + c_ring[qq][1]][tx + c_ring[qq][0]];
-            SC[sr][sc] = (uint16_t)(0x100 | corner_score16_pk(v, ring, threshold));
-        }
-    }
-    // tile mask from the previous frame's feature boxes (as fast_detect_kernel)
-    if (boxes) {
-        const int nb = (h + 15) / 16, ncl = (w + 63) / 64;
-        const int* __restrict__ cells = B.box_band + seq * (size_t)(nb * ncl + 1);
-        const int b0 = max(0, (int)floorf((y0 - B.box_half - 1.f) / 16.f));
-        const int b1 = min(nb - 1, (int)floorf((y0 + FD_TY + B.box_half + 1.f) / 16.f));
-        const int cb0 = max(0, (int)floorf((x0 - B.box_half - 1.f) / 64.f));
-        const int cb1 = min(ncl - 1, (int)floorf((x0 + FD_TX + B.box_half + 1.f) / 64.f));
-        const float* __restrict__ pts = B.box_binned + 2 * seq * (size_t)B.box_stride;
-        for (int bq = b0; bq <= b1; bq++)
-            for (int i = cells[bq * ncl + cb0] + tid, i1 = cells[bq * ncl + cb1 + 1]; i < i1; i += 256) {
-                const float px = pts[2 * i], py = pts[2 * i + 1];
-                const int xa = (int)__builtin_rintf(px - B.box_half), ya = (int)__builtin_rintf(py - B.box_half);
-                const int xb = (int)__builtin_rintf(px + B.box_half), yb = (int)__builtin_rintf(py + B.box_half);
-                int xl = min(xa, xb), xr = max(xa, xb), yt = min(ya, yb), yd = max(ya, yb);
-                xl = max(xl, max(0, x0));
-                xr = min(xr, min(w - 1, x0 + FD_TX - 1));
-                yt = max(yt, max(0, y0));
-                yd = min(yd, min(h - 1, y0 + FD_TY - 1));
-                if (xl > xr || yt > yd) continue;
-                const int c0 = xl - x0, c1 = xr - x0;  // 0..63
-                const unsigned long long span =
-                    (c1 - c0 == 63) ? ~0ull : (((1ull << (c1 - c0 + 1)) - 1ull) << c0);
-                for (int y = yt; y <= yd; y++) atomicAnd(&TM[y - y0], ~span);
-            }
-    }
-    __syncthreads();
-    const int x = x0 + lane;
-    const uint8_t* __restrict__ mask = B.mask ? B.mask + seq * B.npx : nullptr;
-#pragma unroll
-    for (int i = 0; i < FD_TY / 4; i++) {
-        const int r = wv * (FD_TY / 4) + i;
-        const int y = y0 + r;
-        const int c = lane + 1, rr = r + 1;
-        const unsigned v = SC[rr][c];
-        bool keep = (v & 0x100) != 0 && x < w && y < h;
-        if (nonmax) {
-            auto sb = [&](int y2, int x2) { return (int)reinterpret_cast<const uint8_t*>(&SC[y2][x2])[0]; };
-            int m = max(max(sb(rr, c - 1), sb(rr, c + 1)), sb(rr - 1, c - 1));
-            m = max(max(m, sb(rr - 1, c)), sb(rr - 1, c + 1));
-            m = max(max(m, sb(rr + 1, c - 1)), sb(rr + 1, c));
-            m = max(m, sb(rr + 1, c + 1));
-            keep = keep && (int)(v & 0xFF) > m;
-        }
-        if (mask) {
-            const int yy = y < h ? y : h - 1, xx = x < w ? x : w - 1;
-            keep = keep && mask[(size_t)yy * w + xx] != 0;
-        }
-        if (boxes) keep = keep && ((TM[r] >> lane) & 1ull);
-        const unsigned long long bal = __ballot(keep);
-        if (lane == 0) RB[r] = bal;
-    }
-    __syncthreads();
-    if (tid < FD_TY && y0 + tid < h) {
-        const unsigned long long bal = RB[tid];
-        const size_t row = seq * h + y0 + tid;
-        B.bits[row * B.nseg + blockIdx.x] = bal;
-        if (bal) atomicAdd(&B.rowcnt[row], __popcll(bal));
-    }
-}
-
-// ---- queue-NMS form (SVO_FAST_V=4): as fast_detect_w_kernel up to the scores;
-// NMS then visits only the wave's corners instead of every pixel of its rows
-// (the dense pass was ~30 % of the kernel's VALU), and the box mask is applied to
-// the finished row words. Same outputs. ----
 template <int TY>
 __global__ __launch_bounds__(256) void fast_detect_q_kernel(FastDetBatch B, int threshold, int nonmax) {
     constexpr int QSH = TY + 2, QIH = TY + 8;           // score rows (halo 1), staged rows (halo 4)
@@ -705,7 +352,7 @@ __global__ __launch_bounds__(256) void fast_detect_q_kernel(FastDetBatch B, int 
             SC[sr][sc] = (uint16_t)(0x100 | corner_score16_pk(v, ring, threshold));
         }
     }
-    // tile mask from the previous frame's feature boxes (as fast_detect_kernel)
+    // tile mask from the previous frame's feature boxes
     if (boxes) {
         const int nb = (h + 15) / 16, ncl = (w + 63) / 64;
         const int* __restrict__ cells = B.box_band + seq * (size_t)(nb * ncl + 1);
@@ -811,215 +458,6 @@ __global__ __launch_bounds__(256) void fast_box_filter_kernel(FastDetBatch B, in
     }
 }
 
-// ---- SWAR form (SVO_FAST_V=3): as fast_detect_w_kernel, with the compass
-// pre-test on 4 pixels per lane and a register NMS. The staged tile starts 8
-// pixels left of the tile (T column c <-> x = x0 - 8 + c) and the score region
-// 4 pixels left (SC column xs <-> x = x0 - 4 + xs), so a pre-test item -- score
-// row sr, pixels x0 - 4 + 4j .. + 3 -- reads its centre row as three aligned
-// dwords (the +-3 compass pixels by v_alignbyte) and rows +-3 as one dword each,
-// and tests the 4 pixels with packed 16-bit min/max in two halves (bytes 0/2 and
-// 1/3): brighter <=> min(max(p0, p8), max(p4, p12)) > v + t, darker <=>
-// max(min(p0, p8), min(p4, p12)) < v - t -- the same necessary condition as the
-// other forms. NMS reads each score row's 3 neighbours once per wave and keeps
-// the row maxima in registers. Same outputs as fast_detect_kernel. ----
-constexpr int F3_IW = FD_TX + 16;  // staged columns x0 - 8 .. x0 + 71
-constexpr int F3_SW = FD_TX + 8;   // score columns x0 - 4 .. x0 + 67 (18 dwords)
-constexpr int F3_Q = 9 * F3_SW + 8;
-
-typedef unsigned short fu16x2 __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ fu16x2 as_w2(unsigned v) { return __builtin_bit_cast(fu16x2, v); }
-__device__ __forceinline__ unsigned w2_as(fu16x2 v) { return __builtin_bit_cast(unsigned, v); }
-
-// candidate bits (bit b: byte b) of 4 pixels v with compass pixels p0 (dy +3),
-// p8 (dy -3), p4 (dx +3), p12 (dx -3), all packed bytes
-__device__ __forceinline__ unsigned pretest4(unsigned v, unsigned p0, unsigned p8, unsigned p4, unsigned p12, int t) {
-    const fu16x2 t1 = {(unsigned short)(t + 1), (unsigned short)(t + 1)};
-    unsigned z[2];
-#pragma unroll
-    for (int o = 0; o < 2; o++) {  // o = 0: bytes 0, 2; o = 1: bytes 1, 3 (zero-extended)
-        const unsigned sel = o ? 0x0c030c01u : 0x0c020c00u;
-        const fu16x2 V = as_w2(__builtin_amdgcn_perm(0u, v, sel));
-        const fu16x2 A = as_w2(__builtin_amdgcn_perm(0u, p0, sel)), Bv = as_w2(__builtin_amdgcn_perm(0u, p8, sel));
-        const fu16x2 C = as_w2(__builtin_amdgcn_perm(0u, p4, sel)), Dv = as_w2(__builtin_amdgcn_perm(0u, p12, sel));
-        const fu16x2 m = __builtin_elementwise_min(__builtin_elementwise_max(A, Bv), __builtin_elementwise_max(C, Dv));
-        const fu16x2 M = __builtin_elementwise_max(__builtin_elementwise_min(A, Bv), __builtin_elementwise_min(C, Dv));
-        // sign of m - (v + t + 1): not brighter; sign of (v - t - 1) - M: not darker
-        const unsigned x = w2_as(m - (V + t1)), y = w2_as((V - t1) - M);
-        z[o] = ~(x & y);  // bit 15 / 31: candidate
-    }
-    return ((z[0] >> 15) & 1u) | ((z[1] >> 14) & 2u) | ((z[0] >> 29) & 4u) | ((z[1] >> 28) & 8u);
-}
-
-__global__ __launch_bounds__(256) void fast_detect_s_kernel(FastDetBatch B, int threshold, int nonmax) {
-    const ImgLevel L = B.descs[blockIdx.z].lv[0];
-    const int w = L.w, h = L.h;
-    const int x0 = blockIdx.x * FD_TX, y0 = blockIdx.y * FD_TY;
-    const size_t seq = blockIdx.z;
-    __shared__ __attribute__((aligned(16))) uint8_t T[FD_IH][F3_IW];
-    __shared__ uint16_t SC[FD_SH][F3_SW];  // bit 8: corner, low byte: score
-    __shared__ uint16_t CQ[4][F3_Q];
-    __shared__ unsigned long long TM[FD_TY];
-    __shared__ unsigned long long RB[FD_TY];
-    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-    const bool inside = x0 >= 8 && y0 >= 4 && x0 - 8 + F3_IW <= w && y0 - 4 + FD_IH <= h;
-    if (inside) {
-        for (int k = tid; k < FD_IH * (F3_IW / 4); k += 256) {
-            const int r = k / (F3_IW / 4), c4 = k - r * (F3_IW / 4);
-            const uint8_t* src = L.data + (size_t)(y0 - 4 + r) * L.pitch + (x0 - 8 + 4 * c4);
-            *reinterpret_cast<uint32_t*>(&T[r][4 * c4]) = *reinterpret_cast<const uint32_t*>(src);
-        }
-    } else {
-        for (int k = tid; k < FD_IH * F3_IW; k += 256) {
-            const int r = k / F3_IW, c = k - r * F3_IW;
-            const int y = y0 - 4 + r, x = x0 - 8 + c;
-            T[r][c] = ((unsigned)y < (unsigned)h && (unsigned)x < (unsigned)w) ? L.data[(size_t)y * L.pitch + x] : 0;
-        }
-    }
-    const bool boxes = B.box_pts != nullptr;
-    if (boxes && tid < FD_TY) TM[tid] = ~0ull;
-    for (int sr = wv; sr < FD_SH; sr += 4) {  // this wave's score rows
-        SC[sr][lane] = 0;
-        if (lane < F3_SW - 64) SC[sr][64 + lane] = 0;
-    }
-    __syncthreads();
-    // ---- A0: pre-test items (k-th row of the wave sr = wv + 4k, dword j) ----
-    uint16_t* q = CQ[wv];
-    int nq = 0;
-    const int nrows = (FD_SH - wv + 3) / 4, nitems = nrows * (F3_SW / 4);
-    const int lox = max(x0 - 1, 3), hix = min(x0 + FD_TX, w - 4);  // score pixels to test
-    for (int base = 0; base < nitems; base += 64) {
-        const int it = base + lane;
-        const int k = it / (F3_SW / 4), j = it - (F3_SW / 4) * k;
-        const int sr = wv + 4 * k;
-        const int y = y0 - 1 + sr;
-        unsigned cm = 0;
-        if (it < nitems && y >= 3 && y < h - 3) {
-            const int ty = sr + 3;
-            const unsigned d0 = *reinterpret_cast<const unsigned*>(&T[ty][4 * j]);
-            const unsigned d1 = *reinterpret_cast<const unsigned*>(&T[ty][4 * j + 4]);
-            const unsigned d2 = *reinterpret_cast<const unsigned*>(&T[ty][4 * j + 8]);
-            const unsigned up = *reinterpret_cast<const unsigned*>(&T[ty - 3][4 * j + 4]);
-            const unsigned dn = *reinterpret_cast<const unsigned*>(&T[ty + 3][4 * j + 4]);
-            const unsigned p12 = __builtin_amdgcn_alignbyte(d1, d0, 1);  // x - 3
-            const unsigned p4 = __builtin_amdgcn_alignbyte(d2, d1, 3);   // x + 3
-            cm = pretest4(d1, dn, up, p4, p12, threshold);
-            const int xb = x0 - 4 + 4 * j;
-            const int s0 = min(max(lox - xb, 0), 4), e0 = min(max(hix - xb + 1, 0), 4);
-            cm &= ((1u << e0) - 1u) & ~((1u << s0) - 1u);
-        }
-#pragma unroll
-        for (int b = 0; b < 4; b++) {
-            const bool c = (cm >> b) & 1u;
-            const unsigned long long bal = __ballot(c);
-            if (c) q[nq + __popcll(bal & ((1ull << lane) - 1ull))] = (uint16_t)((sr << 7) | (4 * j + b));
-            nq += __popcll(bal);
-        }
-    }
-    // ---- A1: full segment test of the queue, compacted in place to the corners ----
-    int nc = 0;
-    for (int base = 0; base < nq; base += 64) {
-        const int i = base + lane;
-        bool corner = false;
-        int k = 0;
-        if (i < nq) {
-            k = q[i];
-            const int ty = (k >> 7) + 3, tx = (k & 127) + 4;
-            const int v = T[ty][tx];
-            const fs16x2 th = {(short)(v + threshold + 1), (short)(v - threshold)};
-            unsigned acc = 0;
-#pragma unroll
-            for (int qq = 0; qq < 16; qq++) {
-                const int rv = T[ty + c_ring[qq][1]][tx + c_ring[qq][0]];
-                const fs16x2 r2 = {(short)rv, (short)rv};
-                const unsigned sg = as_u(r2 - th);
-                acc |= (sg >> (15 - qq)) & (0x00010001u << qq);
-            }
-            corner = run9(~acc & 0xFFFFu) || run9(acc >> 16);
-        }
-        const unsigned long long bal = __ballot(corner);
-        if (corner) {
-            SC[k >> 7][k & 127] = 0x100;
-            q[nc + __popcll(bal & ((1ull << lane) - 1ull))] = (uint16_t)k;  // index <= i: already read
-        }
-        nc += __popcll(bal);
-    }
-    // ---- B: cornerScore of the corners (NMS only) ----
-    if (nonmax) {
-        for (int i = lane; i < nc; i += 64) {
-            const int k = q[i];
-            const int ty = (k >> 7) + 3, tx = (k & 127) + 4;
-            const int v = T[ty][tx];
-            int ring[16];
-#pragma unroll
-            for (int qq = 0; qq < 16; qq++) ring[qq] = T[ty + c_ring[qq][1]][tx + c_ring[qq][0]];
-            SC[k >> 7][k & 127] = (uint16_t)(0x100 | corner_score16_pk(v, ring, threshold));
-        }
-    }
-    // tile mask from the previous frame's feature boxes (as fast_detect_kernel)
-    if (boxes) {
-        const int nb = (h + 15) / 16, ncl = (w + 63) / 64;
-        const int* __restrict__ cells = B.box_band + seq * (size_t)(nb * ncl + 1);
-        const int b0 = max(0, (int)floorf((y0 - B.box_half - 1.f) / 16.f));
-        const int b1 = min(nb - 1, (int)floorf((y0 + FD_TY + B.box_half + 1.f) / 16.f));
-        const int cb0 = max(0, (int)floorf((x0 - B.box_half - 1.f) / 64.f));
-        const int cb1 = min(ncl - 1, (int)floorf((x0 + FD_TX + B.box_half + 1.f) / 64.f));
-        const float* __restrict__ pts = B.box_binned + 2 * seq * (size_t)B.box_stride;
-        for (int bq = b0; bq <= b1; bq++)
-            for (int i = cells[bq * ncl + cb0] + tid, i1 = cells[bq * ncl + cb1 + 1]; i < i1; i += 256) {
-                const float px = pts[2 * i], py = pts[2 * i + 1];
-                const int xa = (int)__builtin_rintf(px - B.box_half), ya = (int)__builtin_rintf(py - B.box_half);
-                const int xb = (int)__builtin_rintf(px + B.box_half), yb = (int)__builtin_rintf(py + B.box_half);
-                int xl = min(xa, xb), xr = max(xa, xb), yt = min(ya, yb), yd = max(ya, yb);
-                xl = max(xl, max(0, x0));
-                xr = min(xr, min(w - 1, x0 + FD_TX - 1));
-                yt = max(yt, max(0, y0));
-                yd = min(yd, min(h - 1, y0 + FD_TY - 1));
-                if (xl > xr || yt > yd) continue;
-                const int c0 = xl - x0, c1 = xr - x0;  // 0..63
-                const unsigned long long span =
-                    (c1 - c0 == 63) ? ~0ull : (((1ull << (c1 - c0 + 1)) - 1ull) << c0);
-                for (int y = yt; y <= yd; y++) atomicAnd(&TM[y - y0], ~span);
-            }
-    }
-    __syncthreads();
-    // ---- NMS + output: wave wv owns tile rows 8 wv .. 8 wv + 7 (score rows 8 wv ..
-    // 8 wv + 9), lane = column (xs = lane + 4) ----
-    const int x = x0 + lane;
-    const uint8_t* __restrict__ mask = B.mask ? B.mask + seq * B.npx : nullptr;
-    constexpr int RW = FD_TY / 4;
-    unsigned cen[RW + 2];
-    int lr[RW + 2], hm[RW + 2];
-#pragma unroll
-    for (int i = 0; i < RW + 2; i++) {
-        const int sr = wv * RW + i;
-        cen[i] = SC[sr][lane + 4];
-        lr[i] = max((int)(SC[sr][lane + 3] & 0xFF), (int)(SC[sr][lane + 5] & 0xFF));
-        hm[i] = max((int)(cen[i] & 0xFF), lr[i]);
-    }
-#pragma unroll
-    for (int i = 0; i < RW; i++) {
-        const int r = wv * RW + i;
-        const int y = y0 + r;
-        const unsigned v = cen[i + 1];
-        bool keep = (v & 0x100) != 0 && x < w && y < h;
-        if (nonmax) keep = keep && (int)(v & 0xFF) > max(max(hm[i], hm[i + 2]), lr[i + 1]);
-        if (mask) {
-            const int yy = y < h ? y : h - 1, xx = x < w ? x : w - 1;
-            keep = keep && mask[(size_t)yy * w + xx] != 0;
-        }
-        if (boxes) keep = keep && ((TM[r] >> lane) & 1ull);
-        const unsigned long long bal = __ballot(keep);
-        if (lane == 0) RB[r] = bal;
-    }
-    __syncthreads();
-    if (tid < FD_TY && y0 + tid < h) {
-        const unsigned long long bal = RB[tid];
-        const size_t row = seq * h + y0 + tid;
-        B.bits[row * B.nseg + blockIdx.x] = bal;
-        if (bal) atomicAdd(&B.rowcnt[row], __popcll(bal));
-    }
-}
-
 // Box centres of one sequence binned by cell (16-row band x 64-column tile):
 // counting sort, one block per sequence; order within a cell is irrelevant
 // (the mask is an AND of boxes).
@@ -1105,11 +543,6 @@ __global__ __launch_bounds__(kScanBlock) void fast_scan_kernel(FastDetBatch B, i
     if (tid == kScanBlock - 1) {
         const int total = part[kScanBlock - 1];
         B.n_out[seq] = total;
-        if (B.spec_n) {
-            int spec = min(max(B.spec_target - B.spec_tracked[seq] + B.spec_margin, 0), min(total, B.cap));
-            spec = max(min(min(spec, B.spec_cap), B.spec_map_cap - B.spec_map_n[seq]), 0);
-            B.spec_n[seq] = spec;
-        }
     }
 }
 
@@ -1147,11 +580,6 @@ __global__ __launch_bounds__(64) void fast_emit_kernel(FastDetBatch B, int thres
                 kp.y = (float)y;
                 kp.response = resp;
                 out[idx] = kp;
-                if (B.spec_n && idx < B.spec_n[seq]) {  // the speculative stereo LK's input
-                    float* sx = B.spec_xy + 2 * (seq * (size_t)B.spec_cap + idx);
-                    sx[0] = (float)x;
-                    sx[1] = (float)y;
-                }
             }
         }
         off += __popcll(m);
@@ -1202,11 +630,6 @@ hipError_t launch_fast_collect(const FastBatch& b, int nseq, int w, int h, int n
 hipError_t launch_fast_detect(const FastDetBatch& b0, int nseq, int w, int h, int threshold, int nonmax,
                               hipStream_t st, int stage) {
     FastDetBatch b = b0;
-    if (stage == kFastCollect) {
-        hipLaunchKernelGGL(fast_scan_kernel, dim3(nseq), dim3(kScanBlock), 0, st, b, h);
-        hipLaunchKernelGGL(fast_emit_kernel, dim3(h, nseq), dim3(64), 0, st, b, threshold, nonmax);
-        return hipGetLastError();
-    }
     if (stage == kFastBoxes) {
         if (b.mask) return hipErrorInvalidValue;  // a host mask goes with the detection
         if (b.box_pts) {
@@ -1230,28 +653,7 @@ hipError_t launch_fast_detect(const FastDetBatch& b0, int nseq, int w, int h, in
         if (e != hipSuccess) return e;
     }
     dim3 grid((w + FD_TX - 1) / FD_TX, (h + FD_TY - 1) / FD_TY, nseq);
-    // detection form, read per call (the parity tests switch it): 1 block queues,
-    // 2 wave queues, 3 wave queues + SWAR pre-test + register NMS, 4 wave queues +
-    // NMS over the corner queue
-    const char* ev = std::getenv("SVO_FAST_V");
-    const int ver = ev ? std::atoi(ev) : 4;
-    if (ver != 4) b.score_map = nullptr;  // only fast_detect_q_kernel fills it
-    if (ver == 1)
-        hipLaunchKernelGGL(fast_detect_kernel, grid, dim3(256), 0, st, b, threshold, nonmax);
-    else if (ver == 2)
-        hipLaunchKernelGGL(fast_detect_w_kernel, grid, dim3(256), 0, st, b, threshold, nonmax);
-    else if (ver == 3)
-        hipLaunchKernelGGL(fast_detect_s_kernel, grid, dim3(256), 0, st, b, threshold, nonmax);
-    else {
-        // tile height of the queue form (SVO_FAST_QTY: 32 default, 64 -- 81.0 vs 83.6 us
-        // alone per 64-frame launch, but stretched longer beside LK: step within noise)
-        const char* ty = std::getenv("SVO_FAST_QTY");
-        if (ty && std::atoi(ty) == 64)
-            hipLaunchKernelGGL(fast_detect_q_kernel<64>, dim3(grid.x, (h + 63) / 64, nseq), dim3(256), 0, st, b,
-                               threshold, nonmax);
-        else
-            hipLaunchKernelGGL(fast_detect_q_kernel<32>, grid, dim3(256), 0, st, b, threshold, nonmax);
-    }
+    hipLaunchKernelGGL(fast_detect_q_kernel<FD_TY>, grid, dim3(256), 0, st, b, threshold, nonmax);
     if (stage == kFastDetect) return hipGetLastError();
     hipLaunchKernelGGL(fast_scan_kernel, dim3(nseq), dim3(kScanBlock), 0, st, b, h);
     hipLaunchKernelGGL(fast_emit_kernel, dim3(h, nseq), dim3(64), 0, st, b, threshold, nonmax);

@@ -116,39 +116,9 @@ __global__ __launch_bounds__(kPostBlock) void post_lk_kernel(PostLkBatch B) {
     const int n_in = B.n_in[s];
     const uint8_t* __restrict__ st = B.status + o;
     long long it = 0;
-    int n;
-    if (!B.keep_bits) {
-        for (int i = tid; i < n_in; i += kPostBlock) it += B.iters[o + i];
-        n = block_compact<kPostBlock>(n_in, [&](int i) { return st[i] != 0; }, B.xy_in + 2 * o, B.mid_in + o,
-                                      B.xy_out + 2 * o, B.mid_out + o, wsum, &base_s);
-    } else {
-        // LK ran ahead over the last step's tracked points (before its RANSAC) and
-        // over its appended features: the features LK(t) would have tracked are
-        // the inliers (keep_bits) in order, then the appended ones (map ids pend0 +
-        // j), so compacting (inlier && status) ++ status2 gives the same set
-        const uint32_t* __restrict__ kb = B.keep_bits + (size_t)s * B.words_cap;
-        const int n2 = B.n2[s], m2 = B.pm.pend0[s];
-        const uint8_t* __restrict__ st2 = B.status2 + o;
-        auto inl = [&](int i) { return ((kb[i >> 5] >> (i & 31)) & 1u) != 0; };
-        for (int i = tid; i < n_in; i += kPostBlock)
-            if (inl(i)) it += B.iters[o + i];
-        for (int j = tid; j < n2; j += kPostBlock) it += B.iters2[o + j];
-        n = block_compact_fn<kPostBlock>(
-            n_in + n2, [&](int i) { return i < n_in ? inl(i) && st[i] != 0 : st2[i - n_in] != 0; },
-            [&](int i, float& x, float& y, int& m) {
-                if (i < n_in) {
-                    x = B.xy_in[2 * (o + i)];
-                    y = B.xy_in[2 * (o + i) + 1];
-                    m = B.mid_in[o + i];
-                } else {
-                    const int j = i - n_in;
-                    x = B.xy2[2 * (o + j)];
-                    y = B.xy2[2 * (o + j) + 1];
-                    m = m2 + j;
-                }
-            },
-            B.xy_out + 2 * o, B.mid_out + o, wsum, &base_s);
-    }
+    for (int i = tid; i < n_in; i += kPostBlock) it += B.iters[o + i];
+    const int n = block_compact<kPostBlock>(n_in, [&](int i) { return st[i] != 0; }, B.xy_in + 2 * o, B.mid_in + o,
+                                            B.xy_out + 2 * o, B.mid_out + o, wsum, &base_s);
     for (int off = 32; off > 0; off >>= 1) it += __shfl_xor(it, off);
     if (lane == 0) atomicAdd(&it_s, (unsigned long long)it);
     // lane 0 replays the RANSAC draws (they depend only on n) while the block
@@ -212,7 +182,7 @@ __device__ __forceinline__ void tail_body(const TailBatch& T, int s, bool copy_c
         T.n_in[s], [&](int i) { return ((bits[i >> 5] >> (i & 31)) & 1u) != 0; }, T.xy_in + 2 * o, T.mid_in + o,
         T.xy_out + 2 * o, T.mid_out + o, wsum, base_s);
     // new-feature candidates of the keyframe: the first `take` masked corners
-    int take = min(max(T.n_target - n, 0), min(T.cand_n[s], T.cand_cap));
+    int take = min(max(T.n_target[s] - n, 0), min(T.cand_n[s], T.cand_cap));
     take = min(take, T.cap - n);
     take = max(min(take, T.map_cap - T.map_n[s]), 0);
     if (copy_cand) {
@@ -275,10 +245,6 @@ __device__ __forceinline__ void append_body(const AppendBatch& A, int s, int n0,
             const size_t f = o + n0 + d;
             A.xy[2 * f] = xl;
             A.xy[2 * f + 1] = yl;
-            if (A.ap_xy) {  // the new features alone, the next LK-ahead's second input
-                A.ap_xy[2 * (o + d)] = xl;
-                A.ap_xy[2 * (o + d) + 1] = yl;
-            }
             A.mid[f] = m0 + d;
             // left camera frame (double of the float point, as Eigen::Vector3d{p_w.x,
             // p_w.y, p_w.z}); the pose is applied once known (PendingMap)
@@ -327,7 +293,7 @@ __global__ __launch_bounds__(BS) void keyframe_fused_kernel(TailBatch T, AppendB
 
 __global__ __launch_bounds__(kFeBlock) void stereo_prep_kernel(StereoPrepBatch B) {
     const int s = blockIdx.x;
-    int spec = min(max(B.n_target - B.n_tracked[s] + B.margin, 0), min(B.cand_n[s], B.cand_cap));
+    int spec = min(max(B.n_target[s] - B.n_tracked[s] + B.margin, 0), min(B.cand_n[s], B.cand_cap));
     spec = max(min(min(spec, B.cap), B.map_cap - B.map_n[s]), 0);
     const float* c = B.cand + (size_t)B.cand_elem * ((size_t)s * B.cand_cap);
     float* dst = B.st_xy + 2 * (size_t)s * B.cap;
@@ -356,19 +322,13 @@ hipError_t launch_tail(const TailBatch& tb, int nseq, hipStream_t st) {
     return hipGetLastError();
 }
 
-hipError_t launch_append(const AppendBatch& b, int nseq, hipStream_t st, bool small) {
-    if (small)
-        hipLaunchKernelGGL(append_kernel<kFeBlock>, dim3(nseq), dim3(kFeBlock), 0, st, b);
-    else
-        hipLaunchKernelGGL(append_kernel<kAppendBlock>, dim3(nseq), dim3(kAppendBlock), 0, st, b);
+hipError_t launch_append(const AppendBatch& b, int nseq, hipStream_t st) {
+    hipLaunchKernelGGL(append_kernel<kAppendBlock>, dim3(nseq), dim3(kAppendBlock), 0, st, b);
     return hipGetLastError();
 }
 
-hipError_t launch_keyframe_fused(const TailBatch& tb, const AppendBatch& ab, int nseq, hipStream_t st, bool small) {
-    if (small)
-        hipLaunchKernelGGL(keyframe_fused_kernel<kFeBlock>, dim3(nseq), dim3(kFeBlock), 0, st, tb, ab);
-    else
-        hipLaunchKernelGGL(keyframe_fused_kernel<kAppendBlock>, dim3(nseq), dim3(kAppendBlock), 0, st, tb, ab);
+hipError_t launch_keyframe_fused(const TailBatch& tb, const AppendBatch& ab, int nseq, hipStream_t st) {
+    hipLaunchKernelGGL(keyframe_fused_kernel<kAppendBlock>, dim3(nseq), dim3(kAppendBlock), 0, st, tb, ab);
     return hipGetLastError();
 }
 

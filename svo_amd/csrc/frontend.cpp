@@ -10,31 +10,41 @@
 //     keyframe points of t-1 to the world frame, keep status == 1,
 //       gather map points, first RANSAC subsets          [fe_kernels]    :169-175, :182-187, :141
 //     RANSAC: host EPnP chunks <-> GPU scoring launches  [pose.cpp, pnp.hip] calculatePose :191-196
-//     drop outliers + the first (n_features - n) corners [fe_kernels]    :218-229
+//     drop outliers + the keyframe's first corners       [fe_kernels]    :218-229
 //     stereo LK of those corners into right frame t      [lk.hip]        findLeftFeaturesInRight :94-118
 //     |yR - yL| < 40, DLT triangulation, z > 0, append   [fe_kernels]    triangulateNewMapPoints :120-152
+//
+// Which frames are keyframes: every frame, topping the set up to n_features
+// (SVO_KF_EVERY, the benchmark), or Tracking::nextFrame's rule (SVO_KF_REFERENCE,
+// :68-69) -- a per-sequence target (n_features or 0) the keyframe kernels read.
 //
 // FAST runs on the GPU beside LK; the host builds RANSAC hypotheses while the GPU
 // scores; the final pose fits run on the host while the GPU tracks the next frame,
 // so a keyframe's new map points stay in its camera frame until the next step
 // moves them to the world frame with that pose (PendingMap, frontend.hpp).
+//
+// Streams (the box gives a process 4 hardware queues, GPU_MAX_HW_QUEUES): the
+// LK stream (LK, post-LK, scoring, keyframe; highest priority), the FAST stream
+// (box binning, FAST, speculative stereo LK; lowest), the context stream
+// (pyramids, FAST pre-detection) and the copy stream (host copies, SQPnP
+// statistics).
 #include <pthread.h>
 #include <sched.h>
 
 #include <cctype>
 
 #include <algorithm>
-#include <cstdio>
-#include <fstream>
-#include <sstream>
-#include <string>
-#include <cstdlib>
-#include <chrono>
 #include <atomic>
+#include <chrono>
 #include <condition_variable>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
+#include <fstream>
 #include <functional>
 #include <mutex>
+#include <sstream>
+#include <string>
 #include <thread>
 #include <vector>
 
@@ -221,9 +231,23 @@ std::vector<int> host_cpu_plan(int rank, int world, const int* gpu_node) {
     return split(allowed, rank, world);
 }
 
-int world_size_env() {
-    const char* lw = std::getenv("LOCAL_WORLD_SIZE");
-    return lw ? std::max(1, std::atoi(lw)) : 1;
+// LOCAL_RANK / LOCAL_WORLD_SIZE as torch.distributed.run sets them (one process per GPU)
+int local_rank_env() {
+    const char* e = std::getenv("LOCAL_RANK");
+    return e ? std::max(0, std::atoi(e)) : 0;
+}
+int local_world_env() {
+    const char* e = std::getenv("LOCAL_WORLD_SIZE");
+    return e ? std::max(1, std::atoi(e)) : 1;
+}
+
+// host-side step trace (SVO_FE_TRACE=1): label + microseconds since step start
+bool trace_on() {
+    static const bool on = [] {
+        const char* e = std::getenv("SVO_FE_TRACE");
+        return e && e[0] == '1';
+    }();
+    return on;
 }
 
 // NUMA node of HIP device d (-1: unknown), from its PCI address in sysfs
@@ -238,8 +262,13 @@ int device_numa_node(int d) {
     return v;
 }
 
-constexpr int kPhases = 11;
-enum Phase { PH_PYR, PH_LK, PH_POST, PH_STEREO, PH_PNP, PH_TAIL, PH_FAST, PH_BUCKET, PH_APPEND, PH_PYR_R, PH_LK_NEW };
+constexpr int kPhases = 10;
+enum Phase { PH_PYR, PH_LK, PH_POST, PH_STEREO, PH_PNP, PH_TAIL, PH_FAST, PH_BUCKET, PH_APPEND, PH_PYR_R };
+
+// floor of the first RANSAC hypothesis chunk: a floor of 1 saves an EPnP per
+// sequence when one hypothesis is predicted, but the misses' extra scoring
+// rounds measured 2-6 % slower on the KITTI bench
+constexpr int kChunk0 = 2;
 
 }  // namespace
 
@@ -267,79 +296,49 @@ struct svo_frontend {
     float *st_xy, *st_next;  // keyframe candidates (left) and their stereo LK matches (right)
     uint8_t* st_status;
     int* box_band;
-    int *midA, *midB, *nA, *nB, *iters, *kn, *bn, *map_n, *rowcnt, *rowoff, *scr, *cnt, *added, *st_n;
+    int *midA, *midB, *nA, *nB, *iters, *kn, *bn, *map_n, *rowcnt, *rowoff, *scr, *added, *st_n;
     int *pend0, *pend_n;  // PendingMap ranges
     int* spec_n;          // speculative stereo candidates per sequence (StereoPrepBatch)
-    std::vector<int> lk_queued;  // [g] step whose temporal LK is already queued on slice g
-    bool pipe = true;            // next step's LK of a slice queued right behind its keyframe (SVO_FE_PIPE)
     int spec_margin = 32;  // RANSAC drops covered by the speculative stereo LK (SVO_FE_SPEC_MARGIN, < 0: off)
-    // speculative stereo LK queued right behind FAST(t), beside LK(t), sized from
-    // the features before LK (SVO_FE_SPEC_EARLY=1; off by default: measured 0.2-1.5 %
-    // slower than queueing it behind post-LK at all three configs): the margin then
-    // covers LK and RANSAC losses together
-    bool spec_early = false;
-    int spec_t = -1;  // step whose speculative stereo LK went out with its front half
-    int spec_margin_t = 32;  // the margin that speculation used (spec_margin + the last LK losses)
-    // FAST's row scan + emit queued behind the post-LK, filling the speculative
-    // stereo input as they write the corners (one slice, no bucketing, post-LK
-    // speculation): no separate prep kernel and stream wait on the keyframe's path
-    // (SVO_FE_FAST_SPLIT=1; off by default: measured within noise to 1.6 % slower
-    // at the three configs)
-    bool fast_split = false;
-    int lk_loss_max = 0;     // max over sequences of the last step's LK losses (n_before - n_tracked)
-    int min_tracked = 0;     // min over sequences of the last step's tracked count (stereo LK grid hint)
-    // LK ahead (SVO_FE_AHEAD, one slice): LK(t+1) runs over step t's tracked
-    // points right behind its post-LK, beside the host's RANSAC, and a small LK
-    // over the keyframe's appended features follows the keyframe; the next post-LK
-    // keeps the inliers' and the appended features' tracks (PostLkBatch)
-    bool ahead = false;
-    int ahead_t = -1;            // step whose temporal LK ran ahead
-    float *ap_xy = nullptr, *ap_next = nullptr;  // appended features [s][CAP] and their tracks
-    uint8_t* ap_status = nullptr;
-    int* ap_iters = nullptr;
-    hipStream_t st_kf = nullptr;  // RANSAC scoring + keyframe + appended LK (highest priority)
-    hipEvent_t ev_aplk = nullptr;  // appended features' LK done
+    int min_tracked = 0;   // min over sequences of the last step's tracked count (stereo LK grid hint)
     unsigned long long* fbits;
     uint8_t* status;
-    uint32_t* bits_all;
-    double *map, *hyps;
+    double* map;
     // the tracked-point arrays of a step (xyB, obj, nB) and its inlier bits are
     // double-buffered by step parity: the side work of step t (SQPnP statistics,
     // full copy to the host) reads them while step t+1 already runs
     float *xyB_b[2], *obj_b[2];
     int* nB_b[2];
     int front_t = -1;  // step whose first half (LK .. FAST) is already enqueued
-    std::vector<hipEvent_t> ev_tail;  // [g] end of a step's tail on slice g
-    // host mirrors (pinned)
+    // host mirrors (pinned): the full point copies for the fits and long RANSAC runs
     void* hmem = nullptr;
-    int *h_nB, *h_nA, *h_cnt, *h_added;
-    long long* h_itsum;
-    float *h_xyB, *h_obj, *h_samp;   // h_xyB / h_obj: this step's parity half of h_*_b
+    float *h_xyB, *h_obj;  // this step's parity half of h_*_b
     float *h_xyB_b[2], *h_obj_b[2];
-    double *h_hyps, *h_stats;
-    double* h_pose = nullptr;  // [s][12] camera -> world of the last fitted frame (host-coherent)
-    uint32_t *h_bits, *h_best;  // h_best: this step's parity of h_best_b (host-coherent)
+    // host-coherent memory the kernels write / read directly (no D2H copies on
+    // the critical path): post-LK counts / iteration sums / RANSAC subsets, the
+    // keyframe's counts, the inlier bits, statistics, poses, keyframe targets
+    void* zout = nullptr;
+    int *h_nB, *h_nA, *h_added, *h_target;
+    long long* h_itsum;
+    float* h_samp;
+    double *h_stats, *h_pose;   // h_pose: [s][12] camera -> world of the last fitted frame
+    uint32_t* h_best;           // this step's parity of h_best_b
     uint32_t* h_best_b[2];
-    void* zout = nullptr;  // host-coherent: counts, sums, RANSAC subsets, inlier bits, poses
     // host-coherent buffers the scoring kernel reads / writes directly (zero-copy:
     // no H2D of the hypotheses, no D2H of bits / counts, no count memset)
     void* zmem = nullptr;
     double* z_hyps = nullptr;     // [s][kRansacChunk][12]
     uint32_t* z_bits = nullptr;   // [s][kRansacChunk][WORDS]
     int* z_cnt = nullptr;         // [s][kRansacChunk] inliers per hypothesis
-    bool zero_copy = true;
     std::vector<RansacSeq> rs;
     std::vector<int> pred_iters;  // [s] RANSAC hypotheses the last frame's outlier ratio implies
-    int chunk0 = 2;                // floor of the first hypothesis chunk
-    bool pyr_early = true;         // frame t+1's pyramid beside LK(t) (SVO_FE_PYR_EARLY)
-    bool fast_early = true;        // FAST(t) queued behind LK(t), not after it (SVO_FE_FAST_EARLY)
-    bool fast_first = false;       // FAST(t) queued ahead of LK(t) (SVO_FE_FAST_FIRST)
-    int fast_pre = 0;              // FAST detection of frame t+1 queued in step t (SVO_FE_FAST_PRE):
-                                   // 1 on the pyramid stream behind this step's FAST, 2 on the
-                                   // FAST stream behind this step's speculative stereo LK
+    std::vector<uint8_t> kf_prev; // [s] the last frame was a keyframe (SVO_KF_REFERENCE)
+    // FAST pre-detection (SVO_FE_FAST_PRE=1, the default): frame t+1's detection +
+    // NMS without the box mask queued in step t on the context stream (0: FAST
+    // detection behind LK(t) on the FAST stream)
+    int fast_pre = 1;
     int pre_t = -1;                // frame whose unmasked detection sits in fbits / rowcnt / score_map
-    int front_fast_t = -1;         // frame whose FAST chain recorded ev_fdone
-    hipEvent_t ev_pre = nullptr;   // that detection done (pyramid stream)
+    hipEvent_t ev_pre = nullptr;   // that detection done (context stream)
     hipEvent_t ev_fdone = nullptr; // this step's FAST chain done (FAST stream)
     std::vector<double> pose;  // [s][6]
     bool fits_pending = false;
@@ -352,8 +351,7 @@ struct svo_frontend {
     // the final fits, RANSAC past the prefetched subsets and the n <= 5 solve, so
     // they travel on their own stream once requested
     hipStream_t st_copy = nullptr;
-    bool st_copy_owned = true;
-    hipEvent_t ev_gathered = nullptr, ev_full = nullptr;  // ev_full: this step's parity of ev_full_b
+    hipEvent_t ev_full = nullptr;  // this step's parity of ev_full_b
     hipEvent_t ev_full_b[2] = {nullptr, nullptr};
     hipEvent_t ev_pyr_r = nullptr;  // right pyramid of the step's frame built
     bool full_queued = false;
@@ -361,13 +359,11 @@ struct svo_frontend {
     uint8_t* score_map = nullptr;  // [s][npx] FAST scores of the kept corners
     Pool* pool = nullptr;
     std::vector<int> host_cpus;  // the pool's pinned CPU set (svo_host_cpu_plan)
-    // pipeline: slices of the batch [g0[g], g0[g] + gn[g]) on their own streams
-    int G = 1;
-    std::vector<int> g0, gn;
-    std::vector<hipStream_t> gst;     // per slice (high priority)
-    hipStream_t st_fast = nullptr;    // mask + FAST + bucket (low priority)
-    // [0] pyramid done, [1] FAST done, [2 + 2g] LK done, [3 + 2g] post-LK done
-    std::vector<hipEvent_t> ev_sync;
+    hipStream_t st_lk = nullptr;    // LK, post-LK, scoring, keyframe (highest priority)
+    hipStream_t st_fast = nullptr;  // box binning + FAST + bucket + speculative stereo LK (lowest)
+    hipEvent_t ev_pyr = nullptr;    // left pyramid of the step's frame built
+    hipEvent_t ev_fast = nullptr;   // FAST (and the speculative stereo LK behind it) done
+    hipEvent_t ev_lk = nullptr, ev_post = nullptr, ev_tail = nullptr;
     // timing
     hipEvent_t ev[256];
     double phase_ms[kPhases] = {0};
@@ -462,12 +458,16 @@ int fe_fast_and_bucket(svo_frontend* fe, const PyrDesc* descs_cur, bool use_mask
     return SVO_OK;
 }
 
-// SVO_FE_FAST_PRE: frame tn's FAST detection + NMS without the box mask (the mask
-// drops corners after NMS, so it can wait for frame tn-1's features) queued on `st`
-// once the current step's FAST chain has consumed the row words; step tn keeps only
-// the box filter, the recount, scan and emit behind its LK (kFastBoxes)
-static int fe_queue_pre(svo_frontend* fe, int tn, hipStream_t st) {
+// FAST pre-detection: frame tn's FAST detection + NMS without the box mask (the
+// mask drops corners after NMS, so it can wait for frame tn-1's features) queued
+// on the context stream once the current step's FAST chain has consumed the row
+// words (ev_fdone); step tn keeps only the box filter, the recount, scan and emit
+// behind its LK (kFastBoxes). NB: from here on the context stream -- the next
+// right pyramid and the pyramid after next, both queued behind this detection --
+// is serialised behind FAST(tn-1)'s chain on the low-priority FAST stream.
+int fe_queue_pre(svo_frontend* fe, int tn) {
     svo_ctx* ctx = fe->ctx;
+    hipStream_t st = ctx->stream;
     const PyrDesc* dnext = fe->d_desc + (size_t)(tn % fe->T) * fe->S;
     SVO_HIP(ctx, hipStreamWaitEvent(st, fe->ev_fdone, 0));
     FastDetBatch fb = fe_fast_batch(fe, dnext, false);
@@ -480,20 +480,16 @@ static int fe_queue_pre(svo_frontend* fe, int tn, hipStream_t st) {
 
 // findLeftFeaturesInRight: calcOpticalFlowPyrLK(left, right, pts, 11x11, 3,
 // {COUNT+EPS, 30, 0.001}), flags 0 (R:src/tracking.cpp:97-105) of st_xy[0,
-// counts[s]) of sequences [a, a + n) of frame t; max_n bounds every count (the
-// grid). The left frame's derivative pyramid is the one the next step's
-// temporal LK reads.
-int fe_stereo_lk(svo_frontend* fe, int t, int a, int n, const int* counts, int max_n, hipStream_t st,
-                 int grid_hint = 0) {
+// counts[s]) of every sequence of frame t; max_n bounds every count (the grid).
+int fe_stereo_lk(svo_frontend* fe, int t, const int* counts, int max_n, hipStream_t st, int grid_hint = 0) {
     svo_ctx* ctx = fe->ctx;
     const svo_frontend_config& c = fe->cfg;
-    const size_t CAP = fe->CAP;
     int slot;
     SVO_HIP(ctx, hipStreamWaitEvent(st, fe->ev_pyr_r, 0));
-    const PyrDesc* dl = fe->d_desc + (size_t)(t % fe->T) * fe->S + a;
-    const PyrDesc* dr = fe->d_desc_r + (size_t)(t % fe->T) * fe->S + a;
-    LKBatch lb{dl, dr, fe->d_der + (size_t)(t % 3) * fe->S + a, fe->st_xy + 2 * a * CAP, fe->st_next + 2 * a * CAP,
-               fe->st_status + a * CAP, nullptr, nullptr, counts, 0, fe->CAP};
+    const PyrDesc* dl = fe->d_desc + (size_t)(t % fe->T) * fe->S;
+    const PyrDesc* dr = fe->d_desc_r + (size_t)(t % fe->T) * fe->S;
+    LKBatch lb{dl, dr, fe->d_der + (size_t)(t % 3) * fe->S, fe->st_xy, fe->st_next, fe->st_status, nullptr, nullptr,
+               counts, 0, fe->CAP};
     lb.grid_hint = grid_hint;
     LKParams lp;
     lp.win_w = lp.win_h = c.stereo_win;
@@ -504,27 +500,27 @@ int fe_stereo_lk(svo_frontend* fe, int t, int a, int n, const int* counts, int m
     lp.flags = 0;
     lp.min_eig = (float)c.min_eig;
     lp.want_err = 0;
+    lk_apply_env(lp);
     ph_begin(fe, PH_STEREO, st, &slot);
-    SVO_HIP(ctx, launch_lk(lb, n, std::min(std::max(max_n, 0), fe->CAP), lp, st));
+    SVO_HIP(ctx, launch_lk(lb, fe->S, std::min(std::max(max_n, 0), fe->CAP), lp, st));
     ph_end(fe, st, slot);
     return SVO_OK;
 }
 
-// The keyframe of sequences [g0, g0 + n) on stream st (R:src/tracking.cpp:247-255,
-// every frame a keyframe topping the set up to n_features): outlier compaction
-// (inlier bits `bits`, or every point when n_in is all zero) + the first
-// candidates (tail_kernel), their stereo LK into the right frame t
-// (findLeftFeaturesInRight), then filter + triangulation + append (append_kernel).
-// xy_in / mid_in / n_in: the step's tracked points (compacted into xyA / midA / nA).
-// max_take: a host bound on every sequence's candidate count (the stereo LK grid).
-// spec: the speculative stereo LK (fe_queue_spec) already matched every
-// sequence's take candidates: compaction, filter, triangulation and append run
-// as one kernel.
-int fe_keyframe(svo_frontend* fe, int t, int g0, int n, const int* n_in, const uint32_t* bits, const float* xy_in,
-                const int* mid_in, int max_take, hipStream_t st, bool spec = false, bool ap = false) {
+// The keyframe of every sequence on stream st (R:src/tracking.cpp:247-255):
+// outlier compaction (inlier bits `bits`, or every point when n_in is all zero)
+// + the first candidates up to the sequence's target (h_target: n_features on a
+// keyframe, 0 otherwise) (tail_kernel), their stereo LK into the right frame t
+// (findLeftFeaturesInRight), then filter + triangulation + append
+// (append_kernel). xy_in / mid_in / n_in: the step's tracked points (compacted
+// into xyA / midA / nA). max_take: a host bound on every sequence's candidate
+// count (the stereo LK grid). spec: the speculative stereo LK (fe_queue_spec)
+// already matched every sequence's take candidates: compaction, filter,
+// triangulation and append run as one kernel.
+int fe_keyframe(svo_frontend* fe, int t, const int* n_in, const uint32_t* bits, const float* xy_in, const int* mid_in,
+                int max_take, hipStream_t st, bool spec = false) {
     svo_ctx* ctx = fe->ctx;
     const svo_frontend_config& c = fe->cfg;
-    const size_t CAP = fe->CAP, a = g0;
     int slot;
     const bool bucketed = c.bucket_size > 0;
     TailBatch tb;
@@ -533,98 +529,95 @@ int fe_keyframe(svo_frontend* fe, int t, int g0, int n, const int* n_in, const u
     tb.words_cap = fe->WORDS;
     tb.xy_in = xy_in;
     tb.mid_in = mid_in;
-    tb.xy_out = fe->xyA + 2 * a * CAP;
-    tb.mid_out = fe->midA + a * CAP;
-    tb.n_out = fe->nA + a;
+    tb.xy_out = fe->xyA;
+    tb.mid_out = fe->midA;
+    tb.n_out = fe->nA;
     tb.cap = fe->CAP;
-    tb.n_target = c.n_features;
-    tb.cand = bucketed ? fe->cand + 2 * a * fe->BCAP : fe->kps + 3 * a * fe->KCAP;
+    tb.n_target = fe->h_target;
+    tb.cand = bucketed ? fe->cand : fe->kps;
     tb.cand_elem = bucketed ? 2 : 3;
     tb.cand_cap = bucketed ? fe->BCAP : fe->KCAP;
-    tb.cand_n = (bucketed ? fe->bn : fe->kn) + a;
-    tb.map_n = fe->map_n + a;
+    tb.cand_n = bucketed ? fe->bn : fe->kn;
+    tb.map_n = fe->map_n;
     tb.map_cap = fe->MAPCAP;
-    tb.st_xy = fe->st_xy + 2 * a * CAP;
-    tb.st_n = fe->st_n + a;
+    tb.st_xy = fe->st_xy;
+    tb.st_n = fe->st_n;
     AppendBatch ab;
-    ab.n = fe->nA + a;
-    ab.xy = fe->xyA + 2 * a * CAP;
-    ab.mid = fe->midA + a * CAP;
+    ab.n = fe->nA;
+    ab.xy = fe->xyA;
+    ab.mid = fe->midA;
     ab.cap = fe->CAP;
-    ab.st_xy = fe->st_xy + 2 * a * CAP;
-    ab.st_next = fe->st_next + 2 * a * CAP;
-    ab.st_status = fe->st_status + a * CAP;
-    ab.st_n = fe->st_n + a;
+    ab.st_xy = fe->st_xy;
+    ab.st_next = fe->st_next;
+    ab.st_status = fe->st_status;
+    ab.st_n = fe->st_n;
     ab.y_threshold = c.y_threshold;
     std::memcpy(ab.P, c.P_left, sizeof(float) * 12);
     std::memcpy(ab.P + 12, c.P_right, sizeof(float) * 12);
-    ab.map = fe->map + 3 * a * fe->MAPCAP;
-    ab.map_n = fe->map_n + a;
+    ab.map = fe->map;
+    ab.map_n = fe->map_n;
     ab.map_cap = fe->MAPCAP;
-    ab.pend0 = fe->pend0 + a;
-    ab.pend_n = fe->pend_n + a;
-    ab.added = fe->added + a;
-    ab.h_n = fe->h_nA + a;
-    ab.h_added = fe->h_added + a;
-    ab.ap_xy = ap ? fe->ap_xy + 2 * a * CAP : nullptr;  // LK ahead: the new features alone too
+    ab.pend0 = fe->pend0;
+    ab.pend_n = fe->pend_n;
+    ab.added = fe->added;
+    ab.h_n = fe->h_nA;
+    ab.h_added = fe->h_added;
     if (spec) {
         ph_begin(fe, PH_TAIL, st, &slot);
-        SVO_HIP(ctx, launch_keyframe_fused(tb, ab, n, st, ap));
+        SVO_HIP(ctx, launch_keyframe_fused(tb, ab, fe->S, st));
         ph_end(fe, st, slot);
         return SVO_OK;
     }
     ph_begin(fe, PH_TAIL, st, &slot);
-    SVO_HIP(ctx, launch_tail(tb, n, st));
+    SVO_HIP(ctx, launch_tail(tb, fe->S, st));
     ph_end(fe, st, slot);
-    int rc = fe_stereo_lk(fe, t, (int)a, n, fe->st_n + a, max_take, st);
+    int rc = fe_stereo_lk(fe, t, fe->st_n, max_take, st);
     if (rc) return rc;
     ph_begin(fe, PH_APPEND, st, &slot);
-    SVO_HIP(ctx, launch_append(ab, n, st, ap));
+    SVO_HIP(ctx, launch_append(ab, fe->S, st));
     ph_end(fe, st, slot);
     return SVO_OK;
 }
 
-// The speculative stereo LK of step t (StereoPrepBatch) for the sequences [a, a
-// + n) of one slice, on the FAST stream (behind FAST: the candidates) after the
-// slice's post-LK (ev_post: the tracked counts), queued with the post-LK so that
-// no host round trip precedes it: it runs beside the host's RANSAC. max_spec
-// bounds every sequence's spec (the grid; blocks past a sequence's count exit at
-// once). ev_sync[1] is re-recorded behind it, so the keyframe's wait for FAST
-// covers it too.
-int fe_queue_spec(svo_frontend* fe, int t, int a, int n, int max_spec, hipEvent_t ev_post, const int* n_before,
-                  int margin) {
+// The speculative stereo LK of step t (StereoPrepBatch), on the FAST stream
+// (behind FAST: the candidates) after the step's post-LK (the tracked counts),
+// queued with the post-LK so that no host round trip precedes it: it runs beside
+// the host's RANSAC. The keyframe takes the first target - kept candidates and
+// kept <= n_tracked, so the first target - n_tracked + margin cover the take
+// whenever RANSAC drops at most `margin` points. ev_fast is re-recorded behind it,
+// so the keyframe's wait for FAST covers it too.
+int fe_queue_spec(svo_frontend* fe, int t) {
     svo_ctx* ctx = fe->ctx;
     const svo_frontend_config& c = fe->cfg;
-    const size_t CAP = fe->CAP;
     hipStream_t sf = fe->st_fast;
     const bool bucketed = c.bucket_size > 0;
     StereoPrepBatch pb;
-    pb.n_tracked = n_before + a;
-    pb.cand = bucketed ? fe->cand + 2 * a * fe->BCAP : fe->kps + 3 * a * fe->KCAP;
+    pb.n_tracked = fe->nB;
+    pb.cand = bucketed ? fe->cand : fe->kps;
     pb.cand_elem = bucketed ? 2 : 3;
     pb.cand_cap = bucketed ? fe->BCAP : fe->KCAP;
-    pb.cand_n = (bucketed ? fe->bn : fe->kn) + a;
-    pb.map_n = fe->map_n + a;
+    pb.cand_n = bucketed ? fe->bn : fe->kn;
+    pb.map_n = fe->map_n;
     pb.map_cap = fe->MAPCAP;
     pb.cap = fe->CAP;
-    pb.n_target = c.n_features;
-    pb.margin = margin;
-    pb.st_xy = fe->st_xy + 2 * a * CAP;
-    pb.spec_n = fe->spec_n + a;
-    if (ev_post) SVO_HIP(ctx, hipStreamWaitEvent(sf, ev_post, 0));
-    SVO_HIP(ctx, launch_stereo_prep(pb, n, sf));
+    pb.n_target = fe->h_target;
+    pb.margin = fe->spec_margin;
+    pb.st_xy = fe->st_xy;
+    pb.spec_n = fe->spec_n;
+    SVO_HIP(ctx, hipStreamWaitEvent(sf, fe->ev_post, 0));
+    SVO_HIP(ctx, launch_stereo_prep(pb, fe->S, sf));
     // grid for the speculation the last step's smallest tracked count implies
     // (+ slack); the kernel's waves loop over any candidates beyond it
-    const int hint = std::min(fe->CAP, fe->cfg.n_features - fe->min_tracked + margin + 32);
-    int rc = fe_stereo_lk(fe, t, a, n, fe->spec_n + a, max_spec, sf, hint);
+    const int max_spec = std::min(c.n_features + fe->spec_margin, fe->CAP);
+    const int hint = std::min(fe->CAP, c.n_features - fe->min_tracked + fe->spec_margin + 32);
+    int rc = fe_stereo_lk(fe, t, fe->spec_n, max_spec, sf, hint);
     if (rc) return rc;
-    SVO_HIP(ctx, hipEventRecord(fe->ev_sync[1], sf));
+    SVO_HIP(ctx, hipEventRecord(fe->ev_fast, sf));
     return SVO_OK;
 }
 
-PendingMap fe_pending(svo_frontend* fe, int a) {
-    return PendingMap{fe->map + 3 * (size_t)a * fe->MAPCAP, fe->MAPCAP, fe->pend0 + a, fe->pend_n + a,
-                      fe->h_pose + 12 * (size_t)a};
+PendingMap fe_pending(svo_frontend* fe) {
+    return PendingMap{fe->map, fe->MAPCAP, fe->pend0, fe->pend_n, fe->h_pose};
 }
 
 // Frame::pose() of a fitted frame (R:src/tracking.cpp:198-214): the inverse of
@@ -644,15 +637,13 @@ void fe_set_pose(svo_frontend* fe, int s, bool ok, const double rvec[3], const d
     for (int i = 0; i < 3; i++) T[9 + i] = -(T[3 * i] * tvec[0] + T[3 * i + 1] * tvec[1] + T[3 * i + 2] * tvec[2]);
 }
 
-// Full D2H of the step's tracked points and map points (after ev_gathered), on
+// Full D2H of the step's tracked points and map points (after the post-LK), on
 // the copy stream; queued once per step, when first needed or at the step's end.
 int fe_queue_full(svo_frontend* fe) {
     if (fe->full_queued) return SVO_OK;
     svo_ctx* ctx = fe->ctx;
     const size_t S = fe->S, CAP = fe->CAP;
-    SVO_HIP(ctx, hipStreamWaitEvent(fe->st_copy, fe->ev_gathered, 0));
-    // (the copy stream also waited for the RANSAC subsets' D2H: the bulk copy
-    // does not compete with that critical one)
+    SVO_HIP(ctx, hipStreamWaitEvent(fe->st_copy, fe->ev_post, 0));
     SVO_HIP(ctx, hipMemcpyAsync(fe->h_xyB, fe->xyB, sizeof(float) * 2 * S * CAP, hipMemcpyDeviceToHost, fe->st_copy));
     SVO_HIP(ctx, hipMemcpyAsync(fe->h_obj, fe->obj, sizeof(float) * 3 * S * CAP, hipMemcpyDeviceToHost, fe->st_copy));
     SVO_HIP(ctx, hipEventRecord(fe->ev_full, fe->st_copy));
@@ -660,25 +651,19 @@ int fe_queue_full(svo_frontend* fe) {
     return SVO_OK;
 }
 
-// Queue the SQPnP sufficient statistics of the last step's RANSAC inliers (the
-// bits are on the device since that step) on the FAST stream, then their D2H.
-// (on the copy stream -- the box has 4 hardware queues (GPU_MAX_HW_QUEUES), so
-// the step keeps to 4 streams: ctx->stream (pyramids), the slice stream (LK,
-// post-LK, scoring, tail), the FAST stream and the copy stream; written straight
-// to host-coherent memory; the inputs
-// -- inlier bits on the host, points from the post-LK kernel the host already
-// waited for -- need no device-side wait, so they are queued right behind the
-// tail kernel and run beside it, ahead of the next LK)
+// Queue the SQPnP sufficient statistics of the last step's RANSAC inliers on the
+// copy stream, written straight to host-coherent memory. The inputs -- inlier
+// bits on the host, points from the post-LK kernel the host already waited for
+// -- need no device-side wait, so they are queued right behind the keyframe and
+// run beside it, ahead of the next LK (a kernel queued beside a running LK waits
+// for it: LK leaves no registers free).
 int fe_queue_stats(svo_frontend* fe) {
     if (!fe->stats_pending) return SVO_OK;
     svo_ctx* ctx = fe->ctx;
     const int p = fe->stats_parity;
-    // (LK ahead: on the keyframe stream -- the next post-LK waits for the fits
-    // these feed, and the running LK would starve a lower-priority stream)
-    hipStream_t ss = fe->st_kf ? fe->st_kf : fe->st_copy;
     SVO_HIP(ctx, launch_suffstats(fe->obj_b[p], fe->xyB_b[p], fe->nB_b[p], fe->CAP, fe->h_best_b[p], fe->WORDS, fe->S,
-                                  fe->cfg.K, fe->h_stats, ss));
-    SVO_HIP(ctx, hipEventRecord(fe->ev_stats, ss));
+                                  fe->cfg.K, fe->h_stats, fe->st_copy));
+    SVO_HIP(ctx, hipEventRecord(fe->ev_stats, fe->st_copy));
     fe->stats_pending = false;
     return SVO_OK;
 }
@@ -707,6 +692,10 @@ double fe_finish_fits(svo_frontend* fe) {
     return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
 }
 
+hipError_t fe_make_stream(hipStream_t* st, int priority) {
+    return hipStreamCreateWithPriority(st, hipStreamNonBlocking, priority);
+}
+
 }  // namespace
 
 extern "C" {
@@ -718,6 +707,7 @@ int svo_frontend_create(svo_ctx* ctx, const svo_frontend_config* cfg, svo_fronte
         !lk_supported(c.win, c.win) || c.stereo_win <= 2 || c.stereo_max_level < 0 ||
         !lk_supported(c.stereo_win, c.stereo_win) || c.pnp_iterations <= 0 ||
         !(c.pnp_confidence > 0 && c.pnp_confidence < 1) ||
+        (c.keyframe_rule != SVO_KF_EVERY && c.keyframe_rule != SVO_KF_REFERENCE) ||
         (c.bucket_size > 0 && (c.per_bucket <= 0 || c.width / c.bucket_size <= 0)))
         return set_error(ctx, SVO_ERR_ARG, "svo_frontend_create: bad config");
     svo_frontend* fe = new svo_frontend();
@@ -773,7 +763,6 @@ int svo_frontend_create(svo_ctx* ctx, const svo_frontend_config* cfg, svo_fronte
         fe->d_desc_r = carve<PyrDesc>(p, (size_t)fe->T * S);
         fe->xyA = carve<float>(p, 2 * (size_t)S * CAP);
         fe->next_xy = carve<float>(p, 2 * (size_t)S * CAP);
-        fe->xyB = carve<float>(p, 2 * (size_t)S * CAP);
         fe->st_xy = carve<float>(p, 2 * (size_t)S * CAP);
         fe->st_next = carve<float>(p, 2 * (size_t)S * CAP);
         fe->st_status = carve<uint8_t>(p, (size_t)S * CAP);
@@ -781,105 +770,75 @@ int svo_frontend_create(svo_ctx* ctx, const svo_frontend_config* cfg, svo_fronte
         fe->pend0 = carve<int>(p, S);
         fe->pend_n = carve<int>(p, S);
         fe->spec_n = carve<int>(p, S);
-        fe->obj = carve<float>(p, 3 * (size_t)S * CAP);
         fe->kps = carve<float>(p, 3 * (size_t)S * fe->KCAP);
         fe->cand = carve<float>(p, 2 * (size_t)S * fe->BCAP);
         fe->midA = carve<int>(p, (size_t)S * CAP);
         fe->midB = carve<int>(p, (size_t)S * CAP);
         fe->iters = carve<int>(p, (size_t)S * CAP);
         fe->nA = carve<int>(p, S);
-        fe->nB = carve<int>(p, S);
         fe->kn = carve<int>(p, S);
         fe->bn = carve<int>(p, S);
         fe->map_n = carve<int>(p, S);
         fe->added = carve<int>(p, S);
         fe->rowcnt = carve<int>(p, (size_t)S * c.height);
         fe->scr = carve<int>(p, fe->bscr * S);
-        fe->cnt = carve<int>(p, (size_t)S * kRansacChunk);
         fe->status = carve<uint8_t>(p, (size_t)S * CAP);
         fe->fbits = carve<unsigned long long>(p, (size_t)S * c.height * ((c.width + 63) / 64));
         fe->rowoff = carve<int>(p, (size_t)S * c.height);
-        fe->bits_all = carve<uint32_t>(p, (size_t)S * kRansacChunk * fe->WORDS);
         fe->map = carve<double>(p, 3 * (size_t)S * fe->MAPCAP);
-        fe->hyps = carve<double>(p, 12 * (size_t)S * kRansacChunk);
         fe->box_binned = carve<float>(p, 2 * (size_t)S * CAP);
         fe->box_band = carve<int>(p, (size_t)S * fast_box_cells(c.width, c.height));
-        fe->ap_xy = carve<float>(p, 2 * (size_t)S * CAP);
-        fe->ap_next = carve<float>(p, 2 * (size_t)S * CAP);
-        fe->ap_status = carve<uint8_t>(p, (size_t)S * CAP);
-        fe->ap_iters = carve<int>(p, (size_t)S * CAP);
-        fe->xyB_b[0] = fe->xyB;
-        fe->obj_b[0] = fe->obj;
-        fe->nB_b[0] = fe->nB;
-        fe->xyB_b[1] = carve<float>(p, 2 * (size_t)S * CAP);
-        fe->obj_b[1] = carve<float>(p, 3 * (size_t)S * CAP);
-        fe->nB_b[1] = carve<int>(p, S);
+        for (int k = 0; k < 2; k++) {
+            fe->xyB_b[k] = carve<float>(p, 2 * (size_t)S * CAP);
+            fe->obj_b[k] = carve<float>(p, 3 * (size_t)S * CAP);
+            fe->nB_b[k] = carve<int>(p, S);
+        }
+        fe->xyB = fe->xyB_b[0];
+        fe->obj = fe->obj_b[0];
+        fe->nB = fe->nB_b[0];
         bytes = (size_t)(p - (pass == 0 ? dbase0 : (char*)fe->dmem)) + 256;
     }
     (void)hipMemsetAsync(fe->dmem, 0, bytes, ctx->stream);
-    // host mirrors
-    size_t hbytes = 0;
+    // host mirrors (pinned): both parities of the full point copies
     {
-        char* p = nullptr;
-        auto add = [&](size_t b) { p = (char*)(((uintptr_t)p + 255) & ~(uintptr_t)255) + b; };
-        add(sizeof(int) * S * 4);
-        add(sizeof(long long) * S);
-        add(sizeof(float) * 5 * (size_t)S * CAP);
-        add(sizeof(float) * 5 * (size_t)S * CAP);  // the second parity of h_xyB / h_obj
-        add(sizeof(double) * 12 * (size_t)S * kRansacChunk);
-        add(sizeof(int) * (size_t)S * kRansacChunk);
-        add(sizeof(uint32_t) * (size_t)S * kRansacChunk * fe->WORDS);
-        add(sizeof(uint32_t) * (size_t)S * fe->WORDS);
-        add(sizeof(double) * 60 * (size_t)S);
-        add(sizeof(float) * kSampleFloats * kRansacPrefetch * (size_t)S);
-        add(4096);
-        hbytes = (size_t)p;
-    }
-    if (hipHostMalloc(&fe->hmem, hbytes, hipHostMallocDefault) != hipSuccess) {
-        svo_frontend_destroy(fe);
-        return set_error(ctx, SVO_ERR_HIP, "svo_frontend_create: hipHostMalloc");
-    }
-    {
+        const size_t hb = 2 * (((sizeof(float) * 2 * (size_t)S * CAP + 255) & ~(size_t)255) +
+                               ((sizeof(float) * 3 * (size_t)S * CAP + 255) & ~(size_t)255)) + 4096;
+        if (hipHostMalloc(&fe->hmem, hb, hipHostMallocDefault) != hipSuccess) {
+            svo_frontend_destroy(fe);
+            return set_error(ctx, SVO_ERR_HIP, "svo_frontend_create: hipHostMalloc");
+        }
         char* p = (char*)fe->hmem;
-        fe->h_cnt = carve<int>(p, (size_t)S * kRansacChunk);
         for (int k = 0; k < 2; k++) {
             fe->h_xyB_b[k] = carve<float>(p, 2 * (size_t)S * CAP);
             fe->h_obj_b[k] = carve<float>(p, 3 * (size_t)S * CAP);
         }
         fe->h_xyB = fe->h_xyB_b[0];
         fe->h_obj = fe->h_obj_b[0];
-        fe->h_hyps = carve<double>(p, 12 * (size_t)S * kRansacChunk);
-        fe->h_bits = carve<uint32_t>(p, (size_t)S * kRansacChunk * fe->WORDS);
-
-
-
     }
     // zero-copy scoring buffers (coherent: the kernel's writes are visible to the
     // host once the stream is synchronised)
     {
-        const char* e = std::getenv("SVO_FE_ZEROCOPY");
-        fe->zero_copy = !(e && e[0] == '0');
         const size_t zb = ((sizeof(double) * 12 * (size_t)S * kRansacChunk + 255) & ~(size_t)255) +
                           ((sizeof(uint32_t) * (size_t)S * kRansacChunk * fe->WORDS + 255) & ~(size_t)255) +
                           sizeof(int) * (size_t)S * kRansacChunk + 256;
-        if (fe->zero_copy && hipHostMalloc(&fe->zmem, zb, hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess) {
+        if (hipHostMalloc(&fe->zmem, zb, hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess) {
             fe->zmem = nullptr;
-            fe->zero_copy = false;
+            svo_frontend_destroy(fe);
+            return set_error(ctx, SVO_ERR_HIP, "svo_frontend_create: host-coherent scoring buffers");
         }
-        if (fe->zero_copy) {
-            char* p = (char*)fe->zmem;
-            fe->z_hyps = carve<double>(p, 12 * (size_t)S * kRansacChunk);
-            fe->z_bits = carve<uint32_t>(p, (size_t)S * kRansacChunk * fe->WORDS);
-            fe->z_cnt = carve<int>(p, (size_t)S * kRansacChunk);
-        }
+        char* p = (char*)fe->zmem;
+        fe->z_hyps = carve<double>(p, 12 * (size_t)S * kRansacChunk);
+        fe->z_bits = carve<uint32_t>(p, (size_t)S * kRansacChunk * fe->WORDS);
+        fe->z_cnt = carve<int>(p, (size_t)S * kRansacChunk);
     }
     // host-coherent outputs the kernels write directly (no D2H copies on the
-    // critical path): post-LK counts / iteration sums / RANSAC subsets, the tail's
-    // counts; and the inlier bits the tail and the statistics read (parity pair)
+    // critical path): post-LK counts / iteration sums / RANSAC subsets, the
+    // keyframe's counts; the inlier bits the tail and the statistics read (parity
+    // pair); the keyframe targets the keyframe kernels read
     {
         size_t zb = 0;
         auto add = [&](size_t b) { zb = ((zb + 255) & ~(size_t)255) + b; };
-        add(sizeof(int) * S * 3);
+        add(sizeof(int) * S * 4);
         add(sizeof(long long) * S);
         add(sizeof(float) * kSampleFloats * kRansacPrefetch * (size_t)S);
         add(sizeof(uint32_t) * (size_t)S * fe->WORDS);
@@ -897,6 +856,7 @@ int svo_frontend_create(svo_ctx* ctx, const svo_frontend_config* cfg, svo_fronte
         fe->h_nB = carve<int>(p, S);
         fe->h_nA = carve<int>(p, S);
         fe->h_added = carve<int>(p, S);
+        fe->h_target = carve<int>(p, S);
         fe->h_itsum = carve<long long>(p, S);
         fe->h_samp = carve<float>(p, (size_t)kSampleFloats * kRansacPrefetch * S);
         fe->h_best_b[0] = carve<uint32_t>(p, (size_t)S * fe->WORDS);
@@ -931,25 +891,12 @@ int svo_frontend_create(svo_ctx* ctx, const svo_frontend_config* cfg, svo_fronte
     }
     fe->rs.resize(S);
     fe->pred_iters.assign(S, 0);
+    fe->kf_prev.assign(S, 1);
     {
-        const char* e = std::getenv("SVO_FE_CHUNK0");
-        fe->chunk0 = e ? std::max(1, std::atoi(e)) : 2;
-        const char* pe = std::getenv("SVO_FE_PYR_EARLY");
-        fe->pyr_early = !(pe && pe[0] == '0');
-        const char* fe_ = std::getenv("SVO_FE_FAST_EARLY");
-        fe->fast_early = !(fe_ && fe_[0] == '0');
-        const char* ff = std::getenv("SVO_FE_FAST_FIRST");
-        fe->fast_first = ff && ff[0] == '1';
         const char* fp = std::getenv("SVO_FE_FAST_PRE");
-        fe->fast_pre = fp && fp[0] ? std::max(0, std::min(2, std::atoi(fp))) : 1;
-        const char* pp = std::getenv("SVO_FE_PIPE");
-        fe->pipe = !(pp && pp[0] == '0');
+        fe->fast_pre = fp && fp[0] == '0' ? 0 : 1;
         const char* sm = std::getenv("SVO_FE_SPEC_MARGIN");
         fe->spec_margin = sm ? std::atoi(sm) : 32;
-        const char* se = std::getenv("SVO_FE_SPEC_EARLY");
-        fe->spec_early = se && se[0] == '1';
-        const char* fs = std::getenv("SVO_FE_FAST_SPLIT");
-        fe->fast_split = fs && fs[0] == '1';
     }
     // (on the context stream: a first use of the null stream would take a fifth
     // hardware queue and serialise the step's streams)
@@ -960,10 +907,9 @@ int svo_frontend_create(svo_ctx* ctx, const svo_frontend_config* cfg, svo_fronte
     fe->pose.assign((size_t)S * 6, 0.0);
     // host pool: this rank's share of the node's cores (NUMA-local to its GPU),
     // at most 16 threads (the box's CPU share per GPU) and one per sequence
+    const int world = local_world_env();
     {
-        const char* lr = std::getenv("LOCAL_RANK");
-        const char* lw = std::getenv("LOCAL_WORLD_SIZE");
-        const int rank = lr ? std::atoi(lr) : 0, world = lw ? std::max(1, std::atoi(lw)) : 1;
+        const int rank = local_rank_env();
         int ndev = 0;
         (void)hipGetDeviceCount(&ndev);
         std::vector<int> gnode(world, -1);
@@ -976,99 +922,27 @@ int svo_frontend_create(svo_ctx* ctx, const svo_frontend_config* cfg, svo_fronte
         if (pin) fe->host_cpus = host_cpu_plan(std::min(rank, world - 1), world, gnode.data());
     }
     int nt = c.host_threads > 0 ? c.host_threads
-                                : (fe->host_cpus.empty() ? (int)std::thread::hardware_concurrency() / world_size_env()
+                                : (fe->host_cpus.empty() ? (int)std::thread::hardware_concurrency() / world
                                                          : (int)fe->host_cpus.size());
     nt = std::max(1, std::min({nt, S, 16}));
     fe->pool = new Pool(nt - 1, fe->host_cpus);
     for (auto& e : fe->ev) (void)hipEventCreate(&e);
-    // pipeline slices: contiguous, near-equal sequence ranges
     {
-        // default one slice: two prioritised slices (slice 0's RANSAC overlapping
-        // slice 1's LK) measured within noise of one (+1 % over 3 runs at 64
-        // sequences), and one slice keeps LK a single launch per step
-        int G = c.groups > 0 ? c.groups : 1;
-        G = std::max(1, std::min(G, S));
-        fe->G = G;
-        fe->fast_split = fe->fast_split && G == 1 && c.bucket_size <= 0 && fe->spec_margin >= 0 && !fe->spec_early &&
-                         fe->fast_early && !fe->fast_first;
-        if (!(G == 1 && fe->fast_early && !fe->fast_first && !fe->fast_split)) fe->fast_pre = 0;
-        fe->g0.resize(G);
-        fe->gn.resize(G);
-        for (int g = 0; g < G; g++) {
-            fe->g0[g] = (int)((int64_t)S * g / G);
-            fe->gn[g] = (int)((int64_t)S * (g + 1) / G) - fe->g0[g];
-        }
         int least = 0, greatest = 0;
         (void)hipDeviceGetStreamPriorityRange(&least, &greatest);
-        // slice 0 at the highest priority, later slices one level lower: their LKs
-        // run concurrently (no serialisation between slices), slice 0's blocks are
-        // dispatched first and finish first, so its RANSAC overlaps the later LKs
-        fe->gst.assign(G, nullptr);
-        // SVO_FE_SLICE_PRIO=0: every slice at the same (highest) priority
-        const char* spe = std::getenv("SVO_FE_SLICE_PRIO");
-        const bool slice_prio = !(spe && spe[0] == '0');
-        const int normal_pr = std::min(std::max(greatest + 1, greatest), least);
-        // LK ahead (SVO_FE_AHEAD=1, one slice; off by default: measured 61.7k-71.3k
-        // frames/s against 72.1k-73.5k on the KITTI bench -- the step is already
-        // close to GPU-throughput bound (the kernels' solo times add up to more than
-        // the step), and the RANSAC / keyframe / statistics kernels queued beside a
-        // running LK wait for CUs whatever the stream priorities, which puts the
-        // statistics -> fits -> next post-LK chain behind LK instead of beside it).
-        // Its LK stream runs at SVO_FE_LK_PRIO (0 lowest (default), 1 normal, 2
-        // highest) under the keyframe stream (highest).
-        {
-            const char* e = std::getenv("SVO_FE_AHEAD");
-            fe->ahead = G == 1 && e && e[0] == '1';
-        }
-        int lk_pr = greatest;
-        if (fe->ahead) {
-            const char* e = std::getenv("SVO_FE_LK_PRIO");
-            lk_pr = (e && e[0] == '2') ? greatest : (e && e[0] == '1') ? normal_pr : least;
-            if (hipStreamCreateWithPriority(&fe->st_kf, hipStreamNonBlocking, greatest) != hipSuccess) {
-                svo_frontend_destroy(fe);
-                return set_error(ctx, SVO_ERR_HIP, "svo_frontend_create: stream");
-            }
-            (void)hipEventCreateWithFlags(&fe->ev_aplk, hipEventDisableTiming);
-        }
-        for (int g = 0; g < G; g++) {
-            const int pr = fe->ahead ? lk_pr : (g == 0 || !slice_prio) ? greatest : normal_pr;
-            if (hipStreamCreateWithPriority(&fe->gst[g], hipStreamNonBlocking, pr) != hipSuccess) {
-                svo_frontend_destroy(fe);
-                return set_error(ctx, SVO_ERR_HIP, "svo_frontend_create: stream");
-            }
-        }
-        // FAST stream priority (SVO_FE_FAST_PRIO: 0 lowest (default: FAST fills the
-        // CUs LK leaves idle and the post-LK window), 1 normal, 2 highest)
-        // (LK ahead: highest by default -- the speculative stereo LK on it is on
-        // the keyframe's critical path, LK is not)
-        int fast_pr = fe->ahead ? greatest : least;
-        if (const char* e = std::getenv("SVO_FE_FAST_PRIO"))
-            fast_pr = e[0] == '2' ? greatest : e[0] == '1' ? normal_pr : least;
-        if (hipStreamCreateWithPriority(&fe->st_fast, hipStreamNonBlocking, fast_pr) != hipSuccess) {
+        // the LK stream at the highest priority (its chain is the step's critical
+        // path), the FAST stream at the lowest (FAST fills the CUs LK leaves idle
+        // and the post-LK window; the speculative stereo LK behind it is ready
+        // long before the keyframe needs it)
+        if (fe_make_stream(&fe->st_lk, greatest) != hipSuccess || fe_make_stream(&fe->st_fast, least) != hipSuccess ||
+            hipStreamCreateWithFlags(&fe->st_copy, hipStreamNonBlocking) != hipSuccess) {
             svo_frontend_destroy(fe);
             return set_error(ctx, SVO_ERR_HIP, "svo_frontend_create: stream");
         }
-        fe->ev_sync.assign(2 + 2 * G, nullptr);
-        for (auto& e : fe->ev_sync) (void)hipEventCreateWithFlags(&e, hipEventDisableTiming);
-        (void)hipEventCreateWithFlags(&fe->ev_stats, hipEventDisableTiming);
-        (void)hipEventCreateWithFlags(&fe->ev_gathered, hipEventDisableTiming);
-        fe->ev_tail.assign(G, nullptr);
-        fe->lk_queued.assign(G, -1);
-        for (auto& e : fe->ev_tail) (void)hipEventCreateWithFlags(&e, hipEventDisableTiming);
-        for (auto& e : fe->ev_full_b) (void)hipEventCreateWithFlags(&e, hipEventDisableTiming);
+        for (hipEvent_t* e : {&fe->ev_pyr, &fe->ev_fast, &fe->ev_lk, &fe->ev_post, &fe->ev_tail, &fe->ev_stats,
+                              &fe->ev_pyr_r, &fe->ev_pre, &fe->ev_fdone, &fe->ev_full_b[0], &fe->ev_full_b[1]})
+            (void)hipEventCreateWithFlags(e, hipEventDisableTiming);
         fe->ev_full = fe->ev_full_b[0];
-        (void)hipEventCreateWithFlags(&fe->ev_pyr_r, hipEventDisableTiming);
-        (void)hipEventCreateWithFlags(&fe->ev_pre, hipEventDisableTiming);
-        (void)hipEventCreateWithFlags(&fe->ev_fdone, hipEventDisableTiming);
-        // 4 hardware queues: with several slices (or the keyframe stream of LK
-        // ahead) the copy stream's work shares the pyramid stream
-        if (G > 1 || fe->ahead) {
-            fe->st_copy = ctx->stream;
-            fe->st_copy_owned = false;
-        } else if (hipStreamCreateWithFlags(&fe->st_copy, hipStreamNonBlocking) != hipSuccess) {
-            svo_frontend_destroy(fe);
-            return set_error(ctx, SVO_ERR_HIP, "svo_frontend_create: stream");
-        }
     }
     SVO_HIP(ctx, hipMemcpyAsync(fe->d_desc, fe->desc_host.data(), sizeof(PyrDesc) * fe->desc_host.size(),
                                 hipMemcpyHostToDevice, ctx->stream));
@@ -1082,6 +956,11 @@ int svo_frontend_create(svo_ctx* ctx, const svo_frontend_config* cfg, svo_fronte
 void svo_frontend_destroy(svo_frontend* fe) {
     if (!fe) return;
     if (fe->ctx) (void)hipStreamSynchronize(fe->ctx->stream);
+    for (hipStream_t st : {fe->st_lk, fe->st_fast, fe->st_copy})
+        if (st) {
+            (void)hipStreamSynchronize(st);
+            (void)hipStreamDestroy(st);
+        }
     delete fe->pool;
     for (auto* v : {&fe->frames, &fe->frames_r})
         for (auto* f : *v)
@@ -1093,54 +972,20 @@ void svo_frontend_destroy(svo_frontend* fe) {
     if (fe->zout) (void)hipHostFree(fe->zout);
     for (auto& e : fe->ev)
         if (e) (void)hipEventDestroy(e);
-    for (auto& g : fe->gst)
-        if (g) {
-            (void)hipStreamSynchronize(g);
-            (void)hipStreamDestroy(g);
-        }
-    if (fe->st_fast) {
-        (void)hipStreamSynchronize(fe->st_fast);
-        (void)hipStreamDestroy(fe->st_fast);
-    }
-    for (auto& e : fe->ev_sync)
+    for (hipEvent_t e : {fe->ev_pyr, fe->ev_fast, fe->ev_lk, fe->ev_post, fe->ev_tail, fe->ev_stats, fe->ev_pyr_r,
+                         fe->ev_pre, fe->ev_fdone, fe->ev_full_b[0], fe->ev_full_b[1]})
         if (e) (void)hipEventDestroy(e);
-    if (fe->ev_stats) (void)hipEventDestroy(fe->ev_stats);
-    if (fe->ev_pre) (void)hipEventDestroy(fe->ev_pre);
-    if (fe->ev_fdone) (void)hipEventDestroy(fe->ev_fdone);
-    if (fe->st_copy && fe->st_copy_owned) {
-        (void)hipStreamSynchronize(fe->st_copy);
-        (void)hipStreamDestroy(fe->st_copy);
-    }
-    if (fe->ev_gathered) (void)hipEventDestroy(fe->ev_gathered);
-    for (auto& e : fe->ev_tail)
-        if (e) (void)hipEventDestroy(e);
-    for (auto& e : fe->ev_full_b)
-        if (e) (void)hipEventDestroy(e);
-    if (fe->ev_pyr_r) (void)hipEventDestroy(fe->ev_pyr_r);
-    if (fe->st_kf) {
-        (void)hipStreamSynchronize(fe->st_kf);
-        (void)hipStreamDestroy(fe->st_kf);
-    }
-    if (fe->ev_aplk) (void)hipEventDestroy(fe->ev_aplk);
     if (fe->score_map) (void)hipFree(fe->score_map);
     delete fe;
 }
 
-// Drop a prefetched first half (its inputs are about to change): let every
-// stream finish and forget it; the frame pyramids built ahead go too.
+// Let every stream finish and forget the work queued ahead (a prefetched first
+// half, a pyramid built ahead, a pre-detection): their inputs are about to
+// change (new frames, re-init).
 static int fe_drain(svo_frontend* fe) {
     svo_ctx* ctx = fe->ctx;
-    if (fe->front_t < 0 && fe->ahead_t < 0) return SVO_OK;
-    for (auto& g : fe->gst) SVO_HIP(ctx, hipStreamSynchronize(g));
-    if (fe->st_kf) SVO_HIP(ctx, hipStreamSynchronize(fe->st_kf));
-    if (fe->st_fast) SVO_HIP(ctx, hipStreamSynchronize(fe->st_fast));
-    if (fe->st_copy) SVO_HIP(ctx, hipStreamSynchronize(fe->st_copy));
-    SVO_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    for (hipStream_t st : {fe->st_lk, fe->st_fast, fe->st_copy, ctx->stream}) SVO_HIP(ctx, hipStreamSynchronize(st));
     fe->front_t = -1;
-    fe->pyr_ready = -1;
-    fe->ahead_t = -1;  // the next step tracks the kept + appended list (xyA) again
-    fe->spec_t = -1;
-    std::fill(fe->lk_queued.begin(), fe->lk_queued.end(), -1);
     return SVO_OK;
 }
 
@@ -1193,6 +1038,7 @@ int svo_frontend_prebuild_pyramids(svo_frontend* fe) {
 // Tracking::startStereo's first frame (R:src/tracking.cpp:233-235): extractFeatures
 // (FAST without a mask: prevFrame == frame has no features yet), stereo match,
 // triangulation with the identity pose (Frame's default), capped at n_features.
+// Frame t0 is a keyframe under either rule (nextFrame: lastFrameID == 0).
 int svo_frontend_init(svo_frontend* fe, int t0) {
     if (!fe || t0 < 0) return SVO_ERR_ARG;
     int rd = fe_drain(fe);
@@ -1204,6 +1050,8 @@ int svo_frontend_init(svo_frontend* fe, int t0) {
     fe->boxes_binned = false;
     svo_ctx* ctx = fe->ctx;
     const int S = fe->S;
+    for (int s = 0; s < S; s++) fe->h_target[s] = fe->cfg.n_features;
+    std::fill(fe->kf_prev.begin(), fe->kf_prev.end(), 1);
     const PyrDesc* dcur = fe->d_desc + (size_t)(t0 % fe->T) * S;
     SVO_HIP(ctx, launch_pyramid_scharr_batched(dcur, fe->d_der + (size_t)(t0 % 3) * S, S, fe->W, fe->H, fe->nlev,
                                                ctx->stream));
@@ -1216,10 +1064,10 @@ int svo_frontend_init(svo_frontend* fe, int t0) {
     int rc = fe_fast_and_bucket(fe, dcur, false, ctx->stream);
     if (rc) return rc;
     // n_in = nA (zero): nothing to compact, the candidates fill the set
-    rc = fe_keyframe(fe, t0, 0, S, fe->nA, nullptr, fe->xyA, fe->midA, fe->cfg.n_features, ctx->stream);
+    rc = fe_keyframe(fe, t0, fe->nA, nullptr, fe->xyA, fe->midA, fe->cfg.n_features, ctx->stream);
     if (rc) return rc;
     for (int s = 0; s < S; s++) fe_set_pose(fe, s, false, nullptr, nullptr);
-    SVO_HIP(ctx, launch_finalize_map(fe_pending(fe, 0), S, ctx->stream));
+    SVO_HIP(ctx, launch_finalize_map(fe_pending(fe), S, ctx->stream));
     SVO_HIP(ctx, hipStreamSynchronize(ctx->stream));
     ph_collect(fe);
     std::fill(fe->pose.begin(), fe->pose.end(), 0.0);
@@ -1238,183 +1086,52 @@ static LKParams fe_temporal_params(const svo_frontend* fe) {
     lp.flags = c.lk_flags & ~SVO_LK_USE_INITIAL_FLOW;
     lp.min_eig = (float)c.min_eig;
     lp.want_err = 0;
-    {
-        static const bool quad_off = [] {
-            const char* e = std::getenv("SVO_LK_QUAD");
-            return e && e[0] == '0';
-        }();
-        lp.quad = quad_off ? 0 : 1;
-        static const int multi = [] {
-            const char* e = std::getenv("SVO_LK_MULTI");
-            return e ? std::atoi(e) : 41;
-        }();
-        lp.multi = multi;
-    }
+    lk_apply_env(lp);
     return lp;
 }
 
-static int fe_lk_slice(svo_frontend* fe, int t, int g, const float* xy_in, const int* n_in);
-
-// LK ahead: LK(t+1) of the features step t's keyframe appended (ap_xy, added[s]
-// of them, at most max_n), on the keyframe stream right behind it; ev_aplk
-// marks it done for post_lk(t+1)
-static int fe_lk_new(svo_frontend* fe, int t1, int max_n) {
-    svo_ctx* ctx = fe->ctx;
-    const int S = fe->S;
-    hipStream_t sk = fe->st_kf;
-    const PyrDesc* dprev = fe->d_desc + (size_t)((t1 - 1) % fe->T) * S;
-    const PyrDesc* dcur = fe->d_desc + (size_t)(t1 % fe->T) * S;
-    const LKParams lp = fe_temporal_params(fe);
-    LKBatch lb{dprev, dcur, fe->d_der + (size_t)((t1 - 1) % 3) * S, fe->ap_xy, fe->ap_next, fe->ap_status, nullptr,
-               fe->ap_iters, fe->added, 0, fe->CAP};
-    SVO_HIP(ctx, hipStreamWaitEvent(sk, fe->ev_sync[0], 0));  // frame t1's pyramid
-    int slot;
-    ph_begin(fe, PH_LK_NEW, sk, &slot);
-    SVO_HIP(ctx, launch_lk(lb, S, std::min(std::max(max_n, 0), fe->CAP), lp, sk));
-    ph_end(fe, sk, slot);
-    SVO_HIP(ctx, hipEventRecord(fe->ev_aplk, sk));
-    return SVO_OK;
-}
-
-// post_lk's arguments for the sequences [a, a + n) of this step's parity buffers
-static PostLkBatch fe_post_lk_batch(svo_frontend* fe, int a) {
-    const int CAP = fe->CAP;
-    const size_t sfl = (size_t)kSampleFloats * kRansacPrefetch;
-    return PostLkBatch{fe->nA + a, fe->status + (size_t)a * CAP, fe->next_xy + 2 * (size_t)a * CAP,
-                       fe->midA + (size_t)a * CAP, fe->iters + (size_t)a * CAP, fe->xyB + 2 * (size_t)a * CAP,
-                       fe->midB + (size_t)a * CAP, fe->nB + a, fe_pending(fe, a), fe->obj + 3 * (size_t)a * CAP,
-                       CAP, kRansacPrefetch, fe->h_nB + a, fe->h_itsum + a, fe->h_samp + sfl * a};
-}
-
-// post_lk of step t whose LK ran ahead (fe_lk_ahead at step t-1): the first
-// input is step t-1's tracked list (its parity of xyB / nB, tracks in next_xy,
-// ids in midB, compacted in place) filtered by its inlier bits, the second the
-// keyframe's appended features (ap_*)
-static PostLkBatch fe_post_lk_ahead_batch(svo_frontend* fe, int t) {
-    const int p = (t - 1) & 1;
-    PostLkBatch b = fe_post_lk_batch(fe, 0);
-    b.n_in = fe->nB_b[p];
-    b.mid_in = fe->midB;
-    b.keep_bits = fe->h_best_b[p];
-    b.words_cap = fe->WORDS;
-    b.n2 = fe->added;
-    b.xy2 = fe->ap_next;
-    b.status2 = fe->ap_status;
-    b.iters2 = fe->ap_iters;
-    return b;
-}
-
-// Post-LK of step t on every slice, queued once the previous step's poses are
-// set (fe_finish_fits): its keyframe points go to the world frame first.
+// Post-LK of step t, queued once the previous step's poses are set
+// (fe_finish_fits): its keyframe points go to the world frame first. The
+// keyframe's stereo matches go out right behind it, speculatively, beside the
+// host's RANSAC.
 static int fe_post(svo_frontend* fe, int t) {
-    static const bool trace_on = [] {
-        const char* e = std::getenv("SVO_FE_TRACE");
-        return e && e[0] == '1';
-    }();
     const auto t0 = std::chrono::steady_clock::now();
     auto TP = [&](const char* label) {
-        if (trace_on)
+        if (trace_on())
             std::fprintf(stderr, "[fe post t=%d] %8.1f us  %s\n", t,
                          std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count(), label);
     };
     svo_ctx* ctx = fe->ctx;
-    const int G = fe->G;
+    const int CAP = fe->CAP;
+    hipStream_t sl = fe->st_lk;
     int slot;
-    const bool ahead = fe->ahead_t == t;  // (one slice)
-    for (int g = 0; g < G; g++) {
-        hipStream_t sg = fe->gst[g];
-        if (ahead) SVO_HIP(ctx, hipStreamWaitEvent(sg, fe->ev_aplk, 0));
-        ph_begin(fe, PH_POST, sg, &slot);
-        SVO_HIP(ctx, launch_post_lk(ahead ? fe_post_lk_ahead_batch(fe, t) : fe_post_lk_batch(fe, fe->g0[g]), fe->gn[g],
-                                    sg));
-        ph_end(fe, sg, slot);
-        SVO_HIP(ctx, hipEventRecord(fe->ev_sync[3 + 2 * g], sg));
-        TP("post_lk launched");
-        // the keyframe's stereo matches, speculatively, beside this slice's RANSAC
-        if (fe->fast_split) {
-            // FAST's scan + emit of frame t behind the post-LK, writing the first
-            // spec corners to the stereo input, then their stereo LK
-            hipStream_t sf = fe->st_fast;
-            SVO_HIP(ctx, hipStreamWaitEvent(sf, fe->ev_sync[3 + 2 * g], 0));
-            FastDetBatch fb = fe_fast_batch(fe, fe->d_desc + (size_t)(t % fe->T) * fe->S, true);
-            fb.spec_tracked = fe->nB;
-            fb.spec_map_n = fe->map_n;
-            fb.spec_target = fe->cfg.n_features;
-            fb.spec_margin = fe->spec_margin;
-            fb.spec_cap = fe->CAP;
-            fb.spec_map_cap = fe->MAPCAP;
-            fb.spec_xy = fe->st_xy;
-            fb.spec_n = fe->spec_n;
-            SVO_HIP(ctx, launch_fast_detect(fb, fe->S, fe->W, fe->H, fe->cfg.fast_threshold, fe->cfg.fast_nonmax, sf,
-                                            kFastCollect));
-            const int max_spec = std::min(fe->cfg.n_features + fe->spec_margin, fe->CAP);
-            const int hint = std::min(fe->CAP, fe->cfg.n_features - fe->min_tracked + fe->spec_margin + 32);
-            int rq = fe_stereo_lk(fe, t, 0, fe->S, fe->spec_n, max_spec, sf, hint);
-            if (rq) return rq;
-            SVO_HIP(ctx, hipEventRecord(fe->ev_sync[1], sf));
-        } else if (fe->spec_margin >= 0 && fe->spec_t != t) {
-            int rq = fe_queue_spec(fe, t, fe->g0[g], fe->gn[g],
-                                   std::min(fe->cfg.n_features + fe->spec_margin, fe->CAP), fe->ev_sync[3 + 2 * g],
-                                   fe->nB, fe->spec_margin);
-            if (rq) return rq;
-        }
-        TP("spec stereo launched");
+    PostLkBatch pb{fe->nA, fe->status, fe->next_xy, fe->midA, fe->iters, fe->xyB, fe->midB, fe->nB, fe_pending(fe),
+                   fe->obj, CAP, kRansacPrefetch, fe->h_nB, fe->h_itsum, fe->h_samp};
+    ph_begin(fe, PH_POST, sl, &slot);
+    SVO_HIP(ctx, launch_post_lk(pb, fe->S, sl));
+    ph_end(fe, sl, slot);
+    SVO_HIP(ctx, hipEventRecord(fe->ev_post, sl));
+    TP("post_lk launched");
+    if (fe->spec_margin >= 0) {
+        int rq = fe_queue_spec(fe, t);
+        if (rq) return rq;
     }
-    if (fe->fast_pre == 2 && fe->front_fast_t == t) {
-        int rc = fe_queue_pre(fe, t + 1, fe->st_fast);
-        if (rc) return rc;
-    }
-    // every slice's points are gathered once the last slice's post-LK is done
-    SVO_HIP(ctx, hipEventRecord(fe->ev_gathered, fe->gst[G - 1]));
-    // LK ahead: LK(t+1) over these tracked points, right behind the post-LK (frame
-    // t+1's pyramid went out with this step's front half)
-    if (fe->ahead && t + 1 < fe->T && fe->pyr_ready == t + 1) {
-        int rl = fe_lk_slice(fe, t + 1, 0, fe->xyB, fe->nB);
-        if (rl) return rl;
-        fe->ahead_t = t + 1;
-        TP("lk ahead launched");
-    }
-    for (int g = 0; g + 1 < G; g++) SVO_HIP(ctx, hipStreamWaitEvent(fe->st_copy, fe->ev_sync[3 + 2 * g], 0));
+    TP("spec stereo launched");
     // the full point set for the final fits / long RANSAC runs, on the copy stream
     // (parity buffers: the previous step's fits still read theirs)
     return fe_queue_full(fe);
-}
-
-// Temporal LK of step t (frame t-1 -> t, trackFrames R:src/tracking.cpp:154-179)
-// for slice g on its stream, behind the pyramid of frame t (ev_sync[0]).
-static int fe_lk_slice(svo_frontend* fe, int t, int g, const float* xy_in, const int* n_in) {
-    svo_ctx* ctx = fe->ctx;
-    const int S = fe->S, CAP = fe->CAP;
-    const PyrDesc* dprev = fe->d_desc + (size_t)((t - 1) % fe->T) * S;
-    const PyrDesc* dcur = fe->d_desc + (size_t)(t % fe->T) * S;
-    const LKParams lp = fe_temporal_params(fe);
-    const int a = fe->g0[g], n = fe->gn[g];
-    hipStream_t sg = fe->gst[g];
-    const int mp = CAP;  // grid bound: the host counts of the previous tail may not be back yet
-    SVO_HIP(ctx, hipStreamWaitEvent(sg, fe->ev_sync[0], 0));
-    LKBatch lb{dprev + a, dcur + a, fe->d_der + (size_t)((t - 1) % 3) * S + a, xy_in + 2 * (size_t)a * CAP,
-               fe->next_xy + 2 * (size_t)a * CAP, fe->status + (size_t)a * CAP, nullptr,
-               fe->iters + (size_t)a * CAP, n_in + a, 0, CAP};
-    int slot;
-    ph_begin(fe, PH_LK, sg, &slot);
-    SVO_HIP(ctx, launch_lk(lb, n, mp, lp, sg));
-    ph_end(fe, sg, slot);
-    SVO_HIP(ctx, hipEventRecord(fe->ev_sync[2 + 2 * g], sg));
-    fe->lk_queued[g] = t;
-    return SVO_OK;
 }
 
 // First half of a step (enqueue only, no host waits): the previous step's side
 // work if still pending, the pyramid of frame t if not built ahead, temporal LK,
 // FAST, the right pyramid of frame t and frame t+1's left pyramid.
 // svo_frontend_step enqueues the next step's first half right after its own
-// tail, so the GPU goes on with LK while the caller is between steps.
-static int fe_front_lk(svo_frontend* fe, int t) {
+// keyframe, so the GPU goes on with LK while the caller is between steps.
+static int fe_front(svo_frontend* fe, int t) {
     svo_ctx* ctx = fe->ctx;
     hipStream_t st0 = ctx->stream;
-    const int S = fe->S, G = fe->G;
+    const int S = fe->S;
     const PyrDesc* dcur = fe->d_desc + (size_t)(t % fe->T) * S;
-    hipEvent_t ev_pyr = fe->ev_sync[0];
     int slot;
     // this step's parity buffers (the previous step's stay with its side work)
     fe->xyB = fe->xyB_b[t & 1];
@@ -1427,8 +1144,7 @@ static int fe_front_lk(svo_frontend* fe, int t) {
     fe->full_queued = false;
     // 0. the previous step's SQPnP statistics and the binning of the FAST mask's
     //    box centres (frame t-1's features) normally went out at the end of that
-    //    step, ahead of this step's LK (a kernel queued beside LK waits for it:
-    //    LK leaves no registers free); only after init / a reset are they queued here
+    //    step, ahead of this step's LK; only after init / a reset are they queued here
     {
         int rq = fe_queue_stats(fe);
         if (rq) return rq;
@@ -1437,159 +1153,112 @@ static int fe_front_lk(svo_frontend* fe, int t) {
         fe->boxes_binned = false;
     }
     // 1. pyramid of frame t and its Scharr derivative pyramid (used when frame
-    //    t is the prev image of the next step; OpenCV recomputes it per call)
-    //    (built ahead by the previous step's fe_front_rest, which recorded ev_pyr)
+    //    t is the prev image of the next step; OpenCV recomputes it per call),
+    //    normally built ahead by the previous step's front half
     if (fe->pyr_ready != t) {
         ph_begin(fe, PH_PYR, st0, &slot);
         SVO_HIP(ctx, launch_pyramid_scharr_batched(dcur, fe->d_der + (size_t)(t % 3) * S, S, fe->W, fe->H, fe->nlev,
                                                    st0));
         ph_end(fe, st0, slot);
-        SVO_HIP(ctx, hipEventRecord(ev_pyr, st0));
+        SVO_HIP(ctx, hipEventRecord(fe->ev_pyr, st0));
     }
-
-    // 2'. SVO_FE_FAST_FIRST=1: FAST(t) (mask around frame t-1's features + detection,
-    //     step 3b below) submitted ahead of the LK instead of behind it: same FAST
-    //     stream, so it stays ordered behind the box binning of frame t-1's features
-    if (fe->fast_early && fe->fast_first) {
+    // 2. temporal LK (trackFrames, frame t-1 -> t) behind frame t's pyramid
+    {
+        const LKParams lp = fe_temporal_params(fe);
+        const PyrDesc* dprev = fe->d_desc + (size_t)((t - 1) % fe->T) * S;
+        hipStream_t sl = fe->st_lk;
+        SVO_HIP(ctx, hipStreamWaitEvent(sl, fe->ev_pyr, 0));
+        LKBatch lb{dprev, dcur, fe->d_der + (size_t)((t - 1) % 3) * S, fe->xyA, fe->next_xy, fe->status, nullptr,
+                   fe->iters, fe->nA, 0, fe->CAP};
+        ph_begin(fe, PH_LK, sl, &slot);
+        // grid bound CAP: the host counts of the previous keyframe may not be back yet
+        SVO_HIP(ctx, launch_lk(lb, S, fe->CAP, lp, sl));
+        ph_end(fe, sl, slot);
+        SVO_HIP(ctx, hipEventRecord(fe->ev_lk, sl));
+    }
+    // 3. mask around frame t-1's features (the reference masks with prevFrame's
+    //    features, R:src/tracking.cpp:77) + FAST/bucket on frame t, whole batch:
+    //    independent of this step's LK and pose, so it is queued right behind the
+    //    LK on the low-priority FAST stream, where it fills the CUs the LK's last
+    //    waves leave idle and the post-LK window; the keyframe waits for it
+    {
         hipStream_t sf = fe->st_fast;
-        int rc = fe_fast_and_bucket(fe, dcur, true, sf, true, kFastAll);
-        if (rc) return rc;
-        SVO_HIP(ctx, hipEventRecord(fe->ev_sync[1], sf));
-    }
-    // 3. per slice: temporal LK (trackFrames) -- unless the pipelined schedule
-    //    already queued it behind the slice's previous keyframe (fe_lk_slice)
-    for (int g = 0; g < G; g++) {
-        if (fe->lk_queued[g] == t) continue;
-        int rl = fe_lk_slice(fe, t, g, fe->xyA, fe->nA);
-        if (rl) return rl;
-    }
-    // 3b. mask around frame t-1's features (the reference masks with prevFrame's
-    //     features, R:src/tracking.cpp:77) + FAST/bucket on frame t, whole batch:
-    //     independent of this step's LK and pose, so it is queued right behind the
-    //     LK on the low-priority FAST stream, where it fills the CUs the LK's last
-    //     waves leave idle and the post-LK window; the tail waits for it
-    if (fe->fast_early && !fe->fast_first) {
-        hipStream_t sf = fe->st_fast;
-        int stage = fe->fast_split ? kFastDetect : kFastAll;
+        int stage = kFastAll;
         if (fe->fast_pre && fe->pre_t == t) {
-            // SVO_FE_FAST_PRE: frame t was detected (unmasked) during step t-1; only the
-            // box mask of frame t-1's features, the recount, scan and emit remain
+            // frame t was detected (unmasked) during step t-1; only the box mask of
+            // frame t-1's features, the recount, scan and emit remain
             SVO_HIP(ctx, hipStreamWaitEvent(sf, fe->ev_pre, 0));
             stage = kFastBoxes;
         }
         fe->pre_t = -1;
         int rc = fe_fast_and_bucket(fe, dcur, true, sf, true, stage);
         if (rc) return rc;
-        SVO_HIP(ctx, hipEventRecord(fe->ev_sync[1], sf));
-        if (fe->fast_pre) {
-            SVO_HIP(ctx, hipEventRecord(fe->ev_fdone, sf));
-            fe->front_fast_t = t;
-        }
+        SVO_HIP(ctx, hipEventRecord(fe->ev_fast, sf));
+        SVO_HIP(ctx, hipEventRecord(fe->ev_fdone, sf));
     }
-    // 3'. frame t+1's pyramid + Scharr + borders, queued beside this LK: the
-    //     derivative pyramids are triple-buffered (frame f in f % 3), so nothing
-    //     this step reads is overwritten, and the memory-bound pyramid shares the
-    //     GPU with the VALU-bound LK instead of the post-LK window
-    // 3''. the right frame t's pyramid (no derivatives: it is the stereo LK's next
-    //      image), beside LK; the keyframe's stereo LK waits for ev_pyr_r
+    // 4. the right frame t's pyramid (no derivatives: it is the stereo LK's next
+    //    image), beside LK; the keyframe's stereo LK waits for ev_pyr_r
     ph_begin(fe, PH_PYR_R, st0, &slot);
     SVO_HIP(ctx, launch_pyramid_batched(fe->d_desc_r + (size_t)(t % fe->T) * S, S, fe->W, fe->H, fe->nlev, st0));
     ph_end(fe, st0, slot);
     SVO_HIP(ctx, hipEventRecord(fe->ev_pyr_r, st0));
-    // 3c. the keyframe's stereo matches, speculatively, right behind FAST (and frame
-    //     t's left / right pyramids: fe_stereo_lk waits for ev_pyr_r, queued behind
-    //     both): the keyframe takes the first n_features - kept candidates and kept
-    //     <= n_before (the features LK(t) tracks), so the first n_features -
-    //     n_before + margin cover the take whenever LK and RANSAC together lose at
-    //     most `margin` points; fe_queue_spec re-records ev_sync[1]
-    //     (the margin grows by the last step's largest LK loss, which it now covers)
-    if (fe->fast_early && !fe->fast_first && fe->spec_margin >= 0 && fe->spec_early) {
-        const int margin = std::min(fe->spec_margin + fe->lk_loss_max, fe->CAP);
-        int rc = fe_queue_spec(fe, t, 0, S, std::min(fe->cfg.n_features + margin, fe->CAP), nullptr, fe->nA, margin);
-        if (rc) return rc;
-        fe->spec_t = t;
-        fe->spec_margin_t = margin;
-    }
-    if (fe->pyr_early) {
+    // 5. frame t+1's pyramid + Scharr + borders, queued beside this LK: the
+    //    derivative pyramids are triple-buffered (frame f in f % 3), so nothing
+    //    this step reads is overwritten, and the memory-bound pyramid shares the
+    //    GPU with the VALU-bound LK instead of the post-LK window
+    if (t + 1 < fe->T) {
         const int tn = t + 1;
         const PyrDesc* dnext = fe->d_desc + (size_t)(tn % fe->T) * S;
         ph_begin(fe, PH_PYR, st0, &slot);
         SVO_HIP(ctx, launch_pyramid_scharr_batched(dnext, fe->d_der + (size_t)(tn % 3) * S, S, fe->W, fe->H,
                                                    fe->nlev, st0));
         ph_end(fe, st0, slot);
-        SVO_HIP(ctx, hipEventRecord(ev_pyr, st0));
+        SVO_HIP(ctx, hipEventRecord(fe->ev_pyr, st0));
         fe->pyr_ready = tn;
-    }
-    // SVO_FE_FAST_PRE: frame t+1's FAST detection + NMS without the box mask (the
-    // mask drops corners after NMS, so it can wait for frame t's features), on the
-    // pyramid stream once this step's emit has consumed the row words: it fills
-    // the CUs the latency-bound post-LK / stereo chain leaves, and step t+1 keeps
-    // only the box filter, scan and emit behind its LK
-    if (fe->fast_pre == 1) {
-        int rc = fe_queue_pre(fe, t + 1, st0);
-        if (rc) return rc;
+        // 6. FAST pre-detection of frame t+1 (fe_queue_pre), behind its pyramid:
+        //    it fills the CUs the latency-bound post-LK / stereo chain leaves
+        if (fe->fast_pre) {
+            int rc = fe_queue_pre(fe, tn);
+            if (rc) return rc;
+        }
     }
     return SVO_OK;
 }
 
-// The rest of a step's first half: frame t+1's pyramid (SVO_FE_PYR_EARLY=0) and
-// FAST (SVO_FE_FAST_EARLY=0) after every LK of the step.
-static int fe_front_rest(svo_frontend* fe, int t) {
-    svo_ctx* ctx = fe->ctx;
-    hipStream_t st0 = ctx->stream;
-    const int S = fe->S, G = fe->G;
-    const PyrDesc* dcur = fe->d_desc + (size_t)(t % fe->T) * S;
-    hipEvent_t ev_fast = fe->ev_sync[1];
-    int slot;
-    if (!fe->pyr_early) {
-        fe->pyr_ready = -1;
-        const int tn = t + 1;
-        const PyrDesc* dnext = fe->d_desc + (size_t)(tn % fe->T) * S;
-        SVO_HIP(ctx, hipStreamWaitEvent(st0, fe->ev_sync[2 + 2 * (G - 1)], 0));
-        ph_begin(fe, PH_PYR, st0, &slot);
-        SVO_HIP(ctx, launch_pyramid_scharr_batched(dnext, fe->d_der + (size_t)(tn % 3) * S, S, fe->W, fe->H,
-                                                   fe->nlev, st0));
-        ph_end(fe, st0, slot);
-        SVO_HIP(ctx, hipEventRecord(fe->ev_sync[0], st0));
-        fe->pyr_ready = tn;
+// Keyframe targets of step t (read by the speculative stereo prep and the
+// keyframe kernels of this step): n_features on a keyframe, 0 otherwise.
+// SVO_KF_EVERY: every frame. SVO_KF_REFERENCE: Tracking::nextFrame
+// (R:src/tracking.cpp:68-69) -- the previous frame was no keyframe and kept fewer
+// than features_to_track features (h_nA: the count after the previous step).
+static int64_t fe_keyframe_targets(svo_frontend* fe) {
+    const svo_frontend_config& c = fe->cfg;
+    int64_t nkf = 0;
+    for (int s = 0; s < fe->S; s++) {
+        const bool kf = c.keyframe_rule == SVO_KF_EVERY || (!fe->kf_prev[s] && fe->h_nA[s] < c.features_to_track);
+        fe->h_target[s] = kf ? c.n_features : 0;
+        fe->kf_prev[s] = kf ? 1 : 0;
+        nkf += kf ? 1 : 0;
     }
-    if (!fe->fast_early) {
-        hipStream_t sf = fe->st_fast;
-        for (int g = 0; g < G; g++) SVO_HIP(ctx, hipStreamWaitEvent(sf, fe->ev_sync[2 + 2 * g], 0));
-        int rc = fe_fast_and_bucket(fe, dcur, true, sf, true);
-        if (rc) return rc;
-        SVO_HIP(ctx, hipEventRecord(ev_fast, sf));
-    }
-    return SVO_OK;
-}
-
-static int fe_front(svo_frontend* fe, int t) {
-    int rc = fe_front_lk(fe, t);
-    if (rc) return rc;
-    return fe_front_rest(fe, t);
+    return nkf;
 }
 
 int svo_frontend_step(svo_frontend* fe, int t, svo_frontend_stats* stats) {
     if (!fe || t < 1) return SVO_ERR_ARG;
-    // host-side step trace (SVO_FE_TRACE=1): label + microseconds since step start
-    static const bool trace_on = [] {
-        const char* e = std::getenv("SVO_FE_TRACE");
-        return e && e[0] == '1';
-    }();
     // per-round RANSAC inputs / scores on stderr (SVO_FE_DEBUG=1)
     static const bool debug_on = [] {
         const char* e = std::getenv("SVO_FE_DEBUG");
         return e && e[0] == '1';
     }();
+    const bool tr = trace_on();
     const auto trace_t0 = std::chrono::steady_clock::now();
     std::vector<std::pair<const char*, double>> trace;
     auto TP = [&](const char* label) {
-        if (trace_on)
+        if (tr)
             trace.push_back({label, std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() -
                                                                                trace_t0).count()});
     };
     svo_ctx* ctx = fe->ctx;
-    const int S = fe->S, CAP = fe->CAP, G = fe->G;
+    const int S = fe->S, CAP = fe->CAP;
     const svo_frontend_config& c = fe->cfg;
     int slot;
 
@@ -1599,6 +1268,7 @@ int svo_frontend_step(svo_frontend* fe, int t, svo_frontend_stats* stats) {
     }
     fe->front_t = -1;
     TP("front enqueued");
+    const int64_t n_keyframes = fe_keyframe_targets(fe);
     // the previous step's final pose fits: the host does them while the GPU tracks
     // this frame; they set the poses that move the previous keyframe's new map
     // points to the world frame, so this step's post-LK is queued right after
@@ -1609,8 +1279,7 @@ int svo_frontend_step(svo_frontend* fe, int t, svo_frontend_stats* stats) {
         if (rp) return rp;
     }
     TP("post-lk queued");
-    hipEvent_t ev_fast = fe->ev_sync[1];
-    hipStream_t sf = fe->st_fast;
+    hipStream_t sl = fe->st_lk, sf = fe->st_fast;
     int rc = SVO_OK;
     const PyrDesc* dcur = fe->d_desc + (size_t)(t % fe->T) * S;
 
@@ -1623,190 +1292,139 @@ int svo_frontend_step(svo_frontend* fe, int t, svo_frontend_stats* stats) {
     int64_t nhyp = 0, inl = 0;
     std::vector<int> ms(S, 0);
 
-    int lk_loss = 0;  // largest LK loss of this step (n_before - n_tracked), for the next speculation
-    // 4. per slice, in order: calculatePose (RANSAC per sequence, hypotheses
-    //    scored on the GPU), drop outliers (R:src/tracking.cpp:218-229), keyframe
-    for (int g = 0; g < G; g++) {
-        const int a = fe->g0[g], n = fe->gn[g];
-        // the slice stream is idle while the host solves RANSAC -- unless LK(t+1)
-        // runs ahead on it: then scoring and keyframe go on the keyframe stream
-        const bool ahead_next = fe->ahead_t == t + 1;
-        hipStream_t sg = ahead_next ? fe->st_kf : fe->gst[g];
-        hipStream_t sq = sg;
-        TP("ransac begin");
-        auto tw = clk::now();
-        SVO_HIP(ctx, hipEventSynchronize(fe->ev_sync[3 + 2 * g]));
-        TP("lk results on host");
-        ms_wait += ms_since(tw);
-        const bool spec = fe->spec_margin >= 0;  // the stereo LK went out with the post-LK (fe_post)
-        int max_b = 0;
-        bool need_full = false;
-        for (int s = a; s < a + n; s++) {
-            RansacSeq& r = fe->rs[s];
-            r.begin(fe->h_obj + 3 * (size_t)s * CAP, fe->h_xyB + 2 * (size_t)s * CAP, fe->h_nB[s], c.pnp_iterations);
-            r.samp = fe->h_samp + (size_t)kSampleFloats * kRansacPrefetch * s;
-            r.nsamp = kRansacPrefetch;
-            // first chunk sized by the hypotheses the previous frame's outlier ratio
-            // implies (a prediction only: a short chunk costs one more scoring round)
-            // (floor 2, SVO_FE_CHUNK0: a floor of 1 saves an EPnP per sequence when
-            // one hypothesis is predicted, but the extra scoring rounds of the misses
-            // measured slower on the benchmark)
-            r.first_chunk = std::max(fe->chunk0, fe->pred_iters[s]);
-            need_full |= r.direct && !r.done;  // n <= 5: EPnP on all points
-            max_b = std::max(max_b, fe->h_nB[s]);
+    // calculatePose (RANSAC per sequence, hypotheses scored on the GPU), drop
+    // outliers (R:src/tracking.cpp:218-229), keyframe
+    TP("ransac begin");
+    auto tw = clk::now();
+    SVO_HIP(ctx, hipEventSynchronize(fe->ev_post));
+    TP("lk results on host");
+    ms_wait += ms_since(tw);
+    const bool spec = fe->spec_margin >= 0;  // the stereo LK went out with the post-LK (fe_post)
+    bool need_full = false;
+    for (int s = 0; s < S; s++) {
+        RansacSeq& r = fe->rs[s];
+        r.begin(fe->h_obj + 3 * (size_t)s * CAP, fe->h_xyB + 2 * (size_t)s * CAP, fe->h_nB[s], c.pnp_iterations);
+        r.samp = fe->h_samp + (size_t)kSampleFloats * kRansacPrefetch * s;
+        r.nsamp = kRansacPrefetch;
+        // first chunk sized by the hypotheses the previous frame's outlier ratio
+        // implies (a prediction only: a short chunk costs one more scoring round)
+        r.first_chunk = std::max(kChunk0, fe->pred_iters[s]);
+        need_full |= r.direct && !r.done;  // n <= 5: EPnP on all points
+    }
+    bool have_full = false;
+    auto ensure_full = [&]() -> int {
+        if (have_full) return SVO_OK;
+        int rf = fe_queue_full(fe);
+        if (rf) return rf;
+        SVO_HIP(ctx, hipEventSynchronize(fe->ev_full));
+        have_full = true;
+        return SVO_OK;
+    };
+    if (need_full) {
+        int rf = ensure_full();
+        if (rf) return rf;
+    }
+    for (;;) {
+        // sequences still sampling (no pool dispatch once all are done)
+        bool any = false;
+        for (int s = 0; s < S; s++) {
+            any |= !fe->rs[s].done && !fe->rs[s].direct;
+            need_full |= fe->rs[s].next_end() > fe->rs[s].nsamp;
         }
-        bool have_full = false;
-        auto ensure_full = [&]() -> int {
-            if (have_full) return SVO_OK;
-            int rf = fe_queue_full(fe);
-            if (rf) return rf;
-            SVO_HIP(ctx, hipEventSynchronize(fe->ev_full));
-            have_full = true;
-            return SVO_OK;
-        };
-        if (need_full) {
+        if (!any) break;
+        if (need_full) {  // past the prefetched subsets (> 26 hypotheses): rare
             int rf = ensure_full();
             if (rf) return rf;
         }
-        for (;;) {
-            // sequences still sampling (no pool dispatch once all are done)
-            bool any = false;
-            for (int s = a; s < a + n; s++) {
-                any |= !fe->rs[s].done && !fe->rs[s].direct;
-                need_full |= fe->rs[s].next_end() > fe->rs[s].nsamp;
-            }
-            if (!any) break;
-            if (need_full) {  // past the prefetched subsets (> 26 hypotheses): rare
-                int rf = ensure_full();
-                if (rf) return rf;
-            }
-            auto th = clk::now();
-            fe->pool->run(n, [&](int i) { ms[a + i] = fe->rs[a + i].gen_chunk(c.K); });
-            ms_hyp += ms_since(th);
-            TP("hyps generated");
-            int mmax = 0;
-            for (int s = a; s < a + n; s++) mmax = std::max(mmax, ms[s]);
-            if (mmax == 0) break;
-            const bool zc = fe->zero_copy;
-            double* hyp_host = zc ? fe->z_hyps : fe->h_hyps;
-            for (int s = a; s < a + n; s++) {
-                double* dst = hyp_host + 12 * (size_t)s * kRansacChunk;
-                std::memcpy(dst, fe->rs[s].hyp, sizeof(double) * 12 * ms[s]);
-                for (int j = ms[s]; j < mmax; j++) std::memset(dst + 12 * j, 0, sizeof(double) * 12);
-                nhyp += ms[s];
-            }
-            // hypotheses live at stride kRansacChunk; score (and copy back) only the
-            // mmax rows of this round (rows beyond a sequence's own count are ignored)
-            PnpBatch pb{fe->obj + 3 * (size_t)a * CAP, fe->xyB + 2 * (size_t)a * CAP, fe->nB + a, 0, CAP,
-                        fe->hyps + 12 * (size_t)a * kRansacChunk, mmax, nullptr,
-                        fe->bits_all + (size_t)a * kRansacChunk * fe->WORDS, fe->WORDS, fe->cnt + (size_t)a * kRansacChunk};
-            pb.mstride = kRansacChunk;
-            if (zc) {  // the kernel reads the hypotheses and writes bits / counts in host memory
-                pb.hyp = fe->z_hyps + 12 * (size_t)a * kRansacChunk;
-                pb.bits = fe->z_bits + (size_t)a * kRansacChunk * fe->WORDS;
-                pb.cnt = fe->z_cnt + (size_t)a * kRansacChunk;
-            } else {
-                SVO_HIP(ctx, hipMemcpyAsync(fe->hyps + 12 * (size_t)a * kRansacChunk,
-                                            fe->h_hyps + 12 * (size_t)a * kRansacChunk,
-                                            sizeof(double) * 12 * n * kRansacChunk, hipMemcpyHostToDevice, sq));
-            }
-            ph_begin(fe, PH_PNP, sq, &slot);
-            if (zc)
-                SVO_HIP(ctx, launch_pnp_score(pb, n, c.K[0], c.K[4], c.K[2], c.K[5], thr, sq));
-            else
-                SVO_HIP(ctx, launch_pnp_residuals(pb, n, max_b, c.K[0], c.K[4], c.K[2], c.K[5], thr, sq));
-            ph_end(fe, sq, slot);
-            if (!zc) {
-                SVO_HIP(ctx, hipMemcpyAsync(fe->h_cnt + (size_t)a * kRansacChunk, fe->cnt + (size_t)a * kRansacChunk,
-                                            sizeof(int) * n * kRansacChunk, hipMemcpyDeviceToHost, sq));
-                const size_t rowb = sizeof(uint32_t) * (size_t)kRansacChunk * fe->WORDS;
-                SVO_HIP(ctx, hipMemcpy2DAsync(fe->h_bits + (size_t)a * kRansacChunk * fe->WORDS, rowb,
-                                              fe->bits_all + (size_t)a * kRansacChunk * fe->WORDS, rowb,
-                                              sizeof(uint32_t) * (size_t)mmax * fe->WORDS, n, hipMemcpyDeviceToHost,
-                                              sq));
-            }
-            TP("scoring enqueued");
-            SVO_HIP(ctx, hipStreamSynchronize(sq));
-            ms_wait += ms_since(tw);
-            TP("scores on host");
-            // consume is a few compares per hypothesis: cheaper here than a pool dispatch
-            for (int s = a; s < a + n; s++) {
-                if (ms[s] <= 0) continue;
-                int* cnts = (zc ? fe->z_cnt : fe->h_cnt) + (size_t)s * kRansacChunk;
-                const uint32_t* bits = (zc ? fe->z_bits : fe->h_bits) + (size_t)s * kRansacChunk * fe->WORDS;
-                if (debug_on) {
-                    const RansacSeq& r = fe->rs[s];
-                    unsigned hs = 0;
-                    for (int k = 0; k < kSampleFloats * ms[s]; k++) {
-                        unsigned u;
-                        std::memcpy(&u, r.samp + (size_t)kSampleFloats * (r.nh - ms[s]) + k, 4);
-                        hs = hs * 31u + u;
-                    }
-                    std::fprintf(stderr, "[fe dbg t=%d s=%d] n=%d nh=%d m=%d samp=%08x cnt=", t, s, r.n, r.nh, ms[s], hs);
-                    for (int j = 0; j < ms[s]; j++) std::fprintf(stderr, "%d(%d,%.17g) ", cnts[j], (int)r.valid[j], r.hyp[12 * j]);
-                    std::fprintf(stderr, "\n");
+        auto th = clk::now();
+        fe->pool->run(S, [&](int s) { ms[s] = fe->rs[s].gen_chunk(c.K); });
+        ms_hyp += ms_since(th);
+        TP("hyps generated");
+        int mmax = 0;
+        for (int s = 0; s < S; s++) mmax = std::max(mmax, ms[s]);
+        if (mmax == 0) break;
+        for (int s = 0; s < S; s++) {
+            double* dst = fe->z_hyps + 12 * (size_t)s * kRansacChunk;
+            std::memcpy(dst, fe->rs[s].hyp, sizeof(double) * 12 * ms[s]);
+            for (int j = ms[s]; j < mmax; j++) std::memset(dst + 12 * j, 0, sizeof(double) * 12);
+            nhyp += ms[s];
+        }
+        // hypotheses live at stride kRansacChunk; score only the mmax rows of this
+        // round (rows beyond a sequence's own count are ignored). The kernel reads
+        // the hypotheses and writes bits / counts in host-coherent memory.
+        PnpBatch pb{fe->obj, fe->xyB, fe->nB, 0, CAP, fe->z_hyps, mmax, nullptr, fe->z_bits, fe->WORDS, fe->z_cnt};
+        pb.mstride = kRansacChunk;
+        ph_begin(fe, PH_PNP, sl, &slot);
+        SVO_HIP(ctx, launch_pnp_score(pb, S, c.K[0], c.K[4], c.K[2], c.K[5], thr, sl));
+        ph_end(fe, sl, slot);
+        TP("scoring enqueued");
+        SVO_HIP(ctx, hipStreamSynchronize(sl));
+        ms_wait += ms_since(tw);
+        TP("scores on host");
+        // consume is a few compares per hypothesis: cheaper here than a pool dispatch
+        for (int s = 0; s < S; s++) {
+            if (ms[s] <= 0) continue;
+            const int* cnts = fe->z_cnt + (size_t)s * kRansacChunk;
+            const uint32_t* bits = fe->z_bits + (size_t)s * kRansacChunk * fe->WORDS;
+            if (debug_on) {
+                const RansacSeq& r = fe->rs[s];
+                unsigned hs = 0;
+                for (int k = 0; k < kSampleFloats * ms[s]; k++) {
+                    unsigned u;
+                    std::memcpy(&u, r.samp + (size_t)kSampleFloats * (r.nh - ms[s]) + k, 4);
+                    hs = hs * 31u + u;
                 }
-                fe->rs[s].consume(cnts, bits, fe->WORDS, c.pnp_confidence);
+                std::fprintf(stderr, "[fe dbg t=%d s=%d] n=%d nh=%d m=%d samp=%08x cnt=", t, s, r.n, r.nh, ms[s], hs);
+                for (int j = 0; j < ms[s]; j++) std::fprintf(stderr, "%d(%d,%.17g) ", cnts[j], (int)r.valid[j], r.hyp[12 * j]);
+                std::fprintf(stderr, "\n");
             }
-        }
-        // the RANSAC inlier set is the output (R:src/tracking.cpp:218-229); the final
-        // SQPnP-objective fit only refines the pose, from statistics summed on the GPU
-        TP("consumed");
-        auto tf = clk::now();
-        int max_take = 0;  // the keyframe's candidates per sequence are at most n_features - kept
-        bool spec_ok = spec;  // every sequence dropped at most spec_margin points
-        for (int s = a; s < a + n; s++) {
-            RansacSeq& r = fe->rs[s];
-            r.select(c.K, false);
-            const int kept = r.ok ? r.maxGood : (r.n < 4 ? r.n : 0);
-            max_take = std::max(max_take, c.n_features - kept);
-            spec_ok &= fe->spec_t == t ? fe->h_nA[s] - kept <= fe->spec_margin_t : fe->h_nB[s] - kept <= fe->spec_margin;
-            lk_loss = std::max(lk_loss, fe->h_nA[s] - fe->h_nB[s]);
-            uint32_t* b = fe->h_best + (size_t)s * fe->WORDS;
-            std::memset(b, 0, sizeof(uint32_t) * fe->WORDS);
-            if (r.ok) {
-                std::memcpy(b, r.best.data(), sizeof(uint32_t) * r.best.size());
-            } else if (r.n < 4) {
-                // solvePnPRansac would throw (CV_Assert npoints >= 4); keep the frame's
-                // features untouched instead of aborting the batch
-                for (int k = 0; k < r.n; k++) b[k >> 5] |= 1u << (k & 31);
-            }
-            inl += r.ok ? (int64_t)r.maxGood : r.n;
-            fe->pred_iters[s] = (r.ok && r.n > 0)
-                                    ? std::max(1, RansacSeq::predict_iters(c.pnp_confidence,
-                                                                           (double)(r.n - r.maxGood) / r.n,
-                                                                           c.pnp_iterations))
-                                    : 0;
-        }
-        ms_fit += ms_since(tf);
-        TP("selected");
-        // the SQPnP statistics only feed the pose fits, which run during the next
-        // step's LK: they are queued then (fe_queue_stats), off the critical path
-        fe->stats_pending = true;
-        fe->stats_parity = t & 1;
-        // the mask (reads xyA) and FAST (writes kps) must be done before xyA is rewritten / kps read
-        SVO_HIP(ctx, hipStreamWaitEvent(sg, ev_fast, 0));
-        // drop the outliers (the kernel reads the inlier bits from host-coherent
-        // memory), then the keyframe: candidates, stereo LK, triangulation, append
-        rc = fe_keyframe(fe, t, a, n, fe->nB + a, fe->h_best + (size_t)a * fe->WORDS, fe->xyB + 2 * (size_t)a * CAP,
-                         fe->midB + (size_t)a * CAP, max_take, sg, spec_ok, ahead_next);
-        if (rc) return rc;
-        SVO_HIP(ctx, hipEventRecord(fe->ev_tail[g], sg));
-        // LK ahead: the appended features' LK(t+1), which post_lk(t+1) waits for
-        if (ahead_next) {
-            int rl = fe_lk_new(fe, t + 1, max_take);
-            if (rl) return rl;
-        }
-        TP("tail queued");
-        // pipelined schedule: this slice's next LK goes out right behind its
-        // keyframe (frame t+1's pyramid was queued with this step's front), so
-        // the GPU tracks it while the host runs the next slices' RANSAC
-        if (fe->pipe && G > 1 && t + 1 < fe->T && fe->pyr_ready == t + 1) {
-            int rl = fe_lk_slice(fe, t + 1, g, fe->xyA, fe->nA);
-            if (rl) return rl;
+            fe->rs[s].consume(cnts, bits, fe->WORDS, c.pnp_confidence);
         }
     }
-    fe->lk_loss_max = lk_loss;
+    // the RANSAC inlier set is the output (R:src/tracking.cpp:218-229); the final
+    // SQPnP-objective fit only refines the pose, from statistics summed on the GPU
+    TP("consumed");
+    auto tf = clk::now();
+    int max_take = 0;  // the keyframe's candidates per sequence are at most target - kept
+    bool spec_ok = spec;  // every sequence dropped at most spec_margin points
+    for (int s = 0; s < S; s++) {
+        RansacSeq& r = fe->rs[s];
+        r.select(c.K, false);
+        const int kept = r.ok ? r.maxGood : (r.n < 4 ? r.n : 0);
+        max_take = std::max(max_take, fe->h_target[s] - kept);
+        // (a sequence without a keyframe takes nothing: nothing to cover)
+        spec_ok &= fe->h_target[s] == 0 || fe->h_nB[s] - kept <= fe->spec_margin;
+        uint32_t* b = fe->h_best + (size_t)s * fe->WORDS;
+        std::memset(b, 0, sizeof(uint32_t) * fe->WORDS);
+        if (r.ok) {
+            std::memcpy(b, r.best.data(), sizeof(uint32_t) * r.best.size());
+        } else if (r.n < 4) {
+            // solvePnPRansac would throw (CV_Assert npoints >= 4); keep the frame's
+            // features untouched instead of aborting the batch
+            for (int k = 0; k < r.n; k++) b[k >> 5] |= 1u << (k & 31);
+        }
+        inl += r.ok ? (int64_t)r.maxGood : r.n;
+        fe->pred_iters[s] = (r.ok && r.n > 0)
+                                ? std::max(1, RansacSeq::predict_iters(c.pnp_confidence,
+                                                                       (double)(r.n - r.maxGood) / r.n,
+                                                                       c.pnp_iterations))
+                                : 0;
+    }
+    ms_fit += ms_since(tf);
+    TP("selected");
+    // the SQPnP statistics only feed the pose fits, which run during the next
+    // step's LK: they are queued then (fe_queue_stats), off the critical path
+    fe->stats_pending = true;
+    fe->stats_parity = t & 1;
+    // the mask (reads xyA) and FAST (writes kps) must be done before xyA is
+    // rewritten / kps read
+    SVO_HIP(ctx, hipStreamWaitEvent(sl, fe->ev_fast, 0));
+    // drop the outliers (the kernel reads the inlier bits from host-coherent
+    // memory), then the keyframe: candidates, stereo LK, triangulation, append
+    rc = fe_keyframe(fe, t, fe->nB, fe->h_best, fe->xyB, fe->midB, max_take, sl, spec_ok);
+    if (rc) return rc;
+    SVO_HIP(ctx, hipEventRecord(fe->ev_tail, sl));
+    TP("tail queued");
     {
         int mt = fe->CAP;
         for (int s = 0; s < S; s++) mt = std::min(mt, fe->h_nB[s]);
@@ -1814,44 +1432,38 @@ int svo_frontend_step(svo_frontend* fe, int t, svo_frontend_stats* stats) {
     }
     fe->fits_pending = true;  // statistics land with the stream syncs below
     fe->fit_parity = t & 1;
-    // The critical path goes on with the next step's LK right behind this tail;
-    // only the SQPnP statistics of these inliers go to the GPU ahead of it (a
-    // kernel queued beside LK would wait for it: LK leaves no registers free, and
-    // the pose fits need them at the next step's start).
-    for (int g = 0; g < G; g++) SVO_HIP(ctx, hipStreamWaitEvent(sf, fe->ev_tail[g], 0));
+    // The critical path goes on with the next step's LK right behind this
+    // keyframe; only the SQPnP statistics of these inliers go to the GPU ahead of
+    // it (the pose fits need them at the next step's start).
+    SVO_HIP(ctx, hipStreamWaitEvent(sf, fe->ev_tail, 0));
     // this step's counts, before the next step's first half re-fills the mirrors
     int64_t lk_its = 0, tracked = 0;
     for (int s = 0; s < S; s++) {
         lk_its += fe->h_itsum[s];
         tracked += fe->h_nB[s];
     }
-    // the next step's first half goes out now, behind this step's tail, so the
-    // GPU moves on to its LK while the host returns to the caller
-    static const bool prefetch = [] {
-        const char* e = std::getenv("SVO_FE_PREFETCH");
-        return !(e && e[0] == '0');
-    }();
-    const bool ahead = prefetch && t + 1 < fe->T;
     // the binning of these features as the next frame's mask boxes, on the FAST
     // stream ahead of the next step's FAST (queued with its LK)
     SVO_HIP(ctx, launch_box_bin(fe_fast_batch(fe, dcur, true), S, fe->W, fe->H, sf));
     fe->boxes_binned = true;
     rc = fe_queue_stats(fe);
     if (rc) return rc;
-    if (ahead) {
+    // the next step's first half goes out now, behind this step's keyframe, so
+    // the GPU moves on to its LK while the host returns to the caller
+    if (t + 1 < fe->T) {
         rc = fe_front(fe, t + 1);
         if (rc) return rc;
         fe->front_t = t + 1;
     }
     TP("next front queued");
-    // wait for this step's tail only (the statistics, the next frame's pyramid and
-    // the prefetched first half keep running into the next step)
-    auto tw = clk::now();
-    for (int g = 0; g < G; g++) SVO_HIP(ctx, hipEventSynchronize(fe->ev_tail[g]));
+    // wait for this step's keyframe only (the statistics, the next frame's
+    // pyramid and the prefetched first half keep running into the next step)
+    tw = clk::now();
+    SVO_HIP(ctx, hipEventSynchronize(fe->ev_tail));
     ms_wait += ms_since(tw);
     TP("synced");
     ph_collect(fe);
-    if (trace_on) {
+    if (tr) {
         for (auto& e : trace) std::fprintf(stderr, "[fe t=%d] %8.1f us  %s\n", t, e.second, e.first);
     }
     if (stats) {
@@ -1867,6 +1479,7 @@ int svo_frontend_step(svo_frontend* fe, int t, svo_frontend_stats* stats) {
         stats->host_ms_hyp = ms_hyp;
         stats->host_ms_fit = ms_fit;
         stats->host_ms_wait = ms_wait;
+        stats->keyframes = n_keyframes;
     }
     return SVO_OK;
 }
@@ -1876,14 +1489,11 @@ int svo_frontend_synchronize(svo_frontend* fe) {
     svo_ctx* ctx = fe->ctx;
     int rq = fe_queue_stats(fe);
     if (rq) return rq;
-    for (auto& g : fe->gst) SVO_HIP(ctx, hipStreamSynchronize(g));
-    if (fe->st_kf) SVO_HIP(ctx, hipStreamSynchronize(fe->st_kf));
-    if (fe->st_fast) SVO_HIP(ctx, hipStreamSynchronize(fe->st_fast));
-    SVO_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    for (hipStream_t st : {fe->st_lk, fe->st_fast, fe->st_copy, ctx->stream}) SVO_HIP(ctx, hipStreamSynchronize(st));
     fe_finish_fits(fe);
     // the last keyframe's map points to the world frame (the next post-LK finds
     // nothing pending then)
-    SVO_HIP(ctx, launch_finalize_map(fe_pending(fe, 0), fe->S, ctx->stream));
+    SVO_HIP(ctx, launch_finalize_map(fe_pending(fe), fe->S, ctx->stream));
     SVO_HIP(ctx, hipStreamSynchronize(ctx->stream));
     return SVO_OK;
 }

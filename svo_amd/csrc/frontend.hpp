@@ -43,18 +43,6 @@ struct PostLkBatch {
     int* h_n;
     long long* h_iters;
     float* h_samp;  // [s][nh][25]
-    // LK ahead (nullable keep_bits: the plain form above). The temporal LK ran over
-    // the previous step's tracked points before its RANSAC (n_in / status / xy_in
-    // / mid_in / iters: that list) and, separately, over its n2[s] appended
-    // features (status2 / xy2 / iters2; map ids pend0[s] + j): the tracked set is
-    // (keep_bits && status) ++ status2, in that order, as LK over the kept +
-    // appended list would give
-    const uint32_t* keep_bits = nullptr;  // [s][words_cap], host-coherent
-    int words_cap = 0;
-    const int* n2 = nullptr;
-    const float* xy2 = nullptr;
-    const uint8_t* status2 = nullptr;
-    const int* iters2 = nullptr;
 };
 hipError_t launch_post_lk(const PostLkBatch& b, int nseq, hipStream_t st);
 // PendingMap alone (before the map is read by anything but post_lk)
@@ -63,7 +51,7 @@ hipError_t launch_finalize_map(const PendingMap& pm, int nseq, hipStream_t st);
 // The step's tail, part 1, one block per sequence: stable compaction by the
 // RANSAC inlier bits (read from host-coherent memory; R:src/tracking.cpp:218-229)
 // into xy_out / mid_out / n_out, then the keyframe's new-feature candidates: the
-// first take = min(n_target - n, candidates, capacity) masked FAST corners
+// first take = min(n_target[s] - n, candidates, capacity) masked FAST corners
 // (extractFeatures, :74-92), copied to st_xy (the stereo LK's input) with their
 // count in st_n.
 struct TailBatch {
@@ -75,7 +63,8 @@ struct TailBatch {
     float* xy_out;
     int* mid_out;
     int* n_out;
-    int cap, n_target;
+    int cap;
+    const int* n_target;  // [s] host-coherent: n_features on a keyframe, 0 otherwise
     const float* cand;  // candidates, cand_elem floats each, cand_cap per sequence
     int cand_elem, cand_cap;
     const int* cand_n;
@@ -111,15 +100,14 @@ struct AppendBatch {
     int* added;   // nullable
     int* h_n;     // nullable, host-coherent
     int* h_added; // nullable, host-coherent
-    float* ap_xy = nullptr;  // nullable: the appended features alone, [s][cap] (LK ahead's second input)
 };
-hipError_t launch_append(const AppendBatch& b, int nseq, hipStream_t st, bool small = false);
+hipError_t launch_append(const AppendBatch& b, int nseq, hipStream_t st);
 
 // Speculative stereo input, one block per sequence, queued as soon as the step's
 // tracked count n_tracked (post-LK) and the FAST candidates are known, i.e. before
 // the RANSAC: the keyframe takes the first take = min(n_target - kept, ...)
 // candidates, kept <= n_tracked inliers, so the first
-//   spec = min(n_target - n_tracked + margin, cand_n, cand_cap, cap, map_cap - map_n)
+//   spec = min(n_target[s] - n_tracked + margin, cand_n, cand_cap, cap, map_cap - map_n)
 // candidates cover take whenever RANSAC drops at most `margin` points. They are
 // copied to st_xy with their count in spec_n, and their stereo LK runs beside
 // the host's RANSAC (a feature's LK depends on nothing but its own point).
@@ -129,7 +117,8 @@ struct StereoPrepBatch {
     int cand_elem, cand_cap;
     const int* cand_n;
     const int* map_n;
-    int map_cap, cap, n_target, margin;
+    int map_cap, cap, margin;
+    const int* n_target;  // [s], as TailBatch::n_target
     float* st_xy;
     int* spec_n;
 };
@@ -138,9 +127,6 @@ hipError_t launch_stereo_prep(const StereoPrepBatch& b, int nseq, hipStream_t st
 // tail_kernel + append_kernel in one launch, for a step whose speculative stereo
 // LK covered every sequence's take (st_next / st_status already hold the matches
 // of st_xy[0, take)); same results as the two kernels with the LK between them.
-// small: 256-thread blocks (they find room beside a running LK; the default
-// 1024 keeps one SVD of latency for a few hundred candidates on an idle GPU)
-hipError_t launch_keyframe_fused(const TailBatch& tb, const AppendBatch& ab, int nseq, hipStream_t st,
-                                 bool small = false);
+hipError_t launch_keyframe_fused(const TailBatch& tb, const AppendBatch& ab, int nseq, hipStream_t st);
 
 }  // namespace svo

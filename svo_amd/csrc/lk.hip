@@ -915,27 +915,7 @@ __global__ __launch_bounds__(256, MINW) void lk_fast_kernel(LKBatch B, LKDev p) 
 }
 
 // ---------------------------------------------------------------------------
-// Two features per wave (21x21 windows, the reference's temporal call): each
-// 32-lane half owns one feature, so the per-feature work every lane repeats
-// (bilinear weights, bounds / convergence tests, the 2x2 solve) and the exact
-// reduction serve two features, while occupancy stays high (two staged regions
-// per wave). Lane map inside a half, l = 0..31, two vertical 7-row strips per
-// lane (441 pixels on 32 lanes x 14):
-//   l < 21:        column l, rows 0..6 and rows 7..13
-//   21 <= l < 31:  columns 2(l-21) and 2(l-21)+1, rows 14..20
-//   l = 31:        column 20, rows 14..20 (second strip: zero weights)
-// Per-lane int32 sums stay below 2^31 for the first two DPP steps (8 packed
-// pairs x 2 x 8160 x 4080 x 4 lanes); the rest runs on 16-bit halves, the
-// cross-row step by ds_swizzle (xor 16). Same exact integers and float solve:
-// bit-identical to lk_fast_kernel and the oracle's EXACT mode.
-template <int WW, int WH>
-struct DualShape {
-    static_assert(WW == 21 && WH == 21, "the dual lane map is laid out for 21x21 windows");
-    static constexpr int JRW = ru4(WW + 2 * JM + 3), JRH = WH + 1 + 2 * JM;
-    static constexpr int JBYTES = JRW * JRH * 4;
-    static constexpr int WAVE_BYTES = 2 * JBYTES + 16;
-};
-
+// Helpers of the four-features-per-wave kernel (lk_multi_kernel below).
 template <int CTRL>
 __device__ __forceinline__ int dpp_row_add(int v) {
     return v + __builtin_amdgcn_update_dpp(0, v, CTRL, 0xf, 0xf, false);
@@ -944,59 +924,6 @@ __device__ __forceinline__ int swz16_add(int v) {  // + lane ^ 16 (within 32-lan
     return v + __builtin_amdgcn_ds_swizzle(v, 0x401f);
 }
 __device__ __forceinline__ float halves_lane_float(int h, int l) { return ((float)h * 65536.f + (float)l) * FLT_SCALE; }
-
-// Exact 32-lane sums, every lane of the half receiving its half's total.
-__device__ __forceinline__ void half_sum_f2(int x, int y, float& fx, float& fy) {
-    x = dpp_row_add<0xb1>(x);
-    y = dpp_row_add<0xb1>(y);
-    x = dpp_row_add<0x4e>(x);
-    y = dpp_row_add<0x4e>(y);
-    int xh = x >> 16, xl = x & 0xFFFF, yh = y >> 16, yl = y & 0xFFFF;
-    xh = dpp_row_add<0x124>(xh);
-    xl = dpp_row_add<0x124>(xl);
-    yh = dpp_row_add<0x124>(yh);
-    yl = dpp_row_add<0x124>(yl);
-    xh = dpp_row_add<0x128>(xh);
-    xl = dpp_row_add<0x128>(xl);
-    yh = dpp_row_add<0x128>(yh);
-    yl = dpp_row_add<0x128>(yl);
-    xh = swz16_add(xh);
-    xl = swz16_add(xl);
-    yh = swz16_add(yh);
-    yl = swz16_add(yl);
-    fx = halves_lane_float(xh, xl);
-    fy = halves_lane_float(yh, yl);
-}
-__device__ __forceinline__ void half_sum_f3(int x, int y, int z, float& fx, float& fy, float& fz) {
-    x = dpp_row_add<0xb1>(x);
-    y = dpp_row_add<0xb1>(y);
-    z = dpp_row_add<0xb1>(z);
-    x = dpp_row_add<0x4e>(x);
-    y = dpp_row_add<0x4e>(y);
-    z = dpp_row_add<0x4e>(z);
-    int xh = x >> 16, xl = x & 0xFFFF, yh = y >> 16, yl = y & 0xFFFF, zh = z >> 16, zl = z & 0xFFFF;
-    xh = dpp_row_add<0x124>(xh);
-    xl = dpp_row_add<0x124>(xl);
-    yh = dpp_row_add<0x124>(yh);
-    yl = dpp_row_add<0x124>(yl);
-    zh = dpp_row_add<0x124>(zh);
-    zl = dpp_row_add<0x124>(zl);
-    xh = dpp_row_add<0x128>(xh);
-    xl = dpp_row_add<0x128>(xl);
-    yh = dpp_row_add<0x128>(yh);
-    yl = dpp_row_add<0x128>(yl);
-    zh = dpp_row_add<0x128>(zh);
-    zl = dpp_row_add<0x128>(zl);
-    xh = swz16_add(xh);
-    xl = swz16_add(xl);
-    yh = swz16_add(yh);
-    yl = swz16_add(yl);
-    zh = swz16_add(zh);
-    zl = swz16_add(zl);
-    fx = halves_lane_float(xh, xl);
-    fy = halves_lane_float(yh, yl);
-    fz = halves_lane_float(zh, zl);
-}
 
 // 7 rows of one strip: I (x32) / Ix / Iy at the strip's pixels packed by row
 // pairs (4 pairs, the last closed by a zero row), accumulated into the A sums.
@@ -1104,264 +1031,6 @@ __device__ __forceinline__ void stage_padded(unsigned* dst, unsigned* sink, cons
         int r = q * RPP + lr;
         r = r < H ? r : H - 1;
         stage_write(dpl + r * dstride, v[q], lane);
-    }
-}
-
-template <int WW, int WH, int MINW>
-__global__ __launch_bounds__(64, MINW) void lk_dual_kernel(LKBatch B, LKDev p) {
-    using Q = DualShape<WW, WH>;
-    // window + staging margin + dword alignment stay inside the level padding
-    static_assert(WW + JM + 3 <= kPyrPad && WW + 1 <= kDerPad, "padding too small for the window");
-    constexpr int JRW = Q::JRW, JRH = Q::JRH;
-    constexpr int NR = 7, NP = 4;
-    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-    const int lane = threadIdx.x & 63;
-    const int g = lane >> 5, l = lane & 31;
-    const int seq = blockIdx.y;
-    const int n = B.counts ? B.counts[seq] : B.n;
-    const int pt0 = blockIdx.x * 2;
-    if (pt0 >= n) return;
-    const int pt = pt0 + g;
-    const bool live = pt < n;
-    const int ptc = live ? pt : n - 1;  // an idle half shadows a real feature, writes nothing
-    const size_t base = (size_t)seq * B.cap;
-    const float* __restrict__ prev_xy = B.prev_xy + 2 * base;
-    float* __restrict__ next_xy = B.next_xy + 2 * base;
-    const cpyr prev = (cpyr)B.prev + seq;
-    const cpyr next = (cpyr)B.next + seq;
-    const DerivDesc& dprev = B.dprev[seq];
-    unsigned* jregs = reinterpret_cast<unsigned*>(lds);
-    unsigned* sink = reinterpret_cast<unsigned*>(lds + 2 * Q::JBYTES);
-    const unsigned* jmine = jregs + g * (Q::JBYTES / 4);
-
-    // the lane's two strips: (column, first row) and whether strip 2 is real
-    const bool upper = l < 21;
-    const int k2 = l - 21;
-    const int cA = upper ? l : (l < 31 ? 2 * k2 : 20), rA = upper ? 0 : 14;
-    const bool hasB = l < 31;
-    const int cB = upper ? l : (hasB ? 2 * k2 + 1 : 0), rB = upper ? 7 : (hasB ? 14 : 0);
-    constexpr float halfWx = (WW - 1) * 0.5f, halfWy = (WH - 1) * 0.5f;
-    const int rnd_j = 1 << (W_BITS - 6 + kJShift);
-
-    const float px = prev_xy[2 * ptc], py = prev_xy[2 * ptc + 1];
-    float nx = 0.f, ny = 0.f;
-    if (p.flags & SVO_LK_USE_INITIAL_FLOW) {
-        nx = next_xy[2 * ptc];
-        ny = next_xy[2 * ptc + 1];
-    }
-    int st = live ? 1 : 0;
-    float errv = 0.f;
-    int itcount = 0;
-    const int max_level = p.max_level;
-
-    for (int level = max_level; level >= 0; level--) {
-        const ImgLevel I{prev->lv[level].data, prev->lv[level].w, prev->lv[level].h, prev->lv[level].pitch};
-        const ImgLevel J{next->lv[level].data, next->lv[level].w, next->lv[level].h, next->lv[level].pitch};
-        const float lscale = __builtin_amdgcn_ldexpf(1.f, -level);
-        float prevx = px * lscale, prevy = py * lscale;
-        float nextx, nexty;
-        if (level == max_level) {
-            if (p.flags & SVO_LK_USE_INITIAL_FLOW) {
-                nextx = nx * lscale;
-                nexty = ny * lscale;
-            } else {
-                nextx = prevx;
-                nexty = prevy;
-            }
-        } else {
-            nextx = nx * 2.f;
-            nexty = ny * 2.f;
-        }
-        nx = nextx;
-        ny = nexty;
-        prevx -= halfWx;
-        prevy -= halfWy;
-        const int ipx = ufloor(prevx), ipy = ufloor(prevy);
-        const bool inb = !(ipx < -WW || ipx >= I.w || ipy < -WH || ipy >= I.h);
-        if (!inb && level == 0 && live) {
-            st = 0;
-            errv = 0.f;
-        }
-        bool lact = live && inb;
-        const float a = prevx - ipx, b = prevy - ipy;
-        const int iw00 = uround((1.f - a) * (1.f - b) * (1 << W_BITS));
-        const int iw01 = uround(a * (1.f - b) * (1 << W_BITS));
-        const int iw10 = uround((1.f - a) * b * (1 << W_BITS));
-        const int iw11 = (1 << W_BITS) - iw00 - iw01 - iw10;
-        const unsigned IW0 = pack16(iw00, iw01), IW1 = pack16(iw10, iw11);
-
-        int jx0 = ufloor(nextx - halfWx) - JM, jy0 = ufloor(nexty - halfWy) - JM;
-        int jxa = jx0 & ~3;
-        unsigned I2A[NP], GXA[NP], GYA[NP], I2B[NP], GXB[NP], GYB[NP];
-        int a11 = 0, a12 = 0, a22 = 0;
-        {
-            // Levels carry kPyrPad-pixel REFLECT_101 borders and the derivative
-            // levels kDerPad-element zero borders, so every read below is
-            // branch-free. An inactive half (or one whose region lies beyond the
-            // padding: its first bounds test deactivates it) stages and reads at
-            // the level origin; its results are never used.
-            using SL = DualStageLoads<JRW, JRH>;
-            const int lr = lane / SL::LPR, d = lane - lr * SL::LPR;
-            int xs[2], ys[2];
-#pragma unroll
-            for (int f = 0; f < 2; f++) {
-                const int xa = __builtin_amdgcn_readlane(jxa, 32 * f), y0 = __builtin_amdgcn_readlane(jy0, 32 * f);
-                const bool ok = __builtin_amdgcn_readlane((int)lact, 32 * f) && region_in_pad<JRW, JRH>(J, xa, y0);
-                xs[f] = ok ? xa : 0;
-                ys[f] = ok ? y0 : 0;
-            }
-            SL ld;
-#pragma unroll
-            for (int f = 0; f < 2; f++) {
-                gu8 src = (gu8)J.data + xs[f] + 4 * d;
-#pragma unroll
-                for (int q = 0; q < SL::NPS; q++) {
-                    int r = q * SL::RPP + lr;
-                    r = r < JRH ? r : JRH - 1;
-                    ld.v[f][q] = *(gu32)(src + (ptrdiff_t)(ys[f] + r) * J.pitch);
-                }
-            }
-            unsigned PA[NR + 1], PB[NR + 1];
-            u32x2a4 DA[NR + 1], DB[NR + 1];
-            {
-                const int dpitch = dprev.pitch[level];
-                gu32 dsrc = (gu32)dprev.data[level];
-                const int sx = inb ? ipx : 0, sy = inb ? ipy : 0;
-                const int xA = sx + cA, yA = sy + rA, xB = sx + cB, yB = sy + rB;
-                gu8 ia = (gu8)I.data + (ptrdiff_t)yA * I.pitch + xA;
-                gu8 ib = (gu8)I.data + (ptrdiff_t)yB * I.pitch + xB;
-                gu32 qa = dsrc + (ptrdiff_t)yA * dpitch + xA;
-                gu32 qb = dsrc + (ptrdiff_t)yB * dpitch + xB;
-#pragma unroll
-                for (int k = 0; k <= NR; k++) {
-                    PA[k] = __builtin_amdgcn_perm(0u, (unsigned)*(gu16u)(ia + (ptrdiff_t)k * I.pitch), 0x0c010c00u);
-                    DA[k] = *(const __attribute__((address_space(1))) u32x2a4*)(qa + (ptrdiff_t)k * dpitch);
-                    PB[k] = __builtin_amdgcn_perm(0u, (unsigned)*(gu16u)(ib + (ptrdiff_t)k * I.pitch), 0x0c010c00u);
-                    DB[k] = *(const __attribute__((address_space(1))) u32x2a4*)(qb + (ptrdiff_t)k * dpitch);
-                }
-            }
-            const bool wr = d < JRW / 4 && lr < SL::RPP;
-#pragma unroll
-            for (int f = 0; f < 2; f++) {
-                unsigned* dpl = wr ? jregs + f * (Q::JBYTES / 4) + 4 * d : sink;
-                const int dstride = wr ? JRW : 0;
-#pragma unroll
-                for (int q = 0; q < SL::NPS; q++) {
-                    int r = q * SL::RPP + lr;
-                    r = r < JRH ? r : JRH - 1;
-                    stage_write(dpl + r * dstride, ld.v[f][q], lane);
-                }
-            }
-            strip_setup<NR>(PA, DA, IW0, IW1, IW0, IW1, I2A, GXA, GYA, a11, a12, a22);
-            strip_setup<NR>(PB, DB, IW0, IW1, hasB ? IW0 : 0u, hasB ? IW1 : 0u, I2B, GXB, GYB, a11, a12, a22);
-        }
-        wave_lds_sync();
-        float A11, A12, A22;
-        half_sum_f3(a11, a12, a22, A11, A12, A22);
-
-        float D = A11 * A22 - A12 * A12;
-        const float minEig =
-            (A22 + A11 - sqrtf((A11 - A22) * (A11 - A22) + 4.f * A12 * A12)) / (float)(2 * WW * WH);
-        if (lact && p.want_err && (p.flags & SVO_LK_GET_MIN_EIGENVALS)) errv = minEig;
-        if (lact && (minEig < p.min_eig || D < FLT_EPSILON)) {
-            if (level == 0) st = 0;
-            lact = false;
-        }
-        D = 1.f / D;
-
-        nextx -= halfWx;
-        nexty -= halfWy;
-        float pdx = 0.f, pdy = 0.f;
-        for (int j = 0; j < p.max_count; j++) {
-            if (__builtin_amdgcn_ballot_w64(lact) == 0) break;
-            const int inx = ufloor(nextx), iny = ufloor(nexty);
-            if (lact && (inx < -WW || inx >= J.w || iny < -WH || iny >= J.h)) {
-                if (level == 0) st = 0;
-                lact = false;
-            }
-            const bool need = lact && ((unsigned)(inx - jx0) > 2u * JM || (unsigned)(iny - jy0) > 2u * JM);
-            if (need) {
-                jx0 = inx - JM;
-                jy0 = iny - JM;
-                jxa = jx0 & ~3;
-            }
-            unsigned long long nb = __builtin_amdgcn_ballot_w64(need && l == 0);
-            if (nb) {
-                wave_lds_sync();
-                while (nb) {
-                    const int f = (int)(__builtin_ctzll(nb) >> 5);
-                    nb &= nb - 1;
-                    stage_padded<JRW, JRH>(jregs + f * (Q::JBYTES / 4), sink, J,
-                                           __builtin_amdgcn_readlane(jxa, 32 * f),
-                                           __builtin_amdgcn_readlane(jy0, 32 * f), lane);
-                }
-                wave_lds_sync();
-            }
-            itcount += lact ? 1 : 0;
-            const float aa = nextx - inx, bb = nexty - iny;
-            const int w00 = uround((1.f - aa) * (1.f - bb) * (1 << W_BITS));
-            const int w01 = uround(aa * (1.f - bb) * (1 << W_BITS));
-            const int w10 = uround((1.f - aa) * bb * (1 << W_BITS));
-            const int w11 = (1 << W_BITS) - w00 - w01 - w10;
-            const unsigned W0 = pack16(w00, w01), W1 = pack16(w10, w11);
-            int b1 = 0, b2 = 0;
-            {
-                // an inactive half reads inside its own region (results unused)
-                const int ro = lact ? iny - jy0 : 0, co = lact ? inx - jxa : 0;
-                const unsigned* ja = jmine + (ro + rA) * JRW + co + cA;
-                const unsigned* jb = jmine + (ro + rB) * JRW + co + cB;
-                unsigned qa[NR + 1], qb[NR + 1];
-#pragma unroll
-                for (int k = 0; k <= NR; k++) {
-                    qa[k] = ja[k * JRW];
-                    qb[k] = jb[k * JRW];
-                }
-                int jva[2 * NP], jvb[2 * NP];
-                jva[2 * NP - 1] = jvb[2 * NP - 1] = 0;
-#pragma unroll
-                for (int k = 0; k < NR; k++) {  // J x 2^kJShift: descaled value in bits 16..31
-                    jva[k] = sdot2(qa[k], W0, sdot2_r(qa[k + 1], W1, rnd_j));
-                    jvb[k] = sdot2(qb[k], W0, sdot2_r(qb[k + 1], W1, rnd_j));
-                }
-#pragma unroll
-                for (int m = 0; m < NP; m++) {
-                    const unsigned da = pk_sub16(hi16x2(jva[2 * m], jva[2 * m + 1]), I2A[m]);
-                    const unsigned db = pk_sub16(hi16x2(jvb[2 * m], jvb[2 * m + 1]), I2B[m]);
-                    b1 = sdot2(da, GXA[m], b1);
-                    b2 = sdot2(da, GYA[m], b2);
-                    b1 = sdot2(db, GXB[m], b1);
-                    b2 = sdot2(db, GYB[m], b2);
-                }
-            }
-            float fb1, fb2;
-            half_sum_f2(b1, b2, fb1, fb2);
-            const float dx = (A12 * fb2 - A22 * fb1) * D;
-            const float dy = (A12 * fb1 - A11 * fb2) * D;
-            if (lact) {
-                nextx += dx;
-                nexty += dy;
-                nx = nextx + halfWx;
-                ny = nexty + halfWy;
-                if (converged(dx, dy, p.eps2_lo, p.eps2_hi, p.eps2)) {
-                    lact = false;
-                } else if (j > 0 && below_001(dx + pdx) && below_001(dy + pdy)) {
-                    nx -= dx * 0.5f;
-                    ny -= dy * 0.5f;
-                    lact = false;
-                } else {
-                    pdx = dx;
-                    pdy = dy;
-                }
-            }
-        }
-        wave_lds_sync();
-    }
-    if (l == 0 && live) {
-        next_xy[2 * pt] = nx;
-        next_xy[2 * pt + 1] = ny;
-        B.status[base + pt] = (uint8_t)st;
-        if (B.err) B.err[base + pt] = errv;
-        if (B.iters) B.iters[base + pt] = itcount;
     }
 }
 
@@ -1702,23 +1371,6 @@ hipError_t launch_multi(const LKBatch& b, int nseq, int max_n, const LKDev& d, h
 }
 
 template <int WW, int WH>
-hipError_t launch_dual(const LKBatch& b, int nseq, int max_n, const LKDev& d, hipStream_t st) {
-    dim3 grid((max_n + 1) / 2, nseq);
-    constexpr int lds_bytes = DualShape<WW, WH>::WAVE_BYTES;
-    static const int minw = [] {
-        const char* e = std::getenv("SVO_LK_DUAL_MINW");
-        return e ? std::atoi(e) : 4;
-    }();
-    if (minw == 5)
-        hipLaunchKernelGGL((lk_dual_kernel<WW, WH, 5>), grid, dim3(64), lds_bytes, st, b, d);
-    else if (minw == 3)
-        hipLaunchKernelGGL((lk_dual_kernel<WW, WH, 3>), grid, dim3(64), lds_bytes, st, b, d);
-    else
-        hipLaunchKernelGGL((lk_dual_kernel<WW, WH, 4>), grid, dim3(64), lds_bytes, st, b, d);
-    return hipGetLastError();
-}
-
-template <int WW, int WH>
 hipError_t launch_fast(const LKBatch& b, int nseq, int max_n, const LKDev& d, hipStream_t st) {
     const int gn = b.grid_hint > 0 && b.grid_hint < max_n ? b.grid_hint : max_n;
     dim3 grid((gn + 3) / 4, nseq);
@@ -1740,6 +1392,13 @@ hipError_t launch_rpg(const LKBatch& b, int nseq, int max_n, const LKDev& d, hip
 }
 
 }  // namespace
+
+void lk_apply_env(LKParams& p) {
+    const char* gen = std::getenv("SVO_LK_GENERIC");
+    p.generic = gen && gen[0] == '1' ? 1 : 0;
+    const char* quad = std::getenv("SVO_LK_QUAD");
+    p.quad = quad && quad[0] == '0' ? 0 : 1;
+}
 
 bool lk_supported(int win_w, int win_h) {
     if (win_w < 3 || win_h < 3 || win_w + 2 * JM > 64 || win_w + 3 > 64) return false;
@@ -1774,25 +1433,14 @@ hipError_t launch_lk(const LKBatch& b, int nseq, int max_n, const LKParams& lp, 
     d.want_err = lp.want_err;
     d.min_eig = lp.min_eig;
     if (!lp.generic) {
-        // two features per wave: the SAD error (flags 0 + want_err) stays on lk_fast_kernel
-        const bool dual_ok = !(lp.want_err && !(lp.flags & SVO_LK_GET_MIN_EIGENVALS));
-        if (lp.win_w == 21 && lp.win_h == 21 && dual_ok && lp.quad) {
-            // SVO_LK_MULTI: 41 (default) four features per wave, 1-px staging
-            // margin (re-staged when the estimate leaves it; measured 2.7 % faster
-            // alone than the 2-px margin, 42, and 3-px, 43); 2 two per wave
-            // (generic map); 0 the dual kernel (its own lane map)
-            switch (lp.multi) {
-                case 0: return launch_dual<21, 21>(b, nseq, max_n, d, st);
-                case 2: return launch_multi<2, 3>(b, nseq, max_n, d, st);
-                case 43: return launch_multi<4, 3, 3>(b, nseq, max_n, d, st);
-                case 42: return launch_multi<4, 2, 3>(b, nseq, max_n, d, st);
-                case 40: return launch_multi<4, 0, 3>(b, nseq, max_n, d, st);
-                case 47: return launch_multi<4, 2, 3, 4>(b, nseq, max_n, d, st);
-                case 48: return launch_multi<4, 2, 3, 1>(b, nseq, max_n, d, st);
-                case 44: return launch_multi<4, 1, 4>(b, nseq, max_n, d, st);  // <= 128 VGPRs
-                case 45: return launch_multi<4, 1, 3, 1>(b, nseq, max_n, d, st);
-                default: return launch_multi<4, 1, 3>(b, nseq, max_n, d, st);
-            }
+        // four features per wave: the SAD error (flags 0 + want_err) stays on lk_fast_kernel
+        const bool multi_ok = !(lp.want_err && !(lp.flags & SVO_LK_GET_MIN_EIGENVALS));
+        if (lp.win_w == 21 && lp.win_h == 21 && multi_ok && lp.quad) {
+            // four features per wave, 1-px staging margin (re-staged when the
+            // estimate leaves it; measured 2.7 % faster alone than a 2-px margin
+            // and than 3 px; two features per wave (lk_dual_kernel, another lane
+            // map) measured slower and is gone: DESIGN.md)
+            return launch_multi<4, 1, 3>(b, nseq, max_n, d, st);
         }
         if (lp.win_w == 21 && lp.win_h == 21) return launch_fast<21, 21>(b, nseq, max_n, d, st);
         if (lp.win_w == 11 && lp.win_h == 11) return launch_fast<11, 11>(b, nseq, max_n, d, st);

@@ -38,8 +38,18 @@ def transform(T, t, X):
 
 
 class OracleLoop:
-    def __init__(self, scene, n_features=2000, bucket=(0, 0), acc=O.ACC_EXACT):
+    def __init__(self, scene, n_features=2000, bucket=(0, 0), acc=O.ACC_EXACT, max_level=TEMPORAL["max_level"],
+                 rule="every", features_to_track=70):
+        """max_level: the temporal LK's (BASELINE configs: 3 at KITTI and 4K, 4 at
+        1080p); the stereo LK keeps the reference's maxLevel 3.
+        rule: "every" -- every frame a keyframe topping the set up to n_features
+        (the benchmark's loop); "reference" -- Tracking::nextFrame's rule
+        (R:src/tracking.cpp:68-69): a keyframe iff the previous frame was not one
+        and kept fewer than features_to_track features; a keyframe takes every
+        masked corner (extractFeatures, :74-92), n_features being the capacity."""
         self.sc, self.N, self.bucket, self.acc = scene, n_features, bucket, acc
+        self.max_level = max_level
+        self.rule, self.features_to_track = rule, features_to_track
         self.P_left, self.P_right = scene.projections()
 
     def _candidates(self, img, mask):
@@ -69,12 +79,13 @@ class OracleLoop:
         self.pose_T = (np.eye(3), np.zeros(3))
         self.pts, self.X = self._keyframe(self.img, right, cand, *self.pose_T)
         self.pose = (np.zeros(3), np.zeros(3))
+        self.kf_prev = True  # frame t0 is a keyframe (lastFrameID == 0)
         return self
 
     def step(self, t, left=None, right=None):
         B = self.sc.frame(t) if left is None else left
         Br = self.sc.right(t) if right is None else right
-        nx, st, _, it = O.lk(self.img, B, self.pts, TEMPORAL["win"], TEMPORAL["max_level"], TEMPORAL["criteria"],
+        nx, st, _, it = O.lk(self.img, B, self.pts, TEMPORAL["win"], self.max_level, TEMPORAL["criteria"],
                              TEMPORAL["flags"], acc=self.acc, want_err=False)
         keep = st == 1
         p2, X2 = nx[keep], self.X[keep]
@@ -91,9 +102,12 @@ class OracleLoop:
         self.pose = (rv, tv)
         self.pose_T = pose_inverse(rv, tv)
         stats["inliers"] = len(p2)
+        kf = self.rule == "every" or (not self.kf_prev and len(self.pts) < self.features_to_track)
+        self.kf_prev = kf
+        stats["keyframe"] = int(kf)
         mask = O.mask_boxes(B.shape[1], B.shape[0], self.pts, 10.0)
         cand = self._candidates(B, mask)
-        need = max(self.N - len(p2), 0)
+        need = max(self.N - len(p2), 0) if kf else 0
         newL, newX = self._keyframe(B, Br, cand[:need], *self.pose_T)
         self.pts = np.concatenate([p2, newL]).astype(np.float32)
         self.X = np.concatenate([X2, newX]) if len(newL) else X2

@@ -48,6 +48,36 @@ def test_bench_dist_plumbing_gloo(world):
         assert len(flat) == len(set(flat)) == 4 * world   # disjoint shards
 
 
+def test_bench_gpus_flag_launches_ranks():
+    """`python bench.py --gpus 2` with no launcher env starts 2 ranks itself (gloo
+    rendezvous on 127.0.0.1, no GPU call in the parent): world size 2 on every
+    rank, disjoint sequence seeds, the total counted over ranks (--dry-run stops
+    each rank before it touches a GPU)."""
+    import json
+    import subprocess
+    import sys
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "MASTER_PORT")}
+    out = subprocess.run([sys.executable, bench.__file__, "--gpus", "2", "--seq", "3", "--dry-run"],
+                         env=env, capture_output=True, text=True, timeout=240)
+    assert out.returncode == 0, out.stderr[-2000:]
+    lines = [json.loads(x) for x in out.stdout.splitlines() if x.startswith("{")]
+    assert sorted(d["rank"] for d in lines) == [0, 1]
+    assert all(d["world"] == 2 and d["total_sequences"] == 6 for d in lines)
+    seeds = [s for d in lines for s in d["seeds"]]
+    assert len(seeds) == len(set(seeds)) == 6
+
+
+def test_bench_gpus_flag_must_match_launcher():
+    """Under a launcher, --gpus N must equal the world size it started."""
+    import subprocess
+    import sys
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    out = subprocess.run([sys.executable, bench.__file__, "--gpus", "2", "--dry-run"], env=env,
+                         capture_output=True, text=True, timeout=240)
+    assert out.returncode != 0 and "--gpus 2" in out.stderr
+
+
 def _plan_worker(rank, world, port, out):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(world), RANK=str(rank),
                       LOCAL_RANK=str(rank), LOCAL_WORLD_SIZE=str(world))

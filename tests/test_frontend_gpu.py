@@ -36,18 +36,13 @@ def _compare_step(fe, ref, st, rs, t, seq=0, check_map=True):
         np.testing.assert_allclose(fe.map_points(seq), ref.X, rtol=2e-5, atol=1e-6)
 
 
-@pytest.mark.parametrize("ahead", ["1", "0"])
 @pytest.mark.parametrize("spec", ["-1", "0", "32"])
 @pytest.mark.parametrize("bucket", [(0, 0), (50, 4)])
-def test_frontend_matches_oracle_loop(bucket, spec, ahead, monkeypatch):
+def test_frontend_matches_oracle_loop(bucket, spec, monkeypatch):
     """spec: SVO_FE_SPEC_MARGIN -- the keyframe's stereo LK run speculatively beside
     the RANSAC (32: the default; 0: the fused keyframe only when RANSAC dropped
-    nothing, else the serial tail + stereo LK + append; -1: always serial).
-    ahead: SVO_FE_AHEAD -- LK(t+1) over step t's tracked points before its RANSAC,
-    plus a small LK of the appended features, merged by the next post-LK (1), or
-    LK over the kept + appended list after the keyframe (0, the default)."""
+    nothing, else the serial tail + stereo LK + append; -1: always serial)."""
     monkeypatch.setenv("SVO_FE_SPEC_MARGIN", spec)
-    monkeypatch.setenv("SVO_FE_AHEAD", ahead)
     ctx = S.Context(0)
     W, H, N, T = 640, 376, 800, 8
     sc = Scene(W, H, seed=3)
@@ -64,41 +59,14 @@ def test_frontend_matches_oracle_loop(bucket, spec, ahead, monkeypatch):
         np.testing.assert_allclose(O.rodrigues(rv), sc.R(t), atol=3e-3)
 
 
-@pytest.mark.parametrize("split", ["0", "1"])
-@pytest.mark.parametrize("early", ["0", "1"])
-def test_frontend_speculative_stereo_schedules(early, split, monkeypatch):
-    """SVO_FE_SPEC_EARLY: the speculative stereo LK queued with the front half,
-    behind FAST (1; sized from the features before LK) or behind the post-LK (0,
-    the default; sized from the tracked count) -- both against the oracle loop, at
-    a small margin (4; the front-half schedule adds the last step's largest LK loss)."""
-    monkeypatch.setenv("SVO_FE_SPEC_EARLY", early)
-    monkeypatch.setenv("SVO_FE_FAST_SPLIT", split)  # FAST's scan + emit behind post-LK fill the stereo input
-    monkeypatch.setenv("SVO_FE_SPEC_MARGIN", "4")
-    ctx = S.Context(0)
-    W, H, N, T = 640, 376, 800, 8
-    fe = make_frontend(ctx, [Scene(W, H, seed=5)], T, N)
-    fe.init(0)
-    ref = OracleLoop(Scene(W, H, seed=5), N).init(0)
-    for t in range(1, T):
-        st = fe.step(t).as_dict()
-        rs = ref.step(t)
-        _compare_step(fe, ref, st, rs, t)
-
-
 @pytest.mark.parametrize("bucket", [(0, 0), (50, 4)])
-@pytest.mark.parametrize("sched", ["behind", "first", "pre", "pre2", "default"])
-def test_frontend_fast_schedules(sched, bucket, monkeypatch):
-    """Where FAST(t) runs, each against the oracle loop: right behind LK(t) (the
-    default), submitted ahead of it (SVO_FE_FAST_FIRST=1), or detected without the box
-    mask during step t-1 with only the box filter + scan + emit behind LK(t)
-    (SVO_FE_FAST_PRE=1 on the pyramid stream, 2 on the FAST stream behind the
-    speculative stereo LK; the mask drops corners after NMS); and the default."""
-    if sched == "default":
-        monkeypatch.delenv("SVO_FE_FAST_FIRST", raising=False)
-        monkeypatch.delenv("SVO_FE_FAST_PRE", raising=False)
-    else:
-        monkeypatch.setenv("SVO_FE_FAST_FIRST", "1" if sched == "first" else "0")
-        monkeypatch.setenv("SVO_FE_FAST_PRE", {"pre": "1", "pre2": "2"}.get(sched, "0"))
+@pytest.mark.parametrize("pre", ["0", "1"])
+def test_frontend_fast_schedules(pre, bucket, monkeypatch):
+    """Where FAST(t)'s detection runs, each against the oracle loop: behind LK(t) on
+    the FAST stream (SVO_FE_FAST_PRE=0), or unmasked during step t-1 on the
+    context stream with only the box filter + scan + emit behind LK(t) (1, the
+    default; the mask drops corners after NMS)."""
+    monkeypatch.setenv("SVO_FE_FAST_PRE", pre)
     ctx = S.Context(0)
     W, H, N, T = 640, 376, 800, 8
     fe = make_frontend(ctx, [Scene(W, H, seed=7)], T, N, bucket_size=bucket[0], per_bucket=bucket[1])
@@ -108,6 +76,68 @@ def test_frontend_fast_schedules(sched, bucket, monkeypatch):
         st = fe.step(t).as_dict()
         rs = ref.step(t)
         _compare_step(fe, ref, st, rs, t)
+
+
+@pytest.mark.parametrize("pre", ["0", "1"])
+def test_frontend_streaming_ring_and_reinit(pre, monkeypatch):
+    """A ring of T = 3 resident frames filled while the sequence runs (frame t
+    uploaded into slot t % 3 right before step(t)): a pyramid built ahead and a
+    FAST pre-detection of a slot are dropped when its image is replaced. Then a
+    second init on the same front end (everything queued ahead is drained first)
+    and more steps, each against the oracle loop."""
+    monkeypatch.setenv("SVO_FE_FAST_PRE", pre)
+    ctx = S.Context(0)
+    W, H, N, T = 640, 376, 800, 3
+    sc = Scene(W, H, seed=9)
+    fe = S.Frontend(ctx, S.FrontendConfig(W, H, sc.K, n_seq=1, n_frames=T, n_features=N))
+    fe.set_frame(0, 0, sc.frame(0), sc.right(0))
+    fe.init(0)
+    ref = OracleLoop(Scene(W, H, seed=9), N).init(0)
+    for t in range(1, 9):
+        fe.set_frame(0, t % T, sc.frame(t), sc.right(t))
+        st = fe.step(t).as_dict()
+        _compare_step(fe, ref, st, ref.step(t), t)
+    fe.init(8)  # slot 8 % 3 holds frame 8
+    ref = OracleLoop(Scene(W, H, seed=9), N).init(8)
+    assert np.array_equal(fe.features(0), ref.pts)
+    for t in range(9, 13):
+        fe.set_frame(0, t % T, sc.frame(t), sc.right(t))
+        st = fe.step(t).as_dict()
+        _compare_step(fe, ref, st, ref.step(t), t)
+    fe.close()
+
+
+def test_frontend_reference_keyframe_rule():
+    """SVO_KF_REFERENCE: Tracking::nextFrame's rule (R:src/tracking.cpp:68-69) -- a
+    frame is a keyframe iff its predecessor was not one and kept fewer than
+    features_to_track features -- and a keyframe takes every masked corner (up to
+    the capacity n_features), against the oracle loop's same rule. The threshold
+    is set so that the synthetic sequence alternates between keyframes and
+    tracking-only frames."""
+    ctx = S.Context(0)
+    W, H, N, T, F2T = 640, 376, 3000, 10, 100000
+    sc = Scene(W, H, seed=4)
+    fe = make_frontend(ctx, [sc], T, N, keyframe_rule=S.KF_REFERENCE, features_to_track=F2T)
+    fe.init(0)
+    ref = OracleLoop(Scene(W, H, seed=4), N, rule="reference", features_to_track=F2T).init(0)
+    assert np.array_equal(fe.features(0), ref.pts)
+    kfs = []
+    for t in range(1, T):
+        st = fe.step(t).as_dict()
+        rs = ref.step(t)
+        _compare_step(fe, ref, st, rs, t)
+        assert st["keyframes"] == rs["keyframe"]
+        kfs.append(st["keyframes"])
+    assert kfs == [0, 1] * ((T - 1) // 2) + [0] * ((T - 1) % 2)   # prev KF => no KF, else count < F2T => KF
+    # a threshold never reached: only frame 0 is a keyframe
+    fe2 = make_frontend(ctx, [sc], 5, N, keyframe_rule=S.KF_REFERENCE, features_to_track=70)
+    fe2.init(0)
+    ref2 = OracleLoop(Scene(W, H, seed=4), N, rule="reference", features_to_track=70).init(0)
+    for t in range(1, 5):
+        st = fe2.step(t).as_dict()
+        rs = ref2.step(t)
+        _compare_step(fe2, ref2, st, rs, t)
+        assert st["keyframes"] == 0 and st["added"] == 0
 
 
 def test_frontend_200_frames_kitti_matches_oracle_loop():
@@ -128,14 +158,12 @@ def test_frontend_200_frames_kitti_matches_oracle_loop():
     np.testing.assert_allclose(O.rodrigues(rv), sc.R(T - 1), atol=5e-3)
 
 
-@pytest.mark.parametrize("groups", [1, 2, 3])
-def test_frontend_batch_independence(groups):
-    """A sequence's result does not depend on the batch it runs in, nor on the
-    pipeline slicing of the batch (slices overlap LK and host RANSAC)."""
+def test_frontend_batch_independence():
+    """A sequence's result does not depend on the batch it runs in."""
     ctx = S.Context(0)
     W, H, N, T = 1241, 376, 2000, 4
     scenes = [Scene(W, H, seed=s) for s in range(3)]
-    feb = make_frontend(ctx, scenes, T, N, groups=groups)
+    feb = make_frontend(ctx, scenes, T, N)
     feb.init(0)
     solo = [make_frontend(ctx, [sc], T, N) for sc in scenes]
     for f in solo:

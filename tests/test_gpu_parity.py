@@ -85,19 +85,6 @@ def test_frontend_scharr_pyramid_bit_exact(ctx, wh):
 
 
 # ------------------------------------------------------------------ FAST
-@pytest.fixture(params=["block-queue", "wave-queue", "swar", "queue-nms", "queue-nms-64"])
-def fast_kernel(request, monkeypatch):
-    """Every fused detection form (SVO_FAST_V=1 fast_detect_kernel, 2
-    fast_detect_w_kernel, 3 fast_detect_s_kernel, 4 fast_detect_q_kernel with its
-    32-row tile, and the same with the 64-row tile, SVO_FAST_QTY=64) must give the
-    oracle's keypoints."""
-    monkeypatch.setenv("SVO_FAST_V", {"block-queue": "1", "wave-queue": "2", "swar": "3", "queue-nms": "4",
-                                      "queue-nms-64": "4"}[request.param])
-    if request.param == "queue-nms-64":
-        monkeypatch.setenv("SVO_FAST_QTY", "64")
-    return request.param
-
-
 @pytest.mark.parametrize("wh,seed", [((1241, 376), 0), ((160, 120), 3), ((64, 48), 5), ((3840, 2160), 1)])
 def test_fast_score_map_bit_exact(ctx, wh, seed):
     sc, A, _ = frames(*wh, seed=seed)
@@ -111,7 +98,7 @@ def test_fast_score_map_bit_exact(ctx, wh, seed):
 
 @pytest.mark.parametrize("nonmax", [True, False])
 @pytest.mark.parametrize("wh,seed", [((1241, 376), 0), ((160, 120), 2), ((1920, 1080), 4)])
-def test_fast_keypoints_identical(ctx, wh, seed, nonmax, fast_kernel):
+def test_fast_keypoints_identical(ctx, wh, seed, nonmax):
     sc, A, _ = frames(*wh, seed=seed)
     g = ctx.image(A, 0)
     det = S.FastFeatureDetector.create(ctx, 20, nonmax)
@@ -121,7 +108,7 @@ def test_fast_keypoints_identical(ctx, wh, seed, nonmax, fast_kernel):
     assert np.array_equal(got, ref)
 
 
-def test_fast_with_mask_identical(ctx, fast_kernel):
+def test_fast_with_mask_identical(ctx):
     sc, A, _ = frames(1241, 376, seed=0)
     g = ctx.image(A, 0)
     prev = O.fast(A, 20, True)[::3, :2] + np.float32(0.37)
@@ -139,7 +126,7 @@ def test_mask_boxes_edges(ctx):
     assert np.array_equal(ctx.mask_boxes(64, 48, pts, 10.0), O.mask_boxes(64, 48, pts, 10.0))
 
 
-def test_fast_threshold_extremes(ctx, fast_kernel):
+def test_fast_threshold_extremes(ctx):
     sc, A, _ = frames(160, 120, seed=9)
     g = ctx.image(A, 0)
     for t in (0, 1, 254, 255, 300, -5):
@@ -179,16 +166,14 @@ TEMPORAL = dict(win=(21, 21), ml=3, crit=(3, 50, 1e-3), flags=S.LK_GET_MIN_EIGEN
 STEREO = dict(win=(11, 11), ml=3, crit=(3, 30, 1e-3), flags=0)                        # R:src/tracking.cpp:101-105
 
 
-@pytest.fixture(params=["fixed-window", "two-px-margin", "generic", "one-per-wave", "dual", "two-per-wave"])
+@pytest.fixture(params=["fixed-window", "generic", "one-per-wave"])
 def lk_kernel(request, monkeypatch):
     """Every LK kernel: the compile-time-window ones (21x21 four features per
     wave by default, 11x11, 15x15, 31x31), the 21x21 one-feature-per-wave kernel
-    (SVO_LK_QUAD=0), the 21x21 two-per-wave kernels (SVO_LK_MULTI=0: lk_dual_kernel,
-    2: lk_multi_kernel<2>) and the runtime-window one every other size uses
+    (SVO_LK_QUAD=0) and the runtime-window one every other size uses
     (SVO_LK_GENERIC=1)."""
     monkeypatch.setenv("SVO_LK_GENERIC", "1" if request.param == "generic" else "0")
     monkeypatch.setenv("SVO_LK_QUAD", "0" if request.param == "one-per-wave" else "1")
-    monkeypatch.setenv("SVO_LK_MULTI", {"dual": "0", "two-per-wave": "2", "two-px-margin": "42"}.get(request.param, "41"))
     return request.param
 
 
