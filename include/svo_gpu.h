@@ -19,6 +19,8 @@
  *     cv::solvePnPRansac, R:src/tracking.cpp:191-196)
  *   cv::solvePnPRansac(..., SOLVEPNP_SQPNP)                      svo_solve_pnp_ransac
  *     R:src/tracking.cpp:191-196
+ *   cv::solvePnP(..., SOLVEPNP_SQPNP)  (solvePnPRansac's final   svo_solve_pnp_sqpnp
+ *     fit on the inliers, R:src/tracking.cpp:191-196)
  *   cv::triangulatePoints + convertPointsFromHomogeneous          svo_triangulate_points
  *     R:src/tracking.cpp:125-131
  *
@@ -176,6 +178,14 @@ int svo_solve_pnp_ransac(svo_ctx* ctx, const double* obj_xyz, const float* img_x
                          const double K[9], int iterations, float reproj_err,
                          double confidence, double rvec[3], double tvec[3], int* inliers,
                          int* n_inliers);
+
+/* cv::solvePnP(obj(Point3d), img(Point2f), K, zeros(1,4), rvec, tvec, false,
+ * SOLVEPNP_SQPNP): the fit solvePnPRansac ends with (calib3d/src/sqpnp.cpp's cost
+ * and solution search; host only, no context). Returns 1 (pose found), 0
+ * (SQPnP's asserts -- degenerate points -- or no solution in front of the
+ * camera) or SVO_ERR_ARG (null pointers, n < 3). */
+int svo_solve_pnp_sqpnp(const double* obj_xyz, const float* img_xy, int n, const double K[9], double rvec[3],
+                        double tvec[3]);
 
 /* RANSAC's minimal solver alone: SOLVEPNP_EPNP on 5 points, the model estimator
  * solvePnPRansac runs per hypothesis (R:src/tracking.cpp:191-196), for m subsets

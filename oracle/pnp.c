@@ -492,192 +492,6 @@ int svo_oracle_ransac_update_num_iters(double p, double ep, int modelPoints, int
     return denom >= 0 || -num >= maxIters * (-denom) ? maxIters : ora_round_d(num / denom);
 }
 
-/* ---------------------------------------------- final refit: SQPnP objective */
-
-/* Object-space cost of SQPnP: E(r) = r^T Omega r, t(r) = P r, for r = vec(R). */
-static void sqpnp_omega(const double* pw, const double* q, int n, double Om[81], double P[27])
-{
-    double Q[9] = {0}, QA[27] = {0}; /* QA = sum A_i B_i (3x9) */
-    double* AB = (double*)malloc(sizeof(double) * 27 * n);
-    for (int i = 0; i < n; i++) {
-        double x = q[2 * i], y = q[2 * i + 1];
-        double v[3] = {x, y, 1.0};
-        double nn = x * x + y * y + 1.0;
-        double A[9];
-        for (int a = 0; a < 3; a++)
-            for (int b = 0; b < 3; b++) A[a * 3 + b] = (a == b ? 1.0 : 0.0) - v[a] * v[b] / nn;
-        for (int k = 0; k < 9; k++) Q[k] += A[k];
-        double* ABi = AB + 27 * i;
-        const double* p = pw + 3 * i;
-        for (int a = 0; a < 3; a++)
-            for (int c = 0; c < 9; c++) {
-                int row = c / 3; /* B_i[row][c] = p[c%3] */
-                ABi[a * 9 + c] = A[a * 3 + row] * p[c % 3];
-                QA[a * 9 + c] += ABi[a * 9 + c];
-            }
-    }
-    double Qi[9];
-    inv3_pinv(Q, Qi);
-    for (int a = 0; a < 3; a++)
-        for (int c = 0; c < 9; c++) {
-            double s = 0;
-            for (int k = 0; k < 3; k++) s += Qi[a * 3 + k] * QA[k * 9 + c];
-            P[a * 9 + c] = -s;
-        }
-    /* e_i = A_i B_i r + A_i P r = (AB_i + A_i P) r ; Om = sum G_i^T G_i */
-    for (int k = 0; k < 81; k++) Om[k] = 0;
-    for (int i = 0; i < n; i++) {
-        double x = q[2 * i], y = q[2 * i + 1];
-        double v[3] = {x, y, 1.0};
-        double nn = x * x + y * y + 1.0;
-        double A[9];
-        for (int a = 0; a < 3; a++)
-            for (int b = 0; b < 3; b++) A[a * 3 + b] = (a == b ? 1.0 : 0.0) - v[a] * v[b] / nn;
-        double G[27];
-        const double* ABi = AB + 27 * i;
-        for (int a = 0; a < 3; a++)
-            for (int c = 0; c < 9; c++) {
-                double s = ABi[a * 9 + c];
-                for (int k = 0; k < 3; k++) s += A[a * 3 + k] * P[k * 9 + c];
-                G[a * 9 + c] = s;
-            }
-        for (int r = 0; r < 9; r++)
-            for (int c = 0; c < 9; c++) {
-                double s = 0;
-                for (int a = 0; a < 3; a++) s += G[a * 9 + r] * G[a * 9 + c];
-                Om[r * 9 + c] += s;
-            }
-    }
-    free(AB);
-}
-
-static double quad9(const double* Om, const double* r)
-{
-    double s = 0;
-    for (int i = 0; i < 9; i++) {
-        double t = 0;
-        for (int j = 0; j < 9; j++) t += Om[i * 9 + j] * r[j];
-        s += r[i] * t;
-    }
-    return s;
-}
-
-static void nearest_rotation(const double* M, double* R)
-{
-    double w[3], u[9], vt[9];
-    ora_svd(M, 3, 3, w, u, vt);
-    for (int i = 0; i < 3; i++)
-        for (int j = 0; j < 3; j++) R[3 * i + j] = u[3 * i] * vt[j] + u[3 * i + 1] * vt[3 + j] + u[3 * i + 2] * vt[6 + j];
-    double det = R[0] * (R[4] * R[8] - R[5] * R[7]) - R[1] * (R[3] * R[8] - R[5] * R[6]) + R[2] * (R[3] * R[7] - R[4] * R[6]);
-    if (det < 0) {
-        for (int i = 0; i < 3; i++)
-            for (int j = 0; j < 3; j++) R[3 * i + j] = u[3 * i] * vt[j] + u[3 * i + 1] * vt[3 + j] - u[3 * i + 2] * vt[6 + j];
-    }
-}
-
-/* Gauss-Newton on SO(3) (left perturbation) for min r^T Om r. */
-static double so3_refine(const double* Om, double* R)
-{
-    for (int it = 0; it < 100; it++) {
-        /* J columns: vec([e_k]x R) */
-        double J[27];
-        for (int k = 0; k < 3; k++) {
-            double G[9] = {0};
-            if (k == 0) { G[5] = -1; G[7] = 1; }
-            if (k == 1) { G[2] = 1; G[6] = -1; }
-            if (k == 2) { G[1] = -1; G[3] = 1; }
-            for (int i = 0; i < 3; i++)
-                for (int j = 0; j < 3; j++)
-                    J[(i * 3 + j) * 3 + k] = G[i * 3] * R[j] + G[i * 3 + 1] * R[3 + j] + G[i * 3 + 2] * R[6 + j];
-        }
-        double OJ[27], Or[9];
-        for (int i = 0; i < 9; i++) {
-            Or[i] = 0;
-            for (int j = 0; j < 9; j++) Or[i] += Om[i * 9 + j] * R[j];
-            for (int k = 0; k < 3; k++) {
-                OJ[i * 3 + k] = 0;
-                for (int j = 0; j < 9; j++) OJ[i * 3 + k] += Om[i * 9 + j] * J[j * 3 + k];
-            }
-        }
-        double H[9], g[3];
-        for (int a = 0; a < 3; a++) {
-            g[a] = 0;
-            for (int i = 0; i < 9; i++) g[a] += J[i * 3 + a] * Or[i];
-            for (int b = 0; b < 3; b++) {
-                H[a * 3 + b] = 0;
-                for (int i = 0; i < 9; i++) H[a * 3 + b] += J[i * 3 + a] * OJ[i * 3 + b];
-            }
-        }
-        double Hi[9], w[3];
-        inv3_pinv(H, Hi);
-        for (int a = 0; a < 3; a++) w[a] = -(Hi[a * 3] * g[0] + Hi[a * 3 + 1] * g[1] + Hi[a * 3 + 2] * g[2]);
-        double dR[9];
-        svo_oracle_rodrigues(w, dR);
-        double Rn[9];
-        for (int i = 0; i < 3; i++)
-            for (int j = 0; j < 3; j++) Rn[3 * i + j] = dR[3 * i] * R[j] + dR[3 * i + 1] * R[3 + j] + dR[3 * i + 2] * R[6 + j];
-        double e0 = quad9(Om, R), e1 = quad9(Om, Rn);
-        if (e1 > e0) break;
-        memcpy(R, Rn, sizeof(double) * 9);
-        if (w[0] * w[0] + w[1] * w[1] + w[2] * w[2] < 1e-24) break;
-    }
-    return quad9(Om, R);
-}
-
-static int positive_depth_majority(const double* pw, int n, const double* R, const double* t)
-{
-    int pos = 0;
-    for (int i = 0; i < n; i++) {
-        double z = R[6] * pw[3 * i] + R[7] * pw[3 * i + 1] + R[8] * pw[3 * i + 2] + t[2];
-        pos += z > 0;
-    }
-    return 2 * pos >= n;
-}
-
-static void sqpnp_refit(const double* pw, const double* q, int n, const double* R0, double* R, double* t)
-{
-    double Om[81], P[27];
-    sqpnp_omega(pw, q, n, Om, P);
-    double best = DBL_MAX;
-    double cand[9];
-    /* starts: the RANSAC model, and nearest rotations of Omega's two smallest
-     * eigenvectors (both signs), as SQPnP seeds its search */
-    double Oc[81], ev[9], evec[81];
-    memcpy(Oc, Om, sizeof(Oc));
-    ora_sym_eig(Oc, 9, ev, evec);
-    double starts[5][9];
-    memcpy(starts[0], R0, sizeof(double) * 9);
-    for (int s = 0; s < 4; s++) {
-        const double* e = evec + 9 * (8 - (s >> 1));
-        double M[9];
-        double sg = (s & 1) ? -1.0 : 1.0;
-        for (int k = 0; k < 9; k++) M[k] = sg * e[k] * sqrt(3.0);
-        nearest_rotation(M, starts[s + 1]);
-    }
-    for (int s = 0; s < 5; s++) {
-        memcpy(cand, starts[s], sizeof(cand));
-        double E = so3_refine(Om, cand);
-        double tc[3];
-        for (int a = 0; a < 3; a++) {
-            tc[a] = 0;
-            for (int c = 0; c < 9; c++) tc[a] += P[a * 9 + c] * cand[c];
-        }
-        if (!positive_depth_majority(pw, n, cand, tc)) continue;
-        if (E < best) {
-            best = E;
-            memcpy(R, cand, sizeof(double) * 9);
-            memcpy(t, tc, sizeof(double) * 3);
-        }
-    }
-    if (best == DBL_MAX) {
-        memcpy(R, R0, sizeof(double) * 9);
-        for (int a = 0; a < 3; a++) {
-            t[a] = 0;
-            for (int c = 0; c < 9; c++) t[a] += P[a * 9 + c] * R0[c];
-        }
-    }
-}
-
 int svo_oracle_solve_pnp_ransac(const double* obj_d, const float* img, int n, const double K[9],
                                 int iterations, float reproj_err, double confidence,
                                 double rvec[3], double tvec[3], uint8_t* inlier_mask,
@@ -754,12 +568,15 @@ int svo_oracle_solve_pnp_ransac(const double* obj_d, const float* img, int n, co
         ni++;
     }
     double Rf[9], tf[3];
-    sqpnp_refit(pw, q, ni, bestR, Rf, tf);
-    svo_oracle_rodrigues_inv(Rf, rvec);
-    memcpy(tvec, tf, sizeof(tf));
+    if (svo_oracle_sqpnp(pw, q, ni, Rf, tf) == 0) {
+        svo_oracle_rodrigues_inv(Rf, rvec);
+        memcpy(tvec, tf, sizeof(tf));
+    } else {  /* solvePnP would throw; keep the RANSAC model */
+        memcpy(rvec, best_rv, sizeof(best_rv));
+        memcpy(tvec, bestt, sizeof(bestt));
+    }
     memcpy(inlier_mask, best, (size_t)n);
     if (n_inliers) *n_inliers = maxGood;
-    (void)best_rv;
     free(pw); free(q); free(obj); free(best); free(cur);
     return 1;
 }

@@ -161,14 +161,20 @@ int svo_oracle_ransac_update_num_iters(double p, double ep, int model_points, in
 
 /* cv::solvePnPRansac(obj(Point3d), img(Point2f), K, zeros(1,4), rvec, tvec,
  * false, iters, reproj, confidence, inliers, SOLVEPNP_SQPNP) -- RANSAC stage
- * (EPnP minimal kernel, 5-point subsets, cv::RNG(-1)) exactly; the final refit
- * on the inliers minimises the SQPnP objective. Returns 1 on
+ * (EPnP minimal kernel, 5-point subsets, cv::RNG(-1)) exactly; the final
+ * solvePnP(SQPNP) on the inliers by svo_oracle_sqpnp (sqpnp.c). Returns 1 on
  * success, 0 if RANSAC found no model, -1 on bad args (< 4 points).
  * inlier_mask: n bytes. n_hyp_out: hypotheses evaluated. */
 int svo_oracle_solve_pnp_ransac(const double* obj_xyz_d, const float* img_xy, int n,
                                 const double K[9], int iterations, float reproj_err,
                                 double confidence, double rvec[3], double tvec[3],
                                 uint8_t* inlier_mask, int* n_inliers, int* n_hyp_out);
+
+/* calib3d/src/sqpnp.cpp PoseSolver::solve (sqpnp.c): pw n x 3 object points,
+ * q n x 2 normalised image points (undistortPoints with K, zero distortion);
+ * the first (smallest-error) solution. Returns 0 on ok, -1 when SQPnP asserts
+ * (point variance, rank) or finds no solution with positive depth. */
+int svo_oracle_sqpnp(const double* pw, const double* q, int n, double R[9], double t[3]);
 
 /* Subset draw of RANSACPointSetRegistrator::getSubset (modelPoints 5, no
  * checkSubset): draws `k` distinct indices in [0,count). Returns 1 if found. */

@@ -90,6 +90,7 @@ _SIGS = [
     ("svo_solve_pnp_ransac", C.c_int, [_vp, _f64p, _f32p, C.c_int, _f64p, C.c_int, C.c_float,
                                        C.c_double, _f64p, _f64p, _i32p, _i32p]),
     ("svo_epnp_subsets", C.c_int, [_vp, _f32p, C.c_int, _f64p, C.c_int, _f64p, _i32p]),
+    ("svo_solve_pnp_sqpnp", C.c_int, [_f64p, _f32p, C.c_int, _f64p, _f64p, _f64p]),
     ("svo_triangulate_points", C.c_int, [_vp, _f32p, _f32p, _f32p, _f32p, C.c_int, _f32p, _f32p]),
     ("svo_reprojection_jacobians", C.c_int, [_vp, _f64p, _f32p, _i32p, C.c_int, C.c_int, _f64p, _f64p,
                                              C.c_double, _f64p, _f64p, _f64p]),
@@ -121,6 +122,21 @@ _SIGS = [
 ]
 
 SYMBOLS = [s[0] for s in _SIGS]
+
+
+def solve_pnp_sqpnp(obj, img_pts, K):
+    """cv::solvePnP(..., SOLVEPNP_SQPNP) -> (ok, rvec, tvec): solvePnPRansac's final
+    fit (svo_solve_pnp_sqpnp, host code of the library; no GPU context)."""
+    obj = _c(obj, np.float64).reshape(-1, 3)
+    img_pts = _c(img_pts, np.float32).reshape(-1, 2)
+    K = _c(K, np.float64).reshape(9)
+    rv = np.zeros(3)
+    tv = np.zeros(3)
+    rc = lib().svo_solve_pnp_sqpnp(_p(obj, _f64p), _p(img_pts, _f32p), len(obj), _p(K, _f64p), _p(rv, _f64p),
+                                   _p(tv, _f64p))
+    if rc < 0:
+        raise SvoError(f"svo_solve_pnp_sqpnp: error {rc}")
+    return rc == 1, rv, tv
 
 
 def host_cpu_plan(local_rank, local_world, gpu_node=None, cap=4096):

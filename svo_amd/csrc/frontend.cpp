@@ -678,7 +678,7 @@ double fe_finish_fits(svo_frontend* fe) {
     (void)hipEventSynchronize(fe->ev_full_b[fe->fit_parity]);  // cheirality test reads h_obj
     fe->pool->run(fe->S, [&](int s) {
         RansacSeq& r = fe->rs[s];
-        r.fit(fe->cfg.K, fe->h_stats + 60 * (size_t)s);
+        r.fit(fe->cfg.K, fe->h_stats + kSqpnpStats * (size_t)s);
         double* P = &fe->pose[6 * (size_t)s];
         if (r.ok) {
             std::memcpy(P, r.rvec, sizeof(r.rvec));
@@ -843,7 +843,7 @@ int svo_frontend_create(svo_ctx* ctx, const svo_frontend_config* cfg, svo_fronte
         add(sizeof(float) * kSampleFloats * kRansacPrefetch * (size_t)S);
         add(sizeof(uint32_t) * (size_t)S * fe->WORDS);
         add(sizeof(uint32_t) * (size_t)S * fe->WORDS);
-        add(sizeof(double) * 60 * (size_t)S);
+        add(sizeof(double) * kSqpnpStats * (size_t)S);
         add(sizeof(double) * 12 * (size_t)S);
         add(1024);
         if (hipHostMalloc(&fe->zout, zb, hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess) {
@@ -862,7 +862,7 @@ int svo_frontend_create(svo_ctx* ctx, const svo_frontend_config* cfg, svo_fronte
         fe->h_best_b[0] = carve<uint32_t>(p, (size_t)S * fe->WORDS);
         fe->h_best_b[1] = carve<uint32_t>(p, (size_t)S * fe->WORDS);
         fe->h_best = fe->h_best_b[0];
-        fe->h_stats = carve<double>(p, 60 * (size_t)S);
+        fe->h_stats = carve<double>(p, kSqpnpStats * (size_t)S);
         fe->h_pose = carve<double>(p, 12 * (size_t)S);
         for (int s = 0; s < S; s++) fe_set_pose(fe, s, false, nullptr, nullptr);
     }

@@ -11,8 +11,11 @@
 //   scored in chunks; the accept rule is then replayed in iteration order, and
 //   iterations past the (shrinking) niters are discarded -- identical result
 //   to the serial loop.
-//   Final fit (solvePnP SQPNP on the inliers): minimiser of SQPnP's object-space
-//   cost r^T Omega r over SO(3) (multi-start Gauss-Newton), see DESIGN.md.
+//   Final fit (solvePnP SQPNP on the inliers, calib3d/src/sqpnp.cpp): minimiser
+//   of SQPnP's cost r^T Omega r over SO(3) -- Omega as PoseSolver::computeOmega
+//   builds it (the algebraic image-space error [1 0 -x; 0 1 -y](R X + t) with t
+//   eliminated, t = P r) -- by multi-start Gauss-Newton instead of SQPnP's SQP
+//   iterations (same minimiser; the oracle restates the SQP solver: DESIGN.md).
 #include <cfloat>
 #include <cstring>
 #include <vector>
@@ -38,77 +41,84 @@ int update_num_iters(double p, double ep, int model_points, int max_iters) {
     return denom >= 0 || -num >= max_iters * (-denom) ? max_iters : (int)rint(num / denom);
 }
 
-// ---- final fit: SQPnP's object-space cost, E(R) = vec(R)^T Omega vec(R) ----
+// ---- final fit: SQPnP's cost, E(R) = vec(R)^T Omega vec(R) ----
 struct SqpnpCost {
     double Om[81];
-    double P[27];  // t = P vec(R)
+    double P[27];    // t = P vec(R)
+    double mean[3];  // object-point mean (PoseSolver::positiveDepth)
+    bool ok;         // computeOmega's asserts held (point variance, rank)
 };
-
-// Omega = sum_i (B_i + P)^T A_i (B_i + P) with A_i = I - v v^T / v^T v,
-// B_i vec(R) = R p_i, P = -Q^-1 S: expanded through the sufficient statistics
-// Q = sum A_i, S = sum A_i B_i, M = sum B_i^T A_i B_i as Omega = M - S^T Q^-1 S
-// (one pass, ~130 flops per point).
 }  // namespace
 
-// The 60 sufficient statistics of one point set: Q = sum A_i (6 unique),
-// T[u][j] = sum A_i,u p_j (18), U[u][v] = sum A_i,u (p p^T)_v (36); A_i as
-// symmetric 6-vectors. Host twin of pnp.hip's suffstats kernel.
+// The sufficient statistics of one point set (pose.hpp); host twin of pnp.hip's
+// suffstats kernel (same per-point arithmetic, same order within a point).
 void sqpnp_sums(const double* pw, const double* q, int n, double* sums) {
-    double Qs[6] = {0}, T[6][3] = {{0}}, U[6][6] = {{0}};
+    std::memset(sums, 0, sizeof(double) * kSqpnpStats);
     for (int i = 0; i < n; i++) {
-        const double x = q[2 * i], y = q[2 * i + 1];
-        const double in = 1.0 / (x * x + y * y + 1.0);
-        const double As[6] = {1.0 - x * x * in, -x * y * in, -x * in, 1.0 - y * y * in, -y * in, 1.0 - in};
+        const double x = q[2 * i], y = q[2 * i + 1], sq = x * x + y * y;
         const double* p = pw + 3 * (size_t)i;
         const double pp[6] = {p[0] * p[0], p[0] * p[1], p[0] * p[2], p[1] * p[1], p[1] * p[2], p[2] * p[2]};
-        for (int u = 0; u < 6; u++) {
-            Qs[u] += As[u];
-            T[u][0] += As[u] * p[0];
-            T[u][1] += As[u] * p[1];
-            T[u][2] += As[u] * p[2];
-            for (int v = 0; v < 6; v++) U[u][v] += As[u] * pp[v];
+        const double c[4] = {1.0, x, y, sq};
+        sums[0] += 1.0;
+        sums[1] += x;
+        sums[2] += y;
+        sums[3] += sq;
+        for (int u = 0; u < 4; u++) {
+            for (int j = 0; j < 3; j++) sums[4 + 3 * u + j] += c[u] * p[j];
+            for (int v = 0; v < 6; v++) sums[16 + 6 * u + v] += c[u] * pp[v];
         }
     }
-    std::memcpy(sums, Qs, sizeof(Qs));
-    std::memcpy(sums + 6, T, sizeof(T));
-    std::memcpy(sums + 24, U, sizeof(U));
 }
 
 namespace {
 
-// Omega = sum_i (B_i + P)^T A_i (B_i + P) with A_i = I - v v^T / v^T v,
-// B_i vec(R) = R p_i, P = -Q^-1 S, assembled from the sufficient statistics
-// as Omega = M - S^T Q^-1 S.
+// PoseSolver::computeOmega from the statistics: Omega_raw = sum B_i^T A_i^T A_i
+// B_i (blocks XX^T, -x XX^T, -y XX^T, (x^2+y^2) XX^T), qa = sum A_i^T A_i B_i,
+// Q = sum A_i^T A_i, P = -Q^-1 qa, Omega = Omega_raw + qa^T P; ok = false where
+// SQPnP asserts (point variance below 1e-5, largest singular value below 1e-7).
 void sqpnp_assemble(const double* sums, SqpnpCost& c) {
     static const int IDX[3][3] = {{0, 1, 2}, {1, 3, 4}, {2, 4, 5}};  // unique entries of a sym 3x3
-    const double* Qs = sums;
-    auto T = [&](int u, int j) { return sums[6 + 3 * u + j]; };
-    auto U = [&](int u, int v) { return sums[24 + 6 * u + v]; };
-    double Q[9], S[27], Qi[9];
+    const double n = sums[0], sx = sums[1], sy = sums[2], ssq = sums[3];
+    auto SX = [&](int u, int j) { return sums[4 + 3 * u + j]; };           // sum c_u X_j
+    auto SXX = [&](int u, int a, int b) { return sums[16 + 6 * u + IDX[a][b]]; };  // sum c_u X_a X_b
+    double Om[81] = {0}, qa[27] = {0};
     for (int a = 0; a < 3; a++)
-        for (int b = 0; b < 3; b++) Q[3 * a + b] = Qs[IDX[a][b]];
-    for (int a = 0; a < 3; a++)
-        for (int r = 0; r < 3; r++)
-            for (int j = 0; j < 3; j++) S[9 * a + 3 * r + j] = T(IDX[a][r], j);
+        for (int b = 0; b < 3; b++) {
+            Om[9 * a + b] = SXX(0, a, b);
+            Om[9 * (3 + a) + 3 + b] = SXX(0, a, b);
+            Om[9 * a + 6 + b] = Om[9 * (6 + b) + a] = -SXX(1, a, b);
+            Om[9 * (3 + a) + 6 + b] = Om[9 * (6 + b) + 3 + a] = -SXX(2, a, b);
+            Om[9 * (6 + a) + 6 + b] = SXX(3, a, b);
+        }
+    for (int j = 0; j < 3; j++) {
+        qa[j] = SX(0, j);
+        qa[6 + j] = -SX(1, j);
+        qa[9 + 3 + j] = SX(0, j);
+        qa[9 + 6 + j] = -SX(2, j);
+        qa[18 + j] = -SX(1, j);
+        qa[18 + 3 + j] = -SX(2, j);
+        qa[18 + 6 + j] = SX(3, j);
+    }
+    const double Q[9] = {n, 0, -sx, 0, n, -sy, -sx, -sy, ssq};
+    const double detQ = n * (n * ssq - sy * sy - sx * sx);
+    c.ok = n > 0 && detQ / (n * n * n) >= 1e-5;
+    double Qi[9];
     la::pinv3(Q, Qi);
     for (int a = 0; a < 3; a++)
         for (int col = 0; col < 9; col++)
-            c.P[9 * a + col] = -(Qi[3 * a] * S[col] + Qi[3 * a + 1] * S[9 + col] + Qi[3 * a + 2] * S[18 + col]);
-    for (int r = 0; r < 3; r++)
-        for (int j = 0; j < 3; j++)
-            for (int s2 = 0; s2 < 3; s2++)
-                for (int k = 0; k < 3; k++) {
-                    // M[(r,j),(s,k)] = sum A_rs p_j p_k ; minus (S^T Qi S) = + S^T P
-                    const double m = U(IDX[r][s2], IDX[j][k]);
-                    const int R = 3 * r + j, Cc = 3 * s2 + k;
-                    double stp = S[R] * c.P[Cc] + S[9 + R] * c.P[9 + Cc] + S[18 + R] * c.P[18 + Cc];
-                    c.Om[9 * R + Cc] = m + stp;
-                }
+            c.P[9 * a + col] = -(Qi[3 * a] * qa[col] + Qi[3 * a + 1] * qa[9 + col] + Qi[3 * a + 2] * qa[18 + col]);
+    for (int i = 0; i < 9; i++)
+        for (int j = 0; j < 9; j++)
+            c.Om[9 * i + j] = Om[9 * i + j] + (qa[i] * c.P[j] + qa[9 + i] * c.P[9 + j] + qa[18 + i] * c.P[18 + j]);
     for (int r = 0; r < 9; r++)  // symmetrise
         for (int col = 0; col < r; col++) {
             const double v = 0.5 * (c.Om[9 * r + col] + c.Om[9 * col + r]);
             c.Om[9 * r + col] = c.Om[9 * col + r] = v;
         }
+    for (int j = 0; j < 3; j++) c.mean[j] = n > 0 ? SX(0, j) / n : 0.0;
+    double maxd = 0;
+    for (int i = 0; i < 9; i++) maxd = std::max(maxd, c.Om[10 * i]);
+    c.ok = c.ok && maxd >= 1e-7;
 }
 
 double quad(const double* Om, const double* r) {
@@ -159,53 +169,108 @@ double refine_so3(const double* Om, double* R) {
     return quad(Om, R);
 }
 
-// Minimiser of r^T Omega r over SO(3): Gauss-Newton from the RANSAC rotation
-// and from the nearest rotations of Omega's two smallest eigenvectors (both
-// signs); the lowest-cost start whose solution puts at least half the inliers
-// in front of the camera wins (SQPnP's cheirality test).
-void fit_from_cost(const SqpnpCost& c, const float* obj, const std::vector<int>& inl, const double R0[9],
-                   double R[9], double t[3]) {
-    const int n = (int)inl.size();
+// SQPnP's solution search (PoseSolver::solveInternal) over Omega's eigenvectors,
+// with the SQP runs done by Gauss-Newton on SO(3) (refine_so3: the same
+// constrained minimiser from the same start):
+//   the null-space eigenvectors e (eigenvalues below the rank tolerance 1e-7; at
+//   least the smallest), sqrt(3)-scaled: if e is already orthogonal (squared
+//   orthogonality error < 1e-8) it is taken as is, det-signed, with t = P e (no
+//   refinement -- OpenCV's shortcut); else runs from the nearest rotations of +e
+//   and -e; then further eigenvectors while the best error exceeds 3x their
+//   eigenvalue. checkSolution: the object-point mean in front of the camera or a
+//   majority of positive depths; errors within 1e-6 and rotations within 1e-10
+//   are one solution; the first smallest-error solution is solvePnP's.
+struct SqSol {
+    double r[9], t[3], err;
+};
+
+double ortho_err(const double* e) {
+    const double n1 = e[0] * e[0] + e[1] * e[1] + e[2] * e[2], n2 = e[3] * e[3] + e[4] * e[4] + e[5] * e[5],
+                 n3 = e[6] * e[6] + e[7] * e[7] + e[8] * e[8];
+    const double d12 = e[0] * e[3] + e[1] * e[4] + e[2] * e[5], d13 = e[0] * e[6] + e[1] * e[7] + e[2] * e[8],
+                 d23 = e[3] * e[6] + e[4] * e[7] + e[5] * e[8];
+    return (n1 - 1) * (n1 - 1) + (n2 - 1) * (n2 - 1) + (n3 - 1) * (n3 - 1) + 2 * (d12 * d12 + d13 * d13 + d23 * d23);
+}
+
+double det33(const double* m) {
+    return m[0] * (m[4] * m[8] - m[5] * m[7]) - m[1] * (m[3] * m[8] - m[5] * m[6]) + m[2] * (m[3] * m[7] - m[4] * m[6]);
+}
+
+// pt(k, p): object point k of the n fitted points into p[3]
+template <class PointAt>
+void fit_from_cost(const SqpnpCost& c, int n, PointAt pt, double R[9], double t[3], bool* found) {
     double Oc[81], ev[9], evec[81];
     std::memcpy(Oc, c.Om, sizeof(Oc));
-    la::sym_eig_ql(Oc, 9, ev, evec);
-    double starts[5][9], Es[5], ts[5][3];
-    std::memcpy(starts[0], R0, sizeof(double) * 9);
-    for (int s = 0; s < 4; s++) {
-        const double* e = evec + 9 * (8 - (s >> 1));
-        double M[9];
-        for (int k = 0; k < 9; k++) M[k] = ((s & 1) ? -1.0 : 1.0) * e[k];
-        la::nearest_rotation(M, starts[s + 1]);
-    }
-    for (int s = 0; s < 5; s++) {
-        Es[s] = refine_so3(c.Om, starts[s]);
+    la::sym_eig_ql(Oc, 9, ev, evec);  // descending; eigenvector k in row k
+    int nn = 0;
+    while (7 - nn >= 0 && ev[7 - nn] < 1e-7) nn++;
+    nn++;
+    std::vector<SqSol> sols;
+    double min_err = DBL_MAX;
+    auto check = [&](SqSol& s) {
         for (int a = 0; a < 3; a++) {
-            ts[s][a] = 0;
-            for (int col = 0; col < 9; col++) ts[s][a] += c.P[9 * a + col] * starts[s][col];
+            s.t[a] = 0;
+            for (int col = 0; col < 9; col++) s.t[a] += c.P[9 * a + col] * s.r[col];
+        }
+        bool front = dot3(s.r + 6, c.mean) + s.t[2] > 0;
+        if (!front) {
+            int pos = 0;
+            for (int k = 0; k < n; k++) {
+                double p[3];
+                pt(k, p);
+                pos += dot3(s.r + 6, p) + s.t[2] > 0;
+            }
+            front = pos >= n - pos;
+        }
+        if (!front) return;
+        s.err = quad(c.Om, s.r);
+        if (fabs(min_err - s.err) > 1e-6) {
+            if (min_err > s.err) {
+                min_err = s.err;
+                sols.assign(1, s);
+            }
+        } else {
+            bool same = false;
+            for (auto& o : sols) {
+                double d = 0;
+                for (int k = 0; k < 9; k++) d += (o.r[k] - s.r[k]) * (o.r[k] - s.r[k]);
+                if (d < 1e-10) {
+                    if (o.err > s.err) o = s;
+                    same = true;
+                    break;
+                }
+            }
+            if (!same) sols.push_back(s);
+            if (min_err > s.err) min_err = s.err;
+        }
+    };
+    auto from_eigen = [&](const double* e) {
+        for (int sg = 0; sg < 2; sg++) {
+            double m[9];
+            SqSol s;
+            for (int k = 0; k < 9; k++) m[k] = sg ? -e[k] : e[k];
+            la::nearest_rotation(m, s.r);
+            refine_so3(c.Om, s.r);
+            check(s);
+        }
+    };
+    for (int i = 9 - nn; i < 9; i++) {
+        double e[9];
+        for (int k = 0; k < 9; k++) e[k] = 1.7320508075688772 * evec[9 * i + k];
+        if (ortho_err(e) < 1e-8) {
+            SqSol s;
+            const double d = det33(e);
+            for (int k = 0; k < 9; k++) s.r[k] = d * e[k];
+            check(s);
+        } else {
+            from_eigen(e);
         }
     }
-    // candidates in cost order (ties: start order), first cheirality pass wins
-    int ord[5] = {0, 1, 2, 3, 4};
-    for (int i = 1; i < 5; i++)
-        for (int j = i; j > 0 && Es[ord[j]] < Es[ord[j - 1]]; j--) std::swap(ord[j], ord[j - 1]);
-    for (int k = 0; k < 5; k++) {
-        const int s = ord[k];
-        const double* cand = starts[s];
-        int pos = 0;
-        for (int i : inl) {
-            const double p[3] = {obj[3 * i], obj[3 * i + 1], obj[3 * i + 2]};
-            pos += dot3(cand + 6, p) + ts[s][2] > 0;
-        }
-        if (2 * pos < n) continue;
-        std::memcpy(R, cand, sizeof(double) * 9);
-        std::memcpy(t, ts[s], sizeof(double) * 3);
-        return;
-    }
-    std::memcpy(R, R0, sizeof(double) * 9);
-    for (int a = 0; a < 3; a++) {
-        t[a] = 0;
-        for (int col = 0; col < 9; col++) t[a] += c.P[9 * a + col] * R0[col];
-    }
+    for (int k = 1; 9 - nn - k > 0 && min_err > 3 * ev[9 - nn - k]; k++) from_eigen(evec + 9 * (9 - nn - k));
+    *found = !sols.empty();
+    if (!*found) return;
+    std::memcpy(R, sols[0].r, sizeof(double) * 9);  // (rodrigues_inv re-orthonormalises, as cv::Rodrigues)
+    std::memcpy(t, sols[0].t, sizeof(double) * 3);
 }
 
 }  // namespace
@@ -224,6 +289,7 @@ void RansacSeq::begin(const float* o, const float* im, int npts, int iterations)
     rounds = 0;
     best.assign((size_t)(n + 31) / 32, 0u);
     for (int i = 0; i < 9; i++) bestR[i] = (i % 4 == 0) ? 1.0 : 0.0;
+    bestt[0] = bestt[1] = bestt[2] = 0.0;
     direct = n <= 5;
     done = n < 4;
     ok = false;
@@ -299,6 +365,7 @@ void RansacSeq::consume(const int* counts, const uint32_t* bits, int words_cap, 
         if (good > (maxGood > 4 ? maxGood : 4)) {
             std::memcpy(best.data(), bits + (size_t)words_cap * j, sizeof(uint32_t) * words);
             std::memcpy(bestR, hyp + 12 * j, sizeof(double) * 9);
+            std::memcpy(bestt, hyp + 12 * j + 9, sizeof(double) * 3);
             maxGood = good;
             niters = update_num_iters(confidence, (double)(n - good) / n, 5, niters);
         }
@@ -351,7 +418,7 @@ void RansacSeq::fit(const double K[9], const double* sums) {
     if (inliers.empty())  // select(..., false) left the list to here
         for (int i = 0; i < n; i++)
             if ((best[i >> 5] >> (i & 31)) & 1) inliers.push_back(i);
-    double own[60];
+    double own[kSqpnpStats];
     if (!sums) {
         std::vector<double> pw, q;
         inlier_arrays(obj, img, inliers, K, pw, q);
@@ -360,11 +427,30 @@ void RansacSeq::fit(const double K[9], const double* sums) {
     }
     SqpnpCost c;
     sqpnp_assemble(sums, c);
+    fitted = true;
+    if (!c.ok) {  // solvePnP(SQPNP) would assert: keep the RANSAC model (as the oracle)
+        la::rodrigues_inv(bestR, rvec);
+        std::memcpy(tvec, bestt, sizeof(bestt));
+        return;
+    }
     double Rf[9], tf[3];
-    fit_from_cost(c, obj, inliers, bestR, Rf, tf);
+    bool found = false;
+    fit_from_cost(
+        c, (int)inliers.size(),
+        [&](int k, double* p) {
+            const int i = inliers[k];
+            p[0] = obj[3 * i];
+            p[1] = obj[3 * i + 1];
+            p[2] = obj[3 * i + 2];
+        },
+        Rf, tf, &found);
+    if (!found) {  // no solution in front of the camera: solvePnP fails, keep the RANSAC model
+        la::rodrigues_inv(bestR, rvec);
+        std::memcpy(tvec, bestt, sizeof(bestt));
+        return;
+    }
     la::rodrigues_inv(Rf, rvec);
     std::memcpy(tvec, tf, sizeof(tf));
-    fitted = true;
 }
 
 void RansacSeq::finish(const double K[9]) {
@@ -373,6 +459,33 @@ void RansacSeq::finish(const double K[9]) {
 }
 
 }  // namespace svo
+
+// cv::solvePnP(obj, img, K, zeros, rvec, tvec, false, SOLVEPNP_SQPNP) on the host
+// (the fit solvePnPRansac ends with, R:src/tracking.cpp:191-196)
+extern "C" int svo_solve_pnp_sqpnp(const double* obj_xyz, const float* img_xy, int n, const double K[9],
+                                   double rvec[3], double tvec[3]) {
+    using namespace svo;
+    if (!obj_xyz || !img_xy || !K || !rvec || !tvec || n < 3) return SVO_ERR_ARG;
+    std::vector<double> q(2 * (size_t)n);
+    const double ifx = 1. / K[0], ify = 1. / K[4];
+    for (int i = 0; i < n; i++) {
+        q[2 * i] = ((double)img_xy[2 * i] - K[2]) * ifx;
+        q[2 * i + 1] = ((double)img_xy[2 * i + 1] - K[5]) * ify;
+    }
+    double sums[kSqpnpStats];
+    sqpnp_sums(obj_xyz, q.data(), n, sums);
+    SqpnpCost c;
+    sqpnp_assemble(sums, c);
+    if (!c.ok) return 0;
+    double R[9], t[3];
+    bool found = false;
+    fit_from_cost(
+        c, n, [&](int k, double* p) { std::memcpy(p, obj_xyz + 3 * (size_t)k, sizeof(double) * 3); }, R, t, &found);
+    if (!found) return 0;
+    la::rodrigues_inv(R, rvec);
+    std::memcpy(tvec, t, sizeof(t));
+    return 1;
+}
 
 extern "C" int svo_solve_pnp_ransac(svo_ctx* ctx, const double* obj_xyz, const float* img_xy, int n,
                                     const double K[9], int iterations, float reproj_err, double confidence,

@@ -42,7 +42,7 @@ struct RansacSeq {
     bool valid[kRansacChunk];
     double hyp[12 * kRansacChunk];
     std::vector<uint32_t> best;
-    double bestR[9];
+    double bestR[9], bestt[3];
     std::vector<int> inliers;
     double rvec[3] = {0, 0, 0}, tvec[3] = {0, 0, 0};
 
@@ -58,13 +58,17 @@ struct RansacSeq {
     // inlier set of the best model (the output): `best` bits, and the index list
     // too unless list = false (fit() then builds it)
     void select(const double K[9], bool list = true);
-    // final SQPnP-objective fit on the inliers; sums = their 60 sufficient
-    // statistics (sqpnp_sums / the suffstats kernel) or null to compute here
+    // final SQPnP-objective fit on the inliers; sums = their kSqpnpStats
+    // sufficient statistics (sqpnp_sums / the suffstats kernel) or null to compute here
     void fit(const double K[9], const double* sums);
     void finish(const double K[9]);    // select + fit
 };
 
-// Sufficient statistics of the SQPnP cost over n points (60 doubles).
+// Sufficient statistics of SQPnP's cost over n points (kSqpnpStats doubles):
+// [0] n, [1] sum x, [2] sum y, [3] sum (x^2 + y^2), [4..15] sum c X for c in
+// (1, x, y, x^2 + y^2), [16..39] sum c X X^T (6 unique entries each), with (x, y)
+// the normalised image point and X the object point.
+constexpr int kSqpnpStats = 40;
 void sqpnp_sums(const double* pw, const double* q, int n, double* sums);
 
 }  // namespace svo

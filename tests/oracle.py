@@ -57,6 +57,7 @@ def load():
             "svo_oracle_solve_pnp_ransac": (C.c_int, [_f64p, _f32p, C.c_int, _f64p, C.c_int, C.c_float,
                                                       C.c_double, _f64p, _f64p, _u8p, _i32p, _i32p]),
             "svo_oracle_get_subset": (C.c_int, [_u64p, C.c_int, C.c_int, _i32p]),
+            "svo_oracle_sqpnp": (C.c_int, [_f64p, _f64p, C.c_int, _f64p, _f64p]),
             "svo_oracle_triangulate": (None, [_f32p, _f32p, _f32p, _f32p, C.c_int, _f32p, _f32p]),
             "svo_oracle_set_threads": (None, [C.c_int]),
             "svo_oracle_bgr2gray": (None, [_u8p, C.c_int, C.c_int, C.c_int, _u8p]),
@@ -226,6 +227,17 @@ def solve_pnp_ransac(obj, img, K, iterations=100, reproj=8.0, confidence=0.999):
                                             confidence, _p(rv, _f64p), _p(tv, _f64p), _p(mask, _u8p),
                                             C.byref(ni), C.byref(nh))
     return rc, rv, tv, np.nonzero(mask[:n])[0].astype(np.int32), nh.value
+
+
+def sqpnp(pw, q):
+    """calib3d/src/sqpnp.cpp PoseSolver on object points pw (n, 3) and normalised
+    image points q (n, 2): (rc, R, t), rc 0 on success."""
+    pw = _c(pw, np.float64).reshape(-1, 3)
+    q = _c(q, np.float64).reshape(-1, 2)
+    R = np.zeros(9)
+    t = np.zeros(3)
+    rc = load().svo_oracle_sqpnp(_p(pw, _f64p), _p(q, _f64p), len(pw), _p(R, _f64p), _p(t, _f64p))
+    return rc, R.reshape(3, 3), t
 
 
 def update_num_iters(p, ep, model_points, max_iters):

@@ -401,6 +401,17 @@ def test_epnp_wave_matches_host(ctx):
     assert okh.sum() == len(subs)
     assert np.array_equal(okd, okh)
     assert np.array_equal(Rd.view(np.uint64), Rh.view(np.uint64))
+    # ... and against the oracle's independent EPnP (calib3d/src/epnp.cpp restated:
+    # Jacobi eigen-solver + SVD, oracle/pnp.c) on the same subsets: the device
+    # solver's Householder/QL eigen path differs only in the last bits
+    worst_r = worst_t = 0.0
+    for k in range(len(subs)):
+        rc, Ro, to = O.epnp(subs[k, :15].reshape(5, 3), subs[k, 15:].reshape(5, 2), K)
+        assert rc == 0
+        worst_r = max(worst_r, np.abs(Rd[k, :9].reshape(3, 3) - Ro).max())
+        worst_t = max(worst_t, np.abs(Rd[k, 9:] - to).max() / max(1.0, np.abs(to).max()))
+    print(f"device EPnP vs oracle EPnP over {len(subs)} subsets: max |dR| {worst_r:.3g}, max rel |dt| {worst_t:.3g}")
+    assert worst_r < 1e-6 and worst_t < 1e-6
 
 
 def test_pnp_ransac_too_few_points(ctx):

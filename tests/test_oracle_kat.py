@@ -304,3 +304,52 @@ def test_kat_triangulate_exact_projections():
     q1 = P0.astype(np.float64) @ Xb.T; q2 = P1.astype(np.float64) @ Xb.T
     _, xb = O.triangulate(P0, P1, (q1[:2] / q1[2]).T, (q2[:2] / q2[2]).T)
     assert xb[0, 2] < 0 and abs(xb[0, 2] + 8.0) < 1e-3
+
+
+# ------------------------------------------------------------------ SQPnP (solvePnP SOLVEPNP_SQPNP)
+def _sqpnp_case(n, noise, seed):
+    from scipy.spatial.transform import Rotation as Rot
+    rng = np.random.default_rng(seed)
+    X = np.c_[rng.uniform(-15, 15, n), rng.uniform(-4, 4, n), rng.uniform(6, 40, n)]
+    R = Rot.from_rotvec([0.02, -0.05, 0.01]).as_matrix()
+    t = np.array([0.3, -0.1, 0.8])
+    Y = X @ R.T + t
+    q = Y[:, :2] / Y[:, 2:] + rng.normal(0, noise, (n, 2))
+    return X, q, R, t
+
+
+def test_kat_sqpnp_exact_correspondences():
+    """Noise-free normalised projections: SQPnP returns the generating pose."""
+    X, q, R, t = _sqpnp_case(200, 0.0, 1)
+    rc, Rs, ts = O.sqpnp(X, q)
+    assert rc == 0
+    assert np.abs(Rs - R).max() < 1e-9 and np.abs(ts - t).max() < 1e-9
+
+
+def test_kat_sqpnp_is_the_algebraic_cost_minimiser():
+    """With noise, SQPnP's pose is the global minimiser of its cost, the
+    algebraic image-space error [1 0 -x; 0 1 -y](R X + t) summed over the points
+    (PoseSolver::computeOmega): an independent least-squares solve from the
+    generating pose lands on the same pose."""
+    from scipy.optimize import least_squares
+    from scipy.spatial.transform import Rotation as Rot
+    X, q, R, t = _sqpnp_case(500, 6e-4, 2)  # ~0.4 px at KITTI's focal length
+    rc, Rs, ts = O.sqpnp(X, q)
+    assert rc == 0
+
+    def res(p):
+        Y = X @ Rot.from_rotvec(p[:3]).as_matrix().T + p[3:]
+        return np.r_[Y[:, 0] - q[:, 0] * Y[:, 2], Y[:, 1] - q[:, 1] * Y[:, 2]]
+    p = least_squares(res, np.r_[Rot.from_matrix(R).as_rotvec(), t], xtol=1e-15, ftol=1e-15, gtol=1e-15).x
+    assert np.abs(Rot.from_rotvec(p[:3]).as_matrix() - Rs).max() < 1e-8
+    assert np.abs(p[3:] - ts).max() < 1e-8
+    assert np.abs(Rs @ Rs.T - np.eye(3)).max() < 1e-9          # a rotation
+    assert np.abs(Rs - R).max() > 1e-6                          # (and not the noise-free pose)
+
+
+def test_kat_sqpnp_degenerate_image_points():
+    """All image points at one spot: SQPnP's point-variance assert (rc -1)."""
+    X, q, _, _ = _sqpnp_case(50, 0.0, 3)
+    q[:] = q[0]
+    rc, _, _ = O.sqpnp(X, q)
+    assert rc == -1
