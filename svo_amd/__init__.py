@@ -24,8 +24,10 @@ raises ``SvoError`` if the extension or a GPU is missing.
 """
 from __future__ import annotations
 
+import atexit
 import ctypes as C
 import os
+import weakref
 
 import numpy as np
 
@@ -46,6 +48,24 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 def lib_path() -> str:
     # SVO_GPU_LIB: another build of the same library (A/B measurements)
     return os.environ.get("SVO_GPU_LIB") or os.path.join(_HERE, "lib", "libsvo_gpu.so")
+
+
+# Live handles, closed at interpreter exit in dependency order (front ends and
+# images before the contexts they were made on): left to __del__, a context can
+# go first and its dependants then free into a destroyed context.
+_LIVE = {"frontend": weakref.WeakSet(), "image": weakref.WeakSet(), "context": weakref.WeakSet()}
+
+
+def _close_all():
+    for kind in ("frontend", "image", "context"):
+        for obj in list(_LIVE[kind]):
+            try:
+                obj.close()
+            except Exception:
+                pass
+
+
+atexit.register(_close_all)
 
 
 class SvoError(RuntimeError):
@@ -183,6 +203,7 @@ class Image:
 
     def __init__(self, ctx: "Context", handle, w: int, h: int, max_levels: int):
         self.ctx, self.handle, self.w, self.h, self.max_levels = ctx, handle, w, h, max_levels
+        _LIVE["image"].add(self)
 
     def level(self, l: int) -> np.ndarray:
         L = lib()
@@ -258,6 +279,7 @@ class Context:
         if rc != 0:
             raise SvoError(f"svo_ctx_create(device={device}) failed: {rc} (no usable HIP device?)")
         self.handle = h
+        _LIVE["context"].add(self)
 
     def _check(self, rc):
         if rc < 0:
@@ -553,6 +575,7 @@ class Frontend:
         h = _vp()
         ctx._check(lib().svo_frontend_create(ctx.handle, C.byref(cfg), C.byref(h)))
         self.handle = h
+        _LIVE["frontend"].add(self)
 
     def set_frame(self, seq, t, left, right):
         """Stereo pair t of sequence seq: (h, w) grey, or (h, w, 3) BGR converted on the device."""

@@ -11,11 +11,12 @@
 //   scored in chunks; the accept rule is then replayed in iteration order, and
 //   iterations past the (shrinking) niters are discarded -- identical result
 //   to the serial loop.
-//   Final fit (solvePnP SQPNP on the inliers, calib3d/src/sqpnp.cpp): minimiser
-//   of SQPnP's cost r^T Omega r over SO(3) -- Omega as PoseSolver::computeOmega
-//   builds it (the algebraic image-space error [1 0 -x; 0 1 -y](R X + t) with t
-//   eliminated, t = P r) -- by multi-start Gauss-Newton instead of SQPnP's SQP
-//   iterations (same minimiser; the oracle restates the SQP solver: DESIGN.md).
+//   Final fit (solvePnP SQPNP on the inliers, calib3d/src/sqpnp.cpp): SQPnP's
+//   cost r^T Omega r -- Omega as PoseSolver::computeOmega builds it (the
+//   algebraic image-space error [1 0 -x; 0 1 -y](R X + t) with t eliminated,
+//   t = P r), from statistics summed on the GPU -- and its solution search over
+//   Omega's eigenvectors with the same SQP runs (15 steps at most: an unconverged
+//   run can win, as in OpenCV).
 #include <cfloat>
 #include <cstring>
 #include <vector>
@@ -131,47 +132,99 @@ double quad(const double* Om, const double* r) {
     return s;
 }
 
-double refine_so3(const double* Om, double* R) {
-    for (int it = 0; it < 100; it++) {
-        double J[27];  // d vec(exp([w]) R) / dw at 0: columns vec(G_k R)
-        for (int k = 0; k < 3; k++) {
-            double G[9] = {0};
-            if (k == 0) { G[5] = -1; G[7] = 1; }
-            if (k == 1) { G[2] = 1; G[6] = -1; }
-            if (k == 2) { G[1] = -1; G[3] = 1; }
-            for (int i = 0; i < 3; i++)
-                for (int j = 0; j < 3; j++) J[3 * (3 * i + j) + k] = G[3 * i] * R[j] + G[3 * i + 1] * R[3 + j] + G[3 * i + 2] * R[6 + j];
+
+// One SQP step of SQPnP (PoseSolver::solveSQPSystem) at r: the delta minimising
+// (r + delta)^T Om (r + delta) subject to the orthogonality constraints
+// linearised at r, J delta = -h(r) (h: the three row norms - 1 and the three row
+// dot products), from the KKT system [2 Om, J^T; J, 0] [delta; l] = [-2 Om r; -h]
+// solved by Gaussian elimination with partial pivoting (OpenCV solves the same
+// system through an orthonormal row / null-space split of J).
+void sqp_step(const double* Om, const double* r, double* delta) {
+    constexpr int N = 15;
+    double A[N][N + 1] = {{0}};
+    const double* r1 = r;
+    const double* r2 = r + 3;
+    const double* r3 = r + 6;
+    for (int i = 0; i < 9; i++) {
+        double g = 0;
+        for (int j = 0; j < 9; j++) {
+            A[i][j] = 2 * Om[9 * i + j];
+            g += Om[9 * i + j] * r[j];
         }
-        double g[3] = {0, 0, 0}, H[9] = {0};
-        for (int i = 0; i < 9; i++) {
-            double Or = 0, OJ[3] = {0, 0, 0};
-            for (int j = 0; j < 9; j++) {
-                Or += Om[9 * i + j] * R[j];
-                for (int k = 0; k < 3; k++) OJ[k] += Om[9 * i + j] * J[3 * j + k];
-            }
-            for (int a = 0; a < 3; a++) {
-                g[a] += J[3 * i + a] * Or;
-                for (int b = 0; b < 3; b++) H[3 * a + b] += J[3 * i + a] * OJ[b];
-            }
-        }
-        double Hi[9];
-        la::pinv3(H, Hi);
-        double w[3];
-        for (int a = 0; a < 3; a++) w[a] = -(Hi[3 * a] * g[0] + Hi[3 * a + 1] * g[1] + Hi[3 * a + 2] * g[2]);
-        double dR[9], Rn[9];
-        la::rodrigues(w, dR);
-        for (int i = 0; i < 3; i++)
-            for (int j = 0; j < 3; j++) Rn[3 * i + j] = dR[3 * i] * R[j] + dR[3 * i + 1] * R[3 + j] + dR[3 * i + 2] * R[6 + j];
-        if (quad(Om, Rn) > quad(Om, R)) break;
-        std::memcpy(R, Rn, sizeof(Rn));
-        if (w[0] * w[0] + w[1] * w[1] + w[2] * w[2] < 1e-24) break;
+        A[i][N] = -2 * g;
     }
-    return quad(Om, R);
+    double J[6][9] = {{0}};
+    for (int k = 0; k < 3; k++) {
+        J[0][k] = 2 * r1[k];
+        J[1][3 + k] = 2 * r2[k];
+        J[2][6 + k] = 2 * r3[k];
+        J[3][k] = r2[k];
+        J[3][3 + k] = r1[k];
+        J[4][3 + k] = r3[k];
+        J[4][6 + k] = r2[k];
+        J[5][k] = r3[k];
+        J[5][6 + k] = r1[k];
+    }
+    const double h[6] = {dot3(r1, r1) - 1, dot3(r2, r2) - 1, dot3(r3, r3) - 1, dot3(r1, r2), dot3(r2, r3),
+                         dot3(r1, r3)};
+    for (int c = 0; c < 6; c++) {
+        for (int j = 0; j < 9; j++) {
+            A[9 + c][j] = J[c][j];
+            A[j][9 + c] = J[c][j];
+        }
+        A[9 + c][N] = -h[c];
+    }
+    for (int col = 0; col < N; col++) {
+        int piv = col;
+        for (int i = col + 1; i < N; i++)
+            if (fabs(A[i][col]) > fabs(A[piv][col])) piv = i;
+        if (piv != col)
+            for (int j = 0; j <= N; j++) std::swap(A[col][j], A[piv][j]);
+        const double d = A[col][col];
+        if (d == 0) continue;
+        for (int i = col + 1; i < N; i++) {
+            const double f = A[i][col] / d;
+            if (f == 0) continue;
+            for (int j = col; j <= N; j++) A[i][j] -= f * A[col][j];
+        }
+    }
+    double x[N];
+    for (int i = N - 1; i >= 0; i--) {
+        double v = A[i][N];
+        for (int j = i + 1; j < N; j++) v -= A[i][j] * x[j];
+        x[i] = A[i][i] != 0 ? v / A[i][i] : 0.0;
+    }
+    std::memcpy(delta, x, sizeof(double) * 9);
 }
 
-// SQPnP's solution search (PoseSolver::solveInternal) over Omega's eigenvectors,
-// with the SQP runs done by Gauss-Newton on SO(3) (refine_so3: the same
-// constrained minimiser from the same start):
+// PoseSolver::runSQP: at most 15 steps while |delta|^2 > 1e-10; then -r if
+// det < 0, and the nearest rotation only if det > 1.001 (r as is otherwise --
+// its cost and t are taken unprojected, as OpenCV does).
+void sqp_run(const double* Om, const double* r0, double* rhat) {
+    double r[9], delta[9];
+    std::memcpy(r, r0, sizeof(r));
+    double dsq = DBL_MAX;
+    int step = 0;
+    while (dsq > 1e-10 && step++ < 15) {
+        sqp_step(Om, r, delta);
+        dsq = 0;
+        for (int k = 0; k < 9; k++) {
+            r[k] += delta[k];
+            dsq += delta[k] * delta[k];
+        }
+    }
+    double d = r[0] * (r[4] * r[8] - r[5] * r[7]) - r[1] * (r[3] * r[8] - r[5] * r[6]) + r[2] * (r[3] * r[7] - r[4] * r[6]);
+    if (d < 0) {
+        for (double& v : r) v = -v;
+        d = -d;
+    }
+    if (d > 1.001)
+        la::nearest_rotation(r, rhat);
+    else
+        std::memcpy(rhat, r, sizeof(r));
+}
+
+// SQPnP's solution search (PoseSolver::solveInternal) over Omega's eigenvectors:
 //   the null-space eigenvectors e (eigenvalues below the rank tolerance 1e-7; at
 //   least the smallest), sqrt(3)-scaled: if e is already orthogonal (squared
 //   orthogonality error < 1e-8) it is taken as is, det-signed, with t = P e (no
@@ -249,8 +302,9 @@ void fit_from_cost(const SqpnpCost& c, int n, PointAt pt, double R[9], double t[
             double m[9];
             SqSol s;
             for (int k = 0; k < 9; k++) m[k] = sg ? -e[k] : e[k];
-            la::nearest_rotation(m, s.r);
-            refine_so3(c.Om, s.r);
+            double r0[9];
+            la::nearest_rotation(m, r0);
+            sqp_run(c.Om, r0, s.r);
             check(s);
         }
     };
