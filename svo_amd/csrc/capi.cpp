@@ -515,7 +515,7 @@ int svo_pnp_residuals(svo_ctx* ctx, const float* obj_xyz, const float* img_xy, i
 
 int svo_epnp_subsets(svo_ctx* ctx, const float* subsets, int m, const double K[9], int device, double* Rt,
                      int* ok) {
-    if (!ctx || m < 0 || (m > 0 && (!subsets || !Rt || !ok)) || !K)
+    if ((!ctx && device) || m < 0 || (m > 0 && (!subsets || !Rt || !ok)) || !K)
         return set_error(ctx, SVO_ERR_ARG, "svo_epnp_subsets: bad arguments");
     if (m == 0) return SVO_OK;
     if (!device) {
