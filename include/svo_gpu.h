@@ -331,6 +331,14 @@ void svo_frontend_reset_times(svo_frontend* fe);
  * are triple-buffered): after svo_frontend_init(t0) frame t0, after
  * svo_frontend_step(t) frames t and t + 1. Synchronises the front end first. */
 int svo_frontend_scharr_level(svo_frontend* fe, int seq, int t, int level, int16_t* ix, int16_t* iy, int stride);
+/* Level `level` of frame t's left (right = 0) or right (right = 1) pyramid with
+ * its stored REFLECT_101 border: (h + 2 * SVO_PYR_PAD) rows of (w + 2 *
+ * SVO_PYR_PAD) bytes at `stride`, pixel (0, 0) of the level at row / column
+ * SVO_PYR_PAD (the LK kernels read the border instead of testing coordinates).
+ * Same frames as svo_frontend_scharr_level (right: the frame of the last step or
+ * init). Synchronises the front end first. */
+#define SVO_PYR_PAD 32
+int svo_frontend_pyramid_level(svo_frontend* fe, int seq, int t, int right, int level, uint8_t* out, int stride);
 /* The pyramid + Scharr launch chain of frame t (every sequence) timed alone on the
  * context stream: reps rebuilds (identical contents) after one warm-up, HIP
  * events around them; ms per chain. Synchronises the front end first. */

@@ -40,6 +40,7 @@ __all__ = [
 TERM_COUNT = 1
 TERM_EPS = 2
 LK_USE_INITIAL_FLOW = 4
+PYR_PAD = 32  # SVO_PYR_PAD: stored border of every pyramid level
 LK_GET_MIN_EIGENVALS = 8
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
@@ -122,6 +123,7 @@ _SIGS = [
     ("svo_frontend_set_frame_bgr", C.c_int, [_vp, C.c_int, C.c_int, _u8p, _u8p, C.c_int]),
     ("svo_frontend_map_points", C.c_int, [_vp, C.c_int, _f64p, C.c_int, _i32p]),
     ("svo_frontend_time_pyramid", C.c_int, [_vp, C.c_int, C.c_int, _f64p]),
+    ("svo_frontend_pyramid_level", C.c_int, [_vp, C.c_int, C.c_int, C.c_int, C.c_int, C.POINTER(C.c_uint8), C.c_int]),
     ("svo_frontend_scharr_level", C.c_int, [_vp, C.c_int, C.c_int, C.c_int, C.POINTER(C.c_int16),
                                             C.POINTER(C.c_int16), C.c_int]),
     ("svo_frontend_prebuild_pyramids", C.c_int, [_vp]),
@@ -648,6 +650,14 @@ class Frontend:
                                                         ix.ctypes.data_as(C.POINTER(C.c_int16)),
                                                         iy.ctypes.data_as(C.POINTER(C.c_int16)), w))
         return ix, iy
+
+    def pyramid_level(self, seq, t, level, w, h, right=False):
+        """Level `level` (w x h) of frame t's left / right pyramid with its stored
+        REFLECT_101 border of PYR_PAD pixels (svo_frontend_pyramid_level)."""
+        out = np.empty((h + 2 * PYR_PAD, w + 2 * PYR_PAD), np.uint8)
+        self.ctx._check(lib().svo_frontend_pyramid_level(self.handle, int(seq), int(t), int(bool(right)), int(level),
+                                                         out.ctypes.data_as(C.POINTER(C.c_uint8)), out.shape[1]))
+        return out
 
     def host_cpus(self):
         """CPUs the host pool is pinned to (svo_host_cpu_plan's share of this rank)."""

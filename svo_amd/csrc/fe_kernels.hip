@@ -4,6 +4,8 @@
 // DLT triangulation, new map points). One launch covers every sequence of the
 // batch (blockIdx = sequence), so a frame step costs the same number of
 // launches for 1 or 512 sequences.
+#include <cstdlib>
+
 #include "dlt.hpp"
 #include "frontend.hpp"
 
@@ -322,13 +324,27 @@ hipError_t launch_tail(const TailBatch& tb, int nseq, hipStream_t st) {
     return hipGetLastError();
 }
 
+static int append_block() {
+    static const int b = [] {
+        const char* e = std::getenv("SVO_FE_APPEND_BLOCK");
+        return e && std::atoi(e) == 256 ? 256 : kAppendBlock;
+    }();
+    return b;
+}
+
 hipError_t launch_append(const AppendBatch& b, int nseq, hipStream_t st) {
-    hipLaunchKernelGGL(append_kernel<kAppendBlock>, dim3(nseq), dim3(kAppendBlock), 0, st, b);
+    if (append_block() == 256)
+        hipLaunchKernelGGL(append_kernel<256>, dim3(nseq), dim3(256), 0, st, b);
+    else
+        hipLaunchKernelGGL(append_kernel<kAppendBlock>, dim3(nseq), dim3(kAppendBlock), 0, st, b);
     return hipGetLastError();
 }
 
 hipError_t launch_keyframe_fused(const TailBatch& tb, const AppendBatch& ab, int nseq, hipStream_t st) {
-    hipLaunchKernelGGL(keyframe_fused_kernel<kAppendBlock>, dim3(nseq), dim3(kAppendBlock), 0, st, tb, ab);
+    if (append_block() == 256)
+        hipLaunchKernelGGL(keyframe_fused_kernel<256>, dim3(nseq), dim3(256), 0, st, tb, ab);
+    else
+        hipLaunchKernelGGL(keyframe_fused_kernel<kAppendBlock>, dim3(nseq), dim3(kAppendBlock), 0, st, tb, ab);
     return hipGetLastError();
 }
 

@@ -301,6 +301,14 @@ struct svo_frontend {
     int* spec_n;          // speculative stereo candidates per sequence (StereoPrepBatch)
     int spec_margin = 32;  // RANSAC drops covered by the speculative stereo LK (SVO_FE_SPEC_MARGIN, < 0: off)
     int min_tracked = 0;   // min over sequences of the last step's tracked count (stereo LK grid hint)
+    // early speculation (SVO_FE_SPEC_EARLY=1, the default; SVO_KF_EVERY only): the
+    // speculative stereo LK of step t goes out in its first half, behind FAST(t),
+    // sized from the features before LK (nA) with margin spec_margin + lk_loss
+    int spec_early = 1;
+    int spec_t = -1;       // step whose speculation went out early
+    int spec_m = 0;        // its margin (features lost to LK + RANSAC it covers)
+    bool spec_was_early = false;
+    int lk_loss = 0;       // max over sequences of the last step's LK losses
     unsigned long long* fbits;
     uint8_t* status;
     double* map;
@@ -579,20 +587,26 @@ int fe_keyframe(svo_frontend* fe, int t, const int* n_in, const uint32_t* bits, 
     return SVO_OK;
 }
 
-// The speculative stereo LK of step t (StereoPrepBatch), on the FAST stream
-// (behind FAST: the candidates) after the step's post-LK (the tracked counts),
-// queued with the post-LK so that no host round trip precedes it: it runs beside
-// the host's RANSAC. The keyframe takes the first target - kept candidates and
-// kept <= n_tracked, so the first target - n_tracked + margin cover the take
-// whenever RANSAC drops at most `margin` points. ev_fast is re-recorded behind it,
-// so the keyframe's wait for FAST covers it too.
-int fe_queue_spec(svo_frontend* fe, int t) {
+// The speculative stereo LK of step t (StereoPrepBatch) on the FAST stream,
+// behind FAST (the candidates). The keyframe takes the first target - kept
+// candidates, kept <= n_ref, so the first target - n_ref + margin cover the take
+// whenever n_ref - kept <= margin. Two forms:
+//  - early (fe_front, behind FAST(t)): n_ref = the features before LK (nA, final
+//    once the FAST stream has waited for the last keyframe), margin = spec_margin
+//    + the last step's largest LK loss; it runs beside LK(t), so the keyframe
+//    never waits for it (SVO_KF_EVERY only: the targets of a later step are not
+//    known while its first half is queued);
+//  - late (fe_post, behind the post-LK): n_ref = the tracked counts (nB), margin
+//    = spec_margin; it runs beside the host's RANSAC.
+// ev_fast is re-recorded behind it, so the keyframe's wait for FAST covers it too.
+int fe_queue_spec(svo_frontend* fe, int t, bool early) {
     svo_ctx* ctx = fe->ctx;
     const svo_frontend_config& c = fe->cfg;
     hipStream_t sf = fe->st_fast;
     const bool bucketed = c.bucket_size > 0;
+    const int margin = early ? fe->spec_margin + fe->lk_loss : fe->spec_margin;
     StereoPrepBatch pb;
-    pb.n_tracked = fe->nB;
+    pb.n_tracked = early ? fe->nA : fe->nB;
     pb.cand = bucketed ? fe->cand : fe->kps;
     pb.cand_elem = bucketed ? 2 : 3;
     pb.cand_cap = bucketed ? fe->BCAP : fe->KCAP;
@@ -601,18 +615,21 @@ int fe_queue_spec(svo_frontend* fe, int t) {
     pb.map_cap = fe->MAPCAP;
     pb.cap = fe->CAP;
     pb.n_target = fe->h_target;
-    pb.margin = fe->spec_margin;
+    pb.margin = margin;
     pb.st_xy = fe->st_xy;
     pb.spec_n = fe->spec_n;
-    SVO_HIP(ctx, hipStreamWaitEvent(sf, fe->ev_post, 0));
+    if (!early) SVO_HIP(ctx, hipStreamWaitEvent(sf, fe->ev_post, 0));
     SVO_HIP(ctx, launch_stereo_prep(pb, fe->S, sf));
     // grid for the speculation the last step's smallest tracked count implies
     // (+ slack); the kernel's waves loop over any candidates beyond it
-    const int max_spec = std::min(c.n_features + fe->spec_margin, fe->CAP);
-    const int hint = std::min(fe->CAP, c.n_features - fe->min_tracked + fe->spec_margin + 32);
+    const int max_spec = std::min(c.n_features + margin, fe->CAP);
+    const int hint = std::min(fe->CAP, c.n_features - fe->min_tracked + margin + 32);
     int rc = fe_stereo_lk(fe, t, fe->spec_n, max_spec, sf, hint);
     if (rc) return rc;
     SVO_HIP(ctx, hipEventRecord(fe->ev_fast, sf));
+    fe->spec_t = t;
+    fe->spec_m = margin;
+    fe->spec_was_early = early;
     return SVO_OK;
 }
 
@@ -897,6 +914,8 @@ int svo_frontend_create(svo_ctx* ctx, const svo_frontend_config* cfg, svo_fronte
         fe->fast_pre = fp && fp[0] == '0' ? 0 : 1;
         const char* sm = std::getenv("SVO_FE_SPEC_MARGIN");
         fe->spec_margin = sm ? std::atoi(sm) : 32;
+        const char* se = std::getenv("SVO_FE_SPEC_EARLY");
+        fe->spec_early = se && se[0] == '0' ? 0 : 1;
     }
     // (on the context stream: a first use of the null stream would take a fifth
     // hardware queue and serialise the step's streams)
@@ -986,6 +1005,7 @@ static int fe_drain(svo_frontend* fe) {
     svo_ctx* ctx = fe->ctx;
     for (hipStream_t st : {fe->st_lk, fe->st_fast, fe->st_copy, ctx->stream}) SVO_HIP(ctx, hipStreamSynchronize(st));
     fe->front_t = -1;
+    fe->spec_t = -1;
     return SVO_OK;
 }
 
@@ -1112,8 +1132,8 @@ static int fe_post(svo_frontend* fe, int t) {
     ph_end(fe, sl, slot);
     SVO_HIP(ctx, hipEventRecord(fe->ev_post, sl));
     TP("post_lk launched");
-    if (fe->spec_margin >= 0) {
-        int rq = fe_queue_spec(fe, t);
+    if (fe->spec_margin >= 0 && fe->spec_t != t) {
+        int rq = fe_queue_spec(fe, t, false);
         if (rq) return rq;
     }
     TP("spec stereo launched");
@@ -1202,6 +1222,13 @@ static int fe_front(svo_frontend* fe, int t) {
     SVO_HIP(ctx, launch_pyramid_batched(fe->d_desc_r + (size_t)(t % fe->T) * S, S, fe->W, fe->H, fe->nlev, st0));
     ph_end(fe, st0, slot);
     SVO_HIP(ctx, hipEventRecord(fe->ev_pyr_r, st0));
+    // 4b. early speculative stereo LK of frame t (fe_queue_spec), behind FAST(t)
+    //     and this right pyramid
+    if (fe->spec_early && fe->spec_margin >= 0 && fe->cfg.keyframe_rule == SVO_KF_EVERY) {
+        for (int s = 0; s < S; s++) fe->h_target[s] = fe->cfg.n_features;
+        int rc = fe_queue_spec(fe, t, true);
+        if (rc) return rc;
+    }
     // 5. frame t+1's pyramid + Scharr + borders, queued beside this LK: the
     //    derivative pyramids are triple-buffered (frame f in f % 3), so nothing
     //    this step reads is overwritten, and the memory-bound pyramid shares the
@@ -1299,7 +1326,11 @@ int svo_frontend_step(svo_frontend* fe, int t, svo_frontend_stats* stats) {
     SVO_HIP(ctx, hipEventSynchronize(fe->ev_post));
     TP("lk results on host");
     ms_wait += ms_since(tw);
-    const bool spec = fe->spec_margin >= 0;  // the stereo LK went out with the post-LK (fe_post)
+    // the speculative stereo LK went out early (fe_front) or with the post-LK (fe_post)
+    const bool spec = fe->spec_margin >= 0 && fe->spec_t == t;
+    const bool spec_early = spec && fe->spec_was_early;
+    fe->spec_t = -1;
+    int lk_loss = 0;
     bool need_full = false;
     for (int s = 0; s < S; s++) {
         RansacSeq& r = fe->rs[s];
@@ -1393,7 +1424,10 @@ int svo_frontend_step(svo_frontend* fe, int t, svo_frontend_stats* stats) {
         const int kept = r.ok ? r.maxGood : (r.n < 4 ? r.n : 0);
         max_take = std::max(max_take, fe->h_target[s] - kept);
         // (a sequence without a keyframe takes nothing: nothing to cover)
-        spec_ok &= fe->h_target[s] == 0 || fe->h_nB[s] - kept <= fe->spec_margin;
+        // (early: h_nA still holds the count before LK; the keyframe rewrites it)
+        const int n_ref = spec_early ? fe->h_nA[s] : fe->h_nB[s];
+        spec_ok &= fe->h_target[s] == 0 || n_ref - kept <= fe->spec_m;
+        lk_loss = std::max(lk_loss, fe->h_nA[s] - fe->h_nB[s]);
         uint32_t* b = fe->h_best + (size_t)s * fe->WORDS;
         std::memset(b, 0, sizeof(uint32_t) * fe->WORDS);
         if (r.ok) {
@@ -1410,6 +1444,7 @@ int svo_frontend_step(svo_frontend* fe, int t, svo_frontend_stats* stats) {
                                                                        c.pnp_iterations))
                                 : 0;
     }
+    fe->lk_loss = lk_loss;
     ms_fit += ms_since(tf);
     TP("selected");
     // the SQPnP statistics only feed the pose fits, which run during the next
@@ -1560,6 +1595,20 @@ int svo_frontend_scharr_level(svo_frontend* fe, int seq, int t, int level, int16
     DerivDesc dd;
     SVO_HIP(ctx, hipMemcpy(&dd, fe->d_der + (size_t)(t % 3) * fe->S + seq, sizeof(dd), hipMemcpyDeviceToHost));
     return download_deriv_level(ctx, dd, level, L.w, L.h, ix, iy, stride);
+}
+
+int svo_frontend_pyramid_level(svo_frontend* fe, int seq, int t, int right, int level, uint8_t* out, int stride) {
+    static_assert(SVO_PYR_PAD == kPyrPad, "header border width");
+    if (!fe || seq < 0 || seq >= fe->S || t < 0 || level < 0 || level >= fe->nlev || !out) return SVO_ERR_ARG;
+    int rc = svo_frontend_synchronize(fe);
+    if (rc) return rc;
+    svo_ctx* ctx = fe->ctx;
+    const ImgLevel& L = (right ? fe->desc_r_host : fe->desc_host)[(size_t)(t % fe->T) * fe->S + seq].lv[level];
+    const int bw = L.w + 2 * kPyrPad;
+    if (stride < bw) return set_error(ctx, SVO_ERR_ARG, "svo_frontend_pyramid_level: stride");
+    SVO_HIP(ctx, hipMemcpy2D(out, stride, L.data - (ptrdiff_t)kPyrPad * L.pitch - kPyrPad, L.pitch, bw,
+                             L.h + 2 * kPyrPad, hipMemcpyDeviceToHost));
+    return SVO_OK;
 }
 
 int svo_frontend_time_pyramid(svo_frontend* fe, int t, int reps, double* ms_per_launch) {

@@ -8,7 +8,9 @@
 // Unlike the reference, which rebuilds both pyramids on every LK call, a frame's
 // pyramid is built once, kept in HBM and shared by the temporal and stereo LK
 // calls. HBM roofline: reads w*h, writes w*h/4 bytes per level.
+#include <algorithm>
 #include <cstdlib>
+#include <utility>
 
 #include "common.hpp"
 
@@ -23,14 +25,104 @@ __device__ __forceinline__ int refl101(int p, int len) {
     return p;
 }
 
+// The REFLECT_101 border (kPyrPad pixels each side) of one level, written by the
+// block that owns the border pixels' sources: every border pixel (px, py) is a
+// copy of pixel (refl(px), refl(py)) of the level, and the blocks of a launch
+// partition the level's pixels into owned rectangles [ox0, ox1) x [oy0, oy1), so
+// each border pixel has exactly one writer, which already holds its value
+// (val(sx, sy): a staged copy). Only blocks owning pixels within kPyrPad + 1 of
+// an edge do any work.
+//
+// Border coordinates of one axis whose sources lie in [o0, o1): for a level
+// longer than the border (one reflection) two runs, p = -s for s in [lo, lo + nlo)
+// and p = 2 len - 2 - s for s in [hi, hi + nhi); a shorter level reflects
+// several times and every one of the 2 kPyrPad border coordinates is tested.
+struct BorderSpan {
+    int lo, nlo, hi, nhi;
+    bool many;
+    __device__ int count() const { return many ? 2 * kPyrPad : nlo + nhi; }
+    // k-th border coordinate (p) and its source (s); false: not sourced here (many)
+    __device__ bool at(int k, int len, int o0, int o1, int& p, int& s) const {
+        if (many) {
+            p = k < kPyrPad ? k - kPyrPad : len + (k - kPyrPad);
+            s = refl101(p, len);
+            return s >= o0 && s < o1;
+        }
+        if (k < nlo) {
+            s = lo + k;
+            p = -s;
+        } else {
+            s = hi + (k - nlo);
+            p = 2 * len - 2 - s;
+        }
+        return true;
+    }
+};
+__device__ __forceinline__ BorderSpan border_span(int len, int o0, int o1) {
+    BorderSpan b;
+    b.many = len <= kPyrPad;
+    b.lo = max(o0, 1);
+    b.nlo = max(0, min(o1, kPyrPad + 1) - b.lo);
+    b.hi = max(o0, len - 1 - kPyrPad);
+    b.nhi = max(0, min(o1, len - 1) - b.hi);
+    return b;
+}
+
+// rowp(sy): the staged copy of pixel (ox0, sy), 4-byte aligned (the top / bottom
+// band rows go out as dwords), or nullptr (bytes through val). The side bands go
+// out byte by byte: a dword form (aligned groups, four reflected sources each)
+// measured slower (KITTI level 0: 48.7 vs 46.7 us).
+template <class F, class G>
+__device__ __forceinline__ void pad_owned(uint8_t* __restrict__ d, int w, int h, int pitch, int ox0, int ox1, int oy0,
+                                          int oy1, F val, G rowp) {
+    const int tid = threadIdx.x, nt = blockDim.x;
+    const BorderSpan bx = border_span(w, ox0, ox1), by = border_span(h, oy0, oy1);
+    const int ncx = bx.count(), ncy = by.count();
+    // left / right bands of the owned rows
+    if (ncx > 0) {
+        const int n = (oy1 - oy0) * ncx;
+        for (int k = tid; k < n; k += nt) {
+            const int r = k / ncx, j = k - r * ncx;
+            int px, sx;
+            if (bx.at(j, w, ox0, ox1, px, sx)) d[(ptrdiff_t)(oy0 + r) * pitch + px] = val(sx, oy0 + r);
+        }
+    }
+    if (ncy == 0) return;
+    // top / bottom rows whose source rows are owned: the owned columns ...
+    const int ow = ox1 - ox0, nq = (ow + 3) >> 2;
+    for (int k = tid; k < ncy * nq; k += nt) {
+        const int r = k / nq, q = k - r * nq;
+        int py, sy;
+        if (!by.at(r, h, oy0, oy1, py, sy)) continue;
+        uint8_t* drow = d + (ptrdiff_t)py * pitch + ox0 + 4 * q;
+        const uint8_t* srow = rowp(sy);
+        if (srow && 4 * q + 4 <= ow) {
+            *reinterpret_cast<uint32_t*>(drow) = *reinterpret_cast<const uint32_t*>(srow + 4 * q);
+        } else {
+            for (int m = 0; m < 4 && 4 * q + m < ow; m++) drow[m] = val(ox0 + 4 * q + m, sy);
+        }
+    }
+    // ... and the border columns sourced here (corners)
+    if (ncx > 0) {
+        for (int k = tid; k < ncy * ncx; k += nt) {
+            const int r = k / ncx, j = k - r * ncx;
+            int py, sy, px, sx;
+            if (!by.at(r, h, oy0, oy1, py, sy) || !bx.at(j, w, ox0, ox1, px, sx)) continue;
+            d[(ptrdiff_t)py * pitch + px] = val(sx, sy);
+        }
+    }
+}
+
 constexpr int PD_TX = 64;   // output tile width
 constexpr int PD_TY = 16;   // output tile height
 constexpr int PD_IW = 2 * PD_TX + 4;  // 132 input columns
 constexpr int PD_IH = 2 * PD_TY + 4;  // 36 input rows
 
+// pad_src: also write the source level's border pixels whose sources this block
+// owns (the level-l pixels [2x0, 2x0 + 128) x [2y0, 2y0 + 32) under its tile)
 __device__ __forceinline__ void pyr_down_tile(const uint8_t* __restrict__ src, int sw, int sh,
                                               int sp, uint8_t* __restrict__ dst, int dw, int dh,
-                                              int dp) {
+                                              int dp, bool pad_src = false) {
     __shared__ uint8_t T[PD_IH][PD_IW + 4];
     __shared__ int H[PD_IH][PD_TX + 1];
     const int x0 = blockIdx.x * PD_TX, y0 = blockIdx.y * PD_TY;
@@ -55,6 +147,11 @@ __device__ __forceinline__ void pyr_down_tile(const uint8_t* __restrict__ src, i
         H[r][c] = t[0] + 4 * t[1] + 6 * t[2] + 4 * t[3] + t[4];
     }
     __syncthreads();
+    // (after the last barrier: no wait for these stores)
+    if (pad_src)
+        pad_owned(const_cast<uint8_t*>(src), sw, sh, sp, 2 * x0, min(2 * x0 + 2 * PD_TX, sw), 2 * y0,
+                  min(2 * y0 + 2 * PD_TY, sh), [&](int x, int y) { return T[y - sy0][x - sx0]; },
+                  [](int) { return (const uint8_t*)nullptr; });  // (T's column 2x0 is not dword-aligned)
     const int c = tid & 63;
     const int x = x0 + c;
     if (x >= dw) return;
@@ -76,15 +173,16 @@ __global__ __launch_bounds__(256) void pyr_down_kernel(const uint8_t* __restrict
     pyr_down_tile(src, sw, sh, sp, dst, dw, dh, dp);
 }
 
-// Batched form: blockIdx.z = sequence, level l of descs[z] from level l-1.
+// Batched form: blockIdx.z = sequence, level l of descs[z] from level l-1
+// (pad_src: and level l-1's border, pad_owned).
 __global__ __launch_bounds__(256) void pyr_down_batched_kernel(const PyrDesc* __restrict__ descs,
-                                                               int level) {
+                                                               int level, int pad_src) {
     const PyrDesc& P = descs[blockIdx.z];
     const ImgLevel& s = P.lv[level - 1];
     const ImgLevel& d = P.lv[level];
     if ((int)blockIdx.x * PD_TX >= d.w || (int)blockIdx.y * PD_TY >= d.h) return;
     // same body as pyr_down_kernel (inlined call keeps one copy of the math)
-    pyr_down_tile(s.data, s.w, s.h, s.pitch, const_cast<uint8_t*>(d.data), d.w, d.h, d.pitch);
+    pyr_down_tile(s.data, s.w, s.h, s.pitch, const_cast<uint8_t*>(d.data), d.w, d.h, d.pitch, pad_src != 0);
 }
 
 // REFLECT_101 border (kPyrPad pixels each side) of one level, written from the
@@ -138,14 +236,14 @@ hipError_t launch_pyramid_pad(const PyrDesc* d_descs, int nseq, int w, int h, in
     return hipGetLastError();
 }
 
-hipError_t launch_pyramid_batched(const PyrDesc* d_descs, int nseq, int w, int h, int nlevels,
-                                  hipStream_t st) {
+// one launch per level + the border pass (nlevels beyond the fused chain's LDS)
+static hipError_t pyramid_levels(const PyrDesc* d_descs, int nseq, int w, int h, int nlevels, hipStream_t st) {
     int lw = w, lh = h;
     for (int l = 1; l < nlevels; l++) {
         lw = (lw + 1) / 2;
         lh = (lh + 1) / 2;
         dim3 grid((lw + PD_TX - 1) / PD_TX, (lh + PD_TY - 1) / PD_TY, nseq);
-        hipLaunchKernelGGL(pyr_down_batched_kernel, grid, dim3(256), 0, st, d_descs, l);
+        hipLaunchKernelGGL(pyr_down_batched_kernel, grid, dim3(256), 0, st, d_descs, l, 0);
     }
     return launch_pyramid_pad(d_descs, nseq, w, h, nlevels, st);
 }
@@ -182,7 +280,7 @@ constexpr int FS_IH = PD_IH;          // 36 rows
 // NT: the derivative and level stores as non-temporal (streaming) stores
 template <bool NT>
 __global__ __launch_bounds__(256) void pyr_scharr_kernel(const PyrDesc* __restrict__ descs,
-                                                         const DerivDesc* __restrict__ ders, int level) {
+                                                         const DerivDesc* __restrict__ ders, int level, int pad_src) {
     const PyrDesc& P = descs[blockIdx.z];
     const ImgLevel& s = P.lv[level];
     const ImgLevel& d = P.lv[level + 1];
@@ -276,6 +374,12 @@ __global__ __launch_bounds__(256) void pyr_scharr_kernel(const PyrDesc* __restri
         }
     }
     __syncthreads();
+    // level l's border pixels whose sources lie under this tile (after the last
+    // barrier: no wait for these stores)
+    if (pad_src)
+        pad_owned(const_cast<uint8_t*>(s.data), sw, sh, s.pitch, 2 * x0, min(2 * x0 + 2 * PD_TX, sw), 2 * y0,
+                  min(2 * y0 + 2 * PD_TY, sh), [&](int x, int y) { return T[y - sy0][x - xa]; },
+                  [&](int y) { return (const uint8_t*)&T[y - sy0][2 * x0 - xa]; });
     // ---- pyrDown columns: 4 output rows per thread from 11 sliding H rows ----
     const int c = tid & 63;
     const int x = x0 + c;
@@ -297,8 +401,8 @@ __global__ __launch_bounds__(256) void pyr_scharr_kernel(const PyrDesc* __restri
 
 }  // namespace
 
-hipError_t launch_pyramid_scharr_batched(const PyrDesc* d_descs, const DerivDesc* d_ders, int nseq, int w, int h,
-                                         int nlevels, hipStream_t st) {
+static hipError_t pyramid_scharr_levels(const PyrDesc* d_descs, const DerivDesc* d_ders, int nseq, int w, int h,
+                                        int nlevels, hipStream_t st) {
     int lw = w, lh = h;
     for (int l = 0; l + 1 < nlevels; l++) {
         const int nw = (lw + 1) / 2, nh = (lh + 1) / 2;
@@ -310,9 +414,9 @@ hipError_t launch_pyramid_scharr_batched(const PyrDesc* d_descs, const DerivDesc
             return !(e && e[0] == '0');
         }();
         if (nt)
-            hipLaunchKernelGGL(pyr_scharr_kernel<true>, grid, dim3(256), 0, st, d_descs, d_ders, l);
+            hipLaunchKernelGGL(pyr_scharr_kernel<true>, grid, dim3(256), 0, st, d_descs, d_ders, l, 0);
         else
-            hipLaunchKernelGGL(pyr_scharr_kernel<false>, grid, dim3(256), 0, st, d_descs, d_ders, l);
+            hipLaunchKernelGGL(pyr_scharr_kernel<false>, grid, dim3(256), 0, st, d_descs, d_ders, l, 0);
         lw = nw;
         lh = nh;
     }
@@ -320,6 +424,333 @@ hipError_t launch_pyramid_scharr_batched(const PyrDesc* d_descs, const DerivDesc
     hipError_t e = launch_scharr_level(d_descs, d_ders, nseq, lw, lh, nlevels - 1, st);
     if (e != hipSuccess) return e;
     return launch_pyramid_pad(d_descs, nseq, w, h, nlevels, st);
+}
+
+// ---------------------------------------------------------------------------
+// Fused chain: levels 2 .. c of a pyramid (c = nlevels - 1) from level 1, the
+// Scharr derivatives of levels 1 .. c (SCHARR) and the borders of levels 1 .. c,
+// in ONE launch (one block per tile of the coarsest level, per sequence). The
+// per-level launches it replaces were latency-bound from level 1 on (level 1->2
+// 17 us, 2->3 13, Scharr of 3 5, borders 14 for 64 KITTI frames,
+// profiles/r02_pyramid_chain.txt) and each one queued behind whatever ran beside
+// it. A block owns the rectangle under its level-c tile at every level (level l:
+// the tile scaled by 2^(c-l), clipped to the level) and computes, in LDS, the
+// region R_l = owned +- halo_l of every level: halo_c = 1 (the 3x3 Scharr; 0
+// without it), halo_l = 2 halo_(l+1) + 2 (the 5-tap pyrDown of R_(l+1)), level 1
+// staged from HBM. Entries of R_l outside the level hold the REFLECT_101 pixel
+// (the border rule of both pyrDown and Scharr), so every tap is a plain LDS read.
+// Each block writes its owned pixels, their derivatives and the border pixels
+// whose sources it owns (pad_owned): no two blocks write the same byte, and no
+// block reads another's output. Bit-exact integer arithmetic as the per-level
+// kernels (same taps, same rounding).
+// Compile-time shape of the chain of levels S .. C (level S staged from HBM): the
+// level-C tile TW x TH (its level-S footprint is 128 x 32), per level l the
+// owned tile OW x OH, the halos (y: hy_C = 1 for the 3x3 Scharr, hy_l = 2 hy_(l+1)
+// + 2 for the 5-tap pyrDown; x: the same rounded up to 4 so that every region
+// row keeps the owned columns dword-aligned), region RW x RH at pitch PW, LDS
+// offsets (all levels stay resident: the store phase reads them all).
+template <int C, bool SCHARR, int S>
+struct ChainShape {
+    static constexpr int TW = 128 >> (C - S), TH = 32 >> (C - S);
+    static constexpr int hy(int l) { return l >= C ? (SCHARR ? 1 : 0) : 2 * hy(l + 1) + 2; }
+    static constexpr int hx(int l) { return l >= C ? (SCHARR ? 4 : 0) : (2 * hx(l + 1) + 2 + 3) & ~3; }
+    static constexpr int OW(int l) { return TW << (C - l); }
+    static constexpr int OH(int l) { return TH << (C - l); }
+    static constexpr int RW(int l) { return OW(l) + 2 * hx(l); }
+    static constexpr int RH(int l) { return OH(l) + 2 * hy(l); }
+    static constexpr int PW(int l) { return (RW(l) + 15) & ~15; }
+    static constexpr int off(int l) { return l <= S ? 0 : off(l - 1) + PW(l - 1) * RH(l - 1); }
+    static constexpr int hrows(int l) { return 2 * RH(l) + 3; }  // rows pass of level l
+    static constexpr int hbytes() {
+        int b = 0;
+        for (int l = S + 1; l <= C; l++) b = b > hrows(l) * RW(l) * 2 ? b : hrows(l) * RW(l) * 2;
+        return b;
+    }
+    static constexpr int off_h() { return (off(C + 1) + 15) & ~15; }
+    static constexpr int lds() { return off_h() + hbytes(); }
+};
+
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ u16x2 as_u16x2(uint32_t v) { return __builtin_bit_cast(u16x2, v); }
+__device__ __forceinline__ uint32_t as_u32(u16x2 v) { return __builtin_bit_cast(uint32_t, v); }
+// bytes X (low half) and Y (high half) of the 8 bytes {lo, hi} as a u16 pair
+__device__ __forceinline__ u16x2 byte_pair(uint32_t hi, uint32_t lo, int X, int Y) {
+    return as_u16x2(__builtin_amdgcn_perm(hi, lo, 0x0C000C00u | ((unsigned)Y << 16) | (unsigned)X));
+}
+
+// Level l of the chain's phase 1 (LDS only): level 1 staged from HBM (rows
+// reflected by index, columns dword-wise where the dword lies inside the level,
+// byte-wise reflected otherwise); level l >= 2 by pyrDown of level l-1's region,
+// then its entries outside the level set to the reflected pixel.
+template <int C, bool SCHARR, int S, int l>
+__device__ __forceinline__ void chain_build(const PyrDesc& P, uint8_t* lds, uint16_t* H) {
+    using Sh = ChainShape<C, SCHARR, S>;
+    constexpr int RW = Sh::RW(l), RH = Sh::RH(l), PW = Sh::PW(l);
+    const int tid = threadIdx.x;
+    const ImgLevel& L = P.lv[l];
+    const int w = L.w, h = L.h;
+    const int gx = (int)blockIdx.x * Sh::OW(l) - Sh::hx(l), gy = (int)blockIdx.y * Sh::OH(l) - Sh::hy(l);
+    uint8_t* __restrict__ R = lds + Sh::off(l);
+    if constexpr (l == S) {
+        constexpr int DW = RW / 4;
+        for (int k = tid; k < RH * DW; k += 256) {
+            const int r = k / DW, q = k - r * DW;
+            const uint8_t* src = L.data + (size_t)refl101(gy + r, h) * L.pitch;
+            const int x = gx + 4 * q;
+            uint32_t v;
+            if (x >= 0 && x + 4 <= w) {
+                v = *reinterpret_cast<const uint32_t*>(src + x);
+            } else {
+                v = 0;
+#pragma unroll
+                for (int m = 0; m < 4; m++) v |= (uint32_t)src[refl101(x + m, w)] << (8 * m);
+            }
+            *reinterpret_cast<uint32_t*>(R + r * PW + 4 * q) = v;
+        }
+        __syncthreads();
+    } else {
+        constexpr int PWp = Sh::PW(l - 1);
+        const uint8_t* __restrict__ pR = lds + Sh::off(l - 1);
+        constexpr int NQ = RW / 4, NR = Sh::hrows(l);
+        // rows pass: H[r][j] = 1 4 6 4 1 over region row r of level l-1, columns
+        // 2j + 2 .. 2j + 6 (where the halos put level-l column j's taps); 4 outputs
+        // per task from 16 region bytes, as two packed u16 pairs
+        for (int k = tid; k < NR * NQ; k += 256) {
+            const int r = k / NQ, q = k - r * NQ;
+            const uint4 v = *reinterpret_cast<const uint4*>(pR + r * PWp + 8 * q);
+            // outputs 0 / 1 read bytes 2+t / 4+t, outputs 2 / 3 bytes 6+t / 8+t (tap t)
+            const u16x2 a0 = byte_pair(v.y, v.x, 2, 4), a1 = byte_pair(v.y, v.x, 3, 5),
+                        a2 = byte_pair(v.y, v.x, 4, 6), a3 = byte_pair(v.y, v.x, 5, 7),
+                        a4 = byte_pair(v.z, v.y, 2, 4);
+            const u16x2 b0 = byte_pair(v.z, v.y, 2, 4), b1 = byte_pair(v.z, v.y, 3, 5),
+                        b2 = byte_pair(v.z, v.y, 4, 6), b3 = byte_pair(v.z, v.y, 5, 7),
+                        b4 = byte_pair(v.w, v.z, 2, 4);
+            const u16x2 ha = (a0 + a4) + (u16x2)4 * (a1 + a3) + (u16x2)6 * a2;
+            const u16x2 hb = (b0 + b4) + (u16x2)4 * (b1 + b3) + (u16x2)6 * b2;
+            *reinterpret_cast<uint2*>(H + r * RW + 4 * q) = make_uint2(as_u32(ha), as_u32(hb));
+        }
+        __syncthreads();
+        // columns pass: R[i][j] = (1 4 6 4 1 over H rows 2i .. 2i + 4, + 128) >> 8 in
+        // packed u16 (sums <= 65280 + 128), 4 columns per task
+        for (int k = tid; k < RH * NQ; k += 256) {
+            const int i = k / NQ, q = k - i * NQ;
+            const uint16_t* t = H + 2 * i * RW + 4 * q;
+            const uint2 r0 = *reinterpret_cast<const uint2*>(t), r1 = *reinterpret_cast<const uint2*>(t + RW),
+                        r2 = *reinterpret_cast<const uint2*>(t + 2 * RW),
+                        r3 = *reinterpret_cast<const uint2*>(t + 3 * RW),
+                        r4 = *reinterpret_cast<const uint2*>(t + 4 * RW);
+            const u16x2 sa = (as_u16x2(r0.x) + as_u16x2(r4.x)) + (u16x2)4 * (as_u16x2(r1.x) + as_u16x2(r3.x)) +
+                             (u16x2)6 * as_u16x2(r2.x) + (u16x2)128;
+            const u16x2 sb = (as_u16x2(r0.y) + as_u16x2(r4.y)) + (u16x2)4 * (as_u16x2(r1.y) + as_u16x2(r3.y)) +
+                             (u16x2)6 * as_u16x2(r2.y) + (u16x2)128;
+            // the high bytes of the four sums are (s + 128) >> 8
+            *reinterpret_cast<uint32_t*>(R + i * PW + 4 * q) = __builtin_amdgcn_perm(as_u32(sb), as_u32(sa), 0x07050301u);
+        }
+        __syncthreads();
+        // entries outside the level: the reflected pixel -- columns first, then the
+        // rows, which copy whole region rows including their fixed columns
+        const int nxl = max(0, min(-gx, RW)), nxr = max(0, min(gx + RW - w, RW - nxl));
+        if (nxl + nxr > 0) {  // columns [0, nxl) and [RW - nxr, RW) of the region
+            const int nc = nxl + nxr;
+            for (int k = tid; k < RH * nc; k += 256) {
+                const int r = k / nc, j = k - r * nc;
+                const int c = j < nxl ? j : RW - nxr + (j - nxl);
+                R[r * PW + c] = R[r * PW + (refl101(gx + c, w) - gx)];
+            }
+            __syncthreads();
+        }
+        const int nyt = max(0, min(-gy, RH)), nyb = max(0, min(gy + RH - h, RH - nyt));
+        if (nyt + nyb > 0) {  // rows [0, nyt) and [RH - nyb, RH)
+            constexpr int DW = PW / 4;
+            const int n = (nyt + nyb) * DW;
+            for (int k = tid; k < n; k += 256) {
+                const int j = k / DW, q = k - j * DW;
+                const int r = j < nyt ? j : RH - nyb + (j - nyt);
+                *reinterpret_cast<uint32_t*>(R + r * PW + 4 * q) =
+                    *reinterpret_cast<const uint32_t*>(R + (refl101(gy + r, h) - gy) * PW + 4 * q);
+            }
+            __syncthreads();
+        }
+    }
+}
+
+// Level l of the chain's phase 2 (stores only): the owned tile's derivatives
+// (pyr_scharr_kernel's arithmetic, a task = 4 columns x 4 rows from 3 aligned
+// dwords of each of 6 region rows), its pixels (l >= 2; level 1 is written by the
+// level-0 launch) and the border pixels whose sources it owns.
+template <int C, bool SCHARR, int S, int l>
+__device__ __forceinline__ void chain_store(const PyrDesc& P, const DerivDesc* ders, const uint8_t* lds) {
+    using Sh = ChainShape<C, SCHARR, S>;
+    constexpr int PW = Sh::PW(l), HX = Sh::hx(l), HY = Sh::hy(l), OWl = Sh::OW(l), OHl = Sh::OH(l);
+    const int tid = threadIdx.x;
+    const ImgLevel& L = P.lv[l];
+    const int w = L.w, h = L.h;
+    const int ox0 = (int)blockIdx.x * OWl, oy0 = (int)blockIdx.y * OHl;
+    const int ox1 = min(ox0 + OWl, w), oy1 = min(oy0 + OHl, h);
+    const uint8_t* __restrict__ R = lds + Sh::off(l);
+    if constexpr (SCHARR) {
+        uint32_t* __restrict__ out = ders[blockIdx.z].data[l];
+        const int op = ders[blockIdx.z].pitch[l];
+        constexpr int NG = OWl / 4, NT = NG * (OHl / 4);
+        for (int k = tid; k < NT; k += 256) {
+            const int qq = k / NG, g = k - qq * NG;
+            const int x = ox0 + 4 * g;
+            if (x >= w || oy0 + 4 * qq >= h) continue;
+            int rows[6][6];
+#pragma unroll
+            for (int rr = 0; rr < 6; rr++) {
+                const uint8_t* trow = R + (HY + 4 * qq - 1 + rr) * PW + HX + 4 * g - 4;
+                const unsigned a0 = *reinterpret_cast<const unsigned*>(trow);
+                const unsigned a1 = *reinterpret_cast<const unsigned*>(trow + 4);
+                const unsigned a2 = *reinterpret_cast<const unsigned*>(trow + 8);
+                rows[rr][0] = a0 >> 24;
+                rows[rr][1] = a1 & 0xFF;
+                rows[rr][2] = (a1 >> 8) & 0xFF;
+                rows[rr][3] = (a1 >> 16) & 0xFF;
+                rows[rr][4] = a1 >> 24;
+                rows[rr][5] = a2 & 0xFF;
+            }
+#pragma unroll
+            for (int jj = 0; jj < 4; jj++) {
+                const int y = oy0 + 4 * qq + jj;
+                if (y >= h) break;
+                unsigned o[4];
+#pragma unroll
+                for (int m = 0; m < 4; m++) {
+                    const int tl = rows[jj][m], tm = rows[jj][m + 1], tr = rows[jj][m + 2];
+                    const int ml = rows[jj + 1][m], mr = rows[jj + 1][m + 2];
+                    const int bl = rows[jj + 2][m], bm = rows[jj + 2][m + 1], br = rows[jj + 2][m + 2];
+                    const int ix = (3 * (tr + br) + 10 * mr) - (3 * (tl + bl) + 10 * ml);
+                    const int iy = 3 * ((br - tr) + (bl - tl)) + 10 * (bm - tm);
+                    o[m] = ((unsigned)(iy * (1 << kDerShift)) << 16) | ((unsigned)(ix * (1 << kDerShift)) & 0xFFFFu);
+                }
+                uint32_t* d = out + (size_t)y * op + x;
+                if (x + 3 < w) {
+                    *reinterpret_cast<uint4*>(d) = make_uint4(o[0], o[1], o[2], o[3]);
+                } else {
+#pragma unroll
+                    for (int m = 0; m < 4; m++)
+                        if (x + m < w) d[m] = o[m];
+                }
+            }
+        }
+    }
+    uint8_t* __restrict__ dst = const_cast<uint8_t*>(L.data);
+    if constexpr (l > S) {
+        constexpr int NQ = OWl / 4;
+        for (int k = tid; k < NQ * OHl; k += 256) {
+            const int i = k / NQ, q = k - i * NQ;
+            const int x = ox0 + 4 * q, y = oy0 + i;
+            if (x >= w || y >= h) continue;
+            const uint32_t v = *reinterpret_cast<const uint32_t*>(R + (HY + i) * PW + HX + 4 * q);
+            uint8_t* d = dst + (size_t)y * L.pitch + x;
+            if (x + 3 < w) {
+                *reinterpret_cast<uint32_t*>(d) = v;
+            } else {
+#pragma unroll
+                for (int m = 0; m < 4; m++)
+                    if (x + m < w) d[m] = (uint8_t)(v >> (8 * m));
+            }
+        }
+    }
+    const int gx = ox0 - HX, gy = oy0 - HY;
+    pad_owned(dst, w, h, L.pitch, ox0, ox1, oy0, oy1, [&](int x, int y) { return R[(y - gy) * PW + (x - gx)]; },
+              [&](int y) { return R + (y - gy) * PW + HX; });
+}
+
+template <int C, bool SCHARR, int S, int... I>
+__device__ __forceinline__ void chain_all(const PyrDesc& P, const DerivDesc* ders, uint8_t* lds, uint16_t* H,
+                                          std::integer_sequence<int, I...>) {
+    (chain_build<C, SCHARR, S, I + S>(P, lds, H), ...);
+    (chain_store<C, SCHARR, S, I + S>(P, ders, lds), ...);
+}
+
+template <int C, bool SCHARR, int S>
+__global__ __launch_bounds__(256) void pyr_chain_kernel(const PyrDesc* __restrict__ descs,
+                                                        const DerivDesc* __restrict__ ders) {
+    using Sh = ChainShape<C, SCHARR, S>;
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    chain_all<C, SCHARR, S>(descs[blockIdx.z], ders, lds, reinterpret_cast<uint16_t*>(lds + Sh::off_h()),
+                            std::make_integer_sequence<int, C - S + 1>{});
+}
+
+template <int C, bool SCHARR, int S>
+static void launch_chain(const PyrDesc* d_descs, const DerivDesc* d_ders, int nseq, int w, int h, hipStream_t st) {
+    using Sh = ChainShape<C, SCHARR, S>;
+    static_assert(Sh::lds() <= 65536, "chain LDS");
+    int wc = w, hc = h;
+    for (int l = 0; l < C; l++) {
+        wc = (wc + 1) / 2;
+        hc = (hc + 1) / 2;
+    }
+    const dim3 grid((wc + Sh::TW - 1) / Sh::TW, (hc + Sh::TH - 1) / Sh::TH, nseq);
+    hipLaunchKernelGGL((pyr_chain_kernel<C, SCHARR, S>), grid, dim3(256), Sh::lds(), st, d_descs, d_ders);
+}
+
+// The chain's first level: the last two levels of the pyramid (one level for a
+// two-level pyramid). Measured at the KITTI batch (64 frames), the chain of
+// levels 1 .. 3 in one launch ran 47 us: its regions' halos (level 1 staged
+// 184 x 52 for a 128 x 32 tile) cost more VALU than the launches they save, so
+// the larger levels keep the per-level pyr_scharr / pyr_down launches (with their
+// sources' borders fused in) and only the small levels are chained.
+constexpr int chain_start(int c) { return c > 1 ? c - 1 : 1; }
+
+template <bool SCHARR>
+static void launch_chain_c(int c, const PyrDesc* d_descs, const DerivDesc* d_ders, int nseq, int w, int h,
+                           hipStream_t st) {
+    switch (c) {
+        case 1: launch_chain<1, SCHARR, chain_start(1)>(d_descs, d_ders, nseq, w, h, st); break;
+        case 2: launch_chain<2, SCHARR, chain_start(2)>(d_descs, d_ders, nseq, w, h, st); break;
+        case 3: launch_chain<3, SCHARR, chain_start(3)>(d_descs, d_ders, nseq, w, h, st); break;
+        case 4: launch_chain<4, SCHARR, chain_start(4)>(d_descs, d_ders, nseq, w, h, st); break;
+        case 5: launch_chain<5, SCHARR, chain_start(5)>(d_descs, d_ders, nseq, w, h, st); break;
+        case 6: launch_chain<6, SCHARR, chain_start(6)>(d_descs, d_ders, nseq, w, h, st); break;
+        case 7: launch_chain<7, SCHARR, chain_start(7)>(d_descs, d_ders, nseq, w, h, st); break;
+    }
+}
+
+// SVO_PYR_FUSED=0: the per-level launches (A/B; read at every launch, so a test
+// can run both forms in one process)
+static bool fused_on() {
+    const char* e = std::getenv("SVO_PYR_FUSED");
+    return !(e && e[0] == '0');
+}
+
+// pyramid (levels 1 ..) + borders of nseq frames: level 0 -> 1 with level 0's
+// border, then the fused chain (levels 2 .. and the borders of levels 1 ..)
+hipError_t launch_pyramid_batched(const PyrDesc* d_descs, int nseq, int w, int h, int nlevels, hipStream_t st) {
+    const int c = nlevels - 1;
+    if (!fused_on() || c < 1 || c >= kMaxLevels) return pyramid_levels(d_descs, nseq, w, h, nlevels, st);
+    // levels 1 .. chain_start(c) one launch each, every launch also writing its
+    // source level's border; then the chain
+    int lw = w, lh = h;
+    for (int l = 1; l <= chain_start(c); l++) {
+        lw = (lw + 1) / 2;
+        lh = (lh + 1) / 2;
+        hipLaunchKernelGGL(pyr_down_batched_kernel, dim3((lw + PD_TX - 1) / PD_TX, (lh + PD_TY - 1) / PD_TY, nseq),
+                           dim3(256), 0, st, d_descs, l, 1);
+    }
+    launch_chain_c<false>(c, d_descs, nullptr, nseq, w, h, st);
+    return hipGetLastError();
+}
+
+// pyramid (levels 1 ..), derivative levels 0 .. and borders of nseq frames: level
+// 0 -> 1 with level 0's derivative and border, then the fused chain
+hipError_t launch_pyramid_scharr_batched(const PyrDesc* d_descs, const DerivDesc* d_ders, int nseq, int w, int h,
+                                         int nlevels, hipStream_t st) {
+    const int c = nlevels - 1;
+    if (!fused_on() || c < 1 || c >= kMaxLevels)
+        return pyramid_scharr_levels(d_descs, d_ders, nseq, w, h, nlevels, st);
+    // level l -> l + 1 + level l's derivative and border, l < chain_start(c); then the chain
+    int lw = w, lh = h;
+    for (int l = 0; l < chain_start(c); l++) {
+        lw = (lw + 1) / 2;
+        lh = (lh + 1) / 2;
+        hipLaunchKernelGGL(pyr_scharr_kernel<true>, dim3((lw + PD_TX - 1) / PD_TX, (lh + PD_TY - 1) / PD_TY, nseq),
+                           dim3(256), 0, st, d_descs, d_ders, l, 1);
+    }
+    launch_chain_c<true>(c, d_descs, d_ders, nseq, w, h, st);
+    return hipGetLastError();
 }
 
 }  // namespace svo

@@ -84,6 +84,57 @@ def test_frontend_scharr_pyramid_bit_exact(ctx, wh):
     fe.close()
 
 
+def _levels_for_window(w, h, win, max_level):
+    """common.hpp lk_levels_for_window (buildOpticalFlowPyramid's level cap)."""
+    for level in range(max_level + 1):
+        w, h = (w + 1) // 2, (h + 1) // 2
+        if w <= win or h <= win:
+            return level
+    return max_level
+
+
+@pytest.mark.parametrize("wh,max_level,win", [((1241, 376), 3, 21), ((401, 203), 3, 21), ((97, 61), 4, 5),
+                                              ((45, 37), 3, 3), ((1920, 1080), 4, 21), ((130, 70), 1, 21),
+                                              ((66, 34), 2, 5), ((257, 129), 5, 3)])
+@pytest.mark.parametrize("fused", ["1", "0"])
+def test_frontend_pyramids_with_borders(ctx, wh, max_level, win, fused, monkeypatch):
+    """The front end's left pyramids (pyrDown + Scharr + the source level's border
+    per launch; the last two levels, their derivatives and borders in one fused
+    launch) and right pyramids, each
+    level with its stored REFLECT_101 border, against the oracle's pyrDown chain
+    padded by numpy's reflect (= BORDER_REFLECT_101, repeated for tiny levels); the
+    derivatives of every level against the oracle's Scharr. Both forms: the fused
+    chain of the last two levels (SVO_PYR_FUSED=1, the default) and one launch per
+    level + the border pass (0); the switch is read at every launch."""
+    monkeypatch.setenv("SVO_PYR_FUSED", fused)
+    w, h = wh
+    P = S.PYR_PAD
+    scenes = [Scene(w, h, seed=s) for s in (5, 6)]
+    cfg = S.FrontendConfig(w, h, scenes[0].K, n_seq=2, n_frames=3, n_features=300, max_level=max_level,
+                           stereo_max_level=max_level, win=win, stereo_win=win)
+    nlev = _levels_for_window(w, h, win, max_level) + 1
+    fe = S.Frontend(ctx, cfg)
+    for s, sc in enumerate(scenes):
+        for t in range(3):
+            fe.set_frame(s, t, sc.frame(t), sc.right(t))
+    fe.init(0)
+    fe.step(1)   # left pyramids of frames 1 and 2, right pyramid of frame 1
+    for s, sc in enumerate(scenes):
+        for t, right in ((1, False), (2, False), (1, True)):
+            lvl = sc.right(t) if right else sc.frame(t)
+            for l in range(nlev):
+                got = fe.pyramid_level(s, t, l, lvl.shape[1], lvl.shape[0], right=right)
+                ref = np.pad(lvl, P, mode="reflect")
+                assert np.array_equal(got, ref), f"seq {s} t {t} right {right} level {l} ({lvl.shape})"
+                if not right:
+                    ix, iy = fe.scharr(s, t, l, lvl.shape[1], lvl.shape[0])
+                    rd = O.scharr(lvl).astype(np.int32)
+                    assert np.array_equal(ix.astype(np.int32), 4 * rd[..., 0]), f"seq {s} t {t} ix level {l}"
+                    assert np.array_equal(iy.astype(np.int32), 4 * rd[..., 1]), f"seq {s} t {t} iy level {l}"
+                lvl = O.pyr_down(lvl)
+    fe.close()
+
+
 # ------------------------------------------------------------------ FAST
 @pytest.mark.parametrize("wh,seed", [((1241, 376), 0), ((160, 120), 3), ((64, 48), 5), ((3840, 2160), 1)])
 def test_fast_score_map_bit_exact(ctx, wh, seed):

@@ -11,6 +11,7 @@
 #   pmc TAG CONFIG [SEQ]    FETCH_SIZE / WRITE_SIZE passes of a bench run of CONFIG,
 #                           folded into profiles/pmc_summary.json (configs[CONFIG])
 #   mix TAG [BENCH_ARGS]    SQ instruction mix per wave of every step kernel
+#                           (mix TAG --cmd CMD..: of any command's kernels)
 #   lksplit                 LK VALU / time with the iteration cap at 1, 2, 50
 #   lkab "V1 V2 .."         standalone LK kernel time per SVO_LK_MULTI variant
 #   lkmem [LIB ..]          LK memory-pipeline + issue counters (TA, TCP, SQ), per library build
@@ -24,7 +25,7 @@ cd /tmp && export TMPDIR=/tmp
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 O=gpurun_out
 mkdir -p $O
-BQ="python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-single --no-bucketed"
+BQ="python bench.py --steps ${AB_STEPS:-20} --warmup 5 --no-cpu-baseline --no-single --no-bucketed"
 
 fail() { echo "FAILED: $1"; [ -n "$2" ] && tail -30 "$2"; exit 1; }
 
@@ -95,6 +96,7 @@ run_pmc() {
 run_mix() {
     local tag=$1; shift
     local B="python bench.py ${*:---steps 8 --warmup 2 --no-cpu-baseline --no-single --no-bucketed}"
+    [ "$1" = "--cmd" ] && { shift; B="$*"; }
     timeout -s KILL 200 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_WAIT_INST_ANY \
         SQ_ACTIVE_INST_ANY SQ_INSTS_VMEM -d /tmp/ps1 -o run --output-format csv -- $B > $O/mix.log 2>&1 || fail mix1 $O/mix.log
     timeout -s KILL 200 rocprofv3 --pmc SQ_ACTIVE_INST_VALU SQ_BUSY_CYCLES SQ_INSTS_BRANCH SQ_WAIT_INST_LDS \
@@ -192,7 +194,8 @@ run_ab() {
         env $var=$v timeout -k 10 200 $BQ > $O/ab.log 2>&1 || fail ab $O/ab.log
         python -c "
 import json; d=json.loads(open('$O/ab.log').read().strip().splitlines()[-1]); p=d['phase_ms_per_step']
-print('$var=$v', d['value'], d['ms_per_step'], 'lk', p['lk'], 'fast', p['fast'], 'pyr', p['pyramid'])"
+sm=d.get('step_ms', {})
+print('$var=$v', d['value'], d['ms_per_step'], 'median', sm.get('median'), 'p90', sm.get('p90'), 'lk', p['lk'], 'pyr', p['pyramid'])"
     done; done
 }
 
