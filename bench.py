@@ -174,12 +174,17 @@ def cpu_baseline(cfg_name: str, seconds: float):
     from oracle_loop import OracleLoop  # noqa: E402
     from svo_amd.scene import Scene
     W, H, N, _, _ = CONFIGS[cfg_name]
-    # every CPU this process may run on (the rank's share of the node), not
-    # OMP_NUM_THREADS: SURVEY §8(d) asks for LK over all host cores
+    # every CPU this process may use: the affinity mask, capped by OMP_NUM_THREADS
+    # where the machine sets it -- the GPU box exports its per-GPU CPU share there
+    # (16) while its affinity mask and nproc show the whole node (256); SURVEY
+    # §8(d) asks for LK over all the host cores the process has
     try:
         cores = len(os.sched_getaffinity(0))
     except AttributeError:
         cores = os.cpu_count() or 1
+    omp = os.environ.get("OMP_NUM_THREADS", "")
+    if omp.isdigit() and int(omp) > 0:
+        cores = min(cores, int(omp))
 
     def run(threads, secs):
         O.set_threads(threads)
@@ -205,6 +210,41 @@ def cpu_baseline(cfg_name: str, seconds: float):
                               "sample": f"{n1} frames, {dt1:.1f} s, everything on one thread"}}
 
 
+def forward_workload(S, SceneForward, ctx, W, H, N, ML, Sq, K, Wm, threads):
+    """The harder sequence (svo_amd.scene.SceneForward: forward translation with
+    parallax + a textured occluder sliding against the static world, 5-20 % RANSAC
+    outliers, several times more keyframe points) timed like the headline: Sq
+    sequences per launch, Wm warm-up + K timed steps. 16 distinct sequences are
+    rendered (the general renderer's host cost) and each fills Sq / 16 batch slots."""
+    n_dist = min(Sq, 16)
+    T = Wm + K + 1
+    scs = [SceneForward(W, H, seed=1000 + i) for i in range(n_dist)]
+    P = min(T, 2 * scs[0].period)
+    pairs = [[(sc.frame(t), sc.right(t)) for t in range(P)] for sc in scs]
+    fef = S.Frontend(ctx, S.FrontendConfig(W, H, scs[0].K, n_seq=Sq, n_frames=T, n_features=N, max_level=ML,
+                                           host_threads=threads, timing=0))
+    for s in range(Sq):
+        for t in range(T):
+            fef.set_frame(s, t, *pairs[s % n_dist][t % P])
+    fef.init(0)
+    for t in range(1, Wm + 1):
+        fef.step(t)
+    tot = {"tracked": 0, "inliers": 0, "added": 0, "hypotheses": 0}
+    t1 = time.perf_counter()
+    for t in range(Wm + 1, Wm + K + 1):
+        st = fef.step(t).as_dict()
+        for k in tot:
+            tot[k] += st[k]
+    fef.synchronize()
+    dt = time.perf_counter() - t1
+    fef.close()
+    return {"value": round(Sq * K / dt, 2), "unit": "frames/s", "ms_per_step": round(dt / K * 1e3, 4),
+            "steps": K, "warmup": Wm, "distinct_sequences": n_dist,
+            "outlier_ratio": round(1 - tot["inliers"] / max(tot["tracked"], 1), 4),
+            "stats_per_step": {k: round(v / K, 2) for k, v in tot.items()},
+            "scene": "SceneForward: 0.04 m/frame forward (ping-pong), occluder at 8 m sliding 18 px/frame"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -222,6 +262,11 @@ def main():
     ap.add_argument("--no-single", action="store_true")
     ap.add_argument("--no-bucketed", action="store_true",
                     help="skip the second measurement with bucketed selection in the loop")
+    ap.add_argument("--scene", default="rot", choices=("rot", "forward"),
+                    help="rot: the rotation-only scene (the headline); forward: SceneForward (translation "
+                         "parallax + a moving occluder: 5-20%% RANSAC outliers) as the timed workload")
+    ap.add_argument("--no-forward", action="store_true",
+                    help="skip the extra timed pass over the forward/occluder scene (`workloads.forward`)")
     ap.add_argument("--dry-run", action="store_true",
                     help="set up the ranks, print each rank's shard and exit (no GPU call)")
     args = ap.parse_args()
@@ -243,7 +288,7 @@ def main():
             dist.destroy_process_group()
         return
     import svo_amd as S
-    from svo_amd.scene import Scene
+    from svo_amd.scene import Scene, SceneForward
 
     W, H, N, ML, label = CONFIGS[args.config]
     Sq, K, Wm = args.seq, args.steps, args.warmup
@@ -258,7 +303,8 @@ def main():
             device = local % n_dev
     ctx = S.Context(device)
     seeds = sequence_seeds(rank, Sq)
-    scenes = [Scene(W, H, seed=sd) for sd in seeds]
+    scene_cls = SceneForward if args.scene == "forward" else Scene
+    scenes = [scene_cls(W, H, seed=sd) for sd in seeds]
     # the synthetic camera ping-pongs with period 2 * scene.period (32 frames), so
     # P rendered stereo pairs per sequence are reused cyclically (frame t = pair
     # t mod P; rendering is host work outside the timing, all T frames resident)
@@ -345,11 +391,21 @@ def main():
     pyr_avg_s = fe.time_pyramid(Wm + K, 20) / 1e3
     pyr_bytes = Sq * pyr_bytes_per_frame(W, H, ML)
     der_bytes = Sq * deriv_bytes_per_frame(W, H, ML)
-    # the chain's HBM bytes: (nlev - 1) pyr_scharr launches (their average over the
-    # levels x the count = the sum) + the coarsest level's scharr + the borders
-    t_ps, t_sc, t_pad = (pmc_traffic(args.config, k) for k in ("pyr_scharr_kernel", "scharr_kernel",
-                                                                "pad_batched_kernel"))
-    pyr_traffic = ML * t_ps + t_sc + t_pad if None not in (t_ps, t_sc, t_pad) else None
+    # the chain's HBM bytes. Fused (SVO_PYR_FUSED=1, the default; c = the coarsest
+    # level, max(ML, stereo maxLevel 3)): c - 1 pyr_scharr launches (their average
+    # over the levels x the count = the sum) + pyr_chain_kernel (last two levels,
+    # derivatives, borders). Per level: c pyr_scharr + the coarsest scharr + borders.
+    c_lev = max(ML, 3)
+    if os.environ.get("SVO_PYR_FUSED", "1")[:1] == "0":
+        t_ps, t_sc, t_pad = (pmc_traffic(args.config, k) for k in ("pyr_scharr_kernel", "scharr_kernel",
+                                                                    "pad_batched_kernel"))
+        pyr_traffic = c_lev * t_ps + t_sc + t_pad if None not in (t_ps, t_sc, t_pad) else None
+        pyr_kernels = "pyr_scharr_kernel x levels + scharr_kernel (coarsest) + pad_batched_kernel (borders)"
+    else:
+        t_ps, t_ch = (pmc_traffic(args.config, k) for k in ("pyr_scharr_kernel", "pyr_chain_kernel"))
+        pyr_traffic = (c_lev - 1) * t_ps + t_ch if None not in (t_ps, t_ch) else None
+        pyr_kernels = (f"pyr_scharr_kernel x {c_lev - 1} (pyrDown + Scharr + the source level's border) + "
+                       "pyr_chain_kernel (last two levels, their derivatives and borders)")
     single = None
     if not args.no_single and world == 1:
         fe1 = S.Frontend(ctx, S.FrontendConfig(W, H, scenes[0].K, n_seq=1, n_frames=T, n_features=N, max_level=ML))
@@ -388,6 +444,11 @@ def main():
         bucketed = {"value": round(Sq * K / dtb, 2), "unit": "frames/s", "ms_per_step": round(dtb / K * 1e3, 4),
                     "bucket_size": BS, "per_bucket": PB, "steps": K, "warmup": Wm}
         feb.close()
+    forward = None
+    if not args.no_forward and args.scene == "rot" and world == 1:
+        if not all_pairs:
+            fe.close()
+        forward = forward_workload(S, SceneForward, ctx, W, H, N, ML, Sq, K, Wm, args.threads)
     out = {
         "metric": "frames/sec @1241x376, 2000 feats; LK iters/sec; achieved HBM GB/s",
         "value": round(fps, 2),
@@ -400,7 +461,8 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "u8/int32 fixed-point (LK sums exact int, solve f32), f64 PnP",
-        "data": "synthetic (rendered KITTI-size frames, seeded; no dataset on the box)",
+        "data": "synthetic (rendered KITTI-size frames, seeded; no dataset on the box)"
+                + ("; SceneForward (translation + moving occluder)" if args.scene == "forward" else ""),
         "config": {"workload": label, "sequences_per_gpu": Sq, "global_batch": Sq * world,
                    "features": N, "win": 21, "max_level": ML, "parallelism": f"{world} x independent sequences",
                    "host_cpus_rank0": len(host_cpus)},
@@ -408,6 +470,7 @@ def main():
         "achieved_GBps_algorithmic": round(frames * frame_bytes(W, H, N, ML) / dt_max / 1e9, 2),
         "single_stream_fps": round(single, 2) if single else None,
         "bucketed": bucketed,
+        "workloads": {"forward": forward},
         "phase_ms_per_step": {k: round(v[0] / K, 4) for k, v in phases.items()},
         "stats_per_step": {k: round(v / K, 3) for k, v in tot.items()},
         "step_ms": {"median": round(float(np.median(step_s)) * 1e3, 4), "p90": round(float(np.percentile(step_s, 90)) * 1e3, 4),
@@ -428,8 +491,7 @@ def main():
             "launches_timed": lk_n,
         },
         "roofline_pyramid": {
-            "kernel": "pyr_scharr_kernel chain (pyrDown + Scharr of every level, borders), "
-                      f"one new left frame of {Sq} sequences per launch",
+            "kernel": f"pyramid chain: {pyr_kernels}; one new left frame of {Sq} sequences per launch",
             "bound": "hbm",
             "achieved": round(pyr_bytes / pyr_avg_s / 1e9, 2) if pyr_avg_s > 0 else 0.0,
             "peak": HBM_PEAK_GBPS,

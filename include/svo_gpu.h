@@ -378,6 +378,19 @@ int svo_synth_frame_right(const uint8_t* canvas, int cw, int ch, int margin_x, i
                           const double R[9], const double K[9], double bf, int depth_seed,
                           uint64_t noise_seed, int noise, uint8_t* frame, int w, int h);
 
+/* The same depth-field surface seen by a camera with centre C (world) and
+ * rotation R (world -> camera: X_c = R (X - C)) -- a translating camera, so the
+ * frames carry parallax -- in front of n_occ textured rectangles: occ[5 k ..]
+ * = x0, y0, x1, y1, z (the world plane z, x in [x0, x1], y in [y0, y1]), each
+ * drawn from the tw x th texture `occ_tex` (the forward sequences' moving
+ * occluders: their points move against the static world). Per pixel the first
+ * hit along the ray: the surface by a safeguarded Newton solve of X_z =
+ * rho(projection of X from the origin), an occluder by a plane intersection. */
+int svo_synth_view(const uint8_t* canvas, int cw, int ch, int margin_x, int margin_y, const double R[9],
+                   const double C[3], const double K[9], int depth_seed, const double* occ, int n_occ,
+                   const uint8_t* occ_tex, int tw, int th, uint64_t noise_seed, int noise, uint8_t* frame, int w,
+                   int h);
+
 #ifdef __cplusplus
 }
 #endif

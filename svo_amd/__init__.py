@@ -34,7 +34,7 @@ import numpy as np
 __all__ = [
     "SvoError", "lib", "Context", "Image", "FastFeatureDetector",
     "TERM_COUNT", "TERM_EPS", "LK_USE_INITIAL_FLOW", "LK_GET_MIN_EIGENVALS",
-    "synth_canvas", "synth_frame", "synth_frame_right", "lib_path", "Frontend", "FrontendConfig", "FrontendStats",
+    "synth_canvas", "synth_frame", "synth_frame_right", "synth_view", "lib_path", "Frontend", "FrontendConfig", "FrontendStats",
 ]
 
 TERM_COUNT = 1
@@ -141,6 +141,8 @@ _SIGS = [
                                   C.c_uint64, C.c_int, _u8p, C.c_int, C.c_int]),
     ("svo_synth_frame_right", C.c_int, [_u8p, C.c_int, C.c_int, C.c_int, C.c_int, _f64p, _f64p,
                                         C.c_double, C.c_int, C.c_uint64, C.c_int, _u8p, C.c_int, C.c_int]),
+    ("svo_synth_view", C.c_int, [_u8p, C.c_int, C.c_int, C.c_int, C.c_int, _f64p, _f64p, _f64p, C.c_int, _f64p,
+                                 C.c_int, _u8p, C.c_int, C.c_int, C.c_uint64, C.c_int, _u8p, C.c_int, C.c_int]),
 ]
 
 SYMBOLS = [s[0] for s in _SIGS]
@@ -711,6 +713,26 @@ def synth_frame(canvas: np.ndarray, margin: tuple, R, K, noise_seed: int, noise:
     if lib().svo_synth_frame(_p(canvas, _u8p), cw, ch, int(margin[0]), int(margin[1]), _p(R, _f64p),
                              _p(K, _f64p), noise_seed, noise, _p(out, _u8p), w, h) != 0:
         raise SvoError("svo_synth_frame failed")
+    return out
+
+
+def synth_view(canvas: np.ndarray, margin: tuple, R, Cw, K, depth_seed: int, occ, occ_tex, noise_seed: int,
+               noise: int, w: int, h: int) -> np.ndarray:
+    """svo_synth_view: the depth-field surface from camera (R, centre Cw) in front of
+    the rectangles occ ((n, 5): x0, y0, x1, y1, z) textured by occ_tex."""
+    canvas = _c(canvas, np.uint8)
+    R = _c(R, np.float64).reshape(9)
+    Cw = _c(Cw, np.float64).reshape(3)
+    K = _c(K, np.float64).reshape(9)
+    occ = _c(np.zeros((0, 5)) if occ is None else occ, np.float64).reshape(-1, 5)
+    tex = _c(np.zeros((2, 2), np.uint8) if occ_tex is None else occ_tex, np.uint8)
+    out = np.empty((h, w), np.uint8)
+    ch, cw = canvas.shape
+    th, tw = tex.shape
+    if lib().svo_synth_view(_p(canvas, _u8p), cw, ch, int(margin[0]), int(margin[1]), _p(R, _f64p), _p(Cw, _f64p),
+                            _p(K, _f64p), int(depth_seed), _p(occ, _f64p), len(occ), _p(tex, _u8p), tw, th,
+                            noise_seed, noise, _p(out, _u8p), w, h) != 0:
+        raise SvoError("svo_synth_view failed")
     return out
 
 

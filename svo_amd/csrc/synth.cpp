@@ -147,3 +147,85 @@ extern "C" int svo_synth_frame_right(const uint8_t* canvas, int cw, int ch, int 
     });
     return SVO_OK;
 }
+
+// svo_synth_view (include/svo_gpu.h): a general camera (R, C) over the depth-field
+// surface X(cu, cv) = (((cu - cx) / fx) rho, ((cv - cy) / fy) rho, rho), rho =
+// rho(cu, cv) (the surface the rotation-only views and the right view use), plus
+// rectangular occluders in world planes z = const.
+extern "C" int svo_synth_view(const uint8_t* canvas, int cw, int ch, int margin_x, int margin_y, const double R[9],
+                              const double C[3], const double K[9], int depth_seed, const double* occ, int n_occ,
+                              const uint8_t* occ_tex, int tw, int th, uint64_t noise_seed, int noise, uint8_t* frame,
+                              int w, int h) {
+    if (!canvas || !R || !C || !K || !frame || w <= 0 || h <= 0 || n_occ < 0 || (n_occ > 0 && (!occ || !occ_tex)) ||
+        (n_occ > 0 && (tw < 2 || th < 2)))
+        return SVO_ERR_ARG;
+    const double fx = K[0], fy = K[4], cx = K[2], cy = K[5];
+    const double seed = (double)depth_seed;
+    auto bilinear = [](const uint8_t* img, int iw, int ih, double u, double v) {
+        u = u < 0 ? 0 : u > iw - 1.001 ? iw - 1.001 : u;
+        v = v < 0 ? 0 : v > ih - 1.001 ? ih - 1.001 : v;
+        const int iu = (int)u, iv = (int)v;
+        const double a = u - iu, b = v - iv;
+        const uint8_t* c0 = img + (size_t)iv * iw + iu;
+        const uint8_t* c1 = c0 + iw;
+        return (1 - a) * (1 - b) * c0[0] + a * (1 - b) * c0[1] + (1 - a) * b * c1[0] + a * b * c1[1];
+    };
+    for_rows(h, [&](int y0, int y1) {
+        for (int y = y0; y < y1; y++) {
+            double lam_prev = -1.0;  // the previous pixel's ray parameter: a warm start
+            for (int x = 0; x < w; x++) {
+                // world ray d = R^T K^-1 p from C
+                const double dx = (x - cx) / fx, dy = (y - cy) / fy;
+                const double d0 = R[0] * dx + R[3] * dy + R[6];
+                const double d1 = R[1] * dx + R[4] * dy + R[7];
+                const double d2 = R[2] * dx + R[5] * dy + R[8];
+                double val = 128.0;
+                double lam = -1.0;
+                if (d2 > 0) {
+                    // f(lam) = X_z - rho(cu, cv), X = C + lam d: f < 0 at rho's minimum
+                    // 3, > 0 at its maximum 21 -> a bracket; Newton steps inside it
+                    double lo = (3.0 - C[2]) / d2, hi = (21.0 - C[2]) / d2;
+                    lam = lam_prev > lo && lam_prev < hi ? lam_prev : 0.5 * (lo + hi);
+                    double cu = 0, cv = 0;
+                    for (int it = 0; it < 60; it++) {
+                        const double X0 = C[0] + lam * d0, X1 = C[1] + lam * d1, X2 = C[2] + lam * d2;
+                        cu = fx * X0 / X2 + cx;
+                        cv = fy * X1 / X2 + cy;
+                        const double rho = 12.0 + 5.0 * std::sin(cu / 97.0 + seed) + 4.0 * std::cos(cv / 61.0 - 0.5 * seed);
+                        const double f = X2 - rho;
+                        if (std::fabs(f) < 1e-10) break;
+                        if (f < 0) lo = lam; else hi = lam;
+                        const double dcu = fx * (d0 * X2 - X0 * d2) / (X2 * X2);
+                        const double dcv = fy * (d1 * X2 - X1 * d2) / (X2 * X2);
+                        const double drho = 5.0 * std::cos(cu / 97.0 + seed) / 97.0 * dcu -
+                                            4.0 * std::sin(cv / 61.0 - 0.5 * seed) / 61.0 * dcv;
+                        const double fp = d2 - drho;
+                        double nl = fp > 0 ? lam - f / fp : 0.5 * (lo + hi);
+                        if (!(nl > lo && nl < hi)) nl = 0.5 * (lo + hi);
+                        if (hi - lo < 1e-13) break;
+                        lam = nl;
+                    }
+                    val = bilinear(canvas, cw, ch, cu + margin_x, cv + margin_y);
+                    // the nearest occluder in front of the surface point
+                    double best = lam;
+                    for (int k = 0; k < n_occ; k++) {
+                        const double* o = occ + 5 * k;
+                        const double lo_ = (o[4] - C[2]) / d2;
+                        if (!(lo_ > 0 && lo_ < best)) continue;
+                        const double X0 = C[0] + lo_ * d0, X1 = C[1] + lo_ * d1;
+                        if (X0 < o[0] || X0 > o[2] || X1 < o[1] || X1 > o[3]) continue;
+                        best = lo_;
+                        val = bilinear(occ_tex, tw, th, (X0 - o[0]) / (o[2] - o[0]) * (tw - 1),
+                                       (X1 - o[1]) / (o[3] - o[1]) * (th - 1));
+                    }
+                }
+                lam_prev = lam;
+                if (noise > 0)
+                    val += (int)(hash3(noise_seed, (uint64_t)x, (uint64_t)y) % (uint64_t)(2 * noise + 1)) - noise;
+                const int iv8 = (int)std::floor(val + 0.5);
+                frame[(size_t)y * w + x] = (uint8_t)(iv8 < 0 ? 0 : iv8 > 255 ? 255 : iv8);
+            }
+        }
+    });
+    return SVO_OK;
+}

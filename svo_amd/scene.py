@@ -17,7 +17,7 @@ import math
 
 import numpy as np
 
-from . import synth_canvas, synth_frame, synth_frame_right
+from . import synth_canvas, synth_frame, synth_frame_right, synth_view
 
 KITTI_W, KITTI_H = 1241, 376
 # R:configs/config.yaml:8-11 (fx, fy, cx, cy), held as float32 like the
@@ -116,3 +116,49 @@ class Scene:
         Xc = (self.R(t) @ np.asarray(X, np.float64).T)
         uv = self.K @ Xc
         return (uv[:2] / uv[2]).T
+
+
+class SceneForward(Scene):
+    """A harder sequence: the rotating camera of `Scene` also
+    moves forward along the world z axis (ping-pong, `speed` m per frame), so the
+    frames carry depth-dependent parallax (no homography maps one onto the next)
+    and the depth field comes within 3 m; and a textured rectangle in the world
+    plane z = `occ_z` slides sideways at `occ_px` image pixels per frame against
+    the static world, so the map points on it turn into RANSAC outliers as soon
+    as it has moved. Both views are rendered by svo_synth_view (the right camera
+    is the left one shifted by the baseline along its x axis). Frame 0: R = I,
+    C = 0 (the world frame is camera 0's, as the reference's first frame)."""
+
+    def __init__(self, w: int, h: int, seed: int = 0, period: int = 16, speed: float = 0.04,
+                 occ_z: float = 8.0, occ_px: float = 18.0, occ_size=(0.20, 0.45), **kw):
+        super().__init__(w, h, seed=seed, period=period, **kw)
+        self.speed, self.occ_z = speed, occ_z
+        fx, fy = self.K[0, 0], self.K[1, 1]
+        self.occ_step = occ_px * occ_z / fx  # world metres per frame at the occluder's depth
+        hw, hh = occ_z * (w / 2) / fx, occ_z * (h / 2) / fy
+        self.occ_w, self.occ_h = occ_size[0] * 2 * hw, occ_size[1] * 2 * hh
+        self.occ_x0, self.occ_y0 = -0.85 * hw, -0.5 * self.occ_h
+        tw, th = 256, 160
+        self.occ_tex = synth_canvas(seed + 7919, tw, th, tw * th // 40)
+
+    def C(self, t: int) -> np.ndarray:
+        """Camera centre of frame t (world)."""
+        return np.array([0.0, 0.0, self.speed * self.phase(t)])
+
+    def occluders(self, t: int) -> np.ndarray:
+        x0 = self.occ_x0 + self.occ_step * self.phase(t)
+        return np.array([[x0, self.occ_y0, x0 + self.occ_w, self.occ_y0 + self.occ_h, self.occ_z]])
+
+    def _view(self, t: int, centre, noise_seed: int) -> np.ndarray:
+        return synth_view(self.canvas, (self.margin, self.margin), self.R(t), centre, self.K, self.seed,
+                          self.occluders(t), self.occ_tex, noise_seed, self.noise, self.w, self.h)
+
+    def frame(self, t: int) -> np.ndarray:
+        return self._view(t, self.C(t), (self.seed << 20) + t + 1)
+
+    def right(self, t: int, bf: float = STEREO_BF) -> np.ndarray:
+        centre = self.C(t) + self.R(t).T @ np.array([bf / self.K[0, 0], 0.0, 0.0])
+        return self._view(t, centre, (self.seed << 20) + t + (1 << 19))
+
+    def map_points(self, pts, t):  # noqa: D102 -- not a single-ray lookup any more
+        raise NotImplementedError("SceneForward: 3D points come from stereo triangulation")
