@@ -309,6 +309,7 @@ struct svo_frontend {
     int spec_m = 0;        // its margin (features lost to LK + RANSAC it covers)
     bool spec_was_early = false;
     int lk_loss = 0;       // max over sequences of the last step's LK losses
+    int ransac_drop = 0;   // max over sequences of the last step's RANSAC drops
     unsigned long long* fbits;
     uint8_t* status;
     double* map;
@@ -604,7 +605,11 @@ int fe_queue_spec(svo_frontend* fe, int t, bool early) {
     const svo_frontend_config& c = fe->cfg;
     hipStream_t sf = fe->st_fast;
     const bool bucketed = c.bucket_size > 0;
-    const int margin = early ? fe->spec_margin + fe->lk_loss : fe->spec_margin;
+    // spec_margin is the slack over the last step's losses: an outlier-heavy
+    // sequence (the forward / occluder scene drops ~100 of 2000 points a frame)
+    // would otherwise miss the speculation every step and run the serial keyframe
+    // (capped: a sequence whose RANSAC failed dropped everything)
+    const int margin = fe->spec_margin + std::min(fe->ransac_drop, c.n_features / 4) + (early ? fe->lk_loss : 0);
     StereoPrepBatch pb;
     pb.n_tracked = early ? fe->nA : fe->nB;
     pb.cand = bucketed ? fe->cand : fe->kps;
@@ -1330,7 +1335,7 @@ int svo_frontend_step(svo_frontend* fe, int t, svo_frontend_stats* stats) {
     const bool spec = fe->spec_margin >= 0 && fe->spec_t == t;
     const bool spec_early = spec && fe->spec_was_early;
     fe->spec_t = -1;
-    int lk_loss = 0;
+    int lk_loss = 0, ransac_drop = 0;
     bool need_full = false;
     for (int s = 0; s < S; s++) {
         RansacSeq& r = fe->rs[s];
@@ -1428,6 +1433,7 @@ int svo_frontend_step(svo_frontend* fe, int t, svo_frontend_stats* stats) {
         const int n_ref = spec_early ? fe->h_nA[s] : fe->h_nB[s];
         spec_ok &= fe->h_target[s] == 0 || n_ref - kept <= fe->spec_m;
         lk_loss = std::max(lk_loss, fe->h_nA[s] - fe->h_nB[s]);
+        ransac_drop = std::max(ransac_drop, fe->h_nB[s] - kept);
         uint32_t* b = fe->h_best + (size_t)s * fe->WORDS;
         std::memset(b, 0, sizeof(uint32_t) * fe->WORDS);
         if (r.ok) {
@@ -1445,6 +1451,7 @@ int svo_frontend_step(svo_frontend* fe, int t, svo_frontend_stats* stats) {
                                 : 0;
     }
     fe->lk_loss = lk_loss;
+    fe->ransac_drop = ransac_drop;
     ms_fit += ms_since(tf);
     TP("selected");
     // the SQPnP statistics only feed the pose fits, which run during the next
