@@ -1323,6 +1323,8 @@ int svo_frontend_step(svo_frontend* fe, int t, svo_frontend_stats* stats) {
     const float thr = (float)((double)c.pnp_reproj * (double)c.pnp_reproj);
     int64_t nhyp = 0, inl = 0;
     std::vector<int> ms(S, 0);
+    std::vector<int> flat;  // (sequence, hypothesis) pairs of a chunk round
+    flat.reserve((size_t)S * kRansacChunk);
 
     // calculatePose (RANSAC per sequence, hypotheses scored on the GPU), drop
     // outliers (R:src/tracking.cpp:218-229), keyframe
@@ -1373,7 +1375,19 @@ int svo_frontend_step(svo_frontend* fe, int t, svo_frontend_stats* stats) {
             if (rf) return rf;
         }
         auto th = clk::now();
-        fe->pool->run(S, [&](int s) { ms[s] = fe->rs[s].gen_chunk(c.K); });
+        // the chunks' subsets are drawn per sequence (the RNG's order), their EPnP
+        // solves shared out one hypothesis per pool task: a sequence predicted to
+        // need 5 hypotheses no longer keeps one thread busy for 5 solves while
+        // others idle (forward / occluder scene: ~320 solves a step)
+        flat.clear();
+        for (int s = 0; s < S; s++) {
+            ms[s] = fe->rs[s].draw_chunk();
+            for (int j = 0; j < ms[s]; j++) flat.push_back(s * kRansacChunk + j);
+        }
+        fe->pool->run((int)flat.size(), [&](int k) {
+            fe->rs[flat[k] / kRansacChunk].solve(flat[k] % kRansacChunk, c.K);
+        });
+        for (int s = 0; s < S; s++) fe->rs[s].nh += ms[s];
         ms_hyp += ms_since(th);
         TP("hyps generated");
         int mmax = 0;

@@ -370,44 +370,51 @@ int RansacSeq::next_end() const {
     return nh + ((niters - iter) < sched ? (niters - iter) : sched);
 }
 
-int RansacSeq::gen_chunk(const double K[9]) {
+int RansacSeq::draw_chunk() {
     m = 0;
     if (done || direct) return 0;
     const int sched = chunk_size(rounds, first_chunk);
     const int want = (niters - iter) < sched ? (niters - iter) : sched;
     rounds++;
     Rng r{rng};
-    for (int j = 0; j < want; j++) {
-        int idx[5];
+    for (int j = 0; j < want; j++)
         for (int i = 0; i < 5; i++) {
             int v;
             bool dup;
             do {
                 v = r.uniform(0, n);
                 dup = false;
-                for (int k = 0; k < i; k++) dup |= idx[k] == v;
+                for (int k = 0; k < i; k++) dup |= idx[j][k] == v;
             } while (dup);
-            idx[i] = v;
+            idx[j][i] = v;
         }
-        double Rj[9], tj[3], rv[3];
-        const int h = nh + j;
-        if (h < nsamp) {  // the same 5 points, gathered on the device in draw order
-            const float* sp = samp + (size_t)kSampleFloats * h;
-            valid[j] = epnp_pixels(sp, sp + 15, nullptr, 5, K, Rj, tj);
-        } else {
-            valid[j] = epnp_pixels(obj, img, idx, 5, K, Rj, tj);
-        }
-        double* hp = hyp + 12 * j;
-        if (valid[j]) {
-            la::rodrigues_inv(Rj, rv);  // the model is stored as (rvec, tvec)
-            la::rodrigues(rv, hp);
-            std::memcpy(hp + 9, tj, sizeof(tj));
-        } else {
-            for (int k = 0; k < 12; k++) hp[k] = 0;
-        }
-    }
     rng = r.state;
     m = want;
+    return want;
+}
+
+void RansacSeq::solve(int j, const double K[9]) {
+    double Rj[9], tj[3], rv[3];
+    const int h = nh + j;
+    if (h < nsamp) {  // the same 5 points, gathered on the device in draw order
+        const float* sp = samp + (size_t)kSampleFloats * h;
+        valid[j] = epnp_pixels(sp, sp + 15, nullptr, 5, K, Rj, tj);
+    } else {
+        valid[j] = epnp_pixels(obj, img, idx[j], 5, K, Rj, tj);
+    }
+    double* hp = hyp + 12 * j;
+    if (valid[j]) {
+        la::rodrigues_inv(Rj, rv);  // the model is stored as (rvec, tvec)
+        la::rodrigues(rv, hp);
+        std::memcpy(hp + 9, tj, sizeof(tj));
+    } else {
+        for (int k = 0; k < 12; k++) hp[k] = 0;
+    }
+}
+
+int RansacSeq::gen_chunk(const double K[9]) {
+    const int want = draw_chunk();
+    for (int j = 0; j < want; j++) solve(j, K);
     nh += want;
     return want;
 }

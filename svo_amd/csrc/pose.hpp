@@ -41,6 +41,7 @@ struct RansacSeq {
     bool done = true, direct = false, ok = false, fitted = false;
     bool valid[kRansacChunk];
     double hyp[12 * kRansacChunk];
+    int idx[kRansacChunk][5];  // the subsets of the chunk drawn by draw_chunk
     std::vector<uint32_t> best;
     double bestR[9], bestt[3];
     std::vector<int> inliers;
@@ -51,6 +52,11 @@ struct RansacSeq {
     // hypotheses this sequence needs, from its previous frame
     static int predict_iters(double confidence, double ep, int max_iters);
     int gen_chunk(const double K[9]);  // fills hyp[0..m) (R row-major + t); returns m
+    // gen_chunk in two parts, so a pool can solve one chunk's hypotheses on several
+    // threads: draw_chunk draws the chunk's subsets (the RNG's order) and returns
+    // m; solve(j) fills hypothesis j < m
+    int draw_chunk();
+    void solve(int j, const double K[9]);
     // hypotheses generated once the next gen_chunk has run (for deciding whether
     // the full point arrays must be on the host first)
     int next_end() const;
