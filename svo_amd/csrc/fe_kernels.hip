@@ -17,10 +17,13 @@ namespace {
 // finds room on a CU while another slice's LK still occupies the GPU (a
 // 1024-thread block waits for a whole CU to drain).
 constexpr int kFeBlock = 256;
-// The append kernel triangulates every candidate with one thread (a ~2k-flop
-// double Jacobi SVD): 1024 threads per sequence keep its critical-path latency
-// at about one SVD for the usual few hundred candidates.
-constexpr int kAppendBlock = 1024;
+// The append / keyframe kernels triangulate every candidate with one thread (a
+// ~2k-flop double Jacobi SVD, 128 VGPRs). 256 threads per sequence: a block of
+// 1024 such threads needs a whole CU's registers and waited for one to drain
+// beside FAST's pre-detection (keyframe_fused 91 us in the step); at 256 (one
+// wave per SIMD) it starts at once (36 us in the step, 833.6 vs 874 us step
+// period in the same trace); the usual ~50-100 candidates still take one pass.
+constexpr int kAppendBlock = 256;
 // post_lk: its chain of dependent passes (compaction chunks, map-point gathers)
 // is latency-bound; 512 threads halve the chunks of a 2000-feature sequence
 // against 256 and still fit beside FAST's 256-thread blocks
@@ -324,27 +327,13 @@ hipError_t launch_tail(const TailBatch& tb, int nseq, hipStream_t st) {
     return hipGetLastError();
 }
 
-static int append_block() {
-    static const int b = [] {
-        const char* e = std::getenv("SVO_FE_APPEND_BLOCK");
-        return e && std::atoi(e) == 256 ? 256 : kAppendBlock;
-    }();
-    return b;
-}
-
 hipError_t launch_append(const AppendBatch& b, int nseq, hipStream_t st) {
-    if (append_block() == 256)
-        hipLaunchKernelGGL(append_kernel<256>, dim3(nseq), dim3(256), 0, st, b);
-    else
-        hipLaunchKernelGGL(append_kernel<kAppendBlock>, dim3(nseq), dim3(kAppendBlock), 0, st, b);
+    hipLaunchKernelGGL(append_kernel<kAppendBlock>, dim3(nseq), dim3(kAppendBlock), 0, st, b);
     return hipGetLastError();
 }
 
 hipError_t launch_keyframe_fused(const TailBatch& tb, const AppendBatch& ab, int nseq, hipStream_t st) {
-    if (append_block() == 256)
-        hipLaunchKernelGGL(keyframe_fused_kernel<256>, dim3(nseq), dim3(256), 0, st, tb, ab);
-    else
-        hipLaunchKernelGGL(keyframe_fused_kernel<kAppendBlock>, dim3(nseq), dim3(kAppendBlock), 0, st, tb, ab);
+    hipLaunchKernelGGL(keyframe_fused_kernel<kAppendBlock>, dim3(nseq), dim3(kAppendBlock), 0, st, tb, ab);
     return hipGetLastError();
 }
 
