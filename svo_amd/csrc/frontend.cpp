@@ -362,7 +362,8 @@ struct svo_frontend {
     hipStream_t st_copy = nullptr;
     hipEvent_t ev_full = nullptr;  // this step's parity of ev_full_b
     hipEvent_t ev_full_b[2] = {nullptr, nullptr};
-    hipEvent_t ev_pyr_r = nullptr;  // right pyramid of the step's frame built
+    hipEvent_t ev_pyr_r_b[2] = {nullptr, nullptr};  // right pyramid of frame f built: [f & 1]
+    int pyr_r_ready = -1;  // frame whose right pyramid was built ahead (in the previous step)
     bool full_queued = false;
     int fit_parity = 0;  // step parity whose RANSAC results the pending fits refine
     uint8_t* score_map = nullptr;  // [s][npx] FAST scores of the kept corners
@@ -494,7 +495,7 @@ int fe_stereo_lk(svo_frontend* fe, int t, const int* counts, int max_n, hipStrea
     svo_ctx* ctx = fe->ctx;
     const svo_frontend_config& c = fe->cfg;
     int slot;
-    SVO_HIP(ctx, hipStreamWaitEvent(st, fe->ev_pyr_r, 0));
+    SVO_HIP(ctx, hipStreamWaitEvent(st, fe->ev_pyr_r_b[t & 1], 0));
     const PyrDesc* dl = fe->d_desc + (size_t)(t % fe->T) * fe->S;
     const PyrDesc* dr = fe->d_desc_r + (size_t)(t % fe->T) * fe->S;
     LKBatch lb{dl, dr, fe->d_der + (size_t)(t % 3) * fe->S, fe->st_xy, fe->st_next, fe->st_status, nullptr, nullptr,
@@ -964,7 +965,8 @@ int svo_frontend_create(svo_ctx* ctx, const svo_frontend_config* cfg, svo_fronte
             return set_error(ctx, SVO_ERR_HIP, "svo_frontend_create: stream");
         }
         for (hipEvent_t* e : {&fe->ev_pyr, &fe->ev_fast, &fe->ev_lk, &fe->ev_post, &fe->ev_tail, &fe->ev_stats,
-                              &fe->ev_pyr_r, &fe->ev_pre, &fe->ev_fdone, &fe->ev_full_b[0], &fe->ev_full_b[1]})
+                              &fe->ev_pyr_r_b[0], &fe->ev_pyr_r_b[1], &fe->ev_pre, &fe->ev_fdone, &fe->ev_full_b[0],
+                              &fe->ev_full_b[1]})
             (void)hipEventCreateWithFlags(e, hipEventDisableTiming);
         fe->ev_full = fe->ev_full_b[0];
     }
@@ -996,8 +998,8 @@ void svo_frontend_destroy(svo_frontend* fe) {
     if (fe->zout) (void)hipHostFree(fe->zout);
     for (auto& e : fe->ev)
         if (e) (void)hipEventDestroy(e);
-    for (hipEvent_t e : {fe->ev_pyr, fe->ev_fast, fe->ev_lk, fe->ev_post, fe->ev_tail, fe->ev_stats, fe->ev_pyr_r,
-                         fe->ev_pre, fe->ev_fdone, fe->ev_full_b[0], fe->ev_full_b[1]})
+    for (hipEvent_t e : {fe->ev_pyr, fe->ev_fast, fe->ev_lk, fe->ev_post, fe->ev_tail, fe->ev_stats, fe->ev_pyr_r_b[0],
+                         fe->ev_pyr_r_b[1], fe->ev_pre, fe->ev_fdone, fe->ev_full_b[0], fe->ev_full_b[1]})
         if (e) (void)hipEventDestroy(e);
     if (fe->score_map) (void)hipFree(fe->score_map);
     delete fe;
@@ -1023,6 +1025,7 @@ static int fe_set_frame(svo_frontend* fe, int seq, int t, const uint8_t* left, c
     if (rd) return rd;
     if (fe->pyr_ready >= 0 && fe->pyr_ready % fe->T == t) fe->pyr_ready = -1;  // built from the old image
     if (fe->pre_t >= 0 && fe->pre_t % fe->T == t) fe->pre_t = -1;  // detected on the old image
+    if (fe->pyr_r_ready >= 0 && fe->pyr_r_ready % fe->T == t) fe->pyr_r_ready = -1;
     for (int side = 0; side < 2; side++) {
         svo_image* im = (side ? fe->frames_r : fe->frames)[(size_t)seq * fe->T + t];
         const uint8_t* px = side ? right : left;
@@ -1069,6 +1072,7 @@ int svo_frontend_init(svo_frontend* fe, int t0) {
     int rd = fe_drain(fe);
     if (rd) return rd;
     fe->pyr_ready = -1;
+    fe->pyr_r_ready = -1;
     fe->pre_t = -1;
     fe->fits_pending = false;
     fe->stats_pending = false;
@@ -1082,7 +1086,7 @@ int svo_frontend_init(svo_frontend* fe, int t0) {
                                                ctx->stream));
     SVO_HIP(ctx, launch_pyramid_batched(fe->d_desc_r + (size_t)(t0 % fe->T) * S, S, fe->W, fe->H, fe->nlev,
                                         ctx->stream));
-    SVO_HIP(ctx, hipEventRecord(fe->ev_pyr_r, ctx->stream));
+    SVO_HIP(ctx, hipEventRecord(fe->ev_pyr_r_b[t0 & 1], ctx->stream));
     SVO_HIP(ctx, hipMemsetAsync(fe->nA, 0, sizeof(int) * S, ctx->stream));
     SVO_HIP(ctx, hipMemsetAsync(fe->map_n, 0, sizeof(int) * S, ctx->stream));
     SVO_HIP(ctx, hipMemsetAsync(fe->pend_n, 0, sizeof(int) * S, ctx->stream));
@@ -1222,11 +1226,15 @@ static int fe_front(svo_frontend* fe, int t) {
         SVO_HIP(ctx, hipEventRecord(fe->ev_fdone, sf));
     }
     // 4. the right frame t's pyramid (no derivatives: it is the stereo LK's next
-    //    image), beside LK; the keyframe's stereo LK waits for ev_pyr_r
-    ph_begin(fe, PH_PYR_R, st0, &slot);
-    SVO_HIP(ctx, launch_pyramid_batched(fe->d_desc_r + (size_t)(t % fe->T) * S, S, fe->W, fe->H, fe->nlev, st0));
-    ph_end(fe, st0, slot);
-    SVO_HIP(ctx, hipEventRecord(fe->ev_pyr_r, st0));
+    //    image), normally built ahead in the previous step (6b); the stereo LK of
+    //    frame t waits for ev_pyr_r_b[t & 1]
+    if (fe->pyr_r_ready != t) {
+        ph_begin(fe, PH_PYR_R, st0, &slot);
+        SVO_HIP(ctx, launch_pyramid_batched(fe->d_desc_r + (size_t)(t % fe->T) * S, S, fe->W, fe->H, fe->nlev, st0));
+        ph_end(fe, st0, slot);
+        SVO_HIP(ctx, hipEventRecord(fe->ev_pyr_r_b[t & 1], st0));
+    }
+    fe->pyr_r_ready = -1;
     // 4b. early speculative stereo LK of frame t (fe_queue_spec), behind FAST(t)
     //     and this right pyramid
     if (fe->spec_early && fe->spec_margin >= 0 && fe->cfg.keyframe_rule == SVO_KF_EVERY) {
@@ -1253,6 +1261,15 @@ static int fe_front(svo_frontend* fe, int t) {
             int rc = fe_queue_pre(fe, tn);
             if (rc) return rc;
         }
+        // 6b. and frame t+1's right pyramid: ready when step t+1 begins, so its
+        //     speculative stereo LK can start right behind FAST(t+1) beside LK(t+1)
+        //     (built beside LK(t+1) instead, it was starved until LK's end)
+        ph_begin(fe, PH_PYR_R, st0, &slot);
+        SVO_HIP(ctx, launch_pyramid_batched(fe->d_desc_r + (size_t)(tn % fe->T) * S, S, fe->W, fe->H, fe->nlev,
+                                            st0));
+        ph_end(fe, st0, slot);
+        SVO_HIP(ctx, hipEventRecord(fe->ev_pyr_r_b[tn & 1], st0));
+        fe->pyr_r_ready = tn;
     }
     return SVO_OK;
 }
