@@ -93,6 +93,19 @@ class Pool {
         for (auto& t : th_) t.join();
     }
     int size() const { return (int)th_.size(); }
+    // a job without tasks: sleeping workers wake and every worker starts a new
+    // spin window, so a job expected shortly finds them hot (no futex wake-up)
+    void prime() {
+        if (th_.empty()) return;
+        const uint64_t g = gen_.load(std::memory_order_relaxed) + 1;
+        n_.store(0, std::memory_order_relaxed);
+        next_.store(g << 32, std::memory_order_release);
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            gen_.store(g, std::memory_order_release);
+        }
+        if (sleeping_.load(std::memory_order_acquire) > 0) cv_.notify_all();
+    }
     void run(int n, const std::function<void(int)>& fn) {
         if (th_.empty() || n <= 1) {
             for (int i = 0; i < n; i++) fn(i);
@@ -310,6 +323,7 @@ struct svo_frontend {
     bool spec_was_early = false;
     int lk_loss = 0;       // max over sequences of the last step's LK losses
     int ransac_drop = 0;   // max over sequences of the last step's RANSAC drops
+    double post_wait_ms = 0;  // running estimate of the host's wait for the post-LK results
     unsigned long long* fbits;
     uint8_t* status;
     double* map;
@@ -1347,7 +1361,24 @@ int svo_frontend_step(svo_frontend* fe, int t, svo_frontend_stats* stats) {
     // outliers (R:src/tracking.cpp:218-229), keyframe
     TP("ransac begin");
     auto tw = clk::now();
-    SVO_HIP(ctx, hipEventSynchronize(fe->ev_post));
+    {
+        // wait for the post-LK results, priming the pool (its workers sleep after
+        // an idle spin window, and a futex wake-up of 15 threads cost ~40 us on the
+        // critical path) shortly before they are predicted to land
+        const double lead_ms = fe->post_wait_ms - 0.08;
+        bool primed = false;
+        for (;;) {
+            const hipError_t q = hipEventQuery(fe->ev_post);
+            if (q == hipSuccess) break;
+            if (q != hipErrorNotReady) SVO_HIP(ctx, q);
+            if (!primed && ms_since(tw) >= lead_ms) {
+                fe->pool->prime();
+                primed = true;
+            }
+        }
+        const double w = ms_since(tw);
+        fe->post_wait_ms = fe->post_wait_ms > 0 ? 0.75 * fe->post_wait_ms + 0.25 * w : w;
+    }
     TP("lk results on host");
     ms_wait += ms_since(tw);
     // the speculative stereo LK went out early (fe_front) or with the post-LK (fe_post)
