@@ -242,7 +242,7 @@ def forward_workload(S, SceneForward, ctx, W, H, N, ML, Sq, K, Wm, threads):
             "steps": K, "warmup": Wm, "distinct_sequences": n_dist,
             "outlier_ratio": round(1 - tot["inliers"] / max(tot["tracked"], 1), 4),
             "stats_per_step": {k: round(v / K, 2) for k, v in tot.items()},
-            "scene": "SceneForward: 0.04 m/frame forward (ping-pong), occluder at 8 m sliding 18 px/frame"}
+            "scene": "SceneForward: 0.04 m/frame forward (ping-pong), occluder at 8 m sliding 22 px/frame"}
 
 
 def main():

@@ -125,12 +125,12 @@ class SceneForward(Scene):
     and the depth field comes within 3 m; and a textured rectangle in the world
     plane z = `occ_z` slides sideways at `occ_px` image pixels per frame against
     the static world, so the map points on it turn into RANSAC outliers as soon
-    as it has moved. Both views are rendered by svo_synth_view (the right camera
+    as it has moved (defaults: 8-26 % of the tracked points dropped per frame). Both views are rendered by svo_synth_view (the right camera
     is the left one shifted by the baseline along its x axis). Frame 0: R = I,
     C = 0 (the world frame is camera 0's, as the reference's first frame)."""
 
     def __init__(self, w: int, h: int, seed: int = 0, period: int = 16, speed: float = 0.04,
-                 occ_z: float = 8.0, occ_px: float = 18.0, occ_size=(0.20, 0.45), **kw):
+                 occ_z: float = 8.0, occ_px: float = 22.0, occ_size=(0.35, 0.60), **kw):
         super().__init__(w, h, seed=seed, period=period, **kw)
         self.speed, self.occ_z = speed, occ_z
         fx, fy = self.K[0, 0], self.K[1, 1]

@@ -62,9 +62,9 @@ def test_frontend_matches_oracle_loop(bucket, spec, monkeypatch):
 @pytest.mark.parametrize("early", ["1", "0"])
 def test_frontend_forward_occluder_matches_oracle_loop(early, monkeypatch):
     """The harder synthetic sequence (SceneForward: forward translation with
-    parallax, a textured occluder sliding 18 px per frame against the static world)
+    parallax, a textured occluder sliding 22 px per frame against the static world)
     on two sequences at once, step by step against the oracle loop: RANSAC now
-    drops 5-20 % of the tracked points per frame (more than the speculative stereo
+    drops 9-26 % of the tracked points per frame (more than the speculative stereo
     margin covers in some steps, so the serial keyframe path runs too), and the
     keyframes add several times more points than on the rotation-only scene.
     early: SVO_FE_SPEC_EARLY (the speculative stereo LK behind FAST(t) or behind
@@ -76,7 +76,7 @@ def test_frontend_forward_occluder_matches_oracle_loop(early, monkeypatch):
     fe = make_frontend(ctx, [SceneForward(W, H, seed=s) for s in seeds], T, N)
     fe.init(0)
     refs = [OracleLoop(SceneForward(W, H, seed=s), N).init(0) for s in seeds]
-    worst = 0.0
+    drops = []
     for t in range(1, T):
         st = fe.step(t).as_dict()
         rss = [r.step(t) for r in refs]
@@ -91,8 +91,8 @@ def test_frontend_forward_occluder_matches_oracle_loop(early, monkeypatch):
             R = O.rodrigues(rv)
             np.testing.assert_allclose(R, sc.R(t), atol=1e-2)
             np.testing.assert_allclose(-R.T @ tv, sc.C(t), atol=0.1)  # camera centre (m)
-        worst = max(worst, 1 - st["inliers"] / st["tracked"])
-    assert worst > 0.05, f"the occluder should make outliers (worst step {worst:.3f})"
+        drops.append(1 - st["inliers"] / st["tracked"])
+    assert np.mean(drops) > 0.08, f"the occluder should make 10-30 % outliers ({np.round(drops, 3)})"
 
 
 @pytest.mark.parametrize("bucket", [(0, 0), (50, 4)])
