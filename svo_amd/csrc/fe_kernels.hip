@@ -67,17 +67,88 @@ __device__ __forceinline__ int block_compact_fn(int n, Keep keep, Load load, flo
     return *base_s;
 }
 
+// The same compaction for an out-of-place output with at most kCompactChunks
+// chunks of BS: every chunk's keep test is issued up front (one bit per chunk per
+// thread), the (chunk, wave) counts go to LDS, ONE wave turns them into exclusive
+// offsets, then every kept entry is loaded and written -- two barriers instead of
+// three per chunk, and the chunks' global reads in flight together instead of one
+// chunk per barrier round (the post-LK / keyframe kernels sit on the step's
+// critical path, where each round trip is latency). cnt: >= kCompactChunks * BS / 64
+// ints of LDS.
+constexpr int kCompactChunks = 32;
+template <int BS, typename Keep, typename Load>
+__device__ __forceinline__ int block_compact_batched(int n, Keep keep, Load load, float* xy_out, int* mid_out,
+                                                     int* cnt, int* base_s) {
+    constexpr int NW = BS / 64;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int nch = (n + BS - 1) / BS;
+    unsigned flags = 0;
+    for (int c = 0; c < nch; c++) {
+        const int i = c * BS + tid;
+        const bool k = i < n && keep(i);
+        flags |= (unsigned)k << c;
+        const unsigned long long bal = __ballot(k);
+        if (lane == 0) cnt[c * NW + wv] = __popcll(bal);
+    }
+    __syncthreads();
+    if (wv == 0) {
+        // exclusive scan of the nch * NW counts (chunk-major, then wave), E per lane
+        constexpr int EMAX = (kCompactChunks * NW + 63) / 64;
+        const int ne = nch * NW, E = (ne + 63) / 64;
+        int v[EMAX];
+        int sum = 0;
+#pragma unroll
+        for (int e = 0; e < EMAX; e++) {
+            const int j = lane * E + e;
+            v[e] = e < E && j < ne ? cnt[j] : 0;
+            sum += v[e];
+        }
+        int inc = sum;  // inclusive wave scan of the lane sums
+        for (int o = 1; o < 64; o <<= 1) {
+            const int t = __shfl_up(inc, o);
+            if (lane >= o) inc += t;
+        }
+        int run = inc - sum;
+#pragma unroll
+        for (int e = 0; e < EMAX; e++) {
+            const int j = lane * E + e;
+            if (e < E && j < ne) cnt[j] = run;
+            run += v[e];
+        }
+        if (lane == 63) *base_s = inc;
+    }
+    __syncthreads();
+    for (int c = 0; c < nch; c++) {
+        const bool k = (flags >> c) & 1u;
+        const unsigned long long bal = __ballot(k);
+        if (k) {
+            const int i = c * BS + tid;
+            const int d = cnt[c * NW + wv] + __popcll(bal & ((1ull << lane) - 1ull));
+            float x, y;
+            int m;
+            load(i, x, y, m);
+            xy_out[2 * d] = x;
+            xy_out[2 * d + 1] = y;
+            mid_out[d] = m;
+        }
+    }
+    const int total = *base_s;
+    __syncthreads();  // cnt / base_s reusable
+    return total;
+}
+
+// in place (xy_in == xy_out) or beyond kCompactChunks chunks: the per-chunk form
 template <int BS, typename Keep>
 __device__ __forceinline__ int block_compact(int n, Keep keep, const float* xy_in, const int* mid_in, float* xy_out,
-                                             int* mid_out, int* wsum, int* base_s) {
-    return block_compact_fn<BS>(
-        n, keep,
-        [&](int i, float& x, float& y, int& m) {
-            x = xy_in[2 * i];
-            y = xy_in[2 * i + 1];
-            m = mid_in[i];
-        },
-        xy_out, mid_out, wsum, base_s);
+                                             int* mid_out, int* wsum, int* base_s, int* cnt = nullptr) {
+    auto load = [&](int i, float& x, float& y, int& m) {
+        x = xy_in[2 * i];
+        y = xy_in[2 * i + 1];
+        m = mid_in[i];
+    };
+    if (cnt && xy_in != xy_out && n <= kCompactChunks * BS)
+        return block_compact_batched<BS>(n, keep, load, xy_out, mid_out, cnt, base_s);
+    return block_compact_fn<BS>(n, keep, load, xy_out, mid_out, wsum, base_s);
 }
 
 // x mod n for 32-bit x, n >= 1, with a precomputed m = floor((2^32 - 1) / n)
@@ -115,6 +186,7 @@ __global__ __launch_bounds__(kPostBlock) void post_lk_kernel(PostLkBatch B) {
     __shared__ int base_s;
     __shared__ unsigned long long it_s;
     __shared__ int idx[5 * 64];
+    __shared__ int cnt[kCompactChunks * kPostBlock / 64];
     const int tid = threadIdx.x, lane = tid & 63;
     if (tid == 0) it_s = 0;
     finalize_body(B.pm, s);  // (ends with a barrier when it has work; it_s is set before the next one)
@@ -123,16 +195,20 @@ __global__ __launch_bounds__(kPostBlock) void post_lk_kernel(PostLkBatch B) {
     long long it = 0;
     for (int i = tid; i < n_in; i += kPostBlock) it += B.iters[o + i];
     const int n = block_compact<kPostBlock>(n_in, [&](int i) { return st[i] != 0; }, B.xy_in + 2 * o, B.mid_in + o,
-                                            B.xy_out + 2 * o, B.mid_out + o, wsum, &base_s);
+                                            B.xy_out + 2 * o, B.mid_out + o, wsum, &base_s, cnt);
     for (int off = 32; off > 0; off >>= 1) it += __shfl_xor(it, off);
     if (lane == 0) atomicAdd(&it_s, (unsigned long long)it);
     // lane 0 replays the RANSAC draws (they depend only on n) while the block
     // gathers the map points
     const bool draws = n > 5 && B.nh > 0 && B.nh <= 64;
     if (tid == 0 && draws) {
+        // the subset being drawn stays in registers (its duplicate tests were a
+        // chain of dependent LDS reads: ~260 per sequence on the critical path)
         const unsigned m = 0xFFFFFFFFu / (unsigned)n;
         uint64_t sr = ~0ull;
-        for (int j = 0; j < B.nh; j++)
+        for (int j = 0; j < B.nh; j++) {
+            int cur[5];
+#pragma unroll
             for (int i = 0; i < 5; i++) {
                 int v;
                 bool dup;
@@ -140,10 +216,14 @@ __global__ __launch_bounds__(kPostBlock) void post_lk_kernel(PostLkBatch B) {
                     sr = (uint64_t)(uint32_t)sr * 4164903690u + (uint32_t)(sr >> 32);
                     v = (int)fast_mod((uint32_t)sr, (unsigned)n, m);
                     dup = false;
-                    for (int k = 0; k < i; k++) dup |= idx[5 * j + k] == v;
+#pragma unroll
+                    for (int k = 0; k < i; k++) dup |= cur[k] == v;
                 } while (dup);
-                idx[5 * j + i] = v;
+                cur[i] = v;
             }
+#pragma unroll
+            for (int i = 0; i < 5; i++) idx[5 * j + i] = cur[i];
+        }
     }
     const int* __restrict__ mid = B.mid_out + o;
     const double* __restrict__ map = B.pm.map + 3 * (size_t)s * B.pm.map_cap;
@@ -180,12 +260,12 @@ __global__ __launch_bounds__(kPostBlock) void post_lk_kernel(PostLkBatch B) {
 // LK's input; a speculative prep already wrote them otherwise).
 template <int BS>
 __device__ __forceinline__ void tail_body(const TailBatch& T, int s, bool copy_cand, int* wsum, int* base_s,
-                                          int* n_kept, int* take_out) {
+                                          int* n_kept, int* take_out, int* cnt) {
     const size_t o = (size_t)s * T.cap;
     const uint32_t* __restrict__ bits = T.bits + (size_t)s * T.words_cap;
     const int n = block_compact<BS>(
         T.n_in[s], [&](int i) { return ((bits[i >> 5] >> (i & 31)) & 1u) != 0; }, T.xy_in + 2 * o, T.mid_in + o,
-        T.xy_out + 2 * o, T.mid_out + o, wsum, base_s);
+        T.xy_out + 2 * o, T.mid_out + o, wsum, base_s, cnt);
     // new-feature candidates of the keyframe: the first `take` masked corners
     int take = min(max(T.n_target[s] - n, 0), min(T.cand_n[s], T.cand_cap));
     take = min(take, T.cap - n);
@@ -208,8 +288,9 @@ __device__ __forceinline__ void tail_body(const TailBatch& T, int s, bool copy_c
 __global__ __launch_bounds__(kFeBlock) void tail_kernel(TailBatch T) {
     __shared__ int wsum[kFeBlock / 64];
     __shared__ int base_s;
+    __shared__ int cnt[kCompactChunks * kFeBlock / 64];
     int n, take;
-    tail_body<kFeBlock>(T, blockIdx.x, true, wsum, &base_s, &n, &take);
+    tail_body<kFeBlock>(T, blockIdx.x, true, wsum, &base_s, &n, &take, cnt);
 }
 
 // findLeftFeaturesInRight's filter + triangulateNewMapPoints + append for the
@@ -290,9 +371,10 @@ template <int BS>
 __global__ __launch_bounds__(BS) void keyframe_fused_kernel(TailBatch T, AppendBatch A) {
     __shared__ int wsum[BS / 64];
     __shared__ int base_s;
+    __shared__ int cnt[kCompactChunks * BS / 64];
     const int s = blockIdx.x;
     int n, take;
-    tail_body<BS>(T, s, false, wsum, &base_s, &n, &take);
+    tail_body<BS>(T, s, false, wsum, &base_s, &n, &take, cnt);
     append_body<BS>(A, s, n, take, wsum, &base_s);
 }
 
