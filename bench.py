@@ -406,6 +406,12 @@ def main():
         pyr_traffic = (c_lev - 1) * t_ps + t_ch if None not in (t_ps, t_ch) else None
         pyr_kernels = (f"pyr_scharr_kernel x {c_lev - 1} (pyrDown + Scharr + the source level's border) + "
                        "pyr_chain_kernel (last two levels, their derivatives and borders)")
+    # FAST detection (the pre-detection stage: FAST-9 + cornerScore + NMS, unmasked)
+    # of the last frame of every sequence, timed alone the same way; algorithmic
+    # bytes = one read of each W x H u8 frame (one raster pass)
+    fast_avg_s = fe.time_fast(Wm + K, 20) / 1e3 if hasattr(fe, "time_fast") else 0.0
+    fast_bytes = Sq * W * H
+    fast_traffic = pmc_traffic(args.config, "fast_detect_q_kernel")
     single = None
     if not args.no_single and world == 1:
         fe1 = S.Frontend(ctx, S.FrontendConfig(W, H, scenes[0].K, n_seq=1, n_frames=T, n_features=N, max_level=ML))
@@ -504,6 +510,18 @@ def main():
             "avg_launch_us": round(pyr_avg_s * 1e6, 3),
             "timing": "alone, 20 launches (HIP events on the launch stream)",
             "in_step_avg_launch_us": round(pyr_instep_s * 1e6, 3),
+        },
+        "roofline_fast": {
+            "kernel": f"fast_detect_q_kernel<32> (FAST-9 + cornerScore + NMS, 64x32 tiles), {Sq} frames per launch",
+            "bound": "hbm",
+            "achieved": round(fast_bytes / fast_avg_s / 1e9, 2) if fast_avg_s > 0 else 0.0,
+            "peak": HBM_PEAK_GBPS,
+            "unit": "GB/s",
+            "frac": round(fast_bytes / fast_avg_s / 1e9 / HBM_PEAK_GBPS, 4) if fast_avg_s > 0 else 0.0,
+            "traffic": fast_traffic,
+            "algorithmic_bytes_per_launch": fast_bytes,
+            "avg_launch_us": round(fast_avg_s * 1e6, 3),
+            "timing": "alone, 20 launches (HIP events on the launch stream; includes the row-count reset)",
         },
     }
     if not args.no_cpu_baseline and world == 1:  # rank 0 at N = 1 only

@@ -343,6 +343,11 @@ int svo_frontend_pyramid_level(svo_frontend* fe, int seq, int t, int right, int 
  * context stream: reps rebuilds (identical contents) after one warm-up, HIP
  * events around them; ms per chain. Synchronises the front end first. */
 int svo_frontend_time_pyramid(svo_frontend* fe, int t, int reps, double* ms_per_launch);
+/* The front end's FAST detection of frame t (every sequence; FAST-9 + cornerScore +
+ * NMS without the box mask, i.e. the pre-detection stage: extractFeatures' detector,
+ * R:src/tracking.cpp:82) timed alone the same way; ms per launch (row-count reset +
+ * detection kernel). Synchronises the front end first; the next step re-detects. */
+int svo_frontend_time_fast(svo_frontend* fe, int t, int reps, double* ms_per_launch);
 
 /* Host cores for a front end's RANSAC / pose-fit pool when several ranks (one
  * process per GPU) share a node: this process's allowed CPUs ordered by NUMA

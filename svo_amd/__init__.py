@@ -123,6 +123,7 @@ _SIGS = [
     ("svo_frontend_set_frame_bgr", C.c_int, [_vp, C.c_int, C.c_int, _u8p, _u8p, C.c_int]),
     ("svo_frontend_map_points", C.c_int, [_vp, C.c_int, _f64p, C.c_int, _i32p]),
     ("svo_frontend_time_pyramid", C.c_int, [_vp, C.c_int, C.c_int, _f64p]),
+    ("svo_frontend_time_fast", C.c_int, [_vp, C.c_int, C.c_int, _f64p]),
     ("svo_frontend_pyramid_level", C.c_int, [_vp, C.c_int, C.c_int, C.c_int, C.c_int, C.POINTER(C.c_uint8), C.c_int]),
     ("svo_frontend_scharr_level", C.c_int, [_vp, C.c_int, C.c_int, C.c_int, C.POINTER(C.c_int16),
                                             C.POINTER(C.c_int16), C.c_int]),
@@ -632,6 +633,12 @@ class Frontend:
         """ms per pyramid + Scharr launch chain of frame t, timed alone."""
         ms = np.zeros(1)
         self.ctx._check(lib().svo_frontend_time_pyramid(self.handle, int(t), int(reps), _p(ms, _f64p)))
+        return float(ms[0])
+
+    def time_fast(self, t, reps=20):
+        """ms per FAST detection launch (unmasked, every sequence) of frame t, timed alone."""
+        ms = np.zeros(1)
+        self.ctx._check(lib().svo_frontend_time_fast(self.handle, int(t), int(reps), _p(ms, _f64p)))
         return float(ms[0])
 
     def phase_times(self):

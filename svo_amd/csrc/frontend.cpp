@@ -1432,9 +1432,32 @@ int svo_frontend_step(svo_frontend* fe, int t, svo_frontend_stats* stats) {
             ms[s] = fe->rs[s].draw_chunk();
             for (int j = 0; j < ms[s]; j++) flat.push_back(s * kRansacChunk + j);
         }
-        fe->pool->run((int)flat.size(), [&](int k) {
-            fe->rs[flat[k] / kRansacChunk].solve(flat[k] % kRansacChunk, c.K);
-        });
+        if (tr) {
+            // per-task attribution (trace only): which threads ran the solves, how long each took
+            std::vector<std::pair<size_t, double>> tk(flat.size());
+            const auto tb = clk::now();
+            fe->pool->run((int)flat.size(), [&](int k) {
+                const auto a = clk::now();
+                fe->rs[flat[k] / kRansacChunk].solve(flat[k] % kRansacChunk, c.K);
+                tk[k] = {std::hash<std::thread::id>{}(std::this_thread::get_id()),
+                         std::chrono::duration<double, std::micro>(clk::now() - a).count()};
+                (void)tb;
+            });
+            std::vector<size_t> ids;
+            double sum = 0, mx = 0;
+            for (auto& e : tk) {
+                if (std::find(ids.begin(), ids.end(), e.first) == ids.end()) ids.push_back(e.first);
+                sum += e.second;
+                mx = std::max(mx, e.second);
+            }
+            std::fprintf(stderr, "[fe t=%d] pool: %zu solves on %zu threads, mean %.1f us, max %.1f us, wall %.1f us\n", t,
+                         tk.size(), ids.size(), tk.empty() ? 0.0 : sum / tk.size(), mx,
+                         std::chrono::duration<double, std::micro>(clk::now() - tb).count());
+        } else {
+            fe->pool->run((int)flat.size(), [&](int k) {
+                fe->rs[flat[k] / kRansacChunk].solve(flat[k] % kRansacChunk, c.K);
+            });
+        }
         for (int s = 0; s < S; s++) fe->rs[s].nh += ms[s];
         ms_hyp += ms_since(th);
         TP("hyps generated");
@@ -1704,6 +1727,34 @@ int svo_frontend_time_pyramid(svo_frontend* fe, int t, int reps, double* ms_per_
     (void)hipEventDestroy(e1);
     *ms_per_launch = ms / reps;
     fe->pyr_ready = -1;
+    return SVO_OK;
+}
+
+int svo_frontend_time_fast(svo_frontend* fe, int t, int reps, double* ms_per_launch) {
+    if (!fe || t < 0 || reps <= 0 || !ms_per_launch) return SVO_ERR_ARG;
+    int rc = svo_frontend_synchronize(fe);
+    if (rc) return rc;
+    svo_ctx* ctx = fe->ctx;
+    const PyrDesc* d = fe->d_desc + (size_t)(t % fe->T) * fe->S;
+    const FastDetBatch fb = fe_fast_batch(fe, d, false);
+    auto launch = [&]() {
+        return launch_fast_detect(fb, fe->S, fe->W, fe->H, fe->cfg.fast_threshold, fe->cfg.fast_nonmax, ctx->stream,
+                                  kFastDetect);
+    };
+    hipEvent_t e0, e1;
+    SVO_HIP(ctx, hipEventCreate(&e0));
+    SVO_HIP(ctx, hipEventCreate(&e1));
+    SVO_HIP(ctx, launch());  // warm-up
+    SVO_HIP(ctx, hipEventRecord(e0, ctx->stream));
+    for (int i = 0; i < reps; i++) SVO_HIP(ctx, launch());
+    SVO_HIP(ctx, hipEventRecord(e1, ctx->stream));
+    SVO_HIP(ctx, hipEventSynchronize(e1));
+    float ms = 0.f;
+    SVO_HIP(ctx, hipEventElapsedTime(&ms, e0, e1));
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    *ms_per_launch = ms / reps;
+    fe->pre_t = -1;  // the row words now hold frame t's unmasked detection, not a queued one
     return SVO_OK;
 }
 

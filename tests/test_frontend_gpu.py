@@ -236,3 +236,22 @@ def test_frontend_kitti_sequence_keeps_features():
     # init's keyframe + one per step (speculative), + a serial one for a step whose
     # RANSAC dropped more than the speculation covered
     assert T <= pt["stereo_lk"][1] <= 2 * T - 1
+
+
+def test_frontend_kernel_timers_leave_the_sequence_intact():
+    """svo_frontend_time_fast / svo_frontend_time_pyramid (bench.py's roofline legs)
+    between steps: they overwrite the FAST row words / a pyramid built ahead, and
+    the following steps still match the oracle loop (the pre-detection and the
+    pyramid are redone)."""
+    ctx = S.Context(0)
+    W, H, N, T = 640, 376, 800, 8
+    sc = Scene(W, H, seed=5)
+    fe = make_frontend(ctx, [sc], T, N)
+    fe.init(0)
+    ref = OracleLoop(Scene(W, H, seed=5), N).init(0)
+    for t in range(1, T):
+        st = fe.step(t).as_dict()
+        _compare_step(fe, ref, st, ref.step(t), t)
+        if t in (2, 4):
+            assert fe.time_fast(t + 1, 3) > 0
+            assert fe.time_pyramid(t + 1, 2) > 0

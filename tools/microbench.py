@@ -5,6 +5,7 @@
     python tools/microbench.py pyr --reps 20
     python tools/microbench.py fast --reps 20
     python tools/microbench.py fepyr --reps 20 --seq 64   (the front end's batched pyramid chain)
+    python tools/microbench.py fefast --reps 20 --seq 64  (the front end's batched FAST detection)
 """
 import argparse
 import os
@@ -20,7 +21,7 @@ from svo_amd.scene import Scene  # noqa: E402
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("what", choices=["lk", "pyr", "fast", "stereo", "fepyr"])
+    ap.add_argument("what", choices=["lk", "pyr", "fast", "stereo", "fepyr", "fefast"])
     ap.add_argument("--seq", type=int, default=64)
     ap.add_argument("--points", type=int, default=128000)
     ap.add_argument("--reps", type=int, default=5)
@@ -51,6 +52,16 @@ def main():
         for r in range(args.reps):
             ga.upload(A)
         print("pyr done")
+    elif args.what == "fefast":
+        cfg = S.FrontendConfig(args.w, args.h, sc.K, n_seq=args.seq, n_frames=2, n_features=2000, max_level=3)
+        fe = S.Frontend(ctx, cfg)
+        for s_ in range(args.seq):
+            sq = Scene(args.w, args.h, seed=s_)
+            fe.set_frame(s_, 0, sq.frame(0), sq.right(0))
+            fe.set_frame(s_, 1, sq.frame(1), sq.right(1))
+        for r in range(3):
+            ms = fe.time_fast(1, args.reps)
+            print(f"fefast {args.seq} x {args.w}x{args.h}: {ms * 1e3:.1f} us per launch")
     elif args.what == "fepyr":
         cfg = S.FrontendConfig(args.w, args.h, sc.K, n_seq=args.seq, n_frames=2, n_features=2000, max_level=3)
         fe = S.Frontend(ctx, cfg)
