@@ -252,7 +252,12 @@ def main():
     # RANSAC chunk predictions settle); every sequence frame is resident in HBM
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--seq", type=int, default=64, help="independent sequences per GPU (batched launches)")
+    # 128 independent sequences per GPU: the post-LK window (post-LK kernel, host
+    # EPnP, scoring, keyframe: ~0.23 ms, mostly latency) is paid once per step for the
+    # whole batch, so frames/s rises with the batch -- 64: 82.3k, 128: 92.3k, 192:
+    # 94.5k, 256: 95.6k on one box (profiles/r03_batch_curve.txt); 128 keeps a step at
+    # ~1.4 ms (each sequence still advances ~720 frames/s)
+    ap.add_argument("--seq", type=int, default=128, help="independent sequences per GPU (batched launches)")
     ap.add_argument("--config", default="kitti", choices=sorted(CONFIGS))
     ap.add_argument("--threads", type=int, default=0, help="host RANSAC threads (0 = auto)")
     ap.add_argument("--timing", type=int, default=2, choices=(0, 1, 2),

@@ -81,7 +81,7 @@ P
 }
 
 run_pmc() {
-    local tag=$1 cfg=$2 seq=${3:-64}
+    local tag=$1 cfg=$2 seq=${3:-128}
     local B="python bench.py --config $cfg --seq $seq --steps 10 --warmup 3 --no-cpu-baseline --no-single --no-bucketed --no-forward"
     rm -rf $O/pmc_fetch_$cfg $O/pmc_write_$cfg
     timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE -d $O/pmc_fetch_$cfg -o run --output-format csv -- $B \
@@ -222,7 +222,7 @@ run_round() {
     run_smoke
     run_prof "$tag"
     for c in kitti 1080p 4k; do
-        if [ $c = kitti ]; then run_pmc "$tag" $c 64; else run_pmc "$tag" $c 16; fi
+        if [ $c = kitti ]; then run_pmc "$tag" $c 128; else run_pmc "$tag" $c 16; fi
     done
     run_mix "$tag"
     run_bench "$tag" --steps 50 --warmup 10
