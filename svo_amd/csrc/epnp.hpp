@@ -57,11 +57,9 @@ class EPnP {
             rho[i] = (a[0] - b[0]) * (a[0] - b[0]) + (a[1] - b[1]) * (a[1] - b[1]) + (a[2] - b[2]) * (a[2] - b[2]);
         }
         double betas[4][4] = {{0}}, err[4] = {0}, Rs[4][9], ts[4][3];
-        for (int k = 1; k <= 3; k++) {
-            betas_approx(k, L, rho, betas[k]);
-            gauss_newton(L, rho, betas[k]);
-            err[k] = r_and_t(ut, betas[k], Rs[k], ts[k]);
-        }
+        for (int k = 1; k <= 3; k++) betas_approx(k, L, rho, betas[k]);
+        gauss_newton3(L, rho, betas);
+        r_and_t3(ut, betas, Rs, ts, err);
         int N = 1;
         if (err[2] < err[1]) N = 2;
         if (err[3] < err[N]) N = 3;
@@ -141,19 +139,29 @@ class EPnP {
     // least-squares solution up to rounding, which the 5 Gauss-Newton steps then
     // refine (measured: the same models as an SVD solve on 600 RANSAC subsets,
     // same speed; the device solver, epnp_wave.hpp, mirrors this one bit for bit).
-    SVO_HD static void lstsq_qr(const double* A, int nc, const double* rho, double* x) {
-        double Aq[30], bq[6];
-        for (int i = 0; i < 6 * nc; i++) Aq[i] = A[i];
+    template <int NC>
+    SVO_HD static void lstsq_qr(const double* A, const double* rho, double* x) {
+        double Aq[6 * NC], bq[6];
+        for (int i = 0; i < 6 * NC; i++) Aq[i] = A[i];
         for (int i = 0; i < 6; i++) bq[i] = rho[i];
-        qr_solve(Aq, 6, nc, bq, x);
+        qr_solve<6, NC>(Aq, bq, x);
+    }
+    // approximations 2 (NC = 3) and 3 (NC = 5): the first NC columns of L
+    template <int NC>
+    SVO_HD static void lstsq_L(const double* L, const double* rho, double* x) {
+        double A[6 * NC];
+        for (int i = 0; i < 6; i++)
+            for (int k = 0; k < NC; k++) A[NC * i + k] = L[10 * i + k];
+        lstsq_qr<NC>(A, rho, x);
     }
     SVO_HD static void betas_approx(int which, const double* L, const double* rho, double* b) {
         static const int cols1[4] = {0, 1, 3, 6};
-        double A[30], x[5];
+        double x[5];
         if (which == 1) {
+            double A[24];
             for (int i = 0; i < 6; i++)
                 for (int k = 0; k < 4; k++) A[4 * i + k] = L[10 * i + cols1[k]];
-            lstsq_qr(A, 4, rho, x);
+            lstsq_qr<4>(A, rho, x);
             const double sg = x[0] < 0 ? -1.0 : 1.0;
             b[0] = sqrt(sg * x[0]);
             b[1] = sg * x[1] / b[0];
@@ -161,10 +169,10 @@ class EPnP {
             b[3] = sg * x[3] / b[0];
             return;
         }
-        const int nc = which == 2 ? 3 : 5;
-        for (int i = 0; i < 6; i++)
-            for (int k = 0; k < nc; k++) A[nc * i + k] = L[10 * i + k];
-        lstsq_qr(A, nc, rho, x);
+        if (which == 2)
+            lstsq_L<3>(L, rho, x);
+        else
+            lstsq_L<5>(L, rho, x);
         if (x[0] < 0) {
             b[0] = sqrt(-x[0]);
             b[1] = (x[2] < 0) ? sqrt(-x[2]) : 0.0;
@@ -176,8 +184,10 @@ class EPnP {
         b[2] = which == 3 ? x[3] / b[0] : 0.0;
         b[3] = 0.0;
     }
-    SVO_HD static void qr_solve(double* A, int nr, int nc, double* b, double* X) {
-        double A1[8], A2[8];
+    // nr x nc (compile-time sizes: the loops unroll into registers)
+    template <int nr, int nc>
+    SVO_HD static void qr_solve(double* A, double* b, double* X) {
+        double A1[nc], A2[nc];
         for (int k = 0; k < nc; k++) {
             double eta = 0;
             for (int i = k; i < nr; i++) eta = fmax(eta, fabs(A[i * nc + k]));
@@ -216,6 +226,84 @@ class EPnP {
             X[i] = (b[i] - s) / A2[i];
         }
     }
+    // qr_solve of NS independent systems, interleaved column by column (each
+    // system's arithmetic and order exactly as qr_solve; the host core overlaps
+    // the NS dependency chains of divisions and square roots)
+    template <int nr, int nc, int NS>
+    SVO_HD static void qr_solve_n(double (*A)[nr * nc], double (*b)[nr], double (*X)[nc]) {
+        double A1[NS][nc], A2[NS][nc];
+        bool dead[NS];
+        for (int q = 0; q < NS; q++) dead[q] = false;
+        for (int k = 0; k < nc; k++)
+            for (int q = 0; q < NS; q++) {
+                if (dead[q]) continue;
+                double* a = A[q];
+                double eta = 0;
+                for (int i = k; i < nr; i++) eta = fmax(eta, fabs(a[i * nc + k]));
+                if (eta == 0) {
+                    for (int j = 0; j < nc; j++) X[q][j] = 0;
+                    dead[q] = true;
+                    continue;
+                }
+                double sum2 = 0.0;
+                const double ie = 1. / eta;
+                for (int i = k; i < nr; i++) {
+                    a[i * nc + k] *= ie;
+                    sum2 += a[i * nc + k] * a[i * nc + k];
+                }
+                double sigma = sqrt(sum2);
+                if (a[k * nc + k] < 0) sigma = -sigma;
+                a[k * nc + k] += sigma;
+                A1[q][k] = sigma * a[k * nc + k];
+                A2[q][k] = -eta * sigma;
+                for (int j = k + 1; j < nc; j++) {
+                    double sj = 0;
+                    for (int i = k; i < nr; i++) sj += a[i * nc + k] * a[i * nc + j];
+                    const double tau = sj / A1[q][k];
+                    for (int i = k; i < nr; i++) a[i * nc + j] -= tau * a[i * nc + k];
+                }
+            }
+        for (int j = 0; j < nc; j++)
+            for (int q = 0; q < NS; q++) {
+                if (dead[q]) continue;
+                double tau = 0;
+                for (int i = j; i < nr; i++) tau += A[q][i * nc + j] * b[q][i];
+                tau /= A1[q][j];
+                for (int i = j; i < nr; i++) b[q][i] -= tau * A[q][i * nc + j];
+            }
+        for (int q = 0; q < NS; q++)
+            if (!dead[q]) X[q][nc - 1] = b[q][nc - 1] / A2[q][nc - 1];
+        for (int i = nc - 2; i >= 0; i--)
+            for (int q = 0; q < NS; q++) {
+                if (dead[q]) continue;
+                double sx = 0;
+                for (int j = i + 1; j < nc; j++) sx += A[q][i * nc + j] * X[q][j];
+                X[q][i] = (b[q][i] - sx) / A2[q][i];
+            }
+    }
+    // gauss_newton of the three approximations (betas[1..3]) in lock step
+    SVO_HD static void gauss_newton3(const double* L, const double* rho, double (*betas)[4]) {
+        for (int it = 0; it < 5; it++) {
+            double A[3][24], b[3][6], x[3][4];
+            for (int q = 0; q < 3; q++) {
+                const double* be = betas[q + 1];
+                for (int i = 0; i < 6; i++) {
+                    const double* r = L + 10 * i;
+                    A[q][4 * i + 0] = 2 * r[0] * be[0] + r[1] * be[1] + r[3] * be[2] + r[6] * be[3];
+                    A[q][4 * i + 1] = r[1] * be[0] + 2 * r[2] * be[1] + r[4] * be[2] + r[7] * be[3];
+                    A[q][4 * i + 2] = r[3] * be[0] + r[4] * be[1] + 2 * r[5] * be[2] + r[8] * be[3];
+                    A[q][4 * i + 3] = r[6] * be[0] + r[7] * be[1] + r[8] * be[2] + 2 * r[9] * be[3];
+                    b[q][i] = rho[i] - (r[0] * be[0] * be[0] + r[1] * be[0] * be[1] + r[2] * be[1] * be[1] +
+                                        r[3] * be[0] * be[2] + r[4] * be[1] * be[2] + r[5] * be[2] * be[2] +
+                                        r[6] * be[0] * be[3] + r[7] * be[1] * be[3] + r[8] * be[2] * be[3] +
+                                        r[9] * be[3] * be[3]);
+                }
+            }
+            qr_solve_n<6, 4, 3>(A, b, x);
+            for (int q = 0; q < 3; q++)
+                for (int i = 0; i < 4; i++) betas[q + 1][i] += x[q][i];
+        }
+    }
     SVO_HD static void gauss_newton(const double* L, const double* rho, double* be) {
         for (int it = 0; it < 5; it++) {
             double A[24], b[6], x[4];
@@ -230,8 +318,75 @@ class EPnP {
                                  r[6] * be[0] * be[3] + r[7] * be[1] * be[3] + r[8] * be[2] * be[3] +
                                  r[9] * be[3] * be[3]);
             }
-            qr_solve(A, 6, 4, b, x);
+            qr_solve<6, 4>(A, b, x);
             for (int i = 0; i < 4; i++) be[i] += x[i];
+        }
+    }
+    // r_and_t of the three approximations (betas[1..3] -> Rs / ts / err[1..3]),
+    // their Procrustes SVDs in lock step (la::svd3_n); per approximation the same
+    // arithmetic in the same order as r_and_t
+    SVO_HD void r_and_t3(const double* ut, const double (*betas)[4], double (*Rs)[9], double (*ts)[3], double* err) {
+        double pcs[3][3 * kMaxPts], pc0[3][3], pw0[3] = {0, 0, 0}, abt[3][9];
+        for (int i = 0; i < n_; i++)
+            for (int j = 0; j < 3; j++) pw0[j] += pw_[3 * i + j];
+        for (int j = 0; j < 3; j++) pw0[j] /= n_;
+        for (int q = 0; q < 3; q++) {
+            const double* be = betas[q + 1];
+            double ccs[4][3] = {{0}};
+            for (int i = 0; i < 4; i++) {
+                const double* v = ut + 12 * (11 - i);
+                for (int j = 0; j < 4; j++)
+                    for (int k = 0; k < 3; k++) ccs[j][k] += be[i] * v[3 * j + k];
+            }
+            double* P = pcs[q];
+            for (int i = 0; i < n_; i++) {
+                const double* a = &alphas_[4 * i];
+                double* pc = &P[3 * i];
+                for (int j = 0; j < 3; j++)
+                    pc[j] = a[0] * ccs[0][j] + a[1] * ccs[1][j] + a[2] * ccs[2][j] + a[3] * ccs[3][j];
+            }
+            if (P[2] < 0.0)
+                for (int i = 0; i < 3 * n_; i++) P[i] = -P[i];
+            for (int j = 0; j < 3; j++) pc0[q][j] = 0;
+            for (int i = 0; i < n_; i++)
+                for (int j = 0; j < 3; j++) pc0[q][j] += P[3 * i + j];
+            for (int j = 0; j < 3; j++) pc0[q][j] /= n_;
+            for (int i = 0; i < 9; i++) abt[q][i] = 0;
+            for (int i = 0; i < n_; i++) {
+                const double* pc = &P[3 * i];
+                const double* pw = pw_ + 3 * i;
+                for (int j = 0; j < 3; j++)
+                    for (int k = 0; k < 3; k++) abt[q][3 * j + k] += (pc[j] - pc0[q][j]) * (pw[k] - pw0[k]);
+            }
+        }
+        double s[3][3], U[3][9], Vt[3][9];
+        la::svd3_n<3>(abt, s, U, Vt);
+        for (int q = 0; q < 3; q++) {
+            double* R = Rs[q + 1];
+            double* t = ts[q + 1];
+            const double* u = U[q];
+            const double* vt = Vt[q];
+            for (int i = 0; i < 3; i++)
+                for (int j = 0; j < 3; j++)
+                    R[3 * i + j] = u[3 * i] * vt[j] + u[3 * i + 1] * vt[3 + j] + u[3 * i + 2] * vt[6 + j];
+            const double det = R[0] * R[4] * R[8] + R[1] * R[5] * R[6] + R[2] * R[3] * R[7] - R[2] * R[4] * R[6] -
+                               R[1] * R[3] * R[8] - R[0] * R[5] * R[7];
+            if (det < 0) {
+                R[6] = -R[6];
+                R[7] = -R[7];
+                R[8] = -R[8];
+            }
+            for (int k = 0; k < 3; k++) t[k] = pc0[q][k] - dot3(R + 3 * k, pw0);
+            double sum = 0.0;
+            for (int i = 0; i < n_; i++) {
+                const double* pw = pw_ + 3 * i;
+                const double Xc = dot3(R, pw) + t[0], Yc = dot3(R + 3, pw) + t[1];
+                const double iz = 1.0 / (dot3(R + 6, pw) + t[2]);
+                const double ue = uc_ + fu_ * Xc * iz, ve = vc_ + fv_ * Yc * iz;
+                const double du = uv_[2 * i] - ue, dv = uv_[2 * i + 1] - ve;
+                sum += sqrt(du * du + dv * dv);
+            }
+            err[q + 1] = sum / n_;
         }
     }
     SVO_HD double r_and_t(const double* ut, const double* be, double* R, double* t) {

@@ -14,8 +14,12 @@ namespace la {
 
 // Cyclic Jacobi eigen-decomposition of a symmetric n x n (n <= 12) matrix A
 // (row-major, destroyed). Eigenvalues descending in w; eigenvector i in row i of V.
-SVO_HD void sym_eig(double* A, int n, double* w, double* V) {
-    double Q[144];
+// NC > 0: n = NC at compile time (the loops unroll; the same arithmetic in the
+// same order, bit-identical to the runtime-n form).
+template <int NC>
+SVO_HD void sym_eig_impl(double* A, int n_rt, double* w, double* V) {
+    const int n = NC > 0 ? NC : n_rt;
+    double Q[NC > 0 ? NC * NC : 144];
     for (int i = 0; i < n * n; i++) Q[i] = 0;
     for (int i = 0; i < n; i++) Q[i * n + i] = 1;
     for (int sweep = 0; sweep < 60; sweep++) {
@@ -51,7 +55,7 @@ SVO_HD void sym_eig(double* A, int n, double* w, double* V) {
                 }
             }
     }
-    int order[12];
+    int order[NC > 0 ? NC : 12];
     for (int i = 0; i < n; i++) order[i] = i;
     for (int i = 1; i < n; i++) {  // insertion sort, descending
         int v = order[i], j = i - 1;
@@ -65,6 +69,10 @@ SVO_HD void sym_eig(double* A, int n, double* w, double* V) {
         w[i] = A[order[i] * n + order[i]];
         for (int k = 0; k < n; k++) V[i * n + k] = Q[k * n + order[i]];
     }
+}
+SVO_HD void sym_eig(double* A, int n, double* w, double* V) {
+    if (n == 3) return sym_eig_impl<3>(A, 3, w, V);  // EPnP's control points
+    sym_eig_impl<0>(A, n, w, V);
 }
 
 // Symmetric eigen-decomposition by Householder tridiagonalisation and the
@@ -367,9 +375,12 @@ SVO_HD void sym_eig_ql(const double* A, int n, double* w, double* Vt) {
 }
 
 // One-sided Jacobi SVD of a (m x n, m <= 12, n <= 12): a = U diag(s) V^T,
-// s descending; U is m x n (columns), Vt is n x n (rows).
-SVO_HD void svd(const double* a, int m, int n, double* s, double* U, double* Vt) {
-    double W[144], V[144];
+// s descending; U is m x n (columns), Vt is n x n (rows). MC, NC > 0: the sizes
+// at compile time (unrolled, bit-identical to the runtime-size form).
+template <int MC, int NC>
+SVO_HD void svd_impl(const double* a, int m_rt, int n_rt, double* s, double* U, double* Vt) {
+    const int m = MC > 0 ? MC : m_rt, n = NC > 0 ? NC : n_rt;
+    double W[MC > 0 ? MC * NC : 144], V[NC > 0 ? NC * NC : 144];
     for (int i = 0; i < m * n; i++) W[i] = a[i];
     for (int i = 0; i < n * n; i++) V[i] = 0;
     for (int i = 0; i < n; i++) V[i * n + i] = 1;
@@ -401,8 +412,8 @@ SVO_HD void svd(const double* a, int m, int n, double* s, double* U, double* Vt)
             }
         if (!rotated) break;
     }
-    double nrm[12];
-    int order[12];
+    double nrm[NC > 0 ? NC : 12];
+    int order[NC > 0 ? NC : 12];
     for (int j = 0; j < n; j++) {
         double acc = 0;
         for (int k = 0; k < m; k++) acc += W[k * n + j] * W[k * n + j];
@@ -424,6 +435,87 @@ SVO_HD void svd(const double* a, int m, int n, double* s, double* U, double* Vt)
         if (U)
             for (int k = 0; k < m; k++) U[k * n + i] = nrm[c] > 0 ? W[k * n + c] / nrm[c] : 0;
     }
+}
+// svd_impl<3, 3> of NS independent matrices in lock step: each matrix's sweeps,
+// rotations and skips exactly as svd_impl (a matrix whose sweep rotated nothing
+// stops; the others go on), interleaved so that the host core overlaps the NS
+// dependency chains. U may be null.
+template <int NS>
+SVO_HD void svd3_n(const double (*a)[9], double (*s)[3], double (*U)[9], double (*Vt)[9]) {
+    constexpr int m = 3, n = 3;
+    double W[NS][9], V[NS][9];
+    bool done[NS];
+    for (int q = 0; q < NS; q++) {
+        for (int i = 0; i < 9; i++) W[q][i] = a[q][i];
+        for (int i = 0; i < 9; i++) V[q][i] = 0;
+        for (int i = 0; i < n; i++) V[q][i * n + i] = 1;
+        done[q] = false;
+    }
+    for (int sweep = 0; sweep < 60; sweep++) {
+        bool rotated[NS], any = false;
+        for (int q = 0; q < NS; q++) rotated[q] = false;
+        for (int p = 0; p < n - 1; p++)
+            for (int r = p + 1; r < n; r++)
+                for (int q = 0; q < NS; q++) {
+                    if (done[q]) continue;
+                    double al = 0, be = 0, ga = 0;
+                    for (int k = 0; k < m; k++) {
+                        al += W[q][k * n + p] * W[q][k * n + p];
+                        be += W[q][k * n + r] * W[q][k * n + r];
+                        ga += W[q][k * n + p] * W[q][k * n + r];
+                    }
+                    if (ga == 0 || fabs(ga) <= 1e-15 * sqrt(al * be)) continue;
+                    rotated[q] = true;
+                    const double z = (be - al) / (2 * ga);
+                    const double t = (z >= 0 ? 1.0 : -1.0) / (fabs(z) + sqrt(1 + z * z));
+                    const double c = 1 / sqrt(1 + t * t), sn = c * t;
+                    for (int k = 0; k < m; k++) {
+                        const double x = W[q][k * n + p], y = W[q][k * n + r];
+                        W[q][k * n + p] = c * x - sn * y;
+                        W[q][k * n + r] = sn * x + c * y;
+                    }
+                    for (int k = 0; k < n; k++) {
+                        const double x = V[q][k * n + p], y = V[q][k * n + r];
+                        V[q][k * n + p] = c * x - sn * y;
+                        V[q][k * n + r] = sn * x + c * y;
+                    }
+                }
+        for (int q = 0; q < NS; q++) {
+            if (!rotated[q]) done[q] = true;
+            any = any || !done[q];
+        }
+        if (!any) break;
+    }
+    for (int q = 0; q < NS; q++) {
+        double nrm[3];
+        int order[3];
+        for (int j = 0; j < n; j++) {
+            double acc = 0;
+            for (int k = 0; k < m; k++) acc += W[q][k * n + j] * W[q][k * n + j];
+            nrm[j] = sqrt(acc);
+            order[j] = j;
+        }
+        for (int i = 1; i < n; i++) {
+            int v = order[i], j = i - 1;
+            while (j >= 0 && nrm[order[j]] < nrm[v]) {
+                order[j + 1] = order[j];
+                j--;
+            }
+            order[j + 1] = v;
+        }
+        for (int i = 0; i < n; i++) {
+            const int c = order[i];
+            s[q][i] = nrm[c];
+            for (int k = 0; k < n; k++) Vt[q][i * n + k] = V[q][k * n + c];
+            if (U)
+                for (int k = 0; k < m; k++) U[q][k * n + i] = nrm[c] > 0 ? W[q][k * n + c] / nrm[c] : 0;
+        }
+    }
+}
+
+SVO_HD void svd(const double* a, int m, int n, double* s, double* U, double* Vt) {
+    if (m == 3 && n == 3) return svd_impl<3, 3>(a, 3, 3, s, U, Vt);  // Procrustes, pinv3, rotations
+    svd_impl<0, 0>(a, m, n, s, U, Vt);
 }
 
 // Least squares x = pinv(A) b (m x n, m <= 12, n <= 12), as cv::solve(DECOMP_SVD).
