@@ -4,6 +4,7 @@
 // DLT triangulation, new map points). One launch covers every sequence of the
 // batch (blockIdx = sequence), so a frame step costs the same number of
 // launches for 1 or 512 sequences.
+#include <algorithm>
 #include <cstdlib>
 
 #include "dlt.hpp"
@@ -293,9 +294,25 @@ __global__ __launch_bounds__(kFeBlock) void tail_kernel(TailBatch T) {
     tail_body<kFeBlock>(T, blockIdx.x, true, wsum, &base_s, &n, &take, cnt);
 }
 
+// findLeftFeaturesInRight's filter + triangulateNewMapPoints for one stereo match:
+// keep = status && |yR - yL| < y_threshold (float) && p.z > 0 (x3: the point in the
+// left camera frame)
+__device__ __forceinline__ bool stereo_point(const float* P, float y_threshold, bool status, float xl, float yl,
+                                             float xr, float yr, float (&x3)[3]) {
+    bool keep = status && fabsf(yr - yl) < y_threshold;
+    if (keep) {
+        float h[4];
+        dlt_point(P, xl, yl, xr, yr, h);
+        dlt_euclidean(h, x3);
+        keep = x3[2] > 0.f;  // triangulateNewMapPoints: p_w.z > 0
+    }
+    return keep;
+}
+
 // findLeftFeaturesInRight's filter + triangulateNewMapPoints + append for the
 // stereo matches of st_xy[0, take) of sequence s, n0 features already kept.
-template <int BS>
+// PRE: the filter and the points come from stereo_tri_kernel (A.st_X).
+template <int BS, bool PRE>
 __device__ __forceinline__ void append_body(const AppendBatch& A, int s, int n0, int take, int* wsum, int* base_sp) {
     int& base_s = *base_sp;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
@@ -311,14 +328,15 @@ __device__ __forceinline__ void append_body(const AppendBatch& A, int s, int n0,
         if (j < take) {
             xl = A.st_xy[2 * (o + j)];
             yl = A.st_xy[2 * (o + j) + 1];
-            const float xr = A.st_next[2 * (o + j)], yr = A.st_next[2 * (o + j) + 1];
-            // findLeftFeaturesInRight: status && |yR - yL| < y_threshold (float)
-            keep = A.st_status[o + j] != 0 && fabsf(yr - yl) < A.y_threshold;
-            if (keep) {
-                float h[4];
-                dlt_point(A.P, xl, yl, xr, yr, h);
-                dlt_euclidean(h, x3);
-                keep = x3[2] > 0.f;  // triangulateNewMapPoints: p_w.z > 0
+            if (PRE) {
+                const float4 v = A.st_X[o + j];
+                x3[0] = v.x;
+                x3[1] = v.y;
+                x3[2] = v.z;
+                keep = v.w != 0.f;
+            } else {
+                keep = stereo_point(A.P, A.y_threshold, A.st_status[o + j] != 0, xl, yl, A.st_next[2 * (o + j)],
+                                    A.st_next[2 * (o + j) + 1], x3);
             }
         }
         const unsigned long long bal = __ballot(keep);
@@ -364,7 +382,7 @@ __global__ __launch_bounds__(BS) void append_kernel(AppendBatch A) {
     __shared__ int wsum[BS / 64];
     __shared__ int base_s;
     const int s = blockIdx.x;
-    append_body<BS>(A, s, A.n[s], A.st_n[s], wsum, &base_s);
+    append_body<BS, false>(A, s, A.n[s], A.st_n[s], wsum, &base_s);
 }
 
 template <int BS>
@@ -375,7 +393,20 @@ __global__ __launch_bounds__(BS) void keyframe_fused_kernel(TailBatch T, AppendB
     const int s = blockIdx.x;
     int n, take;
     tail_body<BS>(T, s, false, wsum, &base_s, &n, &take, cnt);
-    append_body<BS>(A, s, n, take, wsum, &base_s);
+    append_body<BS, true>(A, s, n, take, wsum, &base_s);
+}
+
+__global__ __launch_bounds__(256) void stereo_tri_kernel(StereoTriBatch B) {
+    const int s = blockIdx.y;
+    const int n = B.spec_n[s];
+    const size_t o = (size_t)s * B.cap;
+    for (int j = blockIdx.x * 256 + threadIdx.x; j < n; j += gridDim.x * 256) {
+        const float xl = B.st_xy[2 * (o + j)], yl = B.st_xy[2 * (o + j) + 1];
+        float x3[3] = {0.f, 0.f, 0.f};
+        const bool keep = stereo_point(B.P, B.y_threshold, B.st_status[o + j] != 0, xl, yl, B.st_next[2 * (o + j)],
+                                       B.st_next[2 * (o + j) + 1], x3);
+        B.st_X[o + j] = make_float4(x3[0], x3[1], x3[2], keep ? 1.f : 0.f);
+    }
 }
 
 __global__ __launch_bounds__(kFeBlock) void stereo_prep_kernel(StereoPrepBatch B) {
@@ -416,6 +447,12 @@ hipError_t launch_append(const AppendBatch& b, int nseq, hipStream_t st) {
 
 hipError_t launch_keyframe_fused(const TailBatch& tb, const AppendBatch& ab, int nseq, hipStream_t st) {
     hipLaunchKernelGGL(keyframe_fused_kernel<kAppendBlock>, dim3(nseq), dim3(kAppendBlock), 0, st, tb, ab);
+    return hipGetLastError();
+}
+
+hipError_t launch_stereo_tri(const StereoTriBatch& b, int nseq, int max_n, hipStream_t st) {
+    const int gx = std::max(1, std::min((max_n + 255) / 256, 64));
+    hipLaunchKernelGGL(stereo_tri_kernel, dim3(gx, nseq), dim3(256), 0, st, b);
     return hipGetLastError();
 }
 

@@ -308,6 +308,7 @@ struct svo_frontend {
     float *xyA, *next_xy, *xyB, *obj, *kps, *cand, *box_binned;
     float *st_xy, *st_next;  // keyframe candidates (left) and their stereo LK matches (right)
     uint8_t* st_status;
+    float4* st_X;  // stereo_tri_kernel's points of the speculative candidates
     int* box_band;
     int *midA, *midB, *nA, *nB, *iters, *kn, *bn, *map_n, *rowcnt, *rowoff, *scr, *added, *st_n;
     int *pend0, *pend_n;  // PendingMap ranges
@@ -586,6 +587,7 @@ int fe_keyframe(svo_frontend* fe, int t, const int* n_in, const uint32_t* bits, 
     ab.added = fe->added;
     ab.h_n = fe->h_nA;
     ab.h_added = fe->h_added;
+    ab.st_X = fe->st_X;
     if (spec) {
         ph_begin(fe, PH_TAIL, st, &slot);
         SVO_HIP(ctx, launch_keyframe_fused(tb, ab, fe->S, st));
@@ -646,6 +648,17 @@ int fe_queue_spec(svo_frontend* fe, int t, bool early) {
     const int hint = std::min(fe->CAP, c.n_features - fe->min_tracked + margin + 32);
     int rc = fe_stereo_lk(fe, t, fe->spec_n, max_spec, sf, hint);
     if (rc) return rc;
+    StereoTriBatch tb;
+    tb.st_xy = fe->st_xy;
+    tb.st_next = fe->st_next;
+    tb.st_status = fe->st_status;
+    tb.spec_n = fe->spec_n;
+    tb.cap = fe->CAP;
+    tb.y_threshold = c.y_threshold;
+    std::memcpy(tb.P, c.P_left, sizeof(float) * 12);
+    std::memcpy(tb.P + 12, c.P_right, sizeof(float) * 12);
+    tb.st_X = fe->st_X;
+    SVO_HIP(ctx, launch_stereo_tri(tb, fe->S, hint, sf));
     SVO_HIP(ctx, hipEventRecord(fe->ev_fast, sf));
     fe->spec_t = t;
     fe->spec_m = margin;
@@ -803,6 +816,7 @@ int svo_frontend_create(svo_ctx* ctx, const svo_frontend_config* cfg, svo_fronte
         fe->st_xy = carve<float>(p, 2 * (size_t)S * CAP);
         fe->st_next = carve<float>(p, 2 * (size_t)S * CAP);
         fe->st_status = carve<uint8_t>(p, (size_t)S * CAP);
+        fe->st_X = carve<float4>(p, (size_t)S * CAP);
         fe->st_n = carve<int>(p, S);
         fe->pend0 = carve<int>(p, S);
         fe->pend_n = carve<int>(p, S);
@@ -1170,7 +1184,17 @@ static int fe_post(svo_frontend* fe, int t) {
 // FAST, the right pyramid of frame t and frame t+1's left pyramid.
 // svo_frontend_step enqueues the next step's first half right after its own
 // keyframe, so the GPU goes on with LK while the caller is between steps.
+// Split in two so that the step can put the next LK on the GPU right behind its
+// keyframe (fe_front_lk) before the side work's launches (fe_front_rest).
+static int fe_front_lk(svo_frontend* fe, int t);
+static int fe_front_rest(svo_frontend* fe, int t);
+static int fe_queue_next_image(svo_frontend* fe, int tn);
 static int fe_front(svo_frontend* fe, int t) {
+    int rc = fe_front_lk(fe, t);
+    return rc ? rc : fe_front_rest(fe, t);
+}
+
+static int fe_front_lk(svo_frontend* fe, int t) {
     svo_ctx* ctx = fe->ctx;
     hipStream_t st0 = ctx->stream;
     const int S = fe->S;
@@ -1191,9 +1215,6 @@ static int fe_front(svo_frontend* fe, int t) {
     {
         int rq = fe_queue_stats(fe);
         if (rq) return rq;
-        if (!fe->boxes_binned)
-            SVO_HIP(ctx, launch_box_bin(fe_fast_batch(fe, dcur, true), S, fe->W, fe->H, fe->st_fast));
-        fe->boxes_binned = false;
     }
     // 1. pyramid of frame t and its Scharr derivative pyramid (used when frame
     //    t is the prev image of the next step; OpenCV recomputes it per call),
@@ -1219,6 +1240,18 @@ static int fe_front(svo_frontend* fe, int t) {
         ph_end(fe, sl, slot);
         SVO_HIP(ctx, hipEventRecord(fe->ev_lk, sl));
     }
+    return SVO_OK;
+}
+
+static int fe_front_rest(svo_frontend* fe, int t) {
+    svo_ctx* ctx = fe->ctx;
+    hipStream_t st0 = ctx->stream;
+    const int S = fe->S;
+    const PyrDesc* dcur = fe->d_desc + (size_t)(t % fe->T) * S;
+    int slot;
+    if (!fe->boxes_binned)
+        SVO_HIP(ctx, launch_box_bin(fe_fast_batch(fe, dcur, true), S, fe->W, fe->H, fe->st_fast));
+    fe->boxes_binned = false;
     // 3. mask around frame t-1's features (the reference masks with prevFrame's
     //    features, R:src/tracking.cpp:77) + FAST/bucket on frame t, whole batch:
     //    independent of this step's LK and pose, so it is queued right behind the
@@ -1260,8 +1293,18 @@ static int fe_front(svo_frontend* fe, int t) {
     //    derivative pyramids are triple-buffered (frame f in f % 3), so nothing
     //    this step reads is overwritten, and the memory-bound pyramid shares the
     //    GPU with the VALU-bound LK instead of the post-LK window
-    if (t + 1 < fe->T) {
-        const int tn = t + 1;
+    if (t + 1 < fe->T) return fe_queue_next_image(fe, t + 1);
+    return SVO_OK;
+}
+
+// Frame tn's left pyramid, its FAST pre-detection and its right pyramid on the
+// context stream (steps 5-6b of the first half of step tn - 1).
+static int fe_queue_next_image(svo_frontend* fe, int tn) {
+    svo_ctx* ctx = fe->ctx;
+    hipStream_t st0 = ctx->stream;
+    const int S = fe->S;
+    int slot;
+    {
         const PyrDesc* dnext = fe->d_desc + (size_t)(tn % fe->T) * S;
         ph_begin(fe, PH_PYR, st0, &slot);
         SVO_HIP(ctx, launch_pyramid_scharr_batched(dnext, fe->d_der + (size_t)(tn % 3) * S, S, fe->W, fe->H,
@@ -1569,16 +1612,21 @@ int svo_frontend_step(svo_frontend* fe, int t, svo_frontend_stats* stats) {
         lk_its += fe->h_itsum[s];
         tracked += fe->h_nB[s];
     }
-    // the binning of these features as the next frame's mask boxes, on the FAST
-    // stream ahead of the next step's FAST (queued with its LK)
-    SVO_HIP(ctx, launch_box_bin(fe_fast_batch(fe, dcur, true), S, fe->W, fe->H, sf));
-    fe->boxes_binned = true;
     rc = fe_queue_stats(fe);
     if (rc) return rc;
     // the next step's first half goes out now, behind this step's keyframe, so
-    // the GPU moves on to its LK while the host returns to the caller
+    // the GPU moves on to its LK while the host returns to the caller: its LK
+    // first (the keyframe -> LK hand-off is on the critical path), then the
+    // binning of these features as the next frame's mask boxes (FAST stream,
+    // ahead of the next step's FAST) and the rest of the first half
     if (t + 1 < fe->T) {
-        rc = fe_front(fe, t + 1);
+        rc = fe_front_lk(fe, t + 1);
+        if (rc) return rc;
+    }
+    SVO_HIP(ctx, launch_box_bin(fe_fast_batch(fe, dcur, true), S, fe->W, fe->H, sf));
+    fe->boxes_binned = true;
+    if (t + 1 < fe->T) {
+        rc = fe_front_rest(fe, t + 1);
         if (rc) return rc;
         fe->front_t = t + 1;
     }

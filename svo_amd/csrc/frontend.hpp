@@ -100,6 +100,7 @@ struct AppendBatch {
     int* added;   // nullable
     int* h_n;     // nullable, host-coherent
     int* h_added; // nullable, host-coherent
+    const float4* st_X;  // keyframe_fused: stereo_tri_kernel's filter + DLT of st_xy[0, spec_n) (x, y, z, keep)
 };
 hipError_t launch_append(const AppendBatch& b, int nseq, hipStream_t st);
 
@@ -123,6 +124,23 @@ struct StereoPrepBatch {
     int* spec_n;
 };
 hipError_t launch_stereo_prep(const StereoPrepBatch& b, int nseq, hipStream_t st);
+
+// findLeftFeaturesInRight's filter + triangulateNewMapPoints' DLT and z > 0 test of
+// the speculative candidates st_xy[0, spec_n[s]) right behind their stereo LK (a
+// candidate's point depends only on its own match and the fixed stereo
+// projections), so the keyframe on the step's critical path only compacts and
+// appends: st_X[s][j] = (x, y, z, keep) in the left camera frame.
+struct StereoTriBatch {
+    const float* st_xy;
+    const float* st_next;
+    const uint8_t* st_status;
+    const int* spec_n;
+    int cap;
+    float y_threshold;
+    float P[24];  // P_left, P_right
+    float4* st_X;
+};
+hipError_t launch_stereo_tri(const StereoTriBatch& b, int nseq, int max_n, hipStream_t st);
 
 // tail_kernel + append_kernel in one launch, for a step whose speculative stereo
 // LK covered every sequence's take (st_next / st_status already hold the matches
