@@ -277,8 +277,11 @@ namespace {
 constexpr int FS_IW = 2 * PD_TX + 8;  // 136 staged columns: sx0 - 2 .. sx0 + 133 (dword aligned)
 constexpr int FS_IH = PD_IH;          // 36 rows
 
-// NT: the derivative and level stores as non-temporal (streaming) stores
-template <bool NT>
+// NT: the derivative and level stores as non-temporal (streaming) stores; SCH:
+// false = pyrDown (+ the source level's border) only, the right frames' pyramid
+// (the dword staging and packed row pass of this kernel, against the byte loads
+// of pyr_down_batched_kernel)
+template <bool NT, bool SCH = true>
 __global__ __launch_bounds__(256) void pyr_scharr_kernel(const PyrDesc* __restrict__ descs,
                                                          const DerivDesc* __restrict__ ders, int level, int pad_src) {
     const PyrDesc& P = descs[blockIdx.z];
@@ -322,7 +325,7 @@ __global__ __launch_bounds__(256) void pyr_scharr_kernel(const PyrDesc* __restri
     // ---- Scharr of level l pixels (2x0 + i, 2y0 + j), i < 128, j < 32: T[2 + j][4 + i];
     // a task: 4 columns x 4 rows from 3 aligned dwords per staged row, one 16-byte
     // store per row (columns >= sw are never written: the zero border stays) ----
-    {
+    if constexpr (SCH) {
         uint32_t* __restrict__ out = ders[blockIdx.z].data[level];
         const int op = ders[blockIdx.z].pitch[level];
         const int g = tid & 31, q = tid >> 5;
@@ -727,8 +730,9 @@ hipError_t launch_pyramid_batched(const PyrDesc* d_descs, int nseq, int w, int h
     for (int l = 1; l <= chain_start(c); l++) {
         lw = (lw + 1) / 2;
         lh = (lh + 1) / 2;
-        hipLaunchKernelGGL(pyr_down_batched_kernel, dim3((lw + PD_TX - 1) / PD_TX, (lh + PD_TY - 1) / PD_TY, nseq),
-                           dim3(256), 0, st, d_descs, l, 1);
+        hipLaunchKernelGGL((pyr_scharr_kernel<true, false>),
+                           dim3((lw + PD_TX - 1) / PD_TX, (lh + PD_TY - 1) / PD_TY, nseq), dim3(256), 0, st, d_descs,
+                           (const DerivDesc*)nullptr, l - 1, 1);
     }
     launch_chain_c<false>(c, d_descs, nullptr, nseq, w, h, st);
     return hipGetLastError();
