@@ -260,8 +260,9 @@ def main():
     ap.add_argument("--seq", type=int, default=128, help="independent sequences per GPU (batched launches)")
     ap.add_argument("--config", default="kitti", choices=sorted(CONFIGS))
     ap.add_argument("--threads", type=int, default=0, help="host RANSAC threads (0 = auto)")
-    ap.add_argument("--timing", type=int, default=2, choices=(0, 1, 2),
-                    help="phase events: 1 all phases, 2 only LK/pyramid/FAST (lighter host tail)")
+    ap.add_argument("--timing", type=int, default=2, choices=(1, 2, 3),
+                    help="phase events: 1 all phases, 2 only LK/pyramid/FAST (lighter host tail), "
+                         "3 the LK launches only (the roofline's)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-single", action="store_true")

@@ -269,7 +269,7 @@ typedef struct svo_frontend_config {
     double pnp_confidence;  /* -> 0.999 */
     double K[9];            /* camera matrix (float-rounded, as the Matx33f K) */
     int host_threads;       /* RANSAC host threads; 0 = auto */
-    int timing;             /* 1 = per-phase HIP events; 2 = only LK, pyramid, FAST */
+    int timing;             /* 1 = per-phase HIP events; 2 = only LK, pyramid, FAST; 3 = only LK */
     int keyframe_rule;      /* SVO_KF_EVERY (default) or SVO_KF_REFERENCE */
     int features_to_track;  /* SVO_KF_REFERENCE threshold, R:configs/config.yaml:15 -> 70 */
     /* stereo keyframe path (R:src/tracking.cpp:94-152) */

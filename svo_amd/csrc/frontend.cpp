@@ -426,6 +426,7 @@ void ph_begin(svo_frontend* fe, int ph, hipStream_t st, int* slot) {
     // timing 2: only the big phases (each event pair costs a few us of host time)
     if (fe->cfg.timing == 2 && ph != PH_LK && ph != PH_PYR && ph != PH_FAST && ph != PH_STEREO && ph != PH_PYR_R)
         return;
+    if (fe->cfg.timing == 3 && ph != PH_LK) return;  // timing 3: the LK launches only (the roofline's)
     const int sl = fe->ev_used;
     bool wrapped = false;  // ring wrapped onto a pair still in flight
     for (const auto& p : fe->pending) wrapped |= p.second == sl;
