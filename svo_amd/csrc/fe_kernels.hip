@@ -77,9 +77,16 @@ __device__ __forceinline__ int block_compact_fn(int n, Keep keep, Load load, flo
 // critical path, where each round trip is latency). cnt: >= kCompactChunks * BS / 64
 // ints of LDS.
 constexpr int kCompactChunks = 32;
-template <int BS, typename Keep, typename Load>
+struct NoHook {
+    __device__ void operator()(int) const {}
+    __device__ void operator()(int, int) const {}
+};
+// after_scan(total): every thread, once the kept count is known (before the
+// entries move); emit(d, m): per kept entry, after its move to rank d (mid m)
+template <int BS, typename Keep, typename Load, typename AfterScan = NoHook, typename Emit = NoHook>
 __device__ __forceinline__ int block_compact_batched(int n, Keep keep, Load load, float* xy_out, int* mid_out,
-                                                     int* cnt, int* base_s) {
+                                                     int* cnt, int* base_s, AfterScan after_scan = {},
+                                                     Emit emit = {}) {
     constexpr int NW = BS / 64;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int nch = (n + BS - 1) / BS;
@@ -119,6 +126,7 @@ __device__ __forceinline__ int block_compact_batched(int n, Keep keep, Load load
         if (lane == 63) *base_s = inc;
     }
     __syncthreads();
+    after_scan(*base_s);
     for (int c = 0; c < nch; c++) {
         const bool k = (flags >> c) & 1u;
         const unsigned long long bal = __ballot(k);
@@ -131,6 +139,7 @@ __device__ __forceinline__ int block_compact_batched(int n, Keep keep, Load load
             xy_out[2 * d] = x;
             xy_out[2 * d + 1] = y;
             mid_out[d] = m;
+            emit(d, m);
         }
     }
     const int total = *base_s;
@@ -180,6 +189,32 @@ __device__ __forceinline__ void finalize_body(const PendingMap& P, int s) {
 
 __global__ __launch_bounds__(kFeBlock) void finalize_map_kernel(PendingMap P) { finalize_body(P, blockIdx.x); }
 
+// RANSAC subset draws of sequence s (OpenCV's MWC RNG; they depend only on n),
+// one thread, the subset being drawn in registers (its duplicate tests were a
+// chain of dependent LDS reads: ~260 per sequence on the critical path)
+__device__ __forceinline__ void ransac_draws(int n, int nh, int* idx) {
+    const unsigned m = 0xFFFFFFFFu / (unsigned)n;
+    uint64_t sr = ~0ull;
+    for (int j = 0; j < nh; j++) {
+        int cur[5];
+#pragma unroll
+        for (int i = 0; i < 5; i++) {
+            int v;
+            bool dup;
+            do {
+                sr = (uint64_t)(uint32_t)sr * 4164903690u + (uint32_t)(sr >> 32);
+                v = (int)fast_mod((uint32_t)sr, (unsigned)n, m);
+                dup = false;
+#pragma unroll
+                for (int k = 0; k < i; k++) dup |= cur[k] == v;
+            } while (dup);
+            cur[i] = v;
+        }
+#pragma unroll
+        for (int i = 0; i < 5; i++) idx[5 * j + i] = cur[i];
+    }
+}
+
 __global__ __launch_bounds__(kPostBlock) void post_lk_kernel(PostLkBatch B) {
     const int s = blockIdx.x;
     const size_t o = (size_t)s * B.cap;
@@ -195,45 +230,48 @@ __global__ __launch_bounds__(kPostBlock) void post_lk_kernel(PostLkBatch B) {
     const uint8_t* __restrict__ st = B.status + o;
     long long it = 0;
     for (int i = tid; i < n_in; i += kPostBlock) it += B.iters[o + i];
-    const int n = block_compact<kPostBlock>(n_in, [&](int i) { return st[i] != 0; }, B.xy_in + 2 * o, B.mid_in + o,
-                                            B.xy_out + 2 * o, B.mid_out + o, wsum, &base_s, cnt);
-    for (int off = 32; off > 0; off >>= 1) it += __shfl_xor(it, off);
-    if (lane == 0) atomicAdd(&it_s, (unsigned long long)it);
-    // lane 0 replays the RANSAC draws (they depend only on n) while the block
-    // gathers the map points
-    const bool draws = n > 5 && B.nh > 0 && B.nh <= 64;
-    if (tid == 0 && draws) {
-        // the subset being drawn stays in registers (its duplicate tests were a
-        // chain of dependent LDS reads: ~260 per sequence on the critical path)
-        const unsigned m = 0xFFFFFFFFu / (unsigned)n;
-        uint64_t sr = ~0ull;
-        for (int j = 0; j < B.nh; j++) {
-            int cur[5];
-#pragma unroll
-            for (int i = 0; i < 5; i++) {
-                int v;
-                bool dup;
-                do {
-                    sr = (uint64_t)(uint32_t)sr * 4164903690u + (uint32_t)(sr >> 32);
-                    v = (int)fast_mod((uint32_t)sr, (unsigned)n, m);
-                    dup = false;
-#pragma unroll
-                    for (int k = 0; k < i; k++) dup |= cur[k] == v;
-                } while (dup);
-                cur[i] = v;
-            }
-#pragma unroll
-            for (int i = 0; i < 5; i++) idx[5 * j + i] = cur[i];
+    const double* __restrict__ map = B.pm.map + 3 * (size_t)s * B.pm.map_cap;
+    const bool nh_ok = B.nh > 0 && B.nh <= 64;
+    int n;
+    if (n_in <= kCompactChunks * kPostBlock) {
+        // the status compaction moves each kept entry and gathers its map point
+        // (one dependent round trip less than a separate gather pass); thread 0
+        // replays the RANSAC draws while the block moves the entries
+        const float* __restrict__ xy_in = B.xy_in + 2 * o;
+        const int* __restrict__ mid_in = B.mid_in + o;
+        float* __restrict__ obj = B.obj + 3 * o;
+        n = block_compact_batched<kPostBlock>(
+            n_in, [&](int i) { return st[i] != 0; },
+            [&](int i, float& x, float& y, int& m) {
+                x = xy_in[2 * i];
+                y = xy_in[2 * i + 1];
+                m = mid_in[i];
+            },
+            B.xy_out + 2 * o, B.mid_out + o, cnt, &base_s,
+            [&](int total) {
+                if (tid == 0 && total > 5 && nh_ok) ransac_draws(total, B.nh, idx);
+            },
+            [&](int d, int m) {
+                const double* X = map + 3 * (size_t)m;
+                obj[3 * d] = (float)X[0];
+                obj[3 * d + 1] = (float)X[1];
+                obj[3 * d + 2] = (float)X[2];
+            });
+    } else {
+        n = block_compact<kPostBlock>(n_in, [&](int i) { return st[i] != 0; }, B.xy_in + 2 * o, B.mid_in + o,
+                                      B.xy_out + 2 * o, B.mid_out + o, wsum, &base_s);
+        if (tid == 0 && n > 5 && nh_ok) ransac_draws(n, B.nh, idx);
+        const int* __restrict__ mid = B.mid_out + o;
+        for (int i = tid; i < n; i += kPostBlock) {
+            const double* X = map + 3 * (size_t)mid[i];
+            B.obj[3 * (o + i)] = (float)X[0];
+            B.obj[3 * (o + i) + 1] = (float)X[1];
+            B.obj[3 * (o + i) + 2] = (float)X[2];
         }
     }
-    const int* __restrict__ mid = B.mid_out + o;
-    const double* __restrict__ map = B.pm.map + 3 * (size_t)s * B.pm.map_cap;
-    for (int i = tid; i < n; i += kPostBlock) {
-        const double* X = map + 3 * (size_t)mid[i];
-        B.obj[3 * (o + i)] = (float)X[0];
-        B.obj[3 * (o + i) + 1] = (float)X[1];
-        B.obj[3 * (o + i) + 2] = (float)X[2];
-    }
+    for (int off = 32; off > 0; off >>= 1) it += __shfl_xor(it, off);
+    if (lane == 0) atomicAdd(&it_s, (unsigned long long)it);
+    const bool draws = n > 5 && nh_ok;
     __syncthreads();
     if (tid == 0) {
         B.n_out[s] = n;
@@ -241,15 +279,17 @@ __global__ __launch_bounds__(kPostBlock) void post_lk_kernel(PostLkBatch B) {
         B.h_iters[s] = (long long)it_s;
     }
     if (draws) {
+        // the subsets' points from the compacted arrays just written (obj holds
+        // (float) of the map point, as the separate gather did)
         const float* __restrict__ xy = B.xy_out + 2 * o;
+        const float* __restrict__ obj = B.obj + 3 * o;
         float* __restrict__ dst = B.h_samp + (size_t)25 * B.nh * s;
         for (int k = tid; k < 5 * B.nh; k += kPostBlock) {
             const int j = k / 5, i = k - 5 * j, p = idx[k];
-            const double* X = map + 3 * (size_t)mid[p];
             float* h = dst + 25 * j;
-            h[3 * i] = (float)X[0];
-            h[3 * i + 1] = (float)X[1];
-            h[3 * i + 2] = (float)X[2];
+            h[3 * i] = obj[3 * p];
+            h[3 * i + 1] = obj[3 * p + 1];
+            h[3 * i + 2] = obj[3 * p + 2];
             h[15 + 2 * i] = xy[2 * p];
             h[15 + 2 * i + 1] = xy[2 * p + 1];
         }
