@@ -45,9 +45,14 @@ __device__ __forceinline__ int descale(int x, int n) { return (x + (1 << (n - 1)
 // only inside the 2^-20 band around it
 __device__ __forceinline__ bool converged(float dx, float dy, float lo, float hi, double eps2) {
     const float sf = dx * dx + dy * dy;
-    if (sf < lo) return true;
-    if (sf > hi) return false;
-    return (double)dx * dx + (double)dy * dy <= eps2;
+    bool c = sf < lo;
+    if (__builtin_expect(sf >= lo && sf <= hi, 0)) {
+        // (a real branch: if-converted, the double products cost every iteration of
+        // every wave ~10 VALU issue slots for a band no lane is in)
+        asm volatile("" ::: "memory");
+        c = (double)dx * dx + (double)dy * dy <= eps2;
+    }
+    return c;
 }
 // `std::abs(a + b) < 0.01` with a float sum promoted to double: the largest float
 // below 0.01 is the bound
