@@ -158,8 +158,15 @@ def pmc_traffic(cfg_name: str, kernel_prefix: str):  # substring of the demangle
     except (OSError, ValueError):
         return None
     for k, v in d.get("configs", {}).get(cfg_name, {}).get("kernels", {}).items():
-        if kernel_prefix in k and not (kernel_prefix == "scharr_kernel" and "pyr_scharr" in k):
-            return v.get("hbm_bytes_per_launch")
+        if kernel_prefix not in k or (kernel_prefix == "scharr_kernel" and "pyr_scharr" in k):
+            continue
+        # the left chain's kernels, not the right pyramid's instances of the same
+        # templates (pyr_scharr_kernel<NT, SCH = false>, pyr_chain_kernel<c, false, s>)
+        if kernel_prefix == "pyr_scharr_kernel" and ", false>" in k:
+            continue
+        if kernel_prefix == "pyr_chain_kernel" and ", false," in k:
+            continue
+        return v.get("hbm_bytes_per_launch")
     return None
 
 
