@@ -217,6 +217,25 @@ def cpu_baseline(cfg_name: str, seconds: float):
                               "sample": f"{n1} frames, {dt1:.1f} s, everything on one thread"}}
 
 
+def slowest_step(step_s, diag, warmup):
+    """The slowest timed step with the library's own account of it: host waits
+    split by what was waited for (post-LK results, RANSAC scoring rounds, the
+    keyframe), launch issue time, RANSAC rounds, the serial keyframe fallback
+    and the full point copy (svo_frontend_stats)."""
+    if not step_s:
+        return None
+    i = int(np.argmax(step_s))
+    d = diag[i]
+    keys = ("host_ms_step", "host_ms_wait_post", "host_ms_wait_score", "host_ms_wait_kf", "host_ms_enqueue",
+            "host_ms_hyp", "host_ms_fit", "ransac_rounds", "max_hypotheses", "hypotheses", "serial_keyframe",
+            "full_copy", "added", "tracked", "inliers")
+    out = {"index": i, "frame": warmup + 1 + i, "wall_ms": round(step_s[i] * 1e3, 3)}
+    out.update({k: (round(d[k], 3) if isinstance(d[k], float) else d[k]) for k in keys})
+    # the part of the step's wall time spent outside the library call (Python, ctypes)
+    out["outside_call_ms"] = round(step_s[i] * 1e3 - d["host_ms_step"], 3)
+    return out
+
+
 def forward_workload(S, SceneForward, ctx, W, H, N, ML, Sq, K, Wm, threads):
     """The harder sequence (svo_amd.scene.SceneForward: forward translation with
     parallax + a textured occluder sliding against the static world, 5-20 % RANSAC
@@ -224,7 +243,7 @@ def forward_workload(S, SceneForward, ctx, W, H, N, ML, Sq, K, Wm, threads):
     sequences per launch, Wm warm-up + K timed steps. 16 distinct sequences are
     rendered (the general renderer's host cost) and each fills Sq / 16 batch slots."""
     n_dist = min(Sq, 16)
-    T = Wm + K + 1
+    T = Wm + K + 2  # as the headline: the last timed step queues the next LK
     scs = [SceneForward(W, H, seed=1000 + i) for i in range(n_dist)]
     P = min(T, 2 * scs[0].period)
     pairs = [[(sc.frame(t), sc.right(t)) for t in range(P)] for sc in scs]
@@ -305,7 +324,11 @@ def main():
 
     W, H, N, ML, label = CONFIGS[args.config]
     Sq, K, Wm = args.seq, args.steps, args.warmup
-    T = Wm + K + 1
+    # frames 0 .. Wm + K + 1: the last timed step (Wm + K) queues the next step's
+    # first half (its LK) as every step does, so the timed window holds K steps'
+    # worth of work -- the LK of step Wm + 1, queued by the last warm-up step, runs
+    # at the window's start, and that of step Wm + K + 1 is waited for at its end
+    T = Wm + K + 2
     device = local
     if world > 1:
         # One rank per GPU; ranks beyond the visible devices (a multi-rank rehearsal on a
@@ -345,12 +368,20 @@ def main():
         host_cpus = []
     feats_after = {}  # features after step t = the inputs of LK(t + 1)
     for t in range(1, Wm + 1):
+        if t == Wm:
+            # the phase timers restart before the last warm-up step: resetting
+            # folds the pending event pairs, which waits for the GPU, so it must
+            # not sit between the warm-up and the timed window (the window would
+            # start on an idle GPU with LK(Wm + 1) already done)
+            fe.reset_times()
         st = fe.step(t).as_dict()
         feats_after[t] = st["features"]
-    fe.reset_times()
     tot = {"lk_iterations": 0, "tracked": 0, "inliers": 0, "added": 0, "hypotheses": 0,
-           "host_ms_hyp": 0.0, "host_ms_fit": 0.0, "host_ms_wait": 0.0}
+           "host_ms_hyp": 0.0, "host_ms_fit": 0.0, "host_ms_wait": 0.0, "host_ms_wait_post": 0.0,
+           "host_ms_wait_score": 0.0, "host_ms_wait_kf": 0.0, "host_ms_enqueue": 0.0, "ransac_rounds": 0,
+           "serial_keyframe": 0, "full_copy": 0}
     step_s = []  # host wall time of each timed step (a slow run shows whether one step or all were slow)
+    step_diag = []  # the library's per-step diagnostics of each timed step
     barrier(dist)
     t0 = time.perf_counter()
     tp = t0
@@ -361,6 +392,7 @@ def main():
         tp = now
         for k in tot:
             tot[k] += st[k]
+        step_diag.append(st)
         feats_after[t] = st["features"]
     fe.synchronize()  # the last step's pose fits / prefetched pyramid belong to the timed work
     barrier(dist)
@@ -374,14 +406,14 @@ def main():
     if rank != 0:
         return
     # roofline of the dominant kernel (by device time): LK. The event pairs folded
-    # after reset_times bracket the LK launches of the last lk_n timed steps
-    # (step Wm+1's LK went out during the warm-up); LK(t) tracks the features left
-    # after step t-1, so those launches processed feats_after[t-1] features each.
+    # since reset_times (before step Wm) bracket the LK launches of steps Wm + 1 ..
+    # Wm + K + 1 (each queued by the step before it); LK(t) tracks the features
+    # left after step t-1, so those launches processed feats_after[t-1] each.
     lk_ms, lk_n = phases["lk"]
     L = ML + 1
-    last = Wm + K
+    last = Wm + K + 1
     lk_units = sum(feats_after[t - 1] for t in range(last - lk_n + 1, last + 1)) if lk_n > 0 else 0
-    assert lk_n <= K, "LK launches timed do not match the steps"
+    assert lk_n <= K + 1, "LK launches timed do not match the steps"
     units_per_launch = lk_units / max(lk_n, 1)
     bytes_per_launch = units_per_launch * lk_bytes_per_feature(L)
     lk_avg_s = lk_ms / max(lk_n, 1) / 1e3
@@ -492,8 +524,11 @@ def main():
         "workloads": {"forward": forward},
         "phase_ms_per_step": {k: round(v[0] / K, 4) for k, v in phases.items()},
         "stats_per_step": {k: round(v / K, 3) for k, v in tot.items()},
-        "step_ms": {"median": round(float(np.median(step_s)) * 1e3, 4), "p90": round(float(np.percentile(step_s, 90)) * 1e3, 4),
-                    "max": round(max(step_s) * 1e3, 4), "min": round(min(step_s) * 1e3, 4)},
+        "step_ms": {"mean": round(float(np.mean(step_s)) * 1e3, 4),
+                    "median": round(float(np.median(step_s)) * 1e3, 4), "p90": round(float(np.percentile(step_s, 90)) * 1e3, 4),
+                    "max": round(max(step_s) * 1e3, 4), "min": round(min(step_s) * 1e3, 4),
+                    "all": [round(x * 1e3, 3) for x in step_s]},
+        "slowest_step": slowest_step(step_s, step_diag, Wm),
         "roofline": {
             "kernel": f"{lk_name}> (temporal LK 21x21, all levels, {lk_desc})",
             "dominant_phase": dominant,

@@ -190,9 +190,12 @@ int svo_solve_pnp_sqpnp(const double* obj_xyz, const float* img_xy, int n, const
 /* RANSAC's minimal solver alone: SOLVEPNP_EPNP on 5 points, the model estimator
  * solvePnPRansac runs per hypothesis (R:src/tracking.cpp:191-196), for m subsets
  * given as 25 floats each (obj xyz x5, then img xy x5, as the front end gathers
- * them). device = 1: one 64-lane wave per subset on the GPU (epnp_wave.hpp);
- * device = 0: the host solver the RANSAC uses. Outputs are bit-identical.
- * Rt: m x 12 doubles (R row-major, t); ok: m ints (0: non-finite model). */
+ * them). device = 0: the host solver the RANSAC uses (OpenCV's epnp.cpp with its
+ * Jacobi SVDs, bit-identical to the oracle's restatement; no context needed);
+ * device = 1: one 64-lane wave per subset on the GPU (epnp_wave.hpp), a QL-based
+ * variant kept off the path; device = 2: that variant's host twin (bit-identical
+ * to device 1; no context needed). Rt: m x 12 doubles (R row-major, t); ok: m
+ * ints (0: non-finite model). */
 int svo_epnp_subsets(svo_ctx* ctx, const float* subsets, int m, const double K[9], int device, double* Rt,
                      int* ok);
 
@@ -291,8 +294,19 @@ typedef struct svo_frontend_stats {
     int64_t hypotheses;     /* RANSAC hypotheses scored on the GPU */
     double host_ms_hyp;     /* host wall time generating hypotheses (EPnP) */
     double host_ms_fit;     /* host wall time in the final fits */
-    double host_ms_wait;    /* host wall time blocked on the GPU */
+    double host_ms_wait;    /* host wall time blocked on the GPU (= the three waits below) */
     int64_t keyframes;      /* sequences whose frame was a keyframe this step */
+    /* per-step diagnostics (what a slow step spent its time on) */
+    double host_ms_wait_post;   /* waiting for the post-LK results (LK + compaction) */
+    double host_ms_wait_score;  /* waiting for the RANSAC scoring launches, all rounds */
+    double host_ms_wait_kf;     /* waiting for the keyframe at the step's end */
+    double host_ms_enqueue;     /* issuing the step's launches (incl. the next front half) */
+    double host_ms_step;        /* the whole call */
+    int64_t ransac_rounds;      /* host <-> GPU RANSAC rounds (chunks) */
+    int64_t max_hypotheses;     /* most hypotheses any one sequence scored */
+    int64_t serial_keyframe;    /* 1: the speculative stereo LK missed, serial keyframe ran */
+    int64_t full_copy;          /* 1: the full point copy was waited for (long RANSAC / n <= 5) */
+    int64_t kf_overflow;        /* corners a keyframe could not take for lack of capacity */
 } svo_frontend_stats;
 
 int svo_frontend_create(svo_ctx* ctx, const svo_frontend_config* cfg, svo_frontend** out);
@@ -361,6 +375,10 @@ int svo_frontend_time_fast(svo_frontend* fe, int t, int reps, double* ms_per_lau
 int svo_host_cpu_plan(int local_rank, int local_world, const int* gpu_node, int* cpus, int cap, int* n);
 /* The CPUs a front end's pool threads are pinned to (empty: not pinned). */
 int svo_frontend_host_cpus(svo_frontend* fe, int* cpus, int cap, int* n);
+/* Self-test of the front end's host pool (no GPU): `jobs` jobs of changing sizes
+ * with primes between them on `threads` threads; *bad = tasks run other than
+ * exactly once, or after their job returned (0 when the pool is correct). */
+int svo_pool_selftest(int threads, int jobs, int64_t* bad);
 
 /* ------------------------------------------------------------ synthetic input
  * Deterministic synthetic KITTI-like frames: a textured canvas

@@ -20,4 +20,12 @@ void ora_svd(const double* a, int m, int n, double* w, double* u, double* vt);
 /* Least-squares solve via SVD pseudo-inverse (cv::solve(..., DECOMP_SVD)). */
 void ora_svd_solve(const double* A, int m, int n, const double* b, double* x);
 
+/* OpenCV's lapack.cpp restated (cvsvd.c): the EPnP solver's SVDs. n <= 16. */
+void ora_cv_jacobi_svd(double* At, int m, int n, int n1, double* W, double* Vt);
+void ora_cv_svd(const double* A, int m, int n, double* w, double* u, double* vt);
+void ora_cv_svd_ut(const double* A, int n, double* w, double* ut);
+void ora_cv_solve_svd(const double* A, int m, int n, const double* b, double* x);
+void ora_cv_invert_svd(const double* A, int n, double* Ai);
+void ora_mul_transposed(const double* src, int rows, int cols, double* dst);
+
 #endif

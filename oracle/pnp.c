@@ -12,10 +12,15 @@
  * core/include/opencv2/core/operations.hpp (cv::RNG).
  *
  * The RANSAC stage (subset sequence, scoring, accept rule, iteration update) is
- * restated exactly; EPnP uses this file's own Jacobi SVD, so hypotheses agree
- * with OpenCV's up to rounding. The final solvePnP(SQPNP) on the inliers is
- * restated as the minimiser of SQPnP's object-space cost (multi-start Gauss-
- * Newton on SO(3)), see DESIGN.md.
+ * restated exactly. EPnP follows epnp.cpp operation by operation, its SVDs /
+ * inverse / least-squares solves being OpenCV's lapack.cpp Jacobi restated in
+ * cvsvd.c (cvSVD, cvInvert(CV_SVD), cvSolve(CV_SVD)), the image points
+ * normalised by undistortPoints into float as OpenCV's CV_32FC2 output, and the
+ * model stored through cv::Rodrigues (its SVD the same Jacobi). The product's
+ * minimal solver restates the same operations (svo_amd/csrc/epnp.hpp), so the
+ * two pick the same basis of the 5-point M^T M's two-dimensional null space and
+ * their hypotheses agree bit for bit (tests/test_epnp_cpu.py). The final
+ * solvePnP(SQPNP) on the inliers is sqpnp.c.
  */
 #include "svo_oracle.h"
 #include "oracle_internal.h"
@@ -72,10 +77,16 @@ void svo_oracle_rodrigues(const double rv[3], double R[9])
 
 void svo_oracle_rodrigues_inv(const double Rin[9], double rv[3])
 {
+    /* cv::Rodrigues: SVD::compute(R, W, U, Vt); R = U * Vt (Matx product: s = 0,
+     * s += u(i,k) vt(k,j) for k = 0..2) */
     double w[3], u[9], vt[9], R[9];
-    ora_svd(Rin, 3, 3, w, u, vt);
+    ora_cv_svd(Rin, 3, 3, w, u, vt);
     for (int i = 0; i < 3; i++)
-        for (int j = 0; j < 3; j++) R[i * 3 + j] = u[i * 3 + 0] * vt[0 * 3 + j] + u[i * 3 + 1] * vt[1 * 3 + j] + u[i * 3 + 2] * vt[2 * 3 + j];
+        for (int j = 0; j < 3; j++) {
+            double acc = 0;
+            for (int k = 0; k < 3; k++) acc += u[i * 3 + k] * vt[k * 3 + j];
+            R[i * 3 + j] = acc;
+        }
     double rx = R[7] - R[5], ry = R[2] - R[6], rz = R[3] - R[1];
     double s = sqrt((rx * rx + ry * ry + rz * rz) * 0.25);
     double c = (R[0] + R[4] + R[8] - 1) * 0.5;
@@ -158,34 +169,19 @@ static void choose_control_points(epnp_t* e)
     for (int i = 0; i < n; i++)
         for (int j = 0; j < 3; j++) e->cws[0][j] += e->pws[3 * i + j];
     for (int j = 0; j < 3; j++) e->cws[0][j] /= n;
-    double M[9] = {0};
-    for (int i = 0; i < n; i++) {
-        double d[3];
-        for (int j = 0; j < 3; j++) d[j] = e->pws[3 * i + j] - e->cws[0][j];
-        for (int a = 0; a < 3; a++)
-            for (int b = 0; b < 3; b++) M[a * 3 + b] += d[a] * d[b];
-    }
+    /* PW0 = pws - c0; cvMulTransposed(PW0, PW0tPW0, 1); cvSVD(U_T) */
+    double* pw0 = (double*)malloc(sizeof(double) * 3 * n);
+    for (int i = 0; i < n; i++)
+        for (int j = 0; j < 3; j++) pw0[3 * i + j] = e->pws[3 * i + j] - e->cws[0][j];
+    double M[9];
+    ora_mul_transposed(pw0, n, 3, M);
+    free(pw0);
     double dc[3], uct[9];
-    ora_sym_eig(M, 3, dc, uct);
+    ora_cv_svd_ut(M, 3, dc, uct);
     for (int i = 1; i < 4; i++) {
-        double ev = dc[i - 1] > 0 ? dc[i - 1] : 0;
-        double k = sqrt(ev / n);
+        double k = sqrt(dc[i - 1] / n);
         for (int j = 0; j < 3; j++) e->cws[i][j] = e->cws[0][j] + k * uct[3 * (i - 1) + j];
     }
-}
-
-static void inv3_pinv(const double* A, double* Ai)
-{
-    double w[3], u[9], vt[9];
-    ora_svd(A, 3, 3, w, u, vt);
-    double tol = w[0] * 3 * DBL_EPSILON;
-    for (int i = 0; i < 3; i++)
-        for (int j = 0; j < 3; j++) {
-            double s = 0;
-            for (int k = 0; k < 3; k++)
-                if (w[k] > tol) s += vt[k * 3 + i] * u[j * 3 + k] / w[k];
-            Ai[i * 3 + j] = s;
-        }
 }
 
 static void compute_barycentric(epnp_t* e)
@@ -193,7 +189,7 @@ static void compute_barycentric(epnp_t* e)
     double cc[9], ci[9];
     for (int i = 0; i < 3; i++)
         for (int j = 1; j < 4; j++) cc[3 * i + j - 1] = e->cws[j][i] - e->cws[0][i];
-    inv3_pinv(cc, ci);
+    ora_cv_invert_svd(cc, 3, ci); /* cvInvert(&CC, &CC_inv, CV_SVD) */
     for (int i = 0; i < e->n; i++) {
         double* pi = e->pws + 3 * i;
         double* a = e->alphas + 4 * i;
@@ -237,7 +233,7 @@ static void find_betas_1(const double* L, const double* rho, double* betas)
     for (int i = 0; i < 6; i++) {
         A[4 * i] = L[10 * i]; A[4 * i + 1] = L[10 * i + 1]; A[4 * i + 2] = L[10 * i + 3]; A[4 * i + 3] = L[10 * i + 6];
     }
-    ora_svd_solve(A, 6, 4, rho, b4);
+    ora_cv_solve_svd(A, 6, 4, rho, b4);
     if (b4[0] < 0) {
         betas[0] = sqrt(-b4[0]);
         betas[1] = -b4[1] / betas[0]; betas[2] = -b4[2] / betas[0]; betas[3] = -b4[3] / betas[0];
@@ -251,7 +247,7 @@ static void find_betas_2(const double* L, const double* rho, double* betas)
 {
     double A[18], b3[3];
     for (int i = 0; i < 6; i++) { A[3 * i] = L[10 * i]; A[3 * i + 1] = L[10 * i + 1]; A[3 * i + 2] = L[10 * i + 2]; }
-    ora_svd_solve(A, 6, 3, rho, b3);
+    ora_cv_solve_svd(A, 6, 3, rho, b3);
     if (b3[0] < 0) {
         betas[0] = sqrt(-b3[0]);
         betas[1] = (b3[2] < 0) ? sqrt(-b3[2]) : 0.0;
@@ -268,7 +264,7 @@ static void find_betas_3(const double* L, const double* rho, double* betas)
     double A[30], b5[5];
     for (int i = 0; i < 6; i++)
         for (int k = 0; k < 5; k++) A[5 * i + k] = L[10 * i + k];
-    ora_svd_solve(A, 6, 5, rho, b5);
+    ora_cv_solve_svd(A, 6, 5, rho, b5);
     if (b5[0] < 0) {
         betas[0] = sqrt(-b5[0]);
         betas[1] = (b5[2] < 0) ? sqrt(-b5[2]) : 0.0;
@@ -336,8 +332,11 @@ static void qr_solve(double* A, int nr, int nc, double* b, double* X)
 
 static void gauss_newton(const double* L, const double* rho, double betas[4])
 {
+    /* x outlives the iterations, as epnp.cpp's: a qr_solve that returns early
+     * (a zero column) leaves the previous step in it */
+    double x[4] = {0, 0, 0, 0};
     for (int it = 0; it < 5; it++) {
-        double A[24], b[6], x[4] = {0, 0, 0, 0};
+        double A[24], b[6];
         for (int i = 0; i < 6; i++) {
             const double* r = L + 10 * i;
             A[4 * i + 0] = 2 * r[0] * betas[0] + r[1] * betas[1] + r[3] * betas[2] + r[6] * betas[3];
@@ -389,8 +388,9 @@ static double compute_R_and_t(epnp_t* e, const double* ut, const double* betas, 
             abt[3 * j + 2] += (pc[j] - pc0[j]) * (pw[2] - pw0[2]);
         }
     }
+    /* cvSVD(&ABt, &D, &U, &V, CV_SVD_MODIFY_A); R[i][j] = dot(U row i, V row j) */
     double w[3], u[9], vt[9];
-    ora_svd(abt, 3, 3, w, u, vt);
+    ora_cv_svd(abt, 3, 3, w, u, vt);
     for (int i = 0; i < 3; i++)
         for (int j = 0; j < 3; j++)
             R[3 * i + j] = u[3 * i + 0] * vt[0 * 3 + j] + u[3 * i + 1] * vt[1 * 3 + j] + u[3 * i + 2] * vt[2 * 3 + j];
@@ -430,9 +430,10 @@ int svo_oracle_epnp(const float* obj, const float* img, int n, const double K[9]
     e.pcs = (double*)malloc(sizeof(double) * 3 * n);
     for (int i = 0; i < n; i++) {
         e.pws[3 * i] = obj[3 * i]; e.pws[3 * i + 1] = obj[3 * i + 1]; e.pws[3 * i + 2] = obj[3 * i + 2];
-        double x = ((double)img[2 * i] - K[2]) * ifx, y = ((double)img[2 * i + 1] - K[5]) * ify;
-        e.us[2 * i] = x * e.fu + e.uc;
-        e.us[2 * i + 1] = y * e.fv + e.vc;
+        /* undistortPoints of CV_32FC2 points writes CV_32FC2 */
+        float x = (float)(((double)img[2 * i] - K[2]) * ifx), y = (float)(((double)img[2 * i + 1] - K[5]) * ify);
+        e.us[2 * i] = (double)x * e.fu + e.uc;
+        e.us[2 * i + 1] = (double)y * e.fv + e.vc;
     }
     choose_control_points(&e);
     compute_barycentric(&e);
@@ -447,21 +448,17 @@ int svo_oracle_epnp(const float* obj, const float* img, int n, const double K[9]
             M2[3 * k] = 0.0; M2[3 * k + 1] = as[k] * e.fv; M2[3 * k + 2] = as[k] * (e.vc - v);
         }
     }
-    double mtm[144] = {0}, d[12], ut[144];
-    for (int r = 0; r < 2 * n; r++)
-        for (int a = 0; a < 12; a++) {
-            double ma = M[r * 12 + a];
-            if (ma == 0) continue;
-            for (int b = 0; b < 12; b++) mtm[a * 12 + b] += ma * M[r * 12 + b];
-        }
+    double mtm[144], d[12], ut[144];
+    ora_mul_transposed(M, 2 * n, 12, mtm); /* cvMulTransposed(M, &MtM, 1) */
     free(M);
-    ora_sym_eig(mtm, 12, d, ut);
+    ora_cv_svd_ut(mtm, 12, d, ut);         /* cvSVD(&MtM, &D, &Ut, 0, MODIFY_A | U_T) */
     double L[60], rho[6];
     compute_L_6x10(ut, L);
     rho[0] = dist2(e.cws[0], e.cws[1]); rho[1] = dist2(e.cws[0], e.cws[2]); rho[2] = dist2(e.cws[0], e.cws[3]);
     rho[3] = dist2(e.cws[1], e.cws[2]); rho[4] = dist2(e.cws[1], e.cws[3]); rho[5] = dist2(e.cws[2], e.cws[3]);
     double Betas[4][4] = {{0}}, rep[4] = {0}, Rs[4][9], ts[4][3];
-    find_betas_1(L, rho, Betas[1]); gauss_newton(L, rho, Betas[1]);
+    find_betas_1(L, rho, Betas[1]);
+    gauss_newton(L, rho, Betas[1]);
     rep[1] = compute_R_and_t(&e, ut, Betas[1], Rs[1], ts[1]);
     find_betas_2(L, rho, Betas[2]); gauss_newton(L, rho, Betas[2]);
     rep[2] = compute_R_and_t(&e, ut, Betas[2], Rs[2], ts[2]);

@@ -137,6 +137,7 @@ _SIGS = [
     ("svo_frontend_reset_times", None, [_vp]),
     ("svo_host_cpu_plan", C.c_int, [C.c_int, C.c_int, _i32p, _i32p, C.c_int, _i32p]),
     ("svo_frontend_host_cpus", C.c_int, [_vp, _i32p, C.c_int, _i32p]),
+    ("svo_pool_selftest", C.c_int, [C.c_int, C.c_int, C.POINTER(C.c_int64)]),
     ("svo_synth_canvas", C.c_int, [C.c_uint64, C.c_int, C.c_int, C.c_int, _u8p]),
     ("svo_synth_frame", C.c_int, [_u8p, C.c_int, C.c_int, C.c_int, C.c_int, _f64p, _f64p,
                                   C.c_uint64, C.c_int, _u8p, C.c_int, C.c_int]),
@@ -162,6 +163,16 @@ def solve_pnp_sqpnp(obj, img_pts, K):
     if rc < 0:
         raise SvoError(f"svo_solve_pnp_sqpnp: error {rc}")
     return rc == 1, rv, tv
+
+
+def pool_selftest(threads=8, jobs=2000):
+    """svo_pool_selftest: tasks of the front end's host pool run other than exactly
+    once over `jobs` jobs of changing sizes (host code, no GPU); 0 = correct."""
+    bad = C.c_int64(0)
+    rc = lib().svo_pool_selftest(int(threads), int(jobs), C.byref(bad))
+    if rc < 0:
+        raise SvoError(f"svo_pool_selftest: error {rc}")
+    return int(bad.value)
 
 
 def host_cpu_plan(local_rank, local_world, gpu_node=None, cap=4096):
@@ -429,9 +440,11 @@ class Context:
                                             _p(mask, _u8p), _p(counts, _i32p)))
         return err, mask, counts
 
-    def epnp_subsets(self, subsets, K, device: bool = True):
+    def epnp_subsets(self, subsets, K, device=True):
         """RANSAC's EPnP on (m, 25) float subsets (obj xyz x5, img xy x5) -> (Rt (m, 12), ok (m,)):
-        one wave per subset on the GPU (device) or the host solver; bit-identical."""
+        device 0 / False: the host solver the RANSAC uses (bit-identical to the
+        oracle's EPnP); 1 / True: the QL variant, one wave per subset on the GPU;
+        2: that variant's host twin (bit-identical to 1)."""
         subsets = _c(subsets, np.float32).reshape(-1, 25)
         K = _c(K, np.float64).reshape(9)
         m = len(subsets)
@@ -561,7 +574,11 @@ class FrontendStats(C.Structure):
     _fields_ = [("lk_iterations", C.c_int64), ("tracked", C.c_int64), ("inliers", C.c_int64),
                 ("added", C.c_int64), ("features", C.c_int64), ("hypotheses", C.c_int64),
                 ("host_ms_hyp", C.c_double), ("host_ms_fit", C.c_double), ("host_ms_wait", C.c_double),
-                ("keyframes", C.c_int64)]
+                ("keyframes", C.c_int64),
+                ("host_ms_wait_post", C.c_double), ("host_ms_wait_score", C.c_double),
+                ("host_ms_wait_kf", C.c_double), ("host_ms_enqueue", C.c_double), ("host_ms_step", C.c_double),
+                ("ransac_rounds", C.c_int64), ("max_hypotheses", C.c_int64), ("serial_keyframe", C.c_int64),
+                ("full_copy", C.c_int64), ("kf_overflow", C.c_int64)]
 
     def as_dict(self):
         return {k: (float(getattr(self, k)) if k.startswith("host_") else int(getattr(self, k)))

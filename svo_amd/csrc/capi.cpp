@@ -1,6 +1,7 @@
 // C ABI of libsvo_gpu.so: context, device images, and the host-pointer entry
 // points that mirror the reference's OpenCV calls (see include/svo_gpu.h for
 // the reference file:line each one replaces).
+#include <algorithm>
 #include <cstdlib>
 #include <cstdarg>
 #include <cstring>
@@ -8,6 +9,8 @@
 
 #include "common.hpp"
 #include "epnp.hpp"
+#include "epnp_ql.hpp"
+#include "pose.hpp"
 
 namespace svo {
 
@@ -515,16 +518,37 @@ int svo_pnp_residuals(svo_ctx* ctx, const float* obj_xyz, const float* img_xy, i
 
 int svo_epnp_subsets(svo_ctx* ctx, const float* subsets, int m, const double K[9], int device, double* Rt,
                      int* ok) {
-    if ((!ctx && device) || m < 0 || (m > 0 && (!subsets || !Rt || !ok)) || !K)
+    if ((!ctx && device == 1) || device < 0 || device > 2 || m < 0 || (m > 0 && (!subsets || !Rt || !ok)) || !K)
         return set_error(ctx, SVO_ERR_ARG, "svo_epnp_subsets: bad arguments");
     if (m == 0) return SVO_OK;
-    if (!device) {
+    if (device == 2) {  // the device solver's host twin (epnp_ql.hpp)
         for (int j = 0; j < m; j++) {
             const float* sp = subsets + 25 * (size_t)j;
             double R[9], t[3];
-            ok[j] = epnp_pixels(sp, sp + 15, nullptr, 5, K, R, t) ? 1 : 0;
+            ok[j] = epnp_pixels_ql(sp, sp + 15, nullptr, 5, K, R, t) ? 1 : 0;
             std::memcpy(Rt + 12 * (size_t)j, R, sizeof(R));
             std::memcpy(Rt + 12 * (size_t)j + 9, t, sizeof(t));
+        }
+        return SVO_OK;
+    }
+    if (!device) {  // the front end's host solver: epnp_pixels_batch, kEpnpLanes subsets at a time
+        for (int j0 = 0; j0 < m; j0 += kEpnpLanes) {
+            const int c = std::min(kEpnpLanes, m - j0);
+            const float *o[kEpnpLanes], *im[kEpnpLanes];
+            const int* id[kEpnpLanes];
+            double R[kEpnpLanes][9], t[kEpnpLanes][3];
+            bool v[kEpnpLanes];
+            for (int q = 0; q < c; q++) {
+                o[q] = subsets + 25 * (size_t)(j0 + q);
+                im[q] = o[q] + 15;
+                id[q] = nullptr;
+            }
+            epnp_pixels_batch(c, o, im, id, K, R, t, v);
+            for (int q = 0; q < c; q++) {
+                ok[j0 + q] = v[q] ? 1 : 0;
+                std::memcpy(Rt + 12 * (size_t)(j0 + q), R[q], sizeof(R[q]));
+                std::memcpy(Rt + 12 * (size_t)(j0 + q) + 9, t[q], sizeof(t[q]));
+            }
         }
         return SVO_OK;
     }

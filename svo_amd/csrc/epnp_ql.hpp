@@ -1,44 +1,33 @@
-// EPnP minimal solver of the host RANSAC (pose.cpp): __host__ __device__, fixed
-// sizes, no allocation, so the same code also runs on the device
-// (tools/epnp_probe.hip measures it there).
+// The round-3 EPnP minimal solver (tred2 / tql2 eigen-decomposition of M^T M,
+// Householder least squares for the betas), kept as the host twin of the
+// device solver epnp_wave.hpp, which mirrors it bit for bit
+// (svo_epnp_subsets(device = 2); test_gpu_parity.py::test_epnp_wave_matches_host).
+// The front end's RANSAC uses epnp.hpp (OpenCV's Jacobi SVDs, bit-identical to
+// the oracle): the QL basis of the 5-point M^T M's two-dimensional null space
+// differs from the Jacobi one, and Gauss-Newton can end in another optimum from
+// it.
 #pragma once
 
+#include "epnp.hpp"
 #include "linalg.hpp"
 
 namespace svo {
 
-SVO_HD double dot3(const double* a, const double* b) { return a[0] * b[0] + a[1] * b[1] + a[2] * b[2]; }
 
-// EPnP (Lepetit, Moreno-Noguer, Fua) as OpenCV's calib3d/src/epnp.cpp computes it,
-// operation by operation: 4 control points (centroid + PCA by cvSVD), barycentric
-// alphas (cvInvert(CV_SVD)), cvMulTransposed(M) and the M^T M null space (the 4
-// left singular vectors of the smallest singular values, cvSVD), beta
-// approximations 1/2/3 (cvSolve(CV_SVD)) + 5 Gauss-Newton steps (epnp's
-// Householder qr_solve), R/t by Procrustes (cvSVD), best of the three by mean
-// reprojection. Every SVD is OpenCV's one-sided Jacobi (la::cv): the 5-point
-// M^T M has a two-dimensional null space, and which basis of it the solver
-// returns decides which local optimum Gauss-Newton reaches -- so the solver
-// mirrors OpenCV's Jacobi step for step, and the oracle (oracle/pnp.c +
-// cvsvd.c) restates the same operations: the two agree bit for bit.
+// EPnP (Lepetit, Moreno-Noguer, Fua) as OpenCV's calib3d/src/epnp.cpp computes it:
+// 4 control points (centroid + PCA), barycentric alphas, M^T M null space (4
+// smallest eigenvectors), beta approximations 1/2/3 + 5 Gauss-Newton steps
+// (Householder QR), R/t by Procrustes, best of the three by mean reprojection.
 // Fixed capacity kMaxPts points (the RANSAC subsets and the direct n <= 5 case),
 // no allocation: the same code runs on the host and in the GPU RANSAC kernel.
-class EPnP {
+class EPnPQL {
    public:
     static constexpr int kMaxPts = 5;
-    SVO_HD EPnP(double fu, double fv, double uc, double vc) : fu_(fu), fv_(fv), uc_(uc), vc_(vc) {}
+    SVO_HD EPnPQL(double fu, double fv, double uc, double vc) : fu_(fu), fv_(fv), uc_(uc), vc_(vc) {}
 
     // pw: n (<= kMaxPts) world points; uv: n pixels. Returns false on non-finite output.
     SVO_HD bool solve(const double* pw, const double* uv, int n, double R[9], double t[3]) {
         if (n > kMaxPts) return false;
-        double MtM[144], ev[12], ut[144];
-        prepare(pw, uv, n, MtM);
-        la::cv::svd_ut<12>(MtM, ev, ut);
-        return finish(ut, R, t);
-    }
-    // solve in two halves around the 12 x 12 SVD (so that a batch of solvers can
-    // run their SVDs together, simd_svd.hpp): prepare -> M^T M; finish(ut, the
-    // left singular vectors of M^T M as rows) -> R, t. pw / uv must outlive finish.
-    SVO_HD void prepare(const double* pw, const double* uv, int n, double* MtM) {
         n_ = n;
         pw_ = pw;
         uv_ = uv;
@@ -46,13 +35,11 @@ class EPnP {
         for (int i = 0; i < 3 * n; i++) pcs_[i] = 0.0;
         control_points();
         barycentric();
-        // fill_M: rows 2i, 2i + 1 per correspondence
-        double Mm[2 * kMaxPts * 12];
+        double MtM[144] = {0};
         for (int i = 0; i < n; i++) {
             const double* a = &alphas_[4 * i];
             const double u = uv[2 * i], v = uv[2 * i + 1];
-            double* r1 = Mm + 24 * i;
-            double* r2 = r1 + 12;
+            double r1[12], r2[12];
             for (int k = 0; k < 4; k++) {
                 r1[3 * k] = a[k] * fu_;
                 r1[3 * k + 1] = 0.0;
@@ -61,10 +48,11 @@ class EPnP {
                 r2[3 * k + 1] = a[k] * fv_;
                 r2[3 * k + 2] = a[k] * (vc_ - v);
             }
+            for (int p = 0; p < 12; p++)
+                for (int q = 0; q < 12; q++) MtM[p * 12 + q] += r1[p] * r1[q] + r2[p] * r2[q];
         }
-        la::cv::mul_transposed<12>(Mm, 2 * n, MtM);
-    }
-    SVO_HD bool finish(const double* ut, double R[9], double t[3]) {
+        double ev[12], ut[144];
+        la::sym_eig_ql(MtM, 12, ev, ut);
         double L[60], rho[6];
         make_L(ut, L);
         const int pairs[6][2] = {{0, 1}, {0, 2}, {0, 3}, {1, 2}, {1, 3}, {2, 3}};
@@ -96,15 +84,17 @@ class EPnP {
         for (int i = 0; i < n_; i++)
             for (int j = 0; j < 3; j++) c0[j] += pw_[3 * i + j];
         for (int j = 0; j < 3; j++) c0[j] /= n_;
-        double pw0[3 * kMaxPts];
-        for (int i = 0; i < n_; i++)
-            for (int j = 0; j < 3; j++) pw0[3 * i + j] = pw_[3 * i + j] - c0[j];
-        double C[9], w[3], V[9];
-        la::cv::mul_transposed<3>(pw0, n_, C);
-        la::cv::svd_ut<3>(C, w, V);
+        double C[9] = {0};
+        for (int i = 0; i < n_; i++) {
+            double d[3] = {pw_[3 * i] - c0[0], pw_[3 * i + 1] - c0[1], pw_[3 * i + 2] - c0[2]};
+            for (int a = 0; a < 3; a++)
+                for (int b = 0; b < 3; b++) C[a * 3 + b] += d[a] * d[b];
+        }
+        double w[3], V[9];
+        la::sym_eig(C, 3, w, V);
         for (int j = 0; j < 3; j++) cws_[0][j] = c0[j];
         for (int i = 1; i < 4; i++) {
-            const double k = sqrt(w[i - 1] / n_);
+            const double k = sqrt((w[i - 1] > 0 ? w[i - 1] : 0.0) / n_);
             for (int j = 0; j < 3; j++) cws_[i][j] = c0[j] + k * V[3 * (i - 1) + j];
         }
     }
@@ -112,7 +102,7 @@ class EPnP {
         double CC[9], CI[9];
         for (int i = 0; i < 3; i++)
             for (int j = 1; j < 4; j++) CC[3 * i + j - 1] = cws_[j][i] - cws_[0][i];
-        la::cv::invert_svd<3>(CC, CI);
+        la::pinv3(CC, CI);
         for (int i = 0; i < n_; i++) {
             const double* p = pw_ + 3 * i;
             double* a = &alphas_[4 * i];
@@ -148,10 +138,18 @@ class EPnP {
             r[9] = dot3(dv[3][i], dv[3][i]);
         }
     }
-    // The 6 x {4, 3, 5} least-squares systems: cvSolve(CV_SVD), as epnp.cpp
+    // The 6 x {4, 3, 5} least-squares systems are solved by Householder QR
+    // (qr_solve, as the Gauss-Newton steps): OpenCV solves them by SVD
+    // (cvSolve(CV_SVD)); for these full-rank systems both give the unique
+    // least-squares solution up to rounding, which the 5 Gauss-Newton steps then
+    // refine (measured: the same models as an SVD solve on 600 RANSAC subsets,
+    // same speed; the device solver, epnp_wave.hpp, mirrors this one bit for bit).
     template <int NC>
     SVO_HD static void lstsq_qr(const double* A, const double* rho, double* x) {
-        la::cv::solve_svd<6, NC>(A, rho, x);
+        double Aq[6 * NC], bq[6];
+        for (int i = 0; i < 6 * NC; i++) Aq[i] = A[i];
+        for (int i = 0; i < 6; i++) bq[i] = rho[i];
+        qr_solve<6, NC>(Aq, bq, x);
     }
     // approximations 2 (NC = 3) and 3 (NC = 5): the first NC columns of L
     template <int NC>
@@ -196,12 +194,12 @@ class EPnP {
     SVO_HD static void qr_solve(double* A, double* b, double* X) {
         double A1[nc], A2[nc];
         for (int k = 0; k < nc; k++) {
-            // epnp.cpp's scale: the largest |A[i][k]| over rows k .. nr - 2 (its
-            // loop advances the row pointer after reading, so the last row is
-            // never compared -- kept: the scale sets the rounding)
-            double eta = fabs(A[k * nc + k]);
-            for (int i = k + 1; i < nr; i++) eta = fmax(eta, fabs(A[(i - 1) * nc + k]));
-            if (eta == 0) return;  // epnp.cpp: X keeps its previous contents
+            double eta = 0;
+            for (int i = k; i < nr; i++) eta = fmax(eta, fabs(A[i * nc + k]));
+            if (eta == 0) {
+                for (int j = 0; j < nc; j++) X[j] = 0;
+                return;
+            }
             double sum2 = 0.0;
             const double ie = 1. / eta;
             for (int i = k; i < nr; i++) {
@@ -245,9 +243,10 @@ class EPnP {
             for (int q = 0; q < NS; q++) {
                 if (dead[q]) continue;
                 double* a = A[q];
-                double eta = fabs(a[k * nc + k]);  // rows k .. nr - 2, as qr_solve
-                for (int i = k + 1; i < nr; i++) eta = fmax(eta, fabs(a[(i - 1) * nc + k]));
-                if (eta == 0) {  // X[q] keeps its previous contents (qr_solve)
+                double eta = 0;
+                for (int i = k; i < nr; i++) eta = fmax(eta, fabs(a[i * nc + k]));
+                if (eta == 0) {
+                    for (int j = 0; j < nc; j++) X[q][j] = 0;
                     dead[q] = true;
                     continue;
                 }
@@ -289,10 +288,8 @@ class EPnP {
     }
     // gauss_newton of the three approximations (betas[1..3]) in lock step
     SVO_HD static void gauss_newton3(const double* L, const double* rho, double (*betas)[4]) {
-        // x outlives the iterations (epnp.cpp's gauss_newton)
-        double x[3][4] = {{0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}};
         for (int it = 0; it < 5; it++) {
-            double A[3][24], b[3][6];
+            double A[3][24], b[3][6], x[3][4];
             for (int q = 0; q < 3; q++) {
                 const double* be = betas[q + 1];
                 for (int i = 0; i < 6; i++) {
@@ -313,9 +310,8 @@ class EPnP {
         }
     }
     SVO_HD static void gauss_newton(const double* L, const double* rho, double* be) {
-        double x[4] = {0, 0, 0, 0};
         for (int it = 0; it < 5; it++) {
-            double A[24], b[6];
+            double A[24], b[6], x[4];
             for (int i = 0; i < 6; i++) {
                 const double* r = L + 10 * i;
                 A[4 * i + 0] = 2 * r[0] * be[0] + r[1] * be[1] + r[3] * be[2] + r[6] * be[3];
@@ -369,7 +365,7 @@ class EPnP {
             }
         }
         double s[3][3], U[3][9], Vt[3][9];
-        for (int q = 0; q < 3; q++) la::cv::svd<3>(abt[q], s[q], U[q], Vt[q]);
+        la::svd3_n<3>(abt, s, U, Vt);
         for (int q = 0; q < 3; q++) {
             double* R = Rs[q + 1];
             double* t = ts[q + 1];
@@ -430,7 +426,7 @@ class EPnP {
                 for (int k = 0; k < 3; k++) abt[3 * j + k] += (pc[j] - pc0[j]) * (pw[k] - pw0[k]);
         }
         double s[3], U[9], Vt[9];
-        la::cv::svd<3>(abt, s, U, Vt);
+        la::svd(abt, 3, 3, s, U, Vt);
         for (int i = 0; i < 3; i++)
             for (int j = 0; j < 3; j++) R[3 * i + j] = U[3 * i] * Vt[j] + U[3 * i + 1] * Vt[3 + j] + U[3 * i + 2] * Vt[6 + j];
         const double det = R[0] * R[4] * R[8] + R[1] * R[5] * R[6] + R[2] * R[3] * R[7] - R[2] * R[4] * R[6] -
@@ -462,31 +458,25 @@ class EPnP {
 };
 
 
-// solvePnP(EPnP)'s inputs as the reference passes them: float object points
-// widened to double, pixels normalised by undistortPoints (x = (u - cx) * (1/fx),
-// written to float: CV_32FC2 in, CV_32FC2 out) and re-projected by epnp's
-// init_points (u' = x fu + uc). idx: the subset (or null for points 0..n-1).
-SVO_HD void epnp_inputs(const float* obj, const float* img, const int* idx, int n, const double K[9], double* pw,
-                        double* uv) {
+// solvePnP(EPnP) with the reference's inputs: float object points widened to
+// double, pixels normalised by undistortPoints (x = (u - cx) * (1/fx)) and
+// re-projected by epnp's init_points (u' = x fu + uc). idx: the subset (or
+// null for points 0..n-1); n <= EPnP::kMaxPts.
+SVO_HD bool epnp_pixels_ql(const float* obj, const float* img, const int* idx, int n, const double K[9], double R[9],
+                        double t[3]) {
+    if (n > EPnPQL::kMaxPts) return false;
+    double pw[3 * EPnPQL::kMaxPts], uv[2 * EPnPQL::kMaxPts];
     const double ifx = 1. / K[0], ify = 1. / K[4];
     for (int k = 0; k < n; k++) {
         const int i = idx ? idx[k] : k;
         pw[3 * k] = obj[3 * i];
         pw[3 * k + 1] = obj[3 * i + 1];
         pw[3 * k + 2] = obj[3 * i + 2];
-        const float x = (float)(((double)img[2 * i] - K[2]) * ifx), y = (float)(((double)img[2 * i + 1] - K[5]) * ify);
-        uv[2 * k] = (double)x * K[0] + K[2];
-        uv[2 * k + 1] = (double)y * K[4] + K[5];
+        const double x = ((double)img[2 * i] - K[2]) * ifx, y = ((double)img[2 * i + 1] - K[5]) * ify;
+        uv[2 * k] = x * K[0] + K[2];
+        uv[2 * k + 1] = y * K[4] + K[5];
     }
-}
-
-// solvePnP(EPnP) of n <= EPnP::kMaxPts points (epnp_inputs)
-SVO_HD bool epnp_pixels(const float* obj, const float* img, const int* idx, int n, const double K[9], double R[9],
-                        double t[3]) {
-    if (n > EPnP::kMaxPts) return false;
-    double pw[3 * EPnP::kMaxPts], uv[2 * EPnP::kMaxPts];
-    epnp_inputs(obj, img, idx, n, K, pw, uv);
-    EPnP e(K[0], K[4], K[2], K[5]);
+    EPnPQL e(K[0], K[4], K[2], K[5]);
     return e.solve(pw, uv, n, R, t);
 }
 

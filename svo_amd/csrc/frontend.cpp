@@ -62,8 +62,11 @@ namespace {
 // before sleeping on a condition variable, so a dispatch normally costs no
 // futex wake-up. The caller works too and spins on a counter of finished TASKS
 // (a worker that wakes late with nothing left to take is not waited for).
-// Tasks are claimed by CAS on (generation << 32 | index), so a worker still
-// holding an old generation can never take (or skip) a task of a newer job.
+// Tasks are claimed by CAS on one word holding (generation, task count, next
+// index): a worker still holding a word of an older job -- generation AND count
+// -- can never take (or skip) a task of a newer one, whatever the sizes of the
+// two jobs (the count is not read from a second variable that a newer job may
+// already have rewritten).
 // Workers are pinned to `cpus` (the rank's share of the node, svo_host_cpu_plan)
 // when it is non-empty. The spin is bounded below one step (SVO_POOL_SPIN_US,
 // default 400 us): between the step's two pool jobs the workers stay hot, across
@@ -97,35 +100,40 @@ class Pool {
     // spin window, so a job expected shortly finds them hot (no futex wake-up)
     void prime() {
         if (th_.empty()) return;
-        const uint64_t g = gen_.load(std::memory_order_relaxed) + 1;
-        n_.store(0, std::memory_order_relaxed);
-        next_.store(g << 32, std::memory_order_release);
-        {
-            std::lock_guard<std::mutex> lk(mu_);
-            gen_.store(g, std::memory_order_release);
-        }
-        if (sleeping_.load(std::memory_order_acquire) > 0) cv_.notify_all();
+        publish(0);
     }
     void run(int n, const std::function<void(int)>& fn) {
-        if (th_.empty() || n <= 1) {
+        if (th_.empty() || n <= 1 || n > (int)kFieldMask) {
             for (int i = 0; i < n; i++) fn(i);
             return;
         }
-        const uint64_t g = gen_.load(std::memory_order_relaxed) + 1;
         fn_ = &fn;
-        n_.store(n, std::memory_order_relaxed);
         done_.store(0, std::memory_order_relaxed);
-        next_.store(g << 32, std::memory_order_release);  // publishes fn_ / n_ to claimers
-        {
-            std::lock_guard<std::mutex> lk(mu_);
-            gen_.store(g, std::memory_order_release);
-        }
-        if (sleeping_.load(std::memory_order_acquire) > 0) cv_.notify_all();
+        const uint64_t g = publish(n);  // the release store of the job word publishes fn_ / done_
         work(g);
         while (done_.load(std::memory_order_acquire) < n) pause();
     }
 
    private:
+    // job word: generation (24 bits) | task count (20) | next index (20)
+    static constexpr int kFieldBits = 20;
+    static constexpr uint64_t kFieldMask = (1ull << kFieldBits) - 1;
+    static constexpr uint64_t kGenMask = (1ull << (64 - 2 * kFieldBits)) - 1;
+    static uint64_t gen_of(uint64_t v) { return v >> (2 * kFieldBits); }
+    static uint64_t cnt_of(uint64_t v) { return (v >> kFieldBits) & kFieldMask; }
+    static uint64_t idx_of(uint64_t v) { return v & kFieldMask; }
+    // a new job of n tasks: its word replaces the old one in a single store, so a
+    // stale CAS (old generation and count) fails from here on
+    uint64_t publish(int n) {
+        const uint64_t g = (gen_.load(std::memory_order_relaxed) + 1) & kGenMask;
+        next_.store((g << (2 * kFieldBits)) | ((uint64_t)n << kFieldBits), std::memory_order_release);
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            gen_.store(g, std::memory_order_release);
+        }
+        if (sleeping_.load(std::memory_order_acquire) > 0) cv_.notify_all();
+        return g;
+    }
     static void pause() {
 #if defined(__x86_64__)
         __builtin_ia32_pause();
@@ -134,9 +142,9 @@ class Pool {
     void work(uint64_t g) {
         for (;;) {
             uint64_t v = next_.load(std::memory_order_acquire);
-            if ((v >> 32) != g || (int)(v & 0xffffffffu) >= n_.load(std::memory_order_relaxed)) return;
+            if (gen_of(v) != g || idx_of(v) >= cnt_of(v)) return;
             if (!next_.compare_exchange_weak(v, v + 1, std::memory_order_acq_rel)) continue;
-            (*fn_)((int)(v & 0xffffffffu));
+            (*fn_)((int)idx_of(v));
             done_.fetch_add(1, std::memory_order_acq_rel);
         }
     }
@@ -169,7 +177,6 @@ class Pool {
     std::mutex mu_;
     std::condition_variable cv_;
     const std::function<void(int)>* fn_ = nullptr;
-    std::atomic<int> n_{0};
     std::atomic<uint64_t> next_{0}, gen_{0};
     std::atomic<int> done_{0}, sleeping_{0};
     std::atomic<bool> stop_{false};
@@ -1368,6 +1375,13 @@ int svo_frontend_step(svo_frontend* fe, int t, svo_frontend_stats* stats) {
     const int S = fe->S, CAP = fe->CAP;
     const svo_frontend_config& c = fe->cfg;
     int slot;
+    using clk = std::chrono::steady_clock;
+    auto ms_since = [](clk::time_point t0) {
+        return std::chrono::duration<double, std::milli>(clk::now() - t0).count();
+    };
+    const auto t_call = clk::now();
+    double ms_enqueue = 0, ms_wait_post = 0, ms_wait_score = 0, ms_wait_kf = 0;
+    int64_t rounds = 0;
 
     if (fe->front_t != t) {
         int rf = fe_front(fe, t);
@@ -1379,22 +1393,21 @@ int svo_frontend_step(svo_frontend* fe, int t, svo_frontend_stats* stats) {
     // the previous step's final pose fits: the host does them while the GPU tracks
     // this frame; they set the poses that move the previous keyframe's new map
     // points to the world frame, so this step's post-LK is queued right after
+    ms_enqueue += ms_since(t_call);
     double ms_fit = fe_finish_fits(fe);
     TP("fits done");
     {
+        const auto te = clk::now();
         int rp = fe_post(fe, t);
         if (rp) return rp;
+        ms_enqueue += ms_since(te);
     }
     TP("post-lk queued");
     hipStream_t sl = fe->st_lk, sf = fe->st_fast;
     int rc = SVO_OK;
     const PyrDesc* dcur = fe->d_desc + (size_t)(t % fe->T) * S;
 
-    using clk = std::chrono::steady_clock;
-    auto ms_since = [](clk::time_point t0) {
-        return std::chrono::duration<double, std::milli>(clk::now() - t0).count();
-    };
-    double ms_hyp = 0, ms_wait = 0;
+    double ms_hyp = 0;
     const float thr = (float)((double)c.pnp_reproj * (double)c.pnp_reproj);
     int64_t nhyp = 0, inl = 0;
     std::vector<int> ms(S, 0);
@@ -1424,7 +1437,7 @@ int svo_frontend_step(svo_frontend* fe, int t, svo_frontend_stats* stats) {
         fe->post_wait_ms = fe->post_wait_ms > 0 ? 0.75 * fe->post_wait_ms + 0.25 * w : w;
     }
     TP("lk results on host");
-    ms_wait += ms_since(tw);
+    ms_wait_post = ms_since(tw);
     // the speculative stereo LK went out early (fe_front) or with the post-LK (fe_post)
     const bool spec = fe->spec_margin >= 0 && fe->spec_t == t;
     const bool spec_early = spec && fe->spec_was_early;
@@ -1463,9 +1476,12 @@ int svo_frontend_step(svo_frontend* fe, int t, svo_frontend_stats* stats) {
         }
         if (!any) break;
         if (need_full) {  // past the prefetched subsets (> 26 hypotheses): rare
+            const auto tfw = clk::now();
             int rf = ensure_full();
             if (rf) return rf;
+            ms_wait_score += ms_since(tfw);
         }
+        rounds++;
         auto th = clk::now();
         // the chunks' subsets are drawn per sequence (the RNG's order), their EPnP
         // solves shared out one hypothesis per pool task: a sequence predicted to
@@ -1476,13 +1492,27 @@ int svo_frontend_step(svo_frontend* fe, int t, svo_frontend_stats* stats) {
             ms[s] = fe->rs[s].draw_chunk();
             for (int j = 0; j < ms[s]; j++) flat.push_back(s * kRansacChunk + j);
         }
+        // one pool task per group of kEpnpLanes hypotheses (epnp_pixels_batch: their
+        // 12 x 12 SVDs in SIMD lanes), groups taken in flat order across sequences
+        const int ntask = ((int)flat.size() + kEpnpLanes - 1) / kEpnpLanes;
+        auto solve_task = [&](int k) {
+            RansacSeq* seqs[kEpnpLanes];
+            int js[kEpnpLanes];
+            const int k0 = k * kEpnpLanes;
+            const int cnt = std::min(kEpnpLanes, (int)flat.size() - k0);
+            for (int q = 0; q < cnt; q++) {
+                seqs[q] = &fe->rs[flat[k0 + q] / kRansacChunk];
+                js[q] = flat[k0 + q] % kRansacChunk;
+            }
+            solve_hypotheses(seqs, js, cnt, c.K);
+        };
         if (tr) {
             // per-task attribution (trace only): which threads ran the solves, how long each took
-            std::vector<std::pair<size_t, double>> tk(flat.size());
+            std::vector<std::pair<size_t, double>> tk(ntask);
             const auto tb = clk::now();
-            fe->pool->run((int)flat.size(), [&](int k) {
+            fe->pool->run(ntask, [&](int k) {
                 const auto a = clk::now();
-                fe->rs[flat[k] / kRansacChunk].solve(flat[k] % kRansacChunk, c.K);
+                solve_task(k);
                 tk[k] = {std::hash<std::thread::id>{}(std::this_thread::get_id()),
                          std::chrono::duration<double, std::micro>(clk::now() - a).count()};
                 (void)tb;
@@ -1494,13 +1524,13 @@ int svo_frontend_step(svo_frontend* fe, int t, svo_frontend_stats* stats) {
                 sum += e.second;
                 mx = std::max(mx, e.second);
             }
-            std::fprintf(stderr, "[fe t=%d] pool: %zu solves on %zu threads, mean %.1f us, max %.1f us, wall %.1f us\n", t,
-                         tk.size(), ids.size(), tk.empty() ? 0.0 : sum / tk.size(), mx,
+            std::fprintf(stderr,
+                         "[fe t=%d] pool: %zu solves in %zu tasks on %zu threads, mean %.1f us, max %.1f us per task, "
+                         "wall %.1f us\n",
+                         t, flat.size(), tk.size(), ids.size(), tk.empty() ? 0.0 : sum / tk.size(), mx,
                          std::chrono::duration<double, std::micro>(clk::now() - tb).count());
         } else {
-            fe->pool->run((int)flat.size(), [&](int k) {
-                fe->rs[flat[k] / kRansacChunk].solve(flat[k] % kRansacChunk, c.K);
-            });
+            fe->pool->run(ntask, solve_task);
         }
         for (int s = 0; s < S; s++) fe->rs[s].nh += ms[s];
         ms_hyp += ms_since(th);
@@ -1523,8 +1553,9 @@ int svo_frontend_step(svo_frontend* fe, int t, svo_frontend_stats* stats) {
         SVO_HIP(ctx, launch_pnp_score(pb, S, c.K[0], c.K[4], c.K[2], c.K[5], thr, sl));
         ph_end(fe, sl, slot);
         TP("scoring enqueued");
+        const auto tsw = clk::now();
         SVO_HIP(ctx, hipStreamSynchronize(sl));
-        ms_wait += ms_since(tw);
+        ms_wait_score += ms_since(tsw);
         TP("scores on host");
         // consume is a few compares per hypothesis: cheaper here than a pool dispatch
         for (int s = 0; s < S; s++) {
@@ -1592,6 +1623,7 @@ int svo_frontend_step(svo_frontend* fe, int t, svo_frontend_stats* stats) {
     SVO_HIP(ctx, hipStreamWaitEvent(sl, fe->ev_fast, 0));
     // drop the outliers (the kernel reads the inlier bits from host-coherent
     // memory), then the keyframe: candidates, stereo LK, triangulation, append
+    const auto tkq = clk::now();
     rc = fe_keyframe(fe, t, fe->nB, fe->h_best, fe->xyB, fe->midB, max_take, sl, spec_ok);
     if (rc) return rc;
     SVO_HIP(ctx, hipEventRecord(fe->ev_tail, sl));
@@ -1632,11 +1664,12 @@ int svo_frontend_step(svo_frontend* fe, int t, svo_frontend_stats* stats) {
         fe->front_t = t + 1;
     }
     TP("next front queued");
+    ms_enqueue += ms_since(tkq);
     // wait for this step's keyframe only (the statistics, the next frame's
     // pyramid and the prefetched first half keep running into the next step)
     tw = clk::now();
     SVO_HIP(ctx, hipEventSynchronize(fe->ev_tail));
-    ms_wait += ms_since(tw);
+    ms_wait_kf = ms_since(tw);
     TP("synced");
     ph_collect(fe);
     if (tr) {
@@ -1654,8 +1687,19 @@ int svo_frontend_step(svo_frontend* fe, int t, svo_frontend_stats* stats) {
         stats->hypotheses = nhyp;
         stats->host_ms_hyp = ms_hyp;
         stats->host_ms_fit = ms_fit;
-        stats->host_ms_wait = ms_wait;
+        stats->host_ms_wait = ms_wait_post + ms_wait_score + ms_wait_kf;
         stats->keyframes = n_keyframes;
+        stats->host_ms_wait_post = ms_wait_post;
+        stats->host_ms_wait_score = ms_wait_score;
+        stats->host_ms_wait_kf = ms_wait_kf;
+        stats->host_ms_enqueue = ms_enqueue;
+        stats->host_ms_step = ms_since(t_call);
+        stats->ransac_rounds = rounds;
+        int64_t mh = 0;
+        for (int s = 0; s < S; s++) mh = std::max<int64_t>(mh, fe->rs[s].nh);
+        stats->max_hypotheses = mh;
+        stats->serial_keyframe = spec_ok ? 0 : 1;
+        stats->full_copy = have_full ? 1 : 0;
     }
     return SVO_OK;
 }
@@ -1840,6 +1884,35 @@ void svo_frontend_reset_times(svo_frontend* fe) {
         fe->phase_ms[i] = 0;
         fe->phase_n[i] = 0;
     }
+}
+
+int svo_pool_selftest(int threads, int jobs, int64_t* bad) {
+    if (threads < 1 || jobs < 1 || !bad) return SVO_ERR_ARG;
+    // jobs of alternating, growing and shrinking sizes with primes between them
+    // (the front end's pattern: per-hypothesis jobs whose size changes every
+    // round): every task of every job must run exactly once, and no task of an
+    // older job may run after its job returned
+    Pool pool(threads - 1);
+    std::vector<std::atomic<int>> hits(4096);
+    std::atomic<int64_t> errors{0};
+    uint64_t rng = 0x9e3779b97f4a7c15ull;
+    for (int j = 0; j < jobs; j++) {
+        rng = rng * 6364136223846793005ull + 1442695040888963407ull;
+        const int n = (j & 1) ? 1 + (int)((rng >> 33) % 4096) : 1 + (int)((rng >> 33) % 8);
+        for (int i = 0; i < n; i++) hits[i].store(0, std::memory_order_relaxed);
+        const int tag = j;
+        std::atomic<int> live{1};
+        pool.run(n, [&, tag](int i) {
+            if (i < 0 || i >= n || !live.load(std::memory_order_acquire) || tag != j) errors.fetch_add(1);
+            if (i >= 0 && i < n) hits[i].fetch_add(1, std::memory_order_relaxed);
+        });
+        live.store(0, std::memory_order_release);
+        for (int i = 0; i < n; i++)
+            if (hits[i].load(std::memory_order_relaxed) != 1) errors.fetch_add(1);
+        if ((rng >> 20) & 1) pool.prime();
+    }
+    *bad = errors.load();
+    return SVO_OK;
 }
 
 }  // extern "C"

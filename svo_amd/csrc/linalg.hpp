@@ -617,5 +617,414 @@ SVO_HD void rodrigues_inv(const double* Rin, double* rv) {
     rv[2] = rz;
 }
 
+// OpenCV 4.x core/src/lapack.cpp restated: the SVD routines calib3d's EPnP calls
+// (cvSVD, cvInvert(CV_SVD), cvSolve(CV_SVD)) and cv::Rodrigues uses, operation by
+// operation, so that the minimal solver's results do not depend on which Jacobi
+// variant picks a basis of a degenerate singular subspace (the 5-point M^T M has
+// a two-dimensional null space). The oracle restates the same functions
+// (oracle/cvsvd.c); tests/test_epnp_cpu.py holds the two EPnP solvers bit for bit.
+namespace cv {
+
+// lapack.cpp's hypot: the larger operand times sqrt(1 + ratio^2)
+SVO_HD double hypot_cv(double a, double b) {
+    a = fabs(a);
+    b = fabs(b);
+    if (a > b) {
+        b /= a;
+        return a * sqrt(1 + b * b);
+    }
+    if (b > 0) {
+        a /= b;
+        return b * sqrt(1 + a * a);
+    }
+    return 0;
+}
+
+// JacobiSVDImpl_<double>(At, ., W, Vt, ., M, N, n1 = N, DBL_MIN, 10 DBL_EPSILON)
+// with a right-singular-vector buffer present (compute_uv, as every caller here):
+// At (N rows of M) becomes the normalised left singular vectors, W the singular
+// values (descending). WANT_V = false skips the rotations of Vt -- its values
+// never reach At or W -- while keeping every At-side step of the Vt-present path
+// (row swaps in the sort, the normalisation).
+template <int M, int N, bool WANT_V>
+SVO_HD void jacobi_tail(double* At, double* Wout, double* Vt);
+template <int M, int N, bool WANT_V>
+SVO_HD void jacobi_svd(double* At, double* Wout, double* Vt) {
+    const double minval = 2.2250738585072014e-308, eps = 2.220446049250313e-16 * 10;
+    double W[N];
+    constexpr int max_iter = M > 30 ? M : 30;
+    for (int i = 0; i < N; i++) {
+        double sd = 0;
+        for (int k = 0; k < M; k++) sd += At[i * M + k] * At[i * M + k];
+        W[i] = sd;
+        if (WANT_V) {
+            for (int k = 0; k < N; k++) Vt[i * N + k] = 0;
+            Vt[i * N + i] = 1;
+        }
+    }
+    for (int iter = 0; iter < max_iter; iter++) {
+        bool changed = false;
+        for (int i = 0; i < N - 1; i++)
+            for (int j = i + 1; j < N; j++) {
+                double* Ai = At + i * M;
+                double* Aj = At + j * M;
+                double a = W[i], p = 0, b = W[j];
+                for (int k = 0; k < M; k++) p += Ai[k] * Aj[k];
+                if (fabs(p) <= eps * sqrt(a * b)) continue;
+                p *= 2;
+                const double beta = a - b, gamma = hypot_cv(p, beta);
+                double c, s;
+                if (beta < 0) {
+                    const double delta = (gamma - beta) * 0.5;
+                    s = sqrt(delta / gamma);
+                    c = p / (gamma * s * 2);
+                } else {
+                    c = sqrt((gamma + beta) / (gamma * 2));
+                    s = p / (gamma * c * 2);
+                }
+                a = b = 0;
+                for (int k = 0; k < M; k++) {
+                    const double t0 = c * Ai[k] + s * Aj[k];
+                    const double t1 = -s * Ai[k] + c * Aj[k];
+                    Ai[k] = t0;
+                    Aj[k] = t1;
+                    a += t0 * t0;
+                    b += t1 * t1;
+                }
+                W[i] = a;
+                W[j] = b;
+                changed = true;
+                if (WANT_V) {
+                    double* Vi = Vt + i * N;
+                    double* Vj = Vt + j * N;
+                    for (int k = 0; k < N; k++) {
+                        const double t0 = c * Vi[k] + s * Vj[k];
+                        const double t1 = -s * Vi[k] + c * Vj[k];
+                        Vi[k] = t0;
+                        Vj[k] = t1;
+                    }
+                }
+            }
+        if (!changed) break;
+    }
+    jacobi_tail<M, N, WANT_V>(At, Wout, Vt);
+}
+
+// jacobi_svd's tail after the sweeps: singular values, the selection sort (rows
+// of At / Vt swapped), the normalisation of the left vectors (a zero singular
+// value gets a random unit vector orthogonal to the previous ones)
+template <int M, int N, bool WANT_V>
+SVO_HD void jacobi_tail(double* At, double* Wout, double* Vt) {
+    const double minval = 2.2250738585072014e-308, eps = 2.220446049250313e-16 * 10;
+    double W[N];
+    for (int i = 0; i < N; i++) {
+        double sd = 0;
+        for (int k = 0; k < M; k++) sd += At[i * M + k] * At[i * M + k];
+        W[i] = sqrt(sd);
+    }
+    for (int i = 0; i < N - 1; i++) {
+        int j = i;
+        for (int k = i + 1; k < N; k++)
+            if (W[j] < W[k]) j = k;
+        if (i != j) {
+            const double tw = W[i];
+            W[i] = W[j];
+            W[j] = tw;
+            for (int k = 0; k < M; k++) {
+                const double t = At[i * M + k];
+                At[i * M + k] = At[j * M + k];
+                At[j * M + k] = t;
+            }
+            if (WANT_V)
+                for (int k = 0; k < N; k++) {
+                    const double t = Vt[i * N + k];
+                    Vt[i * N + k] = Vt[j * N + k];
+                    Vt[j * N + k] = t;
+                }
+        }
+    }
+    for (int i = 0; i < N; i++) Wout[i] = W[i];
+    unsigned long long rng = 0x12345678ull;
+    for (int i = 0; i < N; i++) {
+        double sd = W[i];
+        for (int ii = 0; ii < 100 && sd <= minval; ii++) {
+            // a zero singular value: a random unit vector orthogonal to the
+            // previous left singular vectors (cv::RNG(0x12345678))
+            const double val0 = 1. / M;
+            for (int k = 0; k < M; k++) {
+                rng = (unsigned long long)(unsigned)rng * 4164903690u + (unsigned)(rng >> 32);
+                At[i * M + k] = ((unsigned)rng & 256) != 0 ? val0 : -val0;
+            }
+            for (int it = 0; it < 2; it++)
+                for (int j = 0; j < i; j++) {
+                    sd = 0;
+                    for (int k = 0; k < M; k++) sd += At[i * M + k] * At[j * M + k];
+                    double asum = 0;
+                    for (int k = 0; k < M; k++) {
+                        const double t = At[i * M + k] - sd * At[j * M + k];
+                        At[i * M + k] = t;
+                        asum += fabs(t);
+                    }
+                    asum = asum > eps * 100 ? 1 / asum : 0;
+                    for (int k = 0; k < M; k++) At[i * M + k] *= asum;
+                }
+            sd = 0;
+            for (int k = 0; k < M; k++) sd += At[i * M + k] * At[i * M + k];
+            sd = sqrt(sd);
+        }
+        const double s = sd > minval ? 1 / sd : 0.;
+        for (int k = 0; k < M; k++) At[i * M + k] *= s;
+    }
+}
+
+// jacobi_svd<M, N, false> of NS independent matrices interleaved pair by pair:
+// every matrix's sweeps, skips, rotations and stop exactly as jacobi_svd (a
+// matrix whose sweep rotated nothing stops; the others go on), so each result is
+// bit-identical to its own jacobi_svd -- the interleaving only lets the host core
+// overlap the NS dependency chains of the sequential dot products and the
+// rotation coefficients (one problem's Jacobi is a single serial chain).
+template <int M, int N, int NS>
+SVO_HD void jacobi_svd_n(double (*At)[N * M], double (*Wout)[N]) {
+    const double minval = 2.2250738585072014e-308, eps = 2.220446049250313e-16 * 10;
+    double W[NS][N];
+    bool live[NS];
+    constexpr int max_iter = M > 30 ? M : 30;
+    for (int q = 0; q < NS; q++) {
+        live[q] = true;
+        for (int i = 0; i < N; i++) {
+            double sd = 0;
+            for (int k = 0; k < M; k++) sd += At[q][i * M + k] * At[q][i * M + k];
+            W[q][i] = sd;
+        }
+    }
+    for (int iter = 0; iter < max_iter; iter++) {
+        bool changed[NS], any = false;
+        for (int q = 0; q < NS; q++) changed[q] = false;
+        for (int i = 0; i < N - 1; i++)
+            for (int j = i + 1; j < N; j++) {
+                double p[NS];
+                for (int q = 0; q < NS; q++) {
+                    p[q] = 0;
+                    if (!live[q]) continue;
+                    const double* Ai = At[q] + i * M;
+                    const double* Aj = At[q] + j * M;
+                    for (int k = 0; k < M; k++) p[q] += Ai[k] * Aj[k];
+                }
+                for (int q = 0; q < NS; q++) {
+                    if (!live[q]) continue;
+                    double a = W[q][i], b = W[q][j], pq = p[q];
+                    if (fabs(pq) <= eps * sqrt(a * b)) continue;
+                    pq *= 2;
+                    const double beta = a - b, gamma = hypot_cv(pq, beta);
+                    double c, s;
+                    if (beta < 0) {
+                        const double delta = (gamma - beta) * 0.5;
+                        s = sqrt(delta / gamma);
+                        c = pq / (gamma * s * 2);
+                    } else {
+                        c = sqrt((gamma + beta) / (gamma * 2));
+                        s = pq / (gamma * c * 2);
+                    }
+                    double* Ai = At[q] + i * M;
+                    double* Aj = At[q] + j * M;
+                    a = b = 0;
+                    for (int k = 0; k < M; k++) {
+                        const double t0 = c * Ai[k] + s * Aj[k];
+                        const double t1 = -s * Ai[k] + c * Aj[k];
+                        Ai[k] = t0;
+                        Aj[k] = t1;
+                        a += t0 * t0;
+                        b += t1 * t1;
+                    }
+                    W[q][i] = a;
+                    W[q][j] = b;
+                    changed[q] = true;
+                }
+            }
+        for (int q = 0; q < NS; q++) {
+            if (!changed[q]) live[q] = false;
+            any = any || live[q];
+        }
+        if (!any) break;
+    }
+    for (int q = 0; q < NS; q++) {
+        double* A = At[q];
+        double* Wq = W[q];
+        for (int i = 0; i < N; i++) {
+            double sd = 0;
+            for (int k = 0; k < M; k++) sd += A[i * M + k] * A[i * M + k];
+            Wq[i] = sqrt(sd);
+        }
+        for (int i = 0; i < N - 1; i++) {
+            int j = i;
+            for (int k = i + 1; k < N; k++)
+                if (Wq[j] < Wq[k]) j = k;
+            if (i != j) {
+                const double tw = Wq[i];
+                Wq[i] = Wq[j];
+                Wq[j] = tw;
+                for (int k = 0; k < M; k++) {
+                    const double t = A[i * M + k];
+                    A[i * M + k] = A[j * M + k];
+                    A[j * M + k] = t;
+                }
+            }
+        }
+        for (int i = 0; i < N; i++) Wout[q][i] = Wq[i];
+        unsigned long long rng = 0x12345678ull;
+        for (int i = 0; i < N; i++) {
+            double sd = Wq[i];
+            for (int ii = 0; ii < 100 && sd <= minval; ii++) {
+                const double val0 = 1. / M;
+                for (int k = 0; k < M; k++) {
+                    rng = (unsigned long long)(unsigned)rng * 4164903690u + (unsigned)(rng >> 32);
+                    A[i * M + k] = ((unsigned)rng & 256) != 0 ? val0 : -val0;
+                }
+                for (int it = 0; it < 2; it++)
+                    for (int j = 0; j < i; j++) {
+                        sd = 0;
+                        for (int k = 0; k < M; k++) sd += A[i * M + k] * A[j * M + k];
+                        double asum = 0;
+                        for (int k = 0; k < M; k++) {
+                            const double t = A[i * M + k] - sd * A[j * M + k];
+                            A[i * M + k] = t;
+                            asum += fabs(t);
+                        }
+                        asum = asum > eps * 100 ? 1 / asum : 0;
+                        for (int k = 0; k < M; k++) A[i * M + k] *= asum;
+                    }
+                sd = 0;
+                for (int k = 0; k < M; k++) sd += A[i * M + k] * A[i * M + k];
+                sd = sqrt(sd);
+            }
+            const double s = sd > minval ? 1 / sd : 0.;
+            for (int k = 0; k < M; k++) A[i * M + k] *= s;
+        }
+    }
+}
+
+// cvMulTransposed(src, dst, 1): dst = src^T src (ROWS x COLS src), each upper
+// element summed over the rows in order, the lower triangle mirrored
+template <int COLS>
+SVO_HD void mul_transposed(const double* src, int rows, double* dst) {
+    for (int i = 0; i < COLS; i++)
+        for (int j = i; j < COLS; j++) {
+            double s = 0;
+            for (int k = 0; k < rows; k++) s += src[k * COLS + i] * src[k * COLS + j];
+            dst[i * COLS + j] = s;
+        }
+    for (int i = 0; i < COLS; i++)
+        for (int j = 0; j < i; j++) dst[i * COLS + j] = dst[j * COLS + i];
+}
+
+// cvSVD(A, W, Ut, 0, CV_SVD_U_T) of a square N x N A: rows of ut = left singular
+// vectors
+template <int N>
+SVO_HD void svd_ut(const double* A, double* w, double* ut) {
+    for (int i = 0; i < N; i++)
+        for (int k = 0; k < N; k++) ut[i * N + k] = A[k * N + i];
+    jacobi_svd<N, N, false>(ut, w, nullptr);
+}
+
+// SVD::compute of a square N x N A: u (columns = left vectors), vt (rows)
+template <int N>
+SVO_HD void svd(const double* A, double* w, double* u, double* vt) {
+    double At[N * N];
+    for (int i = 0; i < N; i++)
+        for (int k = 0; k < N; k++) At[i * N + k] = A[k * N + i];
+    jacobi_svd<N, N, true>(At, w, vt);
+    for (int k = 0; k < N; k++)
+        for (int i = 0; i < N; i++) u[k * N + i] = At[i * N + k];
+}
+
+// cv::solve(A, b, x, DECOMP_SVD), one right-hand side, A M x N (M >= N)
+template <int M, int N>
+SVO_HD void solve_svd(const double* A, const double* b, double* x) {
+    double At[N * M], V[N * N], w[N];
+    for (int i = 0; i < N; i++)
+        for (int k = 0; k < M; k++) At[i * M + k] = A[k * N + i];
+    jacobi_svd<M, N, true>(At, w, V);
+    double threshold = 0;
+    for (int j = 0; j < N; j++) x[j] = 0;
+    for (int i = 0; i < N; i++) threshold += w[i];
+    threshold *= 2.220446049250313e-16 * 2;
+    for (int i = 0; i < N; i++) {
+        double wi = w[i];
+        if (fabs(wi) <= threshold) continue;
+        wi = 1 / wi;
+        double s = 0;
+        for (int j = 0; j < M; j++) s += At[i * M + j] * b[j];
+        s *= wi;
+        for (int j = 0; j < N; j++) x[j] = x[j] + s * V[i * N + j];
+    }
+}
+
+// cv::invert(A, Ai, DECOMP_SVD) of an N x N A (SVD::backSubst with the identity)
+template <int N>
+SVO_HD void invert_svd(const double* A, double* Ai) {
+    double u[N * N], vt[N * N], w[N], buf[N];
+    svd<N>(A, w, u, vt);
+    double threshold = 0;
+    for (int i = 0; i < N * N; i++) Ai[i] = 0;
+    for (int i = 0; i < N; i++) threshold += w[i];
+    threshold *= 2.220446049250313e-16 * 2;
+    for (int i = 0; i < N; i++) {
+        double wi = w[i];
+        if (fabs(wi) <= threshold) continue;
+        wi = 1 / wi;
+        for (int j = 0; j < N; j++) buf[j] = u[j * N + i] * wi;
+        for (int r = 0; r < N; r++) {
+            const double sv = vt[i * N + r];
+            for (int j = 0; j < N; j++) Ai[r * N + j] = Ai[r * N + j] + sv * buf[j];
+        }
+    }
+}
+
+// cv::Rodrigues matrix -> vector: SVD::compute(R, W, U, Vt), R = U * Vt (Matx
+// product), then the axis-angle extraction (same as la::rodrigues_inv's)
+SVO_HD void rodrigues_inv(const double* Rin, double* rv) {
+    double w[3], u[9], vt[9], R[9];
+    svd<3>(Rin, w, u, vt);
+    for (int i = 0; i < 3; i++)
+        for (int j = 0; j < 3; j++) {
+            double acc = 0;
+            for (int k = 0; k < 3; k++) acc += u[i * 3 + k] * vt[k * 3 + j];
+            R[i * 3 + j] = acc;
+        }
+    double rx = R[7] - R[5], ry = R[2] - R[6], rz = R[3] - R[1];
+    const double s = sqrt((rx * rx + ry * ry + rz * rz) * 0.25);
+    double c = (R[0] + R[4] + R[8] - 1) * 0.5;
+    c = c > 1. ? 1. : c < -1. ? -1. : c;
+    double th = acos(c);
+    if (s < 1e-5) {
+        if (c > 0) {
+            rx = ry = rz = 0;
+        } else {
+            double t = (R[0] + 1) * 0.5;
+            rx = sqrt(t > 0 ? t : 0.);
+            t = (R[4] + 1) * 0.5;
+            ry = sqrt(t > 0 ? t : 0.) * (R[1] < 0 ? -1. : 1.);
+            t = (R[8] + 1) * 0.5;
+            rz = sqrt(t > 0 ? t : 0.) * (R[2] < 0 ? -1. : 1.);
+            if (fabs(rx) < fabs(ry) && fabs(rx) < fabs(rz) && (R[5] > 0) != (ry * rz > 0)) rz = -rz;
+            th /= sqrt(rx * rx + ry * ry + rz * rz);
+            rx *= th;
+            ry *= th;
+            rz *= th;
+        }
+    } else {
+        double vth = 1 / (2 * s);
+        vth *= th;
+        rx *= vth;
+        ry *= vth;
+        rz *= vth;
+    }
+    rv[0] = rx;
+    rv[1] = ry;
+    rv[2] = rz;
+}
+
+}  // namespace cv
+
 }  // namespace la
 }  // namespace svo

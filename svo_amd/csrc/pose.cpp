@@ -23,6 +23,7 @@
 
 #include "common.hpp"
 #include "epnp.hpp"
+#include "simd_svd.hpp"
 #include "linalg.hpp"
 #include "pose.hpp"
 
@@ -393,30 +394,93 @@ int RansacSeq::draw_chunk() {
     return want;
 }
 
-void RansacSeq::solve(int j, const double K[9]) {
-    double Rj[9], tj[3], rv[3];
+void RansacSeq::subset(int j, const float** o, const float** im, const int** id) const {
     const int h = nh + j;
     if (h < nsamp) {  // the same 5 points, gathered on the device in draw order
         const float* sp = samp + (size_t)kSampleFloats * h;
-        valid[j] = epnp_pixels(sp, sp + 15, nullptr, 5, K, Rj, tj);
+        *o = sp;
+        *im = sp + 15;
+        *id = nullptr;
     } else {
-        valid[j] = epnp_pixels(obj, img, idx[j], 5, K, Rj, tj);
+        *o = obj;
+        *im = img;
+        *id = idx[j];
     }
+}
+
+void RansacSeq::store(int j, bool valid_model, const double R[9], const double t[3]) {
+    valid[j] = valid_model;
     double* hp = hyp + 12 * j;
-    if (valid[j]) {
-        la::rodrigues_inv(Rj, rv);  // the model is stored as (rvec, tvec)
+    if (valid_model) {
+        double rv[3];
+        la::cv::rodrigues_inv(R, rv);  // the model is stored as (rvec, tvec)
         la::rodrigues(rv, hp);
-        std::memcpy(hp + 9, tj, sizeof(tj));
+        std::memcpy(hp + 9, t, sizeof(double) * 3);
     } else {
         for (int k = 0; k < 12; k++) hp[k] = 0;
     }
 }
 
+void RansacSeq::solve(int j, const double K[9]) {
+    const float *o, *im;
+    const int* id;
+    subset(j, &o, &im, &id);
+    double Rj[9], tj[3];
+    const bool v = epnp_pixels(o, im, id, 5, K, Rj, tj);
+    store(j, v, Rj, tj);
+}
+
+void epnp_pixels_batch(int count, const float* const* obj, const float* const* img, const int* const* idx,
+                       const double K[9], double (*R)[9], double (*t)[3], bool* ok) {
+    constexpr int L = kEpnpLanes;
+    if (count <= 0) return;
+    if (count > L) count = L;
+    double pw[L][15], uv[L][10], MtM[L][144], ev[L][12], ut[L][144];
+    EPnP es[L] = {EPnP(K[0], K[4], K[2], K[5]), EPnP(K[0], K[4], K[2], K[5]), EPnP(K[0], K[4], K[2], K[5]),
+                  EPnP(K[0], K[4], K[2], K[5])};
+    for (int q = 0; q < count; q++) {
+        epnp_inputs(obj[q], img[q], idx[q], 5, K, pw[q], uv[q]);
+        es[q].prepare(pw[q], uv[q], 5, MtM[q]);
+    }
+    if (count > 1 && la::cv::simd_svd_ok()) {
+        const double* pa[L];
+        double *pe[L], *pu[L];
+        for (int q = 0; q < L; q++) {
+            pa[q] = MtM[q < count ? q : count - 1];  // idle lanes repeat a live problem
+            pe[q] = ev[q];
+            pu[q] = ut[q];
+        }
+        la::cv::svd_ut_lanes<12, L, 1>(pa, pe, pu);
+    } else {
+        for (int q = 0; q < count; q++) la::cv::svd_ut<12>(MtM[q], ev[q], ut[q]);
+    }
+    for (int q = 0; q < count; q++) ok[q] = es[q].finish(ut[q], R[q], t[q]);
+}
+
 int RansacSeq::gen_chunk(const double K[9]) {
     const int want = draw_chunk();
-    for (int j = 0; j < want; j++) solve(j, K);
+    for (int j0 = 0; j0 < want; j0 += kEpnpLanes) {
+        RansacSeq* seqs[kEpnpLanes];
+        int js[kEpnpLanes];
+        const int c = want - j0 < kEpnpLanes ? want - j0 : kEpnpLanes;
+        for (int q = 0; q < c; q++) {
+            seqs[q] = this;
+            js[q] = j0 + q;
+        }
+        solve_hypotheses(seqs, js, c, K);
+    }
     nh += want;
     return want;
+}
+
+void solve_hypotheses(RansacSeq* const* seqs, const int* js, int count, const double K[9]) {
+    const float *o[kEpnpLanes], *im[kEpnpLanes];
+    const int* id[kEpnpLanes];
+    double R[kEpnpLanes][9], t[kEpnpLanes][3];
+    bool ok[kEpnpLanes];
+    for (int q = 0; q < count; q++) seqs[q]->subset(js[q], &o[q], &im[q], &id[q]);
+    epnp_pixels_batch(count, o, im, id, K, R, t, ok);
+    for (int q = 0; q < count; q++) seqs[q]->store(js[q], ok[q], R[q], t[q]);
 }
 
 void RansacSeq::consume(const int* counts, const uint32_t* bits, int words_cap, double confidence) {
@@ -443,7 +507,7 @@ void RansacSeq::select(const double K[9], bool list) {
     if (direct) {
         double R[9], t[3];
         if (!epnp_pixels(obj, img, nullptr, n, K, R, t)) return;
-        la::rodrigues_inv(R, rvec);
+        la::cv::rodrigues_inv(R, rvec);
         std::memcpy(tvec, t, sizeof(t));
         for (int i = 0; i < n; i++) inliers.push_back(i);
         for (int i = 0; i < n; i++) best[i >> 5] |= 1u << (i & 31);
@@ -490,7 +554,7 @@ void RansacSeq::fit(const double K[9], const double* sums) {
     sqpnp_assemble(sums, c);
     fitted = true;
     if (!c.ok) {  // solvePnP(SQPNP) would assert: keep the RANSAC model (as the oracle)
-        la::rodrigues_inv(bestR, rvec);
+        la::cv::rodrigues_inv(bestR, rvec);
         std::memcpy(tvec, bestt, sizeof(bestt));
         return;
     }
@@ -506,11 +570,11 @@ void RansacSeq::fit(const double K[9], const double* sums) {
         },
         Rf, tf, &found);
     if (!found) {  // no solution in front of the camera: solvePnP fails, keep the RANSAC model
-        la::rodrigues_inv(bestR, rvec);
+        la::cv::rodrigues_inv(bestR, rvec);
         std::memcpy(tvec, bestt, sizeof(bestt));
         return;
     }
-    la::rodrigues_inv(Rf, rvec);
+    la::cv::rodrigues_inv(Rf, rvec);
     std::memcpy(tvec, tf, sizeof(tf));
 }
 
@@ -543,7 +607,7 @@ extern "C" int svo_solve_pnp_sqpnp(const double* obj_xyz, const float* img_xy, i
     fit_from_cost(
         c, n, [&](int k, double* p) { std::memcpy(p, obj_xyz + 3 * (size_t)k, sizeof(double) * 3); }, R, t, &found);
     if (!found) return 0;
-    la::rodrigues_inv(R, rvec);
+    la::cv::rodrigues_inv(R, rvec);
     std::memcpy(tvec, t, sizeof(t));
     return 1;
 }

@@ -21,6 +21,18 @@ constexpr int kRansacChunk = 16;  // hypotheses generated per scoring launch
 constexpr int kRansacPrefetch = 26;
 constexpr int kSampleFloats = 25;  // 5 points x (obj xyz, pixel xy)
 
+// The RANSAC minimal solver batched: EPnP of count <= kEpnpLanes 5-point subsets
+// (subset q: points idx[q][0..5) of obj[q] / img[q], or points 0..4 when idx[q]
+// is null), bit-identical to epnp_pixels on each, the 12 x 12 M^T M SVDs run in
+// SIMD lanes together (simd_svd.hpp). ok[q]: finite model.
+constexpr int kEpnpLanes = 4;
+void epnp_pixels_batch(int count, const float* const* obj, const float* const* img, const int* const* idx,
+                       const double K[9], double (*R)[9], double (*t)[3], bool* ok);
+struct RansacSeq;
+// hypotheses js[q] of sequences seqs[q] (q < count <= kEpnpLanes; drawn by
+// draw_chunk) solved as one epnp_pixels_batch and stored (RansacSeq::store)
+void solve_hypotheses(RansacSeq* const* seqs, const int* js, int count, const double K[9]);
+
 // RANSACPointSetRegistrator::run for PnP (5-point EPnP kernel), split so the
 // hypotheses of many sequences are scored by one batched kernel launch:
 //   begin -> { gen_chunk -> [GPU: score m hypotheses] -> consume } until done -> finish
@@ -57,6 +69,10 @@ struct RansacSeq {
     // m; solve(j) fills hypothesis j < m
     int draw_chunk();
     void solve(int j, const double K[9]);
+    // solve(j) in two halves around a batched EPnP (epnp_pixels_batch): the
+    // subset's points, and the model stored as (rvec, tvec) -> hyp[j]
+    void subset(int j, const float** o, const float** im, const int** id) const;
+    void store(int j, bool valid_model, const double R[9], const double t[3]);
     // hypotheses generated once the next gen_chunk has run (for deciding whether
     // the full point arrays must be on the host first)
     int next_end() const;

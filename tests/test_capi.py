@@ -71,3 +71,12 @@ def test_stereo_synth_is_consistent_with_depth_field():
     patch = L[y - 6:y + 7, x - 6:x + 7].astype(int)
     sad = [np.abs(R[y - 6:y + 7, x - k - 6:x - k + 7].astype(int) - patch).sum() for k in range(0, 40)]
     assert abs(int(np.argmin(sad)) - d) <= 1.0
+
+
+def test_host_pool_runs_every_task_exactly_once():
+    """The front end's host pool (frontend.cpp Pool) under its real pattern: jobs of
+    sizes that change every round (one RANSAC hypothesis per task) with primes
+    between them. A worker left over from an older job must never claim a task
+    of a newer one (the claim word carries generation and count together)."""
+    for threads in (2, 5, 16):
+        assert S.pool_selftest(threads, 4000) == 0, threads

@@ -441,10 +441,11 @@ def _reproj(R, t, sub, K):
 
 
 def test_epnp_wave_matches_host(ctx):
-    """RANSAC's EPnP minimal solver run one 64-lane wave per subset on the GPU
-    (epnp_wave.hpp) vs the host solver the front end uses: bit-identical R / t on
-    5-point subsets of the RANSAC test problems (clean, with outliers, and the
-    near-threshold set)."""
+    """The QL-based EPnP run one 64-lane wave per subset on the GPU (epnp_wave.hpp,
+    off the front end's path) vs its host twin (epnp_ql.hpp, device = 2):
+    bit-identical R / t on 5-point subsets of the RANSAC test problems (clean,
+    with outliers, and the near-threshold set). The front end's own solver
+    (device = 0) is bit-identical to the oracle's (tests/test_epnp_cpu.py)."""
     rng = np.random.default_rng(5)
     subs, clean = [], []
     for seed in range(3):
@@ -456,7 +457,7 @@ def test_epnp_wave_matches_host(ctx):
     subs = np.array(subs, np.float32)
     K = Scene(1241, 376, seed=0).K
     Rd, okd = ctx.epnp_subsets(subs, K, device=True)
-    Rh, okh = ctx.epnp_subsets(subs, K, device=False)
+    Rh, okh = ctx.epnp_subsets(subs, K, device=2)
     assert okh.sum() == len(subs)
     assert np.array_equal(okd, okh)
     assert np.array_equal(Rd.view(np.uint64), Rh.view(np.uint64))
