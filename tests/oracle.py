@@ -229,6 +229,16 @@ def solve_pnp_ransac(obj, img, K, iterations=100, reproj=8.0, confidence=0.999):
     return rc, rv, tv, np.nonzero(mask[:n])[0].astype(np.int32), nh.value
 
 
+def ransac_subsets(n, count):
+    """The first `count` 5-point subsets solvePnPRansac draws for n points
+    (RANSACPointSetRegistrator::getSubset with RNG(-1), ptsetreg.cpp)."""
+    st = C.c_uint64(0xFFFFFFFFFFFFFFFF)
+    out = np.empty((count, 5), np.int32)
+    for k in range(count):
+        load().svo_oracle_get_subset(C.byref(st), n, 5, _p(out[k], _i32p))
+    return out
+
+
 def sqpnp(pw, q):
     """calib3d/src/sqpnp.cpp PoseSolver on object points pw (n, 3) and normalised
     image points q (n, 2): (rc, R, t), rc 0 on success."""

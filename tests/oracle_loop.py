@@ -91,8 +91,10 @@ class OracleLoop:
         p2, X2 = nx[keep], self.X[keep]
         stats = {"lk_iterations": int(it.sum()), "tracked": int(keep.sum())}
         rv, tv = np.zeros(3), np.zeros(3)
+        self.last_pnp = (X2, p2, 0)  # the RANSAC's inputs (tests replay its hypotheses)
         if len(p2) >= 4:
             rc, rv_, tv_, inl, nh = O.solve_pnp_ransac(X2, p2, self.sc.K)
+            self.last_pnp = (X2, p2, nh)
             if rc == 1:
                 p2, X2 = p2[inl], X2[inl]
                 rv, tv = rv_, tv_

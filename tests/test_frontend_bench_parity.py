@@ -127,3 +127,70 @@ def test_frontend_scharr_pyramid_1080p_all_levels():
                 assert np.array_equal(iy.astype(np.int32), 4 * ref[..., 1]), f"seq {s} t {t} iy level {level}"
                 lvl = O.pyr_down(lvl)
     fe.close()
+
+
+def test_bench_forward_128_slots_match_oracle_loop():
+    """bench.py's `workloads.forward` at its own size: 1241x376 / 2000 features /
+    maxLevel 3, 128 batch slots filled by the 16 distinct SceneForward sequences
+    (seeds 1000..1015, each in 8 slots) -- the workload with real RANSAC outliers
+    (occluder + parallax, ~10 % dropped per frame, ~8 hypotheses per sequence).
+    All 16 distinct sequences against their own oracle loop at every step: inlier
+    sets (the feature lists after outlier removal and the keyframe), counts,
+    hypotheses, poses and map points; every hypothesis the oracle's RANSAC drew is
+    re-solved by the product's minimal solver and counted when its bits differ
+    (printed, asserted 0); every other slot bitwise equal to its twin slot."""
+    from svo_amd.scene import SceneForward
+    W, H, N, ML, _ = bench.CONFIGS["kitti"]
+    ctx = S.Context(0)
+    T, n_dist, n_seq = 7, 16, 128
+    scs = [SceneForward(W, H, seed=1000 + i) for i in range(n_dist)]
+    pairs = [[(sc.frame(t), sc.right(t)) for t in range(T)] for sc in scs]
+    fe = S.Frontend(ctx, S.FrontendConfig(W, H, scs[0].K, n_seq=n_seq, n_frames=T, n_features=N, max_level=ML,
+                                          timing=0))
+    for s in range(n_seq):
+        for t in range(T):
+            fe.set_frame(s, t, *pairs[s % n_dist][t])
+    fe.init(0)
+    refs = [OracleLoop(SceneForward(W, H, seed=1000 + i), N, max_level=ML).init(0, *pairs[i][0])
+            for i in range(n_dist)]
+    K = scs[0].K
+    hyps = differ = 0
+    drops = []
+    for t in range(1, T):
+        st = fe.step(t).as_dict()
+        rss = [r.step(t, *pairs[i][t]) for i, r in enumerate(refs)]
+        reps = n_seq // n_dist
+        for k in ("tracked", "inliers", "added", "features", "lk_iterations"):
+            assert st[k] == reps * sum(rs[k] for rs in rss), f"{k} differs at t={t}"
+        # (the product scores whole chunks: a hypothesis drawn past an accept that
+        # lowered niters is scored and ignored, so it scores at least as many)
+        assert st["hypotheses"] >= reps * sum(rs.get("hypotheses", 0) for rs in rss), f"hypotheses at t={t}"
+        for i, ref in enumerate(refs):
+            assert np.array_equal(fe.features(i), ref.pts), f"seq {i}: features differ at t={t}"
+            rv, tv = fe.pose(i)
+            np.testing.assert_allclose(rv, ref.pose[0], atol=1e-7)
+            np.testing.assert_allclose(tv, ref.pose[1], atol=1e-6)
+            if t % 3 == 0:
+                np.testing.assert_allclose(fe.map_points(i), ref.X, rtol=2e-5, atol=1e-6)
+            # the hypotheses of this step's RANSAC, product minimal solver vs oracle
+            X2, p2, nh = ref.last_pnp
+            if nh:
+                obj = X2.astype(np.float32)
+                img = np.ascontiguousarray(p2, np.float32)
+                idx = O.ransac_subsets(len(obj), nh)
+                subs = np.concatenate([obj[idx].reshape(nh, 15), img[idx].reshape(nh, 10)], axis=1)
+                Rt, ok = ctx.epnp_subsets(subs, K, device=0)
+                for k in range(nh):
+                    rc, Ro, to = O.epnp(obj[idx[k]], img[idx[k]], K)
+                    same = (rc == 0) == bool(ok[k]) and (rc != 0 or np.array_equal(
+                        np.r_[Ro.ravel(), to].view(np.uint64), Rt[k].view(np.uint64)))
+                    differ += not same
+                hyps += nh
+        drops.append(1 - st["inliers"] / st["tracked"])
+        for s in range(n_dist, n_seq, 37):  # twin slots
+            assert np.array_equal(fe.features(s), fe.features(s % n_dist)), f"slot {s} vs {s % n_dist} at t={t}"
+    print(f"forward 128 slots: RANSAC drops {np.round(drops, 3)}; {hyps} oracle hypotheses re-solved by the "
+          f"product's EPnP, {differ} differ")
+    assert differ == 0
+    assert np.mean(drops) > 0.05, "the occluder should make RANSAC outliers"
+    fe.close()
