@@ -306,7 +306,9 @@ typedef struct svo_frontend_stats {
     int64_t max_hypotheses;     /* most hypotheses any one sequence scored */
     int64_t serial_keyframe;    /* 1: the speculative stereo LK missed, serial keyframe ran */
     int64_t full_copy;          /* 1: the full point copy was waited for (long RANSAC / n <= 5) */
-    int64_t kf_overflow;        /* corners a keyframe could not take for lack of capacity */
+    int64_t kf_overflow;        /* SVO_KF_REFERENCE: masked corners a keyframe left out for
+                                   lack of capacity (n_features); 0 = every corner taken,
+                                   as extractFeatures (R:src/tracking.cpp:74-92) */
 } svo_frontend_stats;
 
 int svo_frontend_create(svo_ctx* ctx, const svo_frontend_config* cfg, svo_frontend** out);

@@ -321,6 +321,7 @@ __device__ __forceinline__ void tail_body(const TailBatch& T, int s, bool copy_c
     if (threadIdx.x == 0) {
         T.n_out[s] = n;
         T.st_n[s] = take;
+        if (T.h_over) T.h_over[s] = max(T.cand_n[s] - take, 0);
     }
     *n_kept = n;
     *take_out = take;
@@ -349,10 +350,9 @@ __device__ __forceinline__ bool stereo_point(const float* P, float y_threshold, 
     return keep;
 }
 
-// findLeftFeaturesInRight's filter + triangulateNewMapPoints + append for the
-// stereo matches of st_xy[0, take) of sequence s, n0 features already kept.
-// PRE: the filter and the points come from stereo_tri_kernel (A.st_X).
-template <int BS, bool PRE>
+// The append of the stereo matches of st_xy[0, take) of sequence s, n0 features
+// already kept: the filter and the points come from stereo_tri_kernel (A.st_X).
+template <int BS>
 __device__ __forceinline__ void append_body(const AppendBatch& A, int s, int n0, int take, int* wsum, int* base_sp) {
     int& base_s = *base_sp;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
@@ -368,16 +368,11 @@ __device__ __forceinline__ void append_body(const AppendBatch& A, int s, int n0,
         if (j < take) {
             xl = A.st_xy[2 * (o + j)];
             yl = A.st_xy[2 * (o + j) + 1];
-            if (PRE) {
-                const float4 v = A.st_X[o + j];
-                x3[0] = v.x;
-                x3[1] = v.y;
-                x3[2] = v.z;
-                keep = v.w != 0.f;
-            } else {
-                keep = stereo_point(A.P, A.y_threshold, A.st_status[o + j] != 0, xl, yl, A.st_next[2 * (o + j)],
-                                    A.st_next[2 * (o + j) + 1], x3);
-            }
+            const float4 v = A.st_X[o + j];
+            x3[0] = v.x;
+            x3[1] = v.y;
+            x3[2] = v.z;
+            keep = v.w != 0.f;
         }
         const unsigned long long bal = __ballot(keep);
         if (lane == 0) wsum[wv] = __popcll(bal);
@@ -422,7 +417,7 @@ __global__ __launch_bounds__(BS) void append_kernel(AppendBatch A) {
     __shared__ int wsum[BS / 64];
     __shared__ int base_s;
     const int s = blockIdx.x;
-    append_body<BS, false>(A, s, A.n[s], A.st_n[s], wsum, &base_s);
+    append_body<BS>(A, s, A.n[s], A.st_n[s], wsum, &base_s);
 }
 
 template <int BS>
@@ -433,7 +428,7 @@ __global__ __launch_bounds__(BS) void keyframe_fused_kernel(TailBatch T, AppendB
     const int s = blockIdx.x;
     int n, take;
     tail_body<BS>(T, s, false, wsum, &base_s, &n, &take, cnt);
-    append_body<BS, true>(A, s, n, take, wsum, &base_s);
+    append_body<BS>(A, s, n, take, wsum, &base_s);
 }
 
 __global__ __launch_bounds__(256) void stereo_tri_kernel(StereoTriBatch B) {

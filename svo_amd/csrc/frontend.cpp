@@ -261,13 +261,11 @@ int local_world_env() {
     return e ? std::max(1, std::atoi(e)) : 1;
 }
 
-// host-side step trace (SVO_FE_TRACE=1): label + microseconds since step start
-bool trace_on() {
-    static const bool on = [] {
-        const char* e = std::getenv("SVO_FE_TRACE");
-        return e && e[0] == '1';
-    }();
-    return on;
+// host-side step trace (SVO_FE_TRACE=1, read when a front end is created): label
+// + microseconds since step start
+bool trace_env() {
+    const char* e = std::getenv("SVO_FE_TRACE");
+    return e && e[0] == '1';
 }
 
 // NUMA node of HIP device d (-1: unknown), from its PCI address in sysfs
@@ -326,6 +324,7 @@ struct svo_frontend {
     // speculative stereo LK of step t goes out in its first half, behind FAST(t),
     // sized from the features before LK (nA) with margin spec_margin + lk_loss
     int spec_early = 1;
+    bool trace = false;  // SVO_FE_TRACE=1 at create
     int spec_t = -1;       // step whose speculation went out early
     int spec_m = 0;        // its margin (features lost to LK + RANSAC it covers)
     bool spec_was_early = false;
@@ -349,7 +348,7 @@ struct svo_frontend {
     // the critical path): post-LK counts / iteration sums / RANSAC subsets, the
     // keyframe's counts, the inlier bits, statistics, poses, keyframe targets
     void* zout = nullptr;
-    int *h_nB, *h_nA, *h_added, *h_target;
+    int *h_nB, *h_nA, *h_added, *h_target, *h_over;
     long long* h_itsum;
     float* h_samp;
     double *h_stats, *h_pose;   // h_pose: [s][12] camera -> world of the last fitted frame
@@ -540,6 +539,23 @@ int fe_stereo_lk(svo_frontend* fe, int t, const int* counts, int max_n, hipStrea
     return SVO_OK;
 }
 
+// stereo_tri_kernel's inputs for the candidates st_xy[0, counts[s]) (the
+// speculative ones: spec_n; the serial keyframe's take: st_n)
+StereoTriBatch fe_tri_batch(svo_frontend* fe, const int* counts) {
+    const svo_frontend_config& c = fe->cfg;
+    StereoTriBatch tb;
+    tb.st_xy = fe->st_xy;
+    tb.st_next = fe->st_next;
+    tb.st_status = fe->st_status;
+    tb.spec_n = counts;
+    tb.cap = fe->CAP;
+    tb.y_threshold = c.y_threshold;
+    std::memcpy(tb.P, c.P_left, sizeof(float) * 12);
+    std::memcpy(tb.P + 12, c.P_right, sizeof(float) * 12);
+    tb.st_X = fe->st_X;
+    return tb;
+}
+
 // The keyframe of every sequence on stream st (R:src/tracking.cpp:247-255):
 // outlier compaction (inlier bits `bits`, or every point when n_in is all zero)
 // + the first candidates up to the sequence's target (h_target: n_features on a
@@ -575,18 +591,14 @@ int fe_keyframe(svo_frontend* fe, int t, const int* n_in, const uint32_t* bits, 
     tb.map_cap = fe->MAPCAP;
     tb.st_xy = fe->st_xy;
     tb.st_n = fe->st_n;
+    tb.h_over = fe->h_over;
     AppendBatch ab;
     ab.n = fe->nA;
     ab.xy = fe->xyA;
     ab.mid = fe->midA;
     ab.cap = fe->CAP;
     ab.st_xy = fe->st_xy;
-    ab.st_next = fe->st_next;
-    ab.st_status = fe->st_status;
     ab.st_n = fe->st_n;
-    ab.y_threshold = c.y_threshold;
-    std::memcpy(ab.P, c.P_left, sizeof(float) * 12);
-    std::memcpy(ab.P + 12, c.P_right, sizeof(float) * 12);
     ab.map = fe->map;
     ab.map_n = fe->map_n;
     ab.map_cap = fe->MAPCAP;
@@ -607,6 +619,9 @@ int fe_keyframe(svo_frontend* fe, int t, const int* n_in, const uint32_t* bits, 
     ph_end(fe, st, slot);
     int rc = fe_stereo_lk(fe, t, fe->st_n, max_take, st);
     if (rc) return rc;
+    // the take's filter + DLT (the same kernel as behind the speculative stereo
+    // LK), then the append compacts
+    SVO_HIP(ctx, launch_stereo_tri(fe_tri_batch(fe, fe->st_n), fe->S, max_take, st));
     ph_begin(fe, PH_APPEND, st, &slot);
     SVO_HIP(ctx, launch_append(ab, fe->S, st));
     ph_end(fe, st, slot);
@@ -656,17 +671,7 @@ int fe_queue_spec(svo_frontend* fe, int t, bool early) {
     const int hint = std::min(fe->CAP, c.n_features - fe->min_tracked + margin + 32);
     int rc = fe_stereo_lk(fe, t, fe->spec_n, max_spec, sf, hint);
     if (rc) return rc;
-    StereoTriBatch tb;
-    tb.st_xy = fe->st_xy;
-    tb.st_next = fe->st_next;
-    tb.st_status = fe->st_status;
-    tb.spec_n = fe->spec_n;
-    tb.cap = fe->CAP;
-    tb.y_threshold = c.y_threshold;
-    std::memcpy(tb.P, c.P_left, sizeof(float) * 12);
-    std::memcpy(tb.P + 12, c.P_right, sizeof(float) * 12);
-    tb.st_X = fe->st_X;
-    SVO_HIP(ctx, launch_stereo_tri(tb, fe->S, hint, sf));
+    SVO_HIP(ctx, launch_stereo_tri(fe_tri_batch(fe, fe->spec_n), fe->S, hint, sf));
     SVO_HIP(ctx, hipEventRecord(fe->ev_fast, sf));
     fe->spec_t = t;
     fe->spec_m = margin;
@@ -897,7 +902,7 @@ int svo_frontend_create(svo_ctx* ctx, const svo_frontend_config* cfg, svo_fronte
     {
         size_t zb = 0;
         auto add = [&](size_t b) { zb = ((zb + 255) & ~(size_t)255) + b; };
-        add(sizeof(int) * S * 4);
+        for (int k = 0; k < 5; k++) add(sizeof(int) * S);  // h_nB, h_nA, h_added, h_target, h_over
         add(sizeof(long long) * S);
         add(sizeof(float) * kSampleFloats * kRansacPrefetch * (size_t)S);
         add(sizeof(uint32_t) * (size_t)S * fe->WORDS);
@@ -916,6 +921,7 @@ int svo_frontend_create(svo_ctx* ctx, const svo_frontend_config* cfg, svo_fronte
         fe->h_nA = carve<int>(p, S);
         fe->h_added = carve<int>(p, S);
         fe->h_target = carve<int>(p, S);
+        fe->h_over = carve<int>(p, S);
         fe->h_itsum = carve<long long>(p, S);
         fe->h_samp = carve<float>(p, (size_t)kSampleFloats * kRansacPrefetch * S);
         fe->h_best_b[0] = carve<uint32_t>(p, (size_t)S * fe->WORDS);
@@ -958,6 +964,7 @@ int svo_frontend_create(svo_ctx* ctx, const svo_frontend_config* cfg, svo_fronte
         fe->spec_margin = sm ? std::atoi(sm) : 32;
         const char* se = std::getenv("SVO_FE_SPEC_EARLY");
         fe->spec_early = se && se[0] == '0' ? 0 : 1;
+        fe->trace = trace_env();
     }
     // (on the context stream: a first use of the null stream would take a fifth
     // hardware queue and serialise the step's streams)
@@ -1162,7 +1169,7 @@ static LKParams fe_temporal_params(const svo_frontend* fe) {
 static int fe_post(svo_frontend* fe, int t) {
     const auto t0 = std::chrono::steady_clock::now();
     auto TP = [&](const char* label) {
-        if (trace_on())
+        if (fe->trace)
             std::fprintf(stderr, "[fe post t=%d] %8.1f us  %s\n", t,
                          std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count(), label);
     };
@@ -1363,7 +1370,7 @@ int svo_frontend_step(svo_frontend* fe, int t, svo_frontend_stats* stats) {
         const char* e = std::getenv("SVO_FE_DEBUG");
         return e && e[0] == '1';
     }();
-    const bool tr = trace_on();
+    const bool tr = fe->trace;
     const auto trace_t0 = std::chrono::steady_clock::now();
     std::vector<std::pair<const char*, double>> trace;
     auto TP = [&](const char* label) {
@@ -1700,6 +1707,12 @@ int svo_frontend_step(svo_frontend* fe, int t, svo_frontend_stats* stats) {
         stats->max_hypotheses = mh;
         stats->serial_keyframe = spec_ok ? 0 : 1;
         stats->full_copy = have_full ? 1 : 0;
+        // Tracking::nextFrame's rule: a keyframe takes every masked corner, so a
+        // corner left out for lack of capacity (n_features) is a deviation
+        int64_t over = 0;
+        if (c.keyframe_rule == SVO_KF_REFERENCE)
+            for (int s = 0; s < S; s++) over += fe->h_target[s] > 0 ? fe->h_over[s] : 0;
+        stats->kf_overflow = over;
     }
     return SVO_OK;
 }

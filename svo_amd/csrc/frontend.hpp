@@ -72,26 +72,27 @@ struct TailBatch {
     int map_cap;
     float* st_xy;  // [s][cap]
     int* st_n;     // [s]
+    // nullable, host-coherent: candidates beyond the take, cand_n - take (the
+    // detector's raw count: a keyframe under Tracking::nextFrame's rule takes every
+    // masked corner, so anything here is a capacity overflow there)
+    int* h_over;
 };
 hipError_t launch_tail(const TailBatch& tb, int nseq, hipStream_t st);
 
-// The step's tail, part 2 (after the stereo LK of st_xy into the right image),
-// one block per sequence: findLeftFeaturesInRight's filter (status and
-// |yR - yL| < y_threshold, R:src/tracking.cpp:109-114), triangulateNewMapPoints'
-// DLT with P_left / P_right and z > 0 (:120-152), and the survivors appended in
-// order as new features with new map points (left camera frame, pending the
-// frame's pose: PendingMap). h_n / h_added: host-coherent copies of the counts.
+// The step's tail, part 2 (after the stereo LK of st_xy into the right image and
+// stereo_tri_kernel's filter + DLT of its matches, st_X), one block per sequence:
+// the survivors of findLeftFeaturesInRight's filter (status and |yR - yL| <
+// y_threshold, R:src/tracking.cpp:109-114) and triangulateNewMapPoints' z > 0
+// (:120-152) appended in order as new features with new map points (left camera
+// frame, pending the frame's pose: PendingMap) -- a compaction only. h_n /
+// h_added: host-coherent copies of the counts.
 struct AppendBatch {
     int* n;       // features per sequence (in/out)
     float* xy;    // [s][cap]
     int* mid;     // [s][cap]
     int cap;
     const float* st_xy;      // [s][cap] left points
-    const float* st_next;    // [s][cap] right points (stereo LK)
-    const uint8_t* st_status;
     const int* st_n;
-    float y_threshold;
-    float P[24];  // P_left, P_right
     double* map;  // [s][map_cap]
     int* map_n;
     int map_cap;
@@ -100,7 +101,7 @@ struct AppendBatch {
     int* added;   // nullable
     int* h_n;     // nullable, host-coherent
     int* h_added; // nullable, host-coherent
-    const float4* st_X;  // keyframe_fused: stereo_tri_kernel's filter + DLT of st_xy[0, spec_n) (x, y, z, keep)
+    const float4* st_X;  // stereo_tri_kernel's filter + DLT of st_xy[0, n) (x, y, z, keep)
 };
 hipError_t launch_append(const AppendBatch& b, int nseq, hipStream_t st);
 
@@ -126,10 +127,11 @@ struct StereoPrepBatch {
 hipError_t launch_stereo_prep(const StereoPrepBatch& b, int nseq, hipStream_t st);
 
 // findLeftFeaturesInRight's filter + triangulateNewMapPoints' DLT and z > 0 test of
-// the speculative candidates st_xy[0, spec_n[s]) right behind their stereo LK (a
-// candidate's point depends only on its own match and the fixed stereo
-// projections), so the keyframe on the step's critical path only compacts and
-// appends: st_X[s][j] = (x, y, z, keep) in the left camera frame.
+// the candidates st_xy[0, spec_n[s]) right behind their stereo LK (a candidate's
+// point depends only on its own match and the fixed stereo projections), so the
+// keyframe only compacts and appends: st_X[s][j] = (x, y, z, keep) in the left
+// camera frame. The speculative candidates (spec_n), or the serial keyframe's
+// exact take (st_n).
 struct StereoTriBatch {
     const float* st_xy;
     const float* st_next;

@@ -650,7 +650,7 @@ template <int M, int N, bool WANT_V>
 SVO_HD void jacobi_tail(double* At, double* Wout, double* Vt);
 template <int M, int N, bool WANT_V>
 SVO_HD void jacobi_svd(double* At, double* Wout, double* Vt) {
-    const double minval = 2.2250738585072014e-308, eps = 2.220446049250313e-16 * 10;
+    const double eps = 2.220446049250313e-16 * 10;
     double W[N];
     constexpr int max_iter = M > 30 ? M : 30;
     for (int i = 0; i < N; i++) {

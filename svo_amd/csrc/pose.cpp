@@ -77,7 +77,9 @@ namespace {
 // PoseSolver::computeOmega from the statistics: Omega_raw = sum B_i^T A_i^T A_i
 // B_i (blocks XX^T, -x XX^T, -y XX^T, (x^2+y^2) XX^T), qa = sum A_i^T A_i B_i,
 // Q = sum A_i^T A_i, P = -Q^-1 qa, Omega = Omega_raw + qa^T P; ok = false where
-// SQPnP asserts (point variance below 1e-5, largest singular value below 1e-7).
+// SQPnP asserts on the points (their variance below 1e-5); Omega's own asserts
+// (largest singular value below 1e-7, more than 6 null vectors) are checked on
+// its eigenvalues in fit_from_cost.
 void sqpnp_assemble(const double* sums, SqpnpCost& c) {
     static const int IDX[3][3] = {{0, 1, 2}, {1, 3, 4}, {2, 4, 5}};  // unique entries of a sym 3x3
     const double n = sums[0], sx = sums[1], sy = sums[2], ssq = sums[3];
@@ -118,9 +120,6 @@ void sqpnp_assemble(const double* sums, SqpnpCost& c) {
             c.Om[9 * r + col] = c.Om[9 * col + r] = v;
         }
     for (int j = 0; j < 3; j++) c.mean[j] = n > 0 ? SX(0, j) / n : 0.0;
-    double maxd = 0;
-    for (int i = 0; i < 9; i++) maxd = std::max(maxd, c.Om[10 * i]);
-    c.ok = c.ok && maxd >= 1e-7;
 }
 
 double quad(const double* Om, const double* r) {
@@ -250,15 +249,20 @@ double det33(const double* m) {
     return m[0] * (m[4] * m[8] - m[5] * m[7]) - m[1] * (m[3] * m[8] - m[5] * m[6]) + m[2] * (m[3] * m[7] - m[4] * m[6]);
 }
 
-// pt(k, p): object point k of the n fitted points into p[3]
+// pt(k, p): object point k of the n fitted points into p[3]. *found: false when
+// SQPnP asserts on Omega (CV_Assert(s_(0) >= 1e-7): its largest eigenvalue --
+// Omega is symmetric PSD, its singular values are its eigenvalues -- and at most 6
+// null vectors, as oracle/sqpnp.c) or finds no solution in front of the camera.
 template <class PointAt>
 void fit_from_cost(const SqpnpCost& c, int n, PointAt pt, double R[9], double t[3], bool* found) {
     double Oc[81], ev[9], evec[81];
     std::memcpy(Oc, c.Om, sizeof(Oc));
     la::sym_eig_ql(Oc, 9, ev, evec);  // descending; eigenvector k in row k
+    *found = false;
+    if (!(ev[0] >= 1e-7)) return;
     int nn = 0;
     while (7 - nn >= 0 && ev[7 - nn] < 1e-7) nn++;
-    nn++;
+    if (++nn > 6) return;
     std::vector<SqSol> sols;
     double min_err = DBL_MAX;
     auto check = [&](SqSol& s) {

@@ -114,7 +114,7 @@ inline void lanes_tail(vd<L>* At, vd<L>* Wout) {
 // vectors.
 template <int M, int N, int L, int G>
 inline void jacobi_svd_lanes(vd<L> (*At)[N * M], vd<L> (*Wout)[N]) {
-    const double minval = 2.2250738585072014e-308, eps = 2.220446049250313e-16 * 10;
+    const double eps = 2.220446049250313e-16 * 10;
     constexpr int max_iter = M > 30 ? M : 30;
     vd<L> W[G][N];
     vm<L> live[G];

@@ -46,7 +46,10 @@ class OracleLoop:
         (the benchmark's loop); "reference" -- Tracking::nextFrame's rule
         (R:src/tracking.cpp:68-69): a keyframe iff the previous frame was not one
         and kept fewer than features_to_track features; a keyframe takes every
-        masked corner (extractFeatures, :74-92), n_features being the capacity."""
+        masked corner (extractFeatures, :74-92) -- n_features is only the
+        capacity, and stats["kf_overflow"] counts the corners it had no room for
+        (the reference's loop has no cap: a test sizes the capacity so that this
+        stays 0)."""
         self.sc, self.N, self.bucket, self.acc = scene, n_features, bucket, acc
         self.max_level = max_level
         self.rule, self.features_to_track = rule, features_to_track
@@ -75,7 +78,9 @@ class OracleLoop:
         self.t = t0
         self.img = self.sc.frame(t0) if left is None else left
         right = self.sc.right(t0) if right is None else right
-        cand = self._candidates(self.img, None)[: self.N]
+        cand = self._candidates(self.img, None)
+        self.init_overflow = max(len(cand) - self.N, 0)
+        cand = cand[: self.N]
         self.pose_T = (np.eye(3), np.zeros(3))
         self.pts, self.X = self._keyframe(self.img, right, cand, *self.pose_T)
         self.pose = (np.zeros(3), np.zeros(3))
@@ -110,6 +115,7 @@ class OracleLoop:
         mask = O.mask_boxes(B.shape[1], B.shape[0], self.pts, 10.0)
         cand = self._candidates(B, mask)
         need = max(self.N - len(p2), 0) if kf else 0
+        stats["kf_overflow"] = max(len(cand) - need, 0) if kf and self.rule == "reference" else 0
         newL, newX = self._keyframe(B, Br, cand[:need], *self.pose_T)
         self.pts = np.concatenate([p2, newL]).astype(np.float32)
         self.X = np.concatenate([X2, newX]) if len(newL) else X2

@@ -176,6 +176,87 @@ def test_frontend_reference_keyframe_rule():
         assert st["keyframes"] == 0 and st["added"] == 0
 
 
+def test_frontend_reference_keyframe_rule_takes_every_corner_kitti():
+    """SVO_KF_REFERENCE at 1241x376 on frames whose raw FAST count (~3-4k masked
+    corners) exceeds the benchmark's 2000: with the capacity (n_features) sized
+    above the detector's count, a keyframe takes every masked corner, as
+    extractFeatures does (R:src/tracking.cpp:74-92) -- the step reports no
+    overflow (kf_overflow 0) -- and every step matches the oracle loop's
+    reference rule, keyframes and tracking-only frames alternating."""
+    ctx = S.Context(0)
+    W, H, N, T, F2T = 1241, 376, 8192, 7, 100000
+    sc = Scene(W, H, seed=21)
+    raw = len(O.fast(sc.frame(0), 20, True))
+    assert raw > 2000, raw
+    fe = make_frontend(ctx, [sc], T, N, keyframe_rule=S.KF_REFERENCE, features_to_track=F2T)
+    fe.init(0)
+    ref = OracleLoop(Scene(W, H, seed=21), N, rule="reference", features_to_track=F2T).init(0)
+    assert ref.init_overflow == 0 and len(ref.pts) > 2000
+    assert np.array_equal(fe.features(0), ref.pts)
+    kfs = []
+    for t in range(1, T):
+        st = fe.step(t).as_dict()
+        rs = ref.step(t)
+        _compare_step(fe, ref, st, rs, t)
+        assert st["keyframes"] == rs["keyframe"]
+        assert st["kf_overflow"] == rs["kf_overflow"] == 0
+        kfs.append(st["keyframes"])
+    assert kfs == [0, 1, 0, 1, 0, 1]
+    assert max(len(fe.features(0)), len(ref.pts)) > 2000
+
+
+@pytest.mark.parametrize("spec", ["32", "-1"])
+def test_frontend_reference_rule_mixed_batch(spec, monkeypatch):
+    """SVO_KF_REFERENCE with sequences that are keyframes at different steps in the
+    same batch (features_to_track set between their counts), the per-sequence
+    targets running through the speculative stereo prep, the keyframe choice of
+    fused / serial path (SVO_FE_SPEC_MARGIN 32 and -1): each sequence against its
+    own oracle loop."""
+    monkeypatch.setenv("SVO_FE_SPEC_MARGIN", spec)
+    ctx = S.Context(0)
+    W, H, T = 640, 376, 8
+    Ns = (900, 1400, 3000)  # capacities; the batch shares the largest
+    seeds = (4, 6, 12)
+    scenes = [Scene(W, H, seed=sd) for sd in seeds]
+    F2T = 1500  # between the sequences' counts: some keyframe, some not
+    fe = make_frontend(ctx, scenes, T, max(Ns), keyframe_rule=S.KF_REFERENCE, features_to_track=F2T)
+    fe.init(0)
+    refs = [OracleLoop(Scene(W, H, seed=sd), max(Ns), rule="reference", features_to_track=F2T).init(0)
+            for sd in seeds]
+    mixed = False
+    for t in range(1, T):
+        st = fe.step(t).as_dict()
+        rss = [r.step(t) for r in refs]
+        for k in ("tracked", "inliers", "added", "features", "keyframe"):
+            key = "keyframes" if k == "keyframe" else k
+            assert st[key] == sum(rs[k] for rs in rss), f"{k} at t={t}"
+        mixed |= 0 < st["keyframes"] < len(seeds)
+        for q, ref in enumerate(refs):
+            assert np.array_equal(fe.features(q), ref.pts), f"seq {q} features at t={t}"
+            rv, tv = fe.pose(q)
+            np.testing.assert_allclose(rv, ref.pose[0], atol=1e-7)
+            np.testing.assert_allclose(tv, ref.pose[1], atol=1e-6)
+    assert mixed, "some step should have keyframe and tracking-only sequences together"
+
+
+def test_frontend_trace_mode_matches_oracle_loop(monkeypatch):
+    """SVO_FE_TRACE=1 (per-task pool attribution, host trace printing) leaves the
+    results unchanged: the same step-by-step match against the oracle loop."""
+    monkeypatch.setenv("SVO_FE_TRACE", "1")
+    ctx = S.Context(0)
+    W, H, N, T = 640, 376, 800, 5
+    fe = make_frontend(ctx, [SceneForward(W, H, seed=3), SceneForward(W, H, seed=8)], T, N)
+    fe.init(0)
+    refs = [OracleLoop(SceneForward(W, H, seed=sd), N).init(0) for sd in (3, 8)]
+    for t in range(1, T):
+        st = fe.step(t).as_dict()
+        rss = [r.step(t) for r in refs]
+        for k in ("tracked", "inliers", "added", "features"):
+            assert st[k] == sum(rs[k] for rs in rss), f"{k} at t={t}"
+        for q, ref in enumerate(refs):
+            assert np.array_equal(fe.features(q), ref.pts), f"seq {q} features at t={t}"
+
+
 def test_frontend_200_frames_kitti_matches_oracle_loop():
     """BASELINE.json configs[0]: 200 frames of a 1241x376 sequence with 2000
     features, every step against the oracle loop (R:src/tracking.cpp:232-276)."""
