@@ -1048,10 +1048,18 @@ __device__ __forceinline__ void stage_padded(unsigned* dst, unsigned* sink, cons
 // the exact group reduction serve FPW features per instruction. Staged next-
 // image regions (margin QJM) for all FPW features share the wave's LDS slice.
 // Same exact integer sums and float solve as every other LK kernel.
+// JSTRIDE: the groups' regions lie JSTRIDE bytes apart, an odd multiple of 16
+// dwords. ds_read_b32 / ds_read2_b32 bank by (dword address) mod 32 over each
+// 32-lane half -- two groups, reading the same strip pattern at the same offsets
+// of their own regions: at a multiple of 32 dwords apart (JBYTES / 4 = 672 for
+// QJM = 1) every read of the pair collided (2-way: ~1,350 conflict cycles per
+// wave in SQ_LDS_BANK_CONFLICT), 16 banks apart they take disjoint halves.
 template <int QJM>
 struct MultiShape {
     static constexpr int JRW = ru4(21 + 2 * QJM + 3), JRH = 21 + 1 + 2 * QJM;
     static constexpr int JBYTES = JRW * JRH * 4;
+    static constexpr int JSTRIDE = ((JBYTES / 4 + 16) / 32 * 32 + 16) * 4;
+    static_assert(JSTRIDE >= JBYTES && (JSTRIDE / 4) % 32 == 16, "group stride");
 };
 
 // Exact sums over the LPF lanes of each group (every lane receives its group's
@@ -1121,8 +1129,8 @@ __global__ __launch_bounds__(64, MINW) void lk_multi_kernel(LKBatch B, LKDev p) 
     const cpyr next = (cpyr)B.next + seq;
     const DerivDesc& dprev = B.dprev[seq];
     unsigned* jregs = reinterpret_cast<unsigned*>(lds);
-    unsigned* sink = reinterpret_cast<unsigned*>(lds + FPW * Q::JBYTES);
-    const unsigned* jmine = jregs + g * (Q::JBYTES / 4);
+    unsigned* sink = reinterpret_cast<unsigned*>(lds + FPW * Q::JSTRIDE);
+    const unsigned* jmine = jregs + g * (Q::JSTRIDE / 4);
 
     // the lane's strips: column, first row, LDS offset; strip 63 is a dummy
     int scol[K], srow[K];
@@ -1242,7 +1250,7 @@ __global__ __launch_bounds__(64, MINW) void lk_multi_kernel(LKBatch B, LKDev p) 
                     const bool wr = d < JRW / 4 && lr < SL::RPP;
 #pragma unroll
                     for (int f = 0; f < FPW; f++) {
-                        unsigned* dpl = wr ? jregs + f * (Q::JBYTES / 4) + 4 * d : sink;
+                        unsigned* dpl = wr ? jregs + f * (Q::JSTRIDE / 4) + 4 * d : sink;
                         const int dstride = wr ? JRW : 0;
 #pragma unroll
                         for (int q = 0; q < SL::NPS; q++) {
@@ -1297,7 +1305,7 @@ __global__ __launch_bounds__(64, MINW) void lk_multi_kernel(LKBatch B, LKDev p) 
                 while (nb) {
                     const int f = (int)(__builtin_ctzll(nb) / LPF);
                     nb &= nb - 1;
-                    stage_padded<JRW, JRH>(jregs + f * (Q::JBYTES / 4), sink, J,
+                    stage_padded<JRW, JRH>(jregs + f * (Q::JSTRIDE / 4), sink, J,
                                            __builtin_amdgcn_readlane(jxa, LPF * f),
                                            __builtin_amdgcn_readlane(jy0, LPF * f), lane);
                 }
@@ -1370,7 +1378,7 @@ __global__ __launch_bounds__(64, MINW) void lk_multi_kernel(LKBatch B, LKDev p) 
 template <int FPW, int QJM, int MINW = 4, int KKS = 2>
 hipError_t launch_multi(const LKBatch& b, int nseq, int max_n, const LKDev& d, hipStream_t st) {
     dim3 grid((max_n + FPW - 1) / FPW, nseq);
-    constexpr int lds_bytes = FPW * MultiShape<QJM>::JBYTES + 16;
+    constexpr int lds_bytes = FPW * MultiShape<QJM>::JSTRIDE + 16;
     hipLaunchKernelGGL((lk_multi_kernel<FPW, QJM, MINW, KKS>), grid, dim3(64), lds_bytes, st, b, d);
     return hipGetLastError();
 }
