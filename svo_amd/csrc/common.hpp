@@ -268,6 +268,23 @@ hipError_t launch_reproj(const double* d_obj, const float* d_img, const int* d_c
                          double* d_jac, double* d_partial, double* d_normal, hipStream_t st);
 hipError_t launch_suffstats(const float* obj, const float* img, const int* counts, int cap, const uint32_t* bits,
                             int words_cap, int nseq, const double K[9], double* out, hipStream_t st);
+// solvePnPRansac's outcome per sequence as the host's RANSAC left it, the input of
+// the device's final fit: mode 0 no model (identity pose), 1 SQPnP fit on the
+// inliers (R / t: the RANSAC model, kept where SQPnP asserts or finds nothing in
+// front of the camera), 2 given (rv / t: the n <= 5 direct EPnP solve)
+struct SqpnpFitIn {
+    int mode, pad;
+    double R[9], t[3], rv[3];
+};
+// The final SQPnP fits of every sequence, one 64-thread block each (sqpnp.hpp: the
+// cost from the statistics `stats` of suffstats_kernel, Omega's eigenvectors, the
+// SQP runs from its starts in lanes, the solution search replayed in order), then
+// Frame::pose() of the result: pose6[s] = (rvec, tvec), pose12[s] = camera -> world
+// (R^T, -R^T t) for PendingMap. obj / counts / bits: the fitted points (the
+// cheirality majority test).
+hipError_t launch_sqpnp_fit(const double* stats, const SqpnpFitIn* in, const float* obj, const int* counts, int cap,
+                            const uint32_t* bits, int words_cap, int nseq, double* pose6, double* pose12,
+                            hipStream_t st);
 size_t bucket_scratch_ints(int img_w, int img_h, int bucket, int per_bucket, int n);
 hipError_t launch_bucket(const BucketBatch& b, int nseq, int img_w, int img_h, int bucket, int per_bucket,
                          hipStream_t st);

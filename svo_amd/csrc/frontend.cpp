@@ -352,6 +352,8 @@ struct svo_frontend {
     long long* h_itsum;
     float* h_samp;
     double *h_stats, *h_pose;   // h_pose: [s][12] camera -> world of the last fitted frame
+    double* h_pose6;            // [s][6] rvec, tvec of the last fitted frame (sqpnp_fit_kernel)
+    SqpnpFitIn* h_fitin;        // [s] the host RANSAC's outcome the device fit starts from
     uint32_t* h_best;           // this step's parity of h_best_b
     uint32_t* h_best_b[2];
     // host-coherent buffers the scoring kernel reads / writes directly (zero-copy:
@@ -376,7 +378,7 @@ struct svo_frontend {
     int stats_parity = 0;  // step parity whose inliers the pending statistics cover
     bool boxes_binned = false;  // box_bin already queued for the next step's FAST
     int pyr_ready = -1;  // frame index whose pyramid + Scharr were built ahead
-    hipEvent_t ev_stats = nullptr;  // SQPnP statistics of the last step on the host
+    hipEvent_t ev_stats = nullptr;  // SQPnP statistics + final fits of the last step done (copy stream)
     // full copies of the tracked points / map points (h_xyB, h_obj): needed only by
     // the final fits, RANSAC past the prefetched subsets and the n <= 5 solve, so
     // they travel on their own stream once requested
@@ -726,31 +728,24 @@ int fe_queue_stats(svo_frontend* fe) {
     const int p = fe->stats_parity;
     SVO_HIP(ctx, launch_suffstats(fe->obj_b[p], fe->xyB_b[p], fe->nB_b[p], fe->CAP, fe->h_best_b[p], fe->WORDS, fe->S,
                                   fe->cfg.K, fe->h_stats, fe->st_copy));
+    // and the final SQPnP fits from them, on the device: the next post-LK (which
+    // moves the keyframe's new map points with these poses) waits for ev_stats
+    SVO_HIP(ctx, launch_sqpnp_fit(fe->h_stats, fe->h_fitin, fe->obj_b[p], fe->nB_b[p], fe->CAP, fe->h_best_b[p],
+                                  fe->WORDS, fe->S, fe->h_pose6, fe->h_pose, fe->st_copy));
     SVO_HIP(ctx, hipEventRecord(fe->ev_stats, fe->st_copy));
     fe->stats_pending = false;
     return SVO_OK;
 }
 
-// Final SQPnP-objective fits of the last step (from the GPU sufficient
-// statistics in h_stats): refine the reported poses only, so they are run
-// lazily -- at the next step while the GPU tracks, or when a pose is read.
+// The final SQPnP fits of the last step ran on the device (sqpnp_fit_kernel behind
+// the statistics, fe_queue_stats): the host only reads their poses, when asked
+// for one (svo_frontend_pose / _synchronize); the step itself never waits for
+// them (its post-LK kernel waits on the device).
 double fe_finish_fits(svo_frontend* fe) {
     if (!fe->fits_pending) return 0.0;
     auto t0 = std::chrono::steady_clock::now();
     (void)hipEventSynchronize(fe->ev_stats);
-    (void)hipEventSynchronize(fe->ev_full_b[fe->fit_parity]);  // cheirality test reads h_obj
-    fe->pool->run(fe->S, [&](int s) {
-        RansacSeq& r = fe->rs[s];
-        r.fit(fe->cfg.K, fe->h_stats + kSqpnpStats * (size_t)s);
-        double* P = &fe->pose[6 * (size_t)s];
-        if (r.ok) {
-            std::memcpy(P, r.rvec, sizeof(r.rvec));
-            std::memcpy(P + 3, r.tvec, sizeof(r.tvec));
-        } else {
-            std::fill(P, P + 6, 0.0);
-        }
-        fe_set_pose(fe, s, r.ok, P, P + 3);
-    });
+    std::memcpy(fe->pose.data(), fe->h_pose6, sizeof(double) * 6 * (size_t)fe->S);
     fe->fits_pending = false;
     return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
 }
@@ -909,6 +904,8 @@ int svo_frontend_create(svo_ctx* ctx, const svo_frontend_config* cfg, svo_fronte
         add(sizeof(uint32_t) * (size_t)S * fe->WORDS);
         add(sizeof(double) * kSqpnpStats * (size_t)S);
         add(sizeof(double) * 12 * (size_t)S);
+        add(sizeof(double) * 6 * (size_t)S);
+        add(sizeof(SqpnpFitIn) * (size_t)S);
         add(1024);
         if (hipHostMalloc(&fe->zout, zb, hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess) {
             fe->zout = nullptr;
@@ -929,6 +926,8 @@ int svo_frontend_create(svo_ctx* ctx, const svo_frontend_config* cfg, svo_fronte
         fe->h_best = fe->h_best_b[0];
         fe->h_stats = carve<double>(p, kSqpnpStats * (size_t)S);
         fe->h_pose = carve<double>(p, 12 * (size_t)S);
+        fe->h_pose6 = carve<double>(p, 6 * (size_t)S);
+        fe->h_fitin = carve<SqpnpFitIn>(p, (size_t)S);
         for (int s = 0; s < S; s++) fe_set_pose(fe, s, false, nullptr, nullptr);
     }
     // derivative pyramids of three frames of every sequence (t - 1: LK's prev,
@@ -1177,6 +1176,9 @@ static int fe_post(svo_frontend* fe, int t) {
     const int CAP = fe->CAP;
     hipStream_t sl = fe->st_lk;
     int slot;
+    // the previous step's final fits (sqpnp_fit_kernel) set the poses the post-LK
+    // moves the previous keyframe's new map points with
+    SVO_HIP(ctx, hipStreamWaitEvent(sl, fe->ev_stats, 0));
     PostLkBatch pb{fe->nA, fe->status, fe->next_xy, fe->midA, fe->iters, fe->xyB, fe->midB, fe->nB, fe_pending(fe),
                    fe->obj, CAP, kRansacPrefetch, fe->h_nB, fe->h_itsum, fe->h_samp};
     ph_begin(fe, PH_POST, sl, &slot);
@@ -1397,12 +1399,10 @@ int svo_frontend_step(svo_frontend* fe, int t, svo_frontend_stats* stats) {
     fe->front_t = -1;
     TP("front enqueued");
     const int64_t n_keyframes = fe_keyframe_targets(fe);
-    // the previous step's final pose fits: the host does them while the GPU tracks
-    // this frame; they set the poses that move the previous keyframe's new map
-    // points to the world frame, so this step's post-LK is queued right after
+    // the previous step's final pose fits run on the device (fe_queue_stats); this
+    // step's post-LK waits for them there
     ms_enqueue += ms_since(t_call);
-    double ms_fit = fe_finish_fits(fe);
-    TP("fits done");
+    double ms_fit = 0;
     {
         const auto te = clk::now();
         int rp = fe_post(fe, t);
@@ -1593,6 +1593,12 @@ int svo_frontend_step(svo_frontend* fe, int t, svo_frontend_stats* stats) {
     for (int s = 0; s < S; s++) {
         RansacSeq& r = fe->rs[s];
         r.select(c.K, false);
+        // the device's final fit starts from this outcome (fe_queue_stats)
+        SqpnpFitIn& fi = fe->h_fitin[s];
+        fi.mode = !r.ok ? 0 : (r.fitted ? 2 : 1);
+        std::memcpy(fi.R, r.bestR, sizeof(fi.R));
+        std::memcpy(fi.t, r.fitted ? r.tvec : r.bestt, sizeof(fi.t));
+        std::memcpy(fi.rv, r.rvec, sizeof(fi.rv));
         const int kept = r.ok ? r.maxGood : (r.n < 4 ? r.n : 0);
         max_take = std::max(max_take, fe->h_target[s] - kept);
         // (a sequence without a keyframe takes nothing: nothing to cover)

@@ -11,6 +11,7 @@
 // Outputs: optional f32 residuals, inlier bitmask (32 points per word, one
 // ballot per wave), per-hypothesis inlier counts (integer atomics: exact).
 #include "common.hpp"
+#include "sqpnp.hpp"
 
 namespace svo {
 
@@ -187,6 +188,101 @@ __global__ __launch_bounds__(256) void suffstats_kernel(const float* __restrict_
 }
 
 }  // namespace
+
+// solvePnP(SQPNP) on a sequence's RANSAC inliers (SqpnpFitIn mode 1) and the
+// Frame::pose() of every outcome (R:src/tracking.cpp:191-214). Lane 0 assembles the
+// cost and Omega's eigen-decomposition; lanes 0..17 run the SQP from the 18 starts
+// (the 9 eigenvectors, each +- sqrt(3) e) -- every start a search could ask for,
+// each independent of the others; lane 0 then replays the search (sq_select) with
+// those results, which takes the same steps as the host's on-demand runs.
+__global__ __launch_bounds__(64) void sqpnp_fit_kernel(const double* __restrict__ stats,
+                                                       const SqpnpFitIn* __restrict__ in,
+                                                       const float* __restrict__ obj, const int* __restrict__ counts,
+                                                       int cap, const uint32_t* __restrict__ bits, int words_cap,
+                                                       double* __restrict__ pose6, double* __restrict__ pose12) {
+    const int s = blockIdx.x, lane = threadIdx.x;
+    __shared__ sq::SqpnpCost c;
+    __shared__ double ev[9], evec[81], rs[18][9];
+    __shared__ int nn_s;
+    const SqpnpFitIn fin = in[s];
+    if (fin.mode == 1) {
+        if (lane == 0) {
+            sq::sqpnp_assemble(stats + 40 * (size_t)s, c);
+            int nn = -1;
+            if (c.ok) {
+                double Oc[81];
+                for (int k = 0; k < 81; k++) Oc[k] = c.Om[k];
+                la::sym_eig_ql(Oc, 9, ev, evec);
+                nn = sq::sq_null_count(ev);
+            }
+            nn_s = nn;
+        }
+        __syncthreads();
+        if (nn_s >= 0 && lane < 18) sq::sq_start(c, evec, lane, rs[lane]);
+        __syncthreads();
+    }
+    if (lane != 0) return;
+    double rvec[3] = {0, 0, 0}, tvec[3] = {0, 0, 0};
+    if (fin.mode == 2) {
+        for (int k = 0; k < 3; k++) {
+            rvec[k] = fin.rv[k];
+            tvec[k] = fin.t[k];
+        }
+    } else if (fin.mode == 1) {
+        bool found = false;
+        double R[9], t[3];
+        if (nn_s >= 0) {
+            const int n = counts[s];
+            const float* o = obj + 3 * (size_t)s * cap;
+            const uint32_t* b = bits + (size_t)s * words_cap;
+            int n_in = 0;
+            for (int w = 0; w < (n + 31) / 32; w++) n_in += __popc(b[w] & (w == n / 32 ? (1u << (n & 31)) - 1u : ~0u));
+            sq::sq_select(
+                c, ev, evec, nn_s, n_in,
+                [&](int j, double* r) {
+                    for (int k = 0; k < 9; k++) r[k] = rs[j][k];
+                },
+                [&](const double* r, const double* tt) {
+                    int pos = 0;
+                    for (int i = 0; i < n; i++) {
+                        if (!((b[i >> 5] >> (i & 31)) & 1u)) continue;
+                        const double p[3] = {(double)o[3 * i], (double)o[3 * i + 1], (double)o[3 * i + 2]};
+                        pos += dot3(r + 6, p) + tt[2] > 0;
+                    }
+                    return pos;
+                },
+                R, t, &found);
+        }
+        if (found) {
+            la::cv::rodrigues_inv(R, rvec);
+            for (int k = 0; k < 3; k++) tvec[k] = t[k];
+        } else {  // solvePnP(SQPNP) asserted or found nothing: the RANSAC model (as the host)
+            la::cv::rodrigues_inv(fin.R, rvec);
+            for (int k = 0; k < 3; k++) tvec[k] = fin.t[k];
+        }
+    }
+    double* P6 = pose6 + 6 * (size_t)s;
+    for (int k = 0; k < 3; k++) {
+        P6[k] = rvec[k];
+        P6[3 + k] = tvec[k];
+    }
+    // Frame::pose(): the inverse of [R(rvec) | tvec] (svo::SE3d::inverse order)
+    double Rm[9];
+    la::rodrigues(rvec, Rm);
+    double* T = pose12 + 12 * (size_t)s;
+    for (int i = 0; i < 3; i++)
+        for (int j = 0; j < 3; j++) T[3 * i + j] = Rm[3 * j + i];
+    for (int i = 0; i < 3; i++) T[9 + i] = -(T[3 * i] * tvec[0] + T[3 * i + 1] * tvec[1] + T[3 * i + 2] * tvec[2]);
+}
+
+hipError_t launch_sqpnp_fit(const double* stats, const SqpnpFitIn* in, const float* obj, const int* counts, int cap,
+                            const uint32_t* bits, int words_cap, int nseq, double* pose6, double* pose12,
+                            hipStream_t st) {
+    if (nseq <= 0) return hipSuccess;
+    hipLaunchKernelGGL(sqpnp_fit_kernel, dim3(nseq), dim3(64), 0, st, stats, in, obj, counts, cap, bits, words_cap,
+                       pose6, pose12);
+    return hipGetLastError();
+}
 
 hipError_t launch_suffstats(const float* obj, const float* img, const int* counts, int cap, const uint32_t* bits,
                             int words_cap, int nseq, const double K[9], double* out, hipStream_t st) {

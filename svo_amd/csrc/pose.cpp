@@ -26,6 +26,7 @@
 #include "simd_svd.hpp"
 #include "linalg.hpp"
 #include "pose.hpp"
+#include "sqpnp.hpp"
 
 namespace svo {
 
@@ -43,13 +44,6 @@ int update_num_iters(double p, double ep, int model_points, int max_iters) {
     return denom >= 0 || -num >= max_iters * (-denom) ? max_iters : (int)rint(num / denom);
 }
 
-// ---- final fit: SQPnP's cost, E(R) = vec(R)^T Omega vec(R) ----
-struct SqpnpCost {
-    double Om[81];
-    double P[27];    // t = P vec(R)
-    double mean[3];  // object-point mean (PoseSolver::positiveDepth)
-    bool ok;         // computeOmega's asserts held (point variance, rank)
-};
 }  // namespace
 
 // The sufficient statistics of one point set (pose.hpp); host twin of pnp.hip's
@@ -74,262 +68,33 @@ void sqpnp_sums(const double* pw, const double* q, int n, double* sums) {
 
 namespace {
 
-// PoseSolver::computeOmega from the statistics: Omega_raw = sum B_i^T A_i^T A_i
-// B_i (blocks XX^T, -x XX^T, -y XX^T, (x^2+y^2) XX^T), qa = sum A_i^T A_i B_i,
-// Q = sum A_i^T A_i, P = -Q^-1 qa, Omega = Omega_raw + qa^T P; ok = false where
-// SQPnP asserts on the points (their variance below 1e-5); Omega's own asserts
-// (largest singular value below 1e-7, more than 6 null vectors) are checked on
-// its eigenvalues in fit_from_cost.
-void sqpnp_assemble(const double* sums, SqpnpCost& c) {
-    static const int IDX[3][3] = {{0, 1, 2}, {1, 3, 4}, {2, 4, 5}};  // unique entries of a sym 3x3
-    const double n = sums[0], sx = sums[1], sy = sums[2], ssq = sums[3];
-    auto SX = [&](int u, int j) { return sums[4 + 3 * u + j]; };           // sum c_u X_j
-    auto SXX = [&](int u, int a, int b) { return sums[16 + 6 * u + IDX[a][b]]; };  // sum c_u X_a X_b
-    double Om[81] = {0}, qa[27] = {0};
-    for (int a = 0; a < 3; a++)
-        for (int b = 0; b < 3; b++) {
-            Om[9 * a + b] = SXX(0, a, b);
-            Om[9 * (3 + a) + 3 + b] = SXX(0, a, b);
-            Om[9 * a + 6 + b] = Om[9 * (6 + b) + a] = -SXX(1, a, b);
-            Om[9 * (3 + a) + 6 + b] = Om[9 * (6 + b) + 3 + a] = -SXX(2, a, b);
-            Om[9 * (6 + a) + 6 + b] = SXX(3, a, b);
-        }
-    for (int j = 0; j < 3; j++) {
-        qa[j] = SX(0, j);
-        qa[6 + j] = -SX(1, j);
-        qa[9 + 3 + j] = SX(0, j);
-        qa[9 + 6 + j] = -SX(2, j);
-        qa[18 + j] = -SX(1, j);
-        qa[18 + 3 + j] = -SX(2, j);
-        qa[18 + 6 + j] = SX(3, j);
-    }
-    const double Q[9] = {n, 0, -sx, 0, n, -sy, -sx, -sy, ssq};
-    const double detQ = n * (n * ssq - sy * sy - sx * sx);
-    c.ok = n > 0 && detQ / (n * n * n) >= 1e-5;
-    double Qi[9];
-    la::pinv3(Q, Qi);
-    for (int a = 0; a < 3; a++)
-        for (int col = 0; col < 9; col++)
-            c.P[9 * a + col] = -(Qi[3 * a] * qa[col] + Qi[3 * a + 1] * qa[9 + col] + Qi[3 * a + 2] * qa[18 + col]);
-    for (int i = 0; i < 9; i++)
-        for (int j = 0; j < 9; j++)
-            c.Om[9 * i + j] = Om[9 * i + j] + (qa[i] * c.P[j] + qa[9 + i] * c.P[9 + j] + qa[18 + i] * c.P[18 + j]);
-    for (int r = 0; r < 9; r++)  // symmetrise
-        for (int col = 0; col < r; col++) {
-            const double v = 0.5 * (c.Om[9 * r + col] + c.Om[9 * col + r]);
-            c.Om[9 * r + col] = c.Om[9 * col + r] = v;
-        }
-    for (int j = 0; j < 3; j++) c.mean[j] = n > 0 ? SX(0, j) / n : 0.0;
-}
+using sq::SqpnpCost;
+using sq::sqpnp_assemble;
 
-double quad(const double* Om, const double* r) {
-    double s = 0;
-    for (int i = 0; i < 9; i++) {
-        double t = 0;
-        for (int j = 0; j < 9; j++) t += Om[9 * i + j] * r[j];
-        s += r[i] * t;
-    }
-    return s;
-}
-
-
-// One SQP step of SQPnP (PoseSolver::solveSQPSystem) at r: the delta minimising
-// (r + delta)^T Om (r + delta) subject to the orthogonality constraints
-// linearised at r, J delta = -h(r) (h: the three row norms - 1 and the three row
-// dot products), from the KKT system [2 Om, J^T; J, 0] [delta; l] = [-2 Om r; -h]
-// solved by Gaussian elimination with partial pivoting (OpenCV solves the same
-// system through an orthonormal row / null-space split of J).
-void sqp_step(const double* Om, const double* r, double* delta) {
-    constexpr int N = 15;
-    double A[N][N + 1] = {{0}};
-    const double* r1 = r;
-    const double* r2 = r + 3;
-    const double* r3 = r + 6;
-    for (int i = 0; i < 9; i++) {
-        double g = 0;
-        for (int j = 0; j < 9; j++) {
-            A[i][j] = 2 * Om[9 * i + j];
-            g += Om[9 * i + j] * r[j];
-        }
-        A[i][N] = -2 * g;
-    }
-    double J[6][9] = {{0}};
-    for (int k = 0; k < 3; k++) {
-        J[0][k] = 2 * r1[k];
-        J[1][3 + k] = 2 * r2[k];
-        J[2][6 + k] = 2 * r3[k];
-        J[3][k] = r2[k];
-        J[3][3 + k] = r1[k];
-        J[4][3 + k] = r3[k];
-        J[4][6 + k] = r2[k];
-        J[5][k] = r3[k];
-        J[5][6 + k] = r1[k];
-    }
-    const double h[6] = {dot3(r1, r1) - 1, dot3(r2, r2) - 1, dot3(r3, r3) - 1, dot3(r1, r2), dot3(r2, r3),
-                         dot3(r1, r3)};
-    for (int c = 0; c < 6; c++) {
-        for (int j = 0; j < 9; j++) {
-            A[9 + c][j] = J[c][j];
-            A[j][9 + c] = J[c][j];
-        }
-        A[9 + c][N] = -h[c];
-    }
-    for (int col = 0; col < N; col++) {
-        int piv = col;
-        for (int i = col + 1; i < N; i++)
-            if (fabs(A[i][col]) > fabs(A[piv][col])) piv = i;
-        if (piv != col)
-            for (int j = 0; j <= N; j++) std::swap(A[col][j], A[piv][j]);
-        const double d = A[col][col];
-        if (d == 0) continue;
-        for (int i = col + 1; i < N; i++) {
-            const double f = A[i][col] / d;
-            if (f == 0) continue;
-            for (int j = col; j <= N; j++) A[i][j] -= f * A[col][j];
-        }
-    }
-    double x[N];
-    for (int i = N - 1; i >= 0; i--) {
-        double v = A[i][N];
-        for (int j = i + 1; j < N; j++) v -= A[i][j] * x[j];
-        x[i] = A[i][i] != 0 ? v / A[i][i] : 0.0;
-    }
-    std::memcpy(delta, x, sizeof(double) * 9);
-}
-
-// PoseSolver::runSQP: at most 15 steps while |delta|^2 > 1e-10; then -r if
-// det < 0, and the nearest rotation only if det > 1.001 (r as is otherwise --
-// its cost and t are taken unprojected, as OpenCV does).
-void sqp_run(const double* Om, const double* r0, double* rhat) {
-    double r[9], delta[9];
-    std::memcpy(r, r0, sizeof(r));
-    double dsq = DBL_MAX;
-    int step = 0;
-    while (dsq > 1e-10 && step++ < 15) {
-        sqp_step(Om, r, delta);
-        dsq = 0;
-        for (int k = 0; k < 9; k++) {
-            r[k] += delta[k];
-            dsq += delta[k] * delta[k];
-        }
-    }
-    double d = r[0] * (r[4] * r[8] - r[5] * r[7]) - r[1] * (r[3] * r[8] - r[5] * r[6]) + r[2] * (r[3] * r[7] - r[4] * r[6]);
-    if (d < 0) {
-        for (double& v : r) v = -v;
-        d = -d;
-    }
-    if (d > 1.001)
-        la::nearest_rotation(r, rhat);
-    else
-        std::memcpy(rhat, r, sizeof(r));
-}
-
-// SQPnP's solution search (PoseSolver::solveInternal) over Omega's eigenvectors:
-//   the null-space eigenvectors e (eigenvalues below the rank tolerance 1e-7; at
-//   least the smallest), sqrt(3)-scaled: if e is already orthogonal (squared
-//   orthogonality error < 1e-8) it is taken as is, det-signed, with t = P e (no
-//   refinement -- OpenCV's shortcut); else runs from the nearest rotations of +e
-//   and -e; then further eigenvectors while the best error exceeds 3x their
-//   eigenvalue. checkSolution: the object-point mean in front of the camera or a
-//   majority of positive depths; errors within 1e-6 and rotations within 1e-10
-//   are one solution; the first smallest-error solution is solvePnP's.
-struct SqSol {
-    double r[9], t[3], err;
-};
-
-double ortho_err(const double* e) {
-    const double n1 = e[0] * e[0] + e[1] * e[1] + e[2] * e[2], n2 = e[3] * e[3] + e[4] * e[4] + e[5] * e[5],
-                 n3 = e[6] * e[6] + e[7] * e[7] + e[8] * e[8];
-    const double d12 = e[0] * e[3] + e[1] * e[4] + e[2] * e[5], d13 = e[0] * e[6] + e[1] * e[7] + e[2] * e[8],
-                 d23 = e[3] * e[6] + e[4] * e[7] + e[5] * e[8];
-    return (n1 - 1) * (n1 - 1) + (n2 - 1) * (n2 - 1) + (n3 - 1) * (n3 - 1) + 2 * (d12 * d12 + d13 * d13 + d23 * d23);
-}
-
-double det33(const double* m) {
-    return m[0] * (m[4] * m[8] - m[5] * m[7]) - m[1] * (m[3] * m[8] - m[5] * m[6]) + m[2] * (m[3] * m[7] - m[4] * m[6]);
-}
-
+// The SQPnP solution search on the host (sqpnp.hpp): Omega's eigen-decomposition,
+// SQPnP's asserts on it, the starts run in order as the search asks for them.
 // pt(k, p): object point k of the n fitted points into p[3]. *found: false when
-// SQPnP asserts on Omega (CV_Assert(s_(0) >= 1e-7): its largest eigenvalue --
-// Omega is symmetric PSD, its singular values are its eigenvalues -- and at most 6
-// null vectors, as oracle/sqpnp.c) or finds no solution in front of the camera.
+// SQPnP asserts on Omega or finds no solution in front of the camera.
 template <class PointAt>
 void fit_from_cost(const SqpnpCost& c, int n, PointAt pt, double R[9], double t[3], bool* found) {
     double Oc[81], ev[9], evec[81];
     std::memcpy(Oc, c.Om, sizeof(Oc));
     la::sym_eig_ql(Oc, 9, ev, evec);  // descending; eigenvector k in row k
     *found = false;
-    if (!(ev[0] >= 1e-7)) return;
-    int nn = 0;
-    while (7 - nn >= 0 && ev[7 - nn] < 1e-7) nn++;
-    if (++nn > 6) return;
-    std::vector<SqSol> sols;
-    double min_err = DBL_MAX;
-    auto check = [&](SqSol& s) {
-        for (int a = 0; a < 3; a++) {
-            s.t[a] = 0;
-            for (int col = 0; col < 9; col++) s.t[a] += c.P[9 * a + col] * s.r[col];
-        }
-        bool front = dot3(s.r + 6, c.mean) + s.t[2] > 0;
-        if (!front) {
+    const int nn = sq::sq_null_count(ev);
+    if (nn < 0) return;
+    sq::sq_select(
+        c, ev, evec, nn, n, [&](int j, double* r) { sq::sq_start(c, evec, j, r); },
+        [&](const double* r, const double* tt) {
             int pos = 0;
             for (int k = 0; k < n; k++) {
                 double p[3];
                 pt(k, p);
-                pos += dot3(s.r + 6, p) + s.t[2] > 0;
+                pos += dot3(r + 6, p) + tt[2] > 0;
             }
-            front = pos >= n - pos;
-        }
-        if (!front) return;
-        s.err = quad(c.Om, s.r);
-        if (fabs(min_err - s.err) > 1e-6) {
-            if (min_err > s.err) {
-                min_err = s.err;
-                sols.assign(1, s);
-            }
-        } else {
-            bool same = false;
-            for (auto& o : sols) {
-                double d = 0;
-                for (int k = 0; k < 9; k++) d += (o.r[k] - s.r[k]) * (o.r[k] - s.r[k]);
-                if (d < 1e-10) {
-                    if (o.err > s.err) o = s;
-                    same = true;
-                    break;
-                }
-            }
-            if (!same) sols.push_back(s);
-            if (min_err > s.err) min_err = s.err;
-        }
-    };
-    auto from_eigen = [&](const double* e) {
-        for (int sg = 0; sg < 2; sg++) {
-            double m[9];
-            SqSol s;
-            for (int k = 0; k < 9; k++) m[k] = sg ? -e[k] : e[k];
-            double r0[9];
-            la::nearest_rotation(m, r0);
-            sqp_run(c.Om, r0, s.r);
-            check(s);
-        }
-    };
-    for (int i = 9 - nn; i < 9; i++) {
-        double e[9];
-        for (int k = 0; k < 9; k++) e[k] = 1.7320508075688772 * evec[9 * i + k];
-        if (ortho_err(e) < 1e-8) {
-            SqSol s;
-            const double d = det33(e);
-            for (int k = 0; k < 9; k++) s.r[k] = d * e[k];
-            check(s);
-        } else {
-            from_eigen(e);
-        }
-    }
-    for (int k = 1; 9 - nn - k > 0 && min_err > 3 * ev[9 - nn - k]; k++) from_eigen(evec + 9 * (9 - nn - k));
-    *found = !sols.empty();
-    if (!*found) return;
-    std::memcpy(R, sols[0].r, sizeof(double) * 9);  // (rodrigues_inv re-orthonormalises, as cv::Rodrigues)
-    std::memcpy(t, sols[0].t, sizeof(double) * 3);
+            return pos;
+        },
+        R, t, found);
 }
 
 }  // namespace

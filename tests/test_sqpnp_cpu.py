@@ -79,3 +79,23 @@ def test_sqpnp_fit_matches_oracle_along_the_loop(monkeypatch):
     for t in range(1, 8):
         ref.step(t)
     assert worst[0] < 1e-9, worst[0]
+
+
+def test_sqpnp_rank_assert_near_threshold():
+    """SQPnP asserts when Omega's largest singular value is below 1e-7
+    (CV_Assert(s_(0) >= 1e-7)). Omega scales with the square of the object
+    coordinates, so the same problem scaled down crosses the threshold: product
+    (its largest eigenvalue) and oracle (its SVD) agree on which side every scale
+    lands -- fit or assert -- on a sweep that holds both outcomes."""
+    X, uv, K = _problem(200, 0.3, 7, depth=(6, 12))
+    outcomes = []
+    for k in range(48):
+        a = 10.0 ** (-3.0 - k / 12.0)
+        ok, rv, tv = S.solve_pnp_sqpnp(X * a, uv, K)
+        rc, rvo, tvo = _oracle_pose(X * a, uv, K)
+        assert ok == (rc == 0), f"scale {a:.3g}: product {ok}, oracle {rc}"
+        if ok:
+            np.testing.assert_allclose(rv, rvo, atol=1e-7)
+        outcomes.append(ok)
+    assert any(outcomes) and not all(outcomes)
+
