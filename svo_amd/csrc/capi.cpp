@@ -518,8 +518,12 @@ int svo_pnp_residuals(svo_ctx* ctx, const float* obj_xyz, const float* img_xy, i
 
 int svo_epnp_subsets(svo_ctx* ctx, const float* subsets, int m, const double K[9], int device, double* Rt,
                      int* ok) {
-    if ((!ctx && device == 1) || device < 0 || device > 2 || m < 0 || (m > 0 && (!subsets || !Rt || !ok)) || !K)
+    if ((!ctx && device == 1) || device < 0 || device > 5 || m < 0 || (m > 0 && (!subsets || !Rt || !ok)) || !K)
         return set_error(ctx, SVO_ERR_ARG, "svo_epnp_subsets: bad arguments");
+    // 0: the front end's solver as dispatched; 3 / 4 / 5: forced scalar / AVX2 / AVX-512
+    const int isa = device == 3 ? kEpnpScalar : device == 4 ? kEpnpAvx2 : device == 5 ? kEpnpAvx512 : kEpnpAuto;
+    if (device >= 3 && !epnp_isa_supported(isa))
+        return set_error(ctx, SVO_ERR_NODEVICE, "svo_epnp_subsets: instruction set not on this CPU");
     if (m == 0) return SVO_OK;
     if (device == 2) {  // the device solver's host twin (epnp_ql.hpp)
         for (int j = 0; j < m; j++) {
@@ -531,7 +535,7 @@ int svo_epnp_subsets(svo_ctx* ctx, const float* subsets, int m, const double K[9
         }
         return SVO_OK;
     }
-    if (!device) {  // the front end's host solver: epnp_pixels_batch, kEpnpLanes subsets at a time
+    if (device == 0 || device >= 3) {  // the front end's host solver: epnp_pixels_batch, kEpnpLanes at a time
         for (int j0 = 0; j0 < m; j0 += kEpnpLanes) {
             const int c = std::min(kEpnpLanes, m - j0);
             const float *o[kEpnpLanes], *im[kEpnpLanes];
@@ -543,7 +547,7 @@ int svo_epnp_subsets(svo_ctx* ctx, const float* subsets, int m, const double K[9
                 im[q] = o[q] + 15;
                 id[q] = nullptr;
             }
-            epnp_pixels_batch(c, o, im, id, K, R, t, v);
+            epnp_pixels_batch(c, o, im, id, K, R, t, v, isa);
             for (int q = 0; q < c; q++) {
                 ok[j0 + q] = v[q] ? 1 : 0;
                 std::memcpy(Rt + 12 * (size_t)(j0 + q), R[q], sizeof(R[q]));

@@ -268,6 +268,17 @@ bool trace_env() {
     return e && e[0] == '1';
 }
 
+// final SQPnP fits on the device (SVO_FE_DEVICE_FITS=1, read at create) instead of
+// the host pool: sqpnp_fit_kernel runs one sequence per wave with the 9 x 9
+// eigen-decomposition and the solution search serial in one lane, which measured
+// 4.3 ms per 128-sequence launch on MI355X against the pool's 0.17 ms, and the
+// host fits hide behind the wait for the post-LK results -- so the host is the
+// default and the kernel a cross-check of the shared sqpnp.hpp code
+bool device_fits_env() {
+    const char* e = std::getenv("SVO_FE_DEVICE_FITS");
+    return e && e[0] == '1';
+}
+
 // NUMA node of HIP device d (-1: unknown), from its PCI address in sysfs
 int device_numa_node(int d) {
     char bus[64] = {0};
@@ -325,6 +336,7 @@ struct svo_frontend {
     // sized from the features before LK (nA) with margin spec_margin + lk_loss
     int spec_early = 1;
     bool trace = false;  // SVO_FE_TRACE=1 at create
+    bool device_fits = false;  // SVO_FE_DEVICE_FITS=1 at create (device_fits_env)
     int spec_t = -1;       // step whose speculation went out early
     int spec_m = 0;        // its margin (features lost to LK + RANSAC it covers)
     bool spec_was_early = false;
@@ -728,24 +740,43 @@ int fe_queue_stats(svo_frontend* fe) {
     const int p = fe->stats_parity;
     SVO_HIP(ctx, launch_suffstats(fe->obj_b[p], fe->xyB_b[p], fe->nB_b[p], fe->CAP, fe->h_best_b[p], fe->WORDS, fe->S,
                                   fe->cfg.K, fe->h_stats, fe->st_copy));
-    // and the final SQPnP fits from them, on the device: the next post-LK (which
-    // moves the keyframe's new map points with these poses) waits for ev_stats
-    SVO_HIP(ctx, launch_sqpnp_fit(fe->h_stats, fe->h_fitin, fe->obj_b[p], fe->nB_b[p], fe->CAP, fe->h_best_b[p],
-                                  fe->WORDS, fe->S, fe->h_pose6, fe->h_pose, fe->st_copy));
+    // and, with device_fits, the final SQPnP fits from them on the device: the next
+    // post-LK (which moves the keyframe's new map points with these poses) then
+    // waits for ev_stats
+    if (fe->device_fits)
+        SVO_HIP(ctx, launch_sqpnp_fit(fe->h_stats, fe->h_fitin, fe->obj_b[p], fe->nB_b[p], fe->CAP, fe->h_best_b[p],
+                                      fe->WORDS, fe->S, fe->h_pose6, fe->h_pose, fe->st_copy));
     SVO_HIP(ctx, hipEventRecord(fe->ev_stats, fe->st_copy));
     fe->stats_pending = false;
     return SVO_OK;
 }
 
-// The final SQPnP fits of the last step ran on the device (sqpnp_fit_kernel behind
-// the statistics, fe_queue_stats): the host only reads their poses, when asked
-// for one (svo_frontend_pose / _synchronize); the step itself never waits for
-// them (its post-LK kernel waits on the device).
+// Final SQPnP-objective fits of the last step (from the GPU sufficient
+// statistics in h_stats): they refine the reported poses, so they run lazily --
+// at the next step while the GPU tracks, or when a pose is read. With
+// device_fits they ran on the device behind the statistics (fe_queue_stats) and
+// the host only reads their poses.
 double fe_finish_fits(svo_frontend* fe) {
     if (!fe->fits_pending) return 0.0;
     auto t0 = std::chrono::steady_clock::now();
     (void)hipEventSynchronize(fe->ev_stats);
-    std::memcpy(fe->pose.data(), fe->h_pose6, sizeof(double) * 6 * (size_t)fe->S);
+    if (fe->device_fits) {
+        std::memcpy(fe->pose.data(), fe->h_pose6, sizeof(double) * 6 * (size_t)fe->S);
+    } else {
+        (void)hipEventSynchronize(fe->ev_full_b[fe->fit_parity]);  // cheirality test reads h_obj
+        fe->pool->run(fe->S, [&](int s) {
+            RansacSeq& r = fe->rs[s];
+            r.fit(fe->cfg.K, fe->h_stats + kSqpnpStats * (size_t)s);
+            double* P = &fe->pose[6 * (size_t)s];
+            if (r.ok) {
+                std::memcpy(P, r.rvec, sizeof(r.rvec));
+                std::memcpy(P + 3, r.tvec, sizeof(r.tvec));
+            } else {
+                std::fill(P, P + 6, 0.0);
+            }
+            fe_set_pose(fe, s, r.ok, P, P + 3);
+        });
+    }
     fe->fits_pending = false;
     return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
 }
@@ -964,6 +995,7 @@ int svo_frontend_create(svo_ctx* ctx, const svo_frontend_config* cfg, svo_fronte
         const char* se = std::getenv("SVO_FE_SPEC_EARLY");
         fe->spec_early = se && se[0] == '0' ? 0 : 1;
         fe->trace = trace_env();
+        fe->device_fits = device_fits_env();
     }
     // (on the context stream: a first use of the null stream would take a fifth
     // hardware queue and serialise the step's streams)
@@ -1178,7 +1210,7 @@ static int fe_post(svo_frontend* fe, int t) {
     int slot;
     // the previous step's final fits (sqpnp_fit_kernel) set the poses the post-LK
     // moves the previous keyframe's new map points with
-    SVO_HIP(ctx, hipStreamWaitEvent(sl, fe->ev_stats, 0));
+    if (fe->device_fits) SVO_HIP(ctx, hipStreamWaitEvent(sl, fe->ev_stats, 0));
     PostLkBatch pb{fe->nA, fe->status, fe->next_xy, fe->midA, fe->iters, fe->xyB, fe->midB, fe->nB, fe_pending(fe),
                    fe->obj, CAP, kRansacPrefetch, fe->h_nB, fe->h_itsum, fe->h_samp};
     ph_begin(fe, PH_POST, sl, &slot);
@@ -1399,10 +1431,13 @@ int svo_frontend_step(svo_frontend* fe, int t, svo_frontend_stats* stats) {
     fe->front_t = -1;
     TP("front enqueued");
     const int64_t n_keyframes = fe_keyframe_targets(fe);
-    // the previous step's final pose fits run on the device (fe_queue_stats); this
-    // step's post-LK waits for them there
+    // the previous step's final pose fits: the host does them while the GPU tracks
+    // this frame; they set the poses that move the previous keyframe's new map
+    // points to the world frame, so this step's post-LK is queued right after
+    // (with device_fits they ran on the device and the post-LK waits there)
     ms_enqueue += ms_since(t_call);
-    double ms_fit = 0;
+    double ms_fit = fe->device_fits ? 0.0 : fe_finish_fits(fe);
+    TP("fits done");
     {
         const auto te = clk::now();
         int rp = fe_post(fe, t);

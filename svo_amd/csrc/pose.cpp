@@ -23,7 +23,6 @@
 
 #include "common.hpp"
 #include "epnp.hpp"
-#include "simd_svd.hpp"
 #include "linalg.hpp"
 #include "pose.hpp"
 #include "sqpnp.hpp"
@@ -199,31 +198,27 @@ void RansacSeq::solve(int j, const double K[9]) {
     store(j, v, Rj, tj);
 }
 
+bool epnp_isa_supported(int isa) {
+    static const bool avx2 = __builtin_cpu_supports("avx2"), avx512 = __builtin_cpu_supports("avx512f");
+    return isa == kEpnpScalar || (isa == kEpnpAvx2 && avx2) || (isa == kEpnpAvx512 && avx512);
+}
+
 void epnp_pixels_batch(int count, const float* const* obj, const float* const* img, const int* const* idx,
-                       const double K[9], double (*R)[9], double (*t)[3], bool* ok) {
-    constexpr int L = kEpnpLanes;
+                       const double K[9], double (*R)[9], double (*t)[3], bool* ok, int isa) {
     if (count <= 0) return;
-    if (count > L) count = L;
-    double pw[L][15], uv[L][10], MtM[L][144], ev[L][12], ut[L][144];
-    EPnP es[L] = {EPnP(K[0], K[4], K[2], K[5]), EPnP(K[0], K[4], K[2], K[5]), EPnP(K[0], K[4], K[2], K[5]),
-                  EPnP(K[0], K[4], K[2], K[5])};
-    for (int q = 0; q < count; q++) {
-        epnp_inputs(obj[q], img[q], idx[q], 5, K, pw[q], uv[q]);
-        es[q].prepare(pw[q], uv[q], 5, MtM[q]);
-    }
-    if (count > 1 && la::cv::simd_svd_ok()) {
-        const double* pa[L];
-        double *pe[L], *pu[L];
-        for (int q = 0; q < L; q++) {
-            pa[q] = MtM[q < count ? q : count - 1];  // idle lanes repeat a live problem
-            pe[q] = ev[q];
-            pu[q] = ut[q];
-        }
-        la::cv::svd_ut_lanes<12, L, 1>(pa, pe, pu);
+    if (count > kEpnpLanes) count = kEpnpLanes;
+    if (isa == kEpnpAuto)
+        isa = count == 1                            ? kEpnpScalar
+              : epnp_isa_supported(kEpnpAvx512) ? kEpnpAvx512
+              : epnp_isa_supported(kEpnpAvx2)   ? kEpnpAvx2
+                                                : kEpnpScalar;
+    if (isa == kEpnpAvx512) {
+        epnp_batch_avx512(count, obj, img, idx, K, R, t, ok);
+    } else if (isa == kEpnpAvx2) {
+        epnp_batch_avx2(count, obj, img, idx, K, R, t, ok);
     } else {
-        for (int q = 0; q < count; q++) la::cv::svd_ut<12>(MtM[q], ev[q], ut[q]);
+        for (int q = 0; q < count; q++) ok[q] = epnp_pixels(obj[q], img[q], idx[q], 5, K, R[q], t[q]);
     }
-    for (int q = 0; q < count; q++) ok[q] = es[q].finish(ut[q], R[q], t[q]);
 }
 
 int RansacSeq::gen_chunk(const double K[9]) {

@@ -23,10 +23,18 @@ constexpr int kSampleFloats = 25;  // 5 points x (obj xyz, pixel xy)
 
 // The RANSAC minimal solver batched: EPnP of count <= kEpnpLanes 5-point subsets
 // (subset q: points idx[q][0..5) of obj[q] / img[q], or points 0..4 when idx[q]
-// is null), bit-identical to epnp_pixels on each, the 12 x 12 M^T M SVDs run in
-// SIMD lanes together (simd_svd.hpp). ok[q]: finite model.
-constexpr int kEpnpLanes = 4;
+// is null), bit-identical to epnp_pixels on each: the whole solver runs in SIMD
+// lanes (epnp_lanes.hpp), AVX-512 (8 lanes x 2 interleaved groups) or AVX2 (4 x
+// 4) as the CPU has it, else scalar. ok[q]: finite model.
+constexpr int kEpnpLanes = 16;
+enum EpnpIsa { kEpnpAuto = -1, kEpnpScalar = 0, kEpnpAvx2 = 1, kEpnpAvx512 = 2 };
+bool epnp_isa_supported(int isa);
 void epnp_pixels_batch(int count, const float* const* obj, const float* const* img, const int* const* idx,
+                       const double K[9], double (*R)[9], double (*t)[3], bool* ok, int isa = kEpnpAuto);
+// the per-instruction-set bodies (epnp_avx2.cpp, epnp_avx512.cpp; count <= 16)
+void epnp_batch_avx2(int count, const float* const* obj, const float* const* img, const int* const* idx,
+                     const double K[9], double (*R)[9], double (*t)[3], bool* ok);
+void epnp_batch_avx512(int count, const float* const* obj, const float* const* img, const int* const* idx,
                        const double K[9], double (*R)[9], double (*t)[3], bool* ok);
 struct RansacSeq;
 // hypotheses js[q] of sequences seqs[q] (q < count <= kEpnpLanes; drawn by

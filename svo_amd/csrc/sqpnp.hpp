@@ -234,9 +234,11 @@ struct SqSol {
 template <class Run, class Front>
 SVO_HD void sq_select(const SqpnpCost& c, const double* ev, const double* evec, int nn, int n, Run run,
                       Front n_front, double R[9], double t[3], bool* found) {
-    constexpr int kMaxSols = 32;
-    SqSol sols[kMaxSols];
-    int nsol = 0;
+    // OpenCV keeps every distinct solution within 1e-6 of the smallest error and
+    // returns the first; a later one can replace only the first, when it is the
+    // same rotation with a smaller error, so only that one is kept here
+    SqSol best{};
+    bool have = false;
     double min_err = 1.7976931348623157e308;
     auto check = [&](SqSol& s) {
         for (int a = 0; a < 3; a++) {
@@ -253,22 +255,13 @@ SVO_HD void sq_select(const SqpnpCost& c, const double* ev, const double* evec, 
         if (fabs(min_err - s.err) > 1e-6) {
             if (min_err > s.err) {
                 min_err = s.err;
-                sols[0] = s;
-                nsol = 1;
+                best = s;
+                have = true;
             }
         } else {
-            bool same = false;
-            for (int q = 0; q < nsol; q++) {
-                SqSol& o = sols[q];
-                double d = 0;
-                for (int k = 0; k < 9; k++) d += (o.r[k] - s.r[k]) * (o.r[k] - s.r[k]);
-                if (d < 1e-10) {
-                    if (o.err > s.err) o = s;
-                    same = true;
-                    break;
-                }
-            }
-            if (!same && nsol < kMaxSols) sols[nsol++] = s;
+            double d = 0;
+            for (int k = 0; k < 9; k++) d += (best.r[k] - s.r[k]) * (best.r[k] - s.r[k]);
+            if (d < 1e-10 && best.err > s.err) best = s;
             if (min_err > s.err) min_err = s.err;
         }
     };
@@ -292,10 +285,10 @@ SVO_HD void sq_select(const SqpnpCost& c, const double* ev, const double* evec, 
         }
     }
     for (int k = 1; 9 - nn - k > 0 && min_err > 3 * ev[9 - nn - k]; k++) from_eigen(9 - nn - k);
-    *found = nsol > 0;
-    if (!*found) return;
-    for (int k = 0; k < 9; k++) R[k] = sols[0].r[k];  // (rodrigues_inv re-orthonormalises, as cv::Rodrigues)
-    for (int k = 0; k < 3; k++) t[k] = sols[0].t[k];
+    *found = have;
+    if (!have) return;
+    for (int k = 0; k < 9; k++) R[k] = best.r[k];  // (rodrigues_inv re-orthonormalises, as cv::Rodrigues)
+    for (int k = 0; k < 3; k++) t[k] = best.t[k];
 }
 
 }  // namespace sq

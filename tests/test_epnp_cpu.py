@@ -46,8 +46,65 @@ def host_epnp(subs, device=0):
     f32p, f64p, i32p = C.POINTER(C.c_float), C.POINTER(C.c_double), C.POINTER(C.c_int)
     rc = S.lib().svo_epnp_subsets(None, subs.ctypes.data_as(f32p), m, K.ctypes.data_as(f64p), device,
                                   Rt.ctypes.data_as(f64p), ok.ctypes.data_as(i32p))
-    assert rc == 0
+    assert rc == 0, rc
     return Rt, ok
+
+
+def degenerate_subsets(seed, m):
+    """Subsets that drive the solver's rare branches: coplanar, collinear and
+    repeated points, a point at the centroid, all points at one depth, pixels
+    with the same coordinates (rank-deficient M^T M, zero singular values, zero
+    Householder scales, non-finite models)."""
+    rng = np.random.default_rng(seed)
+    base, _, _ = subsets(seed, m, 0.3)
+    out = base.copy()
+    for j in range(m):
+        X = out[j, :15].reshape(5, 3)
+        uv = out[j, 15:].reshape(5, 2)
+        kind = j % 7
+        if kind == 0:
+            X[:, 1] = X[0, 1]  # coplanar
+        elif kind == 1:
+            d = rng.uniform(-1, 1, 3).astype(np.float32)
+            X[:] = X[0] + np.outer(np.arange(5, dtype=np.float32), d)  # collinear
+        elif kind == 2:
+            X[1] = X[0]
+            uv[1] = uv[0]  # a repeated correspondence
+        elif kind == 3:
+            X[:, 2] = X[0, 2]  # one depth
+        elif kind == 4:
+            uv[:] = uv[0]  # every pixel the same
+        elif kind == 5:
+            X[:] = X[0]  # every point the same
+        else:
+            X[4] = X[:4].mean(0)
+    return out
+
+
+@pytest.mark.parametrize("device", [3, 4, 5])
+def test_host_epnp_every_instruction_set_is_the_oracle(device):
+    """The solver's scalar, AVX2-lane and AVX-512-lane forms (svo_epnp_subsets
+    device = 3 / 4 / 5, epnp_lanes.hpp) each give the oracle's bits, on ordinary
+    and on degenerate subsets, with every batch width (counts 1..16 leave idle
+    lanes)."""
+    f32p, f64p, i32p = C.POINTER(C.c_float), C.POINTER(C.c_double), C.POINTER(C.c_int)
+    probe = np.zeros((1, 25), np.float32)
+    rc = S.lib().svo_epnp_subsets(None, probe.ctypes.data_as(f32p), 1, K.ctypes.data_as(f64p), device,
+                                  np.zeros(12).ctypes.data_as(f64p), np.zeros(1, np.int32).ctypes.data_as(i32p))
+    if rc == -4:
+        pytest.skip("instruction set not on this CPU")
+    subs = np.r_[subsets(21, 203, 0.5)[0], degenerate_subsets(22, 140)]
+    differ = nonfinite = 0
+    for lo, hi in ((0, 1), (1, 4), (4, 11), (11, 27), (27, len(subs))):
+        Rt, ok = host_epnp(subs[lo:hi], device)
+        for k in range(lo, hi):
+            rc, Ro, to = O.epnp(subs[k, :15].reshape(5, 3), subs[k, 15:].reshape(5, 2), K)
+            assert rc in (0, -2)  # -2: a non-finite model, reported as ok = 0
+            nonfinite += rc != 0
+            differ += (ok[k - lo] != (rc == 0) or
+                       not np.array_equal(np.r_[Ro.ravel(), to].view(np.uint64), Rt[k - lo].view(np.uint64)))
+    assert differ == 0, f"{differ} of {len(subs)} subsets differ"
+    assert nonfinite > 0  # the degenerate subsets reach the non-finite path
 
 
 @pytest.mark.parametrize("noise", [0.0, 0.3, 3.0])

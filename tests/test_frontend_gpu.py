@@ -257,6 +257,39 @@ def test_frontend_trace_mode_matches_oracle_loop(monkeypatch):
             assert np.array_equal(fe.features(q), ref.pts), f"seq {q} features at t={t}"
 
 
+def test_frontend_device_fits_match_host_fits(monkeypatch):
+    """SVO_FE_DEVICE_FITS=1: the final SQPnP fits run in sqpnp_fit_kernel (the
+    shared sqpnp.hpp code on the device) instead of the host pool -- the same
+    poses bit for bit, hence the same map points and features, and the oracle's
+    poses step by step."""
+    ctx = S.Context(0)
+    W, H, N, T = 640, 376, 800, 6
+    seeds = (3, 8, 5)
+
+    def run(device):
+        monkeypatch.setenv("SVO_FE_DEVICE_FITS", "1" if device else "0")
+        fe = make_frontend(ctx, [SceneForward(W, H, seed=sd) for sd in seeds], T, N)
+        fe.init(0)
+        out = []
+        for t in range(1, T):
+            fe.step(t)
+            out.append([(np.r_[fe.pose(q)], fe.map_points(q).copy(), fe.features(q).copy())
+                        for q in range(len(seeds))])
+        return out
+
+    host, dev = run(False), run(True)
+    refs = [OracleLoop(SceneForward(W, H, seed=sd), N).init(0) for sd in seeds]
+    for t in range(1, T):
+        for q, ref in enumerate(refs):
+            ref.step(t)
+            ph, mh, fh = host[t - 1][q]
+            pd, md, fd = dev[t - 1][q]
+            assert np.array_equal(ph, pd), f"seq {q} pose at t={t}"
+            assert np.array_equal(mh, md) and np.array_equal(fh, fd), f"seq {q} map at t={t}"
+            np.testing.assert_allclose(pd[:3], ref.pose[0], atol=1e-7)
+            np.testing.assert_allclose(pd[3:], ref.pose[1], atol=1e-6)
+
+
 def test_frontend_200_frames_kitti_matches_oracle_loop():
     """BASELINE.json configs[0]: 200 frames of a 1241x376 sequence with 2000
     features, every step against the oracle loop (R:src/tracking.cpp:232-276)."""
