@@ -409,22 +409,23 @@ __global__ __launch_bounds__(256) void fast_detect_q_kernel(FastDetBatch B, int 
         const unsigned long long bal = RB[tid] & (boxes ? TM[tid] : ~0ull);
         const size_t row = seq * h + y0 + tid;
         B.bits[row * B.nseg + blockIdx.x] = bal;
-        if (bal) atomicAdd(&B.rowcnt[row], __popcll(bal));
     }
 }
 
 // ---- box filter of an unmasked detection (kFastBoxes): the previous frame's
 // feature boxes rasterised per 64x32 tile exactly as fast_detect_q_kernel<32> does
 // (cv::rectangle semantics from the band-binned centres), ANDed into the row words
-// the detection wrote, row counts recounted. The boxes are applied after NMS in
+// the detection wrote (fast_scan_kernel counts them). The boxes are applied after NMS in
 // every form, so detecting first and masking later gives the same keypoints. ----
-__global__ __launch_bounds__(256) void fast_box_filter_kernel(FastDetBatch B, int w, int h) {
+__global__ __launch_bounds__(64) void fast_box_filter_kernel(FastDetBatch B, int w, int h) {
+    // one wave per 64 x 32 tile: the lanes first read the box ranges of the tile's
+    // bands (one cell range per band), then take the boxes of all bands together
     constexpr int TY = 32;
     const int x0 = blockIdx.x * FD_TX, y0 = blockIdx.y * TY;
     const size_t seq = blockIdx.z;
     __shared__ unsigned long long TM[TY];
-    const int tid = threadIdx.x;
-    if (tid < TY) TM[tid] = ~0ull;
+    const int lane = threadIdx.x;
+    if (lane < TY) TM[lane] = ~0ull;
     __syncthreads();
     const int nb = (h + 15) / 16, ncl = (w + 63) / 64;
     const int* __restrict__ cells = B.box_band + seq * (size_t)(nb * ncl + 1);
@@ -432,12 +433,28 @@ __global__ __launch_bounds__(256) void fast_box_filter_kernel(FastDetBatch B, in
     const int b1 = min(nb - 1, (int)floorf((y0 + TY + B.box_half + 1.f) / 16.f));
     const int cb0 = max(0, (int)floorf((x0 - B.box_half - 1.f) / 64.f));
     const int cb1 = min(ncl - 1, (int)floorf((x0 + FD_TX + B.box_half + 1.f) / 64.f));
-    const float* __restrict__ pts = B.box_binned + 2 * seq * (size_t)B.box_stride;
-    for (int bq = b0; bq <= b1; bq++)
-        for (int i = cells[bq * ncl + cb0] + tid, i1 = cells[bq * ncl + cb1 + 1]; i < i1; i += 256) {
-            const float px = pts[2 * i], py = pts[2 * i + 1];
-            const int xa = (int)__builtin_rintf(px - B.box_half), ya = (int)__builtin_rintf(py - B.box_half);
-            const int xb = (int)__builtin_rintf(px + B.box_half), yb = (int)__builtin_rintf(py + B.box_half);
+    const float2* __restrict__ pts = reinterpret_cast<const float2*>(B.box_binned + 2 * seq * (size_t)B.box_stride);
+    for (int bb = b0; bb <= b1; bb += 64) {
+        const int nband = min(64, b1 - bb + 1);
+        int lo = 0, cnt = 0;
+        if (lane < nband) {
+            lo = cells[(bb + lane) * ncl + cb0];
+            cnt = cells[(bb + lane) * ncl + cb1 + 1] - lo;
+        }
+        int total = 0;
+        for (int q = 0; q < nband; q++) total += __shfl(cnt, q);
+        for (int j = lane; j < total; j += 64) {
+            // the band holding box j of the concatenated ranges
+            int q = 0, base = 0, c = __shfl(cnt, 0);
+            while (j >= base + c) {
+                base += c;
+                q++;
+                c = __shfl(cnt, q);
+            }
+            const int i = __shfl(lo, q) + (j - base);
+            const float2 pt = pts[i];
+            const int xa = (int)__builtin_rintf(pt.x - B.box_half), ya = (int)__builtin_rintf(pt.y - B.box_half);
+            const int xb = (int)__builtin_rintf(pt.x + B.box_half), yb = (int)__builtin_rintf(pt.y + B.box_half);
             int xl = min(xa, xb), xr = max(xa, xb), yt = min(ya, yb), yd = max(ya, yb);
             xl = max(xl, max(0, x0));
             xr = min(xr, min(w - 1, x0 + FD_TX - 1));
@@ -448,13 +465,12 @@ __global__ __launch_bounds__(256) void fast_box_filter_kernel(FastDetBatch B, in
             const unsigned long long span = (c1 - c0 == 63) ? ~0ull : (((1ull << (c1 - c0 + 1)) - 1ull) << c0);
             for (int y = yt; y <= yd; y++) atomicAnd(&TM[y - y0], ~span);
         }
+    }
     __syncthreads();
-    if (tid < TY && y0 + tid < h) {
-        const size_t row = seq * h + y0 + tid;
+    if (lane < TY && y0 + lane < h) {
+        const size_t row = seq * h + y0 + lane;
         unsigned long long* word = B.bits + row * B.nseg + blockIdx.x;
-        const unsigned long long bal = *word & TM[tid];
-        *word = bal;
-        if (bal) atomicAdd(&B.rowcnt[row], __popcll(bal));
+        *word &= TM[lane];
     }
 }
 
@@ -514,19 +530,26 @@ __global__ __launch_bounds__(256) void box_bin_kernel(FastDetBatch B, int w, int
     }
 }
 
-// exclusive scan of the per-row counts of one sequence (one 256-thread block per
-// sequence -- it finds room beside LK, a 1024-thread block waits for a whole CU):
-// each thread sums a run of consecutive rows, one block scan of the run sums
+// per-row corner counts (popcounts of the row words the detection / box filter
+// wrote: no atomics in those kernels) and their exclusive scan, one sequence per
+// 256-thread block (it finds room beside LK, a 1024-thread block waits for a whole
+// CU): each thread counts a run of consecutive rows, one block scan of the run sums
 constexpr int kScanBlock = 256;
 __global__ __launch_bounds__(kScanBlock) void fast_scan_kernel(FastDetBatch B, int h) {
     const size_t seq = blockIdx.x;
-    const int* __restrict__ cnt = B.rowcnt + seq * h;
+    int* __restrict__ cnt = B.rowcnt + seq * h;
     int* __restrict__ off = B.rowoff + seq * h;
+    const unsigned long long* __restrict__ words = B.bits + seq * (size_t)h * B.nseg;
     __shared__ int part[kScanBlock];
     const int tid = threadIdx.x;
     const int run = (h + kScanBlock - 1) / kScanBlock, y0 = tid * run, y1 = min(h, y0 + run);
     int sum = 0;
-    for (int y = y0; y < y1; y++) sum += cnt[y];
+    for (int y = y0; y < y1; y++) {  // the row's corners: the popcount of its words
+        int c = 0;
+        for (int sgi = 0; sgi < B.nseg; sgi++) c += __popcll(words[(size_t)y * B.nseg + sgi]);
+        cnt[y] = c;
+        sum += c;
+    }
     part[tid] = sum;
     __syncthreads();
     for (int o = 1; o < kScanBlock; o <<= 1) {
@@ -633,21 +656,19 @@ hipError_t launch_fast_detect(const FastDetBatch& b0, int nseq, int w, int h, in
     if (stage == kFastBoxes) {
         if (b.mask) return hipErrorInvalidValue;  // a host mask goes with the detection
         if (b.box_pts) {
-            hipError_t e = hipMemsetAsync(b.rowcnt, 0, sizeof(int) * (size_t)h * nseq, st);
-            if (e != hipSuccess) return e;
+            hipError_t e = hipSuccess;
             if (!b.box_prebinned) {
                 e = launch_box_bin(b, nseq, w, h, st);
                 if (e != hipSuccess) return e;
             }
-            hipLaunchKernelGGL(fast_box_filter_kernel, dim3((w + FD_TX - 1) / FD_TX, (h + 31) / 32, nseq), dim3(256),
+            hipLaunchKernelGGL(fast_box_filter_kernel, dim3((w + FD_TX - 1) / FD_TX, (h + 31) / 32, nseq), dim3(64),
                                0, st, b, w, h);
         }
         hipLaunchKernelGGL(fast_scan_kernel, dim3(nseq), dim3(kScanBlock), 0, st, b, h);
         hipLaunchKernelGGL(fast_emit_kernel, dim3(h, nseq), dim3(64), 0, st, b, threshold, nonmax);
         return hipGetLastError();
     }
-    hipError_t e = hipMemsetAsync(b.rowcnt, 0, sizeof(int) * (size_t)h * nseq, st);
-    if (e != hipSuccess) return e;
+    hipError_t e = hipSuccess;
     if (b.box_pts && !b.box_prebinned) {
         e = launch_box_bin(b, nseq, w, h, st);
         if (e != hipSuccess) return e;

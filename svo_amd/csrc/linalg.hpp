@@ -80,8 +80,9 @@ SVO_HD void sym_eig(double* A, int n, double* w, double* V) {
 // Jacobi for the 12x12 EPnP system. Same convention as sym_eig: A (n x n,
 // n <= 12, row-major) is read only; eigenvalues descending in w; eigenvector
 // i in row i of Vt.
-SVO_HD void sym_eig_ql_n(const double* A, int n, double* w, double* Vt) {
-    double V[144], d[12], e[12];
+// V (n * n), d, e (n each): workspace the caller provides -- the device fit keeps it
+// in LDS (sqpnp_fit_kernel), the host on the stack (sym_eig_ql_n)
+SVO_HD void sym_eig_ql_ws(const double* A, int n, double* w, double* Vt, double* V, double* d, double* e) {
     for (int i = 0; i < n * n; i++) V[i] = A[i];
     // tred2: V <- orthogonal Q, d/e <- diagonal / off-diagonal of Q^T A Q
     for (int j = 0; j < n; j++) d[j] = V[(n - 1) * n + j];
@@ -219,6 +220,10 @@ SVO_HD void sym_eig_ql_n(const double* A, int n, double* w, double* Vt) {
         w[i] = d[order[i]];
         for (int k = 0; k < n; k++) Vt[i * n + k] = V[k * n + order[i]];
     }
+}
+SVO_HD void sym_eig_ql_n(const double* A, int n, double* w, double* Vt) {
+    double V[144], d[12], e[12];
+    sym_eig_ql_ws(A, n, w, Vt, V, d, e);
 }
 
 // sym_eig_ql for a compile-time n with V stored transposed, so that the column

@@ -189,39 +189,184 @@ __global__ __launch_bounds__(256) void suffstats_kernel(const float* __restrict_
 
 }  // namespace
 
+namespace {
+
+// broadcast of lane `src`'s double (src uniform)
+__device__ __forceinline__ double bcast(double v, int src) {
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_readlane((int)(b & 0xffffffffll), src);
+    const int hi = __builtin_amdgcn_readlane((int)(b >> 32), src);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+
+// sq::sqp_step with the 15 x 16 KKT system one row per lane (lanes 0..14, the row
+// in registers): the same elements, the same pivot (the first largest |a| below
+// the diagonal, found by the serial scan), the same eliminations and the same
+// back-substitution order as the scalar routine, so delta is bit-identical.
+// Every lane returns delta. Jw: this wave's LDS rows of J (6 x 9).
+__device__ __noinline__ void sqp_step_wave(const double* Om, const double* r, double* delta, double* Jw) {
+    constexpr int N = 15;
+    const int lane = threadIdx.x & 63;
+    const double* r1 = r;
+    const double* r2 = r + 3;
+    const double* r3 = r + 6;
+    if (lane < 54) {  // J[c][j] = 0 except the row-norm / row-dot entries
+        const int c = lane / 9, j = lane % 9, k = j % 3, blk = j / 3;
+        double v = 0;
+        if (c == 0 && blk == 0) v = 2 * r1[k];
+        if (c == 1 && blk == 1) v = 2 * r2[k];
+        if (c == 2 && blk == 2) v = 2 * r3[k];
+        if (c == 3) v = blk == 0 ? r2[k] : blk == 1 ? r1[k] : 0.0;
+        if (c == 4) v = blk == 1 ? r3[k] : blk == 2 ? r2[k] : 0.0;
+        if (c == 5) v = blk == 0 ? r3[k] : blk == 2 ? r1[k] : 0.0;
+        Jw[lane] = v;
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    const double h[6] = {dot3(r1, r1) - 1, dot3(r2, r2) - 1, dot3(r3, r3) - 1, dot3(r1, r2), dot3(r2, r3),
+                         dot3(r1, r3)};
+    double a[N + 1];
+    for (int j = 0; j <= N; j++) a[j] = 0;
+    if (lane < 9) {
+        double g = 0;
+        for (int j = 0; j < 9; j++) {
+            a[j] = 2 * Om[9 * lane + j];
+            g += Om[9 * lane + j] * r[j];
+        }
+        a[N] = -2 * g;
+        for (int c = 0; c < 6; c++) a[9 + c] = Jw[9 * c + lane];
+    } else if (lane < N) {
+        const int c = lane - 9;
+        for (int j = 0; j < 9; j++) a[j] = Jw[9 * c + j];
+        double hc = h[0];
+        for (int q = 1; q < 6; q++)
+            if (c == q) hc = h[q];
+        a[N] = -hc;
+    }
+#pragma unroll
+    for (int col = 0; col < N; col++) {
+        // the scalar loop's pivot: first strict maximum of |a[i][col]|, i >= col
+        int piv = col;
+        double best = fabs(bcast(a[col], col));
+#pragma unroll
+        for (int i = col + 1; i < N; i++) {
+            const double v = fabs(bcast(a[col], i));
+            if (v > best) {
+                best = v;
+                piv = i;
+            }
+        }
+        double prow[N + 1];  // row col after the swap
+        if (piv != col) {
+#pragma unroll
+            for (int j = 0; j <= N; j++) {
+                const double cj = bcast(a[j], col), pj = bcast(a[j], piv);
+                if (lane == col) a[j] = pj;
+                if (lane == piv) a[j] = cj;
+                prow[j] = pj;
+            }
+        } else {
+#pragma unroll
+            for (int j = 0; j <= N; j++) prow[j] = bcast(a[j], col);
+        }
+        const double d = prow[col];
+        if (d == 0) continue;
+        if (lane > col && lane < N) {
+            const double f = a[col] / d;
+            if (f != 0)
+#pragma unroll
+                for (int j = col; j <= N; j++) a[j] -= f * prow[j];
+        }
+    }
+    double x[N];
+#pragma unroll
+    for (int i = N - 1; i >= 0; i--) {
+        double xi = 0;
+        if (lane == i) {
+            double v = a[N];
+#pragma unroll
+            for (int j = i + 1; j < N; j++) v -= a[j] * x[j];
+            xi = a[i] != 0 ? v / a[i] : 0.0;
+        }
+        x[i] = bcast(xi, i);
+    }
+    for (int k = 0; k < 9; k++) delta[k] = x[k];
+}
+
+// sq::sq_start with sqp_run's steps taken by sqp_step_wave (every lane holds r)
+__device__ void sq_start_wave(const sq::SqpnpCost& c, const double* evec, int j, double* rhat, double* Jw) {
+    const double* ev = evec + 9 * (j >> 1);
+    double m[9], r[9], delta[9];
+    for (int k = 0; k < 9; k++) m[k] = (j & 1) ? -(1.7320508075688772 * ev[k]) : 1.7320508075688772 * ev[k];
+    la::nearest_rotation(m, r);
+    double dsq = 1.7976931348623157e308;
+    int step = 0;
+    while (dsq > 1e-10 && step++ < 15) {
+        sqp_step_wave(c.Om, r, delta, Jw);
+        dsq = 0;
+        for (int k = 0; k < 9; k++) {
+            r[k] += delta[k];
+            dsq += delta[k] * delta[k];
+        }
+    }
+    double d = r[0] * (r[4] * r[8] - r[5] * r[7]) - r[1] * (r[3] * r[8] - r[5] * r[6]) + r[2] * (r[3] * r[7] - r[4] * r[6]);
+    if (d < 0) {
+        for (int k = 0; k < 9; k++) r[k] = -r[k];
+        d = -d;
+    }
+    if (d > 1.001)
+        la::nearest_rotation(r, rhat);
+    else
+        for (int k = 0; k < 9; k++) rhat[k] = r[k];
+}
+
+constexpr int kFitWaves = 9;  // one wave per eigenvector: its two starts, +e and -e
+
+}  // namespace
+
 // solvePnP(SQPNP) on a sequence's RANSAC inliers (SqpnpFitIn mode 1) and the
-// Frame::pose() of every outcome (R:src/tracking.cpp:191-214). Lane 0 assembles the
-// cost and Omega's eigen-decomposition; lanes 0..17 run the SQP from the 18 starts
-// (the 9 eigenvectors, each +- sqrt(3) e) -- every start a search could ask for,
-// each independent of the others; lane 0 then replays the search (sq_select) with
-// those results, which takes the same steps as the host's on-demand runs.
-__global__ __launch_bounds__(64) void sqpnp_fit_kernel(const double* __restrict__ stats,
-                                                       const SqpnpFitIn* __restrict__ in,
-                                                       const float* __restrict__ obj, const int* __restrict__ counts,
-                                                       int cap, const uint32_t* __restrict__ bits, int words_cap,
-                                                       double* __restrict__ pose6, double* __restrict__ pose12) {
-    const int s = blockIdx.x, lane = threadIdx.x;
+// Frame::pose() of every outcome (R:src/tracking.cpp:191-214), one block of 9
+// waves per sequence. Lane 0 assembles the cost and Omega's eigen-decomposition
+// (sym_eig_ql with its workspace in LDS); wave w then runs the SQP from the starts
+// 2w and 2w + 1 (+- sqrt(3) times eigenvector w) with its 15 x 16 KKT systems one
+// row per lane (sqp_step_wave) -- every start a search could ask for, each
+// independent of the others; wave 0 replays the search (sq_select) with those
+// results, which takes the same steps as the host's on-demand runs, its
+// positive-depth counts spread over the lanes. Bit-identical to the host fit
+// (RansacSeq::fit) on the same statistics.
+__global__ __launch_bounds__(64 * kFitWaves) void sqpnp_fit_kernel(const double* __restrict__ stats,
+                                                                   const SqpnpFitIn* __restrict__ in,
+                                                                   const float* __restrict__ obj,
+                                                                   const int* __restrict__ counts, int cap,
+                                                                   const uint32_t* __restrict__ bits, int words_cap,
+                                                                   double* __restrict__ pose6,
+                                                                   double* __restrict__ pose12) {
+    const int s = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     __shared__ sq::SqpnpCost c;
-    __shared__ double ev[9], evec[81], rs[18][9];
+    __shared__ double ev[9], evec[81], rs[18][9], ws[81 + 9 + 9], Jw[kFitWaves][54];
     __shared__ int nn_s;
     const SqpnpFitIn fin = in[s];
     if (fin.mode == 1) {
-        if (lane == 0) {
+        if (tid == 0) {
             sq::sqpnp_assemble(stats + 40 * (size_t)s, c);
             int nn = -1;
             if (c.ok) {
-                double Oc[81];
-                for (int k = 0; k < 81; k++) Oc[k] = c.Om[k];
-                la::sym_eig_ql(Oc, 9, ev, evec);
+                la::sym_eig_ql_ws(c.Om, 9, ev, evec, ws, ws + 81, ws + 90);
                 nn = sq::sq_null_count(ev);
             }
             nn_s = nn;
         }
         __syncthreads();
-        if (nn_s >= 0 && lane < 18) sq::sq_start(c, evec, lane, rs[lane]);
+        if (nn_s >= 0)
+            for (int j = 2 * wave; j < 2 * wave + 2; j++) {
+                double r[9];
+                sq_start_wave(c, evec, j, r, Jw[wave]);
+                if (lane == 0)
+                    for (int k = 0; k < 9; k++) rs[j][k] = r[k];
+            }
         __syncthreads();
     }
-    if (lane != 0) return;
+    if (wave != 0) return;
     double rvec[3] = {0, 0, 0}, tvec[3] = {0, 0, 0};
     if (fin.mode == 2) {
         for (int k = 0; k < 3; k++) {
@@ -236,7 +381,10 @@ __global__ __launch_bounds__(64) void sqpnp_fit_kernel(const double* __restrict_
             const float* o = obj + 3 * (size_t)s * cap;
             const uint32_t* b = bits + (size_t)s * words_cap;
             int n_in = 0;
-            for (int w = 0; w < (n + 31) / 32; w++) n_in += __popc(b[w] & (w == n / 32 ? (1u << (n & 31)) - 1u : ~0u));
+            for (int w = lane; w < (n + 31) / 32; w += 64)
+                n_in += __popc(b[w] & (w == n / 32 ? (1u << (n & 31)) - 1u : ~0u));
+            for (int off = 32; off > 0; off >>= 1) n_in += __shfl_xor(n_in, off);
+            // every lane runs the search (uniform: the same values everywhere)
             sq::sq_select(
                 c, ev, evec, nn_s, n_in,
                 [&](int j, double* r) {
@@ -244,11 +392,12 @@ __global__ __launch_bounds__(64) void sqpnp_fit_kernel(const double* __restrict_
                 },
                 [&](const double* r, const double* tt) {
                     int pos = 0;
-                    for (int i = 0; i < n; i++) {
+                    for (int i = lane; i < n; i += 64) {
                         if (!((b[i >> 5] >> (i & 31)) & 1u)) continue;
                         const double p[3] = {(double)o[3 * i], (double)o[3 * i + 1], (double)o[3 * i + 2]};
                         pos += dot3(r + 6, p) + tt[2] > 0;
                     }
+                    for (int off = 32; off > 0; off >>= 1) pos += __shfl_xor(pos, off);
                     return pos;
                 },
                 R, t, &found);
@@ -261,6 +410,7 @@ __global__ __launch_bounds__(64) void sqpnp_fit_kernel(const double* __restrict_
             for (int k = 0; k < 3; k++) tvec[k] = fin.t[k];
         }
     }
+    if (lane != 0) return;
     double* P6 = pose6 + 6 * (size_t)s;
     for (int k = 0; k < 3; k++) {
         P6[k] = rvec[k];
@@ -279,8 +429,8 @@ hipError_t launch_sqpnp_fit(const double* stats, const SqpnpFitIn* in, const flo
                             const uint32_t* bits, int words_cap, int nseq, double* pose6, double* pose12,
                             hipStream_t st) {
     if (nseq <= 0) return hipSuccess;
-    hipLaunchKernelGGL(sqpnp_fit_kernel, dim3(nseq), dim3(64), 0, st, stats, in, obj, counts, cap, bits, words_cap,
-                       pose6, pose12);
+    hipLaunchKernelGGL(sqpnp_fit_kernel, dim3(nseq), dim3(64 * kFitWaves), 0, st, stats, in, obj, counts, cap, bits,
+                       words_cap, pose6, pose12);
     return hipGetLastError();
 }
 
