@@ -20,6 +20,7 @@ from __future__ import annotations
 
 import argparse
 import json
+import re
 import os
 import sys
 import time
@@ -168,6 +169,42 @@ def pmc_traffic(cfg_name: str, kernel_prefix: str):  # substring of the demangle
             continue
         return v.get("hbm_bytes_per_launch")
     return None
+
+
+VALU_PEAK_G = 256 * 4 * 2.4 / 2  # G wave64 VALU instructions/s: 256 CUs x 4 SIMD-32, 2 cycles each at 2.4 GHz
+
+
+def pmc_valu(kernel_prefix: str, seqs: int):
+    """VALU wave-instructions per launch of a kernel from the committed SQ mix pass
+    (profiles/valu_summary.json, written by tools/gpu.sh mix: SQ_INSTS_VALU per
+    dispatch), scaled from the sequences per launch it was measured at to `seqs`;
+    None when absent."""
+    path = os.path.join(ROOT, "profiles", "valu_summary.json")
+    try:
+        with open(path) as f:
+            d = json.load(f)
+    except (OSError, ValueError):
+        return None, None
+    m = re.search(r"--seq (\d+)", d.get("source", ""))
+    measured = int(m.group(1)) if m else 128
+    for k, v in d.get("kernels", {}).items():
+        if kernel_prefix in k:
+            return v["valu_per_dispatch"] * seqs / measured, d.get("source")
+    return None, None
+
+
+def roofline_valu(lk_name: str, seqs: int, lk_avg_s: float):
+    """LK against the bound that binds it, VALU issue (SURVEY.md 8(d) prices it by
+    bytes; rocprof shows the kernel issue-bound): the mix pass's VALU
+    instructions per launch over this run's live average launch time."""
+    kname = lk_name.split("<")[0]
+    valu, src = pmc_valu(kname, seqs)
+    if valu is None or lk_avg_s <= 0:
+        return None
+    ach = valu / lk_avg_s / 1e9
+    return {"kernel": lk_name + ">", "bound": "valu", "achieved": round(ach, 1), "peak": VALU_PEAK_G,
+            "unit": "G wave-instr/s", "frac": round(ach / VALU_PEAK_G, 4), "valu_per_launch": int(valu),
+            "source": src, "timing": "live average launch time (the roofline's)"}
 
 
 def cpu_baseline(cfg_name: str, seconds: float):
@@ -544,6 +581,7 @@ def main():
             "avg_launch_us": round(lk_avg_s * 1e6, 3),
             "launches_timed": lk_n,
         },
+        "roofline_valu": roofline_valu(lk_name, Sq, lk_avg_s),
         "roofline_pyramid": {
             "kernel": f"pyramid chain: {pyr_kernels}; one new left frame of {Sq} sequences per launch",
             "bound": "hbm",

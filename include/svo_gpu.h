@@ -285,6 +285,14 @@ typedef struct svo_frontend_config {
     int stereo_max_level;   /* -> 3 */
     int stereo_max_count;   /* :97 -> 30 */
     double stereo_epsilon;  /* -> 1e-3 */
+    /* keyframe detector (R:src/tracking.cpp:33-57): 0 = FAST(fast_threshold,
+     * fast_nonmax); 1 = cv::ORB with `orb` (the shipped config, use_orb: 1,
+     * R:configs/config.yaml:19-27) -- ORB keypoints (level-0 coordinates, level
+     * order) replace FAST's as the keyframe's candidates; detected only on the
+     * steps where some sequence takes a keyframe, through the serial keyframe path
+     * (no speculative stereo LK, no FAST pre-detection, no bucketing) */
+    int use_orb;
+    svo_orb_params orb;
 } svo_frontend_config;
 
 typedef struct svo_frontend_stats {

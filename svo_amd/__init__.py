@@ -533,7 +533,9 @@ class FrontendConfig(C.Structure):
     (R:configs/config.yaml:29-32), solvePnPRansac args (:191-196) and
     features_to_track (R:configs/config.yaml:15). keyframe_rule: KF_EVERY (every
     frame a keyframe topping the set up to n_features; the benchmark) or
-    KF_REFERENCE (Tracking::nextFrame's rule, R:src/tracking.cpp:68-69)."""
+    KF_REFERENCE (Tracking::nextFrame's rule, R:src/tracking.cpp:68-69).
+    use_orb=1 + orb=OrbParams(...): the keyframe detector is ORB (the shipped
+    config, R:configs/config.yaml:19-27) instead of FAST."""
     _fields_ = [
         ("width", C.c_int), ("height", C.c_int), ("n_seq", C.c_int), ("n_frames", C.c_int),
         ("n_features", C.c_int), ("max_level", C.c_int), ("win", C.c_int), ("lk_max_count", C.c_int),
@@ -544,7 +546,7 @@ class FrontendConfig(C.Structure):
         ("host_threads", C.c_int), ("timing", C.c_int), ("keyframe_rule", C.c_int), ("features_to_track", C.c_int),
         ("P_left", C.c_float * 12), ("P_right", C.c_float * 12), ("y_threshold", C.c_float),
         ("stereo_win", C.c_int), ("stereo_max_level", C.c_int), ("stereo_max_count", C.c_int),
-        ("stereo_epsilon", C.c_double),
+        ("stereo_epsilon", C.c_double), ("use_orb", C.c_int), ("orb", OrbParams),
     ]
 
     def __init__(self, width, height, K, n_seq=1, n_frames=2, n_features=2000, P_left=None, P_right=None, **kw):
@@ -557,11 +559,13 @@ class FrontendConfig(C.Structure):
                  bucket_size=0, per_bucket=0, pnp_iterations=100, pnp_reproj=8.0, pnp_confidence=0.999,
                  host_threads=0, timing=0, keyframe_rule=KF_EVERY, features_to_track=70, y_threshold=40.0,
                  stereo_win=11, stereo_max_level=3,
-                 stereo_max_count=30, stereo_epsilon=1e-3)
+                 stereo_max_count=30, stereo_epsilon=1e-3, use_orb=0)
+        orb = kw.pop("orb", None)
         d.update(kw)
         self.width, self.height, self.n_seq, self.n_frames, self.n_features = width, height, n_seq, n_frames, n_features
         for k, v in d.items():
             setattr(self, k, v)
+        self.orb = orb if orb is not None else OrbParams()
         self.K[:] = [float(x) for x in np.asarray(K, np.float64).ravel()]
         if P_left is None or P_right is None:
             from .scene import stereo_projections

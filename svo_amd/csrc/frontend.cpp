@@ -49,6 +49,7 @@
 #include <vector>
 
 #include "frontend.hpp"
+#include "orb.hpp"
 #include "linalg.hpp"
 #include "pose.hpp"
 
@@ -337,6 +338,9 @@ struct svo_frontend {
     int spec_early = 1;
     bool trace = false;  // SVO_FE_TRACE=1 at create
     bool device_fits = false;  // SVO_FE_DEVICE_FITS=1 at create (device_fits_env)
+    OrbBatch* orb = nullptr;   // cfg.use_orb: the keyframe detector (orb_batch_detect)
+    std::vector<ImgLevel> orb_lv0;
+    std::vector<int> orb_over;
     int spec_t = -1;       // step whose speculation went out early
     int spec_m = 0;        // its margin (features lost to LK + RANSAC it covers)
     bool spec_was_early = false;
@@ -501,6 +505,21 @@ int fe_fast_and_bucket(svo_frontend* fe, const PyrDesc* descs_cur, bool use_mask
         SVO_HIP(ctx, launch_bucket(bb, fe->S, fe->W, fe->H, fe->cfg.bucket_size, fe->cfg.per_bucket, st));
         ph_end(fe, st, slot);
     }
+    return SVO_OK;
+}
+
+// ORB keyframe detection of frame t of every sequence (cfg.use_orb): its keypoints
+// into kps / kn where FAST's would go, with the box mask around xyA / nA (the
+// previous frame's features, R:src/tracking.cpp:76-79) unless use_mask is false.
+// Synchronous (orb_batch_detect: device stages, then the host's retainBest).
+int fe_orb_detect(svo_frontend* fe, int t, bool use_mask, hipStream_t st) {
+    svo_ctx* ctx = fe->ctx;
+    const int S = fe->S;
+    for (int s = 0; s < S; s++) fe->orb_lv0[s] = fe->desc_host[(size_t)(t % fe->T) * S + s].lv[0];
+    auto par = [fe](int n, const std::function<void(int)>& fn) { fe->pool->run(n, fn); };
+    SVO_HIP(ctx, orb_batch_detect(fe->orb, fe->orb_lv0.data(), use_mask ? fe->xyA : nullptr, fe->nA, fe->CAP, fe->CAP,
+                                  fe->cfg.mask_half, (svo_keypoint*)fe->kps, fe->kn, fe->KCAP, st, par,
+                                  fe->orb_over.data()));
     return SVO_OK;
 }
 
@@ -797,7 +816,8 @@ int svo_frontend_create(svo_ctx* ctx, const svo_frontend_config* cfg, svo_fronte
         !lk_supported(c.stereo_win, c.stereo_win) || c.pnp_iterations <= 0 ||
         !(c.pnp_confidence > 0 && c.pnp_confidence < 1) ||
         (c.keyframe_rule != SVO_KF_EVERY && c.keyframe_rule != SVO_KF_REFERENCE) ||
-        (c.bucket_size > 0 && (c.per_bucket <= 0 || c.width / c.bucket_size <= 0)))
+        (c.bucket_size > 0 && (c.per_bucket <= 0 || c.width / c.bucket_size <= 0)) ||
+        (c.use_orb != 0 && c.use_orb != 1) || (c.use_orb && c.bucket_size > 0))
         return set_error(ctx, SVO_ERR_ARG, "svo_frontend_create: bad config");
     svo_frontend* fe = new svo_frontend();
     fe->ctx = ctx;
@@ -996,6 +1016,20 @@ int svo_frontend_create(svo_ctx* ctx, const svo_frontend_config* cfg, svo_fronte
         fe->spec_early = se && se[0] == '0' ? 0 : 1;
         fe->trace = trace_env();
         fe->device_fits = device_fits_env();
+        if (c.use_orb) {  // ORB: detection at the keyframe, the serial keyframe path
+            fe->fast_pre = 0;
+            fe->spec_margin = -1;
+            fe->spec_early = 0;
+        }
+    }
+    if (c.use_orb) {
+        fe->orb = orb_batch_create(S, c.width, c.height, c.orb);
+        if (!fe->orb) {
+            svo_frontend_destroy(fe);
+            return set_error(ctx, SVO_ERR_ARG, "svo_frontend_create: ORB parameters or workspace");
+        }
+        fe->orb_lv0.resize(S);
+        fe->orb_over.assign(S, 0);
     }
     // (on the context stream: a first use of the null stream would take a fifth
     // hardware queue and serialise the step's streams)
@@ -1076,6 +1110,7 @@ void svo_frontend_destroy(svo_frontend* fe) {
                          fe->ev_pyr_r_b[1], fe->ev_pre, fe->ev_fdone, fe->ev_full_b[0], fe->ev_full_b[1]})
         if (e) (void)hipEventDestroy(e);
     if (fe->score_map) (void)hipFree(fe->score_map);
+    orb_batch_destroy(fe->orb);
     delete fe;
 }
 
@@ -1164,7 +1199,7 @@ int svo_frontend_init(svo_frontend* fe, int t0) {
     SVO_HIP(ctx, hipMemsetAsync(fe->nA, 0, sizeof(int) * S, ctx->stream));
     SVO_HIP(ctx, hipMemsetAsync(fe->map_n, 0, sizeof(int) * S, ctx->stream));
     SVO_HIP(ctx, hipMemsetAsync(fe->pend_n, 0, sizeof(int) * S, ctx->stream));
-    int rc = fe_fast_and_bucket(fe, dcur, false, ctx->stream);
+    int rc = fe->orb ? fe_orb_detect(fe, t0, false, ctx->stream) : fe_fast_and_bucket(fe, dcur, false, ctx->stream);
     if (rc) return rc;
     // n_in = nA (zero): nothing to compact, the candidates fill the set
     rc = fe_keyframe(fe, t0, fe->nA, nullptr, fe->xyA, fe->midA, fe->cfg.n_features, ctx->stream);
@@ -1316,8 +1351,10 @@ static int fe_front_rest(svo_frontend* fe, int t) {
             stage = kFastBoxes;
         }
         fe->pre_t = -1;
-        int rc = fe_fast_and_bucket(fe, dcur, true, sf, true, stage);
-        if (rc) return rc;
+        if (!fe->orb) {  // (ORB detects at the keyframe, fe_orb_detect)
+            int rc = fe_fast_and_bucket(fe, dcur, true, sf, true, stage);
+            if (rc) return rc;
+        }
         SVO_HIP(ctx, hipEventRecord(fe->ev_fast, sf));
         SVO_HIP(ctx, hipEventRecord(fe->ev_fdone, sf));
     }
@@ -1666,6 +1703,18 @@ int svo_frontend_step(svo_frontend* fe, int t, svo_frontend_stats* stats) {
     // step's LK: they are queued then (fe_queue_stats), off the critical path
     fe->stats_pending = true;
     fe->stats_parity = t & 1;
+    // ORB: the keyframe's detection, on the steps that take a keyframe
+    if (fe->orb) {
+        bool any = false;
+        for (int s = 0; s < S; s++) any |= fe->h_target[s] > 0;
+        if (any) {
+            rc = fe_orb_detect(fe, t, true, sf);
+            if (rc) return rc;
+        } else {
+            SVO_HIP(ctx, hipMemsetAsync(fe->kn, 0, sizeof(int) * S, sf));
+        }
+        SVO_HIP(ctx, hipEventRecord(fe->ev_fast, sf));
+    }
     // the mask (reads xyA) and FAST (writes kps) must be done before xyA is
     // rewritten / kps read
     SVO_HIP(ctx, hipStreamWaitEvent(sl, fe->ev_fast, 0));

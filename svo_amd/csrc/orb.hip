@@ -20,21 +20,16 @@
 //
 // Both are small byte-gather kernels; the level images are L2-resident.
 #include "common.hpp"
+#include "orb.hpp"
 
 namespace svo {
 
 // Packed coefficient pair: c0 | c1 << 16 (each in 0..256).
-__global__ void __launch_bounds__(256) orb_resize_kernel(const uint8_t* __restrict__ src, int spitch,
-                                                         const uint8_t* __restrict__ smask, int sw,
-                                                         uint8_t* __restrict__ dst, int dpitch,
-                                                         uint8_t* __restrict__ dmask, int dw, int dh,
-                                                         const int* __restrict__ xofs,
-                                                         const uint32_t* __restrict__ xc,
-                                                         const int* __restrict__ yofs,
-                                                         const uint32_t* __restrict__ yc) {
-    const int x = blockIdx.x * 64 + threadIdx.x;
-    const int y = blockIdx.y * 4 + threadIdx.y;
-    if (x >= dw || y >= dh) return;
+__device__ __forceinline__ void orb_resize_px(const uint8_t* __restrict__ src, int spitch,
+                                              const uint8_t* __restrict__ smask, int sw, uint8_t* __restrict__ dst,
+                                              int dpitch, uint8_t* __restrict__ dmask, int dw, int x, int y,
+                                              const int* __restrict__ xofs, const uint32_t* __restrict__ xc,
+                                              const int* __restrict__ yofs, const uint32_t* __restrict__ yc) {
     const int x0 = xofs[x], y0 = yofs[y];
     const uint32_t cx = xc[x], cy = yc[y];
     const uint32_t cx0 = cx & 0xFFFF, cx1 = cx >> 16, cy0 = cy & 0xFFFF, cy1 = cy >> 16;
@@ -55,6 +50,39 @@ __global__ void __launch_bounds__(256) orb_resize_kernel(const uint8_t* __restri
     }
 }
 
+__global__ void __launch_bounds__(256) orb_resize_kernel(const uint8_t* __restrict__ src, int spitch,
+                                                         const uint8_t* __restrict__ smask, int sw,
+                                                         uint8_t* __restrict__ dst, int dpitch,
+                                                         uint8_t* __restrict__ dmask, int dw, int dh,
+                                                         const int* __restrict__ xofs,
+                                                         const uint32_t* __restrict__ xc,
+                                                         const int* __restrict__ yofs,
+                                                         const uint32_t* __restrict__ yc) {
+    const int x = blockIdx.x * 64 + threadIdx.x;
+    const int y = blockIdx.y * 4 + threadIdx.y;
+    if (x >= dw || y >= dh) return;
+    orb_resize_px(src, spitch, smask, sw, dst, dpitch, dmask, dw, x, y, xofs, xc, yofs, yc);
+}
+
+// the same for one level of every sequence (blockIdx.z)
+__global__ void __launch_bounds__(256) orb_resize_batched_kernel(const PyrDesc* __restrict__ src,
+                                                                 const PyrDesc* __restrict__ dst,
+                                                                 const uint8_t* __restrict__ smask,
+                                                                 size_t smask_stride, int sw,
+                                                                 uint8_t* __restrict__ dmask, size_t dmask_stride,
+                                                                 int dw, int dh, const int* __restrict__ xofs,
+                                                                 const uint32_t* __restrict__ xc,
+                                                                 const int* __restrict__ yofs,
+                                                                 const uint32_t* __restrict__ yc) {
+    const int x = blockIdx.x * 64 + threadIdx.x;
+    const int y = blockIdx.y * 4 + threadIdx.y;
+    if (x >= dw || y >= dh) return;
+    const size_t s = blockIdx.z;
+    const ImgLevel S = src[s].lv[0], D = dst[s].lv[0];
+    orb_resize_px(S.data, S.pitch, dmask ? smask + s * smask_stride : nullptr, sw, const_cast<uint8_t*>(D.data),
+                  D.pitch, dmask ? dmask + s * dmask_stride : nullptr, dw, x, y, xofs, xc, yofs, yc);
+}
+
 hipError_t launch_orb_resize(const uint8_t* src, int spitch, const uint8_t* smask, int sw, uint8_t* dst, int dpitch,
                              uint8_t* dmask, int dw, int dh, const int* xofs, const uint32_t* xc, const int* yofs,
                              const uint32_t* yc, hipStream_t st) {
@@ -65,18 +93,10 @@ hipError_t launch_orb_resize(const uint8_t* src, int spitch, const uint8_t* smas
     return hipGetLastError();
 }
 
-// Per level l: image lv[l] of `levels`, keypoints kps + l*cap (n[l] of them).
-// Points closer than 4 px to the level's edge (never kept by ORB's border
-// filter, which is >= edgeThreshold) get response 0 instead of a read.
-__global__ void __launch_bounds__(256) orb_harris_kernel(PyrDesc levels, const svo_keypoint* __restrict__ kps,
-                                                         const int* __restrict__ n, int cap,
-                                                         float* __restrict__ resp) {
-    const int l = blockIdx.y;
-    const int i = blockIdx.x * 256 + threadIdx.x;
-    const int nl = n[l] < cap ? n[l] : cap;
-    if (i >= nl) return;
-    const ImgLevel L = levels.lv[l];
-    const svo_keypoint k = kps[(size_t)l * cap + i];
+// HarrisResponses (orb.cpp: block 7, k 0.04) at integer point (x0, y0) of level L.
+// Points closer than 4 px to the level's edge (never kept by ORB's border filter,
+// which is >= edgeThreshold) get response 0 instead of a read.
+__device__ float orb_harris_at(const ImgLevel& L, const svo_keypoint& k) {
     // cvRound of integer-valued coordinates
     const int x0 = (int)k.x, y0 = (int)k.y;
     float r = 0.f;
@@ -109,7 +129,30 @@ __global__ void __launch_bounds__(256) orb_harris_kernel(PyrDesc levels, const s
         const float t3 = t2 * sab;
         r = ((t0 - t1) - t3) * scale_sq_sq;
     }
-    resp[(size_t)l * cap + i] = r;
+    return r;
+}
+
+// Per level l: image lv[l] of `levels`, keypoints kps + l*cap (n[l] of them).
+__global__ void __launch_bounds__(256) orb_harris_kernel(PyrDesc levels, const svo_keypoint* __restrict__ kps,
+                                                         const int* __restrict__ n, int cap,
+                                                         float* __restrict__ resp) {
+    const int l = blockIdx.y;
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    const int nl = n[l] < cap ? n[l] : cap;
+    if (i >= nl) return;
+    resp[(size_t)l * cap + i] = orb_harris_at(levels.lv[l], kps[(size_t)l * cap + i]);
+}
+
+// every sequence (blockIdx.z): level l of sequence s is levels[l * nseq + s].lv[0]
+__global__ void __launch_bounds__(256) orb_harris_batched_kernel(const PyrDesc* __restrict__ levels, int nseq,
+                                                                 const svo_keypoint* __restrict__ kps,
+                                                                 const int* __restrict__ n, int cap,
+                                                                 float* __restrict__ resp) {
+    const size_t ls = (size_t)blockIdx.y * nseq + blockIdx.z;
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    const int nl = n[ls] < cap ? n[ls] : cap;
+    if (i >= nl) return;
+    resp[ls * cap + i] = orb_harris_at(levels[ls].lv[0], kps[ls * cap + i]);
 }
 
 hipError_t launch_orb_harris(const PyrDesc& levels, int nlevels, const svo_keypoint* kps, const int* n, int cap,
@@ -117,6 +160,25 @@ hipError_t launch_orb_harris(const PyrDesc& levels, int nlevels, const svo_keypo
     if (max_n <= 0 || nlevels <= 0) return hipSuccess;
     dim3 grid((max_n + 255) / 256, nlevels);
     hipLaunchKernelGGL(orb_harris_kernel, grid, dim3(256), 0, st, levels, kps, n, cap, resp);
+    return hipGetLastError();
+}
+
+hipError_t launch_orb_harris_batched(const PyrDesc* levels, int nlevels, int nseq, const svo_keypoint* kps,
+                                     const int* n, int cap, int max_n, float* resp, hipStream_t st) {
+    if (max_n <= 0 || nlevels <= 0 || nseq <= 0) return hipSuccess;
+    dim3 grid((max_n + 255) / 256, nlevels, nseq);
+    hipLaunchKernelGGL(orb_harris_batched_kernel, grid, dim3(256), 0, st, levels, nseq, kps, n, cap, resp);
+    return hipGetLastError();
+}
+
+hipError_t launch_orb_resize_batched(const PyrDesc* src, const PyrDesc* dst, const uint8_t* smask,
+                                     size_t smask_stride, int sw, uint8_t* dmask, size_t dmask_stride, int dw, int dh,
+                                     int nseq, const int* xofs, const uint32_t* xc, const int* yofs,
+                                     const uint32_t* yc, hipStream_t st) {
+    if (dw <= 0 || dh <= 0 || nseq <= 0) return hipSuccess;
+    dim3 grid((dw + 63) / 64, (dh + 3) / 4, nseq);
+    hipLaunchKernelGGL(orb_resize_batched_kernel, grid, dim3(64, 4), 0, st, src, dst, smask, smask_stride, sw, dmask,
+                       dmask_stride, dw, dh, xofs, xc, yofs, yc);
     return hipGetLastError();
 }
 

@@ -239,6 +239,46 @@ def test_frontend_reference_rule_mixed_batch(spec, monkeypatch):
     assert mixed, "some step should have keyframe and tracking-only sequences together"
 
 
+@pytest.mark.parametrize("rule", ["reference", "every"])
+def test_frontend_orb_matches_oracle_loop(rule):
+    """use_orb = 1, the reference's shipped detector (R:configs/config.yaml:19-27:
+    ORB, 150 features, scale 1.2, 8 levels, patch / edge 31, FAST 20, HARRIS;
+    R:src/tracking.cpp:35-52): the batched front end detects each keyframe with
+    ORB under the box mask (orb_batch_detect: scale + mask pyramids, per-level
+    FAST and Harris for every sequence at once, retainBest on the host) -- every
+    step against the oracle loop with cv::ORB restated (oracle/orb.cpp): counts,
+    bit-identical feature lists (ORB's level-scaled positions), poses. "reference":
+    Tracking::nextFrame's rule with features_to_track 140, so keyframes recur as
+    the forward scene's tracks are lost; "every": every frame tops up to 400."""
+    ctx = S.Context(0)
+    W, H, T = 640, 376, 10
+    seeds = (3, 8)
+    kw = dict(keyframe_rule=S.KF_REFERENCE, features_to_track=140) if rule == "reference" else {}
+    N = 2000 if rule == "reference" else 400
+    fe = make_frontend(ctx, [SceneForward(W, H, seed=sd) for sd in seeds], T, N, use_orb=1, **kw)
+    fe.init(0)
+    refs = [OracleLoop(SceneForward(W, H, seed=sd), N, rule=rule, features_to_track=140, detector="orb").init(0)
+            for sd in seeds]
+    for q, ref in enumerate(refs):
+        assert np.array_equal(fe.features(q), ref.pts), f"seq {q} features at init"
+    kfs = 0
+    for t in range(1, T):
+        st = fe.step(t).as_dict()
+        rss = [r.step(t) for r in refs]
+        for k in ("tracked", "inliers", "added", "features"):
+            assert st[k] == sum(rs[k] for rs in rss), f"{k} at t={t}"
+        if rule == "reference":
+            assert st["keyframes"] == sum(rs["keyframe"] for rs in rss), f"keyframes at t={t}"
+            assert st["kf_overflow"] == 0
+        kfs += st["keyframes"]
+        for q, ref in enumerate(refs):
+            assert np.array_equal(fe.features(q), ref.pts), f"seq {q} features at t={t}"
+            rv, tv = fe.pose(q)
+            np.testing.assert_allclose(rv, ref.pose[0], atol=1e-7)
+            np.testing.assert_allclose(tv, ref.pose[1], atol=1e-6)
+    assert kfs > 0 and st["added"] >= 0
+
+
 def test_frontend_trace_mode_matches_oracle_loop(monkeypatch):
     """SVO_FE_TRACE=1 (per-task pool attribution, host trace printing) leaves the
     results unchanged: the same step-by-step match against the oracle loop."""

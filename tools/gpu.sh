@@ -104,7 +104,7 @@ run_mix() {
     timeout -s KILL 200 rocprofv3 --pmc SQ_ACTIVE_INST_VALU SQ_BUSY_CYCLES SQ_INSTS_BRANCH SQ_WAIT_INST_LDS \
         SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_SCA SQ_INSTS_SMEM -d /tmp/ps2 -o run --output-format csv \
         -- $B >> $O/mix.log 2>&1 || fail mix2 $O/mix.log
-    python - > $O/mix_$tag.txt <<'P'
+    MIX_CMD="$B" MIX_JSON=$O/valu_$tag.json python - > $O/mix_$tag.txt <<'P'
 import csv, glob, collections, re
 agg = collections.defaultdict(lambda: collections.defaultdict(float))
 disp = collections.defaultdict(set)
@@ -115,10 +115,16 @@ for f in glob.glob('/tmp/ps[12]/**/run_counter_collection.csv', recursive=True):
         k = m.group(1)
         agg[k][r['Counter_Name']] += float(r['Counter_Value'])
         disp[k].add((f, r['Dispatch_Id']))
+import json, os
+summ = {}
 for k, d in agg.items():
     n = len(disp[k]) / 2
     w = d.get('SQ_WAVES', 1)
     print(f"{k:28s} disp {n:5.0f} waves/disp {w/n:9.0f} | per wave: " + ' '.join(f"{c.replace('SQ_','')}={v/w:.0f}" for c, v in sorted(d.items()) if c != 'SQ_WAVES'))
+    summ[k] = {"dispatches": n, "waves_per_dispatch": round(w / n, 1),
+               "valu_per_dispatch": round(d.get('SQ_INSTS_VALU', 0) / n), "valu_per_wave": round(d.get('SQ_INSTS_VALU', 0) / w, 1)}
+json.dump({"source": "SQ_INSTS_VALU / SQ_WAVES (rocprofv3 --pmc) of: " + os.environ.get("MIX_CMD", ""), "kernels": summ},
+          open(os.environ["MIX_JSON"], "w"), indent=1)
 P
     cat $O/mix_$tag.txt
     rm -rf /tmp/ps1 /tmp/ps2
