@@ -1040,10 +1040,11 @@ __device__ __forceinline__ void stage_padded(unsigned* dst, unsigned* sink, cons
 }
 
 // ---------------------------------------------------------------------------
-// FPW features per wave (21x21 windows): each group of LPF = 64 / FPW lanes
-// owns one feature; the window's 63 vertical 7-row strips (21 columns x 3 row
-// groups) are dealt to the group's lanes, lane l taking strips l, l + LPF, ...
-// (strip 63, where it exists, carries zero weights). The per-feature work every
+// FPW features per wave (WW x WH windows, WH a multiple of the strip height NR):
+// each group of LPF = 64 / FPW lanes owns one feature; the window's WW x WH / NR
+// vertical NR-row strips (21 x 21: 63 strips of 7 rows, 21 columns x 3 row groups;
+// 11 x 11: 11 strips of 11 rows) are dealt to the group's lanes, lane l taking
+// strips l, l + LPF, ... (slots past the last strip carry zero weights). The per-feature work every
 // lane repeats (bilinear weights, bounds / convergence tests, the 2x2 solve) and
 // the exact group reduction serve FPW features per instruction. Staged next-
 // image regions (margin QJM) for all FPW features share the wave's LDS slice.
@@ -1054,9 +1055,9 @@ __device__ __forceinline__ void stage_padded(unsigned* dst, unsigned* sink, cons
 // of their own regions: at a multiple of 32 dwords apart (JBYTES / 4 = 672 for
 // QJM = 1) every read of the pair collided (2-way: ~1,350 conflict cycles per
 // wave in SQ_LDS_BANK_CONFLICT), 16 banks apart they take disjoint halves.
-template <int QJM>
+template <int QJM, int WW = 21, int WH = 21>
 struct MultiShape {
-    static constexpr int JRW = ru4(21 + 2 * QJM + 3), JRH = 21 + 1 + 2 * QJM;
+    static constexpr int JRW = ru4(WW + 2 * QJM + 3), JRH = WH + 1 + 2 * QJM;
     static constexpr int JBYTES = JRW * JRH * 4;
     static constexpr int JSTRIDE = ((JBYTES / 4 + 16) / 32 * 32 + 16) * 4;
     static_assert(JSTRIDE >= JBYTES && (JSTRIDE / 4) % 32 == 16, "group stride");
@@ -1100,18 +1101,21 @@ __device__ __forceinline__ void group_sum_f(int (&v)[NV], float (&f)[NV]) {
     for (int i = 0; i < NV; i++) f[i] = halves_lane_float(h[i], lo[i]);
 }
 
-template <int FPW, int QJM, int MINW, int KKS = 2>
+template <int FPW, int QJM, int MINW, int KKS = 2, int WW = 21, int WH = 21, int NR = 7>
 __global__ __launch_bounds__(64, MINW) void lk_multi_kernel(LKBatch B, LKDev p) {
-    constexpr int WW = 21, WH = 21;
-    using Q = MultiShape<QJM>;
+    using Q = MultiShape<QJM, WW, WH>;
+    static_assert(WH % NR == 0, "whole strips");
     static_assert(WW + QJM + 3 <= kPyrPad && WW + 1 <= kDerPad, "padding too small for the window");
     constexpr int JRW = Q::JRW, JRH = Q::JRH;
-    constexpr int NR = 7, NP = 4;
+    constexpr int NP = (NR + 1) / 2;              // row pairs per strip (an odd NR closes with a zero row)
+    constexpr int NSTRIP = WW * (WH / NR);
     constexpr int LPF = 64 / FPW;                 // lanes per feature
-    constexpr int K = (63 + LPF - 1) / LPF;       // strips per lane
-    // int32 partial sums: a lane holds <= 7K products |diff * g| <= 8160 * 4080
-    // (A sums: 4080^2); steps while 2^steps * 7K * 8160 * 4080 < 2^31
-    constexpr int STEPS32 = K >= 4 ? 1 : 2;
+    constexpr int K = (NSTRIP + LPF - 1) / LPF;   // strips per lane
+    // int32 partial sums: a lane holds <= NR K products |diff * g| <= 8160 * 4080
+    // (A sums: 4080^2); steps while 2^steps * NR K * 8160 * 4080 < 2^31
+    constexpr long long kProd = (long long)NR * K * 8160 * 4080;
+    constexpr int STEPS32 = 4 * kProd < (1ll << 31) ? 2 : 2 * kProd < (1ll << 31) ? 1 : 0;
+    static_assert(kProd < (1ll << 31), "a lane's partial sums must fit int32");
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     const int lane = threadIdx.x & 63;
     const int g = lane / LPF, l = lane % LPF;
@@ -1132,16 +1136,16 @@ __global__ __launch_bounds__(64, MINW) void lk_multi_kernel(LKBatch B, LKDev p) 
     unsigned* sink = reinterpret_cast<unsigned*>(lds + FPW * Q::JSTRIDE);
     const unsigned* jmine = jregs + g * (Q::JSTRIDE / 4);
 
-    // the lane's strips: column, first row, LDS offset; strip 63 is a dummy
+    // the lane's strips: column, first row, LDS offset; slots past NSTRIP are dummies
     int scol[K], srow[K];
     bool sreal[K];
 #pragma unroll
     for (int k = 0; k < K; k++) {
         const int sidx = l + LPF * k;
-        sreal[k] = sidx < 63;
+        sreal[k] = sidx < NSTRIP;
         const int sc = sreal[k] ? sidx : 0;
-        scol[k] = sc % 21;
-        srow[k] = (sc / 21) * NR;
+        scol[k] = sc % WW;
+        srow[k] = (sc / WW) * NR;
     }
     constexpr float halfWx = (WW - 1) * 0.5f, halfWy = (WH - 1) * 0.5f;
     const int rnd_j = 1 << (W_BITS - 6 + kJShift);
@@ -1375,11 +1379,13 @@ __global__ __launch_bounds__(64, MINW) void lk_multi_kernel(LKBatch B, LKDev p) 
     }
 }
 
-template <int FPW, int QJM, int MINW = 4, int KKS = 2>
+template <int FPW, int QJM, int MINW = 4, int KKS = 2, int WW = 21, int WH = 21, int NR = 7>
 hipError_t launch_multi(const LKBatch& b, int nseq, int max_n, const LKDev& d, hipStream_t st) {
+    // (no grid_hint: a block owns FPW features and does not loop; blocks past a
+    // sequence's count return at once)
     dim3 grid((max_n + FPW - 1) / FPW, nseq);
-    constexpr int lds_bytes = FPW * MultiShape<QJM>::JSTRIDE + 16;
-    hipLaunchKernelGGL((lk_multi_kernel<FPW, QJM, MINW, KKS>), grid, dim3(64), lds_bytes, st, b, d);
+    constexpr int lds_bytes = FPW * MultiShape<QJM, WW, WH>::JSTRIDE + 16;
+    hipLaunchKernelGGL((lk_multi_kernel<FPW, QJM, MINW, KKS, WW, WH, NR>), grid, dim3(64), lds_bytes, st, b, d);
     return hipGetLastError();
 }
 
@@ -1455,6 +1461,10 @@ hipError_t launch_lk(const LKBatch& b, int nseq, int max_n, const LKParams& lp, 
             // map) measured slower and is gone: DESIGN.md)
             return launch_multi<4, 1, 3>(b, nseq, max_n, d, st);
         }
+        // the stereo call's 11 x 11 (findLeftFeaturesInRight, no err): four
+        // features per wave too, one 11-row strip per lane (11 of 16 lanes)
+        if (lp.win_w == 11 && lp.win_h == 11 && multi_ok && lp.quad)
+            return launch_multi<4, 1, 4, 1, 11, 11, 11>(b, nseq, max_n, d, st);
         if (lp.win_w == 21 && lp.win_h == 21) return launch_fast<21, 21>(b, nseq, max_n, d, st);
         if (lp.win_w == 11 && lp.win_h == 11) return launch_fast<11, 11>(b, nseq, max_n, d, st);
         if (lp.win_w == 15 && lp.win_h == 15) return launch_fast<15, 15>(b, nseq, max_n, d, st);

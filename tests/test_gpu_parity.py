@@ -246,6 +246,28 @@ def test_lk_bit_exact(ctx, cfg, wh, seed, n, lk_kernel):
     assert int((gs != ss).sum()) == 0, f"{int((gs != ss).sum())} status flips vs the SSE order"
 
 
+@pytest.mark.parametrize("wh,seed,n", [((1241, 376), 0, 2000), ((160, 120), 1, 300), ((1920, 1080), 2, 4000)])
+def test_lk_stereo_without_err_bit_exact(ctx, wh, seed, n):
+    """The stereo call as the front end makes it (11 x 11, flags 0, no err output:
+    findLeftFeaturesInRight reads status and points only) runs the four-features-
+    per-wave kernel (lk_multi_kernel<.., 11, 11, 11>, one 11-row strip per lane):
+    points and status bit-identical to the oracle's EXACT accumulation, also for
+    points outside the image."""
+    sc, A, B = frames(*wh, seed=seed)
+    pts = O.fast(A, 20, True)[:n, :2]
+    rng = np.random.default_rng(seed)
+    pts = np.concatenate([pts, rng.uniform(-30, max(wh) + 30, (64, 2))]).astype(np.float32)
+    ga, gb = ctx.image(A, 6), ctx.image(B, 6)
+    c = STEREO
+    gn, gs, ge = ctx.calc_optical_flow_pyr_lk(ga, gb, pts, win_size=c["win"], max_level=c["ml"], criteria=c["crit"],
+                                              flags=c["flags"], want_err=False)
+    assert ge is None
+    rn, rs, _, it = O.lk(A, B, pts, c["win"], c["ml"], c["crit"], c["flags"], acc=O.ACC_EXACT)
+    assert np.array_equal(gs, rs), f"status differs at {np.nonzero(gs != rs)[0][:10]}"
+    assert np.array_equal(gn.view(np.uint32), rn.view(np.uint32))
+    assert ctx.lk_last_iterations() == int(it.sum())
+
+
 # BASELINE.json configs[2] / [3] at full size: 1080p, 8000 features, maxLevel 4 (five
 # levels, not clamped by the window) and 4K, 16000 features, maxLevel 3; the temporal
 # call's window / criteria / flags (R:src/tracking.cpp:160-165)
