@@ -424,6 +424,7 @@ __global__ __launch_bounds__(64) void fast_box_filter_kernel(FastDetBatch B, int
     const int x0 = blockIdx.x * FD_TX, y0 = blockIdx.y * TY;
     const size_t seq = blockIdx.z;
     __shared__ unsigned long long TM[TY];
+    __shared__ int band_lo[64], band_end[64];  // box ranges of the tile's bands, concatenated
     const int lane = threadIdx.x;
     if (lane < TY) TM[lane] = ~0ull;
     __syncthreads();
@@ -441,17 +442,23 @@ __global__ __launch_bounds__(64) void fast_box_filter_kernel(FastDetBatch B, int
             lo = cells[(bb + lane) * ncl + cb0];
             cnt = cells[(bb + lane) * ncl + cb1 + 1] - lo;
         }
-        int total = 0;
-        for (int q = 0; q < nband; q++) total += __shfl(cnt, q);
+        // inclusive prefix of the band counts (every lane converged here), to LDS:
+        // the box loop below is divergent, where a lane must not read another
+        // lane's registers (an inactive source lane reads as 0)
+        int incl = cnt;
+        for (int o = 1; o < 64; o <<= 1) {
+            const int v = __shfl_up(incl, o);
+            if (lane >= o) incl += v;
+        }
+        const int total = __shfl(incl, nband - 1);
+        band_lo[lane] = lo;
+        band_end[lane] = incl;
+        __syncthreads();
         for (int j = lane; j < total; j += 64) {
             // the band holding box j of the concatenated ranges
-            int q = 0, base = 0, c = __shfl(cnt, 0);
-            while (j >= base + c) {
-                base += c;
-                q++;
-                c = __shfl(cnt, q);
-            }
-            const int i = __shfl(lo, q) + (j - base);
+            int q = 0;
+            while (j >= band_end[q]) q++;
+            const int i = band_lo[q] + (j - (q > 0 ? band_end[q - 1] : 0));
             const float2 pt = pts[i];
             const int xa = (int)__builtin_rintf(pt.x - B.box_half), ya = (int)__builtin_rintf(pt.y - B.box_half);
             const int xb = (int)__builtin_rintf(pt.x + B.box_half), yb = (int)__builtin_rintf(pt.y + B.box_half);
@@ -465,6 +472,7 @@ __global__ __launch_bounds__(64) void fast_box_filter_kernel(FastDetBatch B, int
             const unsigned long long span = (c1 - c0 == 63) ? ~0ull : (((1ull << (c1 - c0 + 1)) - 1ull) << c0);
             for (int y = yt; y <= yd; y++) atomicAnd(&TM[y - y0], ~span);
         }
+        __syncthreads();  // (band_lo / band_end are rewritten by a next round of bands)
     }
     __syncthreads();
     if (lane < TY && y0 + lane < h) {

@@ -31,7 +31,7 @@ fail() { echo "FAILED: $1"; [ -n "$2" ] && tail -30 "$2"; exit 1; }
 
 run_tests() {
     local args="${*:-tests}"
-    timeout -k 10 900 python -u -m pytest $args -m gpu -x -v --timeout 300 --timeout-method thread \
+    timeout -k 10 900 python -u -m pytest $args -m gpu -x -v --timeout 150 --timeout-method thread \
         -p no:cacheprovider > $O/gpu_tests.log 2>&1 || fail tests $O/gpu_tests.log
     tail -1 $O/gpu_tests.log
 }
