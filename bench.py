@@ -308,6 +308,43 @@ def forward_workload(S, SceneForward, ctx, W, H, N, ML, Sq, K, Wm, threads):
             "scene": "SceneForward: 0.04 m/frame forward (ping-pong), occluder at 8 m sliding 22 px/frame"}
 
 
+def orb_workload(S, SceneForward, ctx, W, H, ML, Sq, K, Wm, threads):
+    """The reference's shipped configuration (R:configs/config.yaml:15,19-27): ORB
+    keyframe detector (150 features, scale 1.2, 8 levels, HARRIS), Tracking::nextFrame's
+    keyframe rule with features_to_track 70 (R:src/tracking.cpp:68-69), on the forward
+    / occluder scene so that tracks are lost and keyframes recur; timed like the
+    headline (Sq sequences per launch, Wm warm-up + K timed steps)."""
+    n_dist = min(Sq, 16)
+    T = Wm + K + 2
+    scs = [SceneForward(W, H, seed=2000 + i) for i in range(n_dist)]
+    P = min(T, 2 * scs[0].period)
+    pairs = [[(sc.frame(t), sc.right(t)) for t in range(P)] for sc in scs]
+    feo = S.Frontend(ctx, S.FrontendConfig(W, H, scs[0].K, n_seq=Sq, n_frames=T, n_features=2000, max_level=ML,
+                                           host_threads=threads, timing=0, use_orb=1,
+                                           keyframe_rule=S.KF_REFERENCE, features_to_track=70))
+    for s in range(Sq):
+        for t in range(T):
+            feo.set_frame(s, t, *pairs[s % n_dist][t % P])
+    feo.init(0)
+    for t in range(1, Wm + 1):
+        feo.step(t)
+    tot = {"tracked": 0, "inliers": 0, "added": 0, "keyframes": 0}
+    t1 = time.perf_counter()
+    for t in range(Wm + 1, Wm + K + 1):
+        st = feo.step(t).as_dict()
+        for k in tot:
+            tot[k] += st[k]
+    feo.synchronize()
+    dt = time.perf_counter() - t1
+    feo.close()
+    return {"value": round(Sq * K / dt, 2), "unit": "frames/s", "ms_per_step": round(dt / K * 1e3, 4),
+            "steps": K, "warmup": Wm, "distinct_sequences": n_dist,
+            "keyframe_ratio": round(tot["keyframes"] / (Sq * K), 4),
+            "stats_per_step": {k: round(v / K, 2) for k, v in tot.items()},
+            "config": "use_orb 1 (150 features, 1.2, 8 levels, HARRIS), SVO_KF_REFERENCE, features_to_track 70, "
+                      "SceneForward"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -329,6 +366,7 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-single", action="store_true")
+    ap.add_argument("--no-orb", action="store_true", help="skip the shipped-config (ORB, reference keyframe rule) workload")
     ap.add_argument("--no-bucketed", action="store_true",
                     help="skip the second measurement with bucketed selection in the loop")
     ap.add_argument("--scene", default="rot", choices=("rot", "forward"),
@@ -537,6 +575,10 @@ def main():
         if not all_pairs:
             fe.close()
         forward = forward_workload(S, SceneForward, ctx, W, H, N, ML, Sq, K, Wm, args.threads)
+    orb = None
+    if not args.no_orb and args.scene == "rot" and world == 1:
+        fe.close()  # (idempotent)
+        orb = orb_workload(S, SceneForward, ctx, W, H, ML, Sq, K, Wm, args.threads)
     out = {
         "metric": "frames/sec @1241x376, 2000 feats; LK iters/sec; achieved HBM GB/s",
         "value": round(fps, 2),
@@ -558,7 +600,7 @@ def main():
         "achieved_GBps_algorithmic": round(frames * frame_bytes(W, H, N, ML) / dt_max / 1e9, 2),
         "single_stream_fps": round(single, 2) if single else None,
         "bucketed": bucketed,
-        "workloads": {"forward": forward},
+        "workloads": {"forward": forward, "orb_reference": orb},
         "phase_ms_per_step": {k: round(v[0] / K, 4) for k, v in phases.items()},
         "stats_per_step": {k: round(v / K, 3) for k, v in tot.items()},
         "step_ms": {"mean": round(float(np.mean(step_s)) * 1e3, 4),
