@@ -197,7 +197,9 @@ def roofline_valu(lk_name: str, seqs: int, lk_avg_s: float):
     """LK against the bound that binds it, VALU issue (SURVEY.md 8(d) prices it by
     bytes; rocprof shows the kernel issue-bound): the mix pass's VALU
     instructions per launch over this run's live average launch time."""
-    kname = lk_name.split("<")[0]
+    # the mix pass keys kernels with their template arguments (the 21 x 21 and the
+    # stereo 11 x 11 instances of lk_multi_kernel are separate entries)
+    kname = "lk_multi_kernel<4, 1, 3, 2, 21, 21, 7>" if lk_name.startswith("lk_multi") else "lk_fast_kernel<21, 21"
     valu, src = pmc_valu(kname, seqs)
     if valu is None or lk_avg_s <= 0:
         return None

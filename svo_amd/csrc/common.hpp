@@ -276,14 +276,16 @@ struct SqpnpFitIn {
     int mode, pad;
     double R[9], t[3], rv[3];
 };
-// The final SQPnP fits of every sequence, one 64-thread block each (sqpnp.hpp: the
-// cost from the statistics `stats` of suffstats_kernel, Omega's eigenvectors, the
-// SQP runs from its starts in lanes, the solution search replayed in order), then
+// The final SQPnP fits of every sequence (sqpnp.hpp), three launches: the cost
+// from the statistics `stats` of suffstats_kernel and Omega's eigenvectors (one
+// wave per sequence), the SQP runs from the 18 starts (a wave per eigenvector and
+// sequence, the KKT rows over lanes), the solution search replayed in order; then
 // Frame::pose() of the result: pose6[s] = (rvec, tvec), pose12[s] = camera -> world
 // (R^T, -R^T t) for PendingMap. obj / counts / bits: the fitted points (the
-// cheirality majority test).
+// cheirality majority test). work: sqpnp_fit_work_bytes(nseq) of device memory.
+size_t sqpnp_fit_work_bytes(int nseq);
 hipError_t launch_sqpnp_fit(const double* stats, const SqpnpFitIn* in, const float* obj, const int* counts, int cap,
-                            const uint32_t* bits, int words_cap, int nseq, double* pose6, double* pose12,
+                            const uint32_t* bits, int words_cap, int nseq, double* pose6, double* pose12, void* work,
                             hipStream_t st);
 size_t bucket_scratch_ints(int img_w, int img_h, int bucket, int per_bucket, int n);
 hipError_t launch_bucket(const BucketBatch& b, int nseq, int img_w, int img_h, int bucket, int per_bucket,

@@ -270,11 +270,10 @@ bool trace_env() {
 }
 
 // final SQPnP fits on the device (SVO_FE_DEVICE_FITS=1, read at create) instead of
-// the host pool: sqpnp_fit_kernel runs one sequence per wave with the 9 x 9
-// eigen-decomposition and the solution search serial in one lane, which measured
-// 4.3 ms per 128-sequence launch on MI355X against the pool's 0.17 ms, and the
-// host fits hide behind the wait for the post-LK results -- so the host is the
-// default and the kernel a cross-check of the shared sqpnp.hpp code
+// the host pool (launch_sqpnp_fit: the eigen-decomposition, the SQP runs over
+// waves, the search). The host's fits take ~0.17 ms per step and hide behind the
+// wait for the post-LK results, while the device's run beside LK and take its
+// CUs (DESIGN.md §6 has the measurements), so the host is the default
 bool device_fits_env() {
     const char* e = std::getenv("SVO_FE_DEVICE_FITS");
     return e && e[0] == '1';
@@ -338,6 +337,7 @@ struct svo_frontend {
     int spec_early = 1;
     bool trace = false;  // SVO_FE_TRACE=1 at create
     bool device_fits = false;  // SVO_FE_DEVICE_FITS=1 at create (device_fits_env)
+    void* fit_work = nullptr;  // device_fits: sqpnp_fit_work_bytes(S)
     OrbBatch* orb = nullptr;   // cfg.use_orb: the keyframe detector (orb_batch_detect)
     std::vector<ImgLevel> orb_lv0;
     std::vector<int> orb_over;
@@ -368,7 +368,7 @@ struct svo_frontend {
     long long* h_itsum;
     float* h_samp;
     double *h_stats, *h_pose;   // h_pose: [s][12] camera -> world of the last fitted frame
-    double* h_pose6;            // [s][6] rvec, tvec of the last fitted frame (sqpnp_fit_kernel)
+    double* h_pose6;            // [s][6] rvec, tvec of the last fitted frame (launch_sqpnp_fit)
     SqpnpFitIn* h_fitin;        // [s] the host RANSAC's outcome the device fit starts from
     uint32_t* h_best;           // this step's parity of h_best_b
     uint32_t* h_best_b[2];
@@ -764,7 +764,7 @@ int fe_queue_stats(svo_frontend* fe) {
     // waits for ev_stats
     if (fe->device_fits)
         SVO_HIP(ctx, launch_sqpnp_fit(fe->h_stats, fe->h_fitin, fe->obj_b[p], fe->nB_b[p], fe->CAP, fe->h_best_b[p],
-                                      fe->WORDS, fe->S, fe->h_pose6, fe->h_pose, fe->st_copy));
+                                      fe->WORDS, fe->S, fe->h_pose6, fe->h_pose, fe->fit_work, fe->st_copy));
     SVO_HIP(ctx, hipEventRecord(fe->ev_stats, fe->st_copy));
     fe->stats_pending = false;
     return SVO_OK;
@@ -1022,6 +1022,10 @@ int svo_frontend_create(svo_ctx* ctx, const svo_frontend_config* cfg, svo_fronte
             fe->spec_early = 0;
         }
     }
+    if (fe->device_fits && hipMalloc(&fe->fit_work, sqpnp_fit_work_bytes(S)) != hipSuccess) {
+        svo_frontend_destroy(fe);
+        return set_error(ctx, SVO_ERR_HIP, "svo_frontend_create: fit workspace");
+    }
     if (c.use_orb) {
         fe->orb = orb_batch_create(S, c.width, c.height, c.orb);
         if (!fe->orb) {
@@ -1111,6 +1115,7 @@ void svo_frontend_destroy(svo_frontend* fe) {
         if (e) (void)hipEventDestroy(e);
     if (fe->score_map) (void)hipFree(fe->score_map);
     orb_batch_destroy(fe->orb);
+    if (fe->fit_work) (void)hipFree(fe->fit_work);
     delete fe;
 }
 
@@ -1243,7 +1248,7 @@ static int fe_post(svo_frontend* fe, int t) {
     const int CAP = fe->CAP;
     hipStream_t sl = fe->st_lk;
     int slot;
-    // the previous step's final fits (sqpnp_fit_kernel) set the poses the post-LK
+    // the previous step's final fits (launch_sqpnp_fit) set the poses the post-LK
     // moves the previous keyframe's new map points with
     if (fe->device_fits) SVO_HIP(ctx, hipStreamWaitEvent(sl, fe->ev_stats, 0));
     PostLkBatch pb{fe->nA, fe->status, fe->next_xy, fe->midA, fe->iters, fe->xyB, fe->midB, fe->nB, fe_pending(fe),

@@ -81,7 +81,7 @@ SVO_HD void sym_eig(double* A, int n, double* w, double* V) {
 // n <= 12, row-major) is read only; eigenvalues descending in w; eigenvector
 // i in row i of Vt.
 // V (n * n), d, e (n each): workspace the caller provides -- the device fit keeps it
-// in LDS (sqpnp_fit_kernel), the host on the stack (sym_eig_ql_n)
+// in LDS (launch_sqpnp_fit), the host on the stack (sym_eig_ql_n)
 SVO_HD void sym_eig_ql_ws(const double* A, int n, double* w, double* Vt, double* V, double* d, double* e) {
     for (int i = 0; i < n * n; i++) V[i] = A[i];
     // tred2: V <- orthogonal Q, d/e <- diagonal / off-diagonal of Q^T A Q

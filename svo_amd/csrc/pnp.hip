@@ -204,7 +204,7 @@ __device__ __forceinline__ double bcast(double v, int src) {
 // the diagonal, found by the serial scan), the same eliminations and the same
 // back-substitution order as the scalar routine, so delta is bit-identical.
 // Every lane returns delta. Jw: this wave's LDS rows of J (6 x 9).
-__device__ __noinline__ void sqp_step_wave(const double* Om, const double* r, double* delta, double* Jw) {
+__device__ void sqp_step_wave(const double* Om, const double* r, double* delta, double* Jw) {
     constexpr int N = 15;
     const int lane = threadIdx.x & 63;
     const double* r1 = r;
@@ -320,53 +320,93 @@ __device__ void sq_start_wave(const sq::SqpnpCost& c, const double* evec, int j,
         for (int k = 0; k < 9; k++) rhat[k] = r[k];
 }
 
-constexpr int kFitWaves = 9;  // one wave per eigenvector: its two starts, +e and -e
+// the device fit's per-sequence state between its three kernels
+struct SqFitWork {
+    sq::SqpnpCost c;
+    double ev[9], evec[81], rs[18][9];
+    int nn, pad;
+};
 
 }  // namespace
 
-// solvePnP(SQPNP) on a sequence's RANSAC inliers (SqpnpFitIn mode 1) and the
-// Frame::pose() of every outcome (R:src/tracking.cpp:191-214), one block of 9
-// waves per sequence. Lane 0 assembles the cost and Omega's eigen-decomposition
-// (sym_eig_ql with its workspace in LDS); wave w then runs the SQP from the starts
-// 2w and 2w + 1 (+- sqrt(3) times eigenvector w) with its 15 x 16 KKT systems one
-// row per lane (sqp_step_wave) -- every start a search could ask for, each
-// independent of the others; wave 0 replays the search (sq_select) with those
-// results, which takes the same steps as the host's on-demand runs, its
-// positive-depth counts spread over the lanes. Bit-identical to the host fit
-// (RansacSeq::fit) on the same statistics.
-__global__ __launch_bounds__(64 * kFitWaves) void sqpnp_fit_kernel(const double* __restrict__ stats,
-                                                                   const SqpnpFitIn* __restrict__ in,
-                                                                   const float* __restrict__ obj,
-                                                                   const int* __restrict__ counts, int cap,
-                                                                   const uint32_t* __restrict__ bits, int words_cap,
-                                                                   double* __restrict__ pose6,
-                                                                   double* __restrict__ pose12) {
-    const int s = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+size_t sqpnp_fit_work_bytes(int nseq) { return sizeof(SqFitWork) * (size_t)nseq; }
+
+namespace {
+
+// 1. the cost from the statistics and Omega's eigen-decomposition (lane 0; the
+//    tred2 / tql2 workspace in LDS), one wave per sequence
+__global__ __launch_bounds__(64) void sqpnp_eig_kernel(const double* __restrict__ stats,
+                                                       const SqpnpFitIn* __restrict__ in, SqFitWork* __restrict__ work) {
+    const int s = blockIdx.x;
+    __shared__ double ws[81 + 9 + 9];
     __shared__ sq::SqpnpCost c;
-    __shared__ double ev[9], evec[81], rs[18][9], ws[81 + 9 + 9], Jw[kFitWaves][54];
-    __shared__ int nn_s;
-    const SqpnpFitIn fin = in[s];
-    if (fin.mode == 1) {
-        if (tid == 0) {
-            sq::sqpnp_assemble(stats + 40 * (size_t)s, c);
-            int nn = -1;
-            if (c.ok) {
-                la::sym_eig_ql_ws(c.Om, 9, ev, evec, ws, ws + 81, ws + 90);
-                nn = sq::sq_null_count(ev);
-            }
-            nn_s = nn;
-        }
-        __syncthreads();
-        if (nn_s >= 0)
-            for (int j = 2 * wave; j < 2 * wave + 2; j++) {
-                double r[9];
-                sq_start_wave(c, evec, j, r, Jw[wave]);
-                if (lane == 0)
-                    for (int k = 0; k < 9; k++) rs[j][k] = r[k];
-            }
-        __syncthreads();
+    __shared__ double ev[9], evec[81];
+    if (threadIdx.x != 0 || in[s].mode != 1) return;
+    SqFitWork& w = work[s];
+    sq::sqpnp_assemble(stats + 40 * (size_t)s, c);
+    int nn = -1;
+    if (c.ok) {
+        la::sym_eig_ql_ws(c.Om, 9, ev, evec, ws, ws + 81, ws + 90);
+        nn = sq::sq_null_count(ev);
     }
-    if (wave != 0) return;
+    w.c = c;
+    for (int k = 0; k < 9; k++) w.ev[k] = ev[k];
+    for (int k = 0; k < 81; k++) w.evec[k] = evec[k];
+    w.nn = nn;
+}
+
+// 2. the SQP runs from starts 2w and 2w + 1 (+- sqrt(3) times eigenvector w), one
+//    wave per (eigenvector, sequence) -- every start a search could ask for, each
+//    independent of the others; the 15 x 16 KKT systems one row per lane
+__global__ __launch_bounds__(64) void sqpnp_sqp_kernel(const SqpnpFitIn* __restrict__ in,
+                                                       SqFitWork* __restrict__ work) {
+    const int w = blockIdx.x, s = blockIdx.y, lane = threadIdx.x;
+    if (in[s].mode != 1) return;
+    SqFitWork& wk = work[s];
+    if (wk.nn < 0) return;
+    __shared__ sq::SqpnpCost c;
+    __shared__ double evec[81], Jw[54];
+    for (int k = lane; k < 81; k += 64) {
+        c.Om[k] = wk.c.Om[k];
+        evec[k] = wk.evec[k];
+    }
+    __syncthreads();
+    for (int j = 2 * w; j < 2 * w + 2; j++) {
+        double r[9];
+        sq_start_wave(c, evec, j, r, Jw);
+        if (lane == 0)
+            for (int k = 0; k < 9; k++) wk.rs[j][k] = r[k];
+    }
+}
+
+// 3. the solution search (sq_select, replayed with the runs above: the same steps
+//    as the host's on-demand runs; every lane runs it, the positive-depth counts
+//    spread over the lanes) and Frame::pose() of every outcome
+__global__ __launch_bounds__(64) void sqpnp_select_kernel(const SqpnpFitIn* __restrict__ in,
+                                                          const SqFitWork* __restrict__ work,
+                                                          const float* __restrict__ obj,
+                                                          const int* __restrict__ counts, int cap,
+                                                          const uint32_t* __restrict__ bits, int words_cap,
+                                                          double* __restrict__ pose6, double* __restrict__ pose12) {
+    const int s = blockIdx.x, lane = threadIdx.x;
+    __shared__ sq::SqpnpCost c;
+    __shared__ double ev[9], evec[81], rs[18][9];
+    const SqpnpFitIn fin = in[s];
+    const SqFitWork& wk = work[s];
+    int nn = -1;
+    if (fin.mode == 1) {
+        nn = wk.nn;
+        for (int k = lane; k < 81; k += 64) {
+            c.Om[k] = wk.c.Om[k];
+            evec[k] = wk.evec[k];
+        }
+        for (int k = lane; k < 27; k += 64) c.P[k] = wk.c.P[k];
+        for (int k = lane; k < 3; k += 64) c.mean[k] = wk.c.mean[k];
+        for (int k = lane; k < 9; k += 64) ev[k] = wk.ev[k];
+        for (int k = lane; k < 18 * 9; k += 64) rs[k / 9][k % 9] = wk.rs[k / 9][k % 9];
+        if (lane == 0) c.ok = wk.c.ok;
+    }
+    __syncthreads();
     double rvec[3] = {0, 0, 0}, tvec[3] = {0, 0, 0};
     if (fin.mode == 2) {
         for (int k = 0; k < 3; k++) {
@@ -376,7 +416,7 @@ __global__ __launch_bounds__(64 * kFitWaves) void sqpnp_fit_kernel(const double*
     } else if (fin.mode == 1) {
         bool found = false;
         double R[9], t[3];
-        if (nn_s >= 0) {
+        if (nn >= 0) {
             const int n = counts[s];
             const float* o = obj + 3 * (size_t)s * cap;
             const uint32_t* b = bits + (size_t)s * words_cap;
@@ -384,9 +424,8 @@ __global__ __launch_bounds__(64 * kFitWaves) void sqpnp_fit_kernel(const double*
             for (int w = lane; w < (n + 31) / 32; w += 64)
                 n_in += __popc(b[w] & (w == n / 32 ? (1u << (n & 31)) - 1u : ~0u));
             for (int off = 32; off > 0; off >>= 1) n_in += __shfl_xor(n_in, off);
-            // every lane runs the search (uniform: the same values everywhere)
             sq::sq_select(
-                c, ev, evec, nn_s, n_in,
+                c, ev, evec, nn, n_in,
                 [&](int j, double* r) {
                     for (int k = 0; k < 9; k++) r[k] = rs[j][k];
                 },
@@ -425,12 +464,17 @@ __global__ __launch_bounds__(64 * kFitWaves) void sqpnp_fit_kernel(const double*
     for (int i = 0; i < 3; i++) T[9 + i] = -(T[3 * i] * tvec[0] + T[3 * i + 1] * tvec[1] + T[3 * i + 2] * tvec[2]);
 }
 
+}  // namespace
+
 hipError_t launch_sqpnp_fit(const double* stats, const SqpnpFitIn* in, const float* obj, const int* counts, int cap,
-                            const uint32_t* bits, int words_cap, int nseq, double* pose6, double* pose12,
+                            const uint32_t* bits, int words_cap, int nseq, double* pose6, double* pose12, void* work,
                             hipStream_t st) {
     if (nseq <= 0) return hipSuccess;
-    hipLaunchKernelGGL(sqpnp_fit_kernel, dim3(nseq), dim3(64 * kFitWaves), 0, st, stats, in, obj, counts, cap, bits,
-                       words_cap, pose6, pose12);
+    SqFitWork* wk = (SqFitWork*)work;
+    hipLaunchKernelGGL(sqpnp_eig_kernel, dim3(nseq), dim3(64), 0, st, stats, in, wk);
+    hipLaunchKernelGGL(sqpnp_sqp_kernel, dim3(9, nseq), dim3(64), 0, st, in, wk);
+    hipLaunchKernelGGL(sqpnp_select_kernel, dim3(nseq), dim3(64), 0, st, in, wk, obj, counts, cap, bits, words_cap,
+                       pose6, pose12);
     return hipGetLastError();
 }
 

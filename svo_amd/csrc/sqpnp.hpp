@@ -3,7 +3,7 @@
 // statistics of the inlier set (pose.hpp kSqpnpStats): __host__ __device__, fixed
 // sizes, no allocation. The host runs it for svo_solve_pnp_sqpnp / svo_solve_pnp_ransac
 // (pose.cpp); the batched front end runs it on the device, one wave per sequence
-// (sqpnp_fit_kernel, pnp.hip), its solution-search starts spread over lanes.
+// (launch_sqpnp_fit, pnp.hip): the SQP starts over waves, the KKT rows over lanes.
 #pragma once
 
 #include "epnp.hpp"

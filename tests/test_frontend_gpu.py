@@ -298,7 +298,7 @@ def test_frontend_trace_mode_matches_oracle_loop(monkeypatch):
 
 
 def test_frontend_device_fits_match_host_fits(monkeypatch):
-    """SVO_FE_DEVICE_FITS=1: the final SQPnP fits run in sqpnp_fit_kernel (the
+    """SVO_FE_DEVICE_FITS=1: the final SQPnP fits run on the device (launch_sqpnp_fit: the
     shared sqpnp.hpp code on the device) instead of the host pool -- the same
     poses bit for bit, hence the same map points and features, and the oracle's
     poses step by step."""

@@ -110,7 +110,7 @@ agg = collections.defaultdict(lambda: collections.defaultdict(float))
 disp = collections.defaultdict(set)
 for f in glob.glob('/tmp/ps[12]/**/run_counter_collection.csv', recursive=True):
     for r in csv.DictReader(open(f)):
-        m = re.search(r'([a-z_0-9]+_kernel)', r['Kernel_Name'])
+        m = re.search(r'([a-z_0-9]+_kernel(<[^(]*>)?)', r['Kernel_Name'])
         if not m: continue
         k = m.group(1)
         agg[k][r['Counter_Name']] += float(r['Counter_Value'])
@@ -120,7 +120,7 @@ summ = {}
 for k, d in agg.items():
     n = len(disp[k]) / 2
     w = d.get('SQ_WAVES', 1)
-    print(f"{k:28s} disp {n:5.0f} waves/disp {w/n:9.0f} | per wave: " + ' '.join(f"{c.replace('SQ_','')}={v/w:.0f}" for c, v in sorted(d.items()) if c != 'SQ_WAVES'))
+    print(f"{k:40s} disp {n:5.0f} waves/disp {w/n:9.0f} | per wave: " + ' '.join(f"{c.replace('SQ_','')}={v/w:.0f}" for c, v in sorted(d.items()) if c != 'SQ_WAVES'))
     summ[k] = {"dispatches": n, "waves_per_dispatch": round(w / n, 1),
                "valu_per_dispatch": round(d.get('SQ_INSTS_VALU', 0) / n), "valu_per_wave": round(d.get('SQ_INSTS_VALU', 0) / w, 1)}
 json.dump({"source": "SQ_INSTS_VALU / SQ_WAVES (rocprofv3 --pmc) of: " + os.environ.get("MIX_CMD", ""), "kernels": summ},
@@ -231,6 +231,7 @@ run_round() {
         if [ $c = kitti ]; then run_pmc "$tag" $c 128; else run_pmc "$tag" $c 16; fi
     done
     run_mix "$tag"
+    run_bench "${tag}_driver" --gpus 1 --steps 20 --warmup 5
     run_bench "$tag" --steps 50 --warmup 10
     for c in 1080p 4k; do run_bench "${tag}_$c" --config $c --seq 16 --steps 20 --warmup 5 --no-cpu-baseline; done
 }
