@@ -148,17 +148,22 @@ def allreduce_sum(dist, v: float) -> float:
     return float(t.item())
 
 
-def pmc_traffic(cfg_name: str, kernel_prefix: str):  # substring of the demangled kernel name
+def pmc_traffic(cfg_name: str, kernel_prefix: str, seqs: int = 0):  # substring of the demangled kernel name
     """Per-launch HBM bytes of a kernel from the rocprofv3 PMC summary measured on
     THIS config's workload (profiles/pmc_summary.json configs[cfg_name], written by
-    tools/pmc_summary.py --config), or None when that config was not measured."""
+    tools/pmc_summary.py --config), scaled from the sequences per launch it was
+    measured at (the source's --seq) to `seqs`; None when that config was not
+    measured."""
     path = os.path.join(ROOT, "profiles", "pmc_summary.json")
     try:
         with open(path) as f:
             d = json.load(f)
     except (OSError, ValueError):
         return None
-    for k, v in d.get("configs", {}).get(cfg_name, {}).get("kernels", {}).items():
+    c = d.get("configs", {}).get(cfg_name, {})
+    m = re.search(r"--seq (\d+)", c.get("source", ""))
+    scale = seqs / int(m.group(1)) if (m and seqs) else 1.0
+    for k, v in c.get("kernels", {}).items():
         if kernel_prefix not in k or (kernel_prefix == "scharr_kernel" and "pyr_scharr" in k):
             continue
         # the left chain's kernels, not the right pyramid's instances of the same
@@ -167,7 +172,8 @@ def pmc_traffic(cfg_name: str, kernel_prefix: str):  # substring of the demangle
             continue
         if kernel_prefix == "pyr_chain_kernel" and ", false," in k:
             continue
-        return v.get("hbm_bytes_per_launch")
+        b = v.get("hbm_bytes_per_launch")
+        return None if b is None else int(b * scale)
     return None
 
 
@@ -354,12 +360,12 @@ def main():
     # RANSAC chunk predictions settle); every sequence frame is resident in HBM
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
-    # 128 independent sequences per GPU: the post-LK window (post-LK kernel, host
-    # EPnP, scoring, keyframe: ~0.23 ms, mostly latency) is paid once per step for the
-    # whole batch, so frames/s rises with the batch -- 64: 82.3k, 128: 92.3k, 192:
-    # 94.5k, 256: 95.6k on one box (profiles/r03_batch_curve.txt); 128 keeps a step at
-    # ~1.4 ms (each sequence still advances ~720 frames/s)
-    ap.add_argument("--seq", type=int, default=128, help="independent sequences per GPU (batched launches)")
+    # 256 independent sequences per GPU: the post-LK chain (post-LK kernel, host
+    # EPnP, scoring, keyframe: ~0.16 ms, mostly latency) is paid once per step for the
+    # whole batch, so frames/s rises with the batch -- round 4, driver window: 128:
+    # 88.3k-89.1k, 256: 94.6k-94.9k (profiles/r04/e_seqcurve.txt); a step takes ~2.7 ms
+    # at 256 (each sequence still advances ~370 frames/s)
+    ap.add_argument("--seq", type=int, default=256, help="independent sequences per GPU (batched launches)")
     ap.add_argument("--config", default="kitti", choices=sorted(CONFIGS))
     ap.add_argument("--threads", type=int, default=0, help="host RANSAC threads (0 = auto)")
     ap.add_argument("--timing", type=int, default=2, choices=(1, 2, 3),
@@ -501,7 +507,7 @@ def main():
         lk_name, lk_desc = "lk_fast_kernel<21, 21", "one feature per wave"
     else:
         lk_name, lk_desc = "lk_multi_kernel<4, 1", "four features per wave"
-    traffic = pmc_traffic(args.config, lk_name)
+    traffic = pmc_traffic(args.config, lk_name, Sq)
     dominant = max(phases, key=lambda k: phases[k][0])
     # pyramid + Scharr of one new left frame per sequence per step (the launch
     # chain pyr_scharr_kernel x levels + the coarsest Scharr + borders)
@@ -519,12 +525,12 @@ def main():
     # derivatives, borders). Per level: c pyr_scharr + the coarsest scharr + borders.
     c_lev = max(ML, 3)
     if os.environ.get("SVO_PYR_FUSED", "1")[:1] == "0":
-        t_ps, t_sc, t_pad = (pmc_traffic(args.config, k) for k in ("pyr_scharr_kernel", "scharr_kernel",
+        t_ps, t_sc, t_pad = (pmc_traffic(args.config, k, Sq) for k in ("pyr_scharr_kernel", "scharr_kernel",
                                                                     "pad_batched_kernel"))
         pyr_traffic = c_lev * t_ps + t_sc + t_pad if None not in (t_ps, t_sc, t_pad) else None
         pyr_kernels = "pyr_scharr_kernel x levels + scharr_kernel (coarsest) + pad_batched_kernel (borders)"
     else:
-        t_ps, t_ch = (pmc_traffic(args.config, k) for k in ("pyr_scharr_kernel", "pyr_chain_kernel"))
+        t_ps, t_ch = (pmc_traffic(args.config, k, Sq) for k in ("pyr_scharr_kernel", "pyr_chain_kernel"))
         pyr_traffic = (c_lev - 1) * t_ps + t_ch if None not in (t_ps, t_ch) else None
         pyr_kernels = (f"pyr_scharr_kernel x {c_lev - 1} (pyrDown + Scharr + the source level's border) + "
                        "pyr_chain_kernel (last two levels, their derivatives and borders)")
@@ -533,7 +539,7 @@ def main():
     # bytes = one read of each W x H u8 frame (one raster pass)
     fast_avg_s = fe.time_fast(Wm + K, 20) / 1e3 if hasattr(fe, "time_fast") else 0.0
     fast_bytes = Sq * W * H
-    fast_traffic = pmc_traffic(args.config, "fast_detect_q_kernel")
+    fast_traffic = pmc_traffic(args.config, "fast_detect_q_kernel", Sq)
     single = None
     if not args.no_single and world == 1:
         fe1 = S.Frontend(ctx, S.FrontendConfig(W, H, scenes[0].K, n_seq=1, n_frames=T, n_features=N, max_level=ML))

@@ -391,6 +391,10 @@ __global__ __launch_bounds__(64) void sqpnp_select_kernel(const SqpnpFitIn* __re
     const int s = blockIdx.x, lane = threadIdx.x;
     __shared__ sq::SqpnpCost c;
     __shared__ double ev[9], evec[81], rs[18][9];
+    // the inliers' object points, compacted, for the positive-depth majority test
+    // (a search calls it for every candidate whose point mean is behind the camera)
+    constexpr int kLdsPts = 2048;
+    __shared__ float lp[3 * kLdsPts];
     const SqpnpFitIn fin = in[s];
     const SqFitWork& wk = work[s];
     int nn = -1;
@@ -424,6 +428,23 @@ __global__ __launch_bounds__(64) void sqpnp_select_kernel(const SqpnpFitIn* __re
             for (int w = lane; w < (n + 31) / 32; w += 64)
                 n_in += __popc(b[w] & (w == n / 32 ? (1u << (n & 31)) - 1u : ~0u));
             for (int off = 32; off > 0; off >>= 1) n_in += __shfl_xor(n_in, off);
+            const bool staged = n_in <= kLdsPts;
+            if (staged) {  // ballot compaction, every lane converged (n is uniform)
+                int base = 0;
+                for (int i0 = 0; i0 < n; i0 += 64) {
+                    const int i = i0 + lane;
+                    const bool inl = i < n && ((b[i >> 5] >> (i & 31)) & 1u);
+                    const unsigned long long m = __ballot(inl);
+                    if (inl) {
+                        const int k = base + __popcll(m & ((1ull << lane) - 1ull));
+                        lp[3 * k] = o[3 * i];
+                        lp[3 * k + 1] = o[3 * i + 1];
+                        lp[3 * k + 2] = o[3 * i + 2];
+                    }
+                    base += __popcll(m);
+                }
+                __syncthreads();
+            }
             sq::sq_select(
                 c, ev, evec, nn, n_in,
                 [&](int j, double* r) {
@@ -431,10 +452,17 @@ __global__ __launch_bounds__(64) void sqpnp_select_kernel(const SqpnpFitIn* __re
                 },
                 [&](const double* r, const double* tt) {
                     int pos = 0;
-                    for (int i = lane; i < n; i += 64) {
-                        if (!((b[i >> 5] >> (i & 31)) & 1u)) continue;
-                        const double p[3] = {(double)o[3 * i], (double)o[3 * i + 1], (double)o[3 * i + 2]};
-                        pos += dot3(r + 6, p) + tt[2] > 0;
+                    if (staged) {
+                        for (int k = lane; k < n_in; k += 64) {
+                            const double p[3] = {(double)lp[3 * k], (double)lp[3 * k + 1], (double)lp[3 * k + 2]};
+                            pos += dot3(r + 6, p) + tt[2] > 0;
+                        }
+                    } else {
+                        for (int i = lane; i < n; i += 64) {
+                            if (!((b[i >> 5] >> (i & 31)) & 1u)) continue;
+                            const double p[3] = {(double)o[3 * i], (double)o[3 * i + 1], (double)o[3 * i + 2]};
+                            pos += dot3(r + 6, p) + tt[2] > 0;
+                        }
                     }
                     for (int off = 32; off > 0; off >>= 1) pos += __shfl_xor(pos, off);
                     return pos;

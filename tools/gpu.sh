@@ -97,7 +97,7 @@ run_pmc() {
 
 run_mix() {
     local tag=$1; shift
-    local B="python bench.py ${*:---steps 8 --warmup 2 --no-cpu-baseline --no-single --no-bucketed --no-forward --no-orb}"
+    local B="python bench.py ${*:---seq 256 --steps 8 --warmup 2 --no-cpu-baseline --no-single --no-bucketed --no-forward --no-orb}"
     [ "$1" = "--cmd" ] && { shift; B="$*"; }
     timeout -s KILL 200 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_WAIT_INST_ANY \
         SQ_ACTIVE_INST_ANY SQ_INSTS_VMEM -d /tmp/ps1 -o run --output-format csv -- $B > $O/mix.log 2>&1 || fail mix1 $O/mix.log
@@ -228,7 +228,7 @@ run_round() {
     run_smoke
     run_prof "$tag"
     for c in kitti 1080p 4k; do
-        if [ $c = kitti ]; then run_pmc "$tag" $c 128; else run_pmc "$tag" $c 16; fi
+        if [ $c = kitti ]; then run_pmc "$tag" $c 256; else run_pmc "$tag" $c 16; fi
     done
     run_mix "$tag"
     run_bench "${tag}_driver" --gpus 1 --steps 20 --warmup 5
