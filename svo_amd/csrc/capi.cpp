@@ -329,6 +329,7 @@ int svo_fast_detect(svo_ctx* ctx, const svo_image* img, int threshold, int nonma
     int* rowoff = rowcnt + L.h + 64;
     if (mask) SVO_HIP(ctx, hipMemcpyAsync(dmask, mask, npx, hipMemcpyHostToDevice, ctx->stream));
     FastDetBatch b{dd, dmask, bits, rowcnt, rowoff, dout, dn, npx, nseg, cap};
+    b.padded = true;  // an svo_image level
     SVO_HIP(ctx, launch_fast_detect(b, 1, L.w, L.h, threshold, nonmax ? 1 : 0, ctx->stream));
     int n = 0;
     SVO_HIP(ctx, hipMemcpyAsync(&n, dn, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));

@@ -137,6 +137,10 @@ struct FastDetBatch {
     // nullable [s][npx]: fast_detect_q_kernel writes the score of every kept corner
     // there, so the emit pass reads one byte instead of re-scoring from the image
     uint8_t* score_map = nullptr;
+    // the images carry the kPyrPad border of svo_image levels (any content: the
+    // detector never uses a pixel outside the image), so every tile stages its
+    // pixels with dword loads; false for unpadded images (ORB's scale levels)
+    bool padded = false;
 };
 // stage: kFastAll detect + scan + emit, kFastDetect detect only (the row counts
 // are cleared first); kFastBoxes: the detection already ran without the box mask

@@ -258,7 +258,8 @@ __global__ __launch_bounds__(256) void fast_detect_q_kernel(FastDetBatch B, int 
     __shared__ unsigned long long TM[TY];
     __shared__ unsigned long long RB[TY];
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-    const bool inside = x0 >= 4 && y0 >= 4 && x0 - 4 + FD_IW <= w && y0 - 4 + QIH <= h;
+    const bool inside = B.padded ? x0 - 4 + FD_IW <= L.pitch - kPyrPad && y0 - 4 + QIH <= h + kPyrPad
+                                 : x0 >= 4 && y0 >= 4 && x0 - 4 + FD_IW <= w && y0 - 4 + QIH <= h;
     if (inside) {
         for (int k = tid; k < QIH * (FD_IW / 4); k += 256) {
             const int r = k / (FD_IW / 4), c4 = k - r * (FD_IW / 4);

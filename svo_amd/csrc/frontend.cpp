@@ -477,6 +477,7 @@ FastDetBatch fe_fast_batch(svo_frontend* fe, const PyrDesc* descs_cur, bool use_
     FastDetBatch fb{descs_cur, nullptr, fe->fbits, fe->rowcnt, fe->rowoff,
                     (svo_keypoint*)fe->kps, fe->kn, fe->npx, (fe->W + 63) / 64, fe->KCAP};
     fb.score_map = fe->score_map;
+    fb.padded = true;  // the frames are svo_image levels
     if (use_mask) {  // boxes around the previous frame's features, rasterised per FAST tile
         fb.box_pts = fe->xyA;
         fb.box_counts = fe->nA;
