@@ -116,7 +116,7 @@ hipError_t launch_fast_collect(const FastBatch& b, int nseq, int w, int h, int n
 struct FastDetBatch {
     const PyrDesc* descs;
     const uint8_t* mask;        // nullable, npx per sequence
-    unsigned long long* bits;   // [s][h][nseg]
+    unsigned long long* bits;   // [s][nseg][h]: one block's rows of a segment contiguous
     int* rowcnt;                // [s][h]
     int* rowoff;                // [s][h]
     svo_keypoint* out;          // [s][cap]

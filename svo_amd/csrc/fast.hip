@@ -408,8 +408,7 @@ __global__ __launch_bounds__(256) void fast_detect_q_kernel(FastDetBatch B, int 
     __syncthreads();
     if (tid < TY && y0 + tid < h) {
         const unsigned long long bal = RB[tid] & (boxes ? TM[tid] : ~0ull);
-        const size_t row = seq * h + y0 + tid;
-        B.bits[row * B.nseg + blockIdx.x] = bal;
+        B.bits[(seq * B.nseg + blockIdx.x) * (size_t)h + y0 + tid] = bal;
     }
 }
 
@@ -477,8 +476,7 @@ __global__ __launch_bounds__(64) void fast_box_filter_kernel(FastDetBatch B, int
     }
     __syncthreads();
     if (lane < TY && y0 + lane < h) {
-        const size_t row = seq * h + y0 + lane;
-        unsigned long long* word = B.bits + row * B.nseg + blockIdx.x;
+        unsigned long long* word = B.bits + (seq * B.nseg + blockIdx.x) * (size_t)h + y0 + lane;
         *word &= TM[lane];
     }
 }
@@ -548,14 +546,14 @@ __global__ __launch_bounds__(kScanBlock) void fast_scan_kernel(FastDetBatch B, i
     const size_t seq = blockIdx.x;
     int* __restrict__ cnt = B.rowcnt + seq * h;
     int* __restrict__ off = B.rowoff + seq * h;
-    const unsigned long long* __restrict__ words = B.bits + seq * (size_t)h * B.nseg;
+    const unsigned long long* __restrict__ words = B.bits + seq * (size_t)h * B.nseg;  // [segment][row]
     __shared__ int part[kScanBlock];
     const int tid = threadIdx.x;
     const int run = (h + kScanBlock - 1) / kScanBlock, y0 = tid * run, y1 = min(h, y0 + run);
     int sum = 0;
     for (int y = y0; y < y1; y++) {  // the row's corners: the popcount of its words
         int c = 0;
-        for (int sgi = 0; sgi < B.nseg; sgi++) c += __popcll(words[(size_t)y * B.nseg + sgi]);
+        for (int sgi = 0; sgi < B.nseg; sgi++) c += __popcll(words[(size_t)sgi * h + y]);
         cnt[y] = c;
         sum += c;
     }
@@ -588,10 +586,10 @@ __global__ __launch_bounds__(64) void fast_emit_kernel(FastDetBatch B, int thres
     if (B.rowcnt[seq * h + y] == 0) return;
     const int lane = threadIdx.x;
     int off = B.rowoff[seq * h + y];
-    const unsigned long long* bits = B.bits + (seq * h + y) * B.nseg;
+    const unsigned long long* bits = B.bits + seq * (size_t)h * B.nseg + y;  // word sgi at bits[sgi * h]
     svo_keypoint* __restrict__ out = B.out + seq * B.cap;
     for (int sgi = 0; sgi < B.nseg; sgi++) {
-        const unsigned long long m = bits[sgi];
+        const unsigned long long m = bits[(size_t)sgi * h];
         if (!m) continue;
         if ((m >> lane) & 1ull) {
             const int idx = off + __popcll(m & ((1ull << lane) - 1ull));
