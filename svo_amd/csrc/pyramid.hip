@@ -303,9 +303,24 @@ __global__ __launch_bounds__(256) void pyr_scharr_kernel(const PyrDesc* __restri
                 *reinterpret_cast<const uint32_t*>(s.data + (size_t)(sy0 + r) * s.pitch + xa + 4 * c4);
         }
     } else {
-        for (int k = tid; k < FS_IH * FS_IW; k += 256) {
-            const int r = k / FS_IW, c = k - r * FS_IW;
-            T[r][c] = s.data[(size_t)refl101(sy0 + r, sh) * s.pitch + refl101(xa + c, sw)];
+        // a border tile: a staged row is a whole source row (REFLECT_101 maps rows to
+        // rows), so every dword inside the columns [0, sw) is still one load; only
+        // the dwords crossing or beyond a side edge take bytes with the column
+        // reflection
+        constexpr int DW = FS_IW / 4;
+        for (int k = tid; k < FS_IH * DW; k += 256) {
+            const int r = k / DW, c4 = k - r * DW;
+            const uint8_t* row = s.data + (size_t)refl101(sy0 + r, sh) * s.pitch;
+            const int xc = xa + 4 * c4;
+            uint32_t v;
+            if (xc >= 0 && xc + 3 < sw) {
+                v = *reinterpret_cast<const uint32_t*>(row + xc);
+            } else {
+                v = 0;
+#pragma unroll
+                for (int b = 0; b < 4; b++) v |= (uint32_t)row[refl101(xc + b, sw)] << (8 * b);
+            }
+            *reinterpret_cast<uint32_t*>(&T[r][4 * c4]) = v;
         }
     }
     __syncthreads();
