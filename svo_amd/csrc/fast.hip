@@ -578,41 +578,43 @@ __global__ __launch_bounds__(kScanBlock) void fast_scan_kernel(FastDetBatch B, i
 
 // raster-order write of one row's keypoints (one wave per row); the FAST
 // score of a kept corner is recomputed from the image (few pixels)
+constexpr int kEmitRows = 8;  // rows per wave: the segment-major words of 8 rows share a line
 __global__ __launch_bounds__(64) void fast_emit_kernel(FastDetBatch B, int threshold, int nonmax) {
-    const int y = blockIdx.x;
     const size_t seq = blockIdx.y;
     const ImgLevel L = B.descs[seq].lv[0];
     const int h = L.h;
-    if (B.rowcnt[seq * h + y] == 0) return;
-    const int lane = threadIdx.x;
-    int off = B.rowoff[seq * h + y];
-    const unsigned long long* bits = B.bits + seq * (size_t)h * B.nseg + y;  // word sgi at bits[sgi * h]
-    svo_keypoint* __restrict__ out = B.out + seq * B.cap;
-    for (int sgi = 0; sgi < B.nseg; sgi++) {
-        const unsigned long long m = bits[(size_t)sgi * h];
-        if (!m) continue;
-        if ((m >> lane) & 1ull) {
-            const int idx = off + __popcll(m & ((1ull << lane) - 1ull));
-            if (idx < B.cap) {
-                const int x = sgi * 64 + lane;
-                float resp = 0.f;
-                if (nonmax && B.score_map) {
-                    resp = (float)B.score_map[seq * B.npx + (size_t)y * L.w + x];
-                } else if (nonmax) {
-                    const uint8_t* p = L.data + (size_t)y * L.pitch + x;
-                    int ring[16];
-#pragma unroll
-                    for (int q = 0; q < 16; q++) ring[q] = p[c_ring[q][1] * L.pitch + c_ring[q][0]];
-                    resp = (float)corner_score16(p[0], ring, threshold);
+    for (int y = blockIdx.x * kEmitRows; y < min(h, (int)(blockIdx.x + 1) * kEmitRows); y++) {
+        if (B.rowcnt[seq * h + y] == 0) continue;
+        const int lane = threadIdx.x;
+        int off = B.rowoff[seq * h + y];
+        const unsigned long long* bits = B.bits + seq * (size_t)h * B.nseg + y;  // word sgi at bits[sgi * h]
+        svo_keypoint* __restrict__ out = B.out + seq * B.cap;
+        for (int sgi = 0; sgi < B.nseg; sgi++) {
+            const unsigned long long m = bits[(size_t)sgi * h];
+            if (!m) continue;
+            if ((m >> lane) & 1ull) {
+                const int idx = off + __popcll(m & ((1ull << lane) - 1ull));
+                if (idx < B.cap) {
+                    const int x = sgi * 64 + lane;
+                    float resp = 0.f;
+                    if (nonmax && B.score_map) {
+                        resp = (float)B.score_map[seq * B.npx + (size_t)y * L.w + x];
+                    } else if (nonmax) {
+                        const uint8_t* p = L.data + (size_t)y * L.pitch + x;
+                        int ring[16];
+    #pragma unroll
+                        for (int q = 0; q < 16; q++) ring[q] = p[c_ring[q][1] * L.pitch + c_ring[q][0]];
+                        resp = (float)corner_score16(p[0], ring, threshold);
+                    }
+                    svo_keypoint kp;
+                    kp.x = (float)x;
+                    kp.y = (float)y;
+                    kp.response = resp;
+                    out[idx] = kp;
                 }
-                svo_keypoint kp;
-                kp.x = (float)x;
-                kp.y = (float)y;
-                kp.response = resp;
-                out[idx] = kp;
             }
+            off += __popcll(m);
         }
-        off += __popcll(m);
     }
 }
 
@@ -672,7 +674,7 @@ hipError_t launch_fast_detect(const FastDetBatch& b0, int nseq, int w, int h, in
                                0, st, b, w, h);
         }
         hipLaunchKernelGGL(fast_scan_kernel, dim3(nseq), dim3(kScanBlock), 0, st, b, h);
-        hipLaunchKernelGGL(fast_emit_kernel, dim3(h, nseq), dim3(64), 0, st, b, threshold, nonmax);
+        hipLaunchKernelGGL(fast_emit_kernel, dim3((h + kEmitRows - 1) / kEmitRows, nseq), dim3(64), 0, st, b, threshold, nonmax);
         return hipGetLastError();
     }
     hipError_t e = hipSuccess;
@@ -684,7 +686,7 @@ hipError_t launch_fast_detect(const FastDetBatch& b0, int nseq, int w, int h, in
     hipLaunchKernelGGL(fast_detect_q_kernel<FD_TY>, grid, dim3(256), 0, st, b, threshold, nonmax);
     if (stage == kFastDetect) return hipGetLastError();
     hipLaunchKernelGGL(fast_scan_kernel, dim3(nseq), dim3(kScanBlock), 0, st, b, h);
-    hipLaunchKernelGGL(fast_emit_kernel, dim3(h, nseq), dim3(64), 0, st, b, threshold, nonmax);
+    hipLaunchKernelGGL(fast_emit_kernel, dim3((h + kEmitRows - 1) / kEmitRows, nseq), dim3(64), 0, st, b, threshold, nonmax);
     return hipGetLastError();
 }
 
