@@ -17,6 +17,7 @@
 // Kernels: (1) tile score kernel -> u16 map {corner bit 8 | score}; (2) per-row
 // keep count; (3) per-row stable write at the row's exclusive offset.
 #include "common.hpp"
+#include "xcd_tile.hpp"
 
 #include <cstdlib>
 
@@ -215,6 +216,11 @@ typedef short fs16x2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ fs16x2 as_s2(unsigned v) { return __builtin_bit_cast(fs16x2, v); }
 __device__ __forceinline__ unsigned as_u(fs16x2 v) { return __builtin_bit_cast(unsigned, v); }
 
+// lanes below this one with their bit set in the wave mask m (v_mbcnt pair)
+__device__ __forceinline__ int rank_below(unsigned long long m) {
+    return (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
+}
+
 // cornerScore<16> (fast_score.cpp) with both chains in one packed pass: low half
 // a0 = max_k max(min(a_k, d[k]), min(a_k, d[k+9])) from threshold, high half the
 // same on e = -d from -inf (= -B of the b-chain); b0 = min(-a0, B), score = -b0 - 1
@@ -242,16 +248,18 @@ __device__ __forceinline__ int corner_score16_pk(int v, const int* ring, int thr
     return (max(a0, nb) - 1) & 0xFF;   // -min(-a0, B) - 1, (uchar) as FAST_t
 }
 
-template <int TY>
+// XT: tiles in XCD order (xcd_tile.hpp)
+template <int TY, bool XT = false>
 __global__ __launch_bounds__(256) void fast_detect_q_kernel(FastDetBatch B, int threshold, int nonmax) {
     constexpr int QSH = TY + 2, QIH = TY + 8;           // score rows (halo 1), staged rows (halo 4)
     constexpr int QQ = ((QSH + 3) / 4) * FD_SW + 8;      // queue entries per wave
     static_assert(2 * ((QSH + 3) / 4) <= 64, "halo pre-test: one lane per (row, side)");
     static_assert(QSH < 512, "queue entries pack (row << 7 | column) into 16 bits");
-    const ImgLevel L = B.descs[blockIdx.z].lv[0];
+    const XcdTile tile = XT ? xcd_tile() : XcdTile{(int)blockIdx.x, (int)blockIdx.y, (int)blockIdx.z};
+    const ImgLevel L = B.descs[tile.z].lv[0];
     const int w = L.w, h = L.h;
-    const int x0 = blockIdx.x * FD_TX, y0 = blockIdx.y * TY;
-    const size_t seq = blockIdx.z;
+    const int x0 = tile.x * FD_TX, y0 = tile.y * TY;
+    const size_t seq = tile.z;
     __shared__ __attribute__((aligned(16))) uint8_t T[QIH][FD_IW];
     __shared__ uint16_t SC[QSH][FD_SW + 2];  // bit 8: corner, low byte: score
     __shared__ uint16_t CQ[4][QQ];
@@ -261,10 +269,20 @@ __global__ __launch_bounds__(256) void fast_detect_q_kernel(FastDetBatch B, int 
     const bool inside = B.padded ? x0 - 4 + FD_IW <= L.pitch - kPyrPad && y0 - 4 + QIH <= h + kPyrPad
                                  : x0 >= 4 && y0 >= 4 && x0 - 4 + FD_IW <= w && y0 - 4 + QIH <= h;
     if (inside) {
-        for (int k = tid; k < QIH * (FD_IW / 4); k += 256) {
-            const int r = k / (FD_IW / 4), c4 = k - r * (FD_IW / 4);
-            const uint8_t* src = L.data + (size_t)(y0 - 4 + r) * L.pitch + (x0 - 4 + 4 * c4);
-            *reinterpret_cast<uint32_t*>(&T[r][4 * c4]) = *reinterpret_cast<const uint32_t*>(src);
+        // thread -> (row r0, dword c4), rows r0 + RP p: all loads in flight before the
+        // first LDS store
+        constexpr int DW = FD_IW / 4, RP = 256 / DW, NP = (QIH + RP - 1) / RP;
+        const int r0 = tid / DW, c4 = tid - r0 * DW;
+        if (r0 < RP) {
+            const uint8_t* src = L.data + (size_t)(y0 - 4 + r0) * L.pitch + (x0 - 4 + 4 * c4);
+            uint32_t v[NP];
+#pragma unroll
+            for (int p = 0; p < NP; p++)
+                v[p] = *reinterpret_cast<const uint32_t*>(src + (size_t)(min(r0 + p * RP, QIH - 1) - r0) * L.pitch);
+            // (rows past the tile load and store its last row again, the same bytes:
+            // no branch, so no wait between the loads)
+#pragma unroll
+            for (int p = 0; p < NP; p++) *reinterpret_cast<uint32_t*>(&T[min(r0 + p * RP, QIH - 1)][4 * c4]) = v[p];
         }
     } else {
         for (int k = tid; k < QIH * FD_IW; k += 256) {
@@ -293,14 +311,37 @@ __global__ __launch_bounds__(256) void fast_detect_q_kernel(FastDetBatch B, int 
             const bool dark = (p0 < lo || p8 < lo) && (p4 < lo || p12 < lo);
             cand = bright || dark;
         }
-        const unsigned long long bal = __ballot(cand);
-        if (cand) q[nq + __popcll(bal & ((1ull << lane) - 1ull))] = (uint16_t)((sr << 7) | sc);
+        const unsigned long long bal = __builtin_amdgcn_ballot_w64(cand);
+        if (cand) q[nq + rank_below(bal)] = (uint16_t)((sr << 7) | sc);
         nq += __popcll(bal);
     };
-    for (int sr = wv; sr < QSH; sr += 4) {
-        SC[sr][lane + 1] = 0;
-        if (lane < 2) SC[sr][lane * 65] = 0;
-        pretest(sr, lane + 1, true);
+    {
+        // columns 1 .. 64 (lane -> sc = lane + 1), unrolled over the rows: one LDS base
+        // per lane (staged row sr, column sc), the five taps at immediate offsets,
+        // branch-free (every tap lies inside the staged tile)
+        const int wvu = __builtin_amdgcn_readfirstlane(wv);
+        const bool colok = x0 + lane >= 3 && x0 + lane < w - 3;
+        const uint8_t* tb = &T[wvu][lane + 1];
+        uint16_t* sb0 = &SC[wvu][lane + 1];
+#pragma unroll
+        for (int i = 0; i < (QSH + 3) / 4; i++) {
+            const int sr = wvu + 4 * i;
+            if (sr < QSH) {
+                sb0[i * 4 * (FD_SW + 2)] = 0;
+                if (lane < 2) SC[sr][lane * 65] = 0;
+                const uint8_t* t = tb + i * 4 * FD_IW;
+                const int v = t[3 * FD_IW + 3], hi = v + hi_t, lo = v + lo_t;
+                const int p8 = t[3], p0 = t[6 * FD_IW + 3], p12 = t[3 * FD_IW], p4 = t[3 * FD_IW + 6];
+                const int y = y0 - 1 + sr;
+                const bool rowok = y >= 3 && y < h - 3;
+                const bool bright = min(max(p0, p8), max(p4, p12)) > hi;
+                const bool dark = max(min(p0, p8), min(p4, p12)) < lo;
+                const bool cand = colok & rowok & (bright | dark);
+                const unsigned long long bal = __builtin_amdgcn_ballot_w64(cand);
+                if (cand) q[nq + rank_below(bal)] = (uint16_t)((sr << 7) | (lane + 1));
+                nq += __popcll(bal);
+            }
+        }
     }
     {
         // halo columns 0 and 65 of the wave's rows (<= 9 rows -> 18 positions)
@@ -332,11 +373,11 @@ __global__ __launch_bounds__(256) void fast_detect_q_kernel(FastDetBatch B, int 
             }
             corner = run9(~acc & 0xFFFFu) || run9(acc >> 16);
         }
-        const unsigned long long bal = __ballot(corner);
+        const unsigned long long bal = __builtin_amdgcn_ballot_w64(corner);
         if (corner) {
             const int sr = k >> 7, sc = k & 127;
             SC[sr][sc] = 0x100;
-            q[nc + __popcll(bal & ((1ull << lane) - 1ull))] = (uint16_t)k;  // index <= i: already read
+            q[nc + rank_below(bal)] = (uint16_t)k;  // index <= i: already read
         }
         nc += __popcll(bal);
     }
@@ -408,7 +449,7 @@ __global__ __launch_bounds__(256) void fast_detect_q_kernel(FastDetBatch B, int 
     __syncthreads();
     if (tid < TY && y0 + tid < h) {
         const unsigned long long bal = RB[tid] & (boxes ? TM[tid] : ~0ull);
-        B.bits[(seq * B.nseg + blockIdx.x) * (size_t)h + y0 + tid] = bal;
+        B.bits[(seq * B.nseg + tile.x) * (size_t)h + y0 + tid] = bal;
     }
 }
 
@@ -683,7 +724,10 @@ hipError_t launch_fast_detect(const FastDetBatch& b0, int nseq, int w, int h, in
         if (e != hipSuccess) return e;
     }
     dim3 grid((w + FD_TX - 1) / FD_TX, (h + FD_TY - 1) / FD_TY, nseq);
-    hipLaunchKernelGGL(fast_detect_q_kernel<FD_TY>, grid, dim3(256), 0, st, b, threshold, nonmax);
+    if (xcd_tiles_on())
+        hipLaunchKernelGGL((fast_detect_q_kernel<FD_TY, true>), grid, dim3(256), 0, st, b, threshold, nonmax);
+    else
+        hipLaunchKernelGGL(fast_detect_q_kernel<FD_TY>, grid, dim3(256), 0, st, b, threshold, nonmax);
     if (stage == kFastDetect) return hipGetLastError();
     hipLaunchKernelGGL(fast_scan_kernel, dim3(nseq), dim3(kScanBlock), 0, st, b, h);
     hipLaunchKernelGGL(fast_emit_kernel, dim3((h + kEmitRows - 1) / kEmitRows, nseq), dim3(64), 0, st, b, threshold, nonmax);

@@ -13,6 +13,7 @@
 #include <utility>
 
 #include "common.hpp"
+#include "xcd_tile.hpp"
 
 namespace svo {
 
@@ -281,13 +282,15 @@ constexpr int FS_IH = PD_IH;          // 36 rows
 // false = pyrDown (+ the source level's border) only, the right frames' pyramid
 // (the dword staging and packed row pass of this kernel, against the byte loads
 // of pyr_down_batched_kernel)
-template <bool NT, bool SCH = true>
+// XT: tiles in XCD order (xcd_tile.hpp)
+template <bool NT, bool SCH = true, bool XT = false>
 __global__ __launch_bounds__(256) void pyr_scharr_kernel(const PyrDesc* __restrict__ descs,
                                                          const DerivDesc* __restrict__ ders, int level, int pad_src) {
-    const PyrDesc& P = descs[blockIdx.z];
+    const XcdTile tile = XT ? xcd_tile() : XcdTile{(int)blockIdx.x, (int)blockIdx.y, (int)blockIdx.z};
+    const PyrDesc& P = descs[tile.z];
     const ImgLevel& s = P.lv[level];
     const ImgLevel& d = P.lv[level + 1];
-    const int x0 = blockIdx.x * PD_TX, y0 = blockIdx.y * PD_TY;
+    const int x0 = tile.x * PD_TX, y0 = tile.y * PD_TY;
     const int sx0 = 2 * x0 - 2, sy0 = 2 * y0 - 2;
     const int xa = sx0 - 2;  // multiple of 4 (x0 is a multiple of 64)
     __shared__ __attribute__((aligned(16))) uint8_t T[FS_IH][FS_IW + 8];  // rows 16-byte aligned (b128 reads)
@@ -296,11 +299,20 @@ __global__ __launch_bounds__(256) void pyr_scharr_kernel(const PyrDesc* __restri
     const int sw = s.w, sh = s.h;
     const bool interior = xa >= 0 && sy0 >= 0 && xa + FS_IW <= sw && sy0 + FS_IH <= sh;
     if (interior) {
-        constexpr int DW = FS_IW / 4;  // 34 dwords per row
-        for (int k = tid; k < FS_IH * DW; k += 256) {
-            const int r = k / DW, c4 = k - r * DW;
-            *reinterpret_cast<uint32_t*>(&T[r][4 * c4]) =
-                *reinterpret_cast<const uint32_t*>(s.data + (size_t)(sy0 + r) * s.pitch + xa + 4 * c4);
+        // thread -> (row r0, dword c4), rows r0 + RP p: all loads in flight before the
+        // first LDS store
+        constexpr int DW = FS_IW / 4, RP = 256 / DW, NP = (FS_IH + RP - 1) / RP;  // 34 dwords per row
+        const int r0 = tid / DW, c4 = tid - r0 * DW;
+        if (r0 < RP) {
+            const uint8_t* src = s.data + (size_t)(sy0 + r0) * s.pitch + xa + 4 * c4;
+            uint32_t v[NP];
+#pragma unroll
+            for (int p = 0; p < NP; p++)
+                v[p] = *reinterpret_cast<const uint32_t*>(src + (size_t)(min(r0 + p * RP, FS_IH - 1) - r0) * s.pitch);
+            // (rows past the tile load and store its last row again, the same bytes:
+            // no branch, so no wait between the loads)
+#pragma unroll
+            for (int p = 0; p < NP; p++) *reinterpret_cast<uint32_t*>(&T[min(r0 + p * RP, FS_IH - 1)][4 * c4]) = v[p];
         }
     } else {
         // a border tile: a staged row is a whole source row (REFLECT_101 maps rows to
@@ -341,8 +353,8 @@ __global__ __launch_bounds__(256) void pyr_scharr_kernel(const PyrDesc* __restri
     // a task: 4 columns x 4 rows from 3 aligned dwords per staged row, one 16-byte
     // store per row (columns >= sw are never written: the zero border stays) ----
     if constexpr (SCH) {
-        uint32_t* __restrict__ out = ders[blockIdx.z].data[level];
-        const int op = ders[blockIdx.z].pitch[level];
+        uint32_t* __restrict__ out = ders[tile.z].data[level];
+        const int op = ders[tile.z].pitch[level];
         const int g = tid & 31, q = tid >> 5;
         const int x = 2 * x0 + 4 * g;
         int rows[6][6];  // staged rows 1 + 4q .. 6 + 4q, T columns 3 + 4g .. 8 + 4g
@@ -745,9 +757,13 @@ hipError_t launch_pyramid_batched(const PyrDesc* d_descs, int nseq, int w, int h
     for (int l = 1; l <= chain_start(c); l++) {
         lw = (lw + 1) / 2;
         lh = (lh + 1) / 2;
-        hipLaunchKernelGGL((pyr_scharr_kernel<true, false>),
-                           dim3((lw + PD_TX - 1) / PD_TX, (lh + PD_TY - 1) / PD_TY, nseq), dim3(256), 0, st, d_descs,
-                           (const DerivDesc*)nullptr, l - 1, 1);
+        const dim3 grid((lw + PD_TX - 1) / PD_TX, (lh + PD_TY - 1) / PD_TY, nseq);
+        if (xcd_tiles_on())
+            hipLaunchKernelGGL((pyr_scharr_kernel<true, false, true>), grid, dim3(256), 0, st, d_descs,
+                               (const DerivDesc*)nullptr, l - 1, 1);
+        else
+            hipLaunchKernelGGL((pyr_scharr_kernel<true, false>), grid, dim3(256), 0, st, d_descs,
+                               (const DerivDesc*)nullptr, l - 1, 1);
     }
     launch_chain_c<false>(c, d_descs, nullptr, nseq, w, h, st);
     return hipGetLastError();
@@ -765,8 +781,11 @@ hipError_t launch_pyramid_scharr_batched(const PyrDesc* d_descs, const DerivDesc
     for (int l = 0; l < chain_start(c); l++) {
         lw = (lw + 1) / 2;
         lh = (lh + 1) / 2;
-        hipLaunchKernelGGL(pyr_scharr_kernel<true>, dim3((lw + PD_TX - 1) / PD_TX, (lh + PD_TY - 1) / PD_TY, nseq),
-                           dim3(256), 0, st, d_descs, d_ders, l, 1);
+        const dim3 grid((lw + PD_TX - 1) / PD_TX, (lh + PD_TY - 1) / PD_TY, nseq);
+        if (xcd_tiles_on())
+            hipLaunchKernelGGL((pyr_scharr_kernel<true, true, true>), grid, dim3(256), 0, st, d_descs, d_ders, l, 1);
+        else
+            hipLaunchKernelGGL(pyr_scharr_kernel<true>, grid, dim3(256), 0, st, d_descs, d_ders, l, 1);
     }
     launch_chain_c<true>(c, d_descs, d_ders, nseq, w, h, st);
     return hipGetLastError();

@@ -203,7 +203,8 @@ run_ab() {
         python -c "
 import json; d=json.loads(open('$O/ab.log').read().strip().splitlines()[-1]); p=d['phase_ms_per_step']
 sm=d.get('step_ms', {})
-print('$var=$v', d['value'], d['ms_per_step'], 'median', sm.get('median'), 'p90', sm.get('p90'), 'lk', p['lk'], 'pyr', p['pyramid'])"
+print('$var=$v', d['value'], d['ms_per_step'], 'median', sm.get('median'), 'p90', sm.get('p90'), 'lk', p['lk'], 'pyr', p['pyramid'],
+      'fast_us', d['roofline_fast']['avg_launch_us'], d['roofline_fast']['frac'], 'pyr_us', d['roofline_pyramid']['avg_launch_us'], d['roofline_pyramid']['frac'])"
     done; done
 }
 
