@@ -278,6 +278,44 @@ namespace {
 constexpr int FS_IW = 2 * PD_TX + 8;  // 136 staged columns: sx0 - 2 .. sx0 + 133 (dword aligned)
 constexpr int FS_IH = PD_IH;          // 36 rows
 
+// Scharr of a 4 x 4 pixel block, packed: a row's 6 columns k = 0 .. 5 (the block's
+// columns -1 .. 4: byte 3 of dword a0, the 4 bytes of a1, byte 0 of a2) as the
+// 16-bit column pairs (k0, k2), (k2, k4), (k1, k3), (k3, k5). Output columns
+// m = 0, 2 and m = 1, 3 are then one packed lane each, and the 16-bit wrap-around
+// arithmetic leaves the stored low 16 bits of ix 2^kDerShift, iy 2^kDerShift
+// unchanged (|values| <= 16320).
+typedef short s16x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ void scharr_pairs(unsigned a0, unsigned a1, unsigned a2, s16x2 (&pr)[4]) {
+    pr[0] = __builtin_bit_cast(s16x2, __builtin_amdgcn_perm(a1, a0, 0x0c050c03u));  // a0.b3, a1.b1
+    pr[1] = __builtin_bit_cast(s16x2, (a1 >> 8) & 0x00FF00FFu);                     // a1.b1, a1.b3
+    pr[2] = __builtin_bit_cast(s16x2, a1 & 0x00FF00FFu);                            // a1.b0, a1.b2
+    pr[3] = __builtin_bit_cast(s16x2, __builtin_amdgcn_perm(a2, a1, 0x0c040c02u));  // a1.b2, a2.b0
+}
+
+// one output row of the block from its top / middle / bottom rows' pairs:
+// o[m] = (iy(m) << 16) | (ix(m) & 0xFFFF), both x 2^kDerShift
+__device__ __forceinline__ void scharr_row(const s16x2 (&t)[4], const s16x2 (&mi)[4], const s16x2 (&b)[4],
+                                           unsigned (&o)[4]) {
+    constexpr short C3 = 3 << kDerShift, C10 = 10 << kDerShift;
+    // vertical smoothing vs = 3 t + 10 m + 3 b and difference d = b - t per pair
+    s16x2 vs[4], dd[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        vs[k] = (t[k] + b[k]) * C3 + mi[k] * C10;
+        dd[k] = b[k] - t[k];
+    }
+    // ix(m) = vs(m + 2) - vs(m); iy(m) = 3 d(m) + 10 d(m + 1) + 3 d(m + 2)
+    const unsigned ue = __builtin_bit_cast(unsigned, (s16x2)(vs[1] - vs[0]));
+    const unsigned uo = __builtin_bit_cast(unsigned, (s16x2)(vs[3] - vs[2]));
+    const unsigned ve = __builtin_bit_cast(unsigned, (s16x2)((dd[0] + dd[1]) * C3 + dd[2] * C10));
+    const unsigned vo = __builtin_bit_cast(unsigned, (s16x2)((dd[2] + dd[3]) * C3 + dd[1] * C10));
+    o[0] = __builtin_amdgcn_perm(ve, ue, 0x05040100u);
+    o[1] = __builtin_amdgcn_perm(vo, uo, 0x05040100u);
+    o[2] = __builtin_amdgcn_perm(ve, ue, 0x07060302u);
+    o[3] = __builtin_amdgcn_perm(vo, uo, 0x07060302u);
+}
+
 // NT: the derivative and level stores as non-temporal (streaming) stores; SCH:
 // false = pyrDown (+ the source level's border) only, the right frames' pyramid
 // (the dword staging and packed row pass of this kernel, against the byte loads
@@ -342,12 +380,22 @@ __global__ __launch_bounds__(256) void pyr_scharr_kernel(const PyrDesc* __restri
         const int r = k >> 4, q = k & 15;
         const uint4 v = *reinterpret_cast<const uint4*>(&T[r][8 * q]);
         const unsigned w4[4] = {v.x, v.y, v.z, v.w};
-        int bt[16];
+        // byte pairs P(i) = (b_i, b_i+4) as 16-bit lanes: outputs m = 0, 2 and m = 1, 3
+        // are one packed lane each (sums <= 16 * 255, no carry between the halves)
+        typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+        u16x2 P[7];  // P[i - 2], i = 2 .. 8
 #pragma unroll
-        for (int i = 0; i < 16; i++) bt[i] = (w4[i >> 2] >> (8 * (i & 3))) & 0xFF;
-#pragma unroll
-        for (int m = 0; m < 4; m++)
-            H[r][4 * q + m] = bt[2 * m + 2] + 4 * bt[2 * m + 3] + 6 * bt[2 * m + 4] + 4 * bt[2 * m + 5] + bt[2 * m + 6];
+        for (int i = 2; i <= 8; i++)
+            P[i - 2] = __builtin_bit_cast(u16x2, __builtin_amdgcn_perm(w4[(i >> 2) + 1], w4[i >> 2],
+                                                                       0x0c000c00u | (i & 3) | ((4u + (i & 3)) << 16)));
+        const unsigned e = __builtin_bit_cast(unsigned, (u16x2)(P[0] + P[4] + (P[1] + P[3]) * (unsigned short)4 +
+                                                                P[2] * (unsigned short)6));
+        const unsigned o = __builtin_bit_cast(unsigned, (u16x2)(P[2] + P[6] + (P[3] + P[5]) * (unsigned short)4 +
+                                                                P[4] * (unsigned short)6));
+        H[r][4 * q + 0] = (int)(e & 0xFFFFu);
+        H[r][4 * q + 1] = (int)(o & 0xFFFFu);
+        H[r][4 * q + 2] = (int)(e >> 16);
+        H[r][4 * q + 3] = (int)(o >> 16);
     }
     // ---- Scharr of level l pixels (2x0 + i, 2y0 + j), i < 128, j < 32: T[2 + j][4 + i];
     // a task: 4 columns x 4 rows from 3 aligned dwords per staged row, one 16-byte
@@ -357,19 +405,14 @@ __global__ __launch_bounds__(256) void pyr_scharr_kernel(const PyrDesc* __restri
         const int op = ders[tile.z].pitch[level];
         const int g = tid & 31, q = tid >> 5;
         const int x = 2 * x0 + 4 * g;
-        int rows[6][6];  // staged rows 1 + 4q .. 6 + 4q, T columns 3 + 4g .. 8 + 4g
+        // staged rows 1 + 4q .. 6 + 4q, T columns 3 + 4g .. 8 + 4g
+        s16x2 pr[6][4];
 #pragma unroll
         for (int rr = 0; rr < 6; rr++) {
             const uint8_t* trow = &T[1 + 4 * q + rr][0];
-            const unsigned a0 = *reinterpret_cast<const unsigned*>(trow + 4 * g);
-            const unsigned a1 = *reinterpret_cast<const unsigned*>(trow + 4 * g + 4);
-            const unsigned a2 = *reinterpret_cast<const unsigned*>(trow + 4 * g + 8);
-            rows[rr][0] = a0 >> 24;
-            rows[rr][1] = a1 & 0xFF;
-            rows[rr][2] = (a1 >> 8) & 0xFF;
-            rows[rr][3] = (a1 >> 16) & 0xFF;
-            rows[rr][4] = a1 >> 24;
-            rows[rr][5] = a2 & 0xFF;
+            scharr_pairs(*reinterpret_cast<const unsigned*>(trow + 4 * g),
+                         *reinterpret_cast<const unsigned*>(trow + 4 * g + 4),
+                         *reinterpret_cast<const unsigned*>(trow + 4 * g + 8), pr[rr]);
         }
         if (x < sw) {
 #pragma unroll
@@ -377,15 +420,7 @@ __global__ __launch_bounds__(256) void pyr_scharr_kernel(const PyrDesc* __restri
                 const int y = 2 * y0 + 4 * q + jj;
                 if (y >= sh) break;
                 unsigned o[4];
-#pragma unroll
-                for (int m = 0; m < 4; m++) {
-                    const int tl = rows[jj][m], tm = rows[jj][m + 1], tr = rows[jj][m + 2];
-                    const int ml = rows[jj + 1][m], mr = rows[jj + 1][m + 2];
-                    const int bl = rows[jj + 2][m], bm = rows[jj + 2][m + 1], br = rows[jj + 2][m + 2];
-                    const int ix = (3 * (tr + br) + 10 * mr) - (3 * (tl + bl) + 10 * ml);
-                    const int iy = 3 * ((br - tr) + (bl - tl)) + 10 * (bm - tm);
-                    o[m] = ((unsigned)(iy * (1 << kDerShift)) << 16) | ((unsigned)(ix * (1 << kDerShift)) & 0xFFFFu);
-                }
+                scharr_row(pr[jj], pr[jj + 1], pr[jj + 2], o);
                 uint32_t* dst = out + (size_t)y * op + x;
                 if (x + 3 < sw) {
                     if constexpr (NT) {
@@ -626,34 +661,19 @@ __device__ __forceinline__ void chain_store(const PyrDesc& P, const DerivDesc* d
             const int qq = k / NG, g = k - qq * NG;
             const int x = ox0 + 4 * g;
             if (x >= w || oy0 + 4 * qq >= h) continue;
-            int rows[6][6];
+            s16x2 pr[6][4];
 #pragma unroll
             for (int rr = 0; rr < 6; rr++) {
                 const uint8_t* trow = R + (HY + 4 * qq - 1 + rr) * PW + HX + 4 * g - 4;
-                const unsigned a0 = *reinterpret_cast<const unsigned*>(trow);
-                const unsigned a1 = *reinterpret_cast<const unsigned*>(trow + 4);
-                const unsigned a2 = *reinterpret_cast<const unsigned*>(trow + 8);
-                rows[rr][0] = a0 >> 24;
-                rows[rr][1] = a1 & 0xFF;
-                rows[rr][2] = (a1 >> 8) & 0xFF;
-                rows[rr][3] = (a1 >> 16) & 0xFF;
-                rows[rr][4] = a1 >> 24;
-                rows[rr][5] = a2 & 0xFF;
+                scharr_pairs(*reinterpret_cast<const unsigned*>(trow), *reinterpret_cast<const unsigned*>(trow + 4),
+                             *reinterpret_cast<const unsigned*>(trow + 8), pr[rr]);
             }
 #pragma unroll
             for (int jj = 0; jj < 4; jj++) {
                 const int y = oy0 + 4 * qq + jj;
                 if (y >= h) break;
                 unsigned o[4];
-#pragma unroll
-                for (int m = 0; m < 4; m++) {
-                    const int tl = rows[jj][m], tm = rows[jj][m + 1], tr = rows[jj][m + 2];
-                    const int ml = rows[jj + 1][m], mr = rows[jj + 1][m + 2];
-                    const int bl = rows[jj + 2][m], bm = rows[jj + 2][m + 1], br = rows[jj + 2][m + 2];
-                    const int ix = (3 * (tr + br) + 10 * mr) - (3 * (tl + bl) + 10 * ml);
-                    const int iy = 3 * ((br - tr) + (bl - tl)) + 10 * (bm - tm);
-                    o[m] = ((unsigned)(iy * (1 << kDerShift)) << 16) | ((unsigned)(ix * (1 << kDerShift)) & 0xFFFFu);
-                }
+                scharr_row(pr[jj], pr[jj + 1], pr[jj + 2], o);
                 uint32_t* d = out + (size_t)y * op + x;
                 if (x + 3 < w) {
                     *reinterpret_cast<uint4*>(d) = make_uint4(o[0], o[1], o[2], o[3]);
