@@ -261,7 +261,7 @@ __global__ __launch_bounds__(256) void fast_detect_q_kernel(FastDetBatch B, int 
     const int x0 = tile.x * FD_TX, y0 = tile.y * TY;
     const size_t seq = tile.z;
     __shared__ __attribute__((aligned(16))) uint8_t T[QIH][FD_IW];
-    __shared__ uint16_t SC[QSH][FD_SW + 2];  // bit 8: corner, low byte: score
+    __shared__ __attribute__((aligned(16))) uint16_t SC[QSH][FD_SW + 2];  // bit 8: corner, low byte: score
     __shared__ uint16_t CQ[4][QQ];
     __shared__ unsigned long long TM[TY];
     __shared__ unsigned long long RB[TY];
@@ -294,6 +294,11 @@ __global__ __launch_bounds__(256) void fast_detect_q_kernel(FastDetBatch B, int 
     const bool boxes = B.box_pts != nullptr;
     if (boxes && tid < TY) TM[tid] = ~0ull;
     if (tid < TY) RB[tid] = 0ull;
+    // score region rows cleared (dwords; before the barrier, away from the tests)
+    for (int k = tid; k < QSH * ((FD_SW + 2) / 2); k += 256) {
+        const int r = k / ((FD_SW + 2) / 2), c2 = k - r * ((FD_SW + 2) / 2);
+        *reinterpret_cast<uint32_t*>(&SC[r][2 * c2]) = 0u;
+    }
     __syncthreads();
     const int hi_t = threshold, lo_t = -threshold;
     // ---- A0: compass pre-test of this wave's rows sr = wv, wv + 4, ... (lane -> column
@@ -318,17 +323,20 @@ __global__ __launch_bounds__(256) void fast_detect_q_kernel(FastDetBatch B, int 
     {
         // columns 1 .. 64 (lane -> sc = lane + 1), unrolled over the rows: one LDS base
         // per lane (staged row sr, column sc), the five taps at immediate offsets,
-        // branch-free (every tap lies inside the staged tile)
+        // branch-free (every tap lies inside the staged tile). All rows' tests first
+        // (straight-line: the next rows' taps load while a row computes), then the
+        // queue writes.
+        constexpr int NRW = (QSH + 3) / 4;
         const int wvu = __builtin_amdgcn_readfirstlane(wv);
         const bool colok = x0 + lane >= 3 && x0 + lane < w - 3;
         const uint8_t* tb = &T[wvu][lane + 1];
-        uint16_t* sb0 = &SC[wvu][lane + 1];
+        unsigned long long bal[NRW];
+        unsigned cm = 0;
 #pragma unroll
-        for (int i = 0; i < (QSH + 3) / 4; i++) {
+        for (int i = 0; i < NRW; i++) {
             const int sr = wvu + 4 * i;
-            if (sr < QSH) {
-                sb0[i * 4 * (FD_SW + 2)] = 0;
-                if (lane < 2) SC[sr][lane * 65] = 0;
+            bal[i] = 0;
+            if (4 * i + 3 < QSH || sr < QSH) {  // (only the last row is not every wave's)
                 const uint8_t* t = tb + i * 4 * FD_IW;
                 const int v = t[3 * FD_IW + 3], hi = v + hi_t, lo = v + lo_t;
                 const int p8 = t[3], p0 = t[6 * FD_IW + 3], p12 = t[3 * FD_IW], p4 = t[3 * FD_IW + 6];
@@ -337,10 +345,14 @@ __global__ __launch_bounds__(256) void fast_detect_q_kernel(FastDetBatch B, int 
                 const bool bright = min(max(p0, p8), max(p4, p12)) > hi;
                 const bool dark = max(min(p0, p8), min(p4, p12)) < lo;
                 const bool cand = colok & rowok & (bright | dark);
-                const unsigned long long bal = __builtin_amdgcn_ballot_w64(cand);
-                if (cand) q[nq + rank_below(bal)] = (uint16_t)((sr << 7) | (lane + 1));
-                nq += __popcll(bal);
+                bal[i] = __builtin_amdgcn_ballot_w64(cand);
+                cm |= (unsigned)cand << i;
             }
+        }
+#pragma unroll
+        for (int i = 0; i < NRW; i++) {
+            if ((cm >> i) & 1u) q[nq + rank_below(bal[i])] = (uint16_t)(((wvu + 4 * i) << 7) | (lane + 1));
+            nq += __popcll(bal[i]);
         }
     }
     {
@@ -349,25 +361,27 @@ __global__ __launch_bounds__(256) void fast_detect_q_kernel(FastDetBatch B, int 
         const int sr = wv + 4 * (lane >> 1), sc = (lane & 1) * 65;
         pretest(sr, sc, lane < 2 * nr);
     }
-    // ---- A1: full segment test of the queue, compacted in place to the corners ----
+    // ---- A1: full segment test of the queue, compacted in place to the corners, and
+    // (NMS only) the corners' cornerScore from the same ring taps ----
     int nc = 0;
     for (int base = 0; base < nq; base += 64) {
         const int i = base + lane;
         bool corner = false;
-        int k = 0;
+        int k = 0, v = 0;
+        int ring[16];
         if (i < nq) {
             k = q[i];
             const int sr = k >> 7, sc = k & 127;
             const int ty = sr + 3, tx = sc + 3;
-            const int v = T[ty][tx];
+            v = T[ty][tx];
             // packed compare: low half r - (v + t + 1) (sign: not brighter), high half
             // r - (v - t) (sign: darker); sign bits gathered to bit q and 16 + q
             const fs16x2 th = {(short)(v + threshold + 1), (short)(v - threshold)};
             unsigned acc = 0;
 #pragma unroll
             for (int qq = 0; qq < 16; qq++) {
-                const int rv = T[ty + c_ring[qq][1]][tx + c_ring[qq][0]];
-                const fs16x2 r2 = {(short)rv, (short)rv};
+                ring[qq] = T[ty + c_ring[qq][1]][tx + c_ring[qq][0]];
+                const fs16x2 r2 = {(short)ring[qq], (short)ring[qq]};
                 const unsigned sg = as_u(r2 - th);
                 acc |= (sg >> (15 - qq)) & (0x00010001u << qq);
             }
@@ -376,23 +390,10 @@ __global__ __launch_bounds__(256) void fast_detect_q_kernel(FastDetBatch B, int 
         const unsigned long long bal = __builtin_amdgcn_ballot_w64(corner);
         if (corner) {
             const int sr = k >> 7, sc = k & 127;
-            SC[sr][sc] = 0x100;
+            SC[sr][sc] = (uint16_t)(0x100 | (nonmax ? corner_score16_pk(v, ring, threshold) : 0));
             q[nc + rank_below(bal)] = (uint16_t)k;  // index <= i: already read
         }
         nc += __popcll(bal);
-    }
-    // ---- B: cornerScore of the corners (NMS only) ----
-    if (nonmax) {
-        for (int i = lane; i < nc; i += 64) {
-            const int k = q[i];
-            const int sr = k >> 7, sc = k & 127;
-            const int ty = sr + 3, tx = sc + 3;
-            const int v = T[ty][tx];
-            int ring[16];
-#pragma unroll
-            for (int qq = 0; qq < 16; qq++) ring[qq] = T[ty + c_ring[qq][1]][tx + c_ring[qq][0]];
-            SC[sr][sc] = (uint16_t)(0x100 | corner_score16_pk(v, ring, threshold));
-        }
     }
     // tile mask from the previous frame's feature boxes
     if (boxes) {
