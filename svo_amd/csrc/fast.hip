@@ -294,10 +294,13 @@ __global__ __launch_bounds__(256) void fast_detect_q_kernel(FastDetBatch B, int 
     const bool boxes = B.box_pts != nullptr;
     if (boxes && tid < TY) TM[tid] = ~0ull;
     if (tid < TY) RB[tid] = 0ull;
-    // score region rows cleared (dwords; before the barrier, away from the tests)
-    for (int k = tid; k < QSH * ((FD_SW + 2) / 2); k += 256) {
-        const int r = k / ((FD_SW + 2) / 2), c2 = k - r * ((FD_SW + 2) / 2);
-        *reinterpret_cast<uint32_t*>(&SC[r][2 * c2]) = 0u;
+    // the wave's score region rows cleared (one dword per lane and row; before the
+    // barrier, away from the tests)
+    if (lane < (FD_SW + 2) / 2) {
+        uint32_t* sc0 = reinterpret_cast<uint32_t*>(&SC[wv][0]) + lane;
+#pragma unroll
+        for (int i = 0; i < (QSH + 3) / 4; i++)
+            if (4 * i + 3 < QSH || wv + 4 * i < QSH) sc0[i * 2 * (FD_SW + 2)] = 0u;
     }
     __syncthreads();
     const int hi_t = threshold, lo_t = -threshold;
@@ -361,27 +364,25 @@ __global__ __launch_bounds__(256) void fast_detect_q_kernel(FastDetBatch B, int 
         const int sr = wv + 4 * (lane >> 1), sc = (lane & 1) * 65;
         pretest(sr, sc, lane < 2 * nr);
     }
-    // ---- A1: full segment test of the queue, compacted in place to the corners, and
-    // (NMS only) the corners' cornerScore from the same ring taps ----
+    // ---- A1: full segment test of the queue, compacted in place to the corners ----
     int nc = 0;
     for (int base = 0; base < nq; base += 64) {
         const int i = base + lane;
         bool corner = false;
-        int k = 0, v = 0;
-        int ring[16];
+        int k = 0;
         if (i < nq) {
             k = q[i];
             const int sr = k >> 7, sc = k & 127;
             const int ty = sr + 3, tx = sc + 3;
-            v = T[ty][tx];
+            const int v = T[ty][tx];
             // packed compare: low half r - (v + t + 1) (sign: not brighter), high half
             // r - (v - t) (sign: darker); sign bits gathered to bit q and 16 + q
             const fs16x2 th = {(short)(v + threshold + 1), (short)(v - threshold)};
             unsigned acc = 0;
 #pragma unroll
             for (int qq = 0; qq < 16; qq++) {
-                ring[qq] = T[ty + c_ring[qq][1]][tx + c_ring[qq][0]];
-                const fs16x2 r2 = {(short)ring[qq], (short)ring[qq]};
+                const int rv = T[ty + c_ring[qq][1]][tx + c_ring[qq][0]];
+                const fs16x2 r2 = {(short)rv, (short)rv};
                 const unsigned sg = as_u(r2 - th);
                 acc |= (sg >> (15 - qq)) & (0x00010001u << qq);
             }
@@ -390,10 +391,24 @@ __global__ __launch_bounds__(256) void fast_detect_q_kernel(FastDetBatch B, int 
         const unsigned long long bal = __builtin_amdgcn_ballot_w64(corner);
         if (corner) {
             const int sr = k >> 7, sc = k & 127;
-            SC[sr][sc] = (uint16_t)(0x100 | (nonmax ? corner_score16_pk(v, ring, threshold) : 0));
+            SC[sr][sc] = 0x100;
             q[nc + rank_below(bal)] = (uint16_t)k;  // index <= i: already read
         }
         nc += __popcll(bal);
+    }
+    // ---- B: cornerScore of the corners (NMS only; a separate pass: a wave's queue
+    // may take two A1 passes, its corners rarely more than one) ----
+    if (nonmax) {
+        for (int i = lane; i < nc; i += 64) {
+            const int k = q[i];
+            const int sr = k >> 7, sc = k & 127;
+            const int ty = sr + 3, tx = sc + 3;
+            const int v = T[ty][tx];
+            int ring[16];
+#pragma unroll
+            for (int qq = 0; qq < 16; qq++) ring[qq] = T[ty + c_ring[qq][1]][tx + c_ring[qq][0]];
+            SC[sr][sc] = (uint16_t)(0x100 | corner_score16_pk(v, ring, threshold));
+        }
     }
     // tile mask from the previous frame's feature boxes
     if (boxes) {
