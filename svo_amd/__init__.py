@@ -291,6 +291,7 @@ class Context:
     def __init__(self, device: int = 0):
         L = lib()
         h = _vp()
+        self.device = device
         rc = L.svo_ctx_create(device, C.byref(h))
         if rc != 0:
             raise SvoError(f"svo_ctx_create(device={device}) failed: {rc} (no usable HIP device?)")

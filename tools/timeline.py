@@ -11,11 +11,13 @@ for r in csv.DictReader(open(f"{d}/run_kernel_trace.csv")):
     n = r["Kernel_Name"]
     m = re.search(r"([a-z_]+kernel)", n)
     short = m.group(1) if m else n.split("(")[0][-32:]
+    if short == "lk_multi_kernel":  # the temporal (21x21) and stereo (11x11) calls
+        short += "_21" if "21, 21" in n else "_11"
     rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), "K:" + short, r.get("Queue_Id", "")))
 for r in csv.DictReader(open(f"{d}/run_memory_copy_trace.csv")):
     rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), "C:" + r["Direction"][:24], r.get("Queue_Id", "")))
 rows.sort()
-lk = [x for x in rows if x[2].startswith("K:lk_multi")] or [x for x in rows if x[2].startswith("K:lk_")]
+lk = [x for x in rows if x[2].startswith("K:lk_multi_kernel_21")] or [x for x in rows if x[2].startswith("K:lk_")]
 # slices of one step launch their LKs together: step starts = LK starts > 100 us apart
 starts = [lk[0][0]]
 for x in lk[1:]:
