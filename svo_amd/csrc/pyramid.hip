@@ -346,7 +346,8 @@ __global__ __launch_bounds__(256) void pyr_scharr_kernel(const PyrDesc* __restri
             uint32_t v[NP];
 #pragma unroll
             for (int p = 0; p < NP; p++)
-                v[p] = *reinterpret_cast<const uint32_t*>(src + (size_t)(min(r0 + p * RP, FS_IH - 1) - r0) * s.pitch);
+                v[p] = *(const __attribute__((address_space(1))) uint32_t*)(src + (size_t)(min(r0 + p * RP, FS_IH - 1) - r0) *
+                                                                                   s.pitch);
             // (rows past the tile load and store its last row again, the same bytes:
             // no branch, so no wait between the loads)
 #pragma unroll
@@ -421,15 +422,16 @@ __global__ __launch_bounds__(256) void pyr_scharr_kernel(const PyrDesc* __restri
                 if (y >= sh) break;
                 unsigned o[4];
                 scharr_row(pr[jj], pr[jj + 1], pr[jj + 2], o);
-                uint32_t* dst = out + (size_t)y * op + x;
+                // global (not flat) stores: no LDS counter traffic behind them
+                __attribute__((address_space(1))) uint32_t* dst =
+                    (__attribute__((address_space(1))) uint32_t*)(out + (size_t)y * op + x);
                 if (x + 3 < sw) {
-                    if constexpr (NT) {
-                        typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
-                        const u32x4 v = {o[0], o[1], o[2], o[3]};
-                        __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(dst));
-                    } else {
-                        *reinterpret_cast<uint4*>(dst) = make_uint4(o[0], o[1], o[2], o[3]);
-                    }
+                    typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+                    const u32x4 v = {o[0], o[1], o[2], o[3]};
+                    if constexpr (NT)
+                        __builtin_nontemporal_store(v, (__attribute__((address_space(1))) u32x4*)dst);
+                    else
+                        *(__attribute__((address_space(1))) u32x4*)dst = v;
                 } else {
 #pragma unroll
                     for (int m = 0; m < 4; m++)
@@ -449,7 +451,7 @@ __global__ __launch_bounds__(256) void pyr_scharr_kernel(const PyrDesc* __restri
     const int c = tid & 63;
     const int x = x0 + c;
     if (x >= d.w) return;
-    uint8_t* __restrict__ dst = const_cast<uint8_t*>(d.data);
+    __attribute__((address_space(1))) uint8_t* dst = (__attribute__((address_space(1))) uint8_t*)d.data;
     const int r0 = (tid >> 6) * (PD_TY / 4);
     int hv[2 * (PD_TY / 4) + 3];
 #pragma unroll
@@ -674,9 +676,11 @@ __device__ __forceinline__ void chain_store(const PyrDesc& P, const DerivDesc* d
                 if (y >= h) break;
                 unsigned o[4];
                 scharr_row(pr[jj], pr[jj + 1], pr[jj + 2], o);
-                uint32_t* d = out + (size_t)y * op + x;
+                __attribute__((address_space(1))) uint32_t* d =
+                    (__attribute__((address_space(1))) uint32_t*)(out + (size_t)y * op + x);
                 if (x + 3 < w) {
-                    *reinterpret_cast<uint4*>(d) = make_uint4(o[0], o[1], o[2], o[3]);
+                    typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+                    *(__attribute__((address_space(1))) u32x4*)d = u32x4{o[0], o[1], o[2], o[3]};
                 } else {
 #pragma unroll
                     for (int m = 0; m < 4; m++)
