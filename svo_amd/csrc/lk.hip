@@ -27,6 +27,7 @@
 //    against the oracle's EXACT mode (OpenCV's own float accumulation order
 //    differs only by rounding of the sums).
 #include "common.hpp"
+#include "xcd_tile.hpp"
 
 #include <cfloat>
 #include <cstdlib>
@@ -107,6 +108,7 @@ struct LKDev {
     float eps2_lo, eps2_hi;  // float brackets of eps2 (see converged())
     int flags, want_err;
     float min_eig;
+    int xcd;  // lk_multi_kernel: blocks in XCD order (xcd_tile.hpp; SVO_LK_XCD=0: raster)
 };
 
 constexpr int JM = 3;  // margin (px) of the staged next-image region around the window
@@ -1119,9 +1121,12 @@ __global__ __launch_bounds__(64, MINW) void lk_multi_kernel(LKBatch B, LKDev p) 
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     const int lane = threadIdx.x & 63;
     const int g = lane / LPF, l = lane % LPF;
-    const int seq = blockIdx.y;
+    // in XCD order the blocks one XCD runs are consecutive features of one sequence
+    // (neighbouring windows: shared L2 lines) instead of every 8th block
+    const XcdTile tile = p.xcd ? xcd_tile() : XcdTile{(int)blockIdx.x, (int)blockIdx.y, 0};
+    const int seq = tile.y;
     const int n = B.counts ? B.counts[seq] : B.n;
-    const int pt0 = blockIdx.x * FPW;
+    const int pt0 = tile.x * FPW;
     if (pt0 >= n) return;
     const int pt = pt0 + g;
     const bool live = pt < n;
@@ -1451,6 +1456,13 @@ hipError_t launch_lk(const LKBatch& b, int nseq, int max_n, const LKParams& lp, 
     d.flags = lp.flags;
     d.want_err = lp.want_err;
     d.min_eig = lp.min_eig;
+    {
+        static const bool lk_xcd = [] {
+            const char* e = std::getenv("SVO_LK_XCD");
+            return !(e && e[0] == '0');
+        }();
+        d.xcd = lk_xcd ? 1 : 0;
+    }
     if (!lp.generic) {
         // four features per wave: the SAD error (flags 0 + want_err) stays on lk_fast_kernel
         const bool multi_ok = !(lp.want_err && !(lp.flags & SVO_LK_GET_MIN_EIGENVALS));
