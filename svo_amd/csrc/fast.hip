@@ -478,8 +478,9 @@ __global__ __launch_bounds__(64) void fast_box_filter_kernel(FastDetBatch B, int
     // one wave per 64 x 32 tile: the lanes first read the box ranges of the tile's
     // bands (one cell range per band), then take the boxes of all bands together
     constexpr int TY = 32;
-    const int x0 = blockIdx.x * FD_TX, y0 = blockIdx.y * TY;
-    const size_t seq = blockIdx.z;
+    const XcdTile tile = xcd_tile();  // (neighbouring tiles' band ranges and words on one L2)
+    const int x0 = tile.x * FD_TX, y0 = tile.y * TY;
+    const size_t seq = tile.z;
     __shared__ unsigned long long TM[TY];
     __shared__ int band_lo[64], band_end[64];  // box ranges of the tile's bands, concatenated
     const int lane = threadIdx.x;
@@ -533,7 +534,7 @@ __global__ __launch_bounds__(64) void fast_box_filter_kernel(FastDetBatch B, int
     }
     __syncthreads();
     if (lane < TY && y0 + lane < h) {
-        unsigned long long* word = B.bits + (seq * B.nseg + blockIdx.x) * (size_t)h + y0 + lane;
+        unsigned long long* word = B.bits + (seq * B.nseg + tile.x) * (size_t)h + y0 + lane;
         *word &= TM[lane];
     }
 }
@@ -637,10 +638,11 @@ __global__ __launch_bounds__(kScanBlock) void fast_scan_kernel(FastDetBatch B, i
 // score of a kept corner is recomputed from the image (few pixels)
 constexpr int kEmitRows = 8;  // rows per wave: the segment-major words of 8 rows share a line
 __global__ __launch_bounds__(64) void fast_emit_kernel(FastDetBatch B, int threshold, int nonmax) {
-    const size_t seq = blockIdx.y;
+    const XcdTile tile = xcd_tile();  // (neighbouring row groups' words on one L2)
+    const size_t seq = tile.y;
     const ImgLevel L = B.descs[seq].lv[0];
     const int h = L.h;
-    for (int y = blockIdx.x * kEmitRows; y < min(h, (int)(blockIdx.x + 1) * kEmitRows); y++) {
+    for (int y = tile.x * kEmitRows; y < min(h, (tile.x + 1) * kEmitRows); y++) {
         if (B.rowcnt[seq * h + y] == 0) continue;
         const int lane = threadIdx.x;
         int off = B.rowoff[seq * h + y];
