@@ -556,7 +556,8 @@ __device__ __forceinline__ void chain_build(const PyrDesc& P, uint8_t* lds, uint
     const int tid = threadIdx.x;
     const ImgLevel& L = P.lv[l];
     const int w = L.w, h = L.h;
-    const int gx = (int)blockIdx.x * Sh::OW(l) - Sh::hx(l), gy = (int)blockIdx.y * Sh::OH(l) - Sh::hy(l);
+    const XcdTile tile = xcd_tile();  // (the chain's tiles in XCD order, as pyr_scharr_kernel's)
+    const int gx = tile.x * Sh::OW(l) - Sh::hx(l), gy = tile.y * Sh::OH(l) - Sh::hy(l);
     uint8_t* __restrict__ R = lds + Sh::off(l);
     if constexpr (l == S) {
         constexpr int DW = RW / 4;
@@ -652,12 +653,13 @@ __device__ __forceinline__ void chain_store(const PyrDesc& P, const DerivDesc* d
     const int tid = threadIdx.x;
     const ImgLevel& L = P.lv[l];
     const int w = L.w, h = L.h;
-    const int ox0 = (int)blockIdx.x * OWl, oy0 = (int)blockIdx.y * OHl;
+    const XcdTile tile = xcd_tile();
+    const int ox0 = tile.x * OWl, oy0 = tile.y * OHl;
     const int ox1 = min(ox0 + OWl, w), oy1 = min(oy0 + OHl, h);
     const uint8_t* __restrict__ R = lds + Sh::off(l);
     if constexpr (SCHARR) {
-        uint32_t* __restrict__ out = ders[blockIdx.z].data[l];
-        const int op = ders[blockIdx.z].pitch[l];
+        uint32_t* __restrict__ out = ders[tile.z].data[l];
+        const int op = ders[tile.z].pitch[l];
         constexpr int NG = OWl / 4, NT = NG * (OHl / 4);
         for (int k = tid; k < NT; k += 256) {
             const int qq = k / NG, g = k - qq * NG;
@@ -724,7 +726,7 @@ __global__ __launch_bounds__(256) void pyr_chain_kernel(const PyrDesc* __restric
                                                         const DerivDesc* __restrict__ ders) {
     using Sh = ChainShape<C, SCHARR, S>;
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-    chain_all<C, SCHARR, S>(descs[blockIdx.z], ders, lds, reinterpret_cast<uint16_t*>(lds + Sh::off_h()),
+    chain_all<C, SCHARR, S>(descs[xcd_tile().z], ders, lds, reinterpret_cast<uint16_t*>(lds + Sh::off_h()),
                             std::make_integer_sequence<int, C - S + 1>{});
 }
 
