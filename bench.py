@@ -148,12 +148,41 @@ def allreduce_sum(dist, v: float) -> float:
     return float(t.item())
 
 
-def pmc_traffic(cfg_name: str, kernel_prefix: str, seqs: int = 0):  # substring of the demangled kernel name
-    """Per-launch HBM bytes of a kernel from the rocprofv3 PMC summary measured on
-    THIS config's workload (profiles/pmc_summary.json configs[cfg_name], written by
-    tools/pmc_summary.py --config), scaled from the sequences per launch it was
-    measured at (the source's --seq) to `seqs`; None when that config was not
-    measured."""
+def kernel_key(name: str):
+    """(bare name, template arguments) of a demangled kernel name as rocprofv3 lists it:
+    'void svo::pyr_chain_kernel<3, true, 2>' -> ('pyr_chain_kernel', ('3', 'true', '2'))."""
+    m = re.match(r"^(?:void\s+)?(?:[A-Za-z_]\w*::)*([A-Za-z_]\w*)\s*(?:<(.*)>)?", name.strip())
+    if not m:
+        return name, ()
+    targs = tuple(a.strip() for a in m.group(2).split(",")) if m.group(2) else ()
+    return m.group(1), targs
+
+
+def pmc_select(kernels: dict, name: str, targs=None):
+    """The one entry of a PMC summary's `kernels` whose bare name is `name` and whose
+    template arguments equal `targs` position by position (None in `targs` = any;
+    `targs` None = no constraint). Exact keys, not substrings: the left chain's
+    pyr_scharr_kernel<true, true, true> and the right pyramid's <true, false, true>
+    share every prefix. More than one match is an error (ambiguous selection)."""
+    hits = []
+    for k, v in kernels.items():
+        n, a = kernel_key(k)
+        if n != name:
+            continue
+        if targs is not None and (len(a) != len(targs) or any(t is not None and t != x for t, x in zip(targs, a))):
+            continue
+        hits.append((k, v))
+    if len(hits) > 1:
+        raise ValueError(f"PMC selection {name}<{targs}> is ambiguous: {[k for k, _ in hits]}")
+    return hits[0] if hits else (None, None)
+
+
+def pmc_traffic(cfg_name: str, name: str, seqs: int = 0, targs=None):
+    """Per-launch HBM bytes of one kernel instance (bare name + template arguments,
+    pmc_select) from the rocprofv3 PMC summary measured on THIS config's workload
+    (profiles/pmc_summary.json configs[cfg_name], written by tools/pmc_summary.py
+    --config), scaled from the sequences per launch it was measured at (the source's
+    --seq) to `seqs`; None when that config or instance was not measured."""
     path = os.path.join(ROOT, "profiles", "pmc_summary.json")
     try:
         with open(path) as f:
@@ -163,19 +192,18 @@ def pmc_traffic(cfg_name: str, kernel_prefix: str, seqs: int = 0):  # substring 
     c = d.get("configs", {}).get(cfg_name, {})
     m = re.search(r"--seq (\d+)", c.get("source", ""))
     scale = seqs / int(m.group(1)) if (m and seqs) else 1.0
-    for k, v in c.get("kernels", {}).items():
-        if kernel_prefix not in k or (kernel_prefix == "scharr_kernel" and "pyr_scharr" in k):
-            continue
-        # the left chain's kernels, not the right pyramid's instances of the same
-        # templates (pyr_scharr_kernel<NT, SCH = false>, pyr_chain_kernel<c, false, s>)
-        if kernel_prefix == "pyr_scharr_kernel" and ", false>" in k:
-            continue
-        if kernel_prefix == "pyr_chain_kernel" and ", false," in k:
-            continue
-        b = v.get("hbm_bytes_per_launch")
-        return None if b is None else int(b * scale)
-    return None
+    _, v = pmc_select(c.get("kernels", {}), name, targs)
+    b = None if v is None else v.get("hbm_bytes_per_launch")
+    return None if b is None else int(b * scale)
 
+
+# template arguments of the instances the rooflines price (pmc_select): the temporal
+# 21 x 21 LK (lk_multi_kernel<FPW 4, QJM 1, MINW 3, KKS 2, 21, 21, NR 7>; the stereo
+# 11 x 11 instance is <4, 1, 4, 1, 11, 11, 11>), the left pyramid's Scharr kernels
+# (second argument SCH = true; the right pyramid's instances have false there)
+LK_TEMPORAL_TARGS = ("4", "1", "3", "2", "21", "21", "7")
+PYR_LEFT_TARGS = (None, "true", None)
+CHAIN_LEFT_TARGS = (None, "true", None)
 
 VALU_PEAK_G = 256 * 4 * 2.4 / 2  # G wave64 VALU instructions/s: 256 CUs x 4 SIMD-32, 2 cycles each at 2.4 GHz
 
@@ -504,10 +532,10 @@ def main():
     # the 21x21 temporal call runs lk_multi_kernel<4, 1 (four features per wave)
     # unless SVO_LK_QUAD=0 (lk_fast_kernel, one per wave; svo_amd/csrc/lk.hip launch_lk)
     if os.environ.get("SVO_LK_QUAD", "1")[:1] == "0":
-        lk_name, lk_desc = "lk_fast_kernel<21, 21", "one feature per wave"
+        lk_name, lk_desc, lk_targs = "lk_fast_kernel<21, 21", "one feature per wave", ("21", "21", None)
     else:
-        lk_name, lk_desc = "lk_multi_kernel<4, 1", "four features per wave"
-    traffic = pmc_traffic(args.config, lk_name, Sq)
+        lk_name, lk_desc, lk_targs = "lk_multi_kernel<4, 1", "four features per wave", LK_TEMPORAL_TARGS
+    traffic = pmc_traffic(args.config, lk_name.split("<")[0], Sq, lk_targs)
     dominant = max(phases, key=lambda k: phases[k][0])
     # pyramid + Scharr of one new left frame per sequence per step (the launch
     # chain pyr_scharr_kernel x levels + the coarsest Scharr + borders)
@@ -525,12 +553,15 @@ def main():
     # derivatives, borders). Per level: c pyr_scharr + the coarsest scharr + borders.
     c_lev = max(ML, 3)
     if os.environ.get("SVO_PYR_FUSED", "1")[:1] == "0":
-        t_ps, t_sc, t_pad = (pmc_traffic(args.config, k, Sq) for k in ("pyr_scharr_kernel", "scharr_kernel",
-                                                                    "pad_batched_kernel"))
+        t_ps, t_sc, t_pad = (pmc_traffic(args.config, k, Sq, a) for k, a in
+                             (("pyr_scharr_kernel", PYR_LEFT_TARGS), ("scharr_kernel", None),
+                              ("pad_batched_kernel", None)))
         pyr_traffic = c_lev * t_ps + t_sc + t_pad if None not in (t_ps, t_sc, t_pad) else None
         pyr_kernels = "pyr_scharr_kernel x levels + scharr_kernel (coarsest) + pad_batched_kernel (borders)"
     else:
-        t_ps, t_ch = (pmc_traffic(args.config, k, Sq) for k in ("pyr_scharr_kernel", "pyr_chain_kernel"))
+        # the left chain (Scharr on): pyr_scharr_kernel<NT, true, XT> + pyr_chain_kernel<c, true, s>
+        t_ps = pmc_traffic(args.config, "pyr_scharr_kernel", Sq, PYR_LEFT_TARGS)
+        t_ch = pmc_traffic(args.config, "pyr_chain_kernel", Sq, CHAIN_LEFT_TARGS)
         pyr_traffic = (c_lev - 1) * t_ps + t_ch if None not in (t_ps, t_ch) else None
         pyr_kernels = (f"pyr_scharr_kernel x {c_lev - 1} (pyrDown + Scharr + the source level's border) + "
                        "pyr_chain_kernel (last two levels, their derivatives and borders)")
@@ -539,7 +570,7 @@ def main():
     # bytes = one read of each W x H u8 frame (one raster pass)
     fast_avg_s = fe.time_fast(Wm + K, 20) / 1e3 if hasattr(fe, "time_fast") else 0.0
     fast_bytes = Sq * W * H
-    fast_traffic = pmc_traffic(args.config, "fast_detect_q_kernel", Sq)
+    fast_traffic = pmc_traffic(args.config, "fast_detect_q_kernel", Sq)  # one instance per config
     single = None
     if not args.no_single and world == 1:
         fe1 = S.Frontend(ctx, S.FrontendConfig(W, H, scenes[0].K, n_seq=1, n_frames=T, n_features=N, max_level=ML))

@@ -293,12 +293,15 @@ int svo_oracle_lk(const uint8_t* prev, const uint8_t* next, int w, int h, int st
     if ((crit_type & SVO_ORACLE_TERM_EPS) == 0) epsilon = 0.01;
     else epsilon = epsilon < 0. ? 0. : epsilon > 10. ? 10. : epsilon;
     epsilon *= epsilon;
+    /* SVO_ORACLE_LEVEL_ITERS: iters_out holds (max_level + 1) x npts counts, one row per level */
+    const int per_level = (acc_mode & SVO_ORACLE_LEVEL_ITERS) != 0;
+    acc_mode &= ~SVO_ORACLE_LEVEL_ITERS;
 
     for (int i = 0; i < npts; i++) status[i] = 1;
-    if (iters_out) memset(iters_out, 0, sizeof(int) * (size_t)npts);
 
     int lw[32], lh[32];
     int ml = svo_oracle_pyramid_levels(w, h, win_w, win_h, max_level, lw, lh);
+    if (iters_out) memset(iters_out, 0, sizeof(int) * (size_t)npts * (per_level ? (size_t)(max_level + 1) : 1));
     size_t total = 0;
     for (int l = 0; l <= ml; l++) total += (size_t)lw[l] * lh[l];
     uint8_t* pp = (uint8_t*)malloc(total);
@@ -321,7 +324,8 @@ int svo_oracle_lk(const uint8_t* prev, const uint8_t* next, int w, int h, int st
 #pragma omp for schedule(dynamic, 64)
             for (int i = 0; i < npts; i++)
                 track_point(&I, &J, i, prev_xy, next_xy, status, err, win_w, win_h, max_count, epsilon,
-                            level, ml, flags, (float)min_eig_threshold, acc_mode, IWin, dIWin, iters_out);
+                            level, ml, flags, (float)min_eig_threshold, acc_mode, IWin, dIWin,
+                            iters_out && per_level ? iters_out + (size_t)level * npts : iters_out);
             free(IWin);
             free(dIWin);
         }

@@ -73,6 +73,8 @@ void svo_oracle_scharr(const uint8_t* src, int w, int h, int stride, int16_t* ds
  * All three use identical integer sampling; they differ only in the rounding of
  * the A/b sums (relative ~1e-7), which the tests bound far below 0.1 px. */
 enum { SVO_ORACLE_ACC_EXACT = 0, SVO_ORACLE_ACC_SCALAR = 1, SVO_ORACLE_ACC_SSE = 2 };
+/* or-ed into acc_mode: iters_out receives (max_level + 1) x npts per-level counts (row = level) */
+#define SVO_ORACLE_LEVEL_ITERS 0x100
 
 #define SVO_ORACLE_LK_GET_MIN_EIGENVALS 8   /* cv::OPTFLOW_LK_GET_MIN_EIGENVALS */
 #define SVO_ORACLE_LK_USE_INITIAL_FLOW  4   /* cv::OPTFLOW_USE_INITIAL_FLOW */

@@ -925,12 +925,35 @@ __global__ __launch_bounds__(256, MINW) void lk_fast_kernel(LKBatch B, LKDev p) 
 // Helpers of the four-features-per-wave kernel (lk_multi_kernel below).
 template <int CTRL>
 __device__ __forceinline__ int dpp_row_add(int v) {
-    return v + __builtin_amdgcn_update_dpp(0, v, CTRL, 0xf, 0xf, false);
+    // quad_perm / row_ror read a valid lane for every lane: bound_ctrl lets the
+    // compiler fold the move into one v_add_u32_dpp (no zero-initialised old value)
+    return v + __builtin_amdgcn_update_dpp(0, v, CTRL, 0xf, 0xf, true);
 }
 __device__ __forceinline__ int swz16_add(int v) {  // + lane ^ 16 (within 32-lane groups)
     return v + __builtin_amdgcn_ds_swizzle(v, 0x401f);
 }
-__device__ __forceinline__ float halves_lane_float(int h, int l) { return ((float)h * 65536.f + (float)l) * FLT_SCALE; }
+// float of the exact h * 2^16 + l (one rounding: the product is exact), NOT scaled by
+// FLT_SCALE -- the callers apply it (A) or fold it into 1 / det (b)
+__device__ __forceinline__ float halves_lane_float(int h, int l) { return __builtin_fmaf((float)h, 65536.f, (float)l); }
+
+// OpenCV's rounded bilinear weights (LKTrackerInvoker: iw00 = cvRound((1 - a)(1 - b)
+// 2^14), iw01, iw10, iw11 = 2^14 - the others), packed for v_dot2 as (w00 | w01 << 16,
+// w10 | w11 << 16). cvRound(p 2^14) for a float product p in [0, 1] is computed as
+// p + 768: that sum lies in [768, 1024), where the float grid is 2^-14, so the
+// addition rounds p to a multiple of 2^-14 with ties to even -- rint's rounding --
+// and the low mantissa bits then hold round(p 2^14) (768.f = 0x44400000 has zero
+// low bits). Fast-rate adds in place of rndne + cvt (both half-rate on gfx950).
+__device__ __forceinline__ unsigned wbits(float p) { return __float_as_uint(p + 768.f); }
+struct BiW {
+    unsigned W0, W1;
+};
+__device__ __forceinline__ BiW bilinear_weights(float a, float b) {
+    const float ia = 1.f - a, ib = 1.f - b;
+    const unsigned b00 = wbits(ia * ib), b01 = wbits(a * ib), b10 = wbits(ia * b);
+    // 2^14 - w00 - w01 - w10 with w = bits - 0x44400000, modulo 2^32 (w11 may be -1)
+    const unsigned w11 = (1u << W_BITS) + 3u * 0x44400000u - b00 - b01 - b10;
+    return {__builtin_amdgcn_perm(b01, b00, 0x05040100u), __builtin_amdgcn_perm(w11, b10, 0x05040100u)};
+}
 
 // 7 rows of one strip: I (x32) / Ix / Iy at the strip's pixels packed by row
 // pairs (4 pairs, the last closed by a zero row), accumulated into the A sums.
@@ -982,63 +1005,79 @@ __device__ __forceinline__ void strip_setup_c(const unsigned* P, const u32x2a4* 
     }
 }
 
-// A level's global loads of a wave are issued back to back (both features'
-// next-image staging dwords, both strips' prev pairs and derivative pairs), then
-// consumed. Staging: lanes own (row, dword) slots, LPR lanes per row (the last
-// one supplies the right pixel of the row's last pair), RPP rows per pass.
+// Staging geometry of a JRW x JRH pair region (JRW = 2 mod 4): each lane loads one
+// aligned dword of a row (LPR dwords cover the JRW + 1 pixels of a row, RPP rows
+// per pass) and writes the four pixel pairs it starts -- entries 4d .. 4d + 3, each
+// pixel scaled by 2^kJShift (<= 32640, int16) so that a bilinear J sum carries
+// CV_DESCALE(., W_BITS - 5) in its high 16 bits, packed by one permute -- as two
+// 8-byte stores (rows are JRW dwords apart: 8- but not 16-byte aligned). The pairs
+// take the next lane's dword for their right pixels (ds_bpermute). No store is
+// masked and nothing goes to a sink:
+//  * a row's last lane (d = LPR - 1) starts only entries JRW - 2, JRW - 1, from its
+//    own dword: its second store repeats its first (same address, same data --
+//    per-lane permute selectors and address);
+//  * lanes past the RPP x LPR slots, and rows past the region in the last pass,
+//    repeat a real slot (row RPP - 1, or row JRH - 1): same load, same neighbour
+//    (the bpermute source is the real slot's neighbour), same store.
+constexpr int kJShift = 7;
+static_assert(W_BITS - 5 + kJShift == 16, "J sums must carry their descaled value in bits 16..31");
+
 template <int JRW, int JRH>
-struct DualStageLoads {
-    static constexpr int LPR = JRW / 4 + 1, RPP = 64 / LPR, NPS = (JRH + RPP - 1) / RPP;
-    unsigned v[2][NPS];
+struct StageGeom {
+    static_assert(JRW % 4 == 2, "rows of 4k + 2 entries: the last lane starts two");
+    static constexpr int LPR = (JRW + 2) / 4, RPP = 64 / LPR, NPS = (JRH + RPP - 1) / RPP;
+    int lr, d;            // the slot this lane loads and writes (lanes past the slots repeat row RPP - 1)
+    int src;              // ds_bpermute byte address of the slot's neighbour
+    unsigned selx, sely;  // permute selectors of the second store's pairs
+    int hi;               // dword offset of the second store from the first (2, or 0 for the last lane)
+    __device__ __forceinline__ explicit StageGeom(int lane) {
+        const int l0 = lane / LPR;
+        lr = l0 < RPP ? l0 : RPP - 1;
+        d = lane - l0 * LPR;
+        src = (lr * LPR + d + 1) << 2;
+        const bool last = d == LPR - 1;
+        selx = last ? 0x0c010c00u : 0x0c030c02u;
+        sely = last ? 0x0c020c01u : 0x0c040c03u;
+        hi = last ? 0 : 2;
+    }
+    __device__ __forceinline__ int row(int q) const {
+        const int r = q * RPP + lr;
+        return r < JRH ? r : JRH - 1;
+    }
+    // entries of pass q's row into the region (its row r = row(q))
+    __device__ __forceinline__ void write(unsigned* region, int r, unsigned v) const {
+        const unsigned nv = (unsigned)__builtin_amdgcn_ds_bpermute(src, (int)v);
+        unsigned* p = region + r * JRW + 4 * d;
+        uint2 a, b;
+        a.x = __builtin_amdgcn_perm(nv, v, 0x0c010c00u) << kJShift;
+        a.y = __builtin_amdgcn_perm(nv, v, 0x0c020c01u) << kJShift;
+        b.x = __builtin_amdgcn_perm(nv, v, selx) << kJShift;
+        b.y = __builtin_amdgcn_perm(nv, v, sely) << kJShift;
+        *reinterpret_cast<uint2*>(p) = a;
+        *reinterpret_cast<uint2*>(p + hi) = b;
+    }
 };
 
-// The staged region (pixel columns xa .. xa + 4 * (JRW / 4 + 1) - 1 read as
-// dwords, rows y0 .. y0 + JRH - 1) lies inside the padded level.
+// The staged region (pixel columns xa .. xa + 4 LPR - 1 read as dwords, rows
+// y0 .. y0 + JRH - 1) lies inside the padded level.
 template <int JRW, int JRH>
 __device__ __forceinline__ bool region_in_pad(const ImgLevel& L, int xa, int y0) {
-    return xa >= -kPyrPad && y0 >= -kPyrPad && xa + 4 * (JRW / 4 + 1) <= L.w + kPyrPad &&
+    return xa >= -kPyrPad && y0 >= -kPyrPad && xa + 4 * StageGeom<JRW, JRH>::LPR <= L.w + kPyrPad &&
            y0 + JRH <= L.h + kPyrPad;
 }
 
-// One staged dword -> four pixel pairs (this lane's dword and the next lane's),
-// each pixel scaled by 2^kJShift (<= 32640, int16): the bilinear J sum then
-// carries CV_DESCALE(., W_BITS - 5) in its high 16 bits, packed by one permute.
-constexpr int kJShift = 7;
-static_assert(W_BITS - 5 + kJShift == 16, "J sums must carry their descaled value in bits 16..31");
-__device__ __forceinline__ void stage_write(unsigned* dst, unsigned v, int lane) {
-    const unsigned nv = (unsigned)__builtin_amdgcn_ds_bpermute((lane + 1) << 2, (int)v);
-    uint4 o;
-    o.x = __builtin_amdgcn_perm(nv, v, 0x0c010c00u) << kJShift;
-    o.y = __builtin_amdgcn_perm(nv, v, 0x0c020c01u) << kJShift;
-    o.z = __builtin_amdgcn_perm(nv, v, 0x0c030c02u) << kJShift;
-    o.w = __builtin_amdgcn_perm(nv, v, 0x0c040c03u) << kJShift;
-    *reinterpret_cast<uint4*>(dst) = o;
-}
-
-// stage_bf for padded levels (the region is known to lie inside the padding)
+// one group's region re-staged at (xa, y0) (inside the padding)
 template <int W, int H>
-__device__ __forceinline__ void stage_padded(unsigned* dst, unsigned* sink, const ImgLevel& L, int xa, int y0,
-                                             int lane) {
-    constexpr int LPR = W / 4 + 1, RPP = 64 / LPR, NP = (H + RPP - 1) / RPP;
-    const int lr = lane / LPR, d = lane - lr * LPR;
+__device__ __forceinline__ void stage_padded(unsigned* dst, const ImgLevel& L, int xa, int y0,
+                                             const StageGeom<W, H>& g) {
+    using G = StageGeom<W, H>;
     const gu8 base = pad_origin(L.data, L.pitch, kPyrPad, 1);
-    const unsigned o0 = (unsigned)(xa + kPyrPad + 4 * d) + (unsigned)(y0 + kPyrPad) * (unsigned)L.pitch;
-    const bool wr = d < W / 4 && lr < RPP;
-    unsigned* dpl = wr ? dst + 4 * d : sink;
-    const int dstride = wr ? W : 0;
-    unsigned v[NP];
+    const unsigned o0 = (unsigned)(xa + kPyrPad + 4 * g.d) + (unsigned)(y0 + kPyrPad) * (unsigned)L.pitch;
+    unsigned v[G::NPS];
 #pragma unroll
-    for (int q = 0; q < NP; q++) {
-        int r = q * RPP + lr;
-        r = r < H ? r : H - 1;
-        v[q] = ldg_off<unsigned>(base, o0 + (unsigned)r * (unsigned)L.pitch);
-    }
+    for (int q = 0; q < G::NPS; q++) v[q] = ldg_off<unsigned>(base, o0 + (unsigned)g.row(q) * (unsigned)L.pitch);
 #pragma unroll
-    for (int q = 0; q < NP; q++) {
-        int r = q * RPP + lr;
-        r = r < H ? r : H - 1;
-        stage_write(dpl + r * dstride, v[q], lane);
-    }
+    for (int q = 0; q < G::NPS; q++) g.write(dst, g.row(q), v[q]);
 }
 
 // ---------------------------------------------------------------------------
@@ -1051,18 +1090,28 @@ __device__ __forceinline__ void stage_padded(unsigned* dst, unsigned* sink, cons
 // the exact group reduction serve FPW features per instruction. Staged next-
 // image regions (margin QJM) for all FPW features share the wave's LDS slice.
 // Same exact integer sums and float solve as every other LK kernel.
-// JSTRIDE: the groups' regions lie JSTRIDE bytes apart, an odd multiple of 16
-// dwords. ds_read_b32 / ds_read2_b32 bank by (dword address) mod 32 over each
-// 32-lane half -- two groups, reading the same strip pattern at the same offsets
-// of their own regions: at a multiple of 32 dwords apart (JBYTES / 4 = 672 for
-// QJM = 1) every read of the pair collided (2-way: ~1,350 conflict cycles per
-// wave in SQ_LDS_BANK_CONFLICT), 16 banks apart they take disjoint halves.
+// Staged region of one group: JRW pair entries x JRH rows. Entry e of row r is the
+// pixel pair (x0 + e, x0 + e + 1) with x0 = jx0 & ~3 (the staging reads aligned
+// dwords), so an estimate inside the +-QJM margin reads entries up to
+// 3 + 2 QJM + WW - 1 and its pair partner: JRW = WW + 2 QJM + 3 entries, not rounded
+// up to a multiple of 4 (21 x 21: 26 x 24 entries, 2,496 B; rounding up to 28 cost
+// 192 B per group and, with the groups' padding, a wave per CU: 4 x 2,752 B held LK
+// at 14 waves per CU, 4 x 2,496 B + the sink admits 16).
+// JSTRIDE: the groups' regions lie JSTRIDE bytes apart, the smallest dword count >=
+// the region with (dwords mod 32) = 16. ds_read_b32 / ds_read2_b32 bank by (dword
+// address) mod 32 over each 32-lane half -- two groups, reading the same strip
+// pattern at the same offsets of their own regions: at a multiple of 32 dwords
+// apart every read of the pair collided (2-way), 16 banks apart they take disjoint
+// halves.
 template <int QJM, int WW = 21, int WH = 21>
 struct MultiShape {
-    static constexpr int JRW = ru4(WW + 2 * QJM + 3), JRH = WH + 1 + 2 * QJM;
+    static constexpr int JRW0 = WW + 2 * QJM + 3;                  // entries the margin needs
+    static constexpr int JRW = JRW0 + (6 - JRW0 % 4) % 4;          // rounded up to 4k + 2
+    static constexpr int JRH = WH + 1 + 2 * QJM;
     static constexpr int JBYTES = JRW * JRH * 4;
-    static constexpr int JSTRIDE = ((JBYTES / 4 + 16) / 32 * 32 + 16) * 4;
-    static_assert(JSTRIDE >= JBYTES && (JSTRIDE / 4) % 32 == 16, "group stride");
+    static constexpr int JSTRIDE = ((JBYTES / 4 + 15) / 32 * 32 + 16) * 4;
+    static_assert(JSTRIDE >= JBYTES && (JSTRIDE / 4) % 32 == 16 && JSTRIDE - JBYTES < 128, "group stride");
+    static_assert(JRW % 4 == 2 && JRW >= JRW0 && JRW < JRW0 + 4, "entries 4k + 2");
 };
 
 // Exact sums over the LPF lanes of each group (every lane receives its group's
@@ -1138,8 +1187,8 @@ __global__ __launch_bounds__(64, MINW) void lk_multi_kernel(LKBatch B, LKDev p) 
     const cpyr next = (cpyr)B.next + seq;
     const DerivDesc& dprev = B.dprev[seq];
     unsigned* jregs = reinterpret_cast<unsigned*>(lds);
-    unsigned* sink = reinterpret_cast<unsigned*>(lds + FPW * Q::JSTRIDE);
     const unsigned* jmine = jregs + g * (Q::JSTRIDE / 4);
+    const StageGeom<JRW, JRH> sg(lane);
 
     // the lane's strips: column, first row, LDS offset; slots past NSTRIP are dummies
     int scol[K], srow[K];
@@ -1188,19 +1237,18 @@ __global__ __launch_bounds__(64, MINW) void lk_multi_kernel(LKBatch B, LKDev p) 
         ny = nexty;
         prevx -= halfWx;
         prevy -= halfWy;
-        const int ipx = ufloor(prevx), ipy = ufloor(prevy);
-        const bool inb = !(ipx < -WW || ipx >= I.w || ipy < -WH || ipy >= I.h);
+        const float fpx = __builtin_floorf(prevx), fpy = __builtin_floorf(prevy);
+        const int ipx = (int)fpx, ipy = (int)fpy;
+        // ipx < -WW || ipx >= I.w || ipy < -WH || ipy >= I.h, one unsigned compare per axis
+        const bool inb = (unsigned)(ipx + WW) < (unsigned)(I.w + WW) && (unsigned)(ipy + WH) < (unsigned)(I.h + WH);
         if (!inb && level == 0 && live) {
             st = 0;
             errv = 0.f;
         }
         bool lact = live && inb;
-        const float a = prevx - ipx, b = prevy - ipy;
-        const int iw00 = uround((1.f - a) * (1.f - b) * (1 << W_BITS));
-        const int iw01 = uround(a * (1.f - b) * (1 << W_BITS));
-        const int iw10 = uround((1.f - a) * b * (1 << W_BITS));
-        const int iw11 = (1 << W_BITS) - iw00 - iw01 - iw10;
-        const unsigned IW0 = pack16(iw00, iw01), IW1 = pack16(iw10, iw11);
+        // a = prevPt.x - iprevPt.x: the float of the floor is the floor (|x| < 2^24)
+        const BiW iw = bilinear_weights(prevx - fpx, prevy - fpy);
+        const unsigned IW0 = iw.W0, IW1 = iw.W1;
 
         int jx0 = ufloor(nextx - halfWx) - QJM, jy0 = ufloor(nexty - halfWy) - QJM;
         int jxa = jx0 & ~3;
@@ -1211,8 +1259,7 @@ __global__ __launch_bounds__(64, MINW) void lk_multi_kernel(LKBatch B, LKDev p) 
             // branch-free reads (padded levels); an inactive group (or one whose
             // region lies beyond the padding: its first bounds test deactivates
             // it) stages and reads at the level origin, results unused
-            using SL = DualStageLoads<JRW, JRH>;
-            const int lr = lane / SL::LPR, d = lane - lr * SL::LPR;
+            using SL = StageGeom<JRW, JRH>;
             int xs[FPW], ys[FPW];
 #pragma unroll
             for (int f = 0; f < FPW; f++) {
@@ -1222,65 +1269,81 @@ __global__ __launch_bounds__(64, MINW) void lk_multi_kernel(LKBatch B, LKDev p) 
                 ys[f] = ok ? y0 : 0;
             }
             unsigned sv[FPW][SL::NPS];
-            const gu8 jbase = pad_origin(J.data, J.pitch, kPyrPad, 1);
+            // wave-uniform row bases (scalar adds) + one per-lane offset for every
+            // feature: 4d + (the lane's pass-0 row) * pitch; the last pass's rows are
+            // clamped to the region (per lane)
+            const gu8 jbase = pad_origin(J.data, J.pitch, kPyrPad, 1) + (size_t)kPyrPad * (J.pitch + 1);
+            const unsigned ol = 4u * (unsigned)sg.d + (unsigned)sg.row(0) * (unsigned)J.pitch;
+            const unsigned olast = 4u * (unsigned)sg.d + (unsigned)sg.row(SL::NPS - 1) * (unsigned)J.pitch;
 #pragma unroll
             for (int f = 0; f < FPW; f++) {
-                const unsigned o0 = (unsigned)(xs[f] + kPyrPad + 4 * d) + (unsigned)(ys[f] + kPyrPad) * (unsigned)J.pitch;
+                const gu8 fb = jbase + xs[f] + (ptrdiff_t)ys[f] * J.pitch;
 #pragma unroll
-                for (int q = 0; q < SL::NPS; q++) {
-                    int r = q * SL::RPP + lr;
-                    r = r < JRH ? r : JRH - 1;
-                    sv[f][q] = ldg_off<unsigned>(jbase, o0 + (unsigned)r * (unsigned)J.pitch);
-                }
+                for (int q = 0; q < SL::NPS; q++)
+                    sv[f][q] = q + 1 < SL::NPS ? ldg_off<unsigned>(fb + (size_t)q * SL::RPP * J.pitch, ol)
+                                               : ldg_off<unsigned>(fb, olast);
             }
             const int dpitch = dprev.pitch[level];
             const gu8 ibase = pad_origin(I.data, I.pitch, kPyrPad, 1);
             const gu8 dbase = pad_origin((const uint8_t*)dprev.data[level], dpitch, kDerPad, 4);
             const int sx = inb ? ipx : 0, sy = inb ? ipy : 0;
-            // strips KKS at a time: loads of a group in flight together
+            const auto load_strip = [&](int k, unsigned* P, u32x2a4* Dv) {
+                // per-lane offsets of the strip's first row; the rows by wave-uniform bases
+                const int x = sx + scol[k], y = sy + srow[k];
+                const unsigned oi = (unsigned)(x + kPyrPad) + (unsigned)(y + kPyrPad) * (unsigned)I.pitch;
+                const unsigned od = 4u * ((unsigned)(x + kDerPad) + (unsigned)(y + kDerPad) * (unsigned)dpitch);
 #pragma unroll
-            for (int k0 = 0; k0 < K; k0 += KKS) {
-                constexpr int KK = K >= KKS ? KKS : 1;
-                unsigned P[KK][NR + 1];
-                u32x2a4 D[KK][NR + 1];
-#pragma unroll
-                for (int kk = 0; kk < KK; kk++) {
-                    const int x = sx + scol[k0 + kk], y = sy + srow[k0 + kk];
-                    const unsigned oi = (unsigned)(x + kPyrPad) + (unsigned)(y + kPyrPad) * (unsigned)I.pitch;
-                    const unsigned od = 4u * ((unsigned)(x + kDerPad) + (unsigned)(y + kDerPad) * (unsigned)dpitch);
-#pragma unroll
-                    for (int r = 0; r <= NR; r++) {
-                        P[kk][r] = __builtin_amdgcn_perm(0u, (unsigned)ldg_off<u16a1>(ibase, oi + (unsigned)r * I.pitch),
-                                                         0x0c010c00u);
-                        D[kk][r] = ldg_off<u32x2a4>(dbase, od + 4u * (unsigned)r * (unsigned)dpitch);
-                    }
+                for (int r = 0; r <= NR; r++) {
+                    P[r] = __builtin_amdgcn_perm(0u, (unsigned)ldg_off<u16a1>(ibase + (size_t)r * I.pitch, oi),
+                                                 0x0c010c00u);
+                    Dv[r] = ldg_off<u32x2a4>(dbase + (size_t)r * 4 * dpitch, od);
                 }
-                if (k0 == 0) {
-                    const bool wr = d < JRW / 4 && lr < SL::RPP;
+            };
+            const auto write_staging = [&] {
 #pragma unroll
-                    for (int f = 0; f < FPW; f++) {
-                        unsigned* dpl = wr ? jregs + f * (Q::JSTRIDE / 4) + 4 * d : sink;
-                        const int dstride = wr ? JRW : 0;
+                for (int f = 0; f < FPW; f++)
 #pragma unroll
-                        for (int q = 0; q < SL::NPS; q++) {
-                            int r = q * SL::RPP + lr;
-                            r = r < JRH ? r : JRH - 1;
-                            stage_write(dpl + r * dstride, sv[f][q], lane);
-                        }
-                    }
+                    for (int q = 0; q < SL::NPS; q++) sg.write(jregs + f * (Q::JSTRIDE / 4), sg.row(q), sv[f][q]);
+            };
+            if constexpr (KKS == 0) {
+                // one strip ahead: strip k + 1's loads in flight while strip k is
+                // set up, and no further (the scheduling barriers keep the compiler
+                // from hoisting every strip's loads: 24 VGPRs per strip in flight)
+                unsigned P[2][NR + 1];
+                u32x2a4 Dv[2][NR + 1];
+                load_strip(0, P[0], Dv[0]);
+                write_staging();
+#pragma unroll
+                for (int k = 0; k < K; k++) {
+                    if (k + 1 < K) load_strip(k + 1, P[(k + 1) & 1], Dv[(k + 1) & 1]);
+                    __builtin_amdgcn_sched_barrier(0);
+                    strip_setup_c<NR>(P[k & 1], Dv[k & 1], IW0, IW1, sreal[k] ? IW0 : 0u, sreal[k] ? IW1 : 0u,
+                                      GX[k], GY[k], asum[0], asum[1], asum[2], csum[0], csum[1]);
+                    __builtin_amdgcn_sched_barrier(0);
                 }
+            } else {
+                // strips KKS at a time: loads of a group in flight together
 #pragma unroll
-                for (int kk = 0; kk < KK; kk++) {
-                    const int k = k0 + kk;
-                    strip_setup_c<NR>(P[kk], D[kk], IW0, IW1, sreal[k] ? IW0 : 0u, sreal[k] ? IW1 : 0u, GX[k],
-                                      GY[k], asum[0], asum[1], asum[2], csum[0], csum[1]);
+                for (int k0 = 0; k0 < K; k0 += KKS) {
+                    constexpr int KK = K >= KKS ? KKS : 1;
+                    unsigned P[KK][NR + 1];
+                    u32x2a4 Dv[KK][NR + 1];
+#pragma unroll
+                    for (int kk = 0; kk < KK; kk++) load_strip(k0 + kk, P[kk], Dv[kk]);
+                    if (k0 == 0) write_staging();
+#pragma unroll
+                    for (int kk = 0; kk < KK; kk++) {
+                        const int k = k0 + kk;
+                        strip_setup_c<NR>(P[kk], Dv[kk], IW0, IW1, sreal[k] ? IW0 : 0u, sreal[k] ? IW1 : 0u, GX[k],
+                                          GY[k], asum[0], asum[1], asum[2], csum[0], csum[1]);
+                    }
                 }
             }
         }
         wave_lds_sync();
         float A[3];
         group_sum_f<LPF, STEPS32>(asum, A);
-        const float A11 = A[0], A12 = A[1], A22 = A[2];
+        const float A11 = A[0] * FLT_SCALE, A12 = A[1] * FLT_SCALE, A22 = A[2] * FLT_SCALE;
 
         float D = A11 * A22 - A12 * A12;
         const float minEig =
@@ -1291,14 +1354,18 @@ __global__ __launch_bounds__(64, MINW) void lk_multi_kernel(LKBatch B, LKDev p) 
             lact = false;
         }
         D = 1.f / D;
+        // the b sums arrive unscaled: (A12 b2 s - A22 b1 s) D == (A12 b2 - A22 b1) (s D)
+        // exactly for s = FLT_SCALE (a power of two commutes with every rounding here)
+        const float Ds = D * FLT_SCALE;
 
         nextx -= halfWx;
         nexty -= halfWy;
         float pdx = 0.f, pdy = 0.f;
         for (int j = 0; j < p.max_count; j++) {
             if (__builtin_amdgcn_ballot_w64(lact) == 0) break;
-            const int inx = ufloor(nextx), iny = ufloor(nexty);
-            if (lact && (inx < -WW || inx >= J.w || iny < -WH || iny >= J.h)) {
+            const float fnx = __builtin_floorf(nextx), fny = __builtin_floorf(nexty);
+            const int inx = (int)fnx, iny = (int)fny;
+            if (lact && !((unsigned)(inx + WW) < (unsigned)(J.w + WW) && (unsigned)(iny + WH) < (unsigned)(J.h + WH))) {
                 if (level == 0) st = 0;
                 lact = false;
             }
@@ -1314,19 +1381,15 @@ __global__ __launch_bounds__(64, MINW) void lk_multi_kernel(LKBatch B, LKDev p) 
                 while (nb) {
                     const int f = (int)(__builtin_ctzll(nb) / LPF);
                     nb &= nb - 1;
-                    stage_padded<JRW, JRH>(jregs + f * (Q::JSTRIDE / 4), sink, J,
+                    stage_padded<JRW, JRH>(jregs + f * (Q::JSTRIDE / 4), J,
                                            __builtin_amdgcn_readlane(jxa, LPF * f),
-                                           __builtin_amdgcn_readlane(jy0, LPF * f), lane);
+                                           __builtin_amdgcn_readlane(jy0, LPF * f), sg);
                 }
                 wave_lds_sync();
             }
             itcount += lact ? 1 : 0;
-            const float aa = nextx - inx, bb = nexty - iny;
-            const int w00 = uround((1.f - aa) * (1.f - bb) * (1 << W_BITS));
-            const int w01 = uround(aa * (1.f - bb) * (1 << W_BITS));
-            const int w10 = uround((1.f - aa) * bb * (1 << W_BITS));
-            const int w11 = (1 << W_BITS) - w00 - w01 - w10;
-            const unsigned W0 = pack16(w00, w01), W1 = pack16(w10, w11);
+            const BiW w = bilinear_weights(nextx - fnx, nexty - fny);
+            const unsigned W0 = w.W0, W1 = w.W1;
             int bsum[2] = {-csum[0], -csum[1]};
             {
                 // an inactive group reads inside its own region (results unused)
@@ -1354,8 +1417,8 @@ __global__ __launch_bounds__(64, MINW) void lk_multi_kernel(LKBatch B, LKDev p) 
             float fb[2];
             group_sum_f<LPF, STEPS32>(bsum, fb);
             const float fb1 = fb[0], fb2 = fb[1];
-            const float dx = (A12 * fb2 - A22 * fb1) * D;
-            const float dy = (A12 * fb1 - A11 * fb2) * D;
+            const float dx = (A12 * fb2 - A22 * fb1) * Ds;
+            const float dy = (A12 * fb1 - A11 * fb2) * Ds;
             if (lact) {
                 nextx += dx;
                 nexty += dy;
@@ -1389,7 +1452,7 @@ hipError_t launch_multi(const LKBatch& b, int nseq, int max_n, const LKDev& d, h
     // (no grid_hint: a block owns FPW features and does not loop; blocks past a
     // sequence's count return at once)
     dim3 grid((max_n + FPW - 1) / FPW, nseq);
-    constexpr int lds_bytes = FPW * MultiShape<QJM, WW, WH>::JSTRIDE + 16;
+    constexpr int lds_bytes = FPW * MultiShape<QJM, WW, WH>::JSTRIDE;
     hipLaunchKernelGGL((lk_multi_kernel<FPW, QJM, MINW, KKS, WW, WH, NR>), grid, dim3(64), lds_bytes, st, b, d);
     return hipGetLastError();
 }
@@ -1471,7 +1534,21 @@ hipError_t launch_lk(const LKBatch& b, int nseq, int max_n, const LKParams& lp, 
             // estimate leaves it; measured 2.7 % faster alone than a 2-px margin
             // and than 3 px; two features per wave (lk_dual_kernel, another lane
             // map) measured slower and is gone: DESIGN.md)
-            return launch_multi<4, 1, 3>(b, nseq, max_n, d, st);
+            // SVO_LK_VARIANT (A/B only): MINW (waves per SIMD the registers are
+            // capped for) and KKS (strips loaded together in the setup)
+            static const int variant = [] {
+                const char* e = std::getenv("SVO_LK_VARIANT");
+                return e ? std::atoi(e) : 0;
+            }();
+            switch (variant) {
+                case 32: return launch_multi<4, 1, 3, 2>(b, nseq, max_n, d, st);
+                case 31: return launch_multi<4, 1, 3, 1>(b, nseq, max_n, d, st);
+                case 42: return launch_multi<4, 1, 4, 2>(b, nseq, max_n, d, st);
+                case 41: return launch_multi<4, 1, 4, 1>(b, nseq, max_n, d, st);
+                case 40: return launch_multi<4, 1, 4, 0>(b, nseq, max_n, d, st);
+                case 30: return launch_multi<4, 1, 3, 0>(b, nseq, max_n, d, st);
+                default: return launch_multi<4, 1, 3>(b, nseq, max_n, d, st);
+            }
         }
         // the stereo call's 11 x 11 (findLeftFeaturesInRight, no err): four
         // features per wave too, one 11-row strip per lane (11 of 16 lanes)

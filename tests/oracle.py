@@ -16,6 +16,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PATH = os.path.join(ROOT, "oracle", "build", "libsvo_oracle.so")
 
 ACC_EXACT, ACC_SCALAR, ACC_SSE = 0, 1, 2
+LEVEL_ITERS = 0x100  # oracle/svo_oracle.h SVO_ORACLE_LEVEL_ITERS
 TERM_COUNT, TERM_EPS = 1, 2
 LK_USE_INITIAL_FLOW, LK_GET_MIN_EIGENVALS = 4, 8
 
@@ -121,7 +122,9 @@ def scharr(img):
 
 
 def lk(prev, nxt, prev_pts, win=(21, 21), max_level=3, criteria=(3, 30, 0.01), flags=0, min_eig=1e-4,
-       acc=ACC_EXACT, next_pts=None, want_err=True):
+       acc=ACC_EXACT, next_pts=None, want_err=True, level_iters=False):
+    """cv::calcOpticalFlowPyrLK (oracle/lk.c). level_iters: iters is (max_level + 1, n), one row
+    per pyramid level (GN iterations of each point at that level), instead of the per-point sum."""
     prev = _c(prev, np.uint8)
     nxt = _c(nxt, np.uint8)
     h, w = prev.shape
@@ -130,10 +133,11 @@ def lk(prev, nxt, prev_pts, win=(21, 21), max_level=3, criteria=(3, 30, 0.01), f
     npts = np.zeros((n, 2), np.float32) if next_pts is None else _c(next_pts, np.float32).reshape(-1, 2).copy()
     st = np.zeros(n, np.uint8)
     err = np.zeros(n, np.float32)
-    iters = np.zeros(n, np.int32)
+    iters = np.zeros((max_level + 1, n) if level_iters else n, np.int32)
     load().svo_oracle_lk(_p(prev, _u8p), _p(nxt, _u8p), w, h, w, _p(pp, _f32p), _p(npts, _f32p), _p(st, _u8p),
                          _p(err, _f32p) if want_err else None, n, win[0], win[1], max_level, criteria[0],
-                         criteria[1], criteria[2], flags, min_eig, acc, _p(iters, _i32p))
+                         criteria[1], criteria[2], flags, min_eig, acc | (LEVEL_ITERS if level_iters else 0),
+                         _p(iters, _i32p))
     return npts, st, err, iters
 
 

@@ -13,7 +13,7 @@
 #   mix TAG [BENCH_ARGS]    SQ instruction mix per wave of every step kernel
 #                           (mix TAG --cmd CMD..: of any command's kernels)
 #   lksplit                 LK VALU / time with the iteration cap at 1, 2, 50
-#   lkab "V1 V2 .."         standalone LK kernel time per SVO_LK_MULTI variant
+#   lkab "V1 V2 .."         standalone LK kernel time per SVO_LK_VARIANT (lk.hip launch_lk)
 #   lkmem [LIB ..]          LK memory-pipeline + issue counters (TA, TCP, SQ), per library build
 #   ab VAR "V1 V2" [RUNS]   bench A/B of an environment switch
 #   abcfg VAR "V1 V2"       the same A/B at the 1080p, 4K and KITTI configs
@@ -155,9 +155,9 @@ P
 run_lkab() {
     for v in ${1:-41}; do
         local T=/tmp/lkab_$v
-        SVO_LK_MULTI=$v timeout -k 10 120 rocprofv3 --kernel-trace --stats -d $T -o run --output-format csv -- \
+        SVO_LK_VARIANT=$v timeout -k 10 120 rocprofv3 --kernel-trace --stats -d $T -o run --output-format csv -- \
             python tools/microbench.py lk --points 128000 --reps 5 > $T.log 2>&1 || fail lkab $T.log
-        echo "== SVO_LK_MULTI=$v"
+        echo "== SVO_LK_VARIANT=$v"
         python3 - $T <<'P'
 import csv, glob, sys
 f = glob.glob(sys.argv[1] + '/**/*kernel_stats.csv', recursive=True)[0]

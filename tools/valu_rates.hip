@@ -58,6 +58,16 @@ PROBE(p_max3_u32, "v_max3_u32 %0, %1, %2, %0")
 PROBE(p_bfe, "v_bfe_u32 %0, %1, 8, 8")
 PROBE(p_and_or, "v_and_or_b32 %0, %1, %2, %0")
 PROBE(p_cndmask, "v_cndmask_b32 %0, %1, %0, vcc")
+PROBE(p_dot2_u32_u16, "v_dot2_u32_u16 %0, %1, %2, %0")
+PROBE(p_pk_mad_i16, "v_pk_mad_i16 %0, %1, %2, %0")
+PROBE(p_mad_i32_i16, "v_mad_i32_i16 %0, %1, %2, %0")
+PROBE(p_mad_i32_i24, "v_mad_i32_i24 %0, %1, %2, %0")
+PROBE(p_mul_u32_u24, "v_mul_u32_u24 %0, %1, %0")
+PROBE(p_alignbyte, "v_alignbyte_b32 %0, %1, %0, %2")
+PROBE(p_pk_sub_i16, "v_pk_sub_i16 %0, %1, %0")
+PROBE(p_add_f32, "v_add_f32 %0, %1, %0")
+PROBE(p_cvt_i32_f32, "v_cvt_i32_f32 %0, %0")
+PROBE(p_rndne_f32, "v_rndne_f32 %0, %0")
 
 typedef void (*probe_t)(unsigned long long*, unsigned*, int);
 
@@ -73,7 +83,10 @@ int main() {
              {"v_pk_mad_u16", p_pk_mad_u16}, {"v_pk_add_u16", p_pk_add_u16}, {"v_dot2_f32_f16", p_dot2_f32_f16},
              {"v_cvt_f32_i32", p_cvt_f32_i32}, {"v_add_u32_dpp", p_add_dpp}, {"v_mov_b32_dpp", p_mov_dpp},
              {"v_sad_u8", p_sad_u8},       {"v_msad_u8", p_msad_u8},       {"v_max3_u32", p_max3_u32},
-             {"v_bfe_u32", p_bfe},         {"v_and_or_b32", p_and_or},     {"v_cndmask_b32", p_cndmask}};
+             {"v_bfe_u32", p_bfe},         {"v_and_or_b32", p_and_or},     {"v_cndmask_b32", p_cndmask},
+             {"v_dot2_u32_u16", p_dot2_u32_u16}, {"v_pk_mad_i16", p_pk_mad_i16}, {"v_mad_i32_i16", p_mad_i32_i16}, {"v_mad_i32_i24", p_mad_i32_i24},
+             {"v_mul_u32_u24", p_mul_u32_u24}, {"v_alignbyte_b32", p_alignbyte}, {"v_pk_sub_i16", p_pk_sub_i16},
+             {"v_add_f32", p_add_f32}, {"v_cvt_i32_f32", p_cvt_i32_f32}, {"v_rndne_f32", p_rndne_f32}};
     const int blocks = 1024, iters = 2000;  // 1024 x 4 waves = 4 waves per SIMD on 256 CUs
     unsigned long long* cyc;
     unsigned* sink;
