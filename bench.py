@@ -344,6 +344,72 @@ def forward_workload(S, SceneForward, ctx, W, H, N, ML, Sq, K, Wm, threads):
             "scene": "SceneForward: 0.04 m/frame forward (ping-pong), occluder at 8 m sliding 22 px/frame"}
 
 
+def stream_workload(S, Scene, ctx, W, H, N, ML, Sq, K, Wm, threads, bgr, Kmat, pairs=None):
+    """Ingest inside the timed window (the reference's loader hands each frame to
+    Tracking as it is read, R:include/async_image_loader.h:36-69): the headline's
+    loop, but every step's stereo pairs travel over PCIe -- svo_frontend_queue_frames:
+    page-locked host frames, asynchronous H2D on the front end's upload stream into a
+    4-slot ring, level 0 written by the batched ingest kernel (grey copy, or
+    cv::cvtColor(BGR2GRAY) on the device when bgr) -- frame t + 2 queued before step
+    t, overlapped with the step. 16 distinct sequences (the headline's first 16, or
+    rendered) fill the Sq slots; every slot gets its own copy (Sq x 2 images per
+    step cross the link). Also reported: the same uploads alone, back to back (the
+    link + conversion ceiling)."""
+    n_dist = min(Sq, 16)
+    T = Wm + K + 3  # frames 0 .. Wm + K + 2 (frame t + 2 queued before step t)
+    if pairs is None:
+        scs = [Scene(W, H, seed=sequence_seeds(0, n_dist)[i]) for i in range(n_dist)]
+        P = min(T, 2 * scs[0].period)
+        pairs = [[(sc.frame(t), sc.right(t)) for t in range(P)] for sc in scs]
+    P = min(T, len(pairs[0]))
+    shape = (P, n_dist, H, W, 3) if bgr else (P, n_dist, H, W)
+    pl, pr = S.PinnedBuffer(shape), S.PinnedBuffer(shape)
+    for p in range(P):
+        for d in range(n_dist):
+            a, b = pairs[d][p]
+            # BGR with equal channels: its grey is the frame itself (the tracking is
+            # the grey run's; the conversion's arithmetic runs all the same)
+            pl.array[p, d] = a[..., None] if bgr else a
+            pr.array[p, d] = b[..., None] if bgr else b
+
+    def queue(fe, t):
+        fe.queue_frames(t, [pl.array[t % P, s % n_dist] for s in range(Sq)],
+                        [pr.array[t % P, s % n_dist] for s in range(Sq)])
+
+    K_img = Sq * 2 * W * H * (3 if bgr else 1)  # bytes over the link per step
+    fe = S.Frontend(ctx, S.FrontendConfig(W, H, Kmat, n_seq=Sq, n_frames=4, n_features=N, max_level=ML,
+                                          host_threads=threads, timing=0))
+    # the link + conversion alone: 8 uploads back to back before init (no step reads the ring yet)
+    for t in range(2):
+        queue(fe, t)
+    fe.upload_wait(1)
+    t1 = time.perf_counter()
+    for t in range(8):
+        queue(fe, t)
+    fe.upload_wait(7)
+    alone = 8 * K_img / (time.perf_counter() - t1) / 1e9
+    print(f"[bench] stream {'bgr' if bgr else 'grey'}: uploads alone {alone:.1f} GB/s", file=sys.stderr, flush=True)
+    for t in range(3):
+        queue(fe, t)
+    fe.init(0)
+    for t in range(1, Wm + 1):
+        queue(fe, t + 2)
+        fe.step(t)
+    t1 = time.perf_counter()
+    for t in range(Wm + 1, Wm + K + 1):
+        queue(fe, t + 2)
+        fe.step(t)
+    fe.synchronize()
+    dt = time.perf_counter() - t1
+    fe.close()
+    pl.close()
+    pr.close()
+    return {"value": round(Sq * K / dt, 2), "unit": "frames/s", "ms_per_step": round(dt / K * 1e3, 4),
+            "steps": K, "warmup": Wm, "input": "BGR 8UC3" if bgr else "grey",
+            "h2d_bytes_per_step": K_img, "h2d_GBps_in_loop": round(K_img * K / dt / 1e9, 2),
+            "h2d_GBps_alone": round(alone, 2), "distinct_sequences": n_dist, "ring_slots": 4}
+
+
 def orb_workload(S, SceneForward, ctx, W, H, ML, Sq, K, Wm, threads):
     """The reference's shipped configuration (R:configs/config.yaml:15,19-27): ORB
     keyframe detector (150 features, scale 1.2, 8 levels, HARRIS), Tracking::nextFrame's
@@ -403,6 +469,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-single", action="store_true")
     ap.add_argument("--no-orb", action="store_true", help="skip the shipped-config (ORB, reference keyframe rule) workload")
+    ap.add_argument("--no-stream", action="store_true",
+                    help="skip the streamed-ingest workloads (frames over PCIe inside the window, grey and BGR)")
     ap.add_argument("--no-bucketed", action="store_true",
                     help="skip the second measurement with bucketed selection in the loop")
     ap.add_argument("--scene", default="rot", choices=("rot", "forward"),
@@ -572,6 +640,7 @@ def main():
     fast_bytes = Sq * W * H
     fast_traffic = pmc_traffic(args.config, "fast_detect_q_kernel", Sq)  # one instance per config
     single = None
+    print("[bench] timed window done; side measurements", file=sys.stderr, flush=True)
     if not args.no_single and world == 1:
         fe1 = S.Frontend(ctx, S.FrontendConfig(W, H, scenes[0].K, n_seq=1, n_frames=T, n_features=N, max_level=ML))
         for t in range(T):
@@ -611,13 +680,22 @@ def main():
         feb.close()
     forward = None
     if not args.no_forward and args.scene == "rot" and world == 1:
+        print("[bench] forward / occluder workload", file=sys.stderr, flush=True)
         if not all_pairs:
             fe.close()
         forward = forward_workload(S, SceneForward, ctx, W, H, N, ML, Sq, K, Wm, args.threads)
     orb = None
     if not args.no_orb and args.scene == "rot" and world == 1:
+        print("[bench] shipped ORB configuration workload", file=sys.stderr, flush=True)
         fe.close()  # (idempotent)
         orb = orb_workload(S, SceneForward, ctx, W, H, ML, Sq, K, Wm, args.threads)
+    stream = None
+    if not args.no_stream and args.scene == "rot" and world == 1:
+        print("[bench] streamed-ingest workloads (grey, BGR)", file=sys.stderr, flush=True)
+        fe.close()
+        firsts = all_pairs[:16] if all_pairs else None
+        stream = {kind: stream_workload(S, Scene, ctx, W, H, N, ML, Sq, K, Wm, args.threads, kind == "bgr",
+                                        scenes[0].K, firsts) for kind in ("grey", "bgr")}
     out = {
         "metric": "frames/sec @1241x376, 2000 feats; LK iters/sec; achieved HBM GB/s",
         "value": round(fps, 2),
@@ -639,7 +717,7 @@ def main():
         "achieved_GBps_algorithmic": round(frames * frame_bytes(W, H, N, ML) / dt_max / 1e9, 2),
         "single_stream_fps": round(single, 2) if single else None,
         "bucketed": bucketed,
-        "workloads": {"forward": forward, "orb_reference": orb},
+        "workloads": {"forward": forward, "orb_reference": orb, "stream": stream},
         "phase_ms_per_step": {k: round(v[0] / K, 4) for k, v in phases.items()},
         "stats_per_step": {k: round(v / K, 3) for k, v in tot.items()},
         "step_ms": {"mean": round(float(np.mean(step_s)) * 1e3, 4),
@@ -692,6 +770,7 @@ def main():
         },
     }
     if not args.no_cpu_baseline and world == 1:  # rank 0 at N = 1 only
+        print("[bench] CPU baseline (oracle loop)", file=sys.stderr, flush=True)
         out["cpu_baseline"] = cpu_baseline(args.config, args.cpu_seconds)
     print(json.dumps(out), flush=True)
 

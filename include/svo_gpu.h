@@ -318,7 +318,11 @@ typedef struct svo_frontend_stats {
     int64_t full_copy;          /* 1: the full point copy was waited for (long RANSAC / n <= 5) */
     int64_t kf_overflow;        /* SVO_KF_REFERENCE: masked corners a keyframe left out for
                                    lack of capacity (n_features); 0 = every corner taken,
-                                   as extractFeatures (R:src/tracking.cpp:74-92) */
+                                   as extractFeatures (R:src/tracking.cpp:74-92); with use_orb
+                                   it includes the ORB keypoints its detector dropped at the
+                                   candidate capacity */
+    double host_ms_orb;         /* use_orb: the keyframe's ORB detection (device stages and the
+                                   host's retainBest, synchronous on the FAST stream) */
 } svo_frontend_stats;
 
 int svo_frontend_create(svo_ctx* ctx, const svo_frontend_config* cfg, svo_frontend** out);
@@ -330,6 +334,24 @@ int svo_frontend_set_frame(svo_frontend* fe, int seq, int t, const uint8_t* left
 /* Same from BGR 8UC3 frames (svo_image_upload_bgr's conversion). */
 int svo_frontend_set_frame_bgr(svo_frontend* fe, int seq, int t, const uint8_t* left_bgr,
                                const uint8_t* right_bgr, int stride);
+/* Streamed frames (R:include/async_image_loader.h:36-69: the loader hands each
+ * stereo pair to Tracking as it arrives; here a whole step's worth at once):
+ * queue frame t of every sequence -- left[s] / right[s] (grey, or BGR 8UC3 when
+ * bgr != 0: cv::cvtColor(BGR2GRAY) on the device), rows `stride` bytes apart --
+ * as asynchronous H2D copies on the front end's upload stream into ring slot
+ * t % n_frames, converted into level 0 there; frame t's pyramid builds wait for
+ * it. Returns at once: the host buffers must stay untouched until
+ * svo_frontend_upload_wait(fe, t) (page-locked memory, svo_pinned_alloc, gives
+ * full PCIe rate; sequences whose buffers follow each other in memory go in one
+ * copy). Ring discipline (n_frames >= 4): before init, any frame; after it,
+ * frame t is queued before step t - 2 is called (t >= last step + 3) and no
+ * earlier than step t - n_frames + 1 returned (t <= last step + n_frames - 1):
+ * a loop queues frames 0 .. 2, calls init(0), then queue(t + 2), step(t). */
+int svo_frontend_queue_frames(svo_frontend* fe, int t, const uint8_t* const* left, const uint8_t* const* right,
+                              int stride, int bgr);
+int svo_frontend_upload_wait(svo_frontend* fe, int t);
+int svo_pinned_alloc(size_t bytes, void** out);
+void svo_pinned_free(void* p);
 /* Build every resident frame's pyramid now (else each step builds its own). */
 int svo_frontend_prebuild_pyramids(svo_frontend* fe);
 /* First keyframe: FAST (+bucket) on frame t0 of every sequence, map points. */

@@ -128,6 +128,10 @@ _SIGS = [
     ("svo_frontend_scharr_level", C.c_int, [_vp, C.c_int, C.c_int, C.c_int, C.POINTER(C.c_int16),
                                             C.POINTER(C.c_int16), C.c_int]),
     ("svo_frontend_prebuild_pyramids", C.c_int, [_vp]),
+    ("svo_frontend_queue_frames", C.c_int, [_vp, C.c_int, C.POINTER(_u8p), C.POINTER(_u8p), C.c_int, C.c_int]),
+    ("svo_frontend_upload_wait", C.c_int, [_vp, C.c_int]),
+    ("svo_pinned_alloc", C.c_int, [C.c_size_t, C.POINTER(_vp)]),
+    ("svo_pinned_free", None, [_vp]),
     ("svo_frontend_init", C.c_int, [_vp, C.c_int]),
     ("svo_frontend_step", C.c_int, [_vp, C.c_int, _vp]),
     ("svo_frontend_synchronize", C.c_int, [_vp]),
@@ -163,6 +167,34 @@ def solve_pnp_sqpnp(obj, img_pts, K):
     if rc < 0:
         raise SvoError(f"svo_solve_pnp_sqpnp: error {rc}")
     return rc == 1, rv, tv
+
+
+class PinnedBuffer:
+    """Page-locked host memory (svo_pinned_alloc) viewed as a numpy array: the
+    source of svo_frontend_queue_frames' H2D copies at full PCIe rate. Freed by
+    close() or when the object goes away (the array view must not outlive it)."""
+
+    def __init__(self, shape, dtype=np.uint8):
+        dtype = np.dtype(dtype)
+        nbytes = int(np.prod(shape)) * dtype.itemsize
+        p = _vp()
+        if lib().svo_pinned_alloc(nbytes, C.byref(p)) != 0 or not p.value:
+            raise SvoError(f"svo_pinned_alloc({nbytes}) failed")
+        self._p = p
+        buf = (C.c_uint8 * nbytes).from_address(p.value)
+        self.array = np.frombuffer(buf, dtype=dtype, count=int(np.prod(shape))).reshape(shape)
+
+    def close(self):
+        if getattr(self, "_p", None) is not None and self._p.value:
+            self.array = None
+            lib().svo_pinned_free(self._p)
+            self._p = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # noqa: BLE001  (interpreter shutdown)
+            pass
 
 
 def pool_selftest(threads=8, jobs=2000):
@@ -583,7 +615,7 @@ class FrontendStats(C.Structure):
                 ("host_ms_wait_post", C.c_double), ("host_ms_wait_score", C.c_double),
                 ("host_ms_wait_kf", C.c_double), ("host_ms_enqueue", C.c_double), ("host_ms_step", C.c_double),
                 ("ransac_rounds", C.c_int64), ("max_hypotheses", C.c_int64), ("serial_keyframe", C.c_int64),
-                ("full_copy", C.c_int64), ("kf_overflow", C.c_int64)]
+                ("full_copy", C.c_int64), ("kf_overflow", C.c_int64), ("host_ms_orb", C.c_double)]
 
     def as_dict(self):
         return {k: (float(getattr(self, k)) if k.startswith("host_") else int(getattr(self, k)))
@@ -619,6 +651,27 @@ class Frontend:
 
     def prebuild_pyramids(self):
         self.ctx._check(lib().svo_frontend_prebuild_pyramids(self.handle))
+
+    def queue_frames(self, t, lefts, rights):
+        """svo_frontend_queue_frames: frame t of every sequence from host arrays
+        (lefts[s], rights[s]: (h, w) grey or (h, w, 3) BGR, all of one shape), queued
+        as asynchronous H2D copies (see include/svo_gpu.h for the ring discipline).
+        The arrays must stay alive and unchanged until upload_wait(t)."""
+        S = self.cfg.n_seq
+        if len(lefts) != S or len(rights) != S:
+            raise SvoError("queue_frames: one left and one right image per sequence")
+        a0 = lefts[0]
+        bgr = a0.ndim == 3
+        for a in list(lefts) + list(rights):
+            if a.shape != a0.shape or a.dtype != np.uint8 or not a.flags["C_CONTIGUOUS"]:
+                raise SvoError("queue_frames: C-contiguous uint8 images of one shape")
+        L = (_u8p * S)(*[a.ctypes.data_as(_u8p) for a in lefts])
+        R = (_u8p * S)(*[a.ctypes.data_as(_u8p) for a in rights])
+        stride = a0.shape[1] * (3 if bgr else 1)
+        self.ctx._check(lib().svo_frontend_queue_frames(self.handle, int(t), L, R, stride, int(bgr)))
+
+    def upload_wait(self, t):
+        self.ctx._check(lib().svo_frontend_upload_wait(self.handle, int(t)))
 
     def init(self, t0=0):
         self.ctx._check(lib().svo_frontend_init(self.handle, t0))

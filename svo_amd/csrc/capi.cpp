@@ -597,4 +597,21 @@ int svo_triangulate_points(svo_ctx* ctx, const float P1[12], const float P2[12],
     return SVO_OK;
 }
 
+// Page-locked host memory for frames streamed with svo_frontend_queue_frames
+// (the reference's loader thread would decode into it: an H2D from pageable
+// memory is staged through a driver bounce buffer at a fraction of the rate).
+int svo_pinned_alloc(size_t bytes, void** out) {
+    if (!out || bytes == 0) return SVO_ERR_ARG;
+    *out = nullptr;
+    if (hipHostMalloc(out, bytes, hipHostMallocDefault) != hipSuccess) {
+        *out = nullptr;
+        return SVO_ERR_HIP;
+    }
+    return SVO_OK;
+}
+
+void svo_pinned_free(void* p) {
+    if (p) (void)hipHostFree(p);
+}
+
 }  // extern "C"

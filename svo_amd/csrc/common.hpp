@@ -92,6 +92,10 @@ hipError_t launch_bgr_to_gray(const uint8_t* bgr, int bpitch, uint8_t* dst, int 
 // H2D of a host BGR image through the context's pinned double buffer and its
 // grey conversion into `level0` (w x h, row pitch `pitch`), on ctx->stream.
 int ingest_bgr(svo_ctx* ctx, const uint8_t* bgr, int stride, int w, int h, uint8_t* level0, int pitch);
+// level 0 of S sequences (descs[s].lv[0]) from a staging block [S][h][spitch]
+// (grey bytes, or BGR converted as launch_bgr_to_gray)
+hipError_t launch_ingest_batched(const uint8_t* stage, size_t seq_stride, int spitch, const PyrDesc* descs, int S,
+                                 int w, int h, bool bgr, hipStream_t st);
 hipError_t launch_pyramid_batched(const PyrDesc* d_descs, int nseq, int w, int h, int nlevels,
                                   hipStream_t st);
 

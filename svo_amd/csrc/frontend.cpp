@@ -419,6 +419,17 @@ struct svo_frontend {
     int64_t phase_n[kPhases] = {0};
     std::vector<std::pair<int, int>> pending;  // (phase, event pair index)
     int ev_used = 0;
+    // streamed frames (svo_frontend_queue_frames): pinned H2D of a step's stereo
+    // pairs on their own stream into a device staging block (double-buffered by
+    // frame parity), the conversion kernel into level 0 of the frame's ring slot;
+    // the pyramid builds of that frame wait for ev_up[slot]
+    hipStream_t st_up = nullptr;
+    uint8_t* up_stage = nullptr;       // [2 parity][2 side][S x up_cap]: the host frames' bytes
+    size_t up_cap = 0;                 // staging bytes per sequence (the widest h * stride seen)
+    size_t up_seq = 0;                 // h * stride of the last queued frame (sequence stride in staging)
+    std::vector<hipEvent_t> ev_up;     // [T] conversion of the slot's frame done
+    std::vector<int> up_t;             // [T] frame last streamed into the slot (-1: none)
+    int stepped = -1;                  // last completed step (init: t0); -1 before init
 };
 
 namespace {
@@ -1115,6 +1126,13 @@ void svo_frontend_destroy(svo_frontend* fe) {
                          fe->ev_pyr_r_b[1], fe->ev_pre, fe->ev_fdone, fe->ev_full_b[0], fe->ev_full_b[1]})
         if (e) (void)hipEventDestroy(e);
     if (fe->score_map) (void)hipFree(fe->score_map);
+    if (fe->st_up) {
+        (void)hipStreamSynchronize(fe->st_up);
+        (void)hipStreamDestroy(fe->st_up);
+    }
+    for (hipEvent_t e : fe->ev_up)
+        if (e) (void)hipEventDestroy(e);
+    if (fe->up_stage) (void)hipFree(fe->up_stage);
     orb_batch_destroy(fe->orb);
     if (fe->fit_work) (void)hipFree(fe->fit_work);
     delete fe;
@@ -1125,7 +1143,8 @@ void svo_frontend_destroy(svo_frontend* fe) {
 // change (new frames, re-init).
 static int fe_drain(svo_frontend* fe) {
     svo_ctx* ctx = fe->ctx;
-    for (hipStream_t st : {fe->st_lk, fe->st_fast, fe->st_copy, ctx->stream}) SVO_HIP(ctx, hipStreamSynchronize(st));
+    for (hipStream_t st : {fe->st_lk, fe->st_fast, fe->st_copy, ctx->stream, fe->st_up})
+        if (st) SVO_HIP(ctx, hipStreamSynchronize(st));
     fe->front_t = -1;
     fe->spec_t = -1;
     return SVO_OK;
@@ -1141,6 +1160,7 @@ static int fe_set_frame(svo_frontend* fe, int seq, int t, const uint8_t* left, c
     if (fe->pyr_ready >= 0 && fe->pyr_ready % fe->T == t) fe->pyr_ready = -1;  // built from the old image
     if (fe->pre_t >= 0 && fe->pre_t % fe->T == t) fe->pre_t = -1;  // detected on the old image
     if (fe->pyr_r_ready >= 0 && fe->pyr_r_ready % fe->T == t) fe->pyr_r_ready = -1;
+    if (!fe->up_t.empty()) fe->up_t[t] = -1;  // (the drain above finished any streamed upload)
     for (int side = 0; side < 2; side++) {
         svo_image* im = (side ? fe->frames_r : fe->frames)[(size_t)seq * fe->T + t];
         const uint8_t* px = side ? right : left;
@@ -1166,9 +1186,88 @@ int svo_frontend_set_frame_bgr(svo_frontend* fe, int seq, int t, const uint8_t* 
     return fe_set_frame(fe, seq, t, left_bgr, right_bgr, stride, true);
 }
 
+// The pyramid builds of frame f (context stream) wait for its streamed upload.
+static int fe_wait_upload(svo_frontend* fe, int f, hipStream_t st) {
+    if (!fe->up_t.empty() && fe->up_t[f % fe->T] == f) SVO_HIP(fe->ctx, hipStreamWaitEvent(st, fe->ev_up[f % fe->T], 0));
+    return SVO_OK;
+}
+
+// Frame f can be built ahead: resident frames are 0 .. n_frames - 1 (a caller
+// that reuses slots with set_frame gets no ahead-builds past them); once frames
+// are streamed (queue_frames), the ring holds the frames queued into it.
+static bool fe_has_frame(const svo_frontend* fe, int f) {
+    if (fe->up_t.empty()) return f < fe->T;
+    return fe->up_t[f % fe->T] == f;
+}
+
+int svo_frontend_queue_frames(svo_frontend* fe, int t, const uint8_t* const* left, const uint8_t* const* right,
+                              int stride, int bgr) {
+    if (!fe || t < 0 || !left || !right || stride < (bgr ? 3 : 1) * fe->W) return SVO_ERR_ARG;
+    svo_ctx* ctx = fe->ctx;
+    const int S = fe->S, T = fe->T, W = fe->W, H = fe->H;
+    if (T < 4) return set_error(ctx, SVO_ERR_ARG, "svo_frontend_queue_frames: needs a ring of n_frames >= 4");
+    for (int s = 0; s < S; s++)
+        if (!left[s] || !right[s]) return SVO_ERR_ARG;
+    // ring discipline: frame t's pyramid is built at the end of step t - 2, so it is
+    // queued before that step (t >= stepped + 3); its slot's previous frame t - T is
+    // no longer read once step t - T + 1 returned (t <= stepped + T - 1)
+    if (fe->stepped >= 0 && (t < fe->stepped + 3 || t > fe->stepped + T - 1))
+        return set_error(ctx, SVO_ERR_ARG, "svo_frontend_queue_frames: frame outside the ring window "
+                                           "(stepped + 3 .. stepped + n_frames - 1)");
+    if (!fe->st_up) {
+        SVO_HIP(ctx, hipStreamCreateWithFlags(&fe->st_up, hipStreamNonBlocking));
+        fe->ev_up.assign(T, nullptr);
+        for (auto& e : fe->ev_up) SVO_HIP(ctx, hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        fe->up_t.assign(T, -1);
+    }
+    // the staging block mirrors the host frames (rows `stride` apart, sequences
+    // H rows apart): a run of sequences whose buffers follow each other in memory
+    // is one contiguous H2D copy; grown (after the queued uploads) for a wider stride
+    const size_t seq_bytes = (size_t)H * stride;
+    if (seq_bytes > fe->up_cap) {
+        SVO_HIP(ctx, hipStreamSynchronize(fe->st_up));
+        if (fe->up_stage) SVO_HIP(ctx, hipFree(fe->up_stage));
+        fe->up_stage = nullptr;
+        fe->up_cap = seq_bytes;
+        SVO_HIP(ctx, hipMalloc(&fe->up_stage, 4 * (size_t)S * fe->up_cap));
+    }
+    fe->up_seq = seq_bytes;  // (the conversion of earlier queued frames captured their own stride)
+    const int slot = t % T;
+    const size_t last_row = (size_t)(bgr ? 3 : 1) * W;  // bytes of a frame's last row (no stride padding after it)
+    uint8_t* stage = fe->up_stage + (size_t)(t & 1) * 2 * S * fe->up_cap;
+    for (int side = 0; side < 2; side++) {
+        const uint8_t* const* src = side ? right : left;
+        uint8_t* dst = stage + (size_t)side * S * fe->up_cap;
+        for (int s0 = 0; s0 < S;) {
+            int s1 = s0 + 1;
+            while (s1 < S && src[s1] == src[s1 - 1] + seq_bytes) s1++;
+            const size_t n = (size_t)(s1 - s0 - 1) * fe->up_seq + (size_t)(H - 1) * stride + last_row;
+            SVO_HIP(ctx, hipMemcpyAsync(dst + (size_t)s0 * fe->up_seq, src[s0], n, hipMemcpyHostToDevice, fe->st_up));
+            s0 = s1;
+        }
+        const PyrDesc* d = (side ? fe->d_desc_r : fe->d_desc) + (size_t)slot * S;
+        SVO_HIP(ctx, launch_ingest_batched(dst, fe->up_seq, stride, d, S, W, H, bgr != 0, fe->st_up));
+    }
+    SVO_HIP(ctx, hipEventRecord(fe->ev_up[slot], fe->st_up));
+    fe->up_t[slot] = t;
+    // anything built ahead from the slot's previous frame is stale
+    if (fe->pyr_ready == t) fe->pyr_ready = -1;
+    if (fe->pyr_r_ready == t) fe->pyr_r_ready = -1;
+    if (fe->pre_t == t) fe->pre_t = -1;
+    return SVO_OK;
+}
+
+int svo_frontend_upload_wait(svo_frontend* fe, int t) {
+    if (!fe || t < 0) return SVO_ERR_ARG;
+    if (fe->up_t.empty() || fe->up_t[t % fe->T] != t) return SVO_OK;
+    SVO_HIP(fe->ctx, hipEventSynchronize(fe->ev_up[t % fe->T]));
+    return SVO_OK;
+}
+
 int svo_frontend_prebuild_pyramids(svo_frontend* fe) {
     if (!fe) return SVO_ERR_ARG;
     for (int t = 0; t < fe->T; t++) {
+        if (!fe->up_t.empty() && fe->up_t[t] >= 0) SVO_HIP(fe->ctx, hipStreamWaitEvent(fe->ctx->stream, fe->ev_up[t], 0));
         SVO_HIP(fe->ctx, launch_pyramid_batched(fe->d_desc + (size_t)t * fe->S, fe->S, fe->W, fe->H, fe->nlev,
                                                 fe->ctx->stream));
         SVO_HIP(fe->ctx, launch_pyramid_batched(fe->d_desc_r + (size_t)t * fe->S, fe->S, fe->W, fe->H, fe->nlev,
@@ -1197,6 +1296,10 @@ int svo_frontend_init(svo_frontend* fe, int t0) {
     for (int s = 0; s < S; s++) fe->h_target[s] = fe->cfg.n_features;
     std::fill(fe->kf_prev.begin(), fe->kf_prev.end(), 1);
     const PyrDesc* dcur = fe->d_desc + (size_t)(t0 % fe->T) * S;
+    {
+        int rw = fe_wait_upload(fe, t0, ctx->stream);
+        if (rw) return rw;
+    }
     SVO_HIP(ctx, launch_pyramid_scharr_batched(dcur, fe->d_der + (size_t)(t0 % 3) * S, S, fe->W, fe->H, fe->nlev,
                                                ctx->stream));
     SVO_HIP(ctx, launch_pyramid_batched(fe->d_desc_r + (size_t)(t0 % fe->T) * S, S, fe->W, fe->H, fe->nlev,
@@ -1215,6 +1318,7 @@ int svo_frontend_init(svo_frontend* fe, int t0) {
     SVO_HIP(ctx, hipStreamSynchronize(ctx->stream));
     ph_collect(fe);
     std::fill(fe->pose.begin(), fe->pose.end(), 0.0);
+    fe->stepped = t0;
     return SVO_OK;
 }
 
@@ -1287,6 +1391,9 @@ static int fe_front(svo_frontend* fe, int t) {
 static int fe_front_lk(svo_frontend* fe, int t) {
     svo_ctx* ctx = fe->ctx;
     hipStream_t st0 = ctx->stream;
+    // (resident frames: the caller keeps slot t % n_frames current, set_frame)
+    if (!fe->up_t.empty() && (!fe_has_frame(fe, t) || !fe_has_frame(fe, t - 1)))
+        return set_error(ctx, SVO_ERR_ARG, "svo_frontend_step: frame %d is not in the ring (queue_frames)", t);
     const int S = fe->S;
     const PyrDesc* dcur = fe->d_desc + (size_t)(t % fe->T) * S;
     int slot;
@@ -1310,6 +1417,8 @@ static int fe_front_lk(svo_frontend* fe, int t) {
     //    t is the prev image of the next step; OpenCV recomputes it per call),
     //    normally built ahead by the previous step's front half
     if (fe->pyr_ready != t) {
+        int rw = fe_wait_upload(fe, t, st0);
+        if (rw) return rw;
         ph_begin(fe, PH_PYR, st0, &slot);
         SVO_HIP(ctx, launch_pyramid_scharr_batched(dcur, fe->d_der + (size_t)(t % 3) * S, S, fe->W, fe->H, fe->nlev,
                                                    st0));
@@ -1368,6 +1477,8 @@ static int fe_front_rest(svo_frontend* fe, int t) {
     //    image), normally built ahead in the previous step (6b); the stereo LK of
     //    frame t waits for ev_pyr_r_b[t & 1]
     if (fe->pyr_r_ready != t) {
+        int rw = fe_wait_upload(fe, t, st0);
+        if (rw) return rw;
         ph_begin(fe, PH_PYR_R, st0, &slot);
         SVO_HIP(ctx, launch_pyramid_batched(fe->d_desc_r + (size_t)(t % fe->T) * S, S, fe->W, fe->H, fe->nlev, st0));
         ph_end(fe, st0, slot);
@@ -1385,7 +1496,7 @@ static int fe_front_rest(svo_frontend* fe, int t) {
     //    derivative pyramids are triple-buffered (frame f in f % 3), so nothing
     //    this step reads is overwritten, and the memory-bound pyramid shares the
     //    GPU with the VALU-bound LK instead of the post-LK window
-    if (t + 1 < fe->T) return fe_queue_next_image(fe, t + 1);
+    if (fe_has_frame(fe, t + 1)) return fe_queue_next_image(fe, t + 1);
     return SVO_OK;
 }
 
@@ -1397,6 +1508,8 @@ static int fe_queue_next_image(svo_frontend* fe, int tn) {
     const int S = fe->S;
     int slot;
     {
+        int rw = fe_wait_upload(fe, tn, st0);
+        if (rw) return rw;
         const PyrDesc* dnext = fe->d_desc + (size_t)(tn % fe->T) * S;
         ph_begin(fe, PH_PYR, st0, &slot);
         SVO_HIP(ctx, launch_pyramid_scharr_batched(dnext, fe->d_der + (size_t)(tn % 3) * S, S, fe->W, fe->H,
@@ -1464,7 +1577,7 @@ int svo_frontend_step(svo_frontend* fe, int t, svo_frontend_stats* stats) {
         return std::chrono::duration<double, std::milli>(clk::now() - t0).count();
     };
     const auto t_call = clk::now();
-    double ms_enqueue = 0, ms_wait_post = 0, ms_wait_score = 0, ms_wait_kf = 0;
+    double ms_enqueue = 0, ms_wait_post = 0, ms_wait_score = 0, ms_wait_kf = 0, ms_orb = 0;
     int64_t rounds = 0;
 
     if (fe->front_t != t) {
@@ -1714,8 +1827,10 @@ int svo_frontend_step(svo_frontend* fe, int t, svo_frontend_stats* stats) {
         bool any = false;
         for (int s = 0; s < S; s++) any |= fe->h_target[s] > 0;
         if (any) {
+            const auto to = clk::now();
             rc = fe_orb_detect(fe, t, true, sf);
             if (rc) return rc;
+            ms_orb += ms_since(to);
         } else {
             SVO_HIP(ctx, hipMemsetAsync(fe->kn, 0, sizeof(int) * S, sf));
         }
@@ -1755,13 +1870,16 @@ int svo_frontend_step(svo_frontend* fe, int t, svo_frontend_stats* stats) {
     // first (the keyframe -> LK hand-off is on the critical path), then the
     // binning of these features as the next frame's mask boxes (FAST stream,
     // ahead of the next step's FAST) and the rest of the first half
-    if (t + 1 < fe->T) {
+    // (streamed frames: the next frame was queued before this step, or the next
+    // step finds it missing and fails loudly in its own first half)
+    const bool next_ok = fe_has_frame(fe, t + 1);
+    if (next_ok) {
         rc = fe_front_lk(fe, t + 1);
         if (rc) return rc;
     }
     SVO_HIP(ctx, launch_box_bin(fe_fast_batch(fe, dcur, true), S, fe->W, fe->H, sf));
     fe->boxes_binned = true;
-    if (t + 1 < fe->T) {
+    if (next_ok) {
         rc = fe_front_rest(fe, t + 1);
         if (rc) return rc;
         fe->front_t = t + 1;
@@ -1807,9 +1925,13 @@ int svo_frontend_step(svo_frontend* fe, int t, svo_frontend_stats* stats) {
         // corner left out for lack of capacity (n_features) is a deviation
         int64_t over = 0;
         if (c.keyframe_rule == SVO_KF_REFERENCE)
-            for (int s = 0; s < S; s++) over += fe->h_target[s] > 0 ? fe->h_over[s] : 0;
+            for (int s = 0; s < S; s++)
+                if (fe->h_target[s] > 0)  // a keyframe: this step's detection ran (ORB: orb_over)
+                    over += fe->h_over[s] + (fe->orb ? fe->orb_over[s] : 0);
         stats->kf_overflow = over;
+        stats->host_ms_orb = ms_orb;
     }
+    fe->stepped = t;
     return SVO_OK;
 }
 

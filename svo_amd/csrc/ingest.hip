@@ -51,4 +51,55 @@ hipError_t launch_bgr_to_gray(const uint8_t* bgr, int bpitch, uint8_t* dst, int 
     return hipGetLastError();
 }
 
+
+// Streamed frames (svo_frontend_queue_frames): level 0 of every sequence's slot
+// from a device staging block that mirrors the host frames byte for byte (rows
+// `spitch` bytes apart, sequences `seq_stride` apart: one contiguous H2D copy per
+// run of sequences -- a pitched 2D copy moves row by row, ~0.1 GB/s at KITTI's
+// 1241-byte rows). BGR: the conversion above; grey: a copy. The rows need not be
+// 4-byte aligned (1241, 3723 B): unaligned dword loads (global memory allows
+// them). Grid (quads / 256, h, S); each sequence's level 0 from the descriptor
+// array (its borders are the pyramid chain's to write).
+typedef uint32_t u32a1 __attribute__((aligned(1)));
+template <bool BGR>
+__global__ void __launch_bounds__(256) ingest_batched_kernel(const uint8_t* __restrict__ stage, size_t seq_stride,
+                                                             int spitch, const PyrDesc* __restrict__ descs, int w,
+                                                             int h) {
+    const int s = blockIdx.z, y = blockIdx.y;
+    const int x = (blockIdx.x * 256 + threadIdx.x) * 4;
+    if (x >= w) return;
+    const ImgLevel L = descs[s].lv[0];
+    const uint8_t* src = stage + (size_t)s * seq_stride + (size_t)y * spitch + (size_t)x * (BGR ? 3 : 1);
+    uint8_t* d = const_cast<uint8_t*>(L.data) + (size_t)y * L.pitch + x;
+    if (x + 4 <= w) {
+        uint32_t out;
+        const u32a1* s4 = reinterpret_cast<const u32a1*>(src);
+        if (BGR) {
+            const uint32_t a = s4[0], b = s4[1], c = s4[2];
+            out = gray_of(a & 255, (a >> 8) & 255, (a >> 16) & 255) |
+                  gray_of(a >> 24, b & 255, (b >> 8) & 255) << 8 |
+                  gray_of((b >> 16) & 255, b >> 24, c & 255) << 16 |
+                  gray_of((c >> 8) & 255, (c >> 16) & 255, c >> 24) << 24;
+        } else {
+            out = s4[0];
+        }
+        *reinterpret_cast<uint32_t*>(d) = out;  // (level 0 rows are 64-byte aligned at x = 0)
+    } else {
+        for (int i = 0; x + i < w; i++)
+            d[i] = BGR ? (uint8_t)gray_of(src[3 * i], src[3 * i + 1], src[3 * i + 2]) : src[i];
+    }
+}
+
+hipError_t launch_ingest_batched(const uint8_t* stage, size_t seq_stride, int spitch, const PyrDesc* descs, int S,
+                                 int w, int h, bool bgr, hipStream_t st) {
+    if (w <= 0 || h <= 0 || S <= 0 || spitch < (bgr ? 3 : 1) * w) return hipErrorInvalidValue;
+    dim3 grid(((w + 3) / 4 + 255) / 256, h, S);
+    if (bgr)
+        hipLaunchKernelGGL(ingest_batched_kernel<true>, grid, dim3(256), 0, st, stage, seq_stride, spitch, descs, w, h);
+    else
+        hipLaunchKernelGGL(ingest_batched_kernel<false>, grid, dim3(256), 0, st, stage, seq_stride, spitch, descs, w,
+                           h);
+    return hipGetLastError();
+}
+
 }  // namespace svo

@@ -39,7 +39,7 @@ def transform(T, t, X):
 
 class OracleLoop:
     def __init__(self, scene, n_features=2000, bucket=(0, 0), acc=O.ACC_EXACT, max_level=TEMPORAL["max_level"],
-                 rule="every", features_to_track=70, detector="fast", orb=None):
+                 rule="every", features_to_track=70, detector="fast", orb=None, nonmax=True):
         """max_level: the temporal LK's (BASELINE configs: 3 at KITTI and 4K, 4 at
         1080p); the stereo LK keeps the reference's maxLevel 3.
         rule: "every" -- every frame a keyframe topping the set up to n_features
@@ -49,20 +49,26 @@ class OracleLoop:
         masked corner (extractFeatures, :74-92) -- n_features is only the
         capacity, and stats["kf_overflow"] counts the corners it had no room for
         (the reference's loop has no cap: a test sizes the capacity so that this
-        stays 0)."""
+        stays 0).
+        nonmax: FAST's nonmaxSuppression. The struct default is true
+        (R:include/config_reader.h:37); the shipped YAML spells the key
+        `nonmaxsuppression` (R:configs/config.yaml:31) while the reader looks up
+        `nonMaxSuppression` (R:include/config_reader.h:80), so with use_orb: 0 the
+        shipped config runs FAST WITHOUT suppression."""
         self.sc, self.N, self.bucket, self.acc = scene, n_features, bucket, acc
+        self.nonmax = nonmax
         self.max_level = max_level
         self.rule, self.features_to_track = rule, features_to_track
         self.detector, self.orb = detector, dict(orb or {})
         self.P_left, self.P_right = scene.projections()
 
     def _candidates(self, img, mask):
-        """extractFeatures' detect (R:src/tracking.cpp:82): FAST(20, NMS) or, with
+        """extractFeatures' detect (R:src/tracking.cpp:82): FAST(20, nonmax) or, with
         detector="orb", cv::ORB (R:src/tracking.cpp:35-52: the shipped config's
         150 features, scale 1.2, 8 levels, patch / edge 31, FAST 20, HARRIS)."""
         if self.detector == "orb":
             return O.orb_detect(img, mask, **self.orb)[0][:, :2]
-        kp = O.fast(img, 20, True, mask)[:, :2]
+        kp = O.fast(img, 20, self.nonmax, mask)[:, :2]
         if self.bucket[0] > 0:
             kp, _ = O.bucket(kp, img.shape[1], img.shape[0], self.bucket[0], self.bucket[1])
         return kp

@@ -205,6 +205,105 @@ def test_frontend_reference_keyframe_rule_takes_every_corner_kitti():
     assert max(len(fe.features(0)), len(ref.pts)) > 2000
 
 
+def test_frontend_fast_without_nms_matches_oracle_loop():
+    """FAST without non-maximum suppression through the loop -- what the shipped
+    YAML actually runs with use_orb: 0 (the key is spelled `nonmaxsuppression`,
+    R:configs/config.yaml:31, the reader asks for `nonMaxSuppression`,
+    R:include/config_reader.h:80, so it reads false) -- at the benchmark's
+    1241x376 / 2000 features: every corner pixel is a candidate (~8x the NMS
+    count, response 0 in raster order), every step against the oracle loop with
+    the same detector."""
+    ctx = S.Context(0)
+    W, H, N, T = 1241, 376, 2000, 9
+    sc = Scene(W, H, seed=11)
+    assert len(O.fast(sc.frame(0), 20, False)) > 4 * len(O.fast(sc.frame(0), 20, True))
+    fe = make_frontend(ctx, [sc], T, N, fast_nonmax=0)
+    fe.init(0)
+    ref = OracleLoop(Scene(W, H, seed=11), N, nonmax=False).init(0)
+    assert np.array_equal(fe.features(0), ref.pts)
+    added = 0
+    for t in range(1, T):
+        st = fe.step(t).as_dict()
+        rs = ref.step(t)
+        _compare_step(fe, ref, st, rs, t)
+        added += rs["added"]
+    assert added > 0
+
+
+def test_frontend_fast_without_nms_reference_rule_kitti():
+    """The shipped config's loop with use_orb: 0: FAST without suppression and
+    Tracking::nextFrame's keyframe rule (features_to_track as the test needs
+    keyframes), a keyframe taking every masked corner -- capacity sized above
+    the unsuppressed corner count (no overflow) -- against the oracle loop."""
+    ctx = S.Context(0)
+    W, H, T, F2T = 1241, 376, 6, 100000
+    sc = Scene(W, H, seed=21)
+    raw = len(O.fast(sc.frame(0), 20, False))
+    N = raw + 4096
+    fe = make_frontend(ctx, [sc], T, N, keyframe_rule=S.KF_REFERENCE, features_to_track=F2T, fast_nonmax=0)
+    fe.init(0)
+    ref = OracleLoop(Scene(W, H, seed=21), N, rule="reference", features_to_track=F2T, nonmax=False).init(0)
+    assert ref.init_overflow == 0 and len(ref.pts) > 4 * 2000
+    assert np.array_equal(fe.features(0), ref.pts)
+    kfs = []
+    for t in range(1, T):
+        st = fe.step(t).as_dict()
+        rs = ref.step(t)
+        _compare_step(fe, ref, st, rs, t, check_map=(t == T - 1))
+        assert st["keyframes"] == rs["keyframe"]
+        assert st["kf_overflow"] == rs["kf_overflow"] == 0
+        kfs.append(st["keyframes"])
+    assert kfs == [0, 1, 0, 1, 0]
+
+
+@pytest.mark.parametrize("f2t", [70, 140])
+def test_frontend_orb_batch_at_bench_size(f2t):
+    """The shipped ORB configuration at the size bench.py times it
+    (workloads.orb_reference: 1241x376, n_features 2000, use_orb 1,
+    Tracking::nextFrame's rule, SceneForward seeds 2000 + i): 64 slots holding 8
+    distinct sequences 8 times, 7 steps. Every distinct sequence against its oracle
+    loop (cv::ORB restated, oracle/orb.cpp) every step, and every slot bitwise equal
+    to the first slot of its sequence. features_to_track 70 is the shipped value
+    (the ORB keyframe at init, then tracking-only steps); 140 makes keyframes recur
+    within the 7 steps, so the batched ORB detection runs mid-sequence as well."""
+    ctx = S.Context(0)
+    W, H, N, T, D, SLOTS = 1241, 376, 2000, 8, 8, 64
+    seeds = [2000 + i for i in range(D)]
+    scenes = [SceneForward(W, H, seed=sd) for sd in seeds]
+    cfg = S.FrontendConfig(W, H, scenes[0].K, n_seq=SLOTS, n_frames=T, n_features=N, use_orb=1,
+                           keyframe_rule=S.KF_REFERENCE, features_to_track=f2t)
+    fe = S.Frontend(ctx, cfg)
+    frames = [[(sc.frame(t), sc.right(t)) for t in range(T)] for sc in scenes]
+    for s in range(SLOTS):
+        for t in range(T):
+            fe.set_frame(s, t, *frames[s % D][t])
+    fe.init(0)
+    refs = [OracleLoop(SceneForward(W, H, seed=sd), N, rule="reference", features_to_track=f2t,
+                       detector="orb").init(0) for sd in seeds]
+    for q, ref in enumerate(refs):
+        assert np.array_equal(fe.features(q), ref.pts), f"seq {q} features at init"
+    kfs = 0
+    for t in range(1, T):
+        st = fe.step(t).as_dict()
+        rss = [r.step(t) for r in refs]
+        for k in ("tracked", "inliers", "added", "features"):
+            assert st[k] == (SLOTS // D) * sum(rs[k] for rs in rss), f"{k} at t={t}"
+        assert st["keyframes"] == (SLOTS // D) * sum(rs["keyframe"] for rs in rss), f"keyframes at t={t}"
+        assert st["kf_overflow"] == 0
+        kfs += st["keyframes"]
+        for q, ref in enumerate(refs):
+            assert np.array_equal(fe.features(q), ref.pts), f"seq {q} features at t={t}"
+            rv, tv = fe.pose(q)
+            np.testing.assert_allclose(rv, ref.pose[0], atol=1e-7)
+            np.testing.assert_allclose(tv, ref.pose[1], atol=1e-6)
+        for s in range(D, SLOTS):
+            assert np.array_equal(fe.features(s), fe.features(s % D)), f"slot {s} at t={t}"
+            assert np.array_equal(np.r_[fe.pose(s)], np.r_[fe.pose(s % D)]), f"slot {s} pose at t={t}"
+    if f2t == 140:
+        assert kfs > 0
+    fe.close()
+
+
 @pytest.mark.parametrize("spec", ["32", "-1"])
 def test_frontend_reference_rule_mixed_batch(spec, monkeypatch):
     """SVO_KF_REFERENCE with sequences that are keyframes at different steps in the
