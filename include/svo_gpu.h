@@ -196,8 +196,9 @@ int svo_solve_pnp_sqpnp(const double* obj_xyz, const float* img_xy, int n, const
  * variant kept off the path; device = 2: that variant's host twin (bit-identical
  * to device 1; no context needed); device = 3 / 4 / 5: the device = 0 solver
  * forced to its scalar / AVX2-lane / AVX-512-lane form (SVO_ERR_NODEVICE when the
- * CPU lacks the instruction set). Rt: m x 12 doubles (R row-major, t); ok: m
- * ints (0: non-finite model). */
+ * CPU lacks the instruction set); device = 6: the device = 0 solver on the GPU, one
+ * lane per subset (epnp_lane.hip; bit-identical to device 0). Rt: m x 12 doubles
+ * (R row-major, t); ok: m ints (0: non-finite model). */
 int svo_epnp_subsets(svo_ctx* ctx, const float* subsets, int m, const double K[9], int device, double* Rt,
                      int* ok);
 

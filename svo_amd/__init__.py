@@ -477,7 +477,9 @@ class Context:
         """RANSAC's EPnP on (m, 25) float subsets (obj xyz x5, img xy x5) -> (Rt (m, 12), ok (m,)):
         device 0 / False: the host solver the RANSAC uses (bit-identical to the
         oracle's EPnP); 1 / True: the QL variant, one wave per subset on the GPU;
-        2: that variant's host twin (bit-identical to 1)."""
+        2: that variant's host twin (bit-identical to 1); 3 / 4 / 5: device 0 forced
+        to its scalar / AVX2 / AVX-512 form; 6: device 0's solver on the GPU, one
+        lane per subset (bit-identical to 0)."""
         subsets = _c(subsets, np.float32).reshape(-1, 25)
         K = _c(K, np.float64).reshape(9)
         m = len(subsets)

@@ -519,11 +519,12 @@ int svo_pnp_residuals(svo_ctx* ctx, const float* obj_xyz, const float* img_xy, i
 
 int svo_epnp_subsets(svo_ctx* ctx, const float* subsets, int m, const double K[9], int device, double* Rt,
                      int* ok) {
-    if ((!ctx && device == 1) || device < 0 || device > 5 || m < 0 || (m > 0 && (!subsets || !Rt || !ok)) || !K)
+    if ((!ctx && (device == 1 || device == 6)) || device < 0 || device > 6 || m < 0 ||
+        (m > 0 && (!subsets || !Rt || !ok)) || !K)
         return set_error(ctx, SVO_ERR_ARG, "svo_epnp_subsets: bad arguments");
     // 0: the front end's solver as dispatched; 3 / 4 / 5: forced scalar / AVX2 / AVX-512
     const int isa = device == 3 ? kEpnpScalar : device == 4 ? kEpnpAvx2 : device == 5 ? kEpnpAvx512 : kEpnpAuto;
-    if (device >= 3 && !epnp_isa_supported(isa))
+    if (device >= 3 && device <= 5 && !epnp_isa_supported(isa))
         return set_error(ctx, SVO_ERR_NODEVICE, "svo_epnp_subsets: instruction set not on this CPU");
     if (m == 0) return SVO_OK;
     if (device == 2) {  // the device solver's host twin (epnp_ql.hpp)
@@ -536,7 +537,7 @@ int svo_epnp_subsets(svo_ctx* ctx, const float* subsets, int m, const double K[9
         }
         return SVO_OK;
     }
-    if (device == 0 || device >= 3) {  // the front end's host solver: epnp_pixels_batch, kEpnpLanes at a time
+    if (device == 0 || (device >= 3 && device <= 5)) {  // the front end's host solver, kEpnpLanes at a time
         for (int j0 = 0; j0 < m; j0 += kEpnpLanes) {
             const int c = std::min(kEpnpLanes, m - j0);
             const float *o[kEpnpLanes], *im[kEpnpLanes];
@@ -566,7 +567,9 @@ int svo_epnp_subsets(svo_ctx* ctx, const float* subsets, int m, const double K[9
     int* dok = (int*)(dsub + 25 * (size_t)m);
     SVO_HIP(ctx, hipMemcpyAsync(dK, K, sizeof(double) * 9, hipMemcpyHostToDevice, ctx->stream));
     SVO_HIP(ctx, hipMemcpyAsync(dsub, subsets, sizeof(float) * 25 * (size_t)m, hipMemcpyHostToDevice, ctx->stream));
-    SVO_HIP(ctx, launch_epnp_wave(dsub, m, dK, dRt, dok, ctx->stream));
+    // 1: a wave per subset (the QL variant); 6: a lane per subset (the front end's solver)
+    SVO_HIP(ctx, device == 6 ? launch_epnp_lanes(dsub, m, dK, dRt, dok, ctx->stream)
+                             : launch_epnp_wave(dsub, m, dK, dRt, dok, ctx->stream));
     SVO_HIP(ctx, hipMemcpyAsync(Rt, dRt, sizeof(double) * 12 * (size_t)m, hipMemcpyDeviceToHost, ctx->stream));
     SVO_HIP(ctx, hipMemcpyAsync(ok, dok, sizeof(int) * (size_t)m, hipMemcpyDeviceToHost, ctx->stream));
     SVO_HIP(ctx, hipStreamSynchronize(ctx->stream));

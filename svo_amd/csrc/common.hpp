@@ -250,6 +250,8 @@ hipError_t launch_pnp_residuals(const PnpBatch& b, int nseq, int max_n, double f
 // RANSAC's EPnP on m 5-point subsets (25 floats each: obj xyz x5, img xy x5), one
 // wave per subset (epnp_wave.hip); Rt: m x 12 doubles, ok: m ints; K on the device
 hipError_t launch_epnp_wave(const float* subsets, int m, const double* K, double* Rt, int* ok, hipStream_t st);
+// one lane per subset, the front end's host solver run in each lane (epnp_lane.hip)
+hipError_t launch_epnp_lanes(const float* subsets, int m, const double* K, double* Rt, int* ok, hipStream_t st);
 hipError_t launch_pnp_score(const PnpBatch& b, int nseq, double fx, double fy, double cx, double cy, float thresh2,
                             hipStream_t st);
 

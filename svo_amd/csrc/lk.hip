@@ -1311,8 +1311,10 @@ __global__ __launch_bounds__(64, MINW) void lk_multi_kernel(LKBatch B, LKDev p) 
                 // from hoisting every strip's loads: 24 VGPRs per strip in flight)
                 unsigned P[2][NR + 1];
                 u32x2a4 Dv[2][NR + 1];
-                load_strip(0, P[0], Dv[0]);
+                // the staging values die before any strip load is in flight
                 write_staging();
+                __builtin_amdgcn_sched_barrier(0);
+                load_strip(0, P[0], Dv[0]);
 #pragma unroll
                 for (int k = 0; k < K; k++) {
                     if (k + 1 < K) load_strip(k + 1, P[(k + 1) & 1], Dv[(k + 1) & 1]);

@@ -179,18 +179,21 @@ def test_bench_forward_128_slots_match_oracle_loop():
                 img = np.ascontiguousarray(p2, np.float32)
                 idx = O.ransac_subsets(len(obj), nh)
                 subs = np.concatenate([obj[idx].reshape(nh, 15), img[idx].reshape(nh, 10)], axis=1)
-                Rt, ok = ctx.epnp_subsets(subs, K, device=0)
+                # device 0: the front end's host solver; 6: the same solver in GPU
+                # lanes, one subset per lane (epnp_lane.hip)
+                sols = [ctx.epnp_subsets(subs, K, device=dv) for dv in (0, 6)]
                 for k in range(nh):
                     rc, Ro, to = O.epnp(obj[idx[k]], img[idx[k]], K)
-                    same = (rc == 0) == bool(ok[k]) and (rc != 0 or np.array_equal(
-                        np.r_[Ro.ravel(), to].view(np.uint64), Rt[k].view(np.uint64)))
-                    differ += not same
+                    for Rt, ok in sols:
+                        same = (rc == 0) == bool(ok[k]) and (rc != 0 or np.array_equal(
+                            np.r_[Ro.ravel(), to].view(np.uint64), Rt[k].view(np.uint64)))
+                        differ += not same
                 hyps += nh
         drops.append(1 - st["inliers"] / st["tracked"])
         for s in range(n_dist, n_seq, 37):  # twin slots
             assert np.array_equal(fe.features(s), fe.features(s % n_dist)), f"slot {s} vs {s % n_dist} at t={t}"
     print(f"forward 128 slots: RANSAC drops {np.round(drops, 3)}; {hyps} oracle hypotheses re-solved by the "
-          f"product's EPnP, {differ} differ")
+          f"product's EPnP on the host and in GPU lanes, {differ} differ")
     assert differ == 0
     assert np.mean(drops) > 0.05, "the occluder should make RANSAC outliers"
     fe.close()

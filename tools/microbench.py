@@ -21,7 +21,7 @@ from svo_amd.scene import Scene  # noqa: E402
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("what", choices=["lk", "pyr", "fast", "stereo", "fepyr", "fefast"])
+    ap.add_argument("what", choices=["lk", "pyr", "fast", "stereo", "fepyr", "fefast", "epnp"])
     ap.add_argument("--seq", type=int, default=64)
     ap.add_argument("--points", type=int, default=128000)
     ap.add_argument("--reps", type=int, default=5)
@@ -70,6 +70,20 @@ def main():
                 fe.set_frame(s_, t, A if t == 0 else B, B)
         ms = fe.time_pyramid(1, args.reps)
         print(f"fepyr {args.seq} x {args.w}x{args.h}: {ms * 1e3:.1f} us per chain")
+    elif args.what == "epnp":
+        # RANSAC's EPnP: device 6 (a GPU lane per subset) vs device 0 (host SIMD
+        # lanes + pool); host wall per call, the kernel time from rocprof
+        sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tests"))
+        from test_epnp_cpu import K as KE, subsets
+        for m in (64, 256, 512, 4096):
+            subs = subsets(7, m, 0.5)[0]
+            for dev in (0, 6):
+                ctx.epnp_subsets(subs, KE, device=dev)
+                t = time.perf_counter()
+                for r in range(args.reps):
+                    ctx.epnp_subsets(subs, KE, device=dev)
+                dt = (time.perf_counter() - t) / args.reps
+                print(f"epnp m={m} device={dev}: {dt * 1e6:.1f} us per call ({dt * 1e6 / m:.2f} us per subset)")
     elif args.what == "fast":
         for r in range(args.reps):
             kp = ctx.fast_detect(ga, 20, True)
