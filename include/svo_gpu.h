@@ -324,6 +324,8 @@ typedef struct svo_frontend_stats {
                                    candidate capacity */
     double host_ms_orb;         /* use_orb: the keyframe's ORB detection (device stages and the
                                    host's retainBest, synchronous on the FAST stream) */
+    int64_t spec_margin;        /* the speculative stereo LK's margin over the expected top-up
+                                   (spec_margin + the last step's largest RANSAC / LK losses) */
 } svo_frontend_stats;
 
 int svo_frontend_create(svo_ctx* ctx, const svo_frontend_config* cfg, svo_frontend** out);

@@ -617,7 +617,8 @@ class FrontendStats(C.Structure):
                 ("host_ms_wait_post", C.c_double), ("host_ms_wait_score", C.c_double),
                 ("host_ms_wait_kf", C.c_double), ("host_ms_enqueue", C.c_double), ("host_ms_step", C.c_double),
                 ("ransac_rounds", C.c_int64), ("max_hypotheses", C.c_int64), ("serial_keyframe", C.c_int64),
-                ("full_copy", C.c_int64), ("kf_overflow", C.c_int64), ("host_ms_orb", C.c_double)]
+                ("full_copy", C.c_int64), ("kf_overflow", C.c_int64), ("host_ms_orb", C.c_double),
+                ("spec_margin", C.c_int64)]
 
     def as_dict(self):
         return {k: (float(getattr(self, k)) if k.startswith("host_") else int(getattr(self, k)))

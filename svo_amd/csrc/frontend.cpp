@@ -1930,6 +1930,7 @@ int svo_frontend_step(svo_frontend* fe, int t, svo_frontend_stats* stats) {
                     over += fe->h_over[s] + (fe->orb ? fe->orb_over[s] : 0);
         stats->kf_overflow = over;
         stats->host_ms_orb = ms_orb;
+        stats->spec_margin = fe->spec_m;
     }
     fe->stepped = t;
     return SVO_OK;

@@ -109,6 +109,7 @@ struct LKDev {
     int flags, want_err;
     float min_eig;
     int xcd;  // lk_multi_kernel: blocks in XCD order (xcd_tile.hpp; SVO_LK_XCD=0: raster)
+    int prefetch;  // lk_multi_kernel: the next level's prev window prefetched (SVO_LK_PREFETCH=1: on)
 };
 
 constexpr int JM = 3;  // margin (px) of the staged next-image region around the window
@@ -1215,7 +1216,10 @@ __global__ __launch_bounds__(64, MINW) void lk_multi_kernel(LKBatch B, LKDev p) 
     int itcount = 0;
     const int max_level = p.max_level;
 
+    unsigned pf = 0;  // the prefetches' dummy destination (p.prefetch)
     for (int level = max_level; level >= 0; level--) {
+        // (the previous level's prefetches, long landed: their register is free again)
+        asm volatile("s_waitcnt vmcnt(0)" : "+v"(pf) : : "memory");
         const ImgLevel I{prev->lv[level].data, prev->lv[level].w, prev->lv[level].h, prev->lv[level].pitch};
         const ImgLevel J{next->lv[level].data, next->lv[level].w, next->lv[level].h, next->lv[level].pitch};
         const float lscale = __builtin_amdgcn_ldexpf(1.f, -level);
@@ -1252,6 +1256,7 @@ __global__ __launch_bounds__(64, MINW) void lk_multi_kernel(LKBatch B, LKDev p) 
 
         int jx0 = ufloor(nextx - halfWx) - QJM, jy0 = ufloor(nexty - halfWy) - QJM;
         int jxa = jx0 & ~3;
+        int jbase = jy0 * JRW + jxa;  // the region origin as an entry offset (iny * JRW + inx - jbase)
         unsigned GX[K][NP], GY[K][NP];
         int asum[3] = {0, 0, 0};
         int csum[2] = {0, 0};  // sum I.Ix, I.Iy over the lane's strips
@@ -1362,6 +1367,30 @@ __global__ __launch_bounds__(64, MINW) void lk_multi_kernel(LKBatch B, LKDev p) 
 
         nextx -= halfWx;
         nexty -= halfWy;
+        // Prefetch of level - 1's prev window (its Scharr pairs and pixel rows, set up at
+        // the next level's start; their position depends only on the point): one dword
+        // at each end of each of its rows, issued now so that the lines travel from HBM
+        // while this level iterates out of LDS. The loads' data is never used: they go
+        // to one dummy register, kept live until the next level's wait, and loads
+        // complete in order, so the compiler's own vmcnt waits only get stricter.
+        if (p.prefetch && level > 0) {
+            const int l1 = level - 1;
+            const float s1 = __builtin_amdgcn_ldexpf(1.f, -l1);
+            const int dp1 = dprev.pitch[l1];
+            const ImgLevel I1{prev->lv[l1].data, prev->lv[l1].w, prev->lv[l1].h, prev->lv[l1].pitch};
+            const int qx = min(max(ufloor(px * s1 - halfWx), 0), I1.w - 1);
+            const int qy = ufloor(py * s1 - halfWy);
+#pragma unroll
+            for (int rr = 0; rr < (WH + 1 + LPF - 1) / LPF; rr++) {
+                const int r = min(max(qy + l + rr * LPF, 0), I1.h - 1);
+                const uint8_t* ir = I1.data + (size_t)r * I1.pitch + qx;
+                const uint8_t* dr = (const uint8_t*)dprev.data[l1] + 4 * ((size_t)r * dp1 + qx);
+                asm volatile("global_load_dword %0, %1, off" : "+v"(pf) : "v"(ir) : "memory");
+                asm volatile("global_load_dword %0, %1, off offset:20" : "+v"(pf) : "v"(ir) : "memory");
+                asm volatile("global_load_dword %0, %1, off" : "+v"(pf) : "v"(dr) : "memory");
+                asm volatile("global_load_dword %0, %1, off offset:84" : "+v"(pf) : "v"(dr) : "memory");
+            }
+        }
         float pdx = 0.f, pdy = 0.f;
         for (int j = 0; j < p.max_count; j++) {
             if (__builtin_amdgcn_ballot_w64(lact) == 0) break;
@@ -1372,13 +1401,14 @@ __global__ __launch_bounds__(64, MINW) void lk_multi_kernel(LKBatch B, LKDev p) 
                 lact = false;
             }
             const bool need = lact && ((unsigned)(inx - jx0) > 2u * QJM || (unsigned)(iny - jy0) > 2u * QJM);
-            if (need) {
-                jx0 = inx - QJM;
-                jy0 = iny - QJM;
-                jxa = jx0 & ~3;
-            }
             unsigned long long nb = __builtin_amdgcn_ballot_w64(need && l == 0);
-            if (nb) {
+            if (nb) {  // (rare: the region's origin moves only inside this branch)
+                if (need) {
+                    jx0 = inx - QJM;
+                    jy0 = iny - QJM;
+                    jxa = jx0 & ~3;
+                    jbase = jy0 * JRW + jxa;
+                }
                 wave_lds_sync();
                 while (nb) {
                     const int f = (int)(__builtin_ctzll(nb) / LPF);
@@ -1394,9 +1424,11 @@ __global__ __launch_bounds__(64, MINW) void lk_multi_kernel(LKBatch B, LKDev p) 
             const unsigned W0 = w.W0, W1 = w.W1;
             int bsum[2] = {-csum[0], -csum[1]};
             {
-                // an inactive group reads inside its own region (results unused)
-                const int ro = lact ? iny - jy0 : 0, co = lact ? inx - jxa : 0;
-                const unsigned* jb = jmine + ro * JRW + co;
+                // (iny - jy0) JRW + (inx - jxa) as one 24-bit multiply-add against the
+                // region origin's offset; an inactive group reads inside its own region
+                // (results unused)
+                const int off = lact ? __mul24(iny, JRW) + inx - jbase : 0;
+                const unsigned* jb = jmine + off;
 #pragma unroll
                 for (int k = 0; k < K; k++) {
                     const unsigned* js = jb + srow[k] * JRW + scol[k];
@@ -1418,6 +1450,9 @@ __global__ __launch_bounds__(64, MINW) void lk_multi_kernel(LKBatch B, LKDev p) 
             }
             float fb[2];
             group_sum_f<LPF, STEPS32>(bsum, fb);
+            // materialised here, ahead of the lane-divergent update below: sunk into
+            // it, the last DPP step splits into v_mov_dpp + a separate add per value
+            asm volatile("" : "+v"(fb[0]), "+v"(fb[1]));
             const float fb1 = fb[0], fb2 = fb[1];
             const float dx = (A12 * fb2 - A22 * fb1) * Ds;
             const float dy = (A12 * fb1 - A11 * fb2) * Ds;
@@ -1527,6 +1562,11 @@ hipError_t launch_lk(const LKBatch& b, int nseq, int max_n, const LKParams& lp, 
             return !(e && e[0] == '0');
         }();
         d.xcd = lk_xcd ? 1 : 0;
+        static const bool lk_pf = [] {
+            const char* e = std::getenv("SVO_LK_PREFETCH");
+            return e && e[0] == '1';
+        }();
+        d.prefetch = lk_pf ? 1 : 0;
     }
     if (!lp.generic) {
         // four features per wave: the SAD error (flags 0 + want_err) stays on lk_fast_kernel

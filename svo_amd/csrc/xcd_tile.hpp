@@ -36,7 +36,14 @@ __device__ __forceinline__ XcdTile xcd_tile() {
     return o;
 }
 
-// SVO_XCD_TILES=0: plain raster order (the A/B of this mapping)
+// SVO_XCD_TILES=0: plain raster order for the two tile kernels whose launch takes
+// an XT template flag -- fast_detect_q_kernel<.., XT> (fast.hip) and
+// pyr_scharr_kernel<.., .., XT> (pyramid.hip). It does NOT switch the other
+// users of xcd_tile(), which always run in XCD order: fast_box_filter_kernel and
+// fast_emit_kernel (fast.hip), pyr_chain_kernel and its tail (pyramid.hip); LK
+// has its own switch (SVO_LK_XCD, lk.hip). The recorded A/B
+// (profiles/r04/n_xcd_tiles_ab.txt) therefore measures those two kernels'
+// mapping only.
 inline bool xcd_tiles_on() {
     static const bool on = [] {
         const char* e = std::getenv("SVO_XCD_TILES");

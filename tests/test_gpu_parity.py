@@ -425,9 +425,11 @@ def test_pnp_ransac_inliers_identical(ctx):
 def test_pnp_ransac_near_threshold(ctx):
     """30 % of the points sit at reprojection error within +-0.5 px^2 of the 8 px
     threshold (64 px^2) under the true pose, so every hypothesis splits them near
-    the boundary: the product's EPnP (QL eigen + Householder QR) and the oracle's
-    (Jacobi + SVD) may differ in the last bits, and any such difference would show
-    as a flipped inlier here. Observed: 0 flips over these seeds."""
+    the boundary: any last-bit difference between the product's EPnP (OpenCV's
+    Jacobi SVDs in SIMD lanes, epnp_lanes.hpp) and the oracle's (oracle/epnp.c +
+    cvsvd.c), or between the two residual computations, would show as a flipped
+    inlier here. The EPnP models are bit-identical (test_epnp_cpu.py), so 0 flips
+    are required, not merely observed."""
     flips = 0
     for seed in range(4):
         sc = Scene(1241, 376, seed=seed)

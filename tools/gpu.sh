@@ -13,11 +13,11 @@
 #   mix TAG [BENCH_ARGS]    SQ instruction mix per wave of every step kernel
 #                           (mix TAG --cmd CMD..: of any command's kernels)
 #   lksplit                 LK VALU / time with the iteration cap at 1, 2, 50
-#   lkab "V1 V2 .."         standalone LK kernel time per SVO_LK_VARIANT (lk.hip launch_lk)
+#   lkab "V1 V2 .."         standalone LK kernel time per SVO_LK_VARIANT (or $LKAB_VAR) value
 #   lkmem [LIB ..]          LK memory-pipeline + issue counters (TA, TCP, SQ), per library build
 #   ab VAR "V1 V2" [RUNS]   bench A/B of an environment switch
 #   abcfg VAR "V1 V2"       the same A/B at the 1080p, 4K and KITTI configs
-#   round TAG               tests, smoke, prof, pmc (3 configs), mix, bench lines
+#   round1 TAG / round2 TAG  the round records: tests, smoke, driver bench + rocprof / PMC, mix, 1080p + 4K
 #
 # Every GPU step has its own time limit; the first failure ends the session.
 set -o pipefail
@@ -155,9 +155,10 @@ P
 run_lkab() {
     for v in ${1:-41}; do
         local T=/tmp/lkab_$v
-        SVO_LK_VARIANT=$v timeout -k 10 120 rocprofv3 --kernel-trace --stats -d $T -o run --output-format csv -- \
-            python tools/microbench.py lk --points 128000 --reps 5 > $T.log 2>&1 || fail lkab $T.log
-        echo "== SVO_LK_VARIANT=$v"
+        ( export "${LKAB_VAR:-SVO_LK_VARIANT}=$v"
+          timeout -k 10 120 rocprofv3 --kernel-trace --stats -d $T -o run --output-format csv -- \
+            python tools/microbench.py lk --points 128000 --reps 5 > $T.log 2>&1 ) || fail lkab $T.log
+        echo "== ${LKAB_VAR:-SVO_LK_VARIANT}=$v"
         python3 - $T <<'P'
 import csv, glob, sys
 f = glob.glob(sys.argv[1] + '/**/*kernel_stats.csv', recursive=True)[0]
@@ -223,18 +224,24 @@ print('$cfg $var=$v', d['value'], d['ms_per_step'], 'lk', p['lk'], 'stereo', p['
     done
 }
 
-run_round() {
+# the round's records in two sessions (each fits one gpurun call): round1 = tests, smoke,
+# the driver's bench command and its rocprof; round2 = PMC passes (3 configs), mix, the
+# 1080p (64 sequences) and 4K (32) bench lines
+run_round1() {
     local tag=$1
     run_tests
     run_smoke
-    run_prof "$tag"
-    for c in kitti 1080p 4k; do
-        if [ $c = kitti ]; then run_pmc "$tag" $c 256; else run_pmc "$tag" $c 16; fi
-    done
-    run_mix "$tag"
     run_bench "${tag}_driver" --gpus 1 --steps 20 --warmup 5
-    run_bench "$tag" --steps 50 --warmup 10
-    for c in 1080p 4k; do run_bench "${tag}_$c" --config $c --seq 16 --steps 20 --warmup 5 --no-cpu-baseline; done
+    run_prof "$tag" --gpus 1 --steps 20 --warmup 5
+}
+run_round2() {
+    local tag=$1
+    run_pmc "$tag" kitti 256
+    run_pmc "$tag" 1080p 64
+    run_pmc "$tag" 4k 32
+    run_mix "$tag"
+    run_bench "${tag}_1080p" --config 1080p --seq 64 --steps 20 --warmup 5 --no-cpu-baseline
+    run_bench "${tag}_4k" --config 4k --seq 32 --steps 20 --warmup 5 --no-cpu-baseline
 }
 
 while [ $# -gt 0 ]; do
@@ -256,7 +263,8 @@ while [ $# -gt 0 ]; do
         lkmem) run_lkmem "${args[@]}" ;;
         ab) run_ab "${args[@]}" ;;
         abcfg) run_abcfg "${args[@]}" ;;
-        round) run_round "${args[@]}" ;;
+        round1) run_round1 "${args[@]}" ;;
+        round2) run_round2 "${args[@]}" ;;
         *) fail "unknown mode $mode" ;;
     esac
 done
