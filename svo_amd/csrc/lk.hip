@@ -109,7 +109,6 @@ struct LKDev {
     int flags, want_err;
     float min_eig;
     int xcd;  // lk_multi_kernel: blocks in XCD order (xcd_tile.hpp; SVO_LK_XCD=0: raster)
-    int prefetch;  // lk_multi_kernel: the next level's prev window prefetched (SVO_LK_PREFETCH=1: on)
 };
 
 constexpr int JM = 3;  // margin (px) of the staged next-image region around the window
@@ -1029,7 +1028,7 @@ struct StageGeom {
     static constexpr int LPR = (JRW + 2) / 4, RPP = 64 / LPR, NPS = (JRH + RPP - 1) / RPP;
     int lr, d;            // the slot this lane loads and writes (lanes past the slots repeat row RPP - 1)
     int src;              // ds_bpermute byte address of the slot's neighbour
-    unsigned selx, sely;  // permute selectors of the second store's pairs
+    unsigned selx, sely;  // permute selectors of the second store's pairs (high bytes)
     int hi;               // dword offset of the second store from the first (2, or 0 for the last lane)
     __device__ __forceinline__ explicit StageGeom(int lane) {
         const int l0 = lane / LPR;
@@ -1037,8 +1036,8 @@ struct StageGeom {
         d = lane - l0 * LPR;
         src = (lr * LPR + d + 1) << 2;
         const bool last = d == LPR - 1;
-        selx = last ? 0x0c010c00u : 0x0c030c02u;
-        sely = last ? 0x0c020c01u : 0x0c040c03u;
+        selx = last ? 0x010c000cu : 0x030c020cu;  // pixel pairs in the halves' high bytes
+        sely = last ? 0x020c010cu : 0x040c030cu;
         hi = last ? 0 : 2;
     }
     __device__ __forceinline__ int row(int q) const {
@@ -1050,10 +1049,14 @@ struct StageGeom {
         const unsigned nv = (unsigned)__builtin_amdgcn_ds_bpermute(src, (int)v);
         unsigned* p = region + r * JRW + 4 * d;
         uint2 a, b;
-        a.x = __builtin_amdgcn_perm(nv, v, 0x0c010c00u) << kJShift;
-        a.y = __builtin_amdgcn_perm(nv, v, 0x0c020c01u) << kJShift;
-        b.x = __builtin_amdgcn_perm(nv, v, selx) << kJShift;
-        b.y = __builtin_amdgcn_perm(nv, v, sely) << kJShift;
+        // each pixel permuted into the high byte of its half (x 256), then one logical
+        // right shift to x 2^kJShift: a fast-rate shift (v_lshrrev; v_lshlrev issues at
+        // the slow rate on gfx950, profiles/r05/a_valu_rates.txt)
+        constexpr int R = 8 - kJShift;
+        a.x = __builtin_amdgcn_perm(nv, v, 0x010c000cu) >> R;
+        a.y = __builtin_amdgcn_perm(nv, v, 0x020c010cu) >> R;
+        b.x = __builtin_amdgcn_perm(nv, v, selx) >> R;
+        b.y = __builtin_amdgcn_perm(nv, v, sely) >> R;
         *reinterpret_cast<uint2*>(p) = a;
         *reinterpret_cast<uint2*>(p + hi) = b;
     }
@@ -1213,13 +1216,14 @@ __global__ __launch_bounds__(64, MINW) void lk_multi_kernel(LKBatch B, LKDev p) 
     }
     int st = live ? 1 : 0;
     float errv = 0.f;
-    int itcount = 0;
+    // iterations per feature, counted from the active-lane ballot: wave-uniform, so
+    // scalar registers (a per-lane counter is the first VGPR spilled under MINW = 4)
+    int itc[FPW];
+#pragma unroll
+    for (int f = 0; f < FPW; f++) itc[f] = 0;
     const int max_level = p.max_level;
 
-    unsigned pf = 0;  // the prefetches' dummy destination (p.prefetch)
     for (int level = max_level; level >= 0; level--) {
-        // (the previous level's prefetches, long landed: their register is free again)
-        asm volatile("s_waitcnt vmcnt(0)" : "+v"(pf) : : "memory");
         const ImgLevel I{prev->lv[level].data, prev->lv[level].w, prev->lv[level].h, prev->lv[level].pitch};
         const ImgLevel J{next->lv[level].data, next->lv[level].w, next->lv[level].h, next->lv[level].pitch};
         const float lscale = __builtin_amdgcn_ldexpf(1.f, -level);
@@ -1367,30 +1371,6 @@ __global__ __launch_bounds__(64, MINW) void lk_multi_kernel(LKBatch B, LKDev p) 
 
         nextx -= halfWx;
         nexty -= halfWy;
-        // Prefetch of level - 1's prev window (its Scharr pairs and pixel rows, set up at
-        // the next level's start; their position depends only on the point): one dword
-        // at each end of each of its rows, issued now so that the lines travel from HBM
-        // while this level iterates out of LDS. The loads' data is never used: they go
-        // to one dummy register, kept live until the next level's wait, and loads
-        // complete in order, so the compiler's own vmcnt waits only get stricter.
-        if (p.prefetch && level > 0) {
-            const int l1 = level - 1;
-            const float s1 = __builtin_amdgcn_ldexpf(1.f, -l1);
-            const int dp1 = dprev.pitch[l1];
-            const ImgLevel I1{prev->lv[l1].data, prev->lv[l1].w, prev->lv[l1].h, prev->lv[l1].pitch};
-            const int qx = min(max(ufloor(px * s1 - halfWx), 0), I1.w - 1);
-            const int qy = ufloor(py * s1 - halfWy);
-#pragma unroll
-            for (int rr = 0; rr < (WH + 1 + LPF - 1) / LPF; rr++) {
-                const int r = min(max(qy + l + rr * LPF, 0), I1.h - 1);
-                const uint8_t* ir = I1.data + (size_t)r * I1.pitch + qx;
-                const uint8_t* dr = (const uint8_t*)dprev.data[l1] + 4 * ((size_t)r * dp1 + qx);
-                asm volatile("global_load_dword %0, %1, off" : "+v"(pf) : "v"(ir) : "memory");
-                asm volatile("global_load_dword %0, %1, off offset:20" : "+v"(pf) : "v"(ir) : "memory");
-                asm volatile("global_load_dword %0, %1, off" : "+v"(pf) : "v"(dr) : "memory");
-                asm volatile("global_load_dword %0, %1, off offset:84" : "+v"(pf) : "v"(dr) : "memory");
-            }
-        }
         float pdx = 0.f, pdy = 0.f;
         for (int j = 0; j < p.max_count; j++) {
             if (__builtin_amdgcn_ballot_w64(lact) == 0) break;
@@ -1419,7 +1399,11 @@ __global__ __launch_bounds__(64, MINW) void lk_multi_kernel(LKBatch B, LKDev p) 
                 }
                 wave_lds_sync();
             }
-            itcount += lact ? 1 : 0;
+            {
+                const unsigned long long act = __builtin_amdgcn_ballot_w64(lact);
+#pragma unroll
+                for (int f = 0; f < FPW; f++) itc[f] += (int)((act >> (LPF * f)) & 1ull);
+            }
             const BiW w = bilinear_weights(nextx - fnx, nexty - fny);
             const unsigned W0 = w.W0, W1 = w.W1;
             int bsum[2] = {-csum[0], -csum[1]};
@@ -1480,7 +1464,12 @@ __global__ __launch_bounds__(64, MINW) void lk_multi_kernel(LKBatch B, LKDev p) 
         next_xy[2 * pt + 1] = ny;
         B.status[base + pt] = (uint8_t)st;
         if (B.err) B.err[base + pt] = errv;
-        if (B.iters) B.iters[base + pt] = itcount;
+        if (B.iters) {
+            int itcount = itc[0];
+#pragma unroll
+            for (int f = 1; f < FPW; f++) itcount = g == f ? itc[f] : itcount;
+            B.iters[base + pt] = itcount;
+        }
     }
 }
 
@@ -1562,11 +1551,6 @@ hipError_t launch_lk(const LKBatch& b, int nseq, int max_n, const LKParams& lp, 
             return !(e && e[0] == '0');
         }();
         d.xcd = lk_xcd ? 1 : 0;
-        static const bool lk_pf = [] {
-            const char* e = std::getenv("SVO_LK_PREFETCH");
-            return e && e[0] == '1';
-        }();
-        d.prefetch = lk_pf ? 1 : 0;
     }
     if (!lp.generic) {
         // four features per wave: the SAD error (flags 0 + want_err) stays on lk_fast_kernel

@@ -60,6 +60,10 @@ PROBE32(p_xor_b32, "v_xor_b32 %0, %1, %0")
 PROBE32(p_mov_b32, "v_mov_b32 %0, %1")
 PROBE32(p_lshr, "v_lshrrev_b32 %0, %1, %0")
 PROBE32(p_ashr, "v_ashrrev_i32 %0, 16, %0")
+PROBE32(p_lshl7, "v_lshlrev_b32 %0, 7, %0")
+PROBE32(p_lshl_v, "v_lshlrev_b32 %0, %1, %0")
+PROBE32(p_lshr1, "v_lshrrev_b32 %0, 1, %0")
+PROBE32(p_perm_c, "v_perm_b32 %0, %1, %0, %2")
 PROBE32(p_max_i32, "v_max_i32 %0, %1, %0")
 PROBE32(p_min_u32, "v_min_u32 %0, %1, %0")
 PROBE32(p_mul_i24, "v_mul_i32_i24 %0, %1, %0")
@@ -97,7 +101,8 @@ int main() {
         E("v_add_u32", p_add_u32) E("v_sub_u32", p_sub_u32) E("v_add_co_u32", p_add_co) E("v_mul_f32", p_mul_f32)
         E("v_add_f32", p_add_f32) E("v_fmac_f32", p_fmac_f32) E("v_max_f32", p_max_f32) E("v_and_b32", p_and_b32)
         E("v_or_b32", p_or_b32) E("v_xor_b32", p_xor_b32) E("v_mov_b32", p_mov_b32) E("v_lshrrev_b32", p_lshr)
-        E("v_ashrrev_i32", p_ashr) E("v_max_i32", p_max_i32) E("v_min_u32", p_min_u32) E("v_mul_i32_i24", p_mul_i24)
+        E("v_ashrrev_i32", p_ashr) E("v_lshlrev_b32(7)", p_lshl7) E("v_lshlrev_b32(v)", p_lshl_v)
+        E("v_lshrrev_b32(1)", p_lshr1) E("v_perm_b32", p_perm_c) E("v_max_i32", p_max_i32) E("v_min_u32", p_min_u32) E("v_mul_i32_i24", p_mul_i24)
         E("v_mul_hi_u32", p_mul_hi) E("v_floor_f32", p_floor) E("v_cvt_f32_u32", p_cvt_u32) E("v_med3_f32", p_med3)
         E("v_fma_f32(vop3)", p_fma_vop3) E("v_add_f32_dpp", p_add_f32_dpp) E("v_add_u32_dpp(quad)", p_add_u32_dpp)
         E("v_pk_add_u16", p_pk_add_u16) E("v_dot2c_f32_bf16", p_dot2c_f32_bf16) E("v_bfi_b32", p_bfi)
