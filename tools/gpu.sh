@@ -154,7 +154,7 @@ P
 
 run_lkab() {
     for v in ${1:-41}; do
-        local T=/tmp/lkab_$v
+        local T=/tmp/lkab_$(basename "$v")
         ( export "${LKAB_VAR:-SVO_LK_VARIANT}=$v"
           timeout -k 10 120 rocprofv3 --kernel-trace --stats -d $T -o run --output-format csv -- \
             python tools/microbench.py lk --points 128000 --reps 5 > $T.log 2>&1 ) || fail lkab $T.log
