@@ -238,9 +238,23 @@ def roofline_valu(lk_name: str, seqs: int, lk_avg_s: float):
     if valu is None or lk_avg_s <= 0:
         return None
     ach = valu / lk_avg_s / 1e9
-    return {"kernel": lk_name + ">", "bound": "valu", "achieved": round(ach, 1), "peak": VALU_PEAK_G,
-            "unit": "G wave-instr/s", "frac": round(ach / VALU_PEAK_G, 4), "valu_per_launch": int(valu),
-            "source": src, "timing": "live average launch time (the roofline's)"}
+    out = {"kernel": lk_name + ">", "bound": "valu", "achieved": round(ach, 1), "peak": VALU_PEAK_G,
+           "unit": "G wave-instr/s", "frac": round(ach / VALU_PEAK_G, 4), "valu_per_launch": int(valu),
+           "source": src, "timing": "live average launch time (the roofline's)"}
+    # gfx950 issues most of LK's instructions (dot2, perm, DPP, cndmask, cmp, cvt, left
+    # shifts) at half the rate of the 1,228.8 G/s peak: the issue rate its own mix
+    # allows (tools/lk_mix_model.py over the compiled ISA, measured per-class rates)
+    try:
+        with open(os.path.join(ROOT, "profiles", "lk_issue_model.json")) as f:
+            mdl = json.load(f)
+        if lk_name.startswith("lk_multi"):
+            out["peak_mix_weighted"] = mdl["peak_mix_G"]
+            out["frac_mix_weighted"] = round(ach / mdl["peak_mix_G"], 4)
+            out["slow_class_share"] = mdl["slow_share"]
+            out["mix_model"] = mdl["source"]
+    except (OSError, ValueError, KeyError):
+        pass
+    return out
 
 
 def cpu_baseline(cfg_name: str, seconds: float):

@@ -94,6 +94,7 @@ def main():
     ap.add_argument("--levels", type=float, default=4.0)
     ap.add_argument("--iters", type=float, default=16.5)
     ap.add_argument("--rare", type=float, default=0.05, help="re-staging executions per iteration")
+    ap.add_argument("--json", default=None, help="write the result here (bench.py reads profiles/lk_issue_model.json)")
     a = ap.parse_args()
     path = a.asm
     if path is None:
@@ -127,6 +128,15 @@ def main():
     print(f"slow-class share {by_cls['slow'] / tot_n:.3f}; mean {ns_per:.3f} ns per wave-instruction per SIMD")
     print(f"mix-weighted VALU peak {peak_mix:.1f} G wave-instr/s (fast-class peak 1228.8; all-fast at "
           f"{FAST_NS} ns: {1024 / FAST_NS:.1f})")
+    if a.json:
+        import json
+        json.dump({"kernel": "lk_multi_kernel<4, 1, 3, 2, 21, 21, 7>", "predicted_valu_per_wave": round(tot_n),
+                   "slow_share": round(by_cls["slow"] / tot_n, 4), "ns_per_instr": round(ns_per, 4),
+                   "peak_mix_G": round(peak_mix, 1), "fast_ns": FAST_NS, "slow_ns": SLOW_NS,
+                   "levels": a.levels, "iters_per_wave": a.iters,
+                   "source": "tools/lk_mix_model.py: the compiled ISA's VALU instructions weighted by block "
+                             "frequency, priced at the measured per-class rates (profiles/r05/e_valu_rates3.txt)"},
+                  open(a.json, "w"), indent=1)
 
 
 if __name__ == "__main__":
