@@ -208,16 +208,20 @@ CHAIN_LEFT_TARGS = (None, "true", None)
 VALU_PEAK_G = 256 * 4 * 2.4 / 2  # G wave64 VALU instructions/s: 256 CUs x 4 SIMD-32, 2 cycles each at 2.4 GHz
 
 
-def pmc_valu(kernel_prefix: str, seqs: int):
+def pmc_valu(kernel_prefix: str, seqs: int, cfg_name: str = "kitti"):
     """VALU wave-instructions per launch of a kernel from the committed SQ mix pass
     (profiles/valu_summary.json, written by tools/gpu.sh mix: SQ_INSTS_VALU per
     dispatch), scaled from the sequences per launch it was measured at to `seqs`;
-    None when absent."""
+    None when absent or measured at another config (its features per sequence and
+    levels differ)."""
     path = os.path.join(ROOT, "profiles", "valu_summary.json")
     try:
         with open(path) as f:
             d = json.load(f)
     except (OSError, ValueError):
+        return None, None
+    mc = re.search(r"--config (\w+)", d.get("source", ""))
+    if (mc.group(1) if mc else "kitti") != cfg_name:
         return None, None
     m = re.search(r"--seq (\d+)", d.get("source", ""))
     measured = int(m.group(1)) if m else 128
@@ -227,14 +231,14 @@ def pmc_valu(kernel_prefix: str, seqs: int):
     return None, None
 
 
-def roofline_valu(lk_name: str, seqs: int, lk_avg_s: float):
+def roofline_valu(lk_name: str, seqs: int, lk_avg_s: float, cfg_name: str = "kitti"):
     """LK against the bound that binds it, VALU issue (SURVEY.md 8(d) prices it by
     bytes; rocprof shows the kernel issue-bound): the mix pass's VALU
     instructions per launch over this run's live average launch time."""
     # the mix pass keys kernels with their template arguments (the 21 x 21 and the
     # stereo 11 x 11 instances of lk_multi_kernel are separate entries)
     kname = "lk_multi_kernel<4, 1, 3, 2, 21, 21, 7>" if lk_name.startswith("lk_multi") else "lk_fast_kernel<21, 21"
-    valu, src = pmc_valu(kname, seqs)
+    valu, src = pmc_valu(kname, seqs, cfg_name)
     if valu is None or lk_avg_s <= 0:
         return None
     ach = valu / lk_avg_s / 1e9
@@ -754,7 +758,7 @@ def main():
             "avg_launch_us": round(lk_avg_s * 1e6, 3),
             "launches_timed": lk_n,
         },
-        "roofline_valu": roofline_valu(lk_name, Sq, lk_avg_s),
+        "roofline_valu": roofline_valu(lk_name, Sq, lk_avg_s, args.config),
         "roofline_pyramid": {
             "kernel": f"pyramid chain: {pyr_kernels}; one new left frame of {Sq} sequences per launch",
             "bound": "hbm",
