@@ -550,9 +550,13 @@ __device__ __forceinline__ void wave_sum_f3(int x, int y, int z, float& fx, floa
 // otherwise picks v_dot2c (accumulator = destination) plus a v_mov of the
 // rounding constant for every use.
 __device__ __forceinline__ int sdot2_r(unsigned a, unsigned b, int c) {
+#ifdef SVO_SDOT2_BUILTIN
+    return sdot2(a, b, c);
+#else
     int d;
     asm("v_dot2_i32_i16 %0, %1, %2, %3" : "=v"(d) : "v"(a), "v"(b), "v"(c));
     return d;
+#endif
 }
 __device__ __forceinline__ unsigned pk_sub16(unsigned a, unsigned b) {
     return __builtin_bit_cast(unsigned, __builtin_bit_cast(s16x2, a) - __builtin_bit_cast(s16x2, b));
