@@ -385,6 +385,12 @@ struct svo_frontend {
     // NMS without the box mask queued in step t on the context stream (0: FAST
     // detection behind LK(t) on the FAST stream)
     int fast_pre = 1;
+    // SVO_FE_PRE_AFTER_POST (default 1): the pre-detection of frame t+1 and its right
+    // pyramid are queued behind step t's post-LK (fe_post) instead of behind frame
+    // t+1's left pyramid, so that they cannot take the CUs ahead of the critical
+    // post-LK when LK runs long (the forward scene: +3 %; the headline: neutral)
+    int pre_after_post = 1;
+    int pre_pending = -1;          // frame whose pre-detection waits for fe_post
     int pre_t = -1;                // frame whose unmasked detection sits in fbits / rowcnt / score_map
     hipEvent_t ev_pre = nullptr;   // that detection done (context stream)
     hipEvent_t ev_fdone = nullptr; // this step's FAST chain done (FAST stream)
@@ -1022,6 +1028,8 @@ int svo_frontend_create(svo_ctx* ctx, const svo_frontend_config* cfg, svo_fronte
     {
         const char* fp = std::getenv("SVO_FE_FAST_PRE");
         fe->fast_pre = fp && fp[0] == '0' ? 0 : 1;
+        const char* pp = std::getenv("SVO_FE_PRE_AFTER_POST");
+        fe->pre_after_post = pp && pp[0] == '0' ? 0 : 1;
         const char* sm = std::getenv("SVO_FE_SPEC_MARGIN");
         fe->spec_margin = sm ? std::atoi(sm) : 32;
         const char* se = std::getenv("SVO_FE_SPEC_EARLY");
@@ -1338,6 +1346,8 @@ static LKParams fe_temporal_params(const svo_frontend* fe) {
     return lp;
 }
 
+static int fe_queue_pre_and_right(svo_frontend* fe, int tn);
+
 // Post-LK of step t, queued once the previous step's poses are set
 // (fe_finish_fits): its keyframe points go to the world frame first. The
 // keyframe's stereo matches go out right behind it, speculatively, beside the
@@ -1363,6 +1373,15 @@ static int fe_post(svo_frontend* fe, int t) {
     ph_end(fe, sl, slot);
     SVO_HIP(ctx, hipEventRecord(fe->ev_post, sl));
     TP("post_lk launched");
+    if (fe->pre_pending == t + 1) {
+        // (SVO_FE_PRE_AFTER_POST) frame t+1's pre-detection and right pyramid, on the
+        // context stream behind this post-LK: when LK runs long, the pre-detection
+        // would otherwise be dispatched ahead of the critical post-LK
+        SVO_HIP(ctx, hipStreamWaitEvent(ctx->stream, fe->ev_post, 0));
+        int rc = fe_queue_pre_and_right(fe, t + 1);
+        if (rc) return rc;
+    }
+    fe->pre_pending = -1;
     if (fe->spec_margin >= 0 && fe->spec_t != t) {
         int rq = fe_queue_spec(fe, t, false);
         if (rq) return rq;
@@ -1517,22 +1536,35 @@ static int fe_queue_next_image(svo_frontend* fe, int tn) {
         ph_end(fe, st0, slot);
         SVO_HIP(ctx, hipEventRecord(fe->ev_pyr, st0));
         fe->pyr_ready = tn;
-        // 6. FAST pre-detection of frame t+1 (fe_queue_pre), behind its pyramid:
-        //    it fills the CUs the latency-bound post-LK / stereo chain leaves
-        if (fe->fast_pre) {
-            int rc = fe_queue_pre(fe, tn);
-            if (rc) return rc;
+        // (pre_after_post: 6 and 6b are queued by fe_post instead, behind the post-LK)
+        if (fe->pre_after_post) {
+            fe->pre_pending = tn;
+            return SVO_OK;
         }
-        // 6b. and frame t+1's right pyramid: ready when step t+1 begins, so its
-        //     speculative stereo LK can start right behind FAST(t+1) beside LK(t+1)
-        //     (built beside LK(t+1) instead, it was starved until LK's end)
-        ph_begin(fe, PH_PYR_R, st0, &slot);
-        SVO_HIP(ctx, launch_pyramid_batched(fe->d_desc_r + (size_t)(tn % fe->T) * S, S, fe->W, fe->H, fe->nlev,
-                                            st0));
-        ph_end(fe, st0, slot);
-        SVO_HIP(ctx, hipEventRecord(fe->ev_pyr_r_b[tn & 1], st0));
-        fe->pyr_r_ready = tn;
+        fe->pre_pending = -1;
     }
+    return fe_queue_pre_and_right(fe, tn);
+}
+
+// 6. FAST pre-detection of frame tn (fe_queue_pre), behind its pyramid: it fills
+//    the CUs the latency-bound post-LK / stereo chain leaves; 6b. then frame tn's
+//    right pyramid: ready when step tn begins, so its speculative stereo LK can
+//    start right behind FAST(tn) beside LK(tn) (built beside LK(tn) instead, it was
+//    starved until LK's end).
+static int fe_queue_pre_and_right(svo_frontend* fe, int tn) {
+    svo_ctx* ctx = fe->ctx;
+    hipStream_t st0 = ctx->stream;
+    const int S = fe->S;
+    int slot;
+    if (fe->fast_pre) {
+        int rc = fe_queue_pre(fe, tn);
+        if (rc) return rc;
+    }
+    ph_begin(fe, PH_PYR_R, st0, &slot);
+    SVO_HIP(ctx, launch_pyramid_batched(fe->d_desc_r + (size_t)(tn % fe->T) * S, S, fe->W, fe->H, fe->nlev, st0));
+    ph_end(fe, st0, slot);
+    SVO_HIP(ctx, hipEventRecord(fe->ev_pyr_r_b[tn & 1], st0));
+    fe->pyr_r_ready = tn;
     return SVO_OK;
 }
 

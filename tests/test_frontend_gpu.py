@@ -96,13 +96,15 @@ def test_frontend_forward_occluder_matches_oracle_loop(early, monkeypatch):
 
 
 @pytest.mark.parametrize("bucket", [(0, 0), (50, 4)])
-@pytest.mark.parametrize("pre", ["0", "1"])
+@pytest.mark.parametrize("pre", ["0", "1", "post"])
 def test_frontend_fast_schedules(pre, bucket, monkeypatch):
     """Where FAST(t)'s detection runs, each against the oracle loop: behind LK(t) on
     the FAST stream (SVO_FE_FAST_PRE=0), or unmasked during step t-1 on the
     context stream with only the box filter + scan + emit behind LK(t) (1, the
-    default; the mask drops corners after NMS)."""
-    monkeypatch.setenv("SVO_FE_FAST_PRE", pre)
+    default; the mask drops corners after NMS), queued behind frame t-1's pyramid
+    or behind step t-1's post-LK ("post": SVO_FE_PRE_AFTER_POST=1)."""
+    monkeypatch.setenv("SVO_FE_FAST_PRE", "1" if pre == "post" else pre)
+    monkeypatch.setenv("SVO_FE_PRE_AFTER_POST", "1" if pre == "post" else "0")
     ctx = S.Context(0)
     W, H, N, T = 640, 376, 800, 8
     fe = make_frontend(ctx, [Scene(W, H, seed=7)], T, N, bucket_size=bucket[0], per_bucket=bucket[1])
