@@ -496,6 +496,11 @@ def main():
                          "parallax + a moving occluder: 5-20%% RANSAC outliers) as the timed workload")
     ap.add_argument("--no-forward", action="store_true",
                     help="skip the extra timed pass over the forward/occluder scene (`workloads.forward`)")
+    ap.add_argument("--legs", default="after", choices=("first", "after"),
+                    help="after (default): the side workloads (single stream, bucketed, forward, ORB, "
+                         "streamed) run behind the headline; first: before it -- measured 12 %% slower for the "
+                         "headline (other front ends created and closed in the process first: "
+                         "profiles/r05/l_legs_order_ab.txt)")
     ap.add_argument("--dry-run", action="store_true",
                     help="set up the ranks, print each rank's shard and exit (no GPU call)")
     args = ap.parse_args()
@@ -558,6 +563,70 @@ def main():
             all_pairs.append(pairs)
         if s % 16 == 15:
             print(f"[bench] rank {rank}: {s + 1}/{Sq} sequences rendered and uploaded", file=sys.stderr, flush=True)
+    side = {"single": None, "bucketed": None, "forward": None, "orb": None, "stream": None}
+
+    def side_legs(close_fe):
+        """The side workloads of the line (each its own front end and timed window)."""
+        print("[bench] side measurements", file=sys.stderr, flush=True)
+        close_fe()  # (legs after the headline: its front end is done with)
+        single = None
+        if not args.no_single and world == 1:
+            fe1 = S.Frontend(ctx, S.FrontendConfig(W, H, scenes[0].K, n_seq=1, n_frames=T, n_features=N, max_level=ML))
+            for t in range(T):
+                fe1.set_frame(0, t, *pairs0[t % P])
+            fe1.init(0)
+            for t in range(1, Wm + 1):
+                fe1.step(t)
+            t1 = time.perf_counter()
+            for t in range(Wm + 1, Wm + K + 1):
+                fe1.step(t)
+            fe1.synchronize()
+            single = K / (time.perf_counter() - t1)
+            fe1.close()
+        forward = None
+        if not args.no_forward and args.scene == "rot" and world == 1:
+            print("[bench] forward / occluder workload", file=sys.stderr, flush=True)
+            forward = forward_workload(S, SceneForward, ctx, W, H, N, ML, Sq, K, Wm, args.threads)
+        orb = None
+        if not args.no_orb and args.scene == "rot" and world == 1:
+            print("[bench] shipped ORB configuration workload", file=sys.stderr, flush=True)
+            orb = orb_workload(S, SceneForward, ctx, W, H, ML, Sq, K, Wm, args.threads)
+        stream = None
+        if not args.no_stream and args.scene == "rot" and world == 1:
+            print("[bench] streamed-ingest workloads (grey, BGR)", file=sys.stderr, flush=True)
+            firsts = all_pairs[:16] if all_pairs else None
+            stream = {kind: stream_workload(S, Scene, ctx, W, H, N, ML, Sq, K, Wm, args.threads, kind == "bgr",
+                                            scenes[0].K, firsts) for kind in ("grey", "bgr")}
+        # (last when the legs run first: the headline's own workload, so the GPU
+        # goes into the headline's warm-up busy)
+        # SURVEY §8(d) lists "FAST + bucket" in the frame metric, but the reference's loop
+        # never buckets (its call site is a TODO, R:src/tracking.cpp:88), so `value` is the
+        # reference's loop; the same batch is timed again with bucketed selection
+        # (bucket.hip, 50-px cells x 4 per cell) between FAST and the keyframe's take
+        bucketed = None
+        if all_pairs:
+            BS, PB = 50, 4
+            feb = S.Frontend(ctx, S.FrontendConfig(W, H, scenes[0].K, n_seq=Sq, n_frames=T, n_features=N, max_level=ML,
+                                                   host_threads=args.threads, timing=0, bucket_size=BS, per_bucket=PB))
+            for s, pairs in enumerate(all_pairs):
+                for t in range(T):
+                    feb.set_frame(s, t, *pairs[t % P])
+            feb.init(0)
+            for t in range(1, Wm + 1):
+                feb.step(t)
+            t1 = time.perf_counter()
+            for t in range(Wm + 1, Wm + K + 1):
+                feb.step(t)
+            feb.synchronize()
+            dtb = time.perf_counter() - t1
+            bucketed = {"value": round(Sq * K / dtb, 2), "unit": "frames/s", "ms_per_step": round(dtb / K * 1e3, 4),
+                        "bucket_size": BS, "per_bucket": PB, "steps": K, "warmup": Wm}
+            feb.close()
+        side.update(single=single, bucketed=bucketed, forward=forward, orb=orb, stream=stream)
+
+    legs_after = args.legs == "after" or world > 1
+    if not legs_after:
+        side_legs(close_fe=lambda: None)
     fe.init(0)
     try:
         host_cpus = fe.host_cpus()  # this rank's pinned share of the node (svo_host_cpu_plan)
@@ -657,63 +726,10 @@ def main():
     fast_avg_s = fe.time_fast(Wm + K, 20) / 1e3 if hasattr(fe, "time_fast") else 0.0
     fast_bytes = Sq * W * H
     fast_traffic = pmc_traffic(args.config, "fast_detect_q_kernel", Sq)  # one instance per config
-    single = None
-    print("[bench] timed window done; side measurements", file=sys.stderr, flush=True)
-    if not args.no_single and world == 1:
-        fe1 = S.Frontend(ctx, S.FrontendConfig(W, H, scenes[0].K, n_seq=1, n_frames=T, n_features=N, max_level=ML))
-        for t in range(T):
-            fe1.set_frame(0, t, *pairs0[t % P])
-        fe1.init(0)
-        for t in range(1, Wm + 1):
-            fe1.step(t)
-        t1 = time.perf_counter()
-        for t in range(Wm + 1, Wm + K + 1):
-            fe1.step(t)
-        fe1.synchronize()
-        single = K / (time.perf_counter() - t1)
-        fe1.close()
-    # SURVEY §8(d) lists "FAST + bucket" in the frame metric, but the reference's loop
-    # never buckets (its call site is a TODO, R:src/tracking.cpp:88), so `value` is the
-    # reference's loop; the same batch is timed again with bucketed selection
-    # (bucket.hip, 50-px cells x 4 per cell) between FAST and the keyframe's take
-    bucketed = None
-    if all_pairs:
-        fe.close()
-        BS, PB = 50, 4
-        feb = S.Frontend(ctx, S.FrontendConfig(W, H, scenes[0].K, n_seq=Sq, n_frames=T, n_features=N, max_level=ML,
-                                               host_threads=args.threads, timing=0, bucket_size=BS, per_bucket=PB))
-        for s, pairs in enumerate(all_pairs):
-            for t in range(T):
-                feb.set_frame(s, t, *pairs[t % P])
-        feb.init(0)
-        for t in range(1, Wm + 1):
-            feb.step(t)
-        t1 = time.perf_counter()
-        for t in range(Wm + 1, Wm + K + 1):
-            feb.step(t)
-        feb.synchronize()
-        dtb = time.perf_counter() - t1
-        bucketed = {"value": round(Sq * K / dtb, 2), "unit": "frames/s", "ms_per_step": round(dtb / K * 1e3, 4),
-                    "bucket_size": BS, "per_bucket": PB, "steps": K, "warmup": Wm}
-        feb.close()
-    forward = None
-    if not args.no_forward and args.scene == "rot" and world == 1:
-        print("[bench] forward / occluder workload", file=sys.stderr, flush=True)
-        if not all_pairs:
-            fe.close()
-        forward = forward_workload(S, SceneForward, ctx, W, H, N, ML, Sq, K, Wm, args.threads)
-    orb = None
-    if not args.no_orb and args.scene == "rot" and world == 1:
-        print("[bench] shipped ORB configuration workload", file=sys.stderr, flush=True)
-        fe.close()  # (idempotent)
-        orb = orb_workload(S, SceneForward, ctx, W, H, ML, Sq, K, Wm, args.threads)
-    stream = None
-    if not args.no_stream and args.scene == "rot" and world == 1:
-        print("[bench] streamed-ingest workloads (grey, BGR)", file=sys.stderr, flush=True)
-        fe.close()
-        firsts = all_pairs[:16] if all_pairs else None
-        stream = {kind: stream_workload(S, Scene, ctx, W, H, N, ML, Sq, K, Wm, args.threads, kind == "bgr",
-                                        scenes[0].K, firsts) for kind in ("grey", "bgr")}
+    print("[bench] timed window done", file=sys.stderr, flush=True)
+    if legs_after:
+        side_legs(close_fe=fe.close)
+    single, bucketed, forward, orb, stream = (side[k] for k in ("single", "bucketed", "forward", "orb", "stream"))
     out = {
         "metric": "frames/sec @1241x376, 2000 feats; LK iters/sec; achieved HBM GB/s",
         "value": round(fps, 2),
@@ -733,6 +749,7 @@ def main():
                    "host_cpus_rank0": len(host_cpus)},
         "lk_iters_per_s": round(lk_iters_total / dt_max, 1),
         "achieved_GBps_algorithmic": round(frames * frame_bytes(W, H, N, ML) / dt_max / 1e9, 2),
+        "side_legs": "after" if legs_after else "first",
         "single_stream_fps": round(single, 2) if single else None,
         "bucketed": bucketed,
         "workloads": {"forward": forward, "orb_reference": orb, "stream": stream},
