@@ -959,16 +959,30 @@ __device__ __forceinline__ BiW bilinear_weights(float a, float b) {
     return {__builtin_amdgcn_perm(b01, b00, 0x05040100u), __builtin_amdgcn_perm(w11, b10, 0x05040100u)};
 }
 
-// 7 rows of one strip: I (x32) / Ix / Iy at the strip's pixels packed by row
-// pairs (4 pairs, the last closed by a zero row), accumulated into the A sums.
-template <int NR>
-__device__ __forceinline__ void strip_setup(const unsigned* P, const u32x2a4* D, unsigned IW0, unsigned IW1,
-                                            unsigned GW0, unsigned GW1, unsigned* I2, unsigned* GX, unsigned* GY,
-                                            int& a11, int& a12, int& a22) {
-    constexpr int NP = (NR + 1) / 2;
+// NR rows of one strip: I (x32) / Ix / Iy at the strip's pixels packed by row pairs
+// (NR / 2 pairs), accumulated into the A sums and into per-lane c1 += I.Ix,
+// c2 += I.Iy (sum (J - I) G = sum J G - sum I G exactly -- int32 wrap-around
+// arithmetic, the per-lane total is the same bounded value -- so an iteration starts
+// its b sums at (-c1, -c2) and needs no J - I subtraction). An odd NR leaves a last
+// row: with ODD = false it is closed by a zero row (one more pair, half empty); with
+// ODD = true its raw sums are returned (li, lx, ly) for odd_pair_setup, which pairs
+// the last rows of two strips.
+__device__ __forceinline__ void pair_setup(unsigned I2, unsigned GXm, unsigned GYm, int& a11, int& a12, int& a22,
+                                           int& c1, int& c2) {
+    a11 = sdot2(GXm, GXm, a11);
+    a12 = sdot2(GXm, GYm, a12);
+    a22 = sdot2(GYm, GYm, a22);
+    c1 = sdot2(I2, GXm, c1);
+    c2 = sdot2(I2, GYm, c2);
+}
+template <int NR, bool ODD>
+__device__ __forceinline__ void strip_setup_c(const unsigned* P, const u32x2a4* D, unsigned IW0, unsigned IW1,
+                                              unsigned GW0, unsigned GW1, unsigned* GX, unsigned* GY, int& a11,
+                                              int& a12, int& a22, int& c1, int& c2, int& li, int& lx, int& ly) {
+    constexpr int NP = ODD ? NR / 2 : (NR + 1) / 2;
     const int rnd_i = 1 << (W_BITS - 6), rnd_d = 1 << (W_BITS + kDerShift - 1);
-    int iv[2 * NP], gx[2 * NP], gy[2 * NP];
-    iv[2 * NP - 1] = gx[2 * NP - 1] = gy[2 * NP - 1] = 0;
+    int iv[NR + 1], gx[NR + 1], gy[NR + 1];
+    iv[NR] = gx[NR] = gy[NR] = 0;
 #pragma unroll
     for (int j = 0; j < NR; j++) {
         iv[j] = sdot2(P[j], IW0, sdot2_r(P[j + 1], IW1, rnd_i)) >> (W_BITS - 5);
@@ -982,31 +996,22 @@ __device__ __forceinline__ void strip_setup(const unsigned* P, const u32x2a4* D,
     static_assert(W_BITS + kDerShift == 16, "derivative sums must carry their descaled value in bits 16..31");
 #pragma unroll
     for (int m = 0; m < NP; m++) {
-        I2[m] = lo16x2(iv[2 * m], iv[2 * m + 1]);
         GX[m] = hi16x2(gx[2 * m], gx[2 * m + 1]);
         GY[m] = hi16x2(gy[2 * m], gy[2 * m + 1]);
-        a11 = sdot2(GX[m], GX[m], a11);
-        a12 = sdot2(GX[m], GY[m], a12);
-        a22 = sdot2(GY[m], GY[m], a22);
+        pair_setup(lo16x2(iv[2 * m], iv[2 * m + 1]), GX[m], GY[m], a11, a12, a22, c1, c2);
+    }
+    if constexpr (ODD) {
+        li = iv[NR - 1];
+        lx = gx[NR - 1];
+        ly = gy[NR - 1];
     }
 }
-
-// strip_setup, returning per-lane sums c1 += I.Ix, c2 += I.Iy over the strip's
-// pixels instead of the I pairs: sum (J - I) G = sum J G - sum I G exactly
-// (int32 wrap-around arithmetic; the per-lane total is the same bounded value),
-// so an iteration starts its b sums at (-c1, -c2) and needs no J - I subtraction.
-template <int NR>
-__device__ __forceinline__ void strip_setup_c(const unsigned* P, const u32x2a4* D, unsigned IW0, unsigned IW1,
-                                              unsigned GW0, unsigned GW1, unsigned* GX, unsigned* GY, int& a11,
-                                              int& a12, int& a22, int& c1, int& c2) {
-    constexpr int NP = (NR + 1) / 2;
-    unsigned I2[NP];
-    strip_setup<NR>(P, D, IW0, IW1, GW0, GW1, I2, GX, GY, a11, a12, a22);
-#pragma unroll
-    for (int m = 0; m < NP; m++) {
-        c1 = sdot2(I2[m], GX[m], c1);
-        c2 = sdot2(I2[m], GY[m], c2);
-    }
+// the last rows of strips k (i0 ..) and k + 1 (i1 ..) as one pair
+__device__ __forceinline__ void odd_pair_setup(int i0, int x0, int y0, int i1, int x1, int y1, unsigned& GXm,
+                                               unsigned& GYm, int& a11, int& a12, int& a22, int& c1, int& c2) {
+    GXm = hi16x2(x0, x1);
+    GYm = hi16x2(y0, y1);
+    pair_setup(lo16x2(i0, i1), GXm, GYm, a11, a12, a22, c1, c2);
 }
 
 // Staging geometry of a JRW x JRH pair region (JRW = 2 mod 4): each lane loads one
@@ -1111,14 +1116,18 @@ __device__ __forceinline__ void stage_padded(unsigned* dst, const ImgLevel& L, i
 // pattern at the same offsets of their own regions: at a multiple of 32 dwords
 // apart every read of the pair collided (2-way), 16 banks apart they take disjoint
 // halves.
-template <int QJM, int WW = 21, int WH = 21>
+// With FPW = 8 (groups of 8 lanes, four per 32-lane half) the residue is 24: the four
+// groups of a half then take the bank octets 0, 24, 16, 8 (and 8 x 2,528 B still
+// admits two waves per SIMD; a residue of 8 would not).
+template <int QJM, int WW = 21, int WH = 21, int FPW = 4>
 struct MultiShape {
     static constexpr int JRW0 = WW + 2 * QJM + 3;                  // entries the margin needs
     static constexpr int JRW = JRW0 + (6 - JRW0 % 4) % 4;          // rounded up to 4k + 2
     static constexpr int JRH = WH + 1 + 2 * QJM;
     static constexpr int JBYTES = JRW * JRH * 4;
-    static constexpr int JSTRIDE = ((JBYTES / 4 + 15) / 32 * 32 + 16) * 4;
-    static_assert(JSTRIDE >= JBYTES && (JSTRIDE / 4) % 32 == 16 && JSTRIDE - JBYTES < 128, "group stride");
+    static constexpr int RES = FPW == 8 ? 24 : 16;
+    static constexpr int JSTRIDE = (JBYTES / 4 + ((RES - JBYTES / 4) % 32 + 32) % 32) * 4;
+    static_assert(JSTRIDE >= JBYTES && (JSTRIDE / 4) % 32 == RES && JSTRIDE - JBYTES < 128, "group stride");
     static_assert(JRW % 4 == 2 && JRW >= JRW0 && JRW < JRW0 + 4, "entries 4k + 2");
 };
 
@@ -1127,6 +1136,8 @@ struct MultiShape {
 // the partial sums provably fit (STEPS32), then 16-bit halves.
 template <int LPF, int STEPS32>
 __device__ __forceinline__ int group_add_step(int v, int step) {
+    // groups of 8 lanes: the third step adds the other quad of the half-row
+    if (LPF == 8 && step == 2) return dpp_row_add<0x141>(v);  // row_half_mirror
     switch (step) {
         case 0: return dpp_row_add<0xb1>(v);   // quad_perm 1,0,3,2
         case 1: return dpp_row_add<0x4e>(v);   // quad_perm 2,3,0,1
@@ -1137,8 +1148,8 @@ __device__ __forceinline__ int group_add_step(int v, int step) {
 }
 template <int LPF, int STEPS32, int NV>
 __device__ __forceinline__ void group_sum_f(int (&v)[NV], float (&f)[NV]) {
-    constexpr int STEPS = LPF == 16 ? 4 : 5;
-    static_assert(LPF == 16 || LPF == 32, "groups of 16 or 32 lanes");
+    constexpr int STEPS = LPF == 8 ? 3 : LPF == 16 ? 4 : 5;
+    static_assert(LPF == 8 || LPF == 16 || LPF == 32, "groups of 8, 16 or 32 lanes");
 #pragma unroll
     for (int s = 0; s < STEPS32; s++)
 #pragma unroll
@@ -1162,14 +1173,18 @@ __device__ __forceinline__ void group_sum_f(int (&v)[NV], float (&f)[NV]) {
 
 template <int FPW, int QJM, int MINW, int KKS = 2, int WW = 21, int WH = 21, int NR = 7>
 __global__ __launch_bounds__(64, MINW) void lk_multi_kernel(LKBatch B, LKDev p) {
-    using Q = MultiShape<QJM, WW, WH>;
+    using Q = MultiShape<QJM, WW, WH, FPW>;
     static_assert(WH % NR == 0, "whole strips");
     static_assert(WW + QJM + 3 <= kPyrPad && WW + 1 <= kDerPad, "padding too small for the window");
     constexpr int JRW = Q::JRW, JRH = Q::JRH;
-    constexpr int NP = (NR + 1) / 2;              // row pairs per strip (an odd NR closes with a zero row)
     constexpr int NSTRIP = WW * (WH / NR);
     constexpr int LPF = 64 / FPW;                 // lanes per feature
     constexpr int K = (NSTRIP + LPF - 1) / LPF;   // strips per lane
+    // an odd strip height pairs the last rows of strips 2i and 2i + 1 (ODD; K even),
+    // otherwise the last row is closed by a zero row
+    constexpr bool ODD = NR % 2 == 1 && K % 2 == 0;
+    constexpr int NP = ODD ? NR / 2 : (NR + 1) / 2;  // full row pairs per strip
+    constexpr int NO = ODD ? K / 2 : 1;              // odd-row pairs per lane
     // int32 partial sums: a lane holds <= NR K products |diff * g| <= 8160 * 4080
     // (A sums: 4080^2); steps while 2^steps * NR K * 8160 * 4080 < 2^31
     constexpr long long kProd = (long long)NR * K * 8160 * 4080;
@@ -1265,7 +1280,8 @@ __global__ __launch_bounds__(64, MINW) void lk_multi_kernel(LKBatch B, LKDev p) 
         int jx0 = ufloor(nextx - halfWx) - QJM, jy0 = ufloor(nexty - halfWy) - QJM;
         int jxa = jx0 & ~3;
         int jbase = jy0 * JRW + jxa;  // the region origin as an entry offset (iny * JRW + inx - jbase)
-        unsigned GX[K][NP], GY[K][NP];
+        unsigned GX[K][NP], GY[K][NP], GXO[NO], GYO[NO];
+        int li[K], lx[K], ly[K];  // (ODD) the strips' last rows until paired
         int asum[3] = {0, 0, 0};
         int csum[2] = {0, 0};  // sum I.Ix, I.Iy over the lane's strips
         {
@@ -1332,8 +1348,12 @@ __global__ __launch_bounds__(64, MINW) void lk_multi_kernel(LKBatch B, LKDev p) 
                 for (int k = 0; k < K; k++) {
                     if (k + 1 < K) load_strip(k + 1, P[(k + 1) & 1], Dv[(k + 1) & 1]);
                     __builtin_amdgcn_sched_barrier(0);
-                    strip_setup_c<NR>(P[k & 1], Dv[k & 1], IW0, IW1, sreal[k] ? IW0 : 0u, sreal[k] ? IW1 : 0u,
-                                      GX[k], GY[k], asum[0], asum[1], asum[2], csum[0], csum[1]);
+                    strip_setup_c<NR, ODD>(P[k & 1], Dv[k & 1], IW0, IW1, sreal[k] ? IW0 : 0u, sreal[k] ? IW1 : 0u,
+                                           GX[k], GY[k], asum[0], asum[1], asum[2], csum[0], csum[1], li[k], lx[k],
+                                           ly[k]);
+                    if (ODD && (k & 1))
+                        odd_pair_setup(li[k - 1], lx[k - 1], ly[k - 1], li[k], lx[k], ly[k], GXO[k / 2], GYO[k / 2],
+                                       asum[0], asum[1], asum[2], csum[0], csum[1]);
                     __builtin_amdgcn_sched_barrier(0);
                 }
             } else {
@@ -1349,8 +1369,12 @@ __global__ __launch_bounds__(64, MINW) void lk_multi_kernel(LKBatch B, LKDev p) 
 #pragma unroll
                     for (int kk = 0; kk < KK; kk++) {
                         const int k = k0 + kk;
-                        strip_setup_c<NR>(P[kk], Dv[kk], IW0, IW1, sreal[k] ? IW0 : 0u, sreal[k] ? IW1 : 0u, GX[k],
-                                          GY[k], asum[0], asum[1], asum[2], csum[0], csum[1]);
+                        strip_setup_c<NR, ODD>(P[kk], Dv[kk], IW0, IW1, sreal[k] ? IW0 : 0u, sreal[k] ? IW1 : 0u,
+                                               GX[k], GY[k], asum[0], asum[1], asum[2], csum[0], csum[1], li[k],
+                                               lx[k], ly[k]);
+                        if (ODD && (k & 1))
+                            odd_pair_setup(li[k - 1], lx[k - 1], ly[k - 1], li[k], lx[k], ly[k], GXO[k / 2],
+                                           GYO[k / 2], asum[0], asum[1], asum[2], csum[0], csum[1]);
                     }
                 }
             }
@@ -1411,31 +1435,53 @@ __global__ __launch_bounds__(64, MINW) void lk_multi_kernel(LKBatch B, LKDev p) 
             const BiW w = bilinear_weights(nextx - fnx, nexty - fny);
             const unsigned W0 = w.W0, W1 = w.W1;
             int bsum[2] = {-csum[0], -csum[1]};
+#ifdef SVO_LK_SPLITB
+            int bsum2[2] = {0, 0};  // odd strips: two shorter accumulation chains per sum
+#endif
             {
                 // (iny - jy0) JRW + (inx - jxa) as one 24-bit multiply-add against the
                 // region origin's offset; an inactive group reads inside its own region
                 // (results unused)
                 const int off = lact ? __mul24(iny, JRW) + inx - jbase : 0;
                 const unsigned* jb = jmine + off;
+                int jlast = 0;  // (ODD) the even strip's last row
 #pragma unroll
                 for (int k = 0; k < K; k++) {
                     const unsigned* js = jb + srow[k] * JRW + scol[k];
                     unsigned q[NR + 1];
 #pragma unroll
                     for (int r = 0; r <= NR; r++) q[r] = js[r * JRW];
-                    int jv[2 * NP];
-                    jv[2 * NP - 1] = 0;
+                    int jv[NR + 1];
+                    jv[NR] = 0;
 #pragma unroll
                     for (int r = 0; r < NR; r++)  // J x 2^kJShift: descaled value in bits 16..31
                         jv[r] = sdot2(q[r], W0, sdot2_r(q[r + 1], W1, rnd_j));
 #pragma unroll
                     for (int m = 0; m < NP; m++) {
                         const unsigned jj = hi16x2(jv[2 * m], jv[2 * m + 1]);  // J; the I part is in csum
-                        bsum[0] = sdot2(jj, GX[k][m], bsum[0]);
-                        bsum[1] = sdot2(jj, GY[k][m], bsum[1]);
+#ifdef SVO_LK_SPLITB
+                        int* bs = (k & 1) ? bsum2 : bsum;
+#else
+                        int* bs = bsum;
+#endif
+                        bs[0] = sdot2(jj, GX[k][m], bs[0]);
+                        bs[1] = sdot2(jj, GY[k][m], bs[1]);
+                    }
+                    if constexpr (ODD) {
+                        if (k & 1) {
+                            const unsigned jj = hi16x2(jlast, jv[NR - 1]);
+                            bsum[0] = sdot2(jj, GXO[k / 2], bsum[0]);
+                            bsum[1] = sdot2(jj, GYO[k / 2], bsum[1]);
+                        } else {
+                            jlast = jv[NR - 1];
+                        }
                     }
                 }
             }
+#ifdef SVO_LK_SPLITB
+            bsum[0] += bsum2[0];
+            bsum[1] += bsum2[1];
+#endif
             float fb[2];
             group_sum_f<LPF, STEPS32>(bsum, fb);
             // materialised here, ahead of the lane-divergent update below: sunk into
@@ -1482,7 +1528,7 @@ hipError_t launch_multi(const LKBatch& b, int nseq, int max_n, const LKDev& d, h
     // (no grid_hint: a block owns FPW features and does not loop; blocks past a
     // sequence's count return at once)
     dim3 grid((max_n + FPW - 1) / FPW, nseq);
-    constexpr int lds_bytes = FPW * MultiShape<QJM, WW, WH>::JSTRIDE;
+    constexpr int lds_bytes = FPW * MultiShape<QJM, WW, WH, FPW>::JSTRIDE;
     hipLaunchKernelGGL((lk_multi_kernel<FPW, QJM, MINW, KKS, WW, WH, NR>), grid, dim3(64), lds_bytes, st, b, d);
     return hipGetLastError();
 }
@@ -1577,6 +1623,9 @@ hipError_t launch_lk(const LKBatch& b, int nseq, int max_n, const LKParams& lp, 
                 case 41: return launch_multi<4, 1, 4, 1>(b, nseq, max_n, d, st);
                 case 40: return launch_multi<4, 1, 4, 0>(b, nseq, max_n, d, st);
                 case 30: return launch_multi<4, 1, 3, 0>(b, nseq, max_n, d, st);
+                case 82: return launch_multi<8, 1, 2, 2>(b, nseq, max_n, d, st);
+                case 81: return launch_multi<8, 1, 2, 1>(b, nseq, max_n, d, st);
+                case 84: return launch_multi<8, 1, 2, 4>(b, nseq, max_n, d, st);
                 default: return launch_multi<4, 1, 3>(b, nseq, max_n, d, st);
             }
         }

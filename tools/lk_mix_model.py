@@ -52,7 +52,8 @@ def cls(op):
     return "fast" if op in FAST else "slow"
 
 
-def kernel_asm(path):
+def kernel_asm(path, kernel=None):
+    KERNEL = kernel or globals()["KERNEL"]
     text = open(path).read().splitlines()
     start = next(i for i, l in enumerate(text) if l.startswith("_Z") and KERNEL in l and l.rstrip().endswith(":")
                  or (l.startswith("_Z") and KERNEL in l.split(":")[0]))
@@ -94,6 +95,7 @@ def main():
     ap.add_argument("--levels", type=float, default=4.0)
     ap.add_argument("--iters", type=float, default=16.5)
     ap.add_argument("--rare", type=float, default=0.05, help="re-staging executions per iteration")
+    ap.add_argument("--kernel", default=KERNEL, help="mangled-name fragment of the instance")
     ap.add_argument("--json", default=None, help="write the result here (bench.py reads profiles/lk_issue_model.json)")
     a = ap.parse_args()
     path = a.asm
@@ -103,7 +105,7 @@ def main():
                f"-I{REPO}/svo_amd/csrc", "--offload-arch=gfx950", "--cuda-device-only", "-S",
                f"{REPO}/svo_amd/csrc/lk.hip", "-o", path]
         subprocess.run(cmd, check=True)
-    bl = blocks(kernel_asm(path))
+    bl = blocks(kernel_asm(path, a.kernel))
     w_of = {0: 1.0, 1: a.levels, 2: a.iters}
     tot_n = tot_ns = 0.0
     by_cls = {"fast": 0.0, "slow": 0.0}
