@@ -1631,8 +1631,15 @@ hipError_t launch_lk(const LKBatch& b, int nseq, int max_n, const LKParams& lp, 
         }
         // the stereo call's 11 x 11 (findLeftFeaturesInRight, no err): four
         // features per wave too, one 11-row strip per lane (11 of 16 lanes)
-        if (lp.win_w == 11 && lp.win_h == 11 && multi_ok && lp.quad)
+        if (lp.win_w == 11 && lp.win_h == 11 && multi_ok && lp.quad) {
+            // SVO_LK_STEREO_FPW (A/B only): 8 features per wave, two strips per lane
+            static const int sfpw = [] {
+                const char* e = std::getenv("SVO_LK_STEREO_FPW");
+                return e ? std::atoi(e) : 4;
+            }();
+            if (sfpw == 8) return launch_multi<8, 1, 4, 1, 11, 11, 11>(b, nseq, max_n, d, st);
             return launch_multi<4, 1, 4, 1, 11, 11, 11>(b, nseq, max_n, d, st);
+        }
         if (lp.win_w == 21 && lp.win_h == 21) return launch_fast<21, 21>(b, nseq, max_n, d, st);
         if (lp.win_w == 11 && lp.win_h == 11) return launch_fast<11, 11>(b, nseq, max_n, d, st);
         if (lp.win_w == 15 && lp.win_h == 15) return launch_fast<15, 15>(b, nseq, max_n, d, st);
