@@ -132,7 +132,7 @@ P
 
 run_lksplit() {
     for c in 1 2 50; do local T=/tmp/lks_$c
-        timeout -s KILL 90 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAVES SQ_BUSY_CYCLES SQ_INSTS_VMEM \
+        timeout -s KILL 90 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAVES SQ_BUSY_CYCLES SQ_INSTS_VMEM SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS \
             -d $T -o run --output-format csv -- python tools/microbench.py lk --points 128000 --reps 2 --count $c \
             > $T.log 2>&1 || fail lksplit-pmc $T.log
         timeout -k 10 90 rocprofv3 --kernel-trace --stats -d ${T}k -o run --output-format csv -- \
