@@ -1444,6 +1444,9 @@ __global__ __launch_bounds__(64, MINW) void lk_multi_kernel(LKBatch B, LKDev p) 
                 // (results unused)
                 const int off = lact ? __mul24(iny, JRW) + inx - jbase : 0;
                 const unsigned* jb = jmine + off;
+#ifndef SVO_LK_NO_SETPRIO
+                __builtin_amdgcn_s_setprio(0);  // the bulk dot2 work: ordinary priority
+#endif
                 int jlast = 0;  // (ODD) the even strip's last row
 #pragma unroll
                 for (int k = 0; k < K; k++) {
@@ -1483,6 +1486,11 @@ __global__ __launch_bounds__(64, MINW) void lk_multi_kernel(LKBatch B, LKDev p) 
             bsum[1] += bsum2[1];
 #endif
             float fb[2];
+#ifndef SVO_LK_NO_SETPRIO
+            // the serial tail (reduction -> solve -> next weights / address): raised so
+            // that this wave's dependent chain issues ahead of the others' bulk work
+            __builtin_amdgcn_s_setprio(2);
+#endif
             group_sum_f<LPF, STEPS32>(bsum, fb);
             // materialised here, ahead of the lane-divergent update below: sunk into
             // it, the last DPP step splits into v_mov_dpp + a separate add per value
