@@ -55,6 +55,12 @@ extern "C" {
 #define SVO_TERM_EPS 2
 #define SVO_LK_USE_INITIAL_FLOW 4
 #define SVO_LK_GET_MIN_EIGENVALS 8
+/* Not an OpenCV flag: sum LK's normal equations in OpenCV's own float order
+ * (LKTrackerInvoker's SSE build: four float lanes + a scalar tail, then its
+ * lane reduction) instead of exactly. With it the results are those of
+ * cv::calcOpticalFlowPyrLK's x86 build bit for bit; without it the sums are
+ * exact integers rounded once (order-independent). */
+#define SVO_LK_OPENCV_ORDER 0x10000
 
 typedef struct svo_ctx svo_ctx;
 typedef struct svo_image svo_image; /* a device-resident 8U image + its pyramid */

@@ -33,7 +33,7 @@ import numpy as np
 
 __all__ = [
     "SvoError", "lib", "Context", "Image", "FastFeatureDetector",
-    "TERM_COUNT", "TERM_EPS", "LK_USE_INITIAL_FLOW", "LK_GET_MIN_EIGENVALS",
+    "TERM_COUNT", "TERM_EPS", "LK_USE_INITIAL_FLOW", "LK_GET_MIN_EIGENVALS", "LK_OPENCV_ORDER",
     "synth_canvas", "synth_frame", "synth_frame_right", "synth_view", "lib_path", "Frontend", "FrontendConfig", "FrontendStats",
 ]
 
@@ -42,6 +42,10 @@ TERM_EPS = 2
 LK_USE_INITIAL_FLOW = 4
 PYR_PAD = 32  # SVO_PYR_PAD: stored border of every pyramid level
 LK_GET_MIN_EIGENVALS = 8
+# SVO_LK_OPENCV_ORDER (not an OpenCV flag): LK's normal equations summed in OpenCV's
+# own float order (its SSE build) instead of exactly -- bit-identical to
+# cv::calcOpticalFlowPyrLK's x86 results (oracle ACC_SSE)
+LK_OPENCV_ORDER = 0x10000
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 

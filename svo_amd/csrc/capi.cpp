@@ -423,7 +423,8 @@ int svo_calc_optical_flow_pyr_lk(svo_ctx* ctx, const svo_image* prev, const svo_
     p.max_level = ml;
     p.max_count = max_count;
     p.eps2 = epsilon * epsilon;
-    p.flags = flags;
+    p.flags = flags & ~SVO_LK_OPENCV_ORDER;
+    p.cv_order = (flags & SVO_LK_OPENCV_ORDER) ? 1 : 0;
     p.min_eig = (float)min_eig_threshold;
     p.want_err = err ? 1 : 0;
     lk_apply_env(p);

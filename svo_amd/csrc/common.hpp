@@ -202,6 +202,7 @@ struct LKParams {
     int want_err;
     int generic = 0;  // 1: always use the runtime-window kernel (tests compare both)
     int quad = 1;     // 21x21: four features per wave; 0: one per wave (lk_fast_kernel)
+    int cv_order = 0; // 1: OpenCV's float summation order (SVO_LK_OPENCV_ORDER, lk_cv_kernel)
 };
 // A/B and test hooks of the kernel choice, read per call: SVO_LK_GENERIC=1 (the
 // runtime-window kernel for every window), SVO_LK_QUAD=0 (21x21 one per wave)

@@ -582,6 +582,7 @@ int fe_stereo_lk(svo_frontend* fe, int t, const int* counts, int max_n, hipStrea
     const double eps = std::min(std::max(c.stereo_epsilon, 0.0), 10.0);
     lp.eps2 = eps * eps;
     lp.flags = 0;
+    lp.cv_order = (c.lk_flags & SVO_LK_OPENCV_ORDER) ? 1 : 0;  // the config's order for both LK calls
     lp.min_eig = (float)c.min_eig;
     lp.want_err = 0;
     lk_apply_env(lp);
@@ -1342,7 +1343,8 @@ static LKParams fe_temporal_params(const svo_frontend* fe) {
     lp.max_count = std::min(std::max(c.lk_max_count, 0), 100);
     const double eps = std::min(std::max(c.lk_epsilon, 0.0), 10.0);
     lp.eps2 = eps * eps;
-    lp.flags = c.lk_flags & ~SVO_LK_USE_INITIAL_FLOW;
+    lp.flags = c.lk_flags & ~(SVO_LK_USE_INITIAL_FLOW | SVO_LK_OPENCV_ORDER);
+    lp.cv_order = (c.lk_flags & SVO_LK_OPENCV_ORDER) ? 1 : 0;
     lp.min_eig = (float)c.min_eig;
     lp.want_err = 0;
     lk_apply_env(lp);

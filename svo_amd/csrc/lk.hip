@@ -412,6 +412,383 @@ __global__ __launch_bounds__(256) void lk_kernel(LKBatch B, LKDev p) {
 }
 
 // ---------------------------------------------------------------------------
+// OpenCV's own float accumulation order (SVO_LK_OPENCV_ORDER): the normal
+// equations summed exactly as LKTrackerInvoker's SSE build sums them
+// (lkpyramid.cpp, the CV_SIMD128 paths; oracle/lk.c:109-157, 186-238 ACC_SSE):
+//  * A11 / A12 / A22: four float lanes over the columns x < se4 (lane x & 3,
+//    rows in order, columns in order within a row), a scalar float chain over
+//    the rest (row by row), then sA + ((q0 + q2) + (q1 + q3));
+//  * b1 / b2 per iteration: four float lanes per sum over x < se8, each adding
+//    float(d[x] G[x] + d[x+4] G[x+4]) for the 8-column blocks in order
+//    (x & 3 = lane), a scalar chain over the rest, then
+//    sb + ((c0 + c2 + 0) + (c1 + c3 + 0)).
+// Every term is an integer, so a float chain equals the exact integer sum
+// whenever the sum of the |terms| of the whole window stays <= 2^24 (every
+// partial sum, and every combination of them, is then an exactly representable
+// integer): the wave computes that bound beside the exact sums and runs the
+// ordered float chains (one lane per chain, the terms staged in LDS in chain
+// order) only when the bound fails. One feature per wave, the strip lane map of
+// lk_kernel; all else (fixed-point sampling, solve, exits, err) as lk_kernel.
+// The chains' term layout in LDS (per quantity, n = win_w * win_h ints):
+//   A (3 quantities): lane k < 4 at k*win_h*M4 + y*M4 + m (x = 4m + k),
+//                     scalar at 4*win_h*M4 + y*(win_w - se4) + (x - se4);
+//   b (2 quantities): lane t < 4 at t*win_h*2*B8 + y*2*B8 + 2*blk + h
+//                     (x = 8blk + t + 4h), scalar at win_h*se8 + y*(win_w - se8) + (x - se8).
+struct CvOrder {
+    int se4, se8;    // OpenCV's SIMD column ends: 4-wide covariance, 8-wide b loop
+    int term_off;    // byte offset of the chain terms in the wave's LDS
+};
+
+__device__ __forceinline__ float lane_f(float v, int l) {
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
+}
+constexpr int kExact24 = 1 << 24;
+
+template <int RPG, bool FULL>
+__global__ __launch_bounds__(64) void lk_cv_kernel(LKBatch B, LKDev p, CvOrder co) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    const int lane = threadIdx.x;
+    const int seq = blockIdx.y;
+    const int n = B.counts ? B.counts[seq] : B.n;
+    const int pt = blockIdx.x;
+    if (pt >= n) return;
+    const size_t base = (size_t)seq * B.cap;
+    const float* __restrict__ prev_xy = B.prev_xy + 2 * base;
+    float* __restrict__ next_xy = B.next_xy + 2 * base;
+    const PyrDesc& prev = B.prev[seq];
+    const PyrDesc& next = B.next[seq];
+    const DerivDesc& dprev = B.dprev[seq];
+    unsigned* ipair = reinterpret_cast<unsigned*>(lds);
+    unsigned* jreg = reinterpret_cast<unsigned*>(lds + p.ip_bytes);
+    int* terms = reinterpret_cast<int*>(lds + co.term_off);
+
+    const int win_w = p.win_w, win_h = p.win_h;
+    const int npx = win_w * win_h;
+    const int sc = lane % win_w;
+    const int sg = lane / win_w;
+    const bool strip = sg < p.groups;
+    const int r0 = sg * RPG;
+    const int i_rpp = 64 / p.ip_w, i_lr = lane / p.ip_w, i_lc = lane - i_lr * p.ip_w;
+    const int j_rpp = 64 / p.jr_w, j_lr = lane / p.jr_w, j_lc = lane - j_lr * p.jr_w;
+
+    // this lane's column in the chain layouts (slot of row y = base + y * stride)
+    const int se4 = co.se4, se8 = co.se8, M4 = se4 >> 2, B8 = se8 >> 3;
+    int a_base, a_stride, b_base, b_stride;
+    if (sc < se4) {
+        a_base = (sc & 3) * win_h * M4 + (sc >> 2);
+        a_stride = M4;
+    } else {
+        a_base = 4 * win_h * M4 + (sc - se4);
+        a_stride = win_w - se4;
+    }
+    if (sc < se8) {
+        b_base = (sc & 3) * win_h * 2 * B8 + 2 * (sc >> 3) + ((sc >> 2) & 1);
+        b_stride = 2 * B8;
+    } else {
+        b_base = win_h * se8 + (sc - se8);
+        b_stride = win_w - se8;
+    }
+    // chain lanes: A: lane = 5q + k (q: A11, A12, A22; k < 4 SIMD lane, 4 scalar);
+    // b: lane = 5q + k (q: b1, b2)
+    const int cq = lane / 5, ck = lane - 5 * (lane / 5);
+    const int a_len = ck < 4 ? win_h * M4 : win_h * (win_w - se4);
+    const int* a_src = terms + cq * npx + (ck < 4 ? ck * win_h * M4 : 4 * win_h * M4);
+    const int b_len = ck < 4 ? win_h * B8 : win_h * (win_w - se8);
+    const int b_step = ck < 4 ? 2 : 1;
+    const int* b_src = terms + cq * npx + (ck < 4 ? ck * win_h * 2 * B8 : win_h * se8);
+
+    const float halfWx = (win_w - 1) * 0.5f, halfWy = (win_h - 1) * 0.5f;
+    const float px = uni_f(prev_xy[2 * pt]), py = uni_f(prev_xy[2 * pt + 1]);
+    float nx = 0.f, ny = 0.f;
+    if (p.flags & SVO_LK_USE_INITIAL_FLOW) {
+        nx = uni_f(next_xy[2 * pt]);
+        ny = uni_f(next_xy[2 * pt + 1]);
+    }
+    int st = 1;
+    float errv = 0.f;
+    int itcount = 0;
+    const int max_level = p.max_level;
+
+    for (int level = max_level; level >= 0; level--) {
+        const ImgLevel I = prev.lv[level];
+        const ImgLevel J = next.lv[level];
+        const float lscale = (float)(1. / (1 << level));
+        float prevx = px * lscale, prevy = py * lscale;
+        float nextx, nexty;
+        if (level == max_level) {
+            if (p.flags & SVO_LK_USE_INITIAL_FLOW) {
+                nextx = nx * lscale;
+                nexty = ny * lscale;
+            } else {
+                nextx = prevx;
+                nexty = prevy;
+            }
+        } else {
+            nextx = nx * 2.f;
+            nexty = ny * 2.f;
+        }
+        nx = nextx;
+        ny = nexty;
+        prevx -= halfWx;
+        prevy -= halfWy;
+        const int ipx = uni_i(ufloor(prevx)), ipy = uni_i(ufloor(prevy));
+        if (ipx < -win_w || ipx >= I.w || ipy < -win_h || ipy >= I.h) {
+            if (level == 0) {
+                st = 0;
+                errv = 0.f;
+            }
+            continue;
+        }
+        float a = prevx - ipx, b = prevy - ipy;
+        const int iw00 = uround((1.f - a) * (1.f - b) * (1 << W_BITS));
+        const int iw01 = uround(a * (1.f - b) * (1 << W_BITS));
+        const int iw10 = uround((1.f - a) * b * (1 << W_BITS));
+        const int iw11 = (1 << W_BITS) - iw00 - iw01 - iw10;
+        const unsigned IW0 = pack16(iw00, iw01), IW1 = pack16(iw10, iw11);
+
+        int jx0 = uni_i(ufloor(nextx - halfWx)) - JM, jy0 = uni_i(ufloor(nexty - halfWy)) - JM;
+        stage_pairs(ipair, I, ipx, ipy, p.ip_w, p.ip_h, i_lr, i_lc, i_rpp);
+        stage_pairs(jreg, J, jx0, jy0, p.jr_w, p.jr_h, j_lr, j_lc, j_rpp);
+        uint32_t dv[RPG + 1][2];
+        {
+            const int dpitch = dprev.pitch[level];
+            gu32 dsrc = (gu32)dprev.data[level];
+            const bool full_in = ipx >= 0 && ipy >= 0 && ipx + win_w < I.w && ipy + win_h < I.h;
+            const int X = ipx + sc;
+            if (full_in) {
+                gu32 q = dsrc + (size_t)(ipy + r0) * dpitch + X;
+#pragma unroll
+                for (int k = 0; k <= RPG; k++) {
+                    dv[k][0] = dv[k][1] = 0;
+                    if (strip && (FULL || r0 + k <= win_h)) {
+                        dv[k][0] = q[(size_t)k * dpitch];
+                        dv[k][1] = q[(size_t)k * dpitch + 1];
+                    }
+                }
+            } else {
+                const bool c0 = X >= 0 && X < I.w, c1 = X + 1 >= 0 && X + 1 < I.w;
+#pragma unroll
+                for (int k = 0; k <= RPG; k++) {
+                    dv[k][0] = dv[k][1] = 0;
+                    const int Y = ipy + r0 + k;
+                    if (strip && (FULL || r0 + k <= win_h) && Y >= 0 && Y < I.h) {
+                        gu32 q = dsrc + (size_t)Y * dpitch + X;
+                        if (c0) dv[k][0] = q[0];
+                        if (c1) dv[k][1] = q[1];
+                    }
+                }
+            }
+        }
+        wave_lds_sync();
+
+        int ival[RPG], gix[RPG], giy[RPG];
+        int a11 = 0, a12 = 0, a22 = 0;
+        {
+            const unsigned* ip = ipair + r0 * p.ip_w + sc;
+            unsigned P0 = strip ? ip[0] : 0u;
+#pragma unroll
+            for (int j = 0; j < RPG; j++) {
+                ival[j] = gix[j] = giy[j] = 0;
+                if (strip && (FULL || r0 + j < win_h)) {
+                    const unsigned P1 = ip[(j + 1) * p.ip_w];
+                    ival[j] = sdot2(P0, IW0, sdot2(P1, IW1, 1 << (W_BITS - 6))) >> (W_BITS - 5);
+                    P0 = P1;
+                    const unsigned X0 = __builtin_amdgcn_perm(dv[j][1], dv[j][0], 0x05040100u);
+                    const unsigned X1 = __builtin_amdgcn_perm(dv[j + 1][1], dv[j + 1][0], 0x05040100u);
+                    const unsigned Y0 = __builtin_amdgcn_perm(dv[j][1], dv[j][0], 0x07060302u);
+                    const unsigned Y1 = __builtin_amdgcn_perm(dv[j + 1][1], dv[j + 1][0], 0x07060302u);
+                    constexpr int DS = W_BITS + kDerShift;
+                    const int ix = sdot2(X0, IW0, sdot2(X1, IW1, 1 << (DS - 1))) >> DS;
+                    const int iy = sdot2(Y0, IW0, sdot2(Y1, IW1, 1 << (DS - 1))) >> DS;
+                    gix[j] = ix;
+                    giy[j] = iy;
+                    a11 += ix * ix;
+                    a12 += ix * iy;
+                    a22 += iy * iy;
+                }
+            }
+        }
+        const double e11 = wave_sum_exact(a11), e12 = wave_sum_exact(a12), e22 = wave_sum_exact(a22);
+        float A11, A12, A22;
+        // sum |Ix Iy| <= (sum Ix^2 + sum Iy^2) / 2: every chain exact under these bounds
+        if (e11 <= kExact24 && e22 <= kExact24 && e11 + e22 <= 2.0 * kExact24) {
+            A11 = (float)e11 * FLT_SCALE;
+            A12 = (float)e12 * FLT_SCALE;
+            A22 = (float)e22 * FLT_SCALE;
+        } else {
+            if (strip) {
+#pragma unroll
+                for (int j = 0; j < RPG; j++) {
+                    if (FULL || r0 + j < win_h) {
+                        const int s = a_base + (r0 + j) * a_stride;
+                        terms[s] = gix[j] * gix[j];
+                        terms[npx + s] = gix[j] * giy[j];
+                        terms[2 * npx + s] = giy[j] * giy[j];
+                    }
+                }
+            }
+            wave_lds_sync();
+            float acc = 0.f;
+            if (lane < 15)
+                for (int i = 0; i < a_len; i++) acc += (float)a_src[i];
+            wave_lds_sync();
+            A11 = (lane_f(acc, 4) + ((lane_f(acc, 0) + lane_f(acc, 2)) + (lane_f(acc, 1) + lane_f(acc, 3)))) *
+                  FLT_SCALE;
+            A12 = (lane_f(acc, 9) + ((lane_f(acc, 5) + lane_f(acc, 7)) + (lane_f(acc, 6) + lane_f(acc, 8)))) *
+                  FLT_SCALE;
+            A22 = (lane_f(acc, 14) + ((lane_f(acc, 10) + lane_f(acc, 12)) + (lane_f(acc, 11) + lane_f(acc, 13)))) *
+                  FLT_SCALE;
+        }
+
+        float D = A11 * A22 - A12 * A12;
+        float minEig = (A22 + A11 - sqrtf((A11 - A22) * (A11 - A22) + 4.f * A12 * A12)) /
+                       (float)(2 * win_w * win_h);
+        if (p.want_err && (p.flags & SVO_LK_GET_MIN_EIGENVALS)) errv = minEig;
+        if (minEig < p.min_eig || D < FLT_EPSILON) {
+            if (level == 0) st = 0;
+            wave_lds_sync();
+            continue;
+        }
+        D = 1.f / D;
+
+        nextx -= halfWx;
+        nexty -= halfWy;
+        float pdx = 0.f, pdy = 0.f;
+        for (int j = 0; j < p.max_count; j++) {
+            const int inx = uni_i(ufloor(nextx)), iny = uni_i(ufloor(nexty));
+            if (inx < -win_w || inx >= J.w || iny < -win_h || iny >= J.h) {
+                if (level == 0) st = 0;
+                break;
+            }
+            itcount++;
+            if (inx < jx0 || inx > jx0 + 2 * JM || iny < jy0 || iny > jy0 + 2 * JM) {
+                jx0 = inx - JM;
+                jy0 = iny - JM;
+                wave_lds_sync();
+                stage_pairs(jreg, J, jx0, jy0, p.jr_w, p.jr_h, j_lr, j_lc, j_rpp);
+                wave_lds_sync();
+            }
+            a = nextx - inx;
+            b = nexty - iny;
+            const int w00 = uround((1.f - a) * (1.f - b) * (1 << W_BITS));
+            const int w01 = uround(a * (1.f - b) * (1 << W_BITS));
+            const int w10 = uround((1.f - a) * b * (1 << W_BITS));
+            const int w11 = (1 << W_BITS) - w00 - w01 - w10;
+            const unsigned W0 = pack16(w00, w01), W1 = pack16(w10, w11);
+            int b1 = 0, b2 = 0, babs = 0;
+            int pb1[RPG], pb2[RPG];
+            if (strip) {
+                const unsigned* jp = jreg + (iny - jy0 + r0) * p.jr_w + (inx - jx0 + sc);
+                unsigned p0 = jp[0];
+#pragma unroll
+                for (int k = 0; k < RPG; k++) {
+                    pb1[k] = pb2[k] = 0;
+                    if (FULL || r0 + k < win_h) {
+                        const unsigned p1 = jp[(k + 1) * p.jr_w];
+                        const int jv = sdot2(p0, W0, sdot2(p1, W1, 1 << (W_BITS - 6))) >> (W_BITS - 5);
+                        const int diff = jv - ival[k];
+                        pb1[k] = diff * gix[k];
+                        pb2[k] = diff * giy[k];
+                        b1 += pb1[k];
+                        b2 += pb2[k];
+                        // |terms| <= 8160 * 4080 < 2^25: capped per lane so 64 lanes cannot overflow
+                        babs = min(babs + abs(pb1[k]) + abs(pb2[k]), kExact24 + 1);
+                        p0 = p1;
+                    }
+                }
+            }
+            float fb1, fb2;
+            if (dpp_sum(babs) <= kExact24) {
+                fb1 = (float)wave_sum_exact(b1) * FLT_SCALE;
+                fb2 = (float)wave_sum_exact(b2) * FLT_SCALE;
+            } else {
+                if (strip) {
+#pragma unroll
+                    for (int k = 0; k < RPG; k++) {
+                        if (FULL || r0 + k < win_h) {
+                            const int s = b_base + (r0 + k) * b_stride;
+                            terms[s] = pb1[k];
+                            terms[npx + s] = pb2[k];
+                        }
+                    }
+                }
+                wave_lds_sync();
+                float acc = 0.f;
+                if (lane < 10)
+                    for (int i = 0; i < b_len; i++) {
+                        const int* q = b_src + i * b_step;
+                        acc += (float)(q[0] + (b_step == 2 ? q[1] : 0));
+                    }
+                wave_lds_sync();
+                fb1 = (lane_f(acc, 4) + (((lane_f(acc, 0) + lane_f(acc, 2)) + 0.f) +
+                                         ((lane_f(acc, 1) + lane_f(acc, 3)) + 0.f))) * FLT_SCALE;
+                fb2 = (lane_f(acc, 9) + (((lane_f(acc, 5) + lane_f(acc, 7)) + 0.f) +
+                                         ((lane_f(acc, 6) + lane_f(acc, 8)) + 0.f))) * FLT_SCALE;
+            }
+            const float dx = (A12 * fb2 - A22 * fb1) * D;
+            const float dy = (A12 * fb1 - A11 * fb2) * D;
+            nextx += dx;
+            nexty += dy;
+            nx = nextx + halfWx;
+            ny = nexty + halfWy;
+            if ((double)dx * dx + (double)dy * dy <= p.eps2) break;
+            if (j > 0 && (double)fabsf(dx + pdx) < 0.01 && (double)fabsf(dy + pdy) < 0.01) {
+                nx -= dx * 0.5f;
+                ny -= dy * 0.5f;
+                break;
+            }
+            pdx = dx;
+            pdy = dy;
+        }
+
+        if (st && p.want_err && level == 0 && !(p.flags & SVO_LK_GET_MIN_EIGENVALS)) {
+            // SAD: sum |diff| <= 2048 * 8160 < 2^24, exact in any order
+            const float npx_ = nx - halfWx, npy_ = ny - halfWy;
+            const int ix0 = uni_i(ufloor(npx_)), iy0 = uni_i(ufloor(npy_));
+            if (ix0 < -win_w || ix0 >= J.w || iy0 < -win_h || iy0 >= J.h) {
+                st = 0;
+                continue;
+            }
+            if (ix0 < jx0 || ix0 > jx0 + 2 * JM || iy0 < jy0 || iy0 > jy0 + 2 * JM) {
+                jx0 = ix0 - JM;
+                jy0 = iy0 - JM;
+                wave_lds_sync();
+                stage_pairs(jreg, J, jx0, jy0, p.jr_w, p.jr_h, j_lr, j_lc, j_rpp);
+                wave_lds_sync();
+            }
+            float aa = npx_ - ix0, bb = npy_ - iy0;
+            const int w00 = uround((1.f - aa) * (1.f - bb) * (1 << W_BITS));
+            const int w01 = uround(aa * (1.f - bb) * (1 << W_BITS));
+            const int w10 = uround((1.f - aa) * bb * (1 << W_BITS));
+            const int w11 = (1 << W_BITS) - w00 - w01 - w10;
+            const unsigned W0 = pack16(w00, w01), W1 = pack16(w10, w11);
+            int sad = 0;
+            if (strip) {
+                const unsigned* jp = jreg + (iy0 - jy0 + r0) * p.jr_w + (ix0 - jx0 + sc);
+#pragma unroll
+                for (int k = 0; k < RPG; k++) {
+                    if (FULL || r0 + k < win_h) {
+                        const int jv = sdot2(jp[k * p.jr_w], W0, sdot2(jp[(k + 1) * p.jr_w], W1,
+                                                                       1 << (W_BITS - 6))) >> (W_BITS - 5);
+                        const int diff = jv - ival[k];
+                        sad += diff < 0 ? -diff : diff;
+                    }
+                }
+            }
+            errv = (float)wave_sum_exact(sad) * 1.f / (float)(32 * win_w * win_h);
+        }
+        wave_lds_sync();
+    }
+    if (lane == 0) {
+        next_xy[2 * pt] = nx;
+        next_xy[2 * pt + 1] = ny;
+        B.status[base + pt] = (uint8_t)st;
+        if (B.err) B.err[base + pt] = errv;
+        if (B.iters) B.iters[base + pt] = itcount;
+    }
+}
+
+// ---------------------------------------------------------------------------
 // Specialised kernel for compile-time window sizes (the reference's 21x21 and
 // 11x11, plus 15x15 / 31x31). Same semantics and lane map as lk_kernel; the
 // differences are all instruction count:
@@ -1562,6 +1939,21 @@ hipError_t launch_rpg(const LKBatch& b, int nseq, int max_n, const LKDev& d, hip
     return hipGetLastError();
 }
 
+template <int RPG>
+hipError_t launch_cv_rpg(const LKBatch& b, int nseq, int max_n, const LKDev& d, hipStream_t st) {
+    CvOrder co;
+    co.se4 = d.win_w >= 4 ? ((d.win_w - 4) / 4 + 1) * 4 : 0;
+    co.se8 = d.win_w >= 8 ? ((d.win_w - 8) / 8 + 1) * 8 : 0;
+    co.term_off = (d.lds_wave + 15) & ~15;
+    const int lds = co.term_off + 3 * d.win_w * d.win_h * 4;
+    dim3 grid(max_n, nseq);
+    if (d.groups * RPG == d.win_h)
+        hipLaunchKernelGGL((lk_cv_kernel<RPG, true>), grid, dim3(64), lds, st, b, d, co);
+    else
+        hipLaunchKernelGGL((lk_cv_kernel<RPG, false>), grid, dim3(64), lds, st, b, d, co);
+    return hipGetLastError();
+}
+
 }  // namespace
 
 void lk_apply_env(LKParams& p) {
@@ -1609,6 +2001,20 @@ hipError_t launch_lk(const LKBatch& b, int nseq, int max_n, const LKParams& lp, 
             return !(e && e[0] == '0');
         }();
         d.xcd = lk_xcd ? 1 : 0;
+    }
+    if (lp.cv_order) {
+        // OpenCV's float summation order: one feature per wave (lk_cv_kernel)
+#define SVO_LK_CV_CASE(R) \
+    case R: return launch_cv_rpg<R>(b, nseq, max_n, d, st);
+        switch (rpg) {
+            SVO_LK_CV_CASE(1) SVO_LK_CV_CASE(2) SVO_LK_CV_CASE(3) SVO_LK_CV_CASE(4) SVO_LK_CV_CASE(5)
+            SVO_LK_CV_CASE(6) SVO_LK_CV_CASE(7) SVO_LK_CV_CASE(8) SVO_LK_CV_CASE(11) SVO_LK_CV_CASE(16)
+            default:
+                break;
+        }
+#undef SVO_LK_CV_CASE
+        if (rpg <= 16) return launch_cv_rpg<16>(b, nseq, max_n, d, st);
+        return launch_cv_rpg<32>(b, nseq, max_n, d, st);
     }
     if (!lp.generic) {
         // four features per wave: the SAD error (flags 0 + want_err) stays on lk_fast_kernel

@@ -17,6 +17,10 @@ namespace svo {
 namespace {
 
 constexpr int kMaxLevel = Tracking::kImageLevels;  // maxLevel of both LK calls, R:src/tracking.cpp:104,163
+// Both LK calls sum in OpenCV's own float order: the drop-in returns what
+// cv::calcOpticalFlowPyrLK returns, bit for bit (the batched front end keeps the
+// exact sums by default).
+constexpr int kLkOrder = SVO_LK_OPENCV_ORDER;
 
 [[noreturn]] void fail(svo_ctx* ctx, const char* what) {
     throw std::runtime_error(std::string(what) + ": " + (ctx ? svo_last_error(ctx) : "no context"));
@@ -156,7 +160,7 @@ void Tracking::findLeftFeaturesInRight(StereoFrame* frame) const {
                                      frame->rightImg().device(mGpu, kMaxLevel),
                                      reinterpret_cast<const float*>(leftPoints.data()), (int)n,
                                      reinterpret_cast<float*>(rightPoints.data()), status.data(), error.data(), 11,
-                                     11, kMaxLevel, SVO_TERM_COUNT | SVO_TERM_EPS, 30, 0.001, 0, 1e-4) != SVO_OK)
+                                     11, kMaxLevel, SVO_TERM_COUNT | SVO_TERM_EPS, 30, 0.001, kLkOrder, 1e-4) != SVO_OK)
         fail(mGpu, "svo_calc_optical_flow_pyr_lk (stereo)");
 
     newLeftFeatures.reserve(n);
@@ -220,7 +224,7 @@ void Tracking::trackFrames(StereoFrame* prev, StereoFrame* curr) {
                                      curr->leftImg().device(mGpu, kMaxLevel),
                                      reinterpret_cast<const float*>(prevPoints.data()), (int)n,
                                      reinterpret_cast<float*>(currPoints.data()), status.data(), error.data(), 21, 21,
-                                     kMaxLevel, SVO_TERM_COUNT | SVO_TERM_EPS, 50, 0.001, SVO_LK_GET_MIN_EIGENVALS,
+                                     kMaxLevel, SVO_TERM_COUNT | SVO_TERM_EPS, 50, 0.001, SVO_LK_GET_MIN_EIGENVALS | kLkOrder,
                                      1e-4) != SVO_OK)
         fail(mGpu, "svo_calc_optical_flow_pyr_lk (temporal)");
 

@@ -5,6 +5,8 @@ triangulateNewMapPoints consumed and produced, R:src/tracking.cpp:74-230) is
 replayed through the CPU restatement on the same inputs.
 
 Bars: LK points/status, FAST keypoints, stereo LK, PnP inlier sets bit-identical;
+the mirror's two LK calls sum in OpenCV's own float order (SVO_LK_OPENCV_ORDER),
+so they are held to the oracle's ACC_SSE restatement of that order;
 triangulated points within 1e-5 relative (float DLT; OpenCV's SVD is not
 restated bit for bit); poses to 1e-7.
 """
@@ -92,7 +94,7 @@ def test_tracking_mirror_stagewise_parity(detector, features_to_track, colour):
             lk_prev, lk_next, st = tr.trace("lk_prev"), tr.trace("lk_next"), tr.trace("lk_status")
             assert np.array_equal(lk_prev, prev_xy)
             on, ost, _, _ = O.lk(frames[t - 1][0], L, lk_prev, (21, 21), 3, (3, 50, 1e-3),
-                                 O.LK_GET_MIN_EIGENVALS, want_err=False)
+                                 O.LK_GET_MIN_EIGENVALS, acc=O.ACC_SSE, want_err=False)
             assert np.array_equal(st, ost)
             assert np.array_equal(lk_next[st == 1].view(np.uint32), on[ost == 1].view(np.uint32))
             obj, img = tr.trace("pnp_obj"), tr.trace("pnp_img")
@@ -124,7 +126,7 @@ def test_tracking_mirror_stagewise_parity(detector, features_to_track, colour):
                 okp = O.fast(L, 20, True, mask)[:, :2]
             assert np.array_equal(kps, okp)
             sr, ss = tr.trace("stereo_right"), tr.trace("stereo_status")
-            on, ost, _, _ = O.lk(L, Rimg, kps, (11, 11), 3, (3, 30, 1e-3), 0)
+            on, ost, _, _ = O.lk(L, Rimg, kps, (11, 11), 3, (3, 30, 1e-3), 0, acc=O.ACC_SSE)
             assert np.array_equal(ss, ost) and np.array_equal(sr.view(np.uint32), on.view(np.uint32))
             kept = (ss == 1) & (np.abs(sr[:, 1] - kps[:, 1]) < 40)
             kl, kr = tr.trace("kept_left"), tr.trace("kept_right")
