@@ -927,13 +927,9 @@ __device__ __forceinline__ void wave_sum_f3(int x, int y, int z, float& fx, floa
 // otherwise picks v_dot2c (accumulator = destination) plus a v_mov of the
 // rounding constant for every use.
 __device__ __forceinline__ int sdot2_r(unsigned a, unsigned b, int c) {
-#ifdef SVO_SDOT2_BUILTIN
-    return sdot2(a, b, c);
-#else
     int d;
     asm("v_dot2_i32_i16 %0, %1, %2, %3" : "=v"(d) : "v"(a), "v"(b), "v"(c));
     return d;
-#endif
 }
 __device__ __forceinline__ unsigned pk_sub16(unsigned a, unsigned b) {
     return __builtin_bit_cast(unsigned, __builtin_bit_cast(s16x2, a) - __builtin_bit_cast(s16x2, b));
@@ -1493,16 +1489,14 @@ __device__ __forceinline__ void stage_padded(unsigned* dst, const ImgLevel& L, i
 // pattern at the same offsets of their own regions: at a multiple of 32 dwords
 // apart every read of the pair collided (2-way), 16 banks apart they take disjoint
 // halves.
-// With FPW = 8 (groups of 8 lanes, four per 32-lane half) the residue is 24: the four
-// groups of a half then take the bank octets 0, 24, 16, 8 (and 8 x 2,528 B still
-// admits two waves per SIMD; a residue of 8 would not).
 template <int QJM, int WW = 21, int WH = 21, int FPW = 4>
 struct MultiShape {
+    static_assert(FPW == 4, "four 16-lane groups per wave");
     static constexpr int JRW0 = WW + 2 * QJM + 3;                  // entries the margin needs
     static constexpr int JRW = JRW0 + (6 - JRW0 % 4) % 4;          // rounded up to 4k + 2
     static constexpr int JRH = WH + 1 + 2 * QJM;
     static constexpr int JBYTES = JRW * JRH * 4;
-    static constexpr int RES = FPW == 8 ? 24 : 16;
+    static constexpr int RES = 16;
     static constexpr int JSTRIDE = (JBYTES / 4 + ((RES - JBYTES / 4) % 32 + 32) % 32) * 4;
     static_assert(JSTRIDE >= JBYTES && (JSTRIDE / 4) % 32 == RES && JSTRIDE - JBYTES < 128, "group stride");
     static_assert(JRW % 4 == 2 && JRW >= JRW0 && JRW < JRW0 + 4, "entries 4k + 2");
@@ -1513,8 +1507,6 @@ struct MultiShape {
 // the partial sums provably fit (STEPS32), then 16-bit halves.
 template <int LPF, int STEPS32>
 __device__ __forceinline__ int group_add_step(int v, int step) {
-    // groups of 8 lanes: the third step adds the other quad of the half-row
-    if (LPF == 8 && step == 2) return dpp_row_add<0x141>(v);  // row_half_mirror
     switch (step) {
         case 0: return dpp_row_add<0xb1>(v);   // quad_perm 1,0,3,2
         case 1: return dpp_row_add<0x4e>(v);   // quad_perm 2,3,0,1
@@ -1525,8 +1517,8 @@ __device__ __forceinline__ int group_add_step(int v, int step) {
 }
 template <int LPF, int STEPS32, int NV>
 __device__ __forceinline__ void group_sum_f(int (&v)[NV], float (&f)[NV]) {
-    constexpr int STEPS = LPF == 8 ? 3 : LPF == 16 ? 4 : 5;
-    static_assert(LPF == 8 || LPF == 16 || LPF == 32, "groups of 8, 16 or 32 lanes");
+    constexpr int STEPS = LPF == 16 ? 4 : 5;
+    static_assert(LPF == 16 || LPF == 32, "groups of 16 or 32 lanes");
 #pragma unroll
     for (int s = 0; s < STEPS32; s++)
 #pragma unroll
@@ -1711,48 +1703,24 @@ __global__ __launch_bounds__(64, MINW) void lk_multi_kernel(LKBatch B, LKDev p) 
 #pragma unroll
                     for (int q = 0; q < SL::NPS; q++) sg.write(jregs + f * (Q::JSTRIDE / 4), sg.row(q), sv[f][q]);
             };
-            if constexpr (KKS == 0) {
-                // one strip ahead: strip k + 1's loads in flight while strip k is
-                // set up, and no further (the scheduling barriers keep the compiler
-                // from hoisting every strip's loads: 24 VGPRs per strip in flight)
-                unsigned P[2][NR + 1];
-                u32x2a4 Dv[2][NR + 1];
-                // the staging values die before any strip load is in flight
-                write_staging();
-                __builtin_amdgcn_sched_barrier(0);
-                load_strip(0, P[0], Dv[0]);
+            // strips KKS at a time: loads of a group in flight together
+            static_assert(KKS >= 1, "strips loaded per setup group");
 #pragma unroll
-                for (int k = 0; k < K; k++) {
-                    if (k + 1 < K) load_strip(k + 1, P[(k + 1) & 1], Dv[(k + 1) & 1]);
-                    __builtin_amdgcn_sched_barrier(0);
-                    strip_setup_c<NR, ODD>(P[k & 1], Dv[k & 1], IW0, IW1, sreal[k] ? IW0 : 0u, sreal[k] ? IW1 : 0u,
-                                           GX[k], GY[k], asum[0], asum[1], asum[2], csum[0], csum[1], li[k], lx[k],
-                                           ly[k]);
+            for (int k0 = 0; k0 < K; k0 += KKS) {
+                constexpr int KK = K >= KKS ? KKS : 1;
+                unsigned P[KK][NR + 1];
+                u32x2a4 Dv[KK][NR + 1];
+#pragma unroll
+                for (int kk = 0; kk < KK; kk++) load_strip(k0 + kk, P[kk], Dv[kk]);
+                if (k0 == 0) write_staging();
+#pragma unroll
+                for (int kk = 0; kk < KK; kk++) {
+                    const int k = k0 + kk;
+                    strip_setup_c<NR, ODD>(P[kk], Dv[kk], IW0, IW1, sreal[k] ? IW0 : 0u, sreal[k] ? IW1 : 0u, GX[k],
+                                           GY[k], asum[0], asum[1], asum[2], csum[0], csum[1], li[k], lx[k], ly[k]);
                     if (ODD && (k & 1))
                         odd_pair_setup(li[k - 1], lx[k - 1], ly[k - 1], li[k], lx[k], ly[k], GXO[k / 2], GYO[k / 2],
                                        asum[0], asum[1], asum[2], csum[0], csum[1]);
-                    __builtin_amdgcn_sched_barrier(0);
-                }
-            } else {
-                // strips KKS at a time: loads of a group in flight together
-#pragma unroll
-                for (int k0 = 0; k0 < K; k0 += KKS) {
-                    constexpr int KK = K >= KKS ? KKS : 1;
-                    unsigned P[KK][NR + 1];
-                    u32x2a4 Dv[KK][NR + 1];
-#pragma unroll
-                    for (int kk = 0; kk < KK; kk++) load_strip(k0 + kk, P[kk], Dv[kk]);
-                    if (k0 == 0) write_staging();
-#pragma unroll
-                    for (int kk = 0; kk < KK; kk++) {
-                        const int k = k0 + kk;
-                        strip_setup_c<NR, ODD>(P[kk], Dv[kk], IW0, IW1, sreal[k] ? IW0 : 0u, sreal[k] ? IW1 : 0u,
-                                               GX[k], GY[k], asum[0], asum[1], asum[2], csum[0], csum[1], li[k],
-                                               lx[k], ly[k]);
-                        if (ODD && (k & 1))
-                            odd_pair_setup(li[k - 1], lx[k - 1], ly[k - 1], li[k], lx[k], ly[k], GXO[k / 2],
-                                           GYO[k / 2], asum[0], asum[1], asum[2], csum[0], csum[1]);
-                    }
                 }
             }
         }
@@ -1812,9 +1780,6 @@ __global__ __launch_bounds__(64, MINW) void lk_multi_kernel(LKBatch B, LKDev p) 
             const BiW w = bilinear_weights(nextx - fnx, nexty - fny);
             const unsigned W0 = w.W0, W1 = w.W1;
             int bsum[2] = {-csum[0], -csum[1]};
-#ifdef SVO_LK_SPLITB
-            int bsum2[2] = {0, 0};  // odd strips: two shorter accumulation chains per sum
-#endif
             {
                 // (iny - jy0) JRW + (inx - jxa) as one 24-bit multiply-add against the
                 // region origin's offset; an inactive group reads inside its own region
@@ -1839,13 +1804,8 @@ __global__ __launch_bounds__(64, MINW) void lk_multi_kernel(LKBatch B, LKDev p) 
 #pragma unroll
                     for (int m = 0; m < NP; m++) {
                         const unsigned jj = hi16x2(jv[2 * m], jv[2 * m + 1]);  // J; the I part is in csum
-#ifdef SVO_LK_SPLITB
-                        int* bs = (k & 1) ? bsum2 : bsum;
-#else
-                        int* bs = bsum;
-#endif
-                        bs[0] = sdot2(jj, GX[k][m], bs[0]);
-                        bs[1] = sdot2(jj, GY[k][m], bs[1]);
+                        bsum[0] = sdot2(jj, GX[k][m], bsum[0]);
+                        bsum[1] = sdot2(jj, GY[k][m], bsum[1]);
                     }
                     if constexpr (ODD) {
                         if (k & 1) {
@@ -1858,10 +1818,6 @@ __global__ __launch_bounds__(64, MINW) void lk_multi_kernel(LKBatch B, LKDev p) 
                     }
                 }
             }
-#ifdef SVO_LK_SPLITB
-            bsum[0] += bsum2[0];
-            bsum[1] += bsum2[1];
-#endif
             float fb[2];
 #ifndef SVO_LK_NO_SETPRIO
             // the serial tail (reduction -> solve -> next weights / address): raised so
@@ -1892,6 +1848,9 @@ __global__ __launch_bounds__(64, MINW) void lk_multi_kernel(LKBatch B, LKDev p) 
                 }
             }
         }
+#ifndef SVO_LK_NO_SETPRIO
+        __builtin_amdgcn_s_setprio(0);  // the next level's setup is bulk work again
+#endif
         wave_lds_sync();
     }
     if (l == 0 && live) {
@@ -2023,37 +1982,14 @@ hipError_t launch_lk(const LKBatch& b, int nseq, int max_n, const LKParams& lp, 
             // four features per wave, 1-px staging margin (re-staged when the
             // estimate leaves it; measured 2.7 % faster alone than a 2-px margin
             // and than 3 px; two features per wave (lk_dual_kernel, another lane
-            // map) measured slower and is gone: DESIGN.md)
-            // SVO_LK_VARIANT (A/B only): MINW (waves per SIMD the registers are
-            // capped for) and KKS (strips loaded together in the setup)
-            static const int variant = [] {
-                const char* e = std::getenv("SVO_LK_VARIANT");
-                return e ? std::atoi(e) : 0;
-            }();
-            switch (variant) {
-                case 32: return launch_multi<4, 1, 3, 2>(b, nseq, max_n, d, st);
-                case 31: return launch_multi<4, 1, 3, 1>(b, nseq, max_n, d, st);
-                case 42: return launch_multi<4, 1, 4, 2>(b, nseq, max_n, d, st);
-                case 41: return launch_multi<4, 1, 4, 1>(b, nseq, max_n, d, st);
-                case 40: return launch_multi<4, 1, 4, 0>(b, nseq, max_n, d, st);
-                case 30: return launch_multi<4, 1, 3, 0>(b, nseq, max_n, d, st);
-                case 82: return launch_multi<8, 1, 2, 2>(b, nseq, max_n, d, st);
-                case 81: return launch_multi<8, 1, 2, 1>(b, nseq, max_n, d, st);
-                case 84: return launch_multi<8, 1, 2, 4>(b, nseq, max_n, d, st);
-                default: return launch_multi<4, 1, 3>(b, nseq, max_n, d, st);
-            }
+            // map) measured slower and is gone; 4 waves/SIMD, 8 features per wave
+            // and one strip ahead in the setup measured slower: DESIGN.md section 5)
+            return launch_multi<4, 1, 3>(b, nseq, max_n, d, st);
         }
         // the stereo call's 11 x 11 (findLeftFeaturesInRight, no err): four
         // features per wave too, one 11-row strip per lane (11 of 16 lanes)
-        if (lp.win_w == 11 && lp.win_h == 11 && multi_ok && lp.quad) {
-            // SVO_LK_STEREO_FPW (A/B only): 8 features per wave, two strips per lane
-            static const int sfpw = [] {
-                const char* e = std::getenv("SVO_LK_STEREO_FPW");
-                return e ? std::atoi(e) : 4;
-            }();
-            if (sfpw == 8) return launch_multi<8, 1, 4, 1, 11, 11, 11>(b, nseq, max_n, d, st);
+        if (lp.win_w == 11 && lp.win_h == 11 && multi_ok && lp.quad)
             return launch_multi<4, 1, 4, 1, 11, 11, 11>(b, nseq, max_n, d, st);
-        }
         if (lp.win_w == 21 && lp.win_h == 21) return launch_fast<21, 21>(b, nseq, max_n, d, st);
         if (lp.win_w == 11 && lp.win_h == 11) return launch_fast<11, 11>(b, nseq, max_n, d, st);
         if (lp.win_w == 15 && lp.win_h == 15) return launch_fast<15, 15>(b, nseq, max_n, d, st);

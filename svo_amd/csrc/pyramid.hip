@@ -474,16 +474,9 @@ static hipError_t pyramid_scharr_levels(const PyrDesc* d_descs, const DerivDesc*
     for (int l = 0; l + 1 < nlevels; l++) {
         const int nw = (lw + 1) / 2, nh = (lh + 1) / 2;
         dim3 grid((nw + PD_TX - 1) / PD_TX, (nh + PD_TY - 1) / PD_TY, nseq);
-        // non-temporal derivative stores (SVO_PYR_NT=0: plain): the chain alone
-        // 97.6 -> 89.5 us per 64 frames, the step unchanged (LK reads them a step later)
-        static const bool nt = [] {
-            const char* e = std::getenv("SVO_PYR_NT");
-            return !(e && e[0] == '0');
-        }();
-        if (nt)
-            hipLaunchKernelGGL(pyr_scharr_kernel<true>, grid, dim3(256), 0, st, d_descs, d_ders, l, 0);
-        else
-            hipLaunchKernelGGL(pyr_scharr_kernel<false>, grid, dim3(256), 0, st, d_descs, d_ders, l, 0);
+        // non-temporal derivative stores: the chain alone 97.6 -> 89.5 us per 64
+        // frames against plain stores, the step unchanged (LK reads them a step later)
+        hipLaunchKernelGGL(pyr_scharr_kernel<true>, grid, dim3(256), 0, st, d_descs, d_ders, l, 0);
         lw = nw;
         lh = nh;
     }

@@ -10,7 +10,11 @@
 #include <thread>
 #include <vector>
 
-#include "svo_gpu.h"
+#include "svo_synth.h"
+
+namespace {
+constexpr int SVO_OK = 0, SVO_ERR_ARG = -1;  // the values of svo_gpu.h's codes
+}
 
 namespace {
 
@@ -148,7 +152,7 @@ extern "C" int svo_synth_frame_right(const uint8_t* canvas, int cw, int ch, int 
     return SVO_OK;
 }
 
-// svo_synth_view (include/svo_gpu.h): a general camera (R, C) over the depth-field
+// svo_synth_view (include/svo_synth.h): a general camera (R, C) over the depth-field
 // surface X(cu, cv) = (((cu - cx) / fx) rho, ((cv - cy) / fy) rho, rho), rho =
 // rho(cu, cv) (the surface the rotation-only views and the right view use), plus
 // rectangular occluders in world planes z = const.

@@ -13,11 +13,109 @@ fx * b / depth, so stereo LK + triangulation recover the depth.
 """
 from __future__ import annotations
 
+import ctypes as C
 import math
+import os
 
 import numpy as np
 
-from . import synth_canvas, synth_frame, synth_frame_right, synth_view
+from . import SvoError
+
+_u8p = C.POINTER(C.c_uint8)
+_f64p = C.POINTER(C.c_double)
+_SYNTH = None
+# include/svo_synth.h (libsvo_synth.so: host code, tests and bench only)
+_SYNTH_SIGS = [
+    ("svo_synth_canvas", C.c_int, [C.c_uint64, C.c_int, C.c_int, C.c_int, _u8p]),
+    ("svo_synth_frame", C.c_int, [_u8p, C.c_int, C.c_int, C.c_int, C.c_int, _f64p, _f64p,
+                                  C.c_uint64, C.c_int, _u8p, C.c_int, C.c_int]),
+    ("svo_synth_frame_right", C.c_int, [_u8p, C.c_int, C.c_int, C.c_int, C.c_int, _f64p, _f64p,
+                                        C.c_double, C.c_int, C.c_uint64, C.c_int, _u8p, C.c_int, C.c_int]),
+    ("svo_synth_view", C.c_int, [_u8p, C.c_int, C.c_int, C.c_int, C.c_int, _f64p, _f64p, _f64p, C.c_int, _f64p,
+                                 C.c_int, _u8p, C.c_int, C.c_int, C.c_uint64, C.c_int, _u8p, C.c_int, C.c_int]),
+]
+SYNTH_SYMBOLS = [s[0] for s in _SYNTH_SIGS]
+
+
+def synth_lib_path() -> str:
+    return os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib", "libsvo_synth.so")
+
+
+def _synth_lib():
+    global _SYNTH
+    if _SYNTH is None:
+        path = synth_lib_path()
+        if not os.path.exists(path):
+            raise SvoError(f"synthetic input library not built: {path} missing (run __graft_entry__.build())")
+        L = C.CDLL(path)
+        for name, res, args in _SYNTH_SIGS:
+            f = getattr(L, name)
+            f.restype = res
+            f.argtypes = args
+        _SYNTH = L
+    return _SYNTH
+
+
+def _p(a, t):
+    return a.ctypes.data_as(t)
+
+
+def _c(a, dtype):
+    return np.ascontiguousarray(a, dtype=dtype)
+
+
+def synth_canvas(seed: int, cw: int, ch: int, n_rect: int) -> np.ndarray:
+    out = np.empty((ch, cw), np.uint8)
+    if _synth_lib().svo_synth_canvas(seed, cw, ch, n_rect, _p(out, _u8p)) != 0:
+        raise SvoError("svo_synth_canvas failed")
+    return out
+
+
+def synth_frame(canvas: np.ndarray, margin: tuple, R, K, noise_seed: int, noise: int, w: int,
+                h: int) -> np.ndarray:
+    canvas = _c(canvas, np.uint8)
+    R = _c(R, np.float64).reshape(9)
+    K = _c(K, np.float64).reshape(9)
+    out = np.empty((h, w), np.uint8)
+    ch, cw = canvas.shape
+    if _synth_lib().svo_synth_frame(_p(canvas, _u8p), cw, ch, int(margin[0]), int(margin[1]), _p(R, _f64p),
+                             _p(K, _f64p), noise_seed, noise, _p(out, _u8p), w, h) != 0:
+        raise SvoError("svo_synth_frame failed")
+    return out
+
+
+def synth_view(canvas: np.ndarray, margin: tuple, R, Cw, K, depth_seed: int, occ, occ_tex, noise_seed: int,
+               noise: int, w: int, h: int) -> np.ndarray:
+    """svo_synth_view: the depth-field surface from camera (R, centre Cw) in front of
+    the rectangles occ ((n, 5): x0, y0, x1, y1, z) textured by occ_tex."""
+    canvas = _c(canvas, np.uint8)
+    R = _c(R, np.float64).reshape(9)
+    Cw = _c(Cw, np.float64).reshape(3)
+    K = _c(K, np.float64).reshape(9)
+    occ = _c(np.zeros((0, 5)) if occ is None else occ, np.float64).reshape(-1, 5)
+    tex = _c(np.zeros((2, 2), np.uint8) if occ_tex is None else occ_tex, np.uint8)
+    out = np.empty((h, w), np.uint8)
+    ch, cw = canvas.shape
+    th, tw = tex.shape
+    if _synth_lib().svo_synth_view(_p(canvas, _u8p), cw, ch, int(margin[0]), int(margin[1]), _p(R, _f64p), _p(Cw, _f64p),
+                            _p(K, _f64p), int(depth_seed), _p(occ, _f64p), len(occ), _p(tex, _u8p), tw, th,
+                            noise_seed, noise, _p(out, _u8p), w, h) != 0:
+        raise SvoError("svo_synth_view failed")
+    return out
+
+
+def synth_frame_right(canvas: np.ndarray, margin: tuple, R, K, bf: float, depth_seed: int, noise_seed: int,
+                      noise: int, w: int, h: int) -> np.ndarray:
+    canvas = _c(canvas, np.uint8)
+    R = _c(R, np.float64).reshape(9)
+    K = _c(K, np.float64).reshape(9)
+    out = np.empty((h, w), np.uint8)
+    ch, cw = canvas.shape
+    if _synth_lib().svo_synth_frame_right(_p(canvas, _u8p), cw, ch, int(margin[0]), int(margin[1]), _p(R, _f64p),
+                                   _p(K, _f64p), float(bf), int(depth_seed), noise_seed, noise, _p(out, _u8p),
+                                   w, h) != 0:
+        raise SvoError("svo_synth_frame_right failed")
+    return out
 
 KITTI_W, KITTI_H = 1241, 376
 # R:configs/config.yaml:8-11 (fx, fy, cx, cy), held as float32 like the

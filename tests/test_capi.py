@@ -7,6 +7,7 @@ import re
 import numpy as np
 
 import svo_amd as S
+import svo_amd.scene as SC
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
@@ -31,12 +32,22 @@ def test_version_string():
     assert S.lib().svo_version().decode().startswith("svo_gpu gfx950")
 
 
+def test_synth_library_is_separate_from_the_product():
+    """The synthetic workload generator (include/svo_synth.h) lives in its own
+    test/bench library; the product library exports none of it."""
+    assert set(declared_symbols("svo_synth.h")) == set(SC.SYNTH_SYMBOLS)
+    syn = ctypes.CDLL(SC.synth_lib_path())
+    gpu = ctypes.CDLL(S.lib_path())
+    for name in SC.SYNTH_SYMBOLS:
+        assert hasattr(syn, name) and not hasattr(gpu, name), name
+
+
 def test_synth_is_deterministic_host_code():
-    a = S.synth_canvas(3, 200, 100, 50)
-    b = S.synth_canvas(3, 200, 100, 50)
+    a = SC.synth_canvas(3, 200, 100, 50)
+    b = SC.synth_canvas(3, 200, 100, 50)
     assert np.array_equal(a, b) and a.std() > 10
     K = np.array([[100, 0, 100], [0, 100, 50], [0, 0, 1]], np.float64)
-    f = S.synth_frame(a, (20, 20), np.eye(3), K, 1, 3, 160, 60)
+    f = SC.synth_frame(a, (20, 20), np.eye(3), K, 1, 3, 160, 60)
     assert f.shape == (60, 160)
 
 
