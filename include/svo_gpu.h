@@ -355,7 +355,11 @@ int svo_frontend_set_frame_bgr(svo_frontend* fe, int seq, int t, const uint8_t* 
  * copy). Ring discipline (n_frames >= 4): before init, any frame; after it,
  * frame t is queued before step t - 2 is called (t >= last step + 3) and no
  * earlier than step t - n_frames + 1 returned (t <= last step + n_frames - 1):
- * a loop queues frames 0 .. 2, calls init(0), then queue(t + 2), step(t). */
+ * a loop queues frames 0 .. 2, calls init(0), then queue(t + 2), step(t). A frame
+ * at or before the last step restarts the loop (everything queued is finished and
+ * forgotten; queue frames t0 .. t0 + 2 and init(t0) again). set_frame(seq, t)
+ * after streaming makes slot t hold frame t, resident. The copy into a slot waits
+ * on the device for the last read of the slot's previous frame. */
 int svo_frontend_queue_frames(svo_frontend* fe, int t, const uint8_t* const* left, const uint8_t* const* right,
                               int stride, int bgr);
 int svo_frontend_upload_wait(svo_frontend* fe, int t);
@@ -422,40 +426,6 @@ int svo_frontend_host_cpus(svo_frontend* fe, int* cpus, int cap, int* n);
  * with primes between them on `threads` threads; *bad = tasks run other than
  * exactly once, or after their job returned (0 when the pool is correct). */
 int svo_pool_selftest(int threads, int jobs, int64_t* bad);
-
-/* ------------------------------------------------------------ synthetic input
- * Deterministic synthetic KITTI-like frames: a textured canvas
- * of random rectangles, box-blurred, seen through a rotating pinhole camera
- * (pure rotation => the frame-to-frame motion is a homography, any depth is
- * consistent). Host-side generator, used by tests and bench only. */
-int svo_synth_canvas(uint64_t seed, int cw, int ch, int n_rect, uint8_t* canvas);
-/* frame = canvas seen by camera rotation R (row-major 3x3, world->camera),
- * intrinsics K; canvas pixel (0,0) sits at image offset (-margin_x, -margin_y)
- * of the unrotated view; adds U[-noise, noise] integer noise (seeded). */
-int svo_synth_frame(const uint8_t* canvas, int cw, int ch, int margin_x, int margin_y,
-                    const double R[9], const double K[9], uint64_t noise_seed, int noise,
-                    uint8_t* frame, int w, int h);
-
-/* Right view of a rectified stereo pair of the same synthetic scene: the
- * canvas surface sits at depth rho(u, v) = 12 + 5 sin(u/97 + seed) +
- * 4 cos(v/61 - seed/2) (world z) and
- * the right camera is the left one shifted by the baseline (fx * b = bf). */
-int svo_synth_frame_right(const uint8_t* canvas, int cw, int ch, int margin_x, int margin_y,
-                          const double R[9], const double K[9], double bf, int depth_seed,
-                          uint64_t noise_seed, int noise, uint8_t* frame, int w, int h);
-
-/* The same depth-field surface seen by a camera with centre C (world) and
- * rotation R (world -> camera: X_c = R (X - C)) -- a translating camera, so the
- * frames carry parallax -- in front of n_occ textured rectangles: occ[5 k ..]
- * = x0, y0, x1, y1, z (the world plane z, x in [x0, x1], y in [y0, y1]), each
- * drawn from the tw x th texture `occ_tex` (the forward sequences' moving
- * occluders: their points move against the static world). Per pixel the first
- * hit along the ray: the surface by a safeguarded Newton solve of X_z =
- * rho(projection of X from the origin), an occluder by a plane intersection. */
-int svo_synth_view(const uint8_t* canvas, int cw, int ch, int margin_x, int margin_y, const double R[9],
-                   const double C[3], const double K[9], int depth_seed, const double* occ, int n_occ,
-                   const uint8_t* occ_tex, int tw, int th, uint64_t noise_seed, int noise, uint8_t* frame, int w,
-                   int h);
 
 #ifdef __cplusplus
 }

@@ -34,7 +34,7 @@ import numpy as np
 __all__ = [
     "SvoError", "lib", "Context", "Image", "FastFeatureDetector",
     "TERM_COUNT", "TERM_EPS", "LK_USE_INITIAL_FLOW", "LK_GET_MIN_EIGENVALS", "LK_OPENCV_ORDER",
-    "synth_canvas", "synth_frame", "synth_frame_right", "synth_view", "lib_path", "Frontend", "FrontendConfig", "FrontendStats",
+    "lib_path", "Frontend", "FrontendConfig", "FrontendStats",
 ]
 
 TERM_COUNT = 1
@@ -146,13 +146,6 @@ _SIGS = [
     ("svo_host_cpu_plan", C.c_int, [C.c_int, C.c_int, _i32p, _i32p, C.c_int, _i32p]),
     ("svo_frontend_host_cpus", C.c_int, [_vp, _i32p, C.c_int, _i32p]),
     ("svo_pool_selftest", C.c_int, [C.c_int, C.c_int, C.POINTER(C.c_int64)]),
-    ("svo_synth_canvas", C.c_int, [C.c_uint64, C.c_int, C.c_int, C.c_int, _u8p]),
-    ("svo_synth_frame", C.c_int, [_u8p, C.c_int, C.c_int, C.c_int, C.c_int, _f64p, _f64p,
-                                  C.c_uint64, C.c_int, _u8p, C.c_int, C.c_int]),
-    ("svo_synth_frame_right", C.c_int, [_u8p, C.c_int, C.c_int, C.c_int, C.c_int, _f64p, _f64p,
-                                        C.c_double, C.c_int, C.c_uint64, C.c_int, _u8p, C.c_int, C.c_int]),
-    ("svo_synth_view", C.c_int, [_u8p, C.c_int, C.c_int, C.c_int, C.c_int, _f64p, _f64p, _f64p, C.c_int, _f64p,
-                                 C.c_int, _u8p, C.c_int, C.c_int, C.c_uint64, C.c_int, _u8p, C.c_int, C.c_int]),
 ]
 
 SYMBOLS = [s[0] for s in _SIGS]
@@ -641,6 +634,7 @@ class Frontend:
         h = _vp()
         ctx._check(lib().svo_frontend_create(ctx.handle, C.byref(cfg), C.byref(h)))
         self.handle = h
+        self._queued = {}  # ring slot -> (t, lefts, rights) of queue_frames, until upload_wait(t)
         _LIVE["frontend"].add(self)
 
     def set_frame(self, seq, t, left, right):
@@ -661,13 +655,19 @@ class Frontend:
 
     def queue_frames(self, t, lefts, rights):
         """svo_frontend_queue_frames: frame t of every sequence from host arrays
-        (lefts[s], rights[s]: (h, w) grey or (h, w, 3) BGR, all of one shape), queued
-        as asynchronous H2D copies (see include/svo_gpu.h for the ring discipline).
-        The arrays must stay alive and unchanged until upload_wait(t)."""
+        (lefts[s], rights[s]: (height, width) grey or (height, width, 3) BGR of the
+        config's size, all of one shape), queued as asynchronous H2D copies (see
+        include/svo_gpu.h for the ring discipline). The copies read the arrays after
+        this call returns: the wrapper keeps them referenced until upload_wait(t) (or
+        until ring slot t % n_frames is queued again); their contents must stay
+        unchanged until then."""
         S = self.cfg.n_seq
         if len(lefts) != S or len(rights) != S:
             raise SvoError("queue_frames: one left and one right image per sequence")
         a0 = lefts[0]
+        hw = (self.cfg.height, self.cfg.width)
+        if a0.shape not in (hw, hw + (3,)):
+            raise SvoError(f"queue_frames: images must be {hw} grey or {hw + (3,)} BGR, got {a0.shape}")
         bgr = a0.ndim == 3
         for a in list(lefts) + list(rights):
             if a.shape != a0.shape or a.dtype != np.uint8 or not a.flags["C_CONTIGUOUS"]:
@@ -676,9 +676,15 @@ class Frontend:
         R = (_u8p * S)(*[a.ctypes.data_as(_u8p) for a in rights])
         stride = a0.shape[1] * (3 if bgr else 1)
         self.ctx._check(lib().svo_frontend_queue_frames(self.handle, int(t), L, R, stride, int(bgr)))
+        # the asynchronous copies read these buffers: hold them until upload_wait(t)
+        self._queued[int(t) % max(self.cfg.n_frames, 1)] = (int(t), list(lefts), list(rights))
 
     def upload_wait(self, t):
         self.ctx._check(lib().svo_frontend_upload_wait(self.handle, int(t)))
+        slot = int(t) % max(self.cfg.n_frames, 1)
+        held = self._queued.get(slot)
+        if held is not None and held[0] == int(t):
+            del self._queued[slot]
 
     def init(self, t0=0):
         self.ctx._check(lib().svo_frontend_init(self.handle, t0))
@@ -759,8 +765,9 @@ class Frontend:
 
     def close(self):
         if getattr(self, "handle", None):
-            lib().svo_frontend_destroy(self.handle)
+            lib().svo_frontend_destroy(self.handle)  # waits for the front end's streams
             self.handle = None
+            self._queued = {}
 
     def __del__(self):
         try:
@@ -784,56 +791,3 @@ class FastFeatureDetector:
         return self.ctx.fast_detect(img, self.threshold, self.nonmax, mask)
 
 
-# -------------------------------------------------------------------- synthetic input
-def synth_canvas(seed: int, cw: int, ch: int, n_rect: int) -> np.ndarray:
-    out = np.empty((ch, cw), np.uint8)
-    if lib().svo_synth_canvas(seed, cw, ch, n_rect, _p(out, _u8p)) != 0:
-        raise SvoError("svo_synth_canvas failed")
-    return out
-
-
-def synth_frame(canvas: np.ndarray, margin: tuple, R, K, noise_seed: int, noise: int, w: int,
-                h: int) -> np.ndarray:
-    canvas = _c(canvas, np.uint8)
-    R = _c(R, np.float64).reshape(9)
-    K = _c(K, np.float64).reshape(9)
-    out = np.empty((h, w), np.uint8)
-    ch, cw = canvas.shape
-    if lib().svo_synth_frame(_p(canvas, _u8p), cw, ch, int(margin[0]), int(margin[1]), _p(R, _f64p),
-                             _p(K, _f64p), noise_seed, noise, _p(out, _u8p), w, h) != 0:
-        raise SvoError("svo_synth_frame failed")
-    return out
-
-
-def synth_view(canvas: np.ndarray, margin: tuple, R, Cw, K, depth_seed: int, occ, occ_tex, noise_seed: int,
-               noise: int, w: int, h: int) -> np.ndarray:
-    """svo_synth_view: the depth-field surface from camera (R, centre Cw) in front of
-    the rectangles occ ((n, 5): x0, y0, x1, y1, z) textured by occ_tex."""
-    canvas = _c(canvas, np.uint8)
-    R = _c(R, np.float64).reshape(9)
-    Cw = _c(Cw, np.float64).reshape(3)
-    K = _c(K, np.float64).reshape(9)
-    occ = _c(np.zeros((0, 5)) if occ is None else occ, np.float64).reshape(-1, 5)
-    tex = _c(np.zeros((2, 2), np.uint8) if occ_tex is None else occ_tex, np.uint8)
-    out = np.empty((h, w), np.uint8)
-    ch, cw = canvas.shape
-    th, tw = tex.shape
-    if lib().svo_synth_view(_p(canvas, _u8p), cw, ch, int(margin[0]), int(margin[1]), _p(R, _f64p), _p(Cw, _f64p),
-                            _p(K, _f64p), int(depth_seed), _p(occ, _f64p), len(occ), _p(tex, _u8p), tw, th,
-                            noise_seed, noise, _p(out, _u8p), w, h) != 0:
-        raise SvoError("svo_synth_view failed")
-    return out
-
-
-def synth_frame_right(canvas: np.ndarray, margin: tuple, R, K, bf: float, depth_seed: int, noise_seed: int,
-                      noise: int, w: int, h: int) -> np.ndarray:
-    canvas = _c(canvas, np.uint8)
-    R = _c(R, np.float64).reshape(9)
-    K = _c(K, np.float64).reshape(9)
-    out = np.empty((h, w), np.uint8)
-    ch, cw = canvas.shape
-    if lib().svo_synth_frame_right(_p(canvas, _u8p), cw, ch, int(margin[0]), int(margin[1]), _p(R, _f64p),
-                                   _p(K, _f64p), float(bf), int(depth_seed), noise_seed, noise, _p(out, _u8p),
-                                   w, h) != 0:
-        raise SvoError("svo_synth_frame_right failed")
-    return out

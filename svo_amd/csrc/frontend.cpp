@@ -431,11 +431,14 @@ struct svo_frontend {
     // frame parity), the conversion kernel into level 0 of the frame's ring slot;
     // the pyramid builds of that frame wait for ev_up[slot]
     hipStream_t st_up = nullptr;
-    uint8_t* up_stage = nullptr;       // [2 parity][2 side][S x up_cap]: the host frames' bytes
+    uint8_t* up_stage = nullptr;       // [2 side][S x up_cap]: the host frames' bytes (copy and conversion
+                                       // run in order on st_up, so one block serves every frame)
     size_t up_cap = 0;                 // staging bytes per sequence (the widest h * stride seen)
     size_t up_seq = 0;                 // h * stride of the last queued frame (sequence stride in staging)
     std::vector<hipEvent_t> ev_up;     // [T] conversion of the slot's frame done
     std::vector<int> up_t;             // [T] frame last streamed into the slot (-1: none)
+    std::vector<hipEvent_t> ev_free;   // [T] the slot's frame f read for the last time (after LK(f + 1))
+    std::vector<char> free_rec;        // [T] ev_free recorded since the slot was last queued
     int stepped = -1;                  // last completed step (init: t0); -1 before init
 };
 
@@ -1144,6 +1147,8 @@ void svo_frontend_destroy(svo_frontend* fe) {
     }
     for (hipEvent_t e : fe->ev_up)
         if (e) (void)hipEventDestroy(e);
+    for (hipEvent_t e : fe->ev_free)
+        if (e) (void)hipEventDestroy(e);
     if (fe->up_stage) (void)hipFree(fe->up_stage);
     orb_batch_destroy(fe->orb);
     if (fe->fit_work) (void)hipFree(fe->fit_work);
@@ -1172,7 +1177,12 @@ static int fe_set_frame(svo_frontend* fe, int seq, int t, const uint8_t* left, c
     if (fe->pyr_ready >= 0 && fe->pyr_ready % fe->T == t) fe->pyr_ready = -1;  // built from the old image
     if (fe->pre_t >= 0 && fe->pre_t % fe->T == t) fe->pre_t = -1;  // detected on the old image
     if (fe->pyr_r_ready >= 0 && fe->pyr_r_ready % fe->T == t) fe->pyr_r_ready = -1;
-    if (!fe->up_t.empty()) fe->up_t[t] = -1;  // (the drain above finished any streamed upload)
+    // the slot now holds frame t, resident (the drain above finished any streamed
+    // upload into it): steps keep finding it in the ring
+    if (!fe->up_t.empty()) {
+        fe->up_t[t] = t;
+        fe->free_rec[t] = 0;
+    }
     for (int side = 0; side < 2; side++) {
         svo_image* im = (side ? fe->frames_r : fe->frames)[(size_t)seq * fe->T + t];
         const uint8_t* px = side ? right : left;
@@ -1223,6 +1233,16 @@ int svo_frontend_queue_frames(svo_frontend* fe, int t, const uint8_t* const* lef
     // ring discipline: frame t's pyramid is built at the end of step t - 2, so it is
     // queued before that step (t >= stepped + 3); its slot's previous frame t - T is
     // no longer read once step t - T + 1 returned (t <= stepped + T - 1)
+    // a frame at or before the last step restarts the loop: everything queued and
+    // built ahead is finished and forgotten, and the window opens as before init
+    if (fe->stepped >= 0 && t <= fe->stepped) {
+        int rd = fe_drain(fe);
+        if (rd) return rd;
+        fe->stepped = -1;
+        fe->pyr_ready = fe->pyr_r_ready = fe->pre_t = -1;
+        std::fill(fe->up_t.begin(), fe->up_t.end(), -1);
+        std::fill(fe->free_rec.begin(), fe->free_rec.end(), 0);
+    }
     if (fe->stepped >= 0 && (t < fe->stepped + 3 || t > fe->stepped + T - 1))
         return set_error(ctx, SVO_ERR_ARG, "svo_frontend_queue_frames: frame outside the ring window "
                                            "(stepped + 3 .. stepped + n_frames - 1)");
@@ -1231,6 +1251,9 @@ int svo_frontend_queue_frames(svo_frontend* fe, int t, const uint8_t* const* lef
         fe->ev_up.assign(T, nullptr);
         for (auto& e : fe->ev_up) SVO_HIP(ctx, hipEventCreateWithFlags(&e, hipEventDisableTiming));
         fe->up_t.assign(T, -1);
+        fe->ev_free.assign(T, nullptr);
+        for (auto& e : fe->ev_free) SVO_HIP(ctx, hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        fe->free_rec.assign(T, 0);
     }
     // the staging block mirrors the host frames (rows `stride` apart, sequences
     // H rows apart): a run of sequences whose buffers follow each other in memory
@@ -1241,12 +1264,16 @@ int svo_frontend_queue_frames(svo_frontend* fe, int t, const uint8_t* const* lef
         if (fe->up_stage) SVO_HIP(ctx, hipFree(fe->up_stage));
         fe->up_stage = nullptr;
         fe->up_cap = seq_bytes;
-        SVO_HIP(ctx, hipMalloc(&fe->up_stage, 4 * (size_t)S * fe->up_cap));
+        SVO_HIP(ctx, hipMalloc(&fe->up_stage, 2 * (size_t)S * fe->up_cap));
     }
     fe->up_seq = seq_bytes;  // (the conversion of earlier queued frames captured their own stride)
     const int slot = t % T;
     const size_t last_row = (size_t)(bgr ? 3 : 1) * W;  // bytes of a frame's last row (no stride padding after it)
-    uint8_t* stage = fe->up_stage + (size_t)(t & 1) * 2 * S * fe->up_cap;
+    uint8_t* stage = fe->up_stage;
+    // the slot's previous frame (t - T) is last read by LK(t - T + 1): the copy into
+    // the slot waits for it on the device, not only by the host's window above
+    if (fe->free_rec[slot]) SVO_HIP(ctx, hipStreamWaitEvent(fe->st_up, fe->ev_free[slot], 0));
+    fe->free_rec[slot] = 0;
     for (int side = 0; side < 2; side++) {
         const uint8_t* const* src = side ? right : left;
         uint8_t* dst = stage + (size_t)side * S * fe->up_cap;
@@ -1462,6 +1489,14 @@ static int fe_front_lk(svo_frontend* fe, int t) {
         SVO_HIP(ctx, launch_lk(lb, S, fe->CAP, lp, sl));
         ph_end(fe, sl, slot);
         SVO_HIP(ctx, hipEventRecord(fe->ev_lk, sl));
+        // frame t-1's images are not read after this LK (its stereo LK and keyframe
+        // ran before it on this stream or were waited for there): its ring slot may
+        // be streamed into once this event fires
+        if (!fe->ev_free.empty()) {
+            const int fs = (t - 1) % fe->T;
+            SVO_HIP(ctx, hipEventRecord(fe->ev_free[fs], sl));
+            fe->free_rec[fs] = 1;
+        }
     }
     return SVO_OK;
 }

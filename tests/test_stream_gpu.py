@@ -97,3 +97,42 @@ def test_queue_frames_ring_discipline():
     fe.step(2)
     fe.upload_wait(4)
     fe.close()
+
+
+def test_queue_frames_shape_restart_and_set_frame():
+    """The wrapper refuses images of another size (the asynchronous copy would read
+    past them); a frame at or before the last step restarts the loop, which then
+    reproduces the first run; set_frame after streaming keeps the slot in the ring."""
+    ctx = S.Context(0)
+    W, H, N = 320, 240, 300
+    sc = Scene(W, H, seed=4)
+    fe = S.Frontend(ctx, S.FrontendConfig(W, H, sc.K, n_seq=1, n_frames=4, n_features=N))
+    frames = [(np.ascontiguousarray(sc.frame(t)), np.ascontiguousarray(sc.right(t))) for t in range(7)]
+    short = np.ascontiguousarray(frames[0][0][:-1])
+    with pytest.raises(S.SvoError):
+        fe.queue_frames(0, [short], [short])
+    rgba = np.zeros((H, W, 4), np.uint8)
+    with pytest.raises(S.SvoError):
+        fe.queue_frames(0, [rgba], [rgba])
+
+    def run(first_step_by_set_frame=False):
+        for t in range(3):
+            fe.queue_frames(t, [frames[t][0].copy()], [frames[t][1].copy()])  # temporaries: held by the wrapper
+        fe.init(0)
+        out = [fe.features(0)]
+        for t in range(1, 5):
+            if t + 2 <= 4:
+                if first_step_by_set_frame and t + 2 == 3:
+                    fe.set_frame(0, 3, frames[3][0], frames[3][1])  # slot 3 = frame 3, resident
+                else:
+                    fe.queue_frames(t + 2, [frames[t + 2][0]], [frames[t + 2][1]])
+            fe.step(t)
+            out.append(fe.features(0))
+        return out
+
+    a = run()
+    b = run()  # frame 0 <= the last step (4): a restart
+    c = run(first_step_by_set_frame=True)
+    for t in range(len(a)):
+        assert np.array_equal(a[t], b[t]) and np.array_equal(a[t], c[t]), f"t={t}"
+    fe.close()
