@@ -338,7 +338,7 @@ __global__ __launch_bounds__(kFeBlock) void tail_kernel(TailBatch T) {
 // findLeftFeaturesInRight's filter + triangulateNewMapPoints for one stereo match:
 // keep = status && |yR - yL| < y_threshold (float) && p.z > 0 (x3: the point in the
 // left camera frame)
-__device__ __forceinline__ bool stereo_point(const float* P, float y_threshold, bool status, float xl, float yl,
+__device__ __forceinline__ bool stereo_point(const float (&P)[24], float y_threshold, bool status, float xl, float yl,
                                              float xr, float yr, float (&x3)[3]) {
     bool keep = status && fabsf(yr - yl) < y_threshold;
     if (keep) {
@@ -431,14 +431,24 @@ __global__ __launch_bounds__(BS) void keyframe_fused_kernel(TailBatch T, AppendB
     append_body<BS>(A, s, n, take, wsum, &base_s);
 }
 
-__global__ __launch_bounds__(256) void stereo_tri_kernel(StereoTriBatch B) {
+// one 64-lane wave per block: the candidates of a sequence are ~ the margin (tens),
+// and a lone wave fits beside LK's three per SIMD where a 256-thread block waits
+__global__ __launch_bounds__(64, 6) void stereo_tri_kernel(StereoTriBatch B) {
     const int s = blockIdx.y;
     const int n = B.spec_n[s];
     const size_t o = (size_t)s * B.cap;
-    for (int j = blockIdx.x * 256 + threadIdx.x; j < n; j += gridDim.x * 256) {
+    for (int j = blockIdx.x * 64 + threadIdx.x; j < n; j += gridDim.x * 64) {
         const float xl = B.st_xy[2 * (o + j)], yl = B.st_xy[2 * (o + j) + 1];
         float x3[3] = {0.f, 0.f, 0.f};
-        const bool keep = stereo_point(B.P, B.y_threshold, B.st_status[o + j] != 0, xl, yl, B.st_next[2 * (o + j)],
+        // the projection matrices converted per point: hoisted out of the loop, their
+        // 24 doubles stayed live through the solve (157 VGPRs)
+        float P[24];
+#pragma unroll
+        for (int k = 0; k < 24; k++) {
+            P[k] = B.P[k];
+            asm volatile("" : "+s"(P[k]));
+        }
+        const bool keep = stereo_point(P, B.y_threshold, B.st_status[o + j] != 0, xl, yl, B.st_next[2 * (o + j)],
                                        B.st_next[2 * (o + j) + 1], x3);
         B.st_X[o + j] = make_float4(x3[0], x3[1], x3[2], keep ? 1.f : 0.f);
     }
@@ -486,8 +496,8 @@ hipError_t launch_keyframe_fused(const TailBatch& tb, const AppendBatch& ab, int
 }
 
 hipError_t launch_stereo_tri(const StereoTriBatch& b, int nseq, int max_n, hipStream_t st) {
-    const int gx = std::max(1, std::min((max_n + 255) / 256, 64));
-    hipLaunchKernelGGL(stereo_tri_kernel, dim3(gx, nseq), dim3(256), 0, st, b);
+    const int gx = std::max(1, std::min((max_n + 63) / 64, 256));
+    hipLaunchKernelGGL(stereo_tri_kernel, dim3(gx, nseq), dim3(64), 0, st, b);
     return hipGetLastError();
 }
 

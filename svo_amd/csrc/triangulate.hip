@@ -22,8 +22,10 @@ __global__ __launch_bounds__(256) void triangulate_kernel(const float* __restric
                                                           float* __restrict__ xyzw, float* __restrict__ xyz) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
-    float h[4];
-    dlt_point(P, p1[2 * i], p1[2 * i + 1], p2[2 * i], p2[2 * i + 1], h);
+    float h[4], Pv[24];
+#pragma unroll
+    for (int k = 0; k < 24; k++) Pv[k] = P[k];
+    dlt_point(Pv, p1[2 * i], p1[2 * i + 1], p2[2 * i], p2[2 * i + 1], h);
     if (xyzw) {
 #pragma unroll
         for (int k = 0; k < 4; k++) xyzw[4 * i + k] = h[k];
