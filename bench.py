@@ -489,6 +489,8 @@ def main():
     ap.add_argument("--no-orb", action="store_true", help="skip the shipped-config (ORB, reference keyframe rule) workload")
     ap.add_argument("--no-stream", action="store_true",
                     help="skip the streamed-ingest workloads (frames over PCIe inside the window, grey and BGR)")
+    ap.add_argument("--no-opencv-order", action="store_true",
+                    help="skip the headline batch timed again with LK in OpenCV's float order (SVO_LK_OPENCV_ORDER)")
     ap.add_argument("--no-bucketed", action="store_true",
                     help="skip the second measurement with bucketed selection in the loop")
     ap.add_argument("--scene", default="rot", choices=("rot", "forward"),
@@ -551,7 +553,7 @@ def main():
                            host_threads=args.threads, timing=args.timing)
     fe = S.Frontend(ctx, cfg)
     pairs0 = None
-    keep_pairs = not args.no_bucketed and world == 1
+    keep_pairs = not (args.no_bucketed and args.no_opencv_order) and world == 1
     all_pairs = []
     for s, sc in enumerate(scenes):
         pairs = [(sc.frame(t), sc.right(t)) for t in range(P)]
@@ -563,7 +565,7 @@ def main():
             all_pairs.append(pairs)
         if s % 16 == 15:
             print(f"[bench] rank {rank}: {s + 1}/{Sq} sequences rendered and uploaded", file=sys.stderr, flush=True)
-    side = {"single": None, "bucketed": None, "forward": None, "orb": None, "stream": None}
+    side = {"single": None, "bucketed": None, "forward": None, "orb": None, "stream": None, "opencv_order": None}
 
     def side_legs(close_fe):
         """The side workloads of the line (each its own front end and timed window)."""
@@ -603,26 +605,39 @@ def main():
         # never buckets (its call site is a TODO, R:src/tracking.cpp:88), so `value` is the
         # reference's loop; the same batch is timed again with bucketed selection
         # (bucket.hip, 50-px cells x 4 per cell) between FAST and the keyframe's take
-        bucketed = None
-        if all_pairs:
-            BS, PB = 50, 4
-            feb = S.Frontend(ctx, S.FrontendConfig(W, H, scenes[0].K, n_seq=Sq, n_frames=T, n_features=N, max_level=ML,
-                                                   host_threads=args.threads, timing=0, bucket_size=BS, per_bucket=PB))
+        def headline_variant(**kw):
+            """The headline batch (same frames) under another configuration: frames/s, ms/step."""
+            fev = S.Frontend(ctx, S.FrontendConfig(W, H, scenes[0].K, n_seq=Sq, n_frames=T, n_features=N, max_level=ML,
+                                                   host_threads=args.threads, timing=0, **kw))
             for s, pairs in enumerate(all_pairs):
                 for t in range(T):
-                    feb.set_frame(s, t, *pairs[t % P])
-            feb.init(0)
+                    fev.set_frame(s, t, *pairs[t % P])
+            fev.init(0)
             for t in range(1, Wm + 1):
-                feb.step(t)
+                fev.step(t)
             t1 = time.perf_counter()
             for t in range(Wm + 1, Wm + K + 1):
-                feb.step(t)
-            feb.synchronize()
-            dtb = time.perf_counter() - t1
-            bucketed = {"value": round(Sq * K / dtb, 2), "unit": "frames/s", "ms_per_step": round(dtb / K * 1e3, 4),
-                        "bucket_size": BS, "per_bucket": PB, "steps": K, "warmup": Wm}
-            feb.close()
-        side.update(single=single, bucketed=bucketed, forward=forward, orb=orb, stream=stream)
+                fev.step(t)
+            fev.synchronize()
+            dtv = time.perf_counter() - t1
+            fev.close()
+            return {"value": round(Sq * K / dtv, 2), "unit": "frames/s", "ms_per_step": round(dtv / K * 1e3, 4),
+                    "steps": K, "warmup": Wm}
+
+        bucketed = opencv_order = None
+        if all_pairs:
+            BS, PB = 50, 4
+            if not args.no_bucketed:
+                bucketed = dict(headline_variant(bucket_size=BS, per_bucket=PB), bucket_size=BS, per_bucket=PB)
+            if not args.no_opencv_order:
+                # both LK calls summed in OpenCV's own float order (SVO_LK_OPENCV_ORDER: the
+                # drop-in Tracking mirror's default, bit-identical to cv::calcOpticalFlowPyrLK's
+                # x86 build) instead of exactly (the headline): one feature per wave
+                print("[bench] OpenCV-order LK workload", file=sys.stderr, flush=True)
+                opencv_order = dict(headline_variant(lk_flags=S.LK_GET_MIN_EIGENVALS | S.LK_OPENCV_ORDER),
+                                    lk="SVO_LK_OPENCV_ORDER (lk_cv_kernel, one feature per wave)")
+        side.update(single=single, bucketed=bucketed, forward=forward, orb=orb, stream=stream,
+                    opencv_order=opencv_order)
 
     legs_after = args.legs == "after" or world > 1
     if not legs_after:
@@ -729,7 +744,8 @@ def main():
     print("[bench] timed window done", file=sys.stderr, flush=True)
     if legs_after:
         side_legs(close_fe=fe.close)
-    single, bucketed, forward, orb, stream = (side[k] for k in ("single", "bucketed", "forward", "orb", "stream"))
+    single, bucketed, forward, orb, stream, opencv_order = (
+        side[k] for k in ("single", "bucketed", "forward", "orb", "stream", "opencv_order"))
     out = {
         "metric": "frames/sec @1241x376, 2000 feats; LK iters/sec; achieved HBM GB/s",
         "value": round(fps, 2),
@@ -752,7 +768,7 @@ def main():
         "side_legs": "after" if legs_after else "first",
         "single_stream_fps": round(single, 2) if single else None,
         "bucketed": bucketed,
-        "workloads": {"forward": forward, "orb_reference": orb, "stream": stream},
+        "workloads": {"forward": forward, "orb_reference": orb, "stream": stream, "opencv_order": opencv_order},
         "phase_ms_per_step": {k: round(v[0] / K, 4) for k, v in phases.items()},
         "stats_per_step": {k: round(v / K, 3) for k, v in tot.items()},
         "step_ms": {"mean": round(float(np.mean(step_s)) * 1e3, 4),

@@ -1,9 +1,13 @@
 """LK accumulation order through the loop (CPU only, oracle vs oracle).
 
-The product's LK kernels sum the normal equations exactly (integers, one
-rounding: lk.hip) and equal the oracle's ACC_EXACT bit for bit (the GPU suite).
-OpenCV sums them in float, SSE-lane order (oracle ACC_SSE). This measures what
-that one deliberate deviation does to the reference's loop
+The product's LK has two summation modes. SVO_LK_OPENCV_ORDER (the drop-in
+Tracking mirror's default) sums the normal equations in OpenCV's own float
+SSE-lane order and equals the oracle's ACC_SSE bit for bit -- per call and
+through 200 frames of the loop, with no exemption (tests/test_lk_opencv_order_gpu.py).
+The batched benchmark front end's default sums exactly (integers, one rounding:
+lk.hip) and equals the oracle's ACC_EXACT bit for bit (the GPU suite). This file
+characterises only that second, documented choice: what exact sums instead of
+OpenCV's float order do to the reference's loop
 (R:src/tracking.cpp:154-179 trackFrames, :181-230 calculatePose) on the
 KITTI-size bench scene and the forward / occluder scene:
 

@@ -6,7 +6,7 @@ cd "${GRAFT_REPO_ROOT:-/root/repo}"
 mkdir -p gpurun_out
 runs=$1; shift
 for r in $(seq $runs); do for a in "$@"; do
-    timeout -k 10 200 python bench.py --steps ${AB_STEPS:-40} --warmup 5 --no-cpu-baseline --no-single --no-bucketed \
+    timeout -k 10 200 python bench.py --steps ${AB_STEPS:-40} --warmup 5 --no-cpu-baseline --no-single --no-bucketed --no-opencv-order \
         --no-forward --no-orb $a > gpurun_out/ab_args.log 2>&1 || { tail -20 gpurun_out/ab_args.log; exit 1; }
     python -c "
 import json; d=json.loads(open('gpurun_out/ab_args.log').read().strip().splitlines()[-1]); sm=d.get('step_ms', {})

@@ -25,7 +25,7 @@ cd /tmp && export TMPDIR=/tmp
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 O=gpurun_out
 mkdir -p $O
-BQ="python bench.py --steps ${AB_STEPS:-20} --warmup 5 --no-cpu-baseline --no-single --no-bucketed --no-forward --no-orb --no-stream ${AB_ARGS:-}"
+BQ="python bench.py --steps ${AB_STEPS:-20} --warmup 5 --no-cpu-baseline --no-single --no-bucketed --no-opencv-order --no-forward --no-orb --no-stream ${AB_ARGS:-}"
 
 fail() { echo "FAILED: $1"; [ -n "$2" ] && tail -30 "$2"; exit 1; }
 
@@ -58,7 +58,7 @@ run_trace() {
     local T=/tmp/svo_trace
     local steps=${1:-12}; shift
     SVO_FE_TRACE=1 timeout -k 10 300 rocprofv3 --kernel-trace --memory-copy-trace -d $T -o run --output-format csv -- \
-        python bench.py --steps $steps --warmup 3 --seq 64 --no-cpu-baseline --no-single --no-bucketed --no-forward --no-orb --no-stream "$@" \
+        python bench.py --steps $steps --warmup 3 --seq 64 --no-cpu-baseline --no-single --no-bucketed --no-opencv-order --no-forward --no-orb --no-stream "$@" \
         > $T.log 2>&1 || fail trace $T.log
     python tools/timeline.py $T > $O/timeline.txt
     grep "fe t=\|fe post t=" $T.log | tail -24 > $O/hosttrace.txt
@@ -67,7 +67,7 @@ run_trace() {
 
 run_prof() {
     local tag=$1; shift
-    local args="${*:---steps 50 --warmup 10 --no-cpu-baseline --no-single --no-bucketed --no-forward --no-orb --no-stream}"
+    local args="${*:---steps 50 --warmup 10 --no-cpu-baseline --no-single --no-bucketed --no-opencv-order --no-forward --no-orb --no-stream}"
     rm -rf $O/prof_$tag
     timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/prof_$tag -o run --output-format csv -- \
         python bench.py $args > $O/prof_$tag.log 2>&1 || fail prof $O/prof_$tag.log
@@ -82,7 +82,7 @@ P
 
 run_pmc() {
     local tag=$1 cfg=$2 seq=${3:-128}
-    local B="python bench.py --config $cfg --seq $seq --steps 10 --warmup 3 --no-cpu-baseline --no-single --no-bucketed --no-forward --no-orb --no-stream"
+    local B="python bench.py --config $cfg --seq $seq --steps 10 --warmup 3 --no-cpu-baseline --no-single --no-bucketed --no-opencv-order --no-forward --no-orb --no-stream"
     rm -rf $O/pmc_fetch_$cfg $O/pmc_write_$cfg
     timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE -d $O/pmc_fetch_$cfg -o run --output-format csv -- $B \
         > $O/pmc_fetch_$cfg.log 2>&1 || fail pmc-fetch $O/pmc_fetch_$cfg.log
@@ -97,7 +97,7 @@ run_pmc() {
 
 run_mix() {
     local tag=$1; shift
-    local B="python bench.py ${*:---seq 256 --steps 8 --warmup 2 --no-cpu-baseline --no-single --no-bucketed --no-forward --no-orb --no-stream}"
+    local B="python bench.py ${*:---seq 256 --steps 8 --warmup 2 --no-cpu-baseline --no-single --no-bucketed --no-opencv-order --no-forward --no-orb --no-stream}"
     [ "$1" = "--cmd" ] && { shift; B="$*"; }
     timeout -s KILL 200 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_WAIT_INST_ANY \
         SQ_ACTIVE_INST_ANY SQ_INSTS_VMEM -d /tmp/ps1 -o run --output-format csv -- $B > $O/mix.log 2>&1 || fail mix1 $O/mix.log
@@ -216,7 +216,7 @@ run_abcfg() {
         [ $cfg = kitti ] && seq=64
         for v in $vals; do
             env $var=$v timeout -k 10 200 python bench.py --config $cfg --seq $seq --steps 20 --warmup 5 --no-cpu-baseline \
-                --no-single --no-bucketed --no-forward --no-orb --no-stream > $O/abc.log 2>&1 || fail abcfg $O/abc.log
+                --no-single --no-bucketed --no-opencv-order --no-forward --no-orb --no-stream > $O/abc.log 2>&1 || fail abcfg $O/abc.log
             python -c "
 import json; d=json.loads(open('$O/abc.log').read().strip().splitlines()[-1]); p=d['phase_ms_per_step']
 print('$cfg $var=$v', d['value'], d['ms_per_step'], 'lk', p['lk'], 'stereo', p['stereo_lk'])"

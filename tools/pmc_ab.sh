@@ -1,7 +1,7 @@
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 O=gpurun_out; mkdir -p $O
-B="python bench.py --seq 256 --steps 6 --warmup 2 --no-cpu-baseline --no-single --no-bucketed --no-forward --no-orb"
+B="python bench.py --seq 256 --steps 6 --warmup 2 --no-cpu-baseline --no-single --no-bucketed --no-opencv-order --no-forward --no-orb"
 for v in 0 1; do
   for c in FETCH_SIZE WRITE_SIZE; do
     rm -rf /tmp/pab_$c_$v

@@ -6,7 +6,7 @@ cd "${GRAFT_REPO_ROOT:-/root/repo}"
 O=gpurun_out
 mkdir -p $O
 for r in $(seq ${2:-1}); do for s in $1; do
-    timeout -k 10 400 python bench.py --seq $s --steps 20 --warmup 5 --no-cpu-baseline --no-single --no-bucketed \
+    timeout -k 10 400 python bench.py --seq $s --steps 20 --warmup 5 --no-cpu-baseline --no-single --no-bucketed --no-opencv-order \
         --no-forward --no-orb > $O/seq_$s.log 2>&1 || { echo "FAILED seq $s"; tail -20 $O/seq_$s.log; exit 1; }
     python3 -c "
 import json; d=json.loads(open('$O/seq_$s.log').read().strip().splitlines()[-1]); sm=d['step_ms']

@@ -8,7 +8,7 @@ O=gpurun_out
 mkdir -p $O
 runs=${1:-3}; shift
 for r in $(seq $runs); do
-    timeout -k 10 300 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-single --no-bucketed --no-forward --no-orb "$@" \
+    timeout -k 10 300 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-single --no-bucketed --no-opencv-order --no-forward --no-orb "$@" \
         > $O/steady_$r.log 2>&1 || { echo "FAILED run $r"; tail -30 $O/steady_$r.log; exit 1; }
     python - $O/steady_$r.log <<'P'
 import json, sys
