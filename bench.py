@@ -803,6 +803,15 @@ def main():
             "algorithmic_bytes_per_launch": pyr_bytes,
             "derivative_bytes_per_launch": der_bytes,
             "achieved_incl_derivatives": round((pyr_bytes + der_bytes) / pyr_avg_s / 1e9, 2) if pyr_avg_s > 0 else 0.0,
+            # PMC bytes over the algorithmic bytes: SURVEY's B_pyr counts the image levels
+            # only; the chain also writes each level's Scharr pair (int16 Ix, Iy per pixel),
+            # the plane OpenCV's calcOpticalFlowPyrLK computes per call and per level
+            # (lkpyramid.cpp: calcSharrDeriv into derivIBuf) -- written once per frame here
+            # and read by both of the reference's LK calls on that frame (stereo, and the
+            # next step's temporal call)
+            "traffic_over_algorithmic": round(pyr_traffic / pyr_bytes, 3) if pyr_traffic else None,
+            "traffic_over_algorithmic_incl_derivatives": (round(pyr_traffic / (pyr_bytes + der_bytes), 3)
+                                                          if pyr_traffic else None),
             "avg_launch_us": round(pyr_avg_s * 1e6, 3),
             "timing": "alone, 20 launches (HIP events on the launch stream)",
             "in_step_avg_launch_us": round(pyr_instep_s * 1e6, 3),

@@ -422,6 +422,11 @@ int svo_frontend_time_fast(svo_frontend* fe, int t, int reps, double* ms_per_lau
 int svo_host_cpu_plan(int local_rank, int local_world, const int* gpu_node, int* cpus, int cap, int* n);
 /* The CPUs a front end's pool threads are pinned to (empty: not pinned). */
 int svo_frontend_host_cpus(svo_frontend* fe, int* cpus, int cap, int* n);
+/* The HIP streams a front end runs on (LK, FAST, copies; hipStream_t as void*):
+ * the context's, shared by every front end created on it, so a long-lived
+ * process that creates and destroys front ends binds one fixed set of hardware
+ * queues. */
+int svo_frontend_streams(svo_frontend* fe, void** streams, int cap, int* n);
 /* Self-test of the front end's host pool (no GPU): `jobs` jobs of changing sizes
  * with primes between them on `threads` threads; *bad = tasks run other than
  * exactly once, or after their job returned (0 when the pool is correct). */

@@ -145,6 +145,7 @@ _SIGS = [
     ("svo_frontend_reset_times", None, [_vp]),
     ("svo_host_cpu_plan", C.c_int, [C.c_int, C.c_int, _i32p, _i32p, C.c_int, _i32p]),
     ("svo_frontend_host_cpus", C.c_int, [_vp, _i32p, C.c_int, _i32p]),
+    ("svo_frontend_streams", C.c_int, [_vp, C.POINTER(_vp), C.c_int, _i32p]),
     ("svo_pool_selftest", C.c_int, [C.c_int, C.c_int, C.POINTER(C.c_int64)]),
 ]
 
@@ -762,6 +763,13 @@ class Frontend:
         n = C.c_int(0)
         self.ctx._check(lib().svo_frontend_host_cpus(self.handle, _p(cpus, _i32p), 4096, C.byref(n)))
         return cpus[:n.value].tolist()
+
+    def streams(self):
+        """The HIP stream handles (LK, FAST, copies) this front end runs on."""
+        arr = (_vp * 3)()
+        n = C.c_int(0)
+        self.ctx._check(lib().svo_frontend_streams(self.handle, arr, 3, C.byref(n)))
+        return [arr[i] for i in range(n.value)]
 
     def close(self):
         if getattr(self, "handle", None):

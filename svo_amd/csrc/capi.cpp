@@ -150,6 +150,11 @@ void svo_ctx_destroy(svo_ctx* ctx) {
         if (ctx->ingest_host[i]) (void)hipHostFree(ctx->ingest_host[i]);
         if (ctx->ingest_ev[i]) (void)hipEventDestroy(ctx->ingest_ev[i]);
     }
+    for (hipStream_t st : {ctx->fe_lk, ctx->fe_fast, ctx->fe_copy, ctx->fe_up})
+        if (st) {
+            (void)hipStreamSynchronize(st);
+            (void)hipStreamDestroy(st);
+        }
     (void)hipStreamDestroy(ctx->stream);
     delete ctx;
 }

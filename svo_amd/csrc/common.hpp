@@ -76,6 +76,13 @@ struct svo_ctx {
     size_t ingest_bytes[2] = {0, 0};
     hipEvent_t ingest_ev[2] = {nullptr, nullptr};
     int ingest_next = 0;
+    // The batched front ends' streams (LK: highest priority, FAST: lowest, copies,
+    // uploads), created with the first front end and shared by every later one on
+    // this context: each stream binds a hardware queue, so a long-lived process
+    // that creates and destroys front ends (a second one made while the first lived
+    // bound three more) keeps one fixed set of queues, and front ends on one
+    // context are ordered on them.
+    hipStream_t fe_lk = nullptr, fe_fast = nullptr, fe_copy = nullptr, fe_up = nullptr;
 };
 
 namespace svo {

@@ -9,6 +9,7 @@
 
 #include "dlt.hpp"
 #include "frontend.hpp"
+#include "suffstats.hpp"
 
 namespace svo {
 
@@ -301,9 +302,14 @@ __global__ __launch_bounds__(kPostBlock) void post_lk_kernel(PostLkBatch B) {
 // LK's input; a speculative prep already wrote them otherwise).
 template <int BS>
 __device__ __forceinline__ void tail_body(const TailBatch& T, int s, bool copy_cand, int* wsum, int* base_s,
-                                          int* n_kept, int* take_out, int* cnt) {
+                                          int* n_kept, int* take_out, int* cnt, double (*spart)[kSuffStats]) {
     const size_t o = (size_t)s * T.cap;
     const uint32_t* __restrict__ bits = T.bits + (size_t)s * T.words_cap;
+    if (T.stats_out) {
+        static_assert(BS == kSuffThreads, "the statistics' reduction order is that of 256 threads");
+        suffstats_block(T.stats_obj + 3 * o, T.xy_in + 2 * o, T.n_in[s], bits, T.ifx, T.ify, T.cx, T.cy, spart,
+                        T.stats_out + kSuffStats * (size_t)s);
+    }
     const int n = block_compact<BS>(
         T.n_in[s], [&](int i) { return ((bits[i >> 5] >> (i & 31)) & 1u) != 0; }, T.xy_in + 2 * o, T.mid_in + o,
         T.xy_out + 2 * o, T.mid_out + o, wsum, base_s, cnt);
@@ -331,8 +337,9 @@ __global__ __launch_bounds__(kFeBlock) void tail_kernel(TailBatch T) {
     __shared__ int wsum[kFeBlock / 64];
     __shared__ int base_s;
     __shared__ int cnt[kCompactChunks * kFeBlock / 64];
+    __shared__ double spart[kSuffThreads / 64][kSuffStats];
     int n, take;
-    tail_body<kFeBlock>(T, blockIdx.x, true, wsum, &base_s, &n, &take, cnt);
+    tail_body<kFeBlock>(T, blockIdx.x, true, wsum, &base_s, &n, &take, cnt, spart);
 }
 
 // findLeftFeaturesInRight's filter + triangulateNewMapPoints for one stereo match:
@@ -425,9 +432,10 @@ __global__ __launch_bounds__(BS) void keyframe_fused_kernel(TailBatch T, AppendB
     __shared__ int wsum[BS / 64];
     __shared__ int base_s;
     __shared__ int cnt[kCompactChunks * BS / 64];
+    __shared__ double spart[kSuffThreads / 64][kSuffStats];
     const int s = blockIdx.x;
     int n, take;
-    tail_body<BS>(T, s, false, wsum, &base_s, &n, &take, cnt);
+    tail_body<BS>(T, s, false, wsum, &base_s, &n, &take, cnt, spart);
     append_body<BS>(A, s, n, take, wsum, &base_s);
 }
 

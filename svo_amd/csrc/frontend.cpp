@@ -391,7 +391,7 @@ struct svo_frontend {
     // post-LK when LK runs long (the forward scene: +3 %; the headline: neutral)
     int pre_after_post = 1;
     int pre_pending = -1;          // frame whose pre-detection waits for fe_post
-    int stats_early = 1;           // SVO_FE_STATS_EARLY: SQPnP statistics queued before the keyframe
+    bool stats_in_tail = false;    // the next fe_keyframe computes the pending SQPnP statistics
     int pre_t = -1;                // frame whose unmasked detection sits in fbits / rowcnt / score_map
     hipEvent_t ev_pre = nullptr;   // that detection done (context stream)
     hipEvent_t ev_fdone = nullptr; // this step's FAST chain done (FAST stream)
@@ -648,6 +648,16 @@ int fe_keyframe(svo_frontend* fe, int t, const int* n_in, const uint32_t* bits, 
     tb.st_xy = fe->st_xy;
     tb.st_n = fe->st_n;
     tb.h_over = fe->h_over;
+    if (fe->stats_in_tail) {
+        // the pending SQPnP statistics of these inliers (the step's bits and points)
+        tb.stats_obj = fe->obj_b[fe->stats_parity];
+        tb.stats_out = fe->h_stats;
+        tb.ifx = 1. / c.K[0];
+        tb.ify = 1. / c.K[4];
+        tb.cx = c.K[2];
+        tb.cy = c.K[5];
+        fe->stats_in_tail = false;
+    }
     AppendBatch ab;
     ab.n = fe->nA;
     ab.xy = fe->xyA;
@@ -1035,8 +1045,6 @@ int svo_frontend_create(svo_ctx* ctx, const svo_frontend_config* cfg, svo_fronte
         fe->fast_pre = fp && fp[0] == '0' ? 0 : 1;
         const char* pp = std::getenv("SVO_FE_PRE_AFTER_POST");
         fe->pre_after_post = pp && pp[0] == '0' ? 0 : 1;
-        const char* se2 = std::getenv("SVO_FE_STATS_EARLY");
-        fe->stats_early = se2 && se2[0] == '0' ? 0 : 1;
         const char* sm = std::getenv("SVO_FE_SPEC_MARGIN");
         fe->spec_margin = sm ? std::atoi(sm) : 32;
         const char* se = std::getenv("SVO_FE_SPEC_EARLY");
@@ -1098,11 +1106,16 @@ int svo_frontend_create(svo_ctx* ctx, const svo_frontend_config* cfg, svo_fronte
         // path), the FAST stream at the lowest (FAST fills the CUs LK leaves idle
         // and the post-LK window; the speculative stereo LK behind it is ready
         // long before the keyframe needs it)
-        if (fe_make_stream(&fe->st_lk, greatest) != hipSuccess || fe_make_stream(&fe->st_fast, least) != hipSuccess ||
-            hipStreamCreateWithFlags(&fe->st_copy, hipStreamNonBlocking) != hipSuccess) {
+        // (the context's: created once, shared by every front end on it, svo_ctx)
+        if ((!ctx->fe_lk && fe_make_stream(&ctx->fe_lk, greatest) != hipSuccess) ||
+            (!ctx->fe_fast && fe_make_stream(&ctx->fe_fast, least) != hipSuccess) ||
+            (!ctx->fe_copy && hipStreamCreateWithFlags(&ctx->fe_copy, hipStreamNonBlocking) != hipSuccess)) {
             svo_frontend_destroy(fe);
             return set_error(ctx, SVO_ERR_HIP, "svo_frontend_create: stream");
         }
+        fe->st_lk = ctx->fe_lk;
+        fe->st_fast = ctx->fe_fast;
+        fe->st_copy = ctx->fe_copy;
         for (hipEvent_t* e : {&fe->ev_pyr, &fe->ev_fast, &fe->ev_lk, &fe->ev_post, &fe->ev_tail, &fe->ev_stats,
                               &fe->ev_pyr_r_b[0], &fe->ev_pyr_r_b[1], &fe->ev_pre, &fe->ev_fdone, &fe->ev_full_b[0],
                               &fe->ev_full_b[1]})
@@ -1121,11 +1134,9 @@ int svo_frontend_create(svo_ctx* ctx, const svo_frontend_config* cfg, svo_fronte
 void svo_frontend_destroy(svo_frontend* fe) {
     if (!fe) return;
     if (fe->ctx) (void)hipStreamSynchronize(fe->ctx->stream);
-    for (hipStream_t st : {fe->st_lk, fe->st_fast, fe->st_copy})
-        if (st) {
-            (void)hipStreamSynchronize(st);
-            (void)hipStreamDestroy(st);
-        }
+    // (the streams are the context's: finished here, destroyed with the context)
+    for (hipStream_t st : {fe->st_lk, fe->st_fast, fe->st_copy, fe->st_up})
+        if (st) (void)hipStreamSynchronize(st);
     delete fe->pool;
     for (auto* v : {&fe->frames, &fe->frames_r})
         for (auto* f : *v)
@@ -1141,10 +1152,6 @@ void svo_frontend_destroy(svo_frontend* fe) {
                          fe->ev_pyr_r_b[1], fe->ev_pre, fe->ev_fdone, fe->ev_full_b[0], fe->ev_full_b[1]})
         if (e) (void)hipEventDestroy(e);
     if (fe->score_map) (void)hipFree(fe->score_map);
-    if (fe->st_up) {
-        (void)hipStreamSynchronize(fe->st_up);
-        (void)hipStreamDestroy(fe->st_up);
-    }
     for (hipEvent_t e : fe->ev_up)
         if (e) (void)hipEventDestroy(e);
     for (hipEvent_t e : fe->ev_free)
@@ -1246,8 +1253,9 @@ int svo_frontend_queue_frames(svo_frontend* fe, int t, const uint8_t* const* lef
     if (fe->stepped >= 0 && (t < fe->stepped + 3 || t > fe->stepped + T - 1))
         return set_error(ctx, SVO_ERR_ARG, "svo_frontend_queue_frames: frame outside the ring window "
                                            "(stepped + 3 .. stepped + n_frames - 1)");
-    if (!fe->st_up) {
-        SVO_HIP(ctx, hipStreamCreateWithFlags(&fe->st_up, hipStreamNonBlocking));
+    if (fe->up_t.empty()) {
+        if (!ctx->fe_up) SVO_HIP(ctx, hipStreamCreateWithFlags(&ctx->fe_up, hipStreamNonBlocking));
+        fe->st_up = ctx->fe_up;
         fe->ev_up.assign(T, nullptr);
         for (auto& e : fe->ev_up) SVO_HIP(ctx, hipEventCreateWithFlags(&e, hipEventDisableTiming));
         fe->up_t.assign(T, -1);
@@ -1890,18 +1898,17 @@ int svo_frontend_step(svo_frontend* fe, int t, svo_frontend_stats* stats) {
     fe->ransac_drop = ransac_drop;
     ms_fit += ms_since(tf);
     TP("selected");
-    // the SQPnP statistics only feed the pose fits, which run during the next
-    // step's LK: they are queued then (fe_queue_stats), off the critical path
+    // the SQPnP statistics of these inliers feed the pose fits the host runs during
+    // the next step's LK. They are computed by the keyframe's outlier compaction
+    // (the same workgroup reads the same points and bits: suffstats.hpp), so they
+    // are done when the keyframe is, ahead of the next LK on the same queue. As a
+    // kernel of their own on the copy stream they were at times dispatched only
+    // after the next LK had filled the GPU -- in a process that had run other front
+    // ends first, every step (host_ms_fit 2.25 ms instead of 0.33: the headline
+    // 12 % slower, profiles/r06/c_legs_order_cause.txt)
     fe->stats_pending = true;
     fe->stats_parity = t & 1;
-    // (SVO_FE_STATS_EARLY, default 1) the statistics go out now, ahead of the
-    // keyframe: queued behind it, they were at times dispatched only after the next
-    // LK had filled the GPU, and the next step's pose fits then waited for that LK
-    // (host_ms_fit 2.2 ms instead of 0.33 in ~1 step of 13)
-    if (fe->stats_early) {
-        rc = fe_queue_stats(fe);
-        if (rc) return rc;
-    }
+    fe->stats_in_tail = true;
     // ORB: the keyframe's detection, on the steps that take a keyframe
     if (fe->orb) {
         bool any = false;
@@ -1925,6 +1932,18 @@ int svo_frontend_step(svo_frontend* fe, int t, svo_frontend_stats* stats) {
     rc = fe_keyframe(fe, t, fe->nB, fe->h_best, fe->xyB, fe->midB, max_take, sl, spec_ok);
     if (rc) return rc;
     SVO_HIP(ctx, hipEventRecord(fe->ev_tail, sl));
+    if (!fe->stats_in_tail) {  // (fe_keyframe took them: done with the compaction)
+        SVO_HIP(ctx, hipEventRecord(fe->ev_stats, sl));
+        if (fe->device_fits) {  // the device's SQPnP fits from them, on the copy stream
+            const int p = fe->stats_parity;
+            SVO_HIP(ctx, hipStreamWaitEvent(fe->st_copy, fe->ev_stats, 0));
+            SVO_HIP(ctx, launch_sqpnp_fit(fe->h_stats, fe->h_fitin, fe->obj_b[p], fe->nB_b[p], fe->CAP,
+                                          fe->h_best_b[p], fe->WORDS, fe->S, fe->h_pose6, fe->h_pose, fe->fit_work,
+                                          fe->st_copy));
+            SVO_HIP(ctx, hipEventRecord(fe->ev_stats, fe->st_copy));
+        }
+        fe->stats_pending = false;
+    }
     TP("tail queued");
     {
         int mt = fe->CAP;
@@ -2176,6 +2195,14 @@ int svo_frontend_host_cpus(svo_frontend* fe, int* cpus, int cap, int* n) {
     if (!fe || cap < 0 || (cap > 0 && !cpus)) return SVO_ERR_ARG;
     for (int i = 0; i < (int)fe->host_cpus.size() && i < cap; i++) cpus[i] = fe->host_cpus[i];
     if (n) *n = (int)fe->host_cpus.size();
+    return SVO_OK;
+}
+
+int svo_frontend_streams(svo_frontend* fe, void** streams, int cap, int* n) {
+    if (!fe || cap < 0 || (cap > 0 && !streams)) return SVO_ERR_ARG;
+    const hipStream_t st[3] = {fe->st_lk, fe->st_fast, fe->st_copy};
+    for (int i = 0; i < 3 && i < cap; i++) streams[i] = (void*)st[i];
+    if (n) *n = 3;
     return SVO_OK;
 }
 

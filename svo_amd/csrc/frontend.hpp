@@ -76,6 +76,12 @@ struct TailBatch {
     // detector's raw count: a keyframe under Tracking::nextFrame's rule takes every
     // masked corner, so anything here is a capacity overflow there)
     int* h_over;
+    // nullable: SQPnP's sufficient statistics of the inliers (suffstats.hpp) into
+    // stats_out[s][40] (host-coherent), from xy_in / stats_obj / bits -- computed by
+    // the same workgroup, so the statistics are done when the keyframe is
+    const float* stats_obj = nullptr;
+    double* stats_out = nullptr;
+    double ifx = 0, ify = 0, cx = 0, cy = 0;
 };
 hipError_t launch_tail(const TailBatch& tb, int nseq, hipStream_t st);
 

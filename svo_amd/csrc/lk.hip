@@ -1540,7 +1540,14 @@ __device__ __forceinline__ void group_sum_f(int (&v)[NV], float (&f)[NV]) {
     for (int i = 0; i < NV; i++) f[i] = halves_lane_float(h[i], lo[i]);
 }
 
-template <int FPW, int QJM, int MINW, int KKS = 2, int WW = 21, int WH = 21, int NR = 7>
+// LOOP (the stereo call): the grid covers LKBatch::grid_hint features per sequence
+// (the expected count) and a block whose sequence holds more takes the tiles
+// gridDim.x, 2 gridDim.x, ... further on; without it (the temporal call) a block
+// owns one tile and blocks past a sequence's count return at once. The stereo
+// call's bound is the feature budget (~2,100 per sequence) while the speculative
+// count is ~100: sized to the bound, 131k of its 134k waves per launch only read a
+// count and exited, dispatched beside LK.
+template <int FPW, int QJM, int MINW, int KKS = 2, int WW = 21, int WH = 21, int NR = 7, bool LOOP = false>
 __global__ __launch_bounds__(64, MINW) void lk_multi_kernel(LKBatch B, LKDev p) {
     using Q = MultiShape<QJM, WW, WH, FPW>;
     static_assert(WH % NR == 0, "whole strips");
@@ -1567,7 +1574,9 @@ __global__ __launch_bounds__(64, MINW) void lk_multi_kernel(LKBatch B, LKDev p) 
     const XcdTile tile = p.xcd ? xcd_tile() : XcdTile{(int)blockIdx.x, (int)blockIdx.y, 0};
     const int seq = tile.y;
     const int n = B.counts ? B.counts[seq] : B.n;
-    const int pt0 = tile.x * FPW;
+    int tx = tile.x;
+next_tile:  // (LOOP: the block's next tile, gridDim.x further on)
+    const int pt0 = tx * FPW;
     if (pt0 >= n) return;
     const int pt = pt0 + g;
     const bool live = pt < n;
@@ -1865,15 +1874,18 @@ __global__ __launch_bounds__(64, MINW) void lk_multi_kernel(LKBatch B, LKDev p) 
             B.iters[base + pt] = itcount;
         }
     }
+    if constexpr (LOOP) {
+        tx += gridDim.x;
+        goto next_tile;
+    }
 }
 
-template <int FPW, int QJM, int MINW = 4, int KKS = 2, int WW = 21, int WH = 21, int NR = 7>
+template <int FPW, int QJM, int MINW = 4, int KKS = 2, int WW = 21, int WH = 21, int NR = 7, bool LOOP = false>
 hipError_t launch_multi(const LKBatch& b, int nseq, int max_n, const LKDev& d, hipStream_t st) {
-    // (no grid_hint: a block owns FPW features and does not loop; blocks past a
-    // sequence's count return at once)
-    dim3 grid((max_n + FPW - 1) / FPW, nseq);
+    const int gn = LOOP && b.grid_hint > 0 && b.grid_hint < max_n ? b.grid_hint : max_n;
+    dim3 grid((gn + FPW - 1) / FPW, nseq);
     constexpr int lds_bytes = FPW * MultiShape<QJM, WW, WH, FPW>::JSTRIDE;
-    hipLaunchKernelGGL((lk_multi_kernel<FPW, QJM, MINW, KKS, WW, WH, NR>), grid, dim3(64), lds_bytes, st, b, d);
+    hipLaunchKernelGGL((lk_multi_kernel<FPW, QJM, MINW, KKS, WW, WH, NR, LOOP>), grid, dim3(64), lds_bytes, st, b, d);
     return hipGetLastError();
 }
 
@@ -1929,6 +1941,9 @@ bool lk_supported(int win_w, int win_h) {
     return rpg <= 32 && win_w * win_h <= 2048;
 }
 
+#ifndef SVO_LK_STEREO_MINW
+#define SVO_LK_STEREO_MINW 4
+#endif
 hipError_t launch_lk(const LKBatch& b, int nseq, int max_n, const LKParams& lp, hipStream_t st) {
     if (max_n <= 0 || nseq <= 0) return hipSuccess;
     LKDev d;
@@ -1989,7 +2004,7 @@ hipError_t launch_lk(const LKBatch& b, int nseq, int max_n, const LKParams& lp, 
         // the stereo call's 11 x 11 (findLeftFeaturesInRight, no err): four
         // features per wave too, one 11-row strip per lane (11 of 16 lanes)
         if (lp.win_w == 11 && lp.win_h == 11 && multi_ok && lp.quad)
-            return launch_multi<4, 1, 4, 1, 11, 11, 11>(b, nseq, max_n, d, st);
+            return launch_multi<4, 1, SVO_LK_STEREO_MINW, 1, 11, 11, 11, true>(b, nseq, max_n, d, st);
         if (lp.win_w == 21 && lp.win_h == 21) return launch_fast<21, 21>(b, nseq, max_n, d, st);
         if (lp.win_w == 11 && lp.win_h == 11) return launch_fast<11, 11>(b, nseq, max_n, d, st);
         if (lp.win_w == 15 && lp.win_h == 15) return launch_fast<15, 15>(b, nseq, max_n, d, st);

@@ -11,6 +11,7 @@
 // Outputs: optional f32 residuals, inlier bitmask (32 points per word, one
 // ballot per wave), per-hypothesis inlier counts (integer atomics: exact).
 #include "common.hpp"
+#include "suffstats.hpp"
 #include "sqpnp.hpp"
 
 namespace svo {
@@ -137,54 +138,17 @@ namespace {
 
 // Sufficient statistics of the SQPnP cost over each sequence's RANSAC inliers
 // (pose.cpp sqpnp_sums, same per-point arithmetic): one block per sequence,
-// kStats per-thread partial sums, reduced in a fixed order (wave shuffles, then
-// the 4 waves in order) so the result is deterministic.
-constexpr int kStats = 40;  // pose.hpp kSqpnpStats
-__global__ __launch_bounds__(256) void suffstats_kernel(const float* __restrict__ obj, const float* __restrict__ img,
-                                                        const int* __restrict__ counts, int cap,
-                                                        const uint32_t* __restrict__ bits, int words_cap, double ifx,
-                                                        double ify, double cx, double cy, double* __restrict__ out) {
+// suffstats.hpp (the keyframe's compaction computes the same in the step).
+__global__ __launch_bounds__(kSuffThreads) void suffstats_kernel(const float* __restrict__ obj,
+                                                                 const float* __restrict__ img,
+                                                                 const int* __restrict__ counts, int cap,
+                                                                 const uint32_t* __restrict__ bits, int words_cap,
+                                                                 double ifx, double ify, double cx, double cy,
+                                                                 double* __restrict__ out) {
+    __shared__ double part[kSuffThreads / 64][kSuffStats];
     const int s = blockIdx.x;
-    const int n = counts[s];
-    const float* o = obj + 3 * (size_t)s * cap;
-    const float* im = img + 2 * (size_t)s * cap;
-    const uint32_t* b = bits + (size_t)s * words_cap;
-    double acc[kStats];
-#pragma unroll
-    for (int k = 0; k < kStats; k++) acc[k] = 0;
-    for (int i = threadIdx.x; i < n; i += 256) {
-        if (!((b[i >> 5] >> (i & 31)) & 1u)) continue;
-        const double x = ((double)im[2 * i] - cx) * ifx, y = ((double)im[2 * i + 1] - cy) * ify;
-        const double sq = x * x + y * y;
-        const double p[3] = {(double)o[3 * i], (double)o[3 * i + 1], (double)o[3 * i + 2]};
-        const double pp[6] = {p[0] * p[0], p[0] * p[1], p[0] * p[2], p[1] * p[1], p[1] * p[2], p[2] * p[2]};
-        const double c[4] = {1.0, x, y, sq};
-        acc[0] += 1.0;
-        acc[1] += x;
-        acc[2] += y;
-        acc[3] += sq;
-#pragma unroll
-        for (int u = 0; u < 4; u++) {
-#pragma unroll
-            for (int j = 0; j < 3; j++) acc[4 + 3 * u + j] += c[u] * p[j];
-#pragma unroll
-            for (int v = 0; v < 6; v++) acc[16 + 6 * u + v] += c[u] * pp[v];
-        }
-    }
-    __shared__ double part[4][kStats];
-    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
-#pragma unroll
-    for (int k = 0; k < kStats; k++) {
-        double v = acc[k];
-#pragma unroll
-        for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, 64);
-        if (lane == 0) part[wv][k] = v;
-    }
-    __syncthreads();
-    if (threadIdx.x < kStats) {
-        const int k = threadIdx.x;
-        out[kStats * (size_t)s + k] = ((part[0][k] + part[1][k]) + part[2][k]) + part[3][k];
-    }
+    suffstats_block(obj + 3 * (size_t)s * cap, img + 2 * (size_t)s * cap, counts[s], bits + (size_t)s * words_cap,
+                    ifx, ify, cx, cy, part, out + kSuffStats * (size_t)s);
 }
 
 }  // namespace
@@ -509,7 +473,7 @@ hipError_t launch_sqpnp_fit(const double* stats, const SqpnpFitIn* in, const flo
 hipError_t launch_suffstats(const float* obj, const float* img, const int* counts, int cap, const uint32_t* bits,
                             int words_cap, int nseq, const double K[9], double* out, hipStream_t st) {
     if (nseq <= 0) return hipSuccess;
-    hipLaunchKernelGGL(suffstats_kernel, dim3(nseq), dim3(256), 0, st, obj, img, counts, cap, bits, words_cap,
+    hipLaunchKernelGGL(suffstats_kernel, dim3(nseq), dim3(kSuffThreads), 0, st, obj, img, counts, cap, bits, words_cap,
                        1. / K[0], 1. / K[4], K[2], K[5], out);
     return hipGetLastError();
 }
