@@ -1795,9 +1795,6 @@ next_tile:  // (LOOP: the block's next tile, gridDim.x further on)
                 // (results unused)
                 const int off = lact ? __mul24(iny, JRW) + inx - jbase : 0;
                 const unsigned* jb = jmine + off;
-#ifndef SVO_LK_NO_SETPRIO
-                __builtin_amdgcn_s_setprio(0);  // the bulk dot2 work: ordinary priority
-#endif
                 int jlast = 0;  // (ODD) the even strip's last row
 #pragma unroll
                 for (int k = 0; k < K; k++) {
@@ -1828,11 +1825,6 @@ next_tile:  // (LOOP: the block's next tile, gridDim.x further on)
                 }
             }
             float fb[2];
-#ifndef SVO_LK_NO_SETPRIO
-            // the serial tail (reduction -> solve -> next weights / address): raised so
-            // that this wave's dependent chain issues ahead of the others' bulk work
-            __builtin_amdgcn_s_setprio(2);
-#endif
             group_sum_f<LPF, STEPS32>(bsum, fb);
             // materialised here, ahead of the lane-divergent update below: sunk into
             // it, the last DPP step splits into v_mov_dpp + a separate add per value
@@ -1857,9 +1849,6 @@ next_tile:  // (LOOP: the block's next tile, gridDim.x further on)
                 }
             }
         }
-#ifndef SVO_LK_NO_SETPRIO
-        __builtin_amdgcn_s_setprio(0);  // the next level's setup is bulk work again
-#endif
         wave_lds_sync();
     }
     if (l == 0 && live) {
@@ -1941,9 +1930,6 @@ bool lk_supported(int win_w, int win_h) {
     return rpg <= 32 && win_w * win_h <= 2048;
 }
 
-#ifndef SVO_LK_STEREO_MINW
-#define SVO_LK_STEREO_MINW 4
-#endif
 hipError_t launch_lk(const LKBatch& b, int nseq, int max_n, const LKParams& lp, hipStream_t st) {
     if (max_n <= 0 || nseq <= 0) return hipSuccess;
     LKDev d;
@@ -2002,9 +1988,13 @@ hipError_t launch_lk(const LKBatch& b, int nseq, int max_n, const LKParams& lp, 
             return launch_multi<4, 1, 3>(b, nseq, max_n, d, st);
         }
         // the stereo call's 11 x 11 (findLeftFeaturesInRight, no err): four
-        // features per wave too, one 11-row strip per lane (11 of 16 lanes)
+        // features per wave too, one 11-row strip per lane (11 of 16 lanes). Capped
+        // at 80 VGPRs (6 waves per SIMD; a few spills in the per-tile / per-level
+        // code, none in the trip loop) so its waves fit beside LK's three per SIMD
+        // (141 VGPRs each): +1.7 % frames/s over 91 VGPRs
+        // (profiles/r06/e_setprio_stereo_minw_ab.txt)
         if (lp.win_w == 11 && lp.win_h == 11 && multi_ok && lp.quad)
-            return launch_multi<4, 1, SVO_LK_STEREO_MINW, 1, 11, 11, 11, true>(b, nseq, max_n, d, st);
+            return launch_multi<4, 1, 6, 1, 11, 11, 11, true>(b, nseq, max_n, d, st);
         if (lp.win_w == 21 && lp.win_h == 21) return launch_fast<21, 21>(b, nseq, max_n, d, st);
         if (lp.win_w == 11 && lp.win_h == 11) return launch_fast<11, 11>(b, nseq, max_n, d, st);
         if (lp.win_w == 15 && lp.win_h == 15) return launch_fast<15, 15>(b, nseq, max_n, d, st);
