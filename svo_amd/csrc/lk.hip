@@ -494,7 +494,6 @@ __global__ __launch_bounds__(64) void lk_cv_kernel(LKBatch B, LKDev p, CvOrder c
     const int a_len = ck < 4 ? win_h * M4 : win_h * (win_w - se4);
     const int* a_src = terms + cq * npx + (ck < 4 ? ck * win_h * M4 : 4 * win_h * M4);
     const int b_len = ck < 4 ? win_h * B8 : win_h * (win_w - se8);
-    const int b_step = ck < 4 ? 2 : 1;
     const int* b_src = terms + cq * npx + (ck < 4 ? ck * win_h * 2 * B8 : win_h * se8);
 
     const float halfWx = (win_w - 1) * 0.5f, halfWy = (win_h - 1) * 0.5f;
@@ -714,11 +713,18 @@ __global__ __launch_bounds__(64) void lk_cv_kernel(LKBatch B, LKDev p, CvOrder c
                 }
                 wave_lds_sync();
                 float acc = 0.f;
-                if (lane < 10)
-                    for (int i = 0; i < b_len; i++) {
-                        const int* q = b_src + i * b_step;
-                        acc += (float)(q[0] + (b_step == 2 ? q[1] : 0));
+                // (two loops: the SIMD-lane chains add a pair per term, the scalar
+                // chain single terms; one loop with a per-term branch on the step cost
+                // ~10 instructions per term and ran max(len) times for both kinds)
+                if (lane < 10) {
+                    if (ck < 4) {
+#pragma unroll 6
+                        for (int i = 0; i < b_len; i++) acc += (float)(b_src[2 * i] + b_src[2 * i + 1]);
+                    } else {
+#pragma unroll 8
+                        for (int i = 0; i < b_len; i++) acc += (float)b_src[i];
                     }
+                }
                 wave_lds_sync();
                 fb1 = (lane_f(acc, 4) + (((lane_f(acc, 0) + lane_f(acc, 2)) + 0.f) +
                                          ((lane_f(acc, 1) + lane_f(acc, 3)) + 0.f))) * FLT_SCALE;

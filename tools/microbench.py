@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Kernel micro-benchmarks through the C ABI (for rocprofv3 runs).
 
-    python tools/microbench.py lk --points 128000 --reps 5
+    python tools/microbench.py lk --points 128000 --reps 5 [--cv]
     python tools/microbench.py pyr --reps 20
     python tools/microbench.py fast --reps 20
     python tools/microbench.py fepyr --reps 20 --seq 64   (the front end's batched pyramid chain)
@@ -28,6 +28,7 @@ def main():
     ap.add_argument("--w", type=int, default=1241)
     ap.add_argument("--h", type=int, default=376)
     ap.add_argument("--count", type=int, default=0, help="override the LK iteration cap")
+    ap.add_argument("--cv", action="store_true", help="LK in OpenCV's float order (SVO_LK_OPENCV_ORDER)")
     args = ap.parse_args()
     ctx = S.Context(0)
     sc = Scene(args.w, args.h, seed=0)
@@ -43,6 +44,8 @@ def main():
             ((11, 11), (3, 30, 1e-3), 0)
         if args.count:
             crit = (crit[0], args.count, crit[2])
+        if args.cv:
+            flags |= S.LK_OPENCV_ORDER
         for r in range(args.reps):
             t = time.perf_counter()
             ctx.calc_optical_flow_pyr_lk(ga, gb, pts, win_size=win, max_level=3, criteria=crit, flags=flags)
