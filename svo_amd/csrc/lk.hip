@@ -1875,6 +1875,426 @@ next_tile:  // (LOOP: the block's next tile, gridDim.x further on)
     }
 }
 
+// ---------------------------------------------------------------------------
+// OpenCV's float summation order, four features per wave (lk_cvq_kernel): the
+// sums of lk_cv_kernel (the same chains, the same 2^24 shortcut, the same
+// combination of lanes: oracle/lk.c ACC_SSE) on lk_multi_kernel's lane map and
+// staging. lk_cv_kernel runs one feature per wave, so its ordered chains -- ten
+// per iteration, fifteen per level -- kept 10-15 of 64 lanes busy; here each
+// 16-lane group runs its own feature's chains on its lanes 0-9 / 0-14, four
+// features at once.
+//  * setup per level: every strip lane samples I (x32), Ix, Iy at its pixels
+//    (fixed point, as lk_multi_kernel) and keeps them; Ix | Iy << 16 go to the
+//    group's LDS window in the A chains' order; the exact A sums decide the
+//    shortcut (A11, A22 <= 2^24: every chain exact);
+//  * iteration: the b terms d Ix, d Iy of every pixel go to the group's LDS region
+//    in the b chains' order (the A window's place: it is no longer read), the
+//    exact |term| total decides the shortcut.
+// Per wave: the four groups' next-image regions (MultiShape), their term regions
+// (2 win_w win_h ints) and the chain results (16 floats per group).
+template <int WW, int WH, int NR>
+struct CvqShape {
+    using Q = MultiShape<1, WW, WH, 4>;
+    static constexpr int NPX = WW * WH;
+    static constexpr int SE4 = WW >= 4 ? ((WW - 4) / 4 + 1) * 4 : 0;  // OpenCV's 4-wide column end
+    static constexpr int SE8 = WW >= 8 ? ((WW - 8) / 8 + 1) * 8 : 0;  // and the 8-wide b loop's
+    static constexpr int M4 = SE4 / 4, B8 = SE8 / 8;
+    static constexpr int TSTRIDE = 2 * NPX;  // ints per group's term region (b1, b2 of a slot adjacent)
+    static constexpr int TERM_OFF = 4 * Q::JSTRIDE;
+    static constexpr int CHAIN_OFF = TERM_OFF + 4 * TSTRIDE * 4;
+    static constexpr int LDS_BYTES = CHAIN_OFF + 4 * 16 * 4;
+    // a pixel's slot in the A chains' order (lane k = x & 3 over x < SE4: row by row,
+    // columns in order; then the scalar chain over the rest)
+    static __device__ __forceinline__ int a_slot(int y, int x) {
+        return x < SE4 ? (x & 3) * WH * M4 + y * M4 + (x >> 2) : 4 * WH * M4 + y * (WW - SE4) + (x - SE4);
+    }
+    // and in the b chains' (lane t = x & 3 over x < SE8: per row and 8-column block
+    // the pair x, x + 4 adjacent; then the scalar chain)
+    static __device__ __forceinline__ int b_slot(int y, int x) {
+        return x < SE8 ? (x & 3) * WH * 2 * B8 + y * 2 * B8 + 2 * (x >> 3) + ((x >> 2) & 1)
+                       : WH * SE8 + y * (WW - SE8) + (x - SE8);
+    }
+};
+
+// group sum of an int32 whose 16-lane total fits int32 (the shortcuts' operands)
+__device__ __forceinline__ int group16_sum(int v) {
+    v = dpp_row_add<0xb1>(v);
+    v = dpp_row_add<0x4e>(v);
+    v = dpp_row_add<0x124>(v);
+    return dpp_row_add<0x128>(v);
+}
+
+template <int WW, int WH, int NR>
+__global__ __launch_bounds__(64, 2) void lk_cvq_kernel(LKBatch B, LKDev p) {
+    constexpr int FPW = 4, LPF = 16;
+    using C = CvqShape<WW, WH, NR>;
+    using Q = typename C::Q;
+    static_assert(WH % NR == 0, "whole strips");
+    static_assert(WW + 4 <= kPyrPad && WW + 1 <= kDerPad, "padding too small for the window");
+    constexpr int JRW = Q::JRW, JRH = Q::JRH, QJM = 1;
+    constexpr int NSTRIP = WW * (WH / NR);
+    constexpr int K = (NSTRIP + LPF - 1) / LPF;
+    constexpr int SE4 = C::SE4, SE8 = C::SE8, M4 = C::M4, B8 = C::B8;
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    const int lane = threadIdx.x & 63;
+    const int g = lane / LPF, l = lane % LPF;
+    const XcdTile tile = p.xcd ? xcd_tile() : XcdTile{(int)blockIdx.x, (int)blockIdx.y, 0};
+    const int seq = tile.y;
+    const int n = B.counts ? B.counts[seq] : B.n;
+    const int pt0 = tile.x * FPW;
+    if (pt0 >= n) return;
+    const int pt = pt0 + g;
+    const bool live = pt < n;
+    const int ptc = live ? pt : n - 1;  // an idle group shadows a real feature, writes nothing
+    const size_t base = (size_t)seq * B.cap;
+    const float* __restrict__ prev_xy = B.prev_xy + 2 * base;
+    float* __restrict__ next_xy = B.next_xy + 2 * base;
+    const cpyr prev = (cpyr)B.prev + seq;
+    const cpyr next = (cpyr)B.next + seq;
+    const DerivDesc& dprev = B.dprev[seq];
+    unsigned* jregs = reinterpret_cast<unsigned*>(lds);
+    const unsigned* jmine = jregs + g * (Q::JSTRIDE / 4);
+    int* terms = reinterpret_cast<int*>(lds + C::TERM_OFF) + g * C::TSTRIDE;
+    float* chains = reinterpret_cast<float*>(lds + C::CHAIN_OFF) + g * 16;
+    const StageGeom<JRW, JRH> sg(lane);
+
+    int scol[K], srow[K];
+    bool sreal[K];
+#pragma unroll
+    for (int k = 0; k < K; k++) {
+        const int sidx = l + LPF * k;
+        sreal[k] = sidx < NSTRIP;
+        const int sc = sreal[k] ? sidx : 0;
+        scol[k] = sc % WW;
+        srow[k] = (sc / WW) * NR;
+    }
+    // the strips' first slots in the A / b chain layouts and their row strides (a
+    // strip is one column): re-derived per level / trip from these (laundered), not
+    // kept per pixel -- 56 hoisted slot registers took the kernel to 308 VGPRs
+    int aslot0[K], astr[K], bslot0[K], bstr[K];
+#pragma unroll
+    for (int k = 0; k < K; k++) {
+        aslot0[k] = C::a_slot(srow[k], scol[k]);
+        astr[k] = C::a_slot(srow[k] + 1, scol[k]) - aslot0[k];
+        bslot0[k] = C::b_slot(srow[k], scol[k]);
+        bstr[k] = C::b_slot(srow[k] + 1, scol[k]) - bslot0[k];
+    }
+    // this lane's chains: A (lanes 0-14: quantity l / 5, SIMD lane l % 5 < 4 or the
+    // scalar chain), b (lanes 0-9: b1 / b2 the same way)
+    const int aq = l / 5, ak = l - 5 * (l / 5);
+    const int a_off = ak < 4 ? ak * WH * M4 : 4 * WH * M4;
+    const int a_len = l < 15 ? (ak < 4 ? WH * M4 : WH * (WW - SE4)) : 0;
+    const int b_off = 2 * (ak < 4 ? ak * WH * 2 * B8 : WH * SE8) + aq;  // (b1, b2 interleaved per slot)
+    const int b_len = l < 10 ? (ak < 4 ? WH * B8 : WH * (WW - SE8)) : 0;
+
+    constexpr float halfWx = (WW - 1) * 0.5f, halfWy = (WH - 1) * 0.5f;
+    const int rnd_i = 1 << (W_BITS - 6), rnd_d = 1 << (W_BITS + kDerShift - 1);
+    const int rnd_j = 1 << (W_BITS - 6 + kJShift);
+
+    const float px = prev_xy[2 * ptc], py = prev_xy[2 * ptc + 1];
+    float nx = 0.f, ny = 0.f;
+    if (p.flags & SVO_LK_USE_INITIAL_FLOW) {
+        nx = next_xy[2 * ptc];
+        ny = next_xy[2 * ptc + 1];
+    }
+    int st = live ? 1 : 0;
+    float errv = 0.f;
+    int itc[FPW];
+#pragma unroll
+    for (int f = 0; f < FPW; f++) itc[f] = 0;
+    const int max_level = p.max_level;
+
+    for (int level = max_level; level >= 0; level--) {
+        const ImgLevel I{prev->lv[level].data, prev->lv[level].w, prev->lv[level].h, prev->lv[level].pitch};
+        const ImgLevel J{next->lv[level].data, next->lv[level].w, next->lv[level].h, next->lv[level].pitch};
+        const float lscale = __builtin_amdgcn_ldexpf(1.f, -level);
+        float prevx = px * lscale, prevy = py * lscale;
+        float nextx, nexty;
+        if (level == max_level) {
+            if (p.flags & SVO_LK_USE_INITIAL_FLOW) {
+                nextx = nx * lscale;
+                nexty = ny * lscale;
+            } else {
+                nextx = prevx;
+                nexty = prevy;
+            }
+        } else {
+            nextx = nx * 2.f;
+            nexty = ny * 2.f;
+        }
+        nx = nextx;
+        ny = nexty;
+        prevx -= halfWx;
+        prevy -= halfWy;
+        const float fpx = __builtin_floorf(prevx), fpy = __builtin_floorf(prevy);
+        const int ipx = (int)fpx, ipy = (int)fpy;
+        const bool inb = (unsigned)(ipx + WW) < (unsigned)(I.w + WW) && (unsigned)(ipy + WH) < (unsigned)(I.h + WH);
+        if (!inb && level == 0 && live) {
+            st = 0;
+            errv = 0.f;
+        }
+        bool lact = live && inb;
+        const BiW iw = bilinear_weights(prevx - fpx, prevy - fpy);
+        const unsigned IW0 = iw.W0, IW1 = iw.W1;
+
+        int jx0 = ufloor(nextx - halfWx) - QJM, jy0 = ufloor(nexty - halfWy) - QJM;
+        int jxa = jx0 & ~3;
+        int jbase = jy0 * JRW + jxa;
+        // per strip pixel: I (x32) | (|Ix| + |Iy|) << 16 and Ix | Iy << 16 (descaled, int16
+        // each; |Ix| + |Iy| <= 8160 prices the b shortcut's bound: |d Ix| + |d Iy| = |d| (|Ix| + |Iy|))
+        unsigned IVS[K][NR];
+        unsigned IXY[K][NR];
+        int a11 = 0, a22 = 0;  // exact partials (the shortcut needs A11 and A22 only)
+        {
+            using SL = StageGeom<JRW, JRH>;
+            int xs[FPW], ys[FPW];
+#pragma unroll
+            for (int f = 0; f < FPW; f++) {
+                const int xa = __builtin_amdgcn_readlane(jxa, LPF * f), y0 = __builtin_amdgcn_readlane(jy0, LPF * f);
+                const bool ok = __builtin_amdgcn_readlane((int)lact, LPF * f) && region_in_pad<JRW, JRH>(J, xa, y0);
+                xs[f] = ok ? xa : 0;
+                ys[f] = ok ? y0 : 0;
+            }
+            {
+                unsigned sv[FPW][SL::NPS];
+                const gu8 jb0 = pad_origin(J.data, J.pitch, kPyrPad, 1) + (size_t)kPyrPad * (J.pitch + 1);
+                const unsigned ol = 4u * (unsigned)sg.d + (unsigned)sg.row(0) * (unsigned)J.pitch;
+                const unsigned olast = 4u * (unsigned)sg.d + (unsigned)sg.row(SL::NPS - 1) * (unsigned)J.pitch;
+#pragma unroll
+                for (int f = 0; f < FPW; f++) {
+                    const gu8 fb = jb0 + xs[f] + (ptrdiff_t)ys[f] * J.pitch;
+#pragma unroll
+                    for (int q = 0; q < SL::NPS; q++)
+                        sv[f][q] = q + 1 < SL::NPS ? ldg_off<unsigned>(fb + (size_t)q * SL::RPP * J.pitch, ol)
+                                                   : ldg_off<unsigned>(fb, olast);
+                }
+#pragma unroll
+                for (int f = 0; f < FPW; f++)
+#pragma unroll
+                    for (int q = 0; q < SL::NPS; q++) sg.write(jregs + f * (Q::JSTRIDE / 4), sg.row(q), sv[f][q]);
+            }
+            const int dpitch = dprev.pitch[level];
+            const gu8 ibase = pad_origin(I.data, I.pitch, kPyrPad, 1);
+            const gu8 dbase = pad_origin((const uint8_t*)dprev.data[level], dpitch, kDerPad, 4);
+            const int sx = inb ? ipx : 0, sy = inb ? ipy : 0;
+#pragma unroll
+            for (int k = 0; k < K; k++) {
+                unsigned P[NR + 1];
+                u32x2a4 Dv[NR + 1];
+                const int x = sx + scol[k], y = sy + srow[k];
+                const unsigned oi = (unsigned)(x + kPyrPad) + (unsigned)(y + kPyrPad) * (unsigned)I.pitch;
+                const unsigned od = 4u * ((unsigned)(x + kDerPad) + (unsigned)(y + kDerPad) * (unsigned)dpitch);
+#pragma unroll
+                for (int r = 0; r <= NR; r++) {
+                    P[r] = __builtin_amdgcn_perm(0u, (unsigned)ldg_off<u16a1>(ibase + (size_t)r * I.pitch, oi),
+                                                 0x0c010c00u);
+                    Dv[r] = ldg_off<u32x2a4>(dbase + (size_t)r * 4 * dpitch, od);
+                }
+                const unsigned GW0 = sreal[k] ? IW0 : 0u, GW1 = sreal[k] ? IW1 : 0u;
+                int as0 = aslot0[k], as1 = astr[k];
+                asm volatile("" : "+v"(as0), "+v"(as1));
+#pragma unroll
+                for (int j = 0; j < NR; j++) {
+                    const int iv = sdot2(P[j], IW0, sdot2_r(P[j + 1], IW1, rnd_i)) >> (W_BITS - 5);
+                    const unsigned X0 = __builtin_amdgcn_perm(Dv[j].y, Dv[j].x, 0x05040100u);
+                    const unsigned X1 = __builtin_amdgcn_perm(Dv[j + 1].y, Dv[j + 1].x, 0x05040100u);
+                    const unsigned Y0 = __builtin_amdgcn_perm(Dv[j].y, Dv[j].x, 0x07060302u);
+                    const unsigned Y1 = __builtin_amdgcn_perm(Dv[j + 1].y, Dv[j + 1].x, 0x07060302u);
+                    const int ix = sdot2(X0, GW0, sdot2_r(X1, GW1, rnd_d)) >> 16;  // CV_DESCALE(., W_BITS)
+                    const int iy = sdot2(Y0, GW0, sdot2_r(Y1, GW1, rnd_d)) >> 16;
+                    IXY[k][j] = pack16(ix, iy);
+                    IVS[k][j] = pack16(iv, abs(ix) + abs(iy));
+                    a11 += ix * ix;
+                    a22 += iy * iy;
+                    if (sreal[k]) terms[as0 + j * as1] = (int)IXY[k][j];
+                }
+                __builtin_amdgcn_sched_barrier(0);  // (one strip's loads in flight at a time)
+            }
+        }
+        wave_lds_sync();
+        // the shortcut: every A chain is exact when A11, A22 <= 2^24 (|Ix Iy| <= (Ix^2 +
+        // Iy^2) / 2); a lane's partials stay < 2^31 (<= NR K 4080^2), capped so that the
+        // group's 16 cannot overflow
+        constexpr int kCap = (1 << 24) + 1;
+        const int e11 = group16_sum(min(a11, kCap)), e22 = group16_sum(min(a22, kCap));
+        const bool a_exact = e11 <= (1 << 24) && e22 <= (1 << 24);
+        float sA[3];
+        {
+            // the exact sums, for the groups the shortcut covers (A12 then too: |A12| <=
+            // 2^24); and the ordered chains if any active group needs them
+            int e12p = 0;
+#pragma unroll
+            for (int k = 0; k < K; k++)
+#pragma unroll
+                for (int j = 0; j < NR; j++) e12p += (int)(short)(IXY[k][j] & 0xffffu) * ((int)IXY[k][j] >> 16);
+            const int e12 = group16_sum(a_exact ? e12p : 0);
+            sA[0] = (float)e11;
+            sA[1] = (float)e12;
+            sA[2] = (float)e22;
+            if (__builtin_amdgcn_ballot_w64(lact && !a_exact)) {
+                float acc = 0.f;
+                const int* src = terms + a_off;
+#pragma unroll 4
+                for (int i = 0; i < a_len; i++) {
+                    const int w = src[i];
+                    const int ix = (int)(short)(w & 0xffff), iy = w >> 16;
+                    acc += (float)(aq == 0 ? ix * ix : aq == 1 ? ix * iy : iy * iy);
+                }
+                if (l < 15) chains[l] = acc;
+                wave_lds_sync();
+                if (!a_exact) {
+#pragma unroll
+                    for (int q = 0; q < 3; q++)
+                        sA[q] = chains[5 * q + 4] + ((chains[5 * q] + chains[5 * q + 2]) + (chains[5 * q + 1] + chains[5 * q + 3]));
+                }
+            }
+        }
+        wave_lds_sync();  // (the A window's reads finish before the b terms reuse it)
+        const float A11 = sA[0] * FLT_SCALE, A12 = sA[1] * FLT_SCALE, A22 = sA[2] * FLT_SCALE;
+        float D = A11 * A22 - A12 * A12;
+        const float minEig = (A22 + A11 - sqrtf((A11 - A22) * (A11 - A22) + 4.f * A12 * A12)) / (float)(2 * WW * WH);
+        if (lact && p.want_err && (p.flags & SVO_LK_GET_MIN_EIGENVALS)) errv = minEig;
+        if (lact && (minEig < p.min_eig || D < FLT_EPSILON)) {
+            if (level == 0) st = 0;
+            lact = false;
+        }
+        D = 1.f / D;
+
+        nextx -= halfWx;
+        nexty -= halfWy;
+        float pdx = 0.f, pdy = 0.f;
+        for (int j = 0; j < p.max_count; j++) {
+            if (__builtin_amdgcn_ballot_w64(lact) == 0) break;
+            const float fnx = __builtin_floorf(nextx), fny = __builtin_floorf(nexty);
+            const int inx = (int)fnx, iny = (int)fny;
+            if (lact && !((unsigned)(inx + WW) < (unsigned)(J.w + WW) && (unsigned)(iny + WH) < (unsigned)(J.h + WH))) {
+                if (level == 0) st = 0;
+                lact = false;
+            }
+            const bool need = lact && ((unsigned)(inx - jx0) > 2u * QJM || (unsigned)(iny - jy0) > 2u * QJM);
+            unsigned long long nb = __builtin_amdgcn_ballot_w64(need && l == 0);
+            if (nb) {
+                if (need) {
+                    jx0 = inx - QJM;
+                    jy0 = iny - QJM;
+                    jxa = jx0 & ~3;
+                    jbase = jy0 * JRW + jxa;
+                }
+                wave_lds_sync();
+                while (nb) {
+                    const int f = (int)(__builtin_ctzll(nb) / LPF);
+                    nb &= nb - 1;
+                    stage_padded<JRW, JRH>(jregs + f * (Q::JSTRIDE / 4), J, __builtin_amdgcn_readlane(jxa, LPF * f),
+                                           __builtin_amdgcn_readlane(jy0, LPF * f), sg);
+                }
+                wave_lds_sync();
+            }
+            {
+                const unsigned long long act = __builtin_amdgcn_ballot_w64(lact);
+#pragma unroll
+                for (int f = 0; f < FPW; f++) itc[f] += (int)((act >> (LPF * f)) & 1ull);
+            }
+            const BiW w = bilinear_weights(nextx - fnx, nexty - fny);
+            const unsigned W0 = w.W0, W1 = w.W1;
+            int b1 = 0, b2 = 0;
+            unsigned babs = 0;
+            {
+                const int off = lact ? __mul24(iny, JRW) + inx - jbase : 0;
+                const unsigned* jb = jmine + off;
+#pragma unroll
+                for (int k = 0; k < K; k++) {
+                    const unsigned* js = jb + srow[k] * JRW + scol[k];
+                    unsigned q[NR + 1];
+#pragma unroll
+                    for (int r = 0; r <= NR; r++) q[r] = js[r * JRW];
+                    int bs0 = bslot0[k], bs1 = bstr[k];
+                    asm volatile("" : "+v"(bs0), "+v"(bs1));
+#pragma unroll
+                    for (int r = 0; r < NR; r++) {
+                        const int jv = sdot2(q[r], W0, sdot2_r(q[r + 1], W1, rnd_j)) >> 16;
+                        const int d = jv - (int)(IVS[k][r] & 0xffffu);
+                        const int t1 = d * (int)(short)(IXY[k][r] & 0xffffu), t2 = d * ((int)IXY[k][r] >> 16);
+                        b1 += t1;
+                        b2 += t2;
+                        // (a lane's <= K NR 8160^2 < 2^31; capped once below so that the
+                        // group's 16 lanes cannot overflow)
+                        babs += __umul24((unsigned)abs(d), IVS[k][r] >> 16);
+                        if (sreal[k]) {
+                            // (b1, b2 of a slot adjacent: one 8-byte store)
+                            int2* tp = reinterpret_cast<int2*>(terms) + (bs0 + r * bs1);
+                            *tp = make_int2(t1, t2);
+                        }
+                    }
+                    __builtin_amdgcn_sched_barrier(0);  // (one strip's temporaries at a time)
+                }
+            }
+            static_assert((long long)K * NR * 8160 * 8160 < (1ll << 31), "a lane's |term| sum must fit int32");
+            const bool b_exact = group16_sum(min((int)babs, kCap)) <= (1 << 24);
+            float fb1 = (float)group16_sum(b_exact ? b1 : 0), fb2 = (float)group16_sum(b_exact ? b2 : 0);
+            if (__builtin_amdgcn_ballot_w64(lact && !b_exact)) {
+                wave_lds_sync();
+                float acc = 0.f;
+                const int* src = terms + b_off;
+                if (ak < 4) {
+#pragma unroll 6
+                    for (int i = 0; i < b_len; i++) acc += (float)(src[4 * i] + src[4 * i + 2]);
+                } else {
+#pragma unroll 8
+                    for (int i = 0; i < b_len; i++) acc += (float)src[2 * i];
+                }
+                if (l < 10) chains[l] = acc;
+                wave_lds_sync();
+                if (!b_exact) {
+                    fb1 = chains[4] + (((chains[0] + chains[2]) + 0.f) + ((chains[1] + chains[3]) + 0.f));
+                    fb2 = chains[9] + (((chains[5] + chains[7]) + 0.f) + ((chains[6] + chains[8]) + 0.f));
+                }
+            }
+            wave_lds_sync();  // (the terms' reads finish before the next iteration's writes)
+            fb1 *= FLT_SCALE;
+            fb2 *= FLT_SCALE;
+            const float dx = (A12 * fb2 - A22 * fb1) * D;
+            const float dy = (A12 * fb1 - A11 * fb2) * D;
+            if (lact) {
+                nextx += dx;
+                nexty += dy;
+                nx = nextx + halfWx;
+                ny = nexty + halfWy;
+                if (converged(dx, dy, p.eps2_lo, p.eps2_hi, p.eps2)) {
+                    lact = false;
+                } else if (j > 0 && below_001(dx + pdx) && below_001(dy + pdy)) {
+                    nx -= dx * 0.5f;
+                    ny -= dy * 0.5f;
+                    lact = false;
+                } else {
+                    pdx = dx;
+                    pdy = dy;
+                }
+            }
+        }
+        wave_lds_sync();
+    }
+    if (l == 0 && live) {
+        next_xy[2 * pt] = nx;
+        next_xy[2 * pt + 1] = ny;
+        B.status[base + pt] = (uint8_t)st;
+        if (B.err) B.err[base + pt] = errv;
+        if (B.iters) {
+            int itcount = itc[0];
+#pragma unroll
+            for (int f = 1; f < FPW; f++) itcount = g == f ? itc[f] : itcount;
+            B.iters[base + pt] = itcount;
+        }
+    }
+}
+
+template <int WW, int WH, int NR>
+hipError_t launch_cvq(const LKBatch& b, int nseq, int max_n, const LKDev& d, hipStream_t st) {
+    dim3 grid((max_n + 3) / 4, nseq);
+    constexpr int lds_bytes = CvqShape<WW, WH, NR>::LDS_BYTES;
+    hipLaunchKernelGGL((lk_cvq_kernel<WW, WH, NR>), grid, dim3(64), lds_bytes, st, b, d);
+    return hipGetLastError();
+}
+
 template <int FPW, int QJM, int MINW = 4, int KKS = 2, int WW = 21, int WH = 21, int NR = 7, bool LOOP = false>
 hipError_t launch_multi(const LKBatch& b, int nseq, int max_n, const LKDev& d, hipStream_t st) {
     const int gn = LOOP && b.grid_hint > 0 && b.grid_hint < max_n ? b.grid_hint : max_n;
@@ -1969,7 +2389,14 @@ hipError_t launch_lk(const LKBatch& b, int nseq, int max_n, const LKParams& lp, 
         d.xcd = lk_xcd ? 1 : 0;
     }
     if (lp.cv_order) {
-        // OpenCV's float summation order: one feature per wave (lk_cv_kernel)
+        // OpenCV's float summation order: the reference's two windows four features
+        // per wave (lk_cvq_kernel; not the SAD error of flags 0 + err), else one per
+        // wave (lk_cv_kernel)
+        const bool multi_ok = !(lp.want_err && !(lp.flags & SVO_LK_GET_MIN_EIGENVALS));
+        if (!lp.generic && lp.quad && multi_ok) {
+            if (lp.win_w == 21 && lp.win_h == 21) return launch_cvq<21, 21, 7>(b, nseq, max_n, d, st);
+            if (lp.win_w == 11 && lp.win_h == 11) return launch_cvq<11, 11, 11>(b, nseq, max_n, d, st);
+        }
 #define SVO_LK_CV_CASE(R) \
     case R: return launch_cv_rpg<R>(b, nseq, max_n, d, st);
         switch (rpg) {

@@ -51,13 +51,23 @@ def _check(ctx, A, B, pts, win, ml, crit, flags, want_err=True):
     return gn, gs
 
 
+@pytest.fixture(params=["four-per-wave", "one-per-wave"])
+def cv_kernel(request, monkeypatch):
+    """Both OpenCV-order kernels: lk_cvq_kernel (21x21 / 11x11, four features per
+    wave; not the SAD error of flags 0 + err) and lk_cv_kernel (one per wave: every
+    other window and SVO_LK_QUAD=0)."""
+    monkeypatch.setenv("SVO_LK_QUAD", "1" if request.param == "four-per-wave" else "0")
+    return request.param
+
+
 @pytest.mark.parametrize("cfg", [TEMPORAL, STEREO], ids=["temporal21", "stereo11"])
 @pytest.mark.parametrize("wh,seed,n", [((1241, 376), 0, 2000), ((160, 120), 1, 300), ((1920, 1080), 2, 4000)])
-def test_lk_opencv_order_bit_exact(ctx, cfg, wh, seed, n):
+@pytest.mark.parametrize("want_err", [True, False], ids=["err", "noerr"])
+def test_lk_opencv_order_bit_exact(ctx, cv_kernel, cfg, wh, seed, n, want_err):
     sc = Scene(*wh, seed=seed)
     A, B = sc.frame(0), sc.frame(1) if cfg is TEMPORAL else sc.right(0)
     pts = O.fast(A, 20, True)[:n, :2]
-    gn, gs = _check(ctx, A, B, pts, cfg["win"], cfg["ml"], cfg["crit"], cfg["flags"])
+    gn, gs = _check(ctx, A, B, pts, cfg["win"], cfg["ml"], cfg["crit"], cfg["flags"], want_err=want_err)
     if wh == (1241, 376):
         # not vacuous: the exact sums (the default) stop elsewhere for some points
         xn, xs, _, _ = O.lk(A, B, pts, cfg["win"], cfg["ml"], cfg["crit"], cfg["flags"], acc=O.ACC_EXACT)
