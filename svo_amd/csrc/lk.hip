@@ -1899,7 +1899,7 @@ struct CvqShape {
     static constexpr int SE4 = WW >= 4 ? ((WW - 4) / 4 + 1) * 4 : 0;  // OpenCV's 4-wide column end
     static constexpr int SE8 = WW >= 8 ? ((WW - 8) / 8 + 1) * 8 : 0;  // and the 8-wide b loop's
     static constexpr int M4 = SE4 / 4, B8 = SE8 / 8;
-    static constexpr int TSTRIDE = 2 * NPX;  // ints per group's term region (b1, b2 of a slot adjacent)
+    static constexpr int TSTRIDE = 2 * NPX;  // ints per group's term region
     static constexpr int TERM_OFF = 4 * Q::JSTRIDE;
     static constexpr int CHAIN_OFF = TERM_OFF + 4 * TSTRIDE * 4;
     static constexpr int LDS_BYTES = CHAIN_OFF + 4 * 16 * 4;
@@ -1925,7 +1925,7 @@ __device__ __forceinline__ int group16_sum(int v) {
 }
 
 template <int WW, int WH, int NR>
-__global__ __launch_bounds__(64, 2) void lk_cvq_kernel(LKBatch B, LKDev p) {
+__global__ __launch_bounds__(64) void lk_cvq_kernel(LKBatch B, LKDev p) {
     constexpr int FPW = 4, LPF = 16;
     using C = CvqShape<WW, WH, NR>;
     using Q = typename C::Q;
@@ -1934,7 +1934,7 @@ __global__ __launch_bounds__(64, 2) void lk_cvq_kernel(LKBatch B, LKDev p) {
     constexpr int JRW = Q::JRW, JRH = Q::JRH, QJM = 1;
     constexpr int NSTRIP = WW * (WH / NR);
     constexpr int K = (NSTRIP + LPF - 1) / LPF;
-    constexpr int SE4 = C::SE4, SE8 = C::SE8, M4 = C::M4, B8 = C::B8;
+    constexpr int NPX = C::NPX, SE4 = C::SE4, SE8 = C::SE8, M4 = C::M4, B8 = C::B8;
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     const int lane = threadIdx.x & 63;
     const int g = lane / LPF, l = lane % LPF;
@@ -1968,23 +1968,12 @@ __global__ __launch_bounds__(64, 2) void lk_cvq_kernel(LKBatch B, LKDev p) {
         scol[k] = sc % WW;
         srow[k] = (sc / WW) * NR;
     }
-    // the strips' first slots in the A / b chain layouts and their row strides (a
-    // strip is one column): re-derived per level / trip from these (laundered), not
-    // kept per pixel -- 56 hoisted slot registers took the kernel to 308 VGPRs
-    int aslot0[K], astr[K], bslot0[K], bstr[K];
-#pragma unroll
-    for (int k = 0; k < K; k++) {
-        aslot0[k] = C::a_slot(srow[k], scol[k]);
-        astr[k] = C::a_slot(srow[k] + 1, scol[k]) - aslot0[k];
-        bslot0[k] = C::b_slot(srow[k], scol[k]);
-        bstr[k] = C::b_slot(srow[k] + 1, scol[k]) - bslot0[k];
-    }
     // this lane's chains: A (lanes 0-14: quantity l / 5, SIMD lane l % 5 < 4 or the
     // scalar chain), b (lanes 0-9: b1 / b2 the same way)
     const int aq = l / 5, ak = l - 5 * (l / 5);
     const int a_off = ak < 4 ? ak * WH * M4 : 4 * WH * M4;
     const int a_len = l < 15 ? (ak < 4 ? WH * M4 : WH * (WW - SE4)) : 0;
-    const int b_off = 2 * (ak < 4 ? ak * WH * 2 * B8 : WH * SE8) + aq;  // (b1, b2 interleaved per slot)
+    const int b_off = aq * NPX + (ak < 4 ? ak * WH * 2 * B8 : WH * SE8);
     const int b_len = l < 10 ? (ak < 4 ? WH * B8 : WH * (WW - SE8)) : 0;
 
     constexpr float halfWx = (WW - 1) * 0.5f, halfWy = (WH - 1) * 0.5f;
@@ -2040,9 +2029,8 @@ __global__ __launch_bounds__(64, 2) void lk_cvq_kernel(LKBatch B, LKDev p) {
         int jx0 = ufloor(nextx - halfWx) - QJM, jy0 = ufloor(nexty - halfWy) - QJM;
         int jxa = jx0 & ~3;
         int jbase = jy0 * JRW + jxa;
-        // per strip pixel: I (x32) | (|Ix| + |Iy|) << 16 and Ix | Iy << 16 (descaled, int16
-        // each; |Ix| + |Iy| <= 8160 prices the b shortcut's bound: |d Ix| + |d Iy| = |d| (|Ix| + |Iy|))
-        unsigned IVS[K][NR];
+        // per strip pixel: I (x32) and Ix | Iy << 16 (descaled, int16 each)
+        int IV[K][NR];
         unsigned IXY[K][NR];
         int a11 = 0, a22 = 0;  // exact partials (the shortcut needs A11 and A22 only)
         {
@@ -2091,11 +2079,9 @@ __global__ __launch_bounds__(64, 2) void lk_cvq_kernel(LKBatch B, LKDev p) {
                     Dv[r] = ldg_off<u32x2a4>(dbase + (size_t)r * 4 * dpitch, od);
                 }
                 const unsigned GW0 = sreal[k] ? IW0 : 0u, GW1 = sreal[k] ? IW1 : 0u;
-                int as0 = aslot0[k], as1 = astr[k];
-                asm volatile("" : "+v"(as0), "+v"(as1));
 #pragma unroll
                 for (int j = 0; j < NR; j++) {
-                    const int iv = sdot2(P[j], IW0, sdot2_r(P[j + 1], IW1, rnd_i)) >> (W_BITS - 5);
+                    IV[k][j] = sdot2(P[j], IW0, sdot2_r(P[j + 1], IW1, rnd_i)) >> (W_BITS - 5);
                     const unsigned X0 = __builtin_amdgcn_perm(Dv[j].y, Dv[j].x, 0x05040100u);
                     const unsigned X1 = __builtin_amdgcn_perm(Dv[j + 1].y, Dv[j + 1].x, 0x05040100u);
                     const unsigned Y0 = __builtin_amdgcn_perm(Dv[j].y, Dv[j].x, 0x07060302u);
@@ -2103,12 +2089,10 @@ __global__ __launch_bounds__(64, 2) void lk_cvq_kernel(LKBatch B, LKDev p) {
                     const int ix = sdot2(X0, GW0, sdot2_r(X1, GW1, rnd_d)) >> 16;  // CV_DESCALE(., W_BITS)
                     const int iy = sdot2(Y0, GW0, sdot2_r(Y1, GW1, rnd_d)) >> 16;
                     IXY[k][j] = pack16(ix, iy);
-                    IVS[k][j] = pack16(iv, abs(ix) + abs(iy));
                     a11 += ix * ix;
                     a22 += iy * iy;
-                    if (sreal[k]) terms[as0 + j * as1] = (int)IXY[k][j];
+                    if (sreal[k]) terms[C::a_slot(srow[k] + j, scol[k])] = (int)IXY[k][j];
                 }
-                __builtin_amdgcn_sched_barrier(0);  // (one strip's loads in flight at a time)
             }
         }
         wave_lds_sync();
@@ -2196,8 +2180,7 @@ __global__ __launch_bounds__(64, 2) void lk_cvq_kernel(LKBatch B, LKDev p) {
             }
             const BiW w = bilinear_weights(nextx - fnx, nexty - fny);
             const unsigned W0 = w.W0, W1 = w.W1;
-            int b1 = 0, b2 = 0;
-            unsigned babs = 0;
+            int b1 = 0, b2 = 0, babs = 0;
             {
                 const int off = lact ? __mul24(iny, JRW) + inx - jbase : 0;
                 const unsigned* jb = jmine + off;
@@ -2207,29 +2190,24 @@ __global__ __launch_bounds__(64, 2) void lk_cvq_kernel(LKBatch B, LKDev p) {
                     unsigned q[NR + 1];
 #pragma unroll
                     for (int r = 0; r <= NR; r++) q[r] = js[r * JRW];
-                    int bs0 = bslot0[k], bs1 = bstr[k];
-                    asm volatile("" : "+v"(bs0), "+v"(bs1));
 #pragma unroll
                     for (int r = 0; r < NR; r++) {
                         const int jv = sdot2(q[r], W0, sdot2_r(q[r + 1], W1, rnd_j)) >> 16;
-                        const int d = jv - (int)(IVS[k][r] & 0xffffu);
+                        const int d = jv - IV[k][r];
                         const int t1 = d * (int)(short)(IXY[k][r] & 0xffffu), t2 = d * ((int)IXY[k][r] >> 16);
                         b1 += t1;
                         b2 += t2;
-                        // (a lane's <= K NR 8160^2 < 2^31; capped once below so that the
-                        // group's 16 lanes cannot overflow)
-                        babs += __umul24((unsigned)abs(d), IVS[k][r] >> 16);
+                        // |terms| <= 8160 * 4080 < 2^25: capped so the group's 16 lanes cannot overflow
+                        babs = min(babs + abs(t1) + abs(t2), kCap);
                         if (sreal[k]) {
-                            // (b1, b2 of a slot adjacent: one 8-byte store)
-                            int2* tp = reinterpret_cast<int2*>(terms) + (bs0 + r * bs1);
-                            *tp = make_int2(t1, t2);
+                            const int s = C::b_slot(srow[k] + r, scol[k]);
+                            terms[s] = t1;
+                            terms[NPX + s] = t2;
                         }
                     }
-                    __builtin_amdgcn_sched_barrier(0);  // (one strip's temporaries at a time)
                 }
             }
-            static_assert((long long)K * NR * 8160 * 8160 < (1ll << 31), "a lane's |term| sum must fit int32");
-            const bool b_exact = group16_sum(min((int)babs, kCap)) <= (1 << 24);
+            const bool b_exact = group16_sum(babs) <= (1 << 24);
             float fb1 = (float)group16_sum(b_exact ? b1 : 0), fb2 = (float)group16_sum(b_exact ? b2 : 0);
             if (__builtin_amdgcn_ballot_w64(lact && !b_exact)) {
                 wave_lds_sync();
@@ -2237,10 +2215,10 @@ __global__ __launch_bounds__(64, 2) void lk_cvq_kernel(LKBatch B, LKDev p) {
                 const int* src = terms + b_off;
                 if (ak < 4) {
 #pragma unroll 6
-                    for (int i = 0; i < b_len; i++) acc += (float)(src[4 * i] + src[4 * i + 2]);
+                    for (int i = 0; i < b_len; i++) acc += (float)(src[2 * i] + src[2 * i + 1]);
                 } else {
 #pragma unroll 8
-                    for (int i = 0; i < b_len; i++) acc += (float)src[2 * i];
+                    for (int i = 0; i < b_len; i++) acc += (float)src[i];
                 }
                 if (l < 10) chains[l] = acc;
                 wave_lds_sync();
