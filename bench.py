@@ -632,10 +632,10 @@ def main():
             if not args.no_opencv_order:
                 # both LK calls summed in OpenCV's own float order (SVO_LK_OPENCV_ORDER: the
                 # drop-in Tracking mirror's default, bit-identical to cv::calcOpticalFlowPyrLK's
-                # x86 build) instead of exactly (the headline): one feature per wave
+                # x86 build) instead of exactly (the headline): four features per wave
                 print("[bench] OpenCV-order LK workload", file=sys.stderr, flush=True)
                 opencv_order = dict(headline_variant(lk_flags=S.LK_GET_MIN_EIGENVALS | S.LK_OPENCV_ORDER),
-                                    lk="SVO_LK_OPENCV_ORDER (lk_cv_kernel, one feature per wave)")
+                                    lk="SVO_LK_OPENCV_ORDER (lk_cvq_kernel, four features per wave)")
         side.update(single=single, bucketed=bucketed, forward=forward, orb=orb, stream=stream,
                     opencv_order=opencv_order)
 
