@@ -109,6 +109,7 @@ struct LKDev {
     int flags, want_err;
     float min_eig;
     int xcd;  // lk_multi_kernel: blocks in XCD order (xcd_tile.hpp; SVO_LK_XCD=0: raster)
+    int tail;  // lk_multi_kernel (21 x 21): a wave's last active feature on all 64 lanes (SVO_LK_TAIL=0: off)
 };
 
 constexpr int JM = 3;  // margin (px) of the staged next-image region around the window
@@ -1545,6 +1546,51 @@ __device__ __forceinline__ void group_sum_f(int (&v)[NV], float (&f)[NV]) {
 #pragma unroll
     for (int i = 0; i < NV; i++) f[i] = halves_lane_float(h[i], lo[i]);
 }
+// the same group reduction stopped before the float: every lane receives its group's
+// exact total as 16-bit-half sums (h, lo), total = h 2^16 + lo
+template <int LPF, int STEPS32>
+__device__ __forceinline__ void group_halves(int v, int& h, int& lo) {
+    constexpr int STEPS = LPF == 16 ? 4 : 5;
+#pragma unroll
+    for (int s = 0; s < STEPS32; s++) v = group_add_step<LPF, STEPS32>(v, s);
+    h = v >> 16;
+    lo = v & 0xFFFF;
+#pragma unroll
+    for (int s = STEPS32; s < STEPS; s++) {
+        h = group_add_step<LPF, STEPS32>(h, s);
+        lo = group_add_step<LPF, STEPS32>(lo, s);
+    }
+}
+// exact 64-lane totals of two int32 partials (|v| < 2^31 / 8 per lane) as half sums in
+// scalars: three int32 DPP steps (8-lane partials), then the halves (wave_sum_f2's steps)
+__device__ __forceinline__ void wave_halves2(int x, int y, int& xh, int& xl, int& yh, int& yl) {
+    x = dpp_add<0xb1, 0xf, true>(x);
+    y = dpp_add<0xb1, 0xf, true>(y);
+    x = dpp_add<0x4e, 0xf, true>(x);
+    y = dpp_add<0x4e, 0xf, true>(y);
+    x = dpp_add<0x114, 0xf, true>(x);
+    y = dpp_add<0x114, 0xf, true>(y);
+    int ah = x >> 16, al = x & 0xFFFF, bh = y >> 16, bl = y & 0xFFFF;
+    ah = dpp_add<0x118, 0xf, true>(ah);
+    al = dpp_add<0x118, 0xf, true>(al);
+    bh = dpp_add<0x118, 0xf, true>(bh);
+    bl = dpp_add<0x118, 0xf, true>(bl);
+    ah = dpp_add<0x142, 0xa, false>(ah);
+    al = dpp_add<0x142, 0xa, false>(al);
+    bh = dpp_add<0x142, 0xa, false>(bh);
+    bl = dpp_add<0x142, 0xa, false>(bl);
+    ah = dpp_add<0x143, 0xc, false>(ah);
+    al = dpp_add<0x143, 0xc, false>(al);
+    bh = dpp_add<0x143, 0xc, false>(bh);
+    bl = dpp_add<0x143, 0xc, false>(bl);
+    xh = __builtin_amdgcn_readlane(ah, 63);
+    xl = __builtin_amdgcn_readlane(al, 63);
+    yh = __builtin_amdgcn_readlane(bh, 63);
+    yl = __builtin_amdgcn_readlane(bl, 63);
+}
+__device__ __forceinline__ float rl_f(float v, int lane) {
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), lane));
+}
 
 // LOOP (the stereo call): the grid covers LKBatch::grid_hint features per sequence
 // (the expected count) and a block whose sequence holds more takes the tiles
@@ -1572,6 +1618,10 @@ __global__ __launch_bounds__(64, MINW) void lk_multi_kernel(LKBatch B, LKDev p) 
     constexpr long long kProd = (long long)NR * K * 8160 * 4080;
     constexpr int STEPS32 = 4 * kProd < (1ll << 31) ? 2 : 2 * kProd < (1ll << 31) ? 1 : 0;
     static_assert(kProd < (1ll << 31), "a lane's partial sums must fit int32");
+    // the single-group tail (below): the 21 x 21 temporal shape, four strips per lane
+    constexpr bool TAIL = !LOOP && FPW == 4 && K == 4 && ODD && NP == 3 && NO == 2;
+    // a tail lane's b partial: NP full row pairs + one odd pair, 8160 * 4080 each
+    static_assert(!TAIL || 8ll * (2 * NP + 2) * 8160 * 4080 < (1ll << 31), "tail partials: 3 int32 DPP steps");
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     const int lane = threadIdx.x & 63;
     const int g = lane / LPF, l = lane % LPF;
@@ -1760,8 +1810,18 @@ next_tile:  // (LOOP: the block's next tile, gridDim.x further on)
         nextx -= halfWx;
         nexty -= halfWy;
         float pdx = 0.f, pdy = 0.f;
+        int tail_j = -1;
         for (int j = 0; j < p.max_count; j++) {
-            if (__builtin_amdgcn_ballot_w64(lact) == 0) break;
+            const unsigned long long act0 = __builtin_amdgcn_ballot_w64(lact);
+            if (act0 == 0) break;
+            if constexpr (TAIL) {
+                // one feature left: its iterations go to all 64 lanes (below)
+                const unsigned long long gm = act0 & 0x0001000100010001ull;
+                if (p.tail && (gm & (gm - 1)) == 0) {
+                    tail_j = j;
+                    break;
+                }
+            }
             const float fnx = __builtin_floorf(nextx), fny = __builtin_floorf(nexty);
             const int inx = (int)fnx, iny = (int)fny;
             if (lact && !((unsigned)(inx + WW) < (unsigned)(J.w + WW) && (unsigned)(iny + WH) < (unsigned)(J.h + WH))) {
@@ -1853,6 +1913,124 @@ next_tile:  // (LOOP: the block's next tile, gridDim.x further on)
                     pdx = dx;
                     pdy = dy;
                 }
+            }
+        }
+        if constexpr (TAIL) {
+            if (tail_j >= 0) {
+                // The single-group tail. One feature (group fs) is still iterating and
+                // the wave's other groups are done with this level, so its iterations
+                // run on all 64 lanes, one strip per lane instead of four: lane t takes
+                // strip (l, k) = ((t >> 1) & 15, 2 (t >> 5) + (t & 1)) of the group's map
+                // -- strips 2i and 2i + 1 of a group lane on neighbouring lanes, so the
+                // odd-row pair that joins their last rows is one DPP move away. The
+                // feature's G pairs move to LDS once (the region of a finished group:
+                // it is not read again this level), its state to scalars. The b sums
+                // stay exact integers: sum J G over the 64 lanes as 16-bit halves minus
+                // the group's sum I G (its csum lanes, halves), rounded to float once
+                // -- the same float as the group path, whatever the distribution.
+                const int fs = (int)(__builtin_ctzll(__builtin_amdgcn_ballot_w64(lact)) / LPF);
+                const int ls = fs * LPF;
+                unsigned* const gst = jregs + ((fs + 1) & (FPW - 1)) * (Q::JSTRIDE / 4);
+                unsigned* const jstar = jregs + fs * (Q::JSTRIDE / 4);
+                if (g == fs) {
+#pragma unroll
+                    for (int k = 0; k < K; k++) {
+                        const int t = ((k >> 1) << 5) | (l << 1) | (k & 1);
+                        const unsigned ox = (k & 1) ? GXO[k >> 1] : 0u, oy = (k & 1) ? GYO[k >> 1] : 0u;
+                        *reinterpret_cast<uint4*>(gst + 8 * t) = uint4{GX[k][0], GX[k][1], GX[k][2], GY[k][0]};
+                        *reinterpret_cast<uint4*>(gst + 8 * t + 4) = uint4{GY[k][1], GY[k][2], ox, oy};
+                    }
+                }
+                int ch0, cl0, ch1, cl1;
+                group_halves<LPF, STEPS32>(csum[0], ch0, cl0);
+                group_halves<LPF, STEPS32>(csum[1], ch1, cl1);
+                ch0 = __builtin_amdgcn_readlane(ch0, ls);
+                cl0 = __builtin_amdgcn_readlane(cl0, ls);
+                ch1 = __builtin_amdgcn_readlane(ch1, ls);
+                cl1 = __builtin_amdgcn_readlane(cl1, ls);
+                wave_lds_sync();
+                const uint4 ga = *reinterpret_cast<const uint4*>(gst + 8 * lane);
+                const uint4 gb = *reinterpret_cast<const uint4*>(gst + 8 * lane + 4);
+                const unsigned TX[NP] = {ga.x, ga.y, ga.z}, TY[NP] = {ga.w, gb.x, gb.y};
+                const unsigned TXO = gb.z, TYO = gb.w;
+                int soff;
+                {
+                    const int sidx = ((lane >> 1) & (LPF - 1)) + LPF * (((lane >> 5) << 1) | (lane & 1));
+                    const int sc = sidx < NSTRIP ? sidx : 0;
+                    soff = (sc / WW) * NR * JRW + sc % WW;
+                }
+                float tnx = rl_f(nextx, ls), tny = rl_f(nexty, ls), tpdx = rl_f(pdx, ls), tpdy = rl_f(pdy, ls);
+                float tox = rl_f(nx, ls), toy = rl_f(ny, ls);
+                const float tA11 = rl_f(A11, ls), tA12 = rl_f(A12, ls), tA22 = rl_f(A22, ls), tDs = rl_f(Ds, ls);
+                int tjx0 = __builtin_amdgcn_readlane(jx0, ls), tjy0 = __builtin_amdgcn_readlane(jy0, ls);
+                int tjbase = __builtin_amdgcn_readlane(jbase, ls);
+                int tst = __builtin_amdgcn_readlane(st, ls);
+                int titc = 0;
+                for (int j = tail_j; j < p.max_count; j++) {
+                    const float fnx = __builtin_floorf(tnx), fny = __builtin_floorf(tny);
+                    const int inx = (int)fnx, iny = (int)fny;
+                    if (!((unsigned)(inx + WW) < (unsigned)(J.w + WW) && (unsigned)(iny + WH) < (unsigned)(J.h + WH))) {
+                        if (level == 0) tst = 0;
+                        break;
+                    }
+                    if ((unsigned)(inx - tjx0) > 2u * QJM || (unsigned)(iny - tjy0) > 2u * QJM) {
+                        tjx0 = inx - QJM;
+                        tjy0 = iny - QJM;
+                        tjbase = tjy0 * JRW + (tjx0 & ~3);
+                        wave_lds_sync();
+                        stage_padded<JRW, JRH>(jstar, J, tjx0 & ~3, tjy0, sg);
+                        wave_lds_sync();
+                    }
+                    titc++;
+                    const BiW w = bilinear_weights(tnx - fnx, tny - fny);
+                    const unsigned* js = jstar + (__mul24(iny, JRW) + inx - tjbase) + soff;
+                    unsigned q[NR + 1];
+#pragma unroll
+                    for (int r = 0; r <= NR; r++) q[r] = js[r * JRW];
+                    int jv[NR];
+#pragma unroll
+                    for (int r = 0; r < NR; r++) jv[r] = sdot2(q[r], w.W0, sdot2_r(q[r + 1], w.W1, rnd_j));
+                    int b0 = 0, b1 = 0;
+#pragma unroll
+                    for (int m = 0; m < NP; m++) {
+                        const unsigned jj = hi16x2(jv[2 * m], jv[2 * m + 1]);
+                        b0 = sdot2(jj, TX[m], b0);
+                        b1 = sdot2(jj, TY[m], b1);
+                    }
+                    {
+                        // the even strip's last row from the neighbouring lane (quad_perm
+                        // 1,0,3,2); even lanes hold zero odd-pair G
+                        const int jp = __builtin_amdgcn_update_dpp(0, jv[NR - 1], 0xb1, 0xf, 0xf, true);
+                        const unsigned jj = hi16x2(jp, jv[NR - 1]);
+                        b0 = sdot2(jj, TXO, b0);
+                        b1 = sdot2(jj, TYO, b1);
+                    }
+                    int h0, l0, h1, l1;
+                    wave_halves2(b0, b1, h0, l0, h1, l1);
+                    const float fb1 = __builtin_fmaf((float)(h0 - ch0), 65536.f, (float)(l0 - cl0));
+                    const float fb2 = __builtin_fmaf((float)(h1 - ch1), 65536.f, (float)(l1 - cl1));
+                    const float dx = (tA12 * fb2 - tA22 * fb1) * tDs;
+                    const float dy = (tA12 * fb1 - tA11 * fb2) * tDs;
+                    tnx += dx;
+                    tny += dy;
+                    tox = tnx + halfWx;
+                    toy = tny + halfWy;
+                    if (converged(dx, dy, p.eps2_lo, p.eps2_hi, p.eps2)) break;
+                    if (j > 0 && below_001(dx + tpdx) && below_001(dy + tpdy)) {
+                        tox -= dx * 0.5f;
+                        toy -= dy * 0.5f;
+                        break;
+                    }
+                    tpdx = dx;
+                    tpdy = dy;
+                }
+                if (g == fs) {
+                    nx = tox;
+                    ny = toy;
+                    st = tst;
+                }
+#pragma unroll
+                for (int f = 0; f < FPW; f++) itc[f] += f == fs ? titc : 0;
             }
         }
         wave_lds_sync();
@@ -2365,6 +2543,11 @@ hipError_t launch_lk(const LKBatch& b, int nseq, int max_n, const LKParams& lp, 
             return !(e && e[0] == '0');
         }();
         d.xcd = lk_xcd ? 1 : 0;
+        static const bool lk_tail = [] {
+            const char* e = std::getenv("SVO_LK_TAIL");
+            return !(e && e[0] == '0');
+        }();
+        d.tail = lk_tail ? 1 : 0;
     }
     if (lp.cv_order) {
         // OpenCV's float summation order: the reference's two windows four features
