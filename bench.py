@@ -160,7 +160,7 @@ def kernel_key(name: str):
 
 def pmc_select(kernels: dict, name: str, targs=None):
     """The one entry of a PMC summary's `kernels` whose bare name is `name` and whose
-    template arguments equal `targs` position by position (None in `targs` = any;
+    first template arguments equal `targs` position by position (None in `targs` = any;
     `targs` None = no constraint). Exact keys, not substrings: the left chain's
     pyr_scharr_kernel<true, true, true> and the right pyramid's <true, false, true>
     share every prefix. More than one match is an error (ambiguous selection)."""
@@ -169,7 +169,8 @@ def pmc_select(kernels: dict, name: str, targs=None):
         n, a = kernel_key(k)
         if n != name:
             continue
-        if targs is not None and (len(a) != len(targs) or any(t is not None and t != x for t, x in zip(targs, a))):
+        # (trailing arguments beyond `targs` are free: round 6 appended LOOP to lk_multi_kernel)
+        if targs is not None and (len(a) < len(targs) or any(t is not None and t != x for t, x in zip(targs, a))):
             continue
         hits.append((k, v))
     if len(hits) > 1:
@@ -198,10 +199,11 @@ def pmc_traffic(cfg_name: str, name: str, seqs: int = 0, targs=None):
 
 
 # template arguments of the instances the rooflines price (pmc_select): the temporal
-# 21 x 21 LK (lk_multi_kernel<FPW 4, QJM 1, MINW 3, KKS 2, 21, 21, NR 7>; the stereo
-# 11 x 11 instance is <4, 1, 4, 1, 11, 11, 11>), the left pyramid's Scharr kernels
-# (second argument SCH = true; the right pyramid's instances have false there)
-LK_TEMPORAL_TARGS = ("4", "1", "3", "2", "21", "21", "7")
+# 21 x 21 LK (lk_multi_kernel<FPW 4, QJM 1, MINW, KKS 2, 21, 21, NR 7>, MINW the waves
+# per SIMD it is built for: 3 until round 6, 4 since; the stereo 11 x 11 instance is
+# <4, 1, 6, 1, 11, 11, 11, true>), the left pyramid's Scharr kernels (second argument
+# SCH = true; the right pyramid's instances have false there)
+LK_TEMPORAL_TARGS = ("4", "1", None, "2", "21", "21", "7")
 PYR_LEFT_TARGS = (None, "true", None)
 CHAIN_LEFT_TARGS = (None, "true", None)
 
@@ -225,8 +227,9 @@ def pmc_valu(kernel_prefix: str, seqs: int, cfg_name: str = "kitti"):
         return None, None
     m = re.search(r"--seq (\d+)", d.get("source", ""))
     measured = int(m.group(1)) if m else 128
+    parts = (kernel_prefix,) if isinstance(kernel_prefix, str) else kernel_prefix
     for k, v in d.get("kernels", {}).items():
-        if kernel_prefix in k:
+        if all(x in k for x in parts):
             return v["valu_per_dispatch"] * seqs / measured, d.get("source")
     return None, None
 
@@ -237,7 +240,7 @@ def roofline_valu(lk_name: str, seqs: int, lk_avg_s: float, cfg_name: str = "kit
     instructions per launch over this run's live average launch time."""
     # the mix pass keys kernels with their template arguments (the 21 x 21 and the
     # stereo 11 x 11 instances of lk_multi_kernel are separate entries)
-    kname = "lk_multi_kernel<4, 1, 3, 2, 21, 21, 7>" if lk_name.startswith("lk_multi") else "lk_fast_kernel<21, 21"
+    kname = ("lk_multi_kernel<4, 1, ", ", 2, 21, 21, 7>") if lk_name.startswith("lk_multi") else "lk_fast_kernel<21, 21"
     valu, src = pmc_valu(kname, seqs, cfg_name)
     if valu is None or lk_avg_s <= 0:
         return None

@@ -40,6 +40,10 @@ def test_pmc_select_exact_instances():
     k, _ = bench.pmc_select(KERNELS, "post_lk_kernel")
     assert k == "svo::post_lk_kernel"
     assert bench.pmc_select(KERNELS, "lk_fast_kernel", ("21", "21", None)) == (None, None)
+    # round 6's keys: the LOOP argument appended, the temporal LK built for 4 waves per SIMD
+    k6 = {"void svo::lk_multi_kernel<4, 1, 6, 1, 11, 11, 11, true>": {"hbm_bytes_per_launch": 1},
+          "void svo::lk_multi_kernel<4, 1, 4, 2, 21, 21, 7, false>": {"hbm_bytes_per_launch": 2}}
+    assert bench.pmc_select(k6, "lk_multi_kernel", bench.LK_TEMPORAL_TARGS)[1] == {"hbm_bytes_per_launch": 2}
     # a bare name with two instances and no constraint is refused, not guessed
     with pytest.raises(ValueError):
         bench.pmc_select(KERNELS, "pyr_scharr_kernel")
