@@ -199,8 +199,8 @@ def pmc_traffic(cfg_name: str, name: str, seqs: int = 0, targs=None):
 
 
 # template arguments of the instances the rooflines price (pmc_select): the temporal
-# 21 x 21 LK (lk_multi_kernel<FPW 4, QJM 1, MINW, KKS 2, 21, 21, NR 7>, MINW the waves
-# per SIMD it is built for: 3 until round 6, 4 since; the stereo 11 x 11 instance is
+# 21 x 21 LK (lk_multi_kernel<FPW 4, QJM 1, MINW 3, KKS 2, 21, 21, NR 7, LOOP false>;
+# MINW free: A/B builds vary it; the stereo 11 x 11 instance is
 # <4, 1, 6, 1, 11, 11, 11, true>), the left pyramid's Scharr kernels (second argument
 # SCH = true; the right pyramid's instances have false there)
 LK_TEMPORAL_TARGS = ("4", "1", None, "2", "21", "21", "7")

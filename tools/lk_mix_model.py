@@ -132,7 +132,7 @@ def main():
           f"{FAST_NS} ns: {1024 / FAST_NS:.1f})")
     if a.json:
         import json
-        json.dump({"kernel": "lk_multi_kernel<4, 1, 3, 2, 21, 21, 7>", "predicted_valu_per_wave": round(tot_n),
+        json.dump({"kernel": "lk_multi_kernel<4, 1, 3, 2, 21, 21, 7, false>", "predicted_valu_per_wave": round(tot_n),
                    "slow_share": round(by_cls["slow"] / tot_n, 4), "ns_per_instr": round(ns_per, 4),
                    "peak_mix_G": round(peak_mix, 1), "fast_ns": FAST_NS, "slow_ns": SLOW_NS,
                    "levels": a.levels, "iters_per_wave": a.iters,
