@@ -113,6 +113,14 @@ struct LKDev {
 };
 
 constexpr int JM = 3;  // margin (px) of the staged next-image region around the window
+// the temporal lk_multi_kernel's launch bound (waves per SIMD) and strips loaded per
+// setup group (A/B builds: make EXTRA=-DSVO_LK_KKS=4 ...)
+#ifndef SVO_LK_MINW
+#define SVO_LK_MINW 3
+#endif
+#ifndef SVO_LK_KKS
+#define SVO_LK_KKS 2
+#endif
 
 typedef const __attribute__((address_space(1))) uint8_t* gu8;  // global (not flat) loads
 typedef const __attribute__((address_space(1))) uint32_t* gu32;
@@ -2579,7 +2587,7 @@ hipError_t launch_lk(const LKBatch& b, int nseq, int max_n, const LKParams& lp, 
             // and than 3 px; two features per wave (lk_dual_kernel, another lane
             // map) measured slower and is gone; 4 waves/SIMD, 8 features per wave
             // and one strip ahead in the setup measured slower: DESIGN.md section 5)
-            return launch_multi<4, 1, 3>(b, nseq, max_n, d, st);
+            return launch_multi<4, 1, SVO_LK_MINW, SVO_LK_KKS>(b, nseq, max_n, d, st);
         }
         // the stereo call's 11 x 11 (findLeftFeaturesInRight, no err): four
         // features per wave too, one 11-row strip per lane (11 of 16 lanes). Capped
