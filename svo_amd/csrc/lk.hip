@@ -2463,7 +2463,13 @@ template <int FPW, int QJM, int MINW = 4, int KKS = 2, int WW = 21, int WH = 21,
 hipError_t launch_multi(const LKBatch& b, int nseq, int max_n, const LKDev& d, hipStream_t st) {
     const int gn = LOOP && b.grid_hint > 0 && b.grid_hint < max_n ? b.grid_hint : max_n;
     dim3 grid((gn + FPW - 1) / FPW, nseq);
-    constexpr int lds_bytes = FPW * MultiShape<QJM, WW, WH, FPW>::JSTRIDE;
+    // SVO_LK_LDS_PAD (bytes, temporal call): a larger LDS carve per wave caps LK's waves
+    // per CU below the 16 its 9,984 B allow, leaving LDS for the kernels that run beside it
+    static const int lds_pad = [] {
+        const char* e = std::getenv("SVO_LK_LDS_PAD");
+        return e ? std::atoi(e) : 0;
+    }();
+    const int lds_bytes = FPW * MultiShape<QJM, WW, WH, FPW>::JSTRIDE + (LOOP ? 0 : lds_pad);
     hipLaunchKernelGGL((lk_multi_kernel<FPW, QJM, MINW, KKS, WW, WH, NR, LOOP>), grid, dim3(64), lds_bytes, st, b, d);
     return hipGetLastError();
 }
