@@ -240,7 +240,7 @@ def roofline_valu(lk_name: str, seqs: int, lk_avg_s: float, cfg_name: str = "kit
     instructions per launch over this run's live average launch time."""
     # the mix pass keys kernels with their template arguments (the 21 x 21 and the
     # stereo 11 x 11 instances of lk_multi_kernel are separate entries)
-    kname = ("lk_multi_kernel<4, 1, ", ", 2, 21, 21, 7>") if lk_name.startswith("lk_multi") else "lk_fast_kernel<21, 21"
+    kname = ("lk_multi_kernel<4, 1, ", ", 2, 21, 21, 7") if lk_name.startswith("lk_multi") else "lk_fast_kernel<21, 21"
     valu, src = pmc_valu(kname, seqs, cfg_name)
     if valu is None or lk_avg_s <= 0:
         return None

@@ -75,3 +75,16 @@ def test_committed_summary_resolves_every_priced_instance():
         assert bench.pmc_select(ks, "pyr_scharr_kernel", bench.PYR_LEFT_TARGS)[0] is not None, cfg
         assert bench.pmc_select(ks, "pyr_chain_kernel", bench.CHAIN_LEFT_TARGS)[0] is not None, cfg
         assert bench.pmc_select(ks, "fast_detect_q_kernel")[0] is not None, cfg
+
+
+def test_valu_lookup_temporal_lk(tmp_path, monkeypatch):
+    # the SQ mix pass keys kernels with all their template arguments (round 6: LOOP appended)
+    prof = tmp_path / "profiles"
+    prof.mkdir()
+    summ = {"source": "SQ_INSTS_VALU / SQ_WAVES of: python bench.py --seq 256 --steps 8",
+            "kernels": {"lk_multi_kernel<4, 1, 6, 1, 11, 11, 11, true>": {"valu_per_dispatch": 1},
+                        "lk_multi_kernel<4, 1, 3, 2, 21, 21, 7, false>": {"valu_per_dispatch": 2}}}
+    (prof / "valu_summary.json").write_text(json.dumps(summ))
+    monkeypatch.setattr(bench, "ROOT", str(tmp_path))
+    r = bench.roofline_valu("lk_multi_kernel<4, 1", 128, 1e-3)
+    assert r is not None and r["valu_per_launch"] == 1  # 2 per 256 sequences, scaled to 128
